@@ -1,0 +1,149 @@
+"""Pin the CPU oracle against the reference's own known answers (no GPU needed).
+
+Known answers used (all from /root/reference, copied as data into tests/golden/ by
+tests/golden/make_fixtures.py or quoted below with their file:line):
+  * unittests/io/4C_gridgenerator_test.cpp:67-130  (node counts, last gid, coordinates 1e-14)
+  * unittests/mat/4C_stvenantkirchhoff_test.cpp:42-130 (stress 1e-4, energy 908.6538)
+  * tests/input_files/solid_ele_hex8_Standard_linear.dat  RESULT DESCRIPTION (1e-12)
+  * tests/input_files/solid_ele_hex27_Standard_linear.dat RESULT DESCRIPTION (1e-12)
+  * tests/input_files/sohex27_patchtest_nl_cost_drt.dat   RESULT DESCRIPTION (1e-9)
+The result-test comparison is absolute (4C_utils_result_test.cpp:98).
+"""
+
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as orc
+from fe_driver import Problem
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load_fixture(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+# --------------------------------------------------------------------------- grid generator
+GG_LO = (-1.0, -2.0, -3.0)
+GG_HI = (2.5, 3.5, 4.5)
+GG_IV = (5, 10, 15)
+GG_OFF = 17
+
+
+def _gridgen_node_set(celltype):
+    n = GG_IV[0] * GG_IV[1] * GG_IV[2]
+    nodes = set()
+    for e in range(n):
+        nodes.update(int(g) for g in orc.hex_nodeids(celltype, e, GG_IV, GG_OFF))
+    return n, sorted(nodes)
+
+
+@pytest.mark.parametrize("celltype,nnodes", [(orc.HEX8, 1056), (orc.HEX27, 7161)])
+def test_gridgenerator_counts_and_last_node(celltype, nnodes):
+    nele, nodes = _gridgen_node_set(celltype)
+    assert nele == 750
+    assert len(nodes) == nnodes
+    assert nodes[-1] == 7177
+    x = orc.node_coords(nodes[-1], GG_IV, GG_OFF, GG_LO, GG_HI)
+    np.testing.assert_allclose(x, [2.5, 3.5, 4.5], atol=1e-14, rtol=0)
+
+
+def test_gridgenerator_rotated():
+    _, nodes = _gridgen_node_set(orc.HEX8)
+    x = orc.node_coords(nodes[-1], GG_IV, GG_OFF, GG_LO, GG_HI, rot=(30.0, 10.0, 7.0))
+    np.testing.assert_allclose(x, [2.6565639116964181, 4.8044393443812901, 2.8980306453470042],
+                               atol=1e-14, rtol=0)
+
+
+def test_box_partition_2x2x2():
+    # 8 ranks on a cube -> 2x2x2 sub-boxes (4C_io_gridgenerator.cpp:87-153)
+    seen = set()
+    for r in range(8):
+        rng = orc.box_section((200, 200, 200), 8, r)
+        assert all(rng[2 * d + 1] - rng[2 * d] == 100 for d in range(3))
+        seen.add(tuple(rng))
+    assert len(seen) == 8
+    assert list(orc.box_section((200, 100, 100), 2, 1)) == [100, 200, 0, 100, 0, 100]
+
+
+# --------------------------------------------------------------------------- material
+def test_stvk_stress_and_energy():
+    E, nu = 210.0, 0.3
+    gl = np.ones(6)
+    s, c = orc.stvk(E, nu, gl)
+    normal = (E / ((1.0 + nu) * (1.0 - 2.0 * nu))) * ((1.0 - nu) + nu + nu)
+    shear = (E / ((1.0 + nu) * (1.0 - 2.0 * nu))) * ((1.0 - 2.0 * nu) / 2.0)
+    np.testing.assert_allclose(s, [normal] * 3 + [shear] * 3, atol=1e-4)
+    assert abs(orc.stvk_energy(E, nu, gl) - 908.6538) < 1e-4
+    assert np.allclose(c, c.T)
+
+
+# --------------------------------------------------------------------------- element level
+def test_gauss_rules_truncated_constants():
+    xi, w = orc.gauss_points(orc.HEX27)
+    assert xi[0, 0] == -0.7745966692415
+    assert w[26] == 0.8888888888889 * 0.8888888888889 * 0.8888888888889
+    xi8, w8 = orc.gauss_points(orc.HEX8)
+    assert np.allclose(np.abs(xi8), 1.0 / np.sqrt(3.0)) and np.all(w8 == 1.0)
+
+
+@pytest.mark.parametrize("celltype", [orc.HEX8, orc.HEX27])
+def test_shape_partition_of_unity(celltype):
+    xi = np.array([0.13, -0.41, 0.77])
+    assert abs(orc.shape(celltype, xi).sum() - 1.0) < 1e-14
+    assert np.abs(orc.shape_deriv(celltype, xi).sum(axis=0)).max() < 1e-14
+
+
+@pytest.mark.parametrize("celltype", [orc.HEX8, orc.HEX27])
+@pytest.mark.parametrize("kinem", [orc.LINEAR, orc.TOTLAG])
+def test_tangent_is_derivative_of_force(celltype, kinem):
+    """K_e must be the consistent linearisation of f_e (finite differences)."""
+    rng = np.random.default_rng(7)
+    n = 8 if celltype == orc.HEX8 else 27
+    # reference coordinates: a jittered unit cube in the element's parameter-space node order
+    par = orc.node_param_coords(celltype)
+    X = 0.5 * (par + 1.0) + 0.05 * rng.standard_normal(par.shape)
+    u = 0.02 * rng.standard_normal((n, 3))
+    err, K, f = orc.solid_evaluate(celltype, kinem, 210.0, 0.3, X, u)
+    assert err == 0
+    h = 1e-6
+    for j in rng.choice(3 * n, size=6, replace=False):
+        up = u.copy().reshape(-1)
+        um = u.copy().reshape(-1)
+        up[j] += h
+        um[j] -= h
+        _, _, fp = orc.solid_evaluate(celltype, kinem, 210.0, 0.3, X, up, want_k=False)
+        _, _, fm = orc.solid_evaluate(celltype, kinem, 210.0, 0.3, X, um, want_k=False)
+        fd = (fp - fm) / (2 * h)
+        assert np.abs(fd - K[:, j]).max() <= 1e-6 * np.abs(K).max()
+    assert np.abs(K - K.T).max() <= 1e-12 * np.abs(K).max()
+
+
+def test_negative_nodal_jacobian_is_reported():
+    par = np.array([[-1, -1, -1], [1, -1, -1], [1, 1, -1], [-1, 1, -1], [-1, -1, 1], [1, -1, 1],
+                    [1, 1, 1], [-1, 1, 1]], dtype=float)
+    X = par.copy()
+    X[[0, 1]] = X[[1, 0]]  # swap two nodes -> inverted element
+    err, _, _ = orc.solid_evaluate(orc.HEX8, orc.LINEAR, 210.0, 0.3, X, np.zeros((8, 3)))
+    assert err == 1
+
+
+# --------------------------------------------------------------------------- end-to-end
+@pytest.mark.parametrize("name", ["solid_ele_hex8_Standard_linear.json",
+                                  "solid_ele_hex27_Standard_linear.json",
+                                  "sohex27_patchtest_nl_cost_drt.json"])
+def test_result_description(name):
+    fx = load_fixture(name)
+    prob = Problem(fx)
+    t_end = float(fx["dynamic"].get("MAXTIME", 1.0))
+    nstep = int(fx["dynamic"].get("NUMSTEP", 1))
+    dt = float(fx["dynamic"].get("TIMESTEP", 1.0))
+    t = min(t_end, nstep * dt)
+    u = prob.solve_statics(t=t)
+    for r in fx["results"]:
+        got = prob.disp(u, r["node"], r["dof"])
+        assert abs(got - r["value"]) <= r["tol"], (r, got)
