@@ -1,0 +1,375 @@
+// fcg_boxmesh.cpp -- per-rank discretization of a structured box, exactly as a 4C rank would hold
+// it after GridGenerator + FillComplete + DofSet::assign_degrees_of_freedom, packaged as an
+// fcg_desc.  Used by the benchmark and the tests to build synthetic meshes of any size natively.
+//
+//   element row map (box split over prime factors of nranks)  4C_io_gridgenerator.cpp:87-153
+//   hex8/hex27 lattice node ids, 4C node order                4C_io_gridgenerator.cpp:329-392
+//   node coordinates (+ rotation about the box midpoint)      4C_io_gridgenerator.cpp:254-323
+//   node ownership: a node shared by several ranks' row elements belongs to the lowest rank
+//                   (Rebalance::build_graph's broadcast/erase sweep, 4C_rebalance_graph_based.cpp:171-198)
+//   column elements: every element with an owned node        4C_fem_discretization_partition.cpp:510-543
+//   DOF gid = 3 * (node gid - min node gid) + d                4C_fem_dofset.cpp:343-351
+//   matrix graph: row = owned DOF, columns = DOFs of every node sharing an element, column map
+//                 ordered like Epetra's FillComplete (own DOFs first, then remote by owner, gid)
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "fourc_gpu.h"
+
+namespace {
+
+struct Section {
+  int32_t lo[3], hi[3];  // element index ranges [lo, hi)
+};
+
+bool box_sections(const int32_t* interval, int nproc, std::vector<Section>& out)
+{
+  std::vector<int> factors;
+  int np = nproc;
+  for (int fac = 2; fac < np + 1;)
+  {
+    if (np % fac == 0)
+    {
+      factors.push_back(fac);
+      np /= fac;
+    }
+    else
+      fac++;
+  }
+  if (np != 1) return false;
+  unsigned sub[3] = {1, 1, 1};
+  const double di[3] = {double(interval[0]), double(interval[1]), double(interval[2])};
+  for (auto f = factors.rbegin(); f != factors.rend(); ++f)
+  {
+    const double r[3] = {di[0] / sub[0], di[1] / sub[1], di[2] / sub[2]};
+    if (r[0] >= r[1] && r[0] >= r[2])
+      sub[0] *= *f;
+    else if (r[1] >= r[0] && r[1] >= r[2])
+      sub[1] *= *f;
+    else if (r[2] >= r[0] && r[2] >= r[1])
+      sub[2] *= *f;
+  }
+  out.resize(nproc);
+  for (int q = 0; q < nproc; ++q)
+  {
+    const unsigned sec[3] = {q % sub[0], (q / sub[0]) % sub[1], q / (sub[0] * sub[1])};
+    for (int d = 0; d < 3; ++d)
+      for (int b = 0; b < 2; ++b)
+      {
+        long v = lround((sec[d] + b) * di[d] / sub[d]);
+        v = std::max(0L, std::min(long(interval[d]), v));
+        (b ? out[q].hi : out[q].lo)[d] = int32_t(v);
+      }
+  }
+  return true;
+}
+
+uint64_t splitmix64(uint64_t x)
+{
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+template <class F>
+void parallel_for(int64_t n, F f)
+{
+  unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  if (n < 4096) nt = 1;
+  std::atomic<int64_t> next{0};
+  auto body = [&]() {
+    for (;;)
+    {
+      const int64_t s = next.fetch_add(1024);
+      if (s >= n) break;
+      for (int64_t i = s; i < std::min(n, s + 1024); ++i) f(i);
+    }
+  };
+  std::vector<std::thread> th;
+  for (unsigned t = 1; t < nt; ++t) th.emplace_back(body);
+  body();
+  for (auto& t : th) t.join();
+}
+
+}  // namespace
+
+struct fcg_box_mesh {
+  fcg_box box;
+  int rank = 0, nranks = 1, npe = 8;
+  int64_t n_ele_global = 0, n_ele_row = 0;
+  std::vector<int32_t> ele_nodes, ele_gid;
+  std::vector<double> node_x;
+  std::vector<int64_t> node_gid;
+  std::vector<int32_t> node_owner, node_dof_col, node_dof_row;
+  std::vector<int32_t> row_gid, col_gid;
+  std::vector<int64_t> rowptr;
+  std::vector<int32_t> col_lid;
+};
+
+extern "C" {
+
+int fcg_box_mesh_create(const fcg_box* box, int rank, int nranks, fcg_box_mesh** out)
+{
+  if (!box || !out || nranks < 1 || rank < 0 || rank >= nranks) return FCG_ERR_ARG;
+  *out = nullptr;
+  for (int d = 0; d < 3; ++d)
+    if (box->interval[d] <= 0 || !(box->lower[d] < box->upper[d])) return FCG_ERR_ARG;
+  if (box->celltype != FCG_HEX8 && box->celltype != FCG_HEX27) return FCG_ERR_ARG;
+  std::vector<Section> secs;
+  if (!box_sections(box->interval, nranks, secs)) return FCG_ERR_ARG;
+
+  auto* m = new fcg_box_mesh();
+  m->box = *box;
+  m->rank = rank;
+  m->nranks = nranks;
+  const bool h27 = box->celltype == FCG_HEX27;
+  const int npe = h27 ? 27 : 8;
+  m->npe = npe;
+  const int64_t IX = box->interval[0], IY = box->interval[1], IZ = box->interval[2];
+  const int64_t NX = 2 * IX + 1, NY = 2 * IY + 1, NZ = 2 * IZ + 1;
+  m->n_ele_global = IX * IY * IZ;
+  const Section& my = secs[rank];
+  m->n_ele_row = int64_t(my.hi[0] - my.lo[0]) * (my.hi[1] - my.lo[1]) * (my.hi[2] - my.lo[2]);
+
+  // lowest rank whose closed lattice box holds the node
+  auto owner_of = [&](int64_t i, int64_t j, int64_t k) -> int {
+    for (int q = 0; q < nranks; ++q)
+    {
+      const Section& s = secs[q];
+      if (s.hi[0] <= s.lo[0] || s.hi[1] <= s.lo[1] || s.hi[2] <= s.lo[2]) continue;
+      if (i >= 2 * s.lo[0] && i <= 2 * s.hi[0] && j >= 2 * s.lo[1] && j <= 2 * s.hi[1] &&
+          k >= 2 * s.lo[2] && k <= 2 * s.hi[2])
+        return q;
+    }
+    return -1;
+  };
+  // create_hex_element node lattice positions (4C_io_gridgenerator.cpp:348-380), as offsets
+  static const int off27[27][3] = {{0, 0, 0}, {2, 0, 0}, {2, 2, 0}, {0, 2, 0}, {0, 0, 2},
+      {2, 0, 2}, {2, 2, 2}, {0, 2, 2}, {1, 0, 0}, {2, 1, 0}, {1, 2, 0}, {0, 1, 0}, {0, 0, 1},
+      {2, 0, 1}, {2, 2, 1}, {0, 2, 1}, {1, 0, 2}, {2, 1, 2}, {1, 2, 2}, {0, 1, 2}, {1, 1, 0},
+      {1, 0, 1}, {2, 1, 1}, {1, 2, 1}, {0, 1, 1}, {1, 1, 2}, {1, 1, 1}};
+
+  // column elements: candidates in the section grown by one layer
+  int64_t clo[3], chi[3];
+  for (int d = 0; d < 3; ++d)
+  {
+    clo[d] = std::max<int64_t>(0, my.lo[d] - 1);
+    chi[d] = std::min<int64_t>(box->interval[d], my.hi[d] + 1);
+  }
+  std::vector<int64_t> col_ele;
+  for (int64_t ez = clo[2]; ez < chi[2]; ++ez)
+    for (int64_t ey = clo[1]; ey < chi[1]; ++ey)
+      for (int64_t ex = clo[0]; ex < chi[0]; ++ex)
+      {
+        bool has = false;
+        for (int a = 0; a < npe && !has; ++a)
+          has = owner_of(2 * ex + off27[a][0], 2 * ey + off27[a][1], 2 * ez + off27[a][2]) == rank;
+        if (has) col_ele.push_back((ez * IY + ey) * IX + ex);
+      }
+  const int64_t nce = int64_t(col_ele.size());
+
+  // column nodes: lattice index -> local id
+  std::vector<int64_t> lat;  // lattice linear index of every node touched
+  lat.reserve(nce * npe);
+  for (int64_t e : col_ele)
+  {
+    const int64_t ex = e % IX, ey = (e / IX) % IY, ez = e / (IX * IY);
+    for (int a = 0; a < npe; ++a)
+      lat.push_back(((2 * ez + off27[a][2]) * NY + 2 * ey + off27[a][1]) * NX + 2 * ex + off27[a][0]);
+  }
+  std::vector<int64_t> uniq(lat);
+  std::sort(uniq.begin(), uniq.end());
+  uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+  const int64_t ncn = int64_t(uniq.size());
+  std::vector<int32_t> own(ncn);
+  for (int64_t n = 0; n < ncn; ++n)
+  {
+    const int64_t L = uniq[n];
+    own[n] = owner_of(L % NX, (L / NX) % NY, L / (NX * NY));
+  }
+  // order: owned by gid, then ghosts by (owner, gid)  (Epetra column-map order)
+  std::vector<int64_t> order(ncn);
+  for (int64_t n = 0; n < ncn; ++n) order[n] = n;
+  std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+    const int oa = own[a] == rank ? -1 : own[a], ob = own[b] == rank ? -1 : own[b];
+    if (oa != ob) return oa < ob;
+    return uniq[a] < uniq[b];
+  });
+  std::vector<int32_t> newid(ncn);
+  for (int64_t i = 0; i < ncn; ++i) newid[order[i]] = int32_t(i);
+
+  m->node_gid.resize(ncn);
+  m->node_owner.resize(ncn);
+  m->node_x.resize(3 * ncn);
+  m->node_dof_col.resize(ncn);
+  m->node_dof_row.resize(ncn, -1);
+  int64_t n_owned = 0;
+  for (int64_t i = 0; i < ncn; ++i)
+  {
+    const int64_t n = order[i];
+    const int64_t L = uniq[n];
+    m->node_gid[i] = box->first_node_gid + L;
+    m->node_owner[i] = own[n];
+    m->node_dof_col[i] = int32_t(3 * i);
+    if (own[n] == rank) m->node_dof_row[i] = int32_t(3 * n_owned++);
+    // coordinates (4C_io_gridgenerator.cpp:283-317)
+    const int64_t ii = L % NX, jj = (L / NX) % NY, kk = L / (NX * NY);
+    const int64_t lidx[3] = {ii, jj, kk};
+    double c[3];
+    for (int d = 0; d < 3; ++d)
+      c[d] = double(lidx[d]) / (2 * box->interval[d]) * (box->upper[d] - box->lower[d]) + box->lower[d];
+    if (box->jitter != 0.0 && ii > 0 && ii < NX - 1 && jj > 0 && jj < NY - 1 && kk > 0 && kk < NZ - 1)
+    {
+      for (int d = 0; d < 3; ++d)
+      {
+        const uint64_t z = splitmix64(box->jitter_seed + 3 * uint64_t(L) + d);
+        const double u01 = double(z >> 11) * (1.0 / 9007199254740992.0);
+        const double h = (box->upper[d] - box->lower[d]) / box->interval[d];
+        c[d] += box->jitter * h * (2.0 * u01 - 1.0);
+      }
+    }
+    double cm[3] = {0, 0, 0};
+    if (box->rotation[0] != 0.0 || box->rotation[1] != 0.0 || box->rotation[2] != 0.0)
+      for (int d = 0; d < 3; ++d) cm[d] = (box->upper[d] + box->lower[d]) / 2.;
+    for (int ax = 0; ax < 3; ++ax)
+    {
+      if (box->rotation[ax] == 0.0) continue;
+      double dx[3] = {c[0] - cm[0], c[1] - cm[1], c[2] - cm[2]};
+      const double ca = std::cos(box->rotation[ax] * M_PI / 180), sa = std::sin(box->rotation[ax] * M_PI / 180);
+      c[0] = cm[0];
+      c[1] = cm[1];
+      c[2] = cm[2];
+      c[(ax + 1) % 3] += ca * dx[(ax + 1) % 3] + sa * dx[(ax + 2) % 3];
+      c[(ax + 2) % 3] += ca * dx[(ax + 2) % 3] - sa * dx[(ax + 1) % 3];
+      c[ax] += dx[ax];
+    }
+    for (int d = 0; d < 3; ++d) m->node_x[3 * i + d] = c[d];
+  }
+  // element connectivity in local column-node ids
+  m->ele_nodes.resize(nce * npe);
+  m->ele_gid.resize(nce);
+  for (int64_t e = 0; e < nce; ++e)
+  {
+    m->ele_gid[e] = int32_t(col_ele[e]);
+    for (int a = 0; a < npe; ++a)
+    {
+      const int64_t L = lat[e * npe + a];
+      const int64_t n = std::lower_bound(uniq.begin(), uniq.end(), L) - uniq.begin();
+      m->ele_nodes[e * npe + a] = newid[n];
+    }
+  }
+  // dof gids of the maps
+  m->row_gid.resize(3 * n_owned);
+  m->col_gid.resize(3 * ncn);
+  for (int64_t i = 0; i < ncn; ++i)
+  {
+    const int64_t dof0 = 3 * (m->node_gid[i] - box->first_node_gid);
+    for (int d = 0; d < 3; ++d) m->col_gid[3 * i + d] = int32_t(dof0 + d);
+    if (m->node_dof_row[i] >= 0)
+      for (int d = 0; d < 3; ++d) m->row_gid[m->node_dof_row[i] + d] = int32_t(dof0 + d);
+  }
+  // graph: owned node -> incident column elements -> neighbour nodes
+  std::vector<int64_t> adj_ptr(n_owned + 1, 0);
+  for (int64_t i = 0; i < nce * npe; ++i)
+  {
+    const int32_t n = m->ele_nodes[i];
+    if (n < n_owned) adj_ptr[n + 1]++;  // owned nodes are the first n_owned local ids
+  }
+  for (int64_t n = 0; n < n_owned; ++n) adj_ptr[n + 1] += adj_ptr[n];
+  std::vector<int32_t> adj(adj_ptr[n_owned]);
+  {
+    std::vector<int64_t> fill(adj_ptr.begin(), adj_ptr.end() - 1);
+    for (int64_t e = 0; e < nce; ++e)
+      for (int a = 0; a < npe; ++a)
+      {
+        const int32_t n = m->ele_nodes[e * npe + a];
+        if (n < n_owned) adj[fill[n]++] = int32_t(e);
+      }
+  }
+  std::vector<int32_t> nnb(n_owned);
+  std::vector<std::vector<int32_t>> nb(n_owned);
+  parallel_for(n_owned, [&](int64_t n) {
+    std::vector<int32_t>& v = nb[n];
+    v.reserve(8 * npe);
+    for (int64_t k = adj_ptr[n]; k < adj_ptr[n + 1]; ++k)
+      for (int a = 0; a < npe; ++a) v.push_back(m->ele_nodes[int64_t(adj[k]) * npe + a]);
+    std::sort(v.begin(), v.end());
+    v.erase(std::unique(v.begin(), v.end()), v.end());
+    nnb[n] = int32_t(v.size());
+  });
+  m->rowptr.resize(3 * n_owned + 1);
+  m->rowptr[0] = 0;
+  for (int64_t n = 0; n < n_owned; ++n)
+    for (int d = 0; d < 3; ++d) m->rowptr[3 * n + d + 1] = m->rowptr[3 * n + d] + 3 * int64_t(nnb[n]);
+  m->col_lid.resize(m->rowptr[3 * n_owned]);
+  parallel_for(n_owned, [&](int64_t n) {
+    const std::vector<int32_t>& v = nb[n];
+    for (int d = 0; d < 3; ++d)
+    {
+      int32_t* c = m->col_lid.data() + m->rowptr[3 * n + d];
+      for (size_t k = 0; k < v.size(); ++k)
+        for (int j = 0; j < 3; ++j) c[3 * k + j] = 3 * v[k] + j;  // node_dof_col == 3 * local id
+    }
+    std::vector<int32_t>().swap(nb[n]);
+  });
+  *out = m;
+  return FCG_OK;
+}
+
+int fcg_box_mesh_destroy(fcg_box_mesh* m)
+{
+  delete m;
+  return FCG_OK;
+}
+
+int fcg_box_mesh_desc(const fcg_box_mesh* m, int kinematics, double youngs, double poisson,
+    int device, fcg_desc* o)
+{
+  if (!m || !o) return FCG_ERR_ARG;
+  std::memset(o, 0, sizeof(*o));
+  o->abi_version = FCG_ABI_VERSION;
+  o->celltype = m->box.celltype;
+  o->kinematics = kinematics;
+  o->device = device;
+  o->youngs = youngs;
+  o->poisson = poisson;
+  o->n_ele = int64_t(m->ele_gid.size());
+  o->n_node = int64_t(m->node_gid.size());
+  o->n_rows = int64_t(m->row_gid.size());
+  o->n_cols = int64_t(m->col_gid.size());
+  o->ele_nodes = m->ele_nodes.data();
+  o->ele_gid = m->ele_gid.data();
+  o->node_x = m->node_x.data();
+  o->node_dof_col = m->node_dof_col.data();
+  o->node_dof_row = m->node_dof_row.data();
+  o->node_dof_kcol = nullptr;
+  o->rowptr = m->rowptr.data();
+  o->col_lid = m->col_lid.data();
+  return FCG_OK;
+}
+
+int fcg_box_mesh_maps(const fcg_box_mesh* m, const int32_t** row_gid, const int32_t** col_gid,
+    const int64_t** node_gid, const int32_t** node_owner)
+{
+  if (!m) return FCG_ERR_ARG;
+  if (row_gid) *row_gid = m->row_gid.data();
+  if (col_gid) *col_gid = m->col_gid.data();
+  if (node_gid) *node_gid = m->node_gid.data();
+  if (node_owner) *node_owner = m->node_owner.data();
+  return FCG_OK;
+}
+
+int fcg_box_mesh_counts(const fcg_box_mesh* m, int64_t* n_ele_global, int64_t* n_ele_row)
+{
+  if (!m) return FCG_ERR_ARG;
+  if (n_ele_global) *n_ele_global = m->n_ele_global;
+  if (n_ele_row) *n_ele_row = m->n_ele_row;
+  return FCG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,465 @@
+// fcg_context.cpp -- C ABI entry points: context creation (the assembly plan, i.e. this path's
+// FillComplete), device-resident and host-pointer evaluate, timing and info.
+//
+// Plan built here once per pattern (the reference rebuilds nothing either: the stiffness keeps
+// its graph, `savegraph=true`, 4C_structure_new_timint_basedataglobalstate.cpp:650-652):
+//   * incidences = (column element e, local node a) with node a owned by this rank, grouped by
+//     the owned node (ascending row LID) and ordered by element index inside a node -- the order
+//     in which the assembly kernel sums, hence bitwise-reproducible results;
+//   * for every incidence and every local node b of the element, the position of b's first DOF
+//     column inside the row of a -- the stride-3 fast path of SparseMatrix::assemble
+//     (4C_linalg_sparsematrix.cpp:497-543) resolved once on the host instead of by a
+//     lower_bound per element and row at every Newton iteration.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "fcg_internal.hpp"
+
+namespace {
+
+std::mutex g_err_mutex;
+std::string g_create_error;
+
+void set_create_error(const std::string& s)
+{
+  std::lock_guard<std::mutex> lk(g_err_mutex);
+  g_create_error = s;
+}
+
+template <class F>
+void parallel_for(int64_t n, F f)
+{
+  unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  if (n < 4096) nt = 1;
+  std::vector<std::thread> th;
+  std::atomic<int64_t> next{0};
+  const int64_t chunk = 1024;
+  auto body = [&]() {
+    for (;;)
+    {
+      const int64_t s = next.fetch_add(chunk);
+      if (s >= n) break;
+      const int64_t e = std::min(n, s + chunk);
+      for (int64_t i = s; i < e; ++i) f(i);
+    }
+  };
+  for (unsigned t = 1; t < nt; ++t) th.emplace_back(body);
+  body();
+  for (auto& t : th) t.join();
+}
+
+template <class T>
+hipError_t upload(T** dst, const T* src, int64_t n, int64_t& bytes)
+{
+  *dst = nullptr;
+  if (n == 0) return hipSuccess;
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(dst), sizeof(T) * n);
+  if (e != hipSuccess) return e;
+  bytes += sizeof(T) * n;
+  if (src) return hipMemcpy(*dst, src, sizeof(T) * n, hipMemcpyHostToDevice);
+  return hipSuccess;
+}
+
+void free_mesh(fcg::DeviceMesh& m)
+{
+  void* ptrs[] = {m.ele_nodes, m.ele_gid, m.node_x, m.node_dof_col, m.inc_of, m.inc_ptr,
+      m.rownode_row0, m.inc_pos, m.rowptr, m.scratch, m.err};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  m = fcg::DeviceMesh{};
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* fcg_last_error(const fcg_ctx* ctx)
+{
+  if (ctx) return ctx->last_error.c_str();
+  std::lock_guard<std::mutex> lk(g_err_mutex);
+  return g_create_error.c_str();
+}
+
+int fcg_create(const fcg_desc* d, fcg_ctx** out)
+{
+  if (!d || !out) return FCG_ERR_ARG;
+  *out = nullptr;
+  if (d->abi_version != FCG_ABI_VERSION)
+  {
+    set_create_error("abi_version mismatch");
+    return FCG_ERR_ARG;
+  }
+  if ((d->celltype != FCG_HEX8 && d->celltype != FCG_HEX27) ||
+      (d->kinematics != FCG_LINEAR && d->kinematics != FCG_TOTLAG))
+  {
+    set_create_error("unsupported celltype/kinematics");
+    return FCG_ERR_ARG;
+  }
+  // Mat::PAR::StVenantKirchhoff parameter checks (4C_mat_stvenantkirchhoff.cpp:26-28)
+  if (!(d->youngs > 0.0) || d->poisson >= 0.5 || d->poisson < -1.0)
+  {
+    set_create_error("Young's modulus must be > 0 and Poisson's ratio in [-1;0.5)");
+    return FCG_ERR_ARG;
+  }
+  if (d->n_ele < 0 || d->n_node < 0 || d->n_rows < 0 || d->n_cols < 0 ||
+      (d->n_ele > 0 && (!d->ele_nodes || !d->node_x || !d->node_dof_col || !d->node_dof_row)) ||
+      (d->n_rows > 0 && (!d->rowptr || !d->col_lid)) || d->n_ele >= (int64_t(1) << 31))
+  {
+    set_create_error("invalid descriptor arrays/sizes");
+    return FCG_ERR_ARG;
+  }
+  const int npe = d->celltype == FCG_HEX27 ? 27 : 8;
+  const int maxrow = npe == 8 ? 81 : 375;
+  const int32_t* kcol = d->node_dof_kcol ? d->node_dof_kcol : d->node_dof_col;
+
+  // --- validate connectivity
+  for (int64_t i = 0; i < d->n_ele * npe; ++i)
+    if (d->ele_nodes[i] < 0 || d->ele_nodes[i] >= d->n_node)
+    {
+      set_create_error("element references a node outside [0, n_node)");
+      return FCG_ERR_ARG;
+    }
+  for (int64_t n = 0; n < d->n_node; ++n)
+  {
+    if (d->node_dof_col[n] < 0 || d->node_dof_col[n] + 3 > d->n_cols)
+    {
+      set_create_error("node_dof_col out of range");
+      return FCG_ERR_ARG;
+    }
+    if (d->node_dof_row[n] >= 0 && d->node_dof_row[n] + 3 > d->n_rows)
+    {
+      set_create_error("node_dof_row out of range");
+      return FCG_ERR_ARG;
+    }
+  }
+
+  // --- owned row nodes, ascending by row LID
+  std::vector<int32_t> rownodes;
+  for (int64_t n = 0; n < d->n_node; ++n)
+    if (d->node_dof_row[n] >= 0) rownodes.push_back(int32_t(n));
+  std::sort(rownodes.begin(), rownodes.end(),
+      [&](int32_t a, int32_t b) { return d->node_dof_row[a] < d->node_dof_row[b]; });
+  std::vector<int32_t> rn_of_node(d->n_node, -1);
+  for (size_t i = 0; i < rownodes.size(); ++i) rn_of_node[rownodes[i]] = int32_t(i);
+  const int64_t nrn = int64_t(rownodes.size());
+
+  // --- CSR structure of node rows: 3 consecutive rows with identical column lists
+  std::string err;
+  std::mutex err_m;
+  std::vector<int32_t> row0(nrn);
+  int32_t max_rowlen = 0;
+  for (int64_t r = 0; r < nrn; ++r)
+  {
+    row0[r] = d->node_dof_row[rownodes[r]];
+    const int64_t s = d->rowptr[row0[r]];
+    const int64_t len = d->rowptr[row0[r] + 1] - s;
+    max_rowlen = std::max<int32_t>(max_rowlen, int32_t(len));
+    if (len > maxrow || d->rowptr[row0[r] + 2] - d->rowptr[row0[r] + 1] != len ||
+        d->rowptr[row0[r] + 3] - d->rowptr[row0[r] + 2] != len)
+    {
+      set_create_error("node rows must have 3 equal-length rows of <= 3*neighbours columns");
+      return FCG_ERR_ARG;
+    }
+  }
+  parallel_for(nrn, [&](int64_t r) {
+    const int64_t s = d->rowptr[row0[r]];
+    const int64_t len = d->rowptr[row0[r] + 1] - s;
+    for (int i = 1; i < 3; ++i)
+      if (std::memcmp(d->col_lid + s, d->col_lid + s + i * len, sizeof(int32_t) * len) != 0)
+      {
+        std::lock_guard<std::mutex> lk(err_m);
+        err = "the 3 rows of a node must share one column pattern";
+      }
+  });
+  if (!err.empty())
+  {
+    set_create_error(err);
+    return FCG_ERR_ARG;
+  }
+
+  // --- incidences grouped by owned node
+  std::vector<int64_t> inc_ptr(nrn + 1, 0);
+  for (int64_t i = 0; i < d->n_ele * npe; ++i)
+  {
+    const int32_t rn = rn_of_node[d->ele_nodes[i]];
+    if (rn >= 0) inc_ptr[rn + 1]++;
+  }
+  for (int64_t r = 0; r < nrn; ++r) inc_ptr[r + 1] += inc_ptr[r];
+  const int64_t n_inc = inc_ptr[nrn];
+  if (n_inc >= (int64_t(1) << 31))
+  {
+    set_create_error("too many incidences for one context (> 2^31)");
+    return FCG_ERR_ARG;
+  }
+  std::vector<int32_t> inc_of(d->n_ele * npe, -1);
+  std::vector<int32_t> inc_ele(n_inc);
+  std::vector<uint8_t> inc_a(n_inc);
+  {
+    std::vector<int64_t> fill(inc_ptr.begin(), inc_ptr.end() - 1);
+    for (int64_t e = 0; e < d->n_ele; ++e)
+      for (int a = 0; a < npe; ++a)
+      {
+        const int32_t rn = rn_of_node[d->ele_nodes[e * npe + a]];
+        if (rn < 0) continue;
+        const int64_t k = fill[rn]++;
+        inc_of[e * npe + a] = int32_t(k);
+        inc_ele[k] = int32_t(e);
+        inc_a[k] = uint8_t(a);
+      }
+  }
+  // --- positions of every element node's DOF triple inside the row (stride fast path)
+  std::vector<uint16_t> inc_pos(n_inc * npe);
+  parallel_for(nrn, [&](int64_t r) {
+    const int64_t s = d->rowptr[row0[r]];
+    const int64_t len = d->rowptr[row0[r] + 1] - s;
+    const int32_t* cols = d->col_lid + s;
+    for (int64_t k = inc_ptr[r]; k < inc_ptr[r + 1]; ++k)
+    {
+      const int32_t* en = d->ele_nodes + int64_t(inc_ele[k]) * npe;
+      for (int b = 0; b < npe; ++b)
+      {
+        const int32_t c = kcol[en[b]];
+        const int32_t* it = std::lower_bound(cols, cols + len, c);
+        const int64_t pos = it - cols;
+        if (it == cols + len || *it != c || pos + 3 > len || cols[pos + 1] != c + 1 ||
+            cols[pos + 2] != c + 2)
+        {
+          std::lock_guard<std::mutex> lk(err_m);
+          err = "matrix graph lacks an element coupling or a node's DOF columns are not "
+                "contiguous (SparseMatrix::assemble stride fast path)";
+          return;
+        }
+        inc_pos[k * npe + b] = uint16_t(pos);
+      }
+    }
+  });
+  if (!err.empty())
+  {
+    set_create_error(err);
+    return FCG_ERR_ARG;
+  }
+
+  // --- device
+  fcg_ctx* ctx = new fcg_ctx();
+  ctx->device = d->device;
+  hipError_t he = hipSetDevice(d->device);
+  if (he == hipSuccess) he = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  if (he != hipSuccess)
+  {
+    set_create_error(std::string("HIP: ") + hipGetErrorString(he));
+    delete ctx;
+    return FCG_ERR_DEVICE;
+  }
+  fcg::upload_constant_tables(d->celltype);
+  fcg::DeviceMesh& m = ctx->mesh;
+  m.celltype = d->celltype;
+  m.kinem = d->kinematics;
+  m.npe = npe;
+  m.n_ele = d->n_ele;
+  m.n_node = d->n_node;
+  m.n_rows = d->n_rows;
+  m.n_cols = d->n_cols;
+  m.nnz = d->n_rows ? d->rowptr[d->n_rows] : 0;
+  m.n_rownodes = nrn;
+  m.n_inc = n_inc;
+  m.max_rowlen = max_rowlen;
+  // StVK constants, fill_cmat (4C_mat_stvenantkirchhoff.cpp:123-144)
+  const double nu = d->poisson;
+  const double mfac = d->youngs / ((1.0 + nu) * (1.0 - 2.0 * nu));
+  m.cdiag = mfac * (1.0 - nu);
+  m.lambda = mfac * nu;
+  m.mu = mfac * 0.5 * (1.0 - 2.0 * nu);
+  std::vector<int32_t> eg;
+  if (!d->ele_gid)
+  {
+    eg.resize(d->n_ele);
+    for (int64_t e = 0; e < d->n_ele; ++e) eg[e] = int32_t(e);
+  }
+  int64_t& bytes = ctx->device_bytes;
+  he = hipSuccess;
+  auto chk = [&](hipError_t x) {
+    if (he == hipSuccess) he = x;
+  };
+  chk(upload(&m.ele_nodes, d->ele_nodes, d->n_ele * npe, bytes));
+  chk(upload(&m.ele_gid, d->ele_gid ? d->ele_gid : eg.data(), d->n_ele, bytes));
+  chk(upload(&m.node_x, d->node_x, d->n_node * 3, bytes));
+  chk(upload(&m.node_dof_col, d->node_dof_col, d->n_node, bytes));
+  chk(upload(&m.inc_of, inc_of.data(), d->n_ele * npe, bytes));
+  chk(upload(&m.inc_ptr, inc_ptr.data(), nrn + 1, bytes));
+  chk(upload(&m.rownode_row0, row0.data(), nrn, bytes));
+  chk(upload(&m.inc_pos, inc_pos.data(), n_inc * npe, bytes));
+  chk(upload(&m.rowptr, d->rowptr, d->n_rows + 1, bytes));
+  chk(upload<double>(&m.scratch, nullptr, n_inc * fcg::record_doubles(npe), bytes));
+  chk(upload<int32_t>(&m.err, nullptr, 2, bytes));
+  for (auto& ev : ctx->timing.ev) chk(hipEventCreate(&ev));
+  if (he != hipSuccess)
+  {
+    set_create_error(std::string("HIP allocation/copy failed: ") + hipGetErrorString(he));
+    fcg_destroy(ctx);
+    return FCG_ERR_DEVICE;
+  }
+  *out = ctx;
+  return FCG_OK;
+}
+
+int fcg_destroy(fcg_ctx* ctx)
+{
+  if (!ctx) return FCG_OK;
+  (void)hipSetDevice(ctx->device);
+  free_mesh(ctx->mesh);
+  for (auto& ev : ctx->timing.ev)
+    if (ev) (void)hipEventDestroy(ev);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->h_u) (void)hipFree(ctx->h_u);
+  if (ctx->h_f) (void)hipFree(ctx->h_f);
+  if (ctx->h_k) (void)hipFree(ctx->h_k);
+  delete ctx;
+  return FCG_OK;
+}
+
+int fcg_evaluate_device(fcg_ctx* ctx, int action, int mode, const double* d_u_col,
+    double* d_fint_row, double* d_K_vals, void* stream_ptr, int32_t* bad_ele_gid)
+{
+  if (!ctx) return FCG_ERR_ARG;
+  fcg::DeviceMesh& m = ctx->mesh;
+  const bool want_k = (action == FCG_CALC_NLNSTIFF);
+  if ((action != FCG_CALC_NLNSTIFF && action != FCG_CALC_INTERNALFORCE) ||
+      (mode != FCG_ACCUMULATE && mode != FCG_OVERWRITE) ||
+      (m.n_ele > 0 && !d_u_col) || (m.n_rows > 0 && !d_fint_row) ||
+      (want_k && m.nnz > 0 && !d_K_vals))
+  {
+    ctx->last_error = "invalid evaluate arguments";
+    return FCG_ERR_ARG;
+  }
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = stream_ptr ? static_cast<hipStream_t>(stream_ptr) : ctx->stream;
+  const int32_t init[2] = {0, INT32_MAX};
+  hipError_t he = hipMemcpyAsync(m.err, init, sizeof(init), hipMemcpyHostToDevice, s);
+  auto& T = ctx->timing;
+  if (T.enabled && he == hipSuccess) he = hipEventRecord(T.ev[0], s);
+  if (he == hipSuccess) he = fcg::launch_element(m, d_u_col, want_k, s);
+  if (T.enabled && he == hipSuccess) he = hipEventRecord(T.ev[1], s);
+  if (he == hipSuccess)
+    he = fcg::launch_assemble(m, want_k, mode == FCG_OVERWRITE, d_K_vals, d_fint_row, s);
+  if (T.enabled && he == hipSuccess) he = hipEventRecord(T.ev[2], s);
+  int32_t errv[2] = {0, INT32_MAX};
+  if (he == hipSuccess) he = hipMemcpyAsync(errv, m.err, sizeof(errv), hipMemcpyDeviceToHost, s);
+  if (he == hipSuccess) he = hipStreamSynchronize(s);
+  if (he != hipSuccess)
+  {
+    ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
+    return FCG_ERR_DEVICE;
+  }
+  if (T.enabled)
+  {
+    float a = 0.f, b = 0.f;
+    (void)hipEventElapsedTime(&a, T.ev[0], T.ev[1]);
+    (void)hipEventElapsedTime(&b, T.ev[1], T.ev[2]);
+    T.ms_element = a;
+    T.ms_assemble = b;
+  }
+  if (errv[0] != 0)
+  {
+    int32_t gid = -1;
+    if (errv[1] >= 0 && errv[1] < m.n_ele)
+      (void)hipMemcpy(&gid, m.ele_gid + errv[1], sizeof(int32_t), hipMemcpyDeviceToHost);
+    if (bad_ele_gid) *bad_ele_gid = gid;
+    ctx->last_error = errv[0] == FCG_ERR_NODAL_DETJ
+                          ? "determinant of jacobian <= 0 at one node of element " + std::to_string(gid)
+                          : "singular 3x3 matrix in element " + std::to_string(gid);
+    return errv[0];
+  }
+  return FCG_OK;
+}
+
+int fcg_evaluate(fcg_ctx* ctx, int action, const double* u_col, double* fint_row, double* K_vals,
+    int32_t* bad_ele_gid)
+{
+  if (!ctx) return FCG_ERR_ARG;
+  fcg::DeviceMesh& m = ctx->mesh;
+  const bool want_k = (action == FCG_CALC_NLNSTIFF) && K_vals;
+  (void)hipSetDevice(ctx->device);
+  hipError_t he = hipSuccess;
+  if (!ctx->h_u && m.n_cols) he = hipMalloc(&ctx->h_u, sizeof(double) * m.n_cols);
+  if (he == hipSuccess && !ctx->h_f && m.n_rows) he = hipMalloc(&ctx->h_f, sizeof(double) * m.n_rows);
+  if (he == hipSuccess && want_k && !ctx->h_k && m.nnz) he = hipMalloc(&ctx->h_k, sizeof(double) * m.nnz);
+  if (he == hipSuccess && m.n_cols) he = hipMemcpy(ctx->h_u, u_col, sizeof(double) * m.n_cols, hipMemcpyHostToDevice);
+  if (he == hipSuccess && m.n_rows) he = hipMemcpy(ctx->h_f, fint_row, sizeof(double) * m.n_rows, hipMemcpyHostToDevice);
+  if (he == hipSuccess && want_k && m.nnz) he = hipMemcpy(ctx->h_k, K_vals, sizeof(double) * m.nnz, hipMemcpyHostToDevice);
+  if (he != hipSuccess)
+  {
+    ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
+    return FCG_ERR_DEVICE;
+  }
+  const int rc = fcg_evaluate_device(ctx, want_k ? FCG_CALC_NLNSTIFF : FCG_CALC_INTERNALFORCE,
+      FCG_ACCUMULATE, ctx->h_u, ctx->h_f, ctx->h_k, nullptr, bad_ele_gid);
+  if (rc != FCG_OK) return rc;
+  if (m.n_rows) he = hipMemcpy(fint_row, ctx->h_f, sizeof(double) * m.n_rows, hipMemcpyDeviceToHost);
+  if (he == hipSuccess && want_k && m.nnz)
+    he = hipMemcpy(K_vals, ctx->h_k, sizeof(double) * m.nnz, hipMemcpyDeviceToHost);
+  if (he != hipSuccess)
+  {
+    ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
+    return FCG_ERR_DEVICE;
+  }
+  return FCG_OK;
+}
+
+int fcg_set_timing(fcg_ctx* ctx, int enable)
+{
+  if (!ctx) return FCG_ERR_ARG;
+  ctx->timing.enabled = enable != 0;
+  return FCG_OK;
+}
+
+int fcg_get_timing(const fcg_ctx* ctx, double* ms_element, double* ms_assemble)
+{
+  if (!ctx) return FCG_ERR_ARG;
+  if (ms_element) *ms_element = ctx->timing.ms_element;
+  if (ms_assemble) *ms_assemble = ctx->timing.ms_assemble;
+  return 2;
+}
+
+int fcg_get_info(const fcg_ctx* ctx, fcg_info* info)
+{
+  if (!ctx || !info) return FCG_ERR_ARG;
+  const fcg::DeviceMesh& m = ctx->mesh;
+  info->n_ele = m.n_ele;
+  info->n_node = m.n_node;
+  info->n_rows = m.n_rows;
+  info->n_cols = m.n_cols;
+  info->nnz = m.nnz;
+  info->n_incidences = m.n_inc;
+  info->scratch_bytes = m.n_inc * fcg::record_doubles(m.npe) * int64_t(sizeof(double));
+  info->device_bytes = ctx->device_bytes;
+  return FCG_OK;
+}
+
+int fcg_device_alloc(int device, int64_t bytes, void** d_ptr)
+{
+  if (!d_ptr || bytes < 0) return FCG_ERR_ARG;
+  if (hipSetDevice(device) != hipSuccess) return FCG_ERR_DEVICE;
+  return hipMalloc(d_ptr, bytes > 0 ? bytes : 1) == hipSuccess ? FCG_OK : FCG_ERR_DEVICE;
+}
+int fcg_device_free(void* p) { return hipFree(p) == hipSuccess ? FCG_OK : FCG_ERR_DEVICE; }
+int fcg_memcpy_h2d(void* dst, const void* src, int64_t n)
+{
+  return hipMemcpy(dst, src, n, hipMemcpyHostToDevice) == hipSuccess ? FCG_OK : FCG_ERR_DEVICE;
+}
+int fcg_memcpy_d2h(void* dst, const void* src, int64_t n)
+{
+  return hipMemcpy(dst, src, n, hipMemcpyDeviceToHost) == hipSuccess ? FCG_OK : FCG_ERR_DEVICE;
+}
+int fcg_memset_device(void* dst, int v, int64_t n)
+{
+  return hipMemset(dst, v, n) == hipSuccess ? FCG_OK : FCG_ERR_DEVICE;
+}
+
+}  // extern "C"

@@ -1,0 +1,63 @@
+// fcg_internal.hpp -- context layout and kernel launch interface shared by the HIP translation
+// units of libfourc_gpu.  Not part of the public ABI (include/fourc_gpu.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "fourc_gpu.h"
+
+namespace fcg {
+
+// Per-incidence scratch record written by the element kernel and consumed by the row-assembly
+// kernel: the element's block-row of node a (3 rows x 3*npe columns, b-major) then f_a (3).
+inline int64_t record_doubles(int npe) { return 9 * int64_t(npe) + 3; }
+
+struct DeviceMesh {
+  int celltype = 0, kinem = 0, npe = 8;
+  int64_t n_ele = 0, n_node = 0, n_rows = 0, n_cols = 0, nnz = 0;
+  int64_t n_rownodes = 0, n_inc = 0;
+  double lambda = 0, mu = 0, cdiag = 0;  // StVK: C_00 = cdiag, C_01 = lambda, C_33 = mu
+
+  int32_t* ele_nodes = nullptr;     // [n_ele][npe]
+  int32_t* ele_gid = nullptr;       // [n_ele]
+  double* node_x = nullptr;         // [n_node][3]
+  int32_t* node_dof_col = nullptr;  // [n_node]
+  int32_t* inc_of = nullptr;        // [n_ele][npe] incidence id or -1
+  int64_t* inc_ptr = nullptr;       // [n_rownodes+1]
+  int32_t* rownode_row0 = nullptr;  // [n_rownodes]
+  uint16_t* inc_pos = nullptr;      // [n_inc][npe] column position of node b in the row
+  int64_t* rowptr = nullptr;        // [n_rows+1]
+  double* scratch = nullptr;        // [n_inc][record_doubles(npe)]
+  int32_t* err = nullptr;           // [2]: code, min failing element index
+  int32_t max_rowlen = 0;
+};
+
+struct Timing {
+  bool enabled = false;
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  double ms_element = 0.0, ms_assemble = 0.0;
+};
+
+void upload_constant_tables(int celltype);  // GP / nodal derivative tables -> __constant__
+hipError_t launch_element(const DeviceMesh& m, const double* d_u_col, bool want_k,
+    hipStream_t stream);
+hipError_t launch_assemble(const DeviceMesh& m, bool want_k, bool overwrite, double* d_K,
+    double* d_fint, hipStream_t stream);
+
+}  // namespace fcg
+
+struct fcg_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  fcg::DeviceMesh mesh;
+  fcg::Timing timing;
+  std::string last_error;
+  int64_t device_bytes = 0;
+  // staging buffers for the host-pointer entry point
+  double* h_u = nullptr;
+  double* h_f = nullptr;
+  double* h_k = nullptr;
+};

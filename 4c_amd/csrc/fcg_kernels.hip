@@ -1,0 +1,634 @@
+// fcg_kernels.hip -- CDNA4 (gfx950) kernels of the solid element evaluation + assembly path.
+//
+//  element_kernel   Discretization::evaluate's column-element loop + SolidEleCalc's Gauss-point
+//                   loop (4C_fem_discretization_evaluate.cpp:83-102,
+//                   4C_solid_3D_ele_calc.cpp:110-240): gathers X and u, checks the nodal Jacobian
+//                   determinants, evaluates J^-1, N_XYZ, strains, StVK stresses, f_e and K_e, and
+//                   writes every owned block-row of K_e plus f_a into an incidence-ordered scratch.
+//  assemble_kernel  SparseMatrix::assemble + LinAlg::assemble(Vector) for owned rows
+//                   (4C_linalg_sparsematrix.cpp:444-576, 4C_linalg_utils_sparse_algebra_assemble.cpp:72-92)
+//                   as a deterministic gather: one wavefront per owned row node sums the block-rows
+//                   of its incident elements in LDS (fixed element order -> bitwise reproducible, no
+//                   atomics) and writes the node's 3 CSR rows once, coalesced.
+//
+// Isotropic StVK lets the element stiffness be written without the 6 x 3n B-matrix:
+//   linear:  K_ab = sum_g fac [ lambda a b^T + mu b a^T + mu (a.b) I ]           a = N_XYZ of node a
+//   TotLag:  K_ab = sum_g fac [ lambda (Fa)(Fb)^T + mu (Fb)(Fa)^T + mu (a.b) F F^T + (a.S.b) I ]
+// which is B_a^T C B_b (+ K_geo, calc_lib.hpp:872-927) with C from fill_cmat
+// (4C_mat_stvenantkirchhoff.cpp:115-145); see DESIGN.md for the derivation.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+#include "fcg_internal.hpp"
+#include "fcg_shape.hpp"
+
+namespace fcg {
+
+// ---------------------------------------------------------------------------------- tables
+__constant__ double c_dN8_gp[8 * 8 * 3];      // [g][node][d]
+__constant__ double c_dN8_node[8 * 8 * 3];    // [at node][node][d]
+__constant__ double c_w8[8];
+__constant__ double c_dN27_gp[27 * 27 * 3];
+__constant__ double c_dN27_node[27 * 27 * 3];
+__constant__ double c_w27[27];
+__constant__ uint16_t c_pairs27[378];          // symmetric pairs a <= b, packed a | b << 8
+
+template <int NPE> struct Tables;
+template <> struct Tables<8> {
+  __device__ static const double* dNgp() { return c_dN8_gp; }
+  __device__ static const double* dNnode() { return c_dN8_node; }
+  __device__ static const double* w() { return c_w8; }
+};
+template <> struct Tables<27> {
+  __device__ static const double* dNgp() { return c_dN27_gp; }
+  __device__ static const double* dNnode() { return c_dN27_node; }
+  __device__ static const double* w() { return c_w27; }
+};
+
+void upload_constant_tables(int /*celltype*/)
+{
+  static bool done = false;
+  if (done) return;
+  for (int ct = 0; ct < 2; ++ct)
+  {
+    const int n = num_nodes(ct);
+    double xi[81], w[27], xn[81];
+    gauss_rule(ct, xi, w);
+    node_param_coords(ct, xn);
+    double gp[27 * 27 * 3], nd[27 * 27 * 3];
+    for (int g = 0; g < n; ++g) shape_deriv(ct, &xi[3 * g], &gp[3 * n * g]);
+    for (int g = 0; g < n; ++g) shape_deriv(ct, &xn[3 * g], &nd[3 * n * g]);
+    if (ct == kHex8)
+    {
+      (void)hipMemcpyToSymbol(HIP_SYMBOL(c_dN8_gp), gp, sizeof(double) * 8 * 8 * 3);
+      (void)hipMemcpyToSymbol(HIP_SYMBOL(c_dN8_node), nd, sizeof(double) * 8 * 8 * 3);
+      (void)hipMemcpyToSymbol(HIP_SYMBOL(c_w8), w, sizeof(double) * 8);
+    }
+    else
+    {
+      (void)hipMemcpyToSymbol(HIP_SYMBOL(c_dN27_gp), gp, sizeof(gp));
+      (void)hipMemcpyToSymbol(HIP_SYMBOL(c_dN27_node), nd, sizeof(nd));
+      (void)hipMemcpyToSymbol(HIP_SYMBOL(c_w27), w, sizeof(double) * 27);
+    }
+  }
+  uint16_t pairs[378];
+  int p = 0;
+  for (int a = 0; a < 27; ++a)
+    for (int b = a; b < 27; ++b) pairs[p++] = uint16_t(a | (b << 8));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(c_pairs27), pairs, sizeof(pairs));
+  done = true;
+}
+
+// ---------------------------------------------------------------------------------- helpers
+// invert3x3 of the reference (4C_linalg_fixedsizematrix.hpp:1382-1409), column-major m[r + 3c].
+__device__ inline double invert3x3(double* m)
+{
+  const double t00 = m[4] * m[8] - m[5] * m[7];
+  const double t10 = m[2] * m[7] - m[1] * m[8];
+  const double t20 = m[1] * m[5] - m[2] * m[4];
+  const double det = m[0] * t00 + m[3] * t10 + m[6] * t20;
+  if (det == 0.0) return 0.0;
+  const double id = 1.0 / det;
+  const double t01 = m[3], t11 = m[4], t12 = m[7];
+  const double r3 = id * (m[5] * m[6] - t01 * m[8]);
+  const double r4 = id * (m[0] * m[8] - m[2] * m[6]);
+  const double r7 = id * (m[1] * m[6] - m[0] * t12);
+  const double r5 = id * (m[2] * t01 - m[0] * m[5]);
+  const double r6 = id * (t01 * t12 - t11 * m[6]);
+  const double r8 = id * (m[0] * t11 - m[1] * t01);
+  m[3] = r3;
+  m[4] = r4;
+  m[7] = r7;
+  m[5] = r5;
+  m[6] = r6;
+  m[8] = r8;
+  m[0] = id * t00;
+  m[1] = id * t10;
+  m[2] = id * t20;
+  return det;
+}
+
+// J(i,j) = sum_c dN(i,c) X(j,c)  (multiply_nt(deriv, xref), calc_lib.hpp:444)
+template <int NPE>
+__device__ inline void jacobian(const double* __restrict__ dN, const double* __restrict__ X, double* J)
+{
+#pragma unroll
+  for (int k = 0; k < 9; ++k) J[k] = 0.0;
+  for (int c = 0; c < NPE; ++c)
+  {
+    const double d0 = dN[3 * c + 0], d1 = dN[3 * c + 1], d2 = dN[3 * c + 2];
+    const double x0 = X[3 * c + 0], x1 = X[3 * c + 1], x2 = X[3 * c + 2];
+    J[0] += d0 * x0; J[1] += d1 * x0; J[2] += d2 * x0;
+    J[3] += d0 * x1; J[4] += d1 * x1; J[5] += d2 * x1;
+    J[6] += d0 * x2; J[7] += d1 * x2; J[8] += d2 * x2;
+  }
+}
+
+template <int NPE, int KIN>
+struct ElementShared {
+  static constexpr int NGP = NPE;
+  double X[3 * NPE];
+  double U[3 * NPE];
+  double NX[NGP * NPE * 3];               // [g][c][d]
+  double P[KIN ? NGP * NPE * 3 : 1];      // F * N_XYZ_c  (TotLag)
+  double invJ[NGP * 9];
+  double fac[NGP];
+  double S[NGP * 6];                      // PK2 stress, Voigt xx yy zz xy yz zx
+  double F[KIN ? NGP * 9 : 1];
+  double M[KIN ? NGP * 6 : 1];            // F F^T (sym)
+  int bad;
+};
+
+struct ElementArgs {
+  int64_t n_ele;
+  const int32_t* ele_nodes;
+  const double* node_x;
+  const int32_t* node_dof_col;
+  const double* u_col;
+  const int32_t* inc_of;
+  double* scratch;
+  int32_t* err;
+  double lambda, mu, cdiag;
+  int want_k;
+};
+
+// ---------------------------------------------------------------------------------- element
+template <int NPE, int KIN, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void element_kernel(ElementArgs A)
+{
+  constexpr int NGP = NPE;
+  constexpr bool SYM = (NPE == 27);             // hex27: compute a<=b and mirror
+  constexpr int NPAIR = SYM ? NPE * (NPE + 1) / 2 : NPE * NPE;
+  constexpr int REC = 9 * NPE + 3;
+  constexpr int ROWLEN = 3 * NPE;
+  __shared__ ElementShared<NPE, KIN> sh;
+  const int tid = threadIdx.x;
+  const double* dNgp = Tables<NPE>::dNgp();
+  const double* dNnode = Tables<NPE>::dNnode();
+  const double* wgp = Tables<NPE>::w();
+
+  for (int64_t e = blockIdx.x; e < A.n_ele; e += gridDim.x)
+  {
+    const int32_t* en = A.ele_nodes + e * NPE;
+    // 1. gather reference coordinates and displacements (evaluate_element_nodes, calc_lib.hpp:180-203)
+    for (int v = tid; v < 3 * NPE; v += BLOCK)
+    {
+      const int a = v / 3, d = v - 3 * (v / 3);
+      const int node = en[a];
+      sh.X[v] = A.node_x[3 * int64_t(node) + d];
+      sh.U[v] = A.u_col[A.node_dof_col[node] + d];
+    }
+    if (tid == 0) sh.bad = 0;
+    __syncthreads();
+
+    // 2. nodal det J > 0 check (calc_lib.hpp:475-496) and GP Jacobian inverses (calc_lib.hpp:435-448)
+    if (tid < NPE)
+    {
+      double J[9];
+      jacobian<NPE>(dNnode + 3 * NPE * tid, sh.X, J);
+      const double det = invert3x3(J);
+      if (det == 0.0) atomicMax(&sh.bad, 2);
+      else if (!(det > 0)) atomicMax(&sh.bad, 1);
+    }
+    else if (tid < NPE + NGP)
+    {
+      const int g = tid - NPE;
+      double J[9];
+      jacobian<NPE>(dNgp + 3 * NPE * g, sh.X, J);
+      const double det = invert3x3(J);
+      if (det == 0.0) atomicMax(&sh.bad, 2);
+#pragma unroll
+      for (int k = 0; k < 9; ++k) sh.invJ[9 * g + k] = J[k];
+      sh.fac[g] = det * wgp[g];
+    }
+    __syncthreads();
+    if (sh.bad)
+    {
+      if (tid == 0)
+      {
+        atomicMax(&A.err[0], sh.bad);
+        atomicMin(&A.err[1], int32_t(e));
+      }
+      __syncthreads();
+      continue;
+    }
+
+    // 3. N_XYZ = J^-1 dN (multiply(inverse_jacobian, derivatives))
+    for (int v = tid; v < NGP * NPE; v += BLOCK)
+    {
+      const int g = v / NPE, c = v - NPE * (v / NPE);
+      const double* iJ = sh.invJ + 9 * g;
+      const double* d = dNgp + 3 * (NPE * g + c);
+      const double d0 = d[0], d1 = d[1], d2 = d[2];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) sh.NX[3 * v + i] = iJ[i] * d0 + iJ[i + 3] * d1 + iJ[i + 6] * d2;
+    }
+    __syncthreads();
+
+    // 4. strains and StVK stress per Gauss point
+    if (tid < NGP)
+    {
+      const int g = tid;
+      const double* NX = sh.NX + 3 * NPE * g;
+      double E[6];
+      if (KIN == 0)
+      {
+        // evaluate_linear_strain_gradient + evaluate_linear_gl_strain (calc_lib.hpp:682-799)
+        for (int k = 0; k < 6; ++k) E[k] = 0.0;
+        for (int c = 0; c < NPE; ++c)
+        {
+          const double n0 = NX[3 * c], n1 = NX[3 * c + 1], n2 = NX[3 * c + 2];
+          const double u0 = sh.U[3 * c], u1 = sh.U[3 * c + 1], u2 = sh.U[3 * c + 2];
+          E[0] += n0 * u0;
+          E[1] += n1 * u1;
+          E[2] += n2 * u2;
+          E[3] += n1 * u0 + n0 * u1;
+          E[4] += n2 * u1 + n1 * u2;
+          E[5] += n2 * u0 + n0 * u2;
+        }
+      }
+      else
+      {
+        // evaluate_deformation_gradient (calc_lib.hpp:579-605): hex8 from current coordinates,
+        // hex27 as I + u N_XYZ^T.  F(i,j) column-major.
+        double F[9];
+        for (int k = 0; k < 9; ++k) F[k] = 0.0;
+        for (int c = 0; c < NPE; ++c)
+        {
+          const double n0 = NX[3 * c], n1 = NX[3 * c + 1], n2 = NX[3 * c + 2];
+          double q[3];
+#pragma unroll
+          for (int i = 0; i < 3; ++i) q[i] = (NPE == 8) ? sh.X[3 * c + i] + sh.U[3 * c + i] : sh.U[3 * c + i];
+#pragma unroll
+          for (int i = 0; i < 3; ++i)
+          {
+            F[i + 0] += q[i] * n0;
+            F[i + 3] += q[i] * n1;
+            F[i + 6] += q[i] * n2;
+          }
+        }
+        if (NPE != 8)
+        {
+          F[0] += 1.0;
+          F[4] += 1.0;
+          F[8] += 1.0;
+        }
+        // inverse of F must exist (evaluate_spatial_material_mapping, calc_lib.hpp:562)
+        {
+          double Fi[9];
+#pragma unroll
+          for (int k = 0; k < 9; ++k) Fi[k] = F[k];
+          if (invert3x3(Fi) == 0.0) atomicMax(&sh.bad, 2);
+        }
+        // C = F^T F, E = (C - I)/2 with engineering shear (calc_lib.hpp:639-676)
+        double C[9];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j)
+            C[i + 3 * j] = F[3 * i] * F[3 * j] + F[3 * i + 1] * F[3 * j + 1] + F[3 * i + 2] * F[3 * j + 2];
+        E[0] = 0.5 * (C[0] - 1.0);
+        E[1] = 0.5 * (C[4] - 1.0);
+        E[2] = 0.5 * (C[8] - 1.0);
+        E[3] = C[3];
+        E[4] = C[7];
+        E[5] = C[2];
+        double* Fs = sh.F + 9 * g;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) Fs[k] = F[k];
+        double* Ms = sh.M + 6 * g;  // F F^T: xx yy zz xy yz zx
+        Ms[0] = F[0] * F[0] + F[3] * F[3] + F[6] * F[6];
+        Ms[1] = F[1] * F[1] + F[4] * F[4] + F[7] * F[7];
+        Ms[2] = F[2] * F[2] + F[5] * F[5] + F[8] * F[8];
+        Ms[3] = F[0] * F[1] + F[3] * F[4] + F[6] * F[7];
+        Ms[4] = F[1] * F[2] + F[4] * F[5] + F[7] * F[8];
+        Ms[5] = F[2] * F[0] + F[5] * F[3] + F[8] * F[6];
+      }
+      // So3Material::evaluate -> S = C E (4C_mat_stvenantkirchhoff.cpp:169-177)
+      double* S = sh.S + 6 * g;
+      S[0] = A.cdiag * E[0] + A.lambda * E[1] + A.lambda * E[2];
+      S[1] = A.lambda * E[0] + A.cdiag * E[1] + A.lambda * E[2];
+      S[2] = A.lambda * E[0] + A.lambda * E[1] + A.cdiag * E[2];
+      S[3] = A.mu * E[3];
+      S[4] = A.mu * E[4];
+      S[5] = A.mu * E[5];
+    }
+    __syncthreads();
+    if (KIN == 1)
+    {
+      if (sh.bad)
+      {
+        if (tid == 0)
+        {
+          atomicMax(&A.err[0], sh.bad);
+          atomicMin(&A.err[1], int32_t(e));
+        }
+        __syncthreads();
+        continue;
+      }
+      // P_c = F N_XYZ_c
+      for (int v = tid; v < NGP * NPE; v += BLOCK)
+      {
+        const int g = v / NPE;
+        const double* F = sh.F + 9 * g;
+        const double n0 = sh.NX[3 * v], n1 = sh.NX[3 * v + 1], n2 = sh.NX[3 * v + 2];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) sh.P[3 * v + i] = F[i] * n0 + F[i + 3] * n1 + F[i + 6] * n2;
+      }
+      __syncthreads();
+    }
+
+    const int32_t* inc = A.inc_of + e * NPE;
+
+    // 5. internal force f_a = sum_g fac F S N_XYZ_a  (add_internal_force_vector, calc_lib.hpp:851-860)
+    if (tid < NPE)
+    {
+      const int a = tid;
+      const int32_t ia = inc[a];
+      if (ia >= 0)
+      {
+        double f[3] = {0.0, 0.0, 0.0};
+        for (int g = 0; g < NGP; ++g)
+        {
+          const double* S = sh.S + 6 * g;
+          const double* n = sh.NX + 3 * (NPE * g + a);
+          const double fc = sh.fac[g];
+          double t[3];
+          t[0] = S[0] * n[0] + S[3] * n[1] + S[5] * n[2];
+          t[1] = S[3] * n[0] + S[1] * n[1] + S[4] * n[2];
+          t[2] = S[5] * n[0] + S[4] * n[1] + S[2] * n[2];
+          if (KIN == 1)
+          {
+            const double* F = sh.F + 9 * g;
+            const double s0 = F[0] * t[0] + F[3] * t[1] + F[6] * t[2];
+            const double s1 = F[1] * t[0] + F[4] * t[1] + F[7] * t[2];
+            const double s2 = F[2] * t[0] + F[5] * t[1] + F[8] * t[2];
+            t[0] = s0;
+            t[1] = s1;
+            t[2] = s2;
+          }
+          f[0] += fc * t[0];
+          f[1] += fc * t[1];
+          f[2] += fc * t[2];
+        }
+        double* rec = A.scratch + int64_t(ia) * REC + 9 * NPE;
+        rec[0] = f[0];
+        rec[1] = f[1];
+        rec[2] = f[2];
+      }
+    }
+
+    // 6. element stiffness blocks K_ab (add_elastic/geometric_stiffness_matrix, calc_lib.hpp:872-927)
+    if (A.want_k)
+    {
+      for (int p = tid; p < NPAIR; p += BLOCK)
+      {
+        int a, b;
+        if (SYM)
+        {
+          const uint16_t pr = c_pairs27[p];
+          a = pr & 0xff;
+          b = pr >> 8;
+        }
+        else
+        {
+          a = p / NPE;
+          b = p - NPE * (p / NPE);
+        }
+        const int32_t ia = inc[a];
+        const int32_t ib = inc[b];
+        if (ia < 0 && (!SYM || ib < 0)) continue;
+        double G[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) G[k] = 0.0;
+        double H[6] = {0, 0, 0, 0, 0, 0};
+        double geo = 0.0;
+        for (int g = 0; g < NGP; ++g)
+        {
+          const double fc = sh.fac[g];
+          const double* na = sh.NX + 3 * (NPE * g + a);
+          const double* nb = sh.NX + 3 * (NPE * g + b);
+          if (KIN == 0)
+          {
+            const double fa0 = fc * na[0], fa1 = fc * na[1], fa2 = fc * na[2];
+            const double b0 = nb[0], b1 = nb[1], b2 = nb[2];
+            G[0] += fa0 * b0; G[3] += fa0 * b1; G[6] += fa0 * b2;
+            G[1] += fa1 * b0; G[4] += fa1 * b1; G[7] += fa1 * b2;
+            G[2] += fa2 * b0; G[5] += fa2 * b1; G[8] += fa2 * b2;
+          }
+          else
+          {
+            const double* pa = sh.P + 3 * (NPE * g + a);
+            const double* pb = sh.P + 3 * (NPE * g + b);
+            const double fa0 = fc * pa[0], fa1 = fc * pa[1], fa2 = fc * pa[2];
+            const double b0 = pb[0], b1 = pb[1], b2 = pb[2];
+            G[0] += fa0 * b0; G[3] += fa0 * b1; G[6] += fa0 * b2;
+            G[1] += fa1 * b0; G[4] += fa1 * b1; G[7] += fa1 * b2;
+            G[2] += fa2 * b0; G[5] += fa2 * b1; G[8] += fa2 * b2;
+            const double a0 = na[0], a1 = na[1], a2 = na[2];
+            const double c0 = nb[0], c1 = nb[1], c2 = nb[2];
+            const double t = fc * (a0 * c0 + a1 * c1 + a2 * c2);
+            const double* M = sh.M + 6 * g;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) H[k] += t * M[k];
+            const double* S = sh.S + 6 * g;
+            const double sb0 = S[0] * c0 + S[3] * c1 + S[5] * c2;
+            const double sb1 = S[3] * c0 + S[1] * c1 + S[4] * c2;
+            const double sb2 = S[5] * c0 + S[4] * c1 + S[2] * c2;
+            geo += fc * (a0 * sb0 + a1 * sb1 + a2 * sb2);
+          }
+        }
+        // K_ij = lambda G_ij + mu G_ji + mu tr(G) delta_ij      (linear)
+        // K_ij = lambda G_ij + mu G_ji + mu H_ij + geo delta_ij (TotLag)
+        double K[9];
+        const double lam = A.lambda, mu = A.mu;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) K[i + 3 * j] = lam * G[i + 3 * j] + mu * G[j + 3 * i];
+        if (KIN == 0)
+        {
+          const double tr = mu * (G[0] + G[4] + G[8]);
+          K[0] += tr;
+          K[4] += tr;
+          K[8] += tr;
+        }
+        else
+        {
+          K[0] += mu * H[0] + geo;
+          K[4] += mu * H[1] + geo;
+          K[8] += mu * H[2] + geo;
+          K[1] += mu * H[3]; K[3] += mu * H[3];
+          K[5] += mu * H[4]; K[7] += mu * H[4];
+          K[2] += mu * H[5]; K[6] += mu * H[5];
+        }
+        if (ia >= 0)
+        {
+          double* rec = A.scratch + int64_t(ia) * REC + 3 * b;
+#pragma unroll
+          for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) rec[i * ROWLEN + j] = K[i + 3 * j];
+        }
+        if (SYM && a != b && ib >= 0)
+        {
+          double* rec = A.scratch + int64_t(ib) * REC + 3 * a;
+#pragma unroll
+          for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) rec[i * ROWLEN + j] = K[j + 3 * i];
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------- assembly
+struct AssembleArgs {
+  int64_t n_rownodes;
+  const int64_t* inc_ptr;
+  const int32_t* rownode_row0;
+  const uint16_t* inc_pos;
+  const double* scratch;
+  const int64_t* rowptr;
+  double* K;
+  double* fint;
+};
+
+template <int NPE, bool WANT_K, bool OVERWRITE>
+__global__ __launch_bounds__(64) void assemble_kernel(AssembleArgs A)
+{
+  constexpr int REC = 9 * NPE + 3;
+  constexpr int ROWLEN = 3 * NPE;
+  constexpr int MAXROW = (NPE == 8) ? 81 : 375;
+  __shared__ double acc[WANT_K ? 3 * MAXROW : 1];
+  const int lane = threadIdx.x;
+  for (int64_t r = blockIdx.x; r < A.n_rownodes; r += gridDim.x)
+  {
+    const int32_t row0 = A.rownode_row0[r];
+    const int64_t base = A.rowptr[row0];
+    const int rowlen = int(A.rowptr[row0 + 1] - base);
+    if (WANT_K)
+      for (int v = lane; v < 3 * rowlen; v += 64) acc[v] = 0.0;
+    double f = 0.0;
+    __syncthreads();
+    const int64_t k0 = A.inc_ptr[r], k1 = A.inc_ptr[r + 1];
+    for (int64_t k = k0; k < k1; ++k)
+    {
+      const double* src = A.scratch + k * REC;
+      if (WANT_K)
+      {
+        const uint16_t* pos = A.inc_pos + k * NPE;
+        for (int v = lane; v < 9 * NPE; v += 64)
+        {
+          const int i = v / ROWLEN;
+          const int rem = v - ROWLEN * i;
+          const int b = rem / 3;
+          const int j = rem - 3 * b;
+          acc[i * rowlen + pos[b] + j] += src[v];
+        }
+      }
+      if (lane < 3) f += src[9 * NPE + lane];
+      __syncthreads();
+    }
+    if (WANT_K)
+    {
+      double* dst = A.K + base;  // the node's 3 rows are contiguous (checked at setup)
+      for (int v = lane; v < 3 * rowlen; v += 64)
+      {
+        if (OVERWRITE)
+          dst[v] = acc[v];
+        else
+          dst[v] += acc[v];
+      }
+    }
+    if (lane < 3)
+    {
+      if (OVERWRITE)
+        A.fint[row0 + lane] = f;
+      else
+        A.fint[row0 + lane] += f;
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------- launchers
+static int grid_for(int64_t work, int cap)
+{
+  return int(work < cap ? (work > 0 ? work : 1) : cap);
+}
+
+hipError_t launch_element(const DeviceMesh& m, const double* d_u_col, bool want_k, hipStream_t stream)
+{
+  if (m.n_ele == 0) return hipSuccess;
+  ElementArgs a;
+  a.n_ele = m.n_ele;
+  a.ele_nodes = m.ele_nodes;
+  a.node_x = m.node_x;
+  a.node_dof_col = m.node_dof_col;
+  a.u_col = d_u_col;
+  a.inc_of = m.inc_of;
+  a.scratch = m.scratch;
+  a.err = m.err;
+  a.lambda = m.lambda;
+  a.mu = m.mu;
+  a.cdiag = m.cdiag;
+  a.want_k = want_k ? 1 : 0;
+  if (m.npe == 8)
+  {
+    const int grid = grid_for(m.n_ele, 256 * 32);
+    if (m.kinem == 0)
+      hipLaunchKernelGGL((element_kernel<8, 0, 64>), dim3(grid), dim3(64), 0, stream, a);
+    else
+      hipLaunchKernelGGL((element_kernel<8, 1, 64>), dim3(grid), dim3(64), 0, stream, a);
+  }
+  else
+  {
+    const int grid = grid_for(m.n_ele, 256 * 8);
+    if (m.kinem == 0)
+      hipLaunchKernelGGL((element_kernel<27, 0, 256>), dim3(grid), dim3(256), 0, stream, a);
+    else
+      hipLaunchKernelGGL((element_kernel<27, 1, 256>), dim3(grid), dim3(256), 0, stream, a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_assemble(const DeviceMesh& m, bool want_k, bool overwrite, double* d_K,
+    double* d_fint, hipStream_t stream)
+{
+  if (m.n_rownodes == 0) return hipSuccess;
+  AssembleArgs a;
+  a.n_rownodes = m.n_rownodes;
+  a.inc_ptr = m.inc_ptr;
+  a.rownode_row0 = m.rownode_row0;
+  a.inc_pos = m.inc_pos;
+  a.scratch = m.scratch;
+  a.rowptr = m.rowptr;
+  a.K = d_K;
+  a.fint = d_fint;
+  const int grid = grid_for(m.n_rownodes, 256 * 32);
+#define FCG_ASM(NPE)                                                                               \
+  if (want_k && overwrite)                                                                         \
+    hipLaunchKernelGGL((assemble_kernel<NPE, true, true>), dim3(grid), dim3(64), 0, stream, a);    \
+  else if (want_k)                                                                                 \
+    hipLaunchKernelGGL((assemble_kernel<NPE, true, false>), dim3(grid), dim3(64), 0, stream, a);   \
+  else if (overwrite)                                                                              \
+    hipLaunchKernelGGL((assemble_kernel<NPE, false, true>), dim3(grid), dim3(64), 0, stream, a);   \
+  else                                                                                             \
+    hipLaunchKernelGGL((assemble_kernel<NPE, false, false>), dim3(grid), dim3(64), 0, stream, a);
+  if (m.npe == 8)
+  {
+    FCG_ASM(8)
+  }
+  else
+  {
+    FCG_ASM(27)
+  }
+#undef FCG_ASM
+  return hipGetLastError();
+}
+
+}  // namespace fcg

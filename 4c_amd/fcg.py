@@ -1,0 +1,268 @@
+"""ctypes binding of libfourc_gpu (include/fourc_gpu.h) for tests, bench and Python hosts.
+
+This is glue, not the product: every evaluation goes through the C ABI into the HIP kernels of
+4c_amd/csrc.  There is no CPU fallback -- if the shared library is missing the import fails loudly.
+Device buffers are torch tensors on `cuda:N` (PyTorch supplies device memory and streams only).
+"""
+
+import ctypes
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libfourc_gpu.so")
+
+HEX8, HEX27 = 0, 1
+LINEAR, TOTLAG = 0, 1
+CALC_NLNSTIFF, CALC_INTERNALFORCE = 0, 1
+ACCUMULATE, OVERWRITE = 0, 1
+ABI_VERSION = 1
+
+STATUS = {0: "FCG_OK", 1: "FCG_ERR_NODAL_DETJ", 2: "FCG_ERR_SINGULAR", 3: "FCG_ERR_ARG",
+          4: "FCG_ERR_DEVICE"}
+
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_dp = ctypes.POINTER(ctypes.c_double)
+
+
+class FcgDesc(ctypes.Structure):
+    _fields_ = [("abi_version", ctypes.c_int32), ("celltype", ctypes.c_int32),
+                ("kinematics", ctypes.c_int32), ("device", ctypes.c_int32),
+                ("youngs", ctypes.c_double), ("poisson", ctypes.c_double),
+                ("n_ele", ctypes.c_int64), ("n_node", ctypes.c_int64), ("n_rows", ctypes.c_int64),
+                ("n_cols", ctypes.c_int64), ("ele_nodes", _i32p), ("ele_gid", _i32p),
+                ("node_x", _dp), ("node_dof_col", _i32p), ("node_dof_row", _i32p),
+                ("node_dof_kcol", _i32p), ("rowptr", _i64p), ("col_lid", _i32p)]
+
+
+class FcgBox(ctypes.Structure):
+    _fields_ = [("celltype", ctypes.c_int32), ("interval", ctypes.c_int32 * 3),
+                ("lower", ctypes.c_double * 3), ("upper", ctypes.c_double * 3),
+                ("rotation", ctypes.c_double * 3), ("first_node_gid", ctypes.c_int64),
+                ("jitter", ctypes.c_double), ("jitter_seed", ctypes.c_uint64)]
+
+
+class FcgInfo(ctypes.Structure):
+    _fields_ = [("n_ele", ctypes.c_int64), ("n_node", ctypes.c_int64), ("n_rows", ctypes.c_int64),
+                ("n_cols", ctypes.c_int64), ("nnz", ctypes.c_int64),
+                ("n_incidences", ctypes.c_int64), ("scratch_bytes", ctypes.c_int64),
+                ("device_bytes", ctypes.c_int64)]
+
+
+# every symbol declared in include/fourc_gpu.h
+EXPORTS = ["fcg_create", "fcg_destroy", "fcg_last_error", "fcg_evaluate", "fcg_evaluate_device",
+           "fcg_device_alloc", "fcg_device_free", "fcg_memcpy_h2d", "fcg_memcpy_d2h",
+           "fcg_memset_device", "fcg_set_timing", "fcg_get_timing", "fcg_get_info",
+           "fcg_box_mesh_create", "fcg_box_mesh_destroy", "fcg_box_mesh_desc", "fcg_box_mesh_maps",
+           "fcg_box_mesh_counts"]
+
+_lib = None
+
+
+class FcgError(RuntimeError):
+    def __init__(self, code, msg, bad_ele_gid=-1):
+        super().__init__(f"{STATUS.get(code, code)}: {msg}")
+        self.code = code
+        self.bad_ele_gid = bad_ele_gid
+
+
+def lib():
+    """Load libfourc_gpu.so (built by `make -C 4c_amd`); raise if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not built: run `make -C 4c_amd` (no CPU fallback exists)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp = ctypes.c_void_p
+    L.fcg_create.argtypes = [ctypes.POINTER(FcgDesc), ctypes.POINTER(vp)]
+    L.fcg_destroy.argtypes = [vp]
+    L.fcg_last_error.argtypes = [vp]
+    L.fcg_last_error.restype = ctypes.c_char_p
+    L.fcg_evaluate.argtypes = [vp, ctypes.c_int, _dp, _dp, _dp, _i32p]
+    L.fcg_evaluate_device.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp, vp, vp, _i32p]
+    L.fcg_device_alloc.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.POINTER(vp)]
+    L.fcg_device_free.argtypes = [vp]
+    L.fcg_memcpy_h2d.argtypes = [vp, vp, ctypes.c_int64]
+    L.fcg_memcpy_d2h.argtypes = [vp, vp, ctypes.c_int64]
+    L.fcg_memset_device.argtypes = [vp, ctypes.c_int, ctypes.c_int64]
+    L.fcg_set_timing.argtypes = [vp, ctypes.c_int]
+    L.fcg_get_timing.argtypes = [vp, _dp, _dp]
+    L.fcg_get_info.argtypes = [vp, ctypes.POINTER(FcgInfo)]
+    L.fcg_box_mesh_create.argtypes = [ctypes.POINTER(FcgBox), ctypes.c_int, ctypes.c_int,
+                                      ctypes.POINTER(vp)]
+    L.fcg_box_mesh_destroy.argtypes = [vp]
+    L.fcg_box_mesh_desc.argtypes = [vp, ctypes.c_int, ctypes.c_double, ctypes.c_double,
+                                    ctypes.c_int, ctypes.POINTER(FcgDesc)]
+    L.fcg_box_mesh_maps.argtypes = [vp, ctypes.POINTER(_i32p), ctypes.POINTER(_i32p),
+                                    ctypes.POINTER(_i64p), ctypes.POINTER(_i32p)]
+    L.fcg_box_mesh_counts.argtypes = [vp, _i64p, _i64p]
+    _lib = L
+    return L
+
+
+def _np_ptr(a, t):
+    return a.ctypes.data_as(t)
+
+
+def _tensor_ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class BoxMesh:
+    """One rank of a GridGenerator box (the fcg_box_mesh_* builder), as numpy views."""
+
+    def __init__(self, celltype, interval, lower=(0.0, 0.0, 0.0), upper=(1.0, 1.0, 1.0),
+                 rotation=(0.0, 0.0, 0.0), first_node_gid=0, jitter=0.0, seed=20251015,
+                 rank=0, nranks=1):
+        L = lib()
+        box = FcgBox()
+        box.celltype = celltype
+        for d in range(3):
+            box.interval[d] = int(interval[d])
+            box.lower[d] = float(lower[d])
+            box.upper[d] = float(upper[d])
+            box.rotation[d] = float(rotation[d])
+        box.first_node_gid = int(first_node_gid)
+        box.jitter = float(jitter)
+        box.jitter_seed = int(seed)
+        self.box = box
+        self.celltype = celltype
+        self.npe = 8 if celltype == HEX8 else 27
+        self.rank, self.nranks = rank, nranks
+        h = ctypes.c_void_p()
+        rc = L.fcg_box_mesh_create(ctypes.byref(box), rank, nranks, ctypes.byref(h))
+        if rc != 0:
+            raise FcgError(rc, "fcg_box_mesh_create failed")
+        self._h = h
+        d = FcgDesc()
+        L.fcg_box_mesh_desc(h, LINEAR, 1.0, 0.0, 0, ctypes.byref(d))
+        self.n_ele, self.n_node = d.n_ele, d.n_node
+        self.n_rows, self.n_cols = d.n_rows, d.n_cols
+
+        def view(p, n, dt):
+            if n == 0:
+                return np.zeros(0, dtype=dt)
+            return np.ctypeslib.as_array(p, shape=(n,)).astype(dt, copy=True)
+
+        self.ele_nodes = view(d.ele_nodes, d.n_ele * self.npe, np.int32).reshape(-1, self.npe)
+        self.ele_gid = view(d.ele_gid, d.n_ele, np.int32)
+        self.node_x = view(d.node_x, d.n_node * 3, np.float64).reshape(-1, 3)
+        self.node_dof_col = view(d.node_dof_col, d.n_node, np.int32)
+        self.node_dof_row = view(d.node_dof_row, d.n_node, np.int32)
+        self.rowptr = view(d.rowptr, d.n_rows + 1, np.int64)
+        self.nnz = int(self.rowptr[-1]) if d.n_rows else 0
+        self.col_lid = view(d.col_lid, self.nnz, np.int32)
+        rg, cg, ng, no = _i32p(), _i32p(), _i64p(), _i32p()
+        L.fcg_box_mesh_maps(h, ctypes.byref(rg), ctypes.byref(cg), ctypes.byref(ng), ctypes.byref(no))
+        self.row_gid = view(rg, d.n_rows, np.int32)
+        self.col_gid = view(cg, d.n_cols, np.int32)
+        self.node_gid = view(ng, d.n_node, np.int64)
+        self.node_owner = view(no, d.n_node, np.int32)
+        ng_, nr_ = ctypes.c_int64(), ctypes.c_int64()
+        L.fcg_box_mesh_counts(h, ctypes.byref(ng_), ctypes.byref(nr_))
+        self.n_ele_global, self.n_ele_row = ng_.value, nr_.value
+        # the builder's arrays are copied; release the native mesh
+        L.fcg_box_mesh_destroy(h)
+        self._h = None
+
+    def desc(self, kinematics, youngs, poisson, device=0):
+        d = FcgDesc()
+        d.abi_version = ABI_VERSION
+        d.celltype = self.celltype
+        d.kinematics = kinematics
+        d.device = device
+        d.youngs = youngs
+        d.poisson = poisson
+        d.n_ele, d.n_node, d.n_rows, d.n_cols = self.n_ele, self.n_node, self.n_rows, self.n_cols
+        d.ele_nodes = _np_ptr(self.ele_nodes, _i32p)
+        d.ele_gid = _np_ptr(self.ele_gid, _i32p)
+        d.node_x = _np_ptr(self.node_x, _dp)
+        d.node_dof_col = _np_ptr(self.node_dof_col, _i32p)
+        d.node_dof_row = _np_ptr(self.node_dof_row, _i32p)
+        d.node_dof_kcol = None
+        d.rowptr = _np_ptr(self.rowptr, _i64p)
+        d.col_lid = _np_ptr(self.col_lid, _i32p)
+        return d
+
+    def node_displacement(self, amplitude):
+        """Synthetic state u(X) = A (sin2piX cospiY, sinpiY cos2piZ, sin2piZ cospiX)."""
+        X = self.node_x
+        u = np.empty_like(X)
+        u[:, 0] = np.sin(2 * np.pi * X[:, 0]) * np.cos(np.pi * X[:, 1])
+        u[:, 1] = np.sin(np.pi * X[:, 1]) * np.cos(2 * np.pi * X[:, 2])
+        u[:, 2] = np.sin(2 * np.pi * X[:, 2]) * np.cos(np.pi * X[:, 0])
+        return amplitude * u
+
+    def u_col(self, amplitude):
+        u = np.zeros(self.n_cols)
+        un = self.node_displacement(amplitude)
+        for d in range(3):
+            u[self.node_dof_col + d] = un[:, d]
+        return u
+
+
+class Evaluator:
+    """Device context (fcg_ctx): the MI355X replacement of Discretization::evaluate for SOLID
+    hex8/hex27 + StVK.  Keeps 4C's error behaviour: a non-zero status raises FcgError."""
+
+    def __init__(self, desc_or_mesh, kinematics=LINEAR, youngs=210.0, poisson=0.3, device=0):
+        L = lib()
+        if isinstance(desc_or_mesh, BoxMesh):
+            self._mesh = desc_or_mesh
+            desc = desc_or_mesh.desc(kinematics, youngs, poisson, device)
+        else:
+            self._mesh = None
+            desc = desc_or_mesh
+        self.device = desc.device
+        h = ctypes.c_void_p()
+        rc = L.fcg_create(ctypes.byref(desc), ctypes.byref(h))
+        if rc != 0:
+            raise FcgError(rc, L.fcg_last_error(None).decode())
+        self._h = h
+        info = FcgInfo()
+        L.fcg_get_info(h, ctypes.byref(info))
+        self.info = info
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().fcg_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _raise(self, rc, bad):
+        raise FcgError(rc, lib().fcg_last_error(self._h).decode(), bad)
+
+    def evaluate(self, action, u_col, fint_row, K_vals=None):
+        """Host-pointer path (blocking, `+=` semantics like SparseMatrix::assemble)."""
+        bad = ctypes.c_int32(-1)
+        rc = lib().fcg_evaluate(self._h, action, _np_ptr(u_col, _dp), _np_ptr(fint_row, _dp),
+                                _np_ptr(K_vals, _dp) if K_vals is not None else None,
+                                ctypes.byref(bad))
+        if rc != 0:
+            self._raise(rc, bad.value)
+
+    def evaluate_device(self, action, mode, u_col, fint_row, K_vals=None, stream=None):
+        """Device-resident path; tensors are float64 torch tensors on this device."""
+        bad = ctypes.c_int32(-1)
+        s = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
+        rc = lib().fcg_evaluate_device(self._h, action, mode, _tensor_ptr(u_col),
+                                       _tensor_ptr(fint_row), _tensor_ptr(K_vals), s,
+                                       ctypes.byref(bad))
+        if rc != 0:
+            self._raise(rc, bad.value)
+
+    def set_timing(self, enable):
+        lib().fcg_set_timing(self._h, 1 if enable else 0)
+
+    def timing(self):
+        a, b = ctypes.c_double(), ctypes.c_double()
+        lib().fcg_get_timing(self._h, ctypes.byref(a), ctypes.byref(b))
+        return a.value, b.value

@@ -1,0 +1,250 @@
+"""Benchmark: element evaluations/s and global-assembly wall time of 4C's SOLID hex8 linear
+elasticity path (BASELINE.json config 2: 1M hex8 per GPU, K and r assembled) on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
+
+One step = Discretization::set_state (row -> column import of the displacement; RCCL all-to-all
+of the ghost DOFs when N > 1) + Discretization::evaluate(struct_calc_nlnstiff) with zero() fused
+(K and f_int of the rank's owned rows written once) + the residual-norm all-reduce.
+Weak scaling: every rank owns a 100^3 hex8 box of the GridGenerator split (N=8 -> 200^3, 8M).
+Inputs (mesh, u) are resident in HBM before the timed region.  Synthetic data: grid-generator box
+[0,1]^3 scaled per rank count, interior jitter 0.1h (SplitMix64 seed 20251015),
+u = 1e-3 (sin2piX cospiY, sinpiY cos2piZ, sin2piZ cospiX), StVK E=210 nu=0.3.
+"""
+
+import argparse
+import json
+import os
+import platform
+import subprocess
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import importlib  # noqa: E402
+
+pkg = importlib.import_module("4c_amd")
+fcg = pkg.fcg
+halo = importlib.import_module("4c_amd.halo")
+
+HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+FP64_PEAK_TFS = 78.6      # MI355X FP64 vector (= matrix) spec, SURVEY.md §8d
+# SURVEY.md §8d algorithmic figures for hex8 linear K + r (per element)
+ALG_BYTES_PER_ELE = 2069.0
+ALG_FLOP_PER_ELE = 41.4e3
+
+
+def weak_interval(n, world):
+    """Global INTERVALS such that the GridGenerator box split gives every rank n^3 elements."""
+    iv = [n, n, n]
+    sub = [1, 1, 1]
+    w = world
+    f = 2
+    factors = []
+    while w > 1:
+        if w % f == 0:
+            factors.append(f)
+            w //= f
+        else:
+            f += 1
+    for fac in reversed(factors):
+        ratios = [iv[d] * 1.0 / sub[d] for d in range(3)]
+        d = int(np.argmax(ratios))  # first maximum, the reference's tie order
+        sub[d] *= fac
+        iv[d] = n * sub[d]
+    return tuple(iv)
+
+
+def cpu_baseline(n, kinem, threads):
+    """Oracle (4C-faithful restatement, oracle/) on the host cores: reference MPI semantics with
+    `threads` workers as ranks, each assembling its own rows.  Bounded sample: one evaluation of
+    the full n^3 mesh (about 10-30 s of CPU work in total)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+    import parity_util
+    import tempfile
+    out = os.path.join(tempfile.gettempdir(), f"liborc_native_{os.getpid()}.so")
+    flags = ["-march=native"]
+    oracle_lib.build(force=True, extra_flags=flags, out=out)
+    oracle_lib._lib = None
+    oracle_lib.load(out)
+    oracle_lib._lib = oracle_lib.load(out)
+    mesh = fcg.BoxMesh(fcg.HEX8, (n, n, n), jitter=0.1, seed=20251015)
+    u = mesh.u_col(1e-3)
+    # single-core rate on a small slab, then all-core on the full mesh
+    small = fcg.BoxMesh(fcg.HEX8, (n, n, max(2, n // 20)), jitter=0.1, seed=20251015)
+    us = small.u_col(1e-3)
+    t = time.perf_counter()
+    parity_util.oracle_evaluate(small, kinem, 210.0, 0.3, us, nworkers=1)
+    t1 = time.perf_counter() - t
+    t = time.perf_counter()
+    err, _, _, _ = parity_util.oracle_evaluate(mesh, kinem, 210.0, 0.3, u, nworkers=threads)
+    tn = time.perf_counter() - t
+    assert err == 0
+    try:
+        model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
+    except Exception:
+        model = platform.processor()
+    return {
+        "value": mesh.n_ele / tn, "unit": "element-evaluations/s", "cores": threads,
+        "kind": "port",
+        "sample": f"one struct_calc_nlnstiff evaluation of the full {n}^3 hex8 mesh "
+                  f"({mesh.n_ele} elements, K+r assembled), {threads} threads as ranks; "
+                  f"single-core {small.n_ele / t1:.4g} elem/s on {small.n_ele} elements",
+        "wall_s": tn, "single_core_value": small.n_ele / t1, "cpu_model": model,
+        "compiler": "gcc -O3 -march=native -fopenmp",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=100, help="elements per direction per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    iv = weak_interval(args.n, world)
+    t_setup = time.perf_counter()
+    mesh = fcg.BoxMesh(fcg.HEX8, iv, lower=(0.0, 0.0, 0.0),
+                       upper=(iv[0] / args.n, iv[1] / args.n, iv[2] / args.n),
+                       jitter=0.1, seed=20251015, rank=rank, nranks=world)
+    ev = fcg.Evaluator(mesh, kinematics=fcg.LINEAR, youngs=210.0, poisson=0.3, device=local)
+    t_setup = time.perf_counter() - t_setup
+
+    u_col_h = mesh.u_col(1e-3)
+    col_lid_of_row = {int(g): i for i, g in enumerate(mesh.col_gid)}
+    u_row = torch.from_numpy(u_col_h[[col_lid_of_row[int(g)] for g in mesh.row_gid]]).to(dev)
+    u_col = torch.zeros(mesh.n_cols, dtype=torch.float64, device=dev)
+    f = torch.zeros(mesh.n_rows, dtype=torch.float64, device=dev)
+    K = torch.zeros(mesh.nnz, dtype=torch.float64, device=dev)
+    imp = None
+    if world > 1:
+        imp = halo.HaloImport(mesh.row_gid, mesh.col_gid, halo.col_owner_of(mesh), rank, world, dev)
+    else:
+        u_col.copy_(torch.from_numpy(u_col_h).to(dev))
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        if imp is not None:
+            imp(u_row, u_col)
+        ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u_col, f, K, stream=stream)
+        return halo.residual_norm(f)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    ev.set_timing(True)
+    t_el, t_as = [], []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        a, b = ev.timing()
+        t_el.append(a)
+        t_as.append(b)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    ev.set_timing(False)
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = elapsed.item()
+    ms_step = 1e3 * elapsed / args.steps
+    n_ele_global = mesh.n_ele_global
+    value = n_ele_global / (elapsed / args.steps)
+
+    ms_el = float(np.mean(t_el))
+    ms_as = float(np.mean(t_as))
+    ms_kern = ms_el + ms_as
+    n_row_ele = mesh.n_ele_row
+    achieved = ALG_BYTES_PER_ELE * n_row_ele / (ms_kern * 1e-3) / 1e9
+    flops = ALG_FLOP_PER_ELE * n_row_ele / (ms_kern * 1e-3) / 1e12
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_r01.json")
+    if os.path.exists(pmc_path):
+        try:
+            pmc = json.load(open(pmc_path))
+            if pmc.get("workload") == f"hex8-linear-{args.n}^3-per-gpu":
+                traffic = pmc.get("hbm_bytes_per_evaluate")
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": "element-evaluations/sec (hex8 linear elasticity, K+r global assembly)",
+        "value": value,
+        "unit": "element-evaluations/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (GridGenerator box, jitter 0.1h, analytic displacement field)",
+        "config": {
+            "workload": f"hex8-linear-{args.n}^3-per-gpu",
+            "baseline_config": "BASELINE.json configs[1] (1M hex8, K and r on 1 MI355X)"
+                               if world == 1 else "BASELINE.json configs[3] (weak-scaled, RCCL)",
+            "global_intervals": list(iv),
+            "elements_global": n_ele_global,
+            "elements_evaluated_per_gpu": mesh.n_ele,
+            "dofs_owned_rank0": mesh.n_rows,
+            "nnz_rank0": mesh.nnz,
+            "material": "StVenantKirchhoff E=210 nu=0.3",
+            "assembly": "zero+assemble fused (FCG_OVERWRITE), owned rows, no atomics",
+            "parallelism": f"element partition x{world} (GridGenerator box split, ghost layer, "
+                           f"RCCL halo all-to-all)" if world > 1 else "single GPU",
+            "setup_s_rank0": t_setup,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "element_kernel + assemble_kernel (one evaluate)",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "alg_bytes_per_element": ALG_BYTES_PER_ELE,
+            "ms_element_kernel": ms_el,
+            "ms_assemble_kernel": ms_as,
+            "fp64_tflops_alg": flops,
+            "fp64_frac": flops / FP64_PEAK_TFS,
+        },
+        "assembly_wall_ms": ms_step,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(args.n, fcg.LINEAR, args.cpu_threads)
+        except Exception as e:  # report, never hide
+            out["cpu_baseline"] = {"value": None, "error": repr(e)}
+    if rank == 0:
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

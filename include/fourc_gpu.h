@@ -1,0 +1,172 @@
+/*
+ * fourc_gpu.h -- C ABI of the MI355X-native solid element evaluation + global assembly path.
+ *
+ * Drop-in boundary for 4C's
+ *   Core::FE::Discretization::evaluate(params, systemmatrix1, systemmatrix2,
+ *                                      systemvector1, systemvector2, systemvector3)
+ *     (src/core/fem/src/discretization/4C_fem_discretization_evaluate.cpp:31-61,65-103)
+ * for the actions struct_calc_nlnstiff / struct_calc_internalforce
+ *     (src/core/legacy_enum_definitions/4C_legacy_enum_definitions_element_actions.hpp:19-75)
+ * of SOLID hex8 / hex27 elements with DisplacementBased(LinearKinematics)Formulation and
+ * Mat::StVenantKirchhoff (src/solid_3D_ele/4C_solid_3D_ele_evaluate.cpp:57-117,
+ * src/solid_3D_ele/4C_solid_3D_ele_calc.cpp:110-240, src/mat/4C_mat_stvenantkirchhoff.cpp:169-177).
+ *
+ * The element loop, the Gauss-point loop and SparseMatrix::assemble / LinAlg::assemble(Vector)
+ * (src/core/linalg/src/sparse/4C_linalg_sparsematrix.cpp:426-576,
+ *  src/core/linalg/src/sparse/4C_linalg_utils_sparse_algebra_assemble.cpp:72-92) run as HIP
+ * kernels on gfx950.  Plain pointers and sizes only; no torch/HIP types in the signatures.
+ * See INTEGRATION.md for the 4C-side binding.
+ */
+#ifndef FOURC_GPU_H
+#define FOURC_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FCG_ABI_VERSION 1
+
+/* Cell types (Core::FE::CellType::hex8 / hex27) */
+enum fcg_celltype { FCG_HEX8 = 0, FCG_HEX27 = 1 };
+/* Kinematics (Inpar::Solid::KinemType::linear / nonlinearTotLag) */
+enum fcg_kinem { FCG_LINEAR = 0, FCG_TOTLAG = 1 };
+/* Actions (Core::Elements::ActionType struct_calc_nlnstiff / struct_calc_internalforce) */
+enum fcg_action { FCG_CALC_NLNSTIFF = 0, FCG_CALC_INTERNALFORCE = 1 };
+/* Assembly mode: ACCUMULATE is the reference's `+=` into caller-zeroed storage
+ * (SparseMatrix::assemble); OVERWRITE fuses SparseMatrix::zero() + assemble
+ * (4C_structure_new_model_evaluator_structure.cpp:143-151 followed by evaluate): every owned
+ * row is written exactly once, untouched entries become 0. */
+enum fcg_mode { FCG_ACCUMULATE = 0, FCG_OVERWRITE = 1 };
+
+/* Return codes.  The host shim turns non-zero codes into exceptions, like FOUR_C_THROW. */
+enum fcg_status {
+  FCG_OK = 0,
+  FCG_ERR_NODAL_DETJ = 1,   /* det J <= 0 at an element node (4C_solid_3D_ele_calc_lib.hpp:475-496) */
+  FCG_ERR_SINGULAR = 2,     /* det == 0 in invert3x3 (4C_linalg_fixedsizematrix.hpp:1394) */
+  FCG_ERR_ARG = 3,          /* invalid argument / unsupported layout */
+  FCG_ERR_DEVICE = 4        /* HIP / RCCL failure */
+};
+
+/*
+ * Everything the element loop needs from a 4C discretization on ONE rank, in the rank's local
+ * numbering.  All arrays are host memory and are copied; nothing is retained after fcg_create.
+ *   - column elements (owned + ghost, 4C_fem_discretization_evaluate.cpp:83) with their local
+ *     column-node ids in 4C node order;
+ *   - column nodes with reference coordinates, the column-map LID of their first DOF
+ *     (Map::LID of DofSet::dof(node, 0); DOFs of a node are consecutive LIDs) and, if the node is
+ *     owned (lmowner == myrank), the row-map LID of its first DOF, else -1;
+ *   - the CSR graph of the Epetra_CrsMatrix after FillComplete (ExtractCrsDataPointers): int64
+ *     row pointers over the owned DOF rows and int32 column LIDs sorted within each row.
+ */
+typedef struct fcg_desc {
+  int32_t abi_version;    /* FCG_ABI_VERSION */
+  int32_t celltype;       /* fcg_celltype */
+  int32_t kinematics;     /* fcg_kinem */
+  int32_t device;         /* HIP device ordinal */
+  double youngs;          /* MAT_Struct_StVenantKirchhoff YOUNG (> 0) */
+  double poisson;         /* NUE, in [-1, 0.5) */
+  int64_t n_ele;          /* column elements */
+  int64_t n_node;         /* column nodes */
+  int64_t n_rows;         /* owned DOF rows (dof row map size) */
+  int64_t n_cols;         /* dof column map size (length of u_col) */
+  const int32_t* ele_nodes;    /* [n_ele][nodes per element] column-node ids */
+  const int32_t* ele_gid;      /* [n_ele] element GIDs (error reporting); may be NULL */
+  const double* node_x;        /* [n_node][3] reference coordinates */
+  const int32_t* node_dof_col; /* [n_node] column LID of the node's first DOF */
+  const int32_t* node_dof_row; /* [n_node] row LID of the node's first DOF, -1 if not owned */
+  const int32_t* node_dof_kcol;/* [n_node] LID of the node's first DOF in the MATRIX column map
+                                  (Epetra_CrsMatrix::ColMap after FillComplete); NULL = same as
+                                  node_dof_col */
+  const int64_t* rowptr;       /* [n_rows + 1] */
+  const int32_t* col_lid;      /* [rowptr[n_rows]] */
+} fcg_desc;
+
+typedef struct fcg_ctx fcg_ctx;
+
+/* Builds the device-resident mirror of the element set and the assembly plan
+ * (the "FillComplete" of this path).  Returns FCG_OK and *out, or an error code. */
+int fcg_create(const fcg_desc* desc, fcg_ctx** out);
+int fcg_destroy(fcg_ctx* ctx);
+/* Text of the last error on this context (or of the last failed fcg_create when ctx == NULL). */
+const char* fcg_last_error(const fcg_ctx* ctx);
+
+/*
+ * Discretization::evaluate on host buffers (blocking, reference semantics):
+ *   u_col    [n_cols]   displacement column vector (Discretization::set_state("displacement"))
+ *   fint_row [n_rows]   systemvector1, += on owned rows
+ *   K_vals   [nnz]      systemmatrix1 values in the CSR order of desc->col_lid, += (may be NULL
+ *                       for FCG_CALC_INTERNALFORCE)
+ *   bad_ele_gid         on FCG_ERR_NODAL_DETJ / FCG_ERR_SINGULAR: GID of the failing element
+ */
+int fcg_evaluate(fcg_ctx* ctx, int action, const double* u_col, double* fint_row, double* K_vals,
+    int32_t* bad_ele_gid);
+
+/*
+ * The same on device-resident buffers (HBM) for a GPU-resident Newton loop.
+ *   mode    fcg_mode (ACCUMULATE = +=, OVERWRITE = zero + assemble fused)
+ *   stream  hipStream_t to run on (NULL = the context's own stream); the call returns after the
+ *           stream has drained (matching the synchronous Newton loop of the reference).
+ */
+int fcg_evaluate_device(fcg_ctx* ctx, int action, int mode, const double* d_u_col,
+    double* d_fint_row, double* d_K_vals, void* stream, int32_t* bad_ele_gid);
+
+/* Device allocations owned by the caller (convenience for hosts without a HIP toolchain). */
+int fcg_device_alloc(int device, int64_t bytes, void** d_ptr);
+int fcg_device_free(void* d_ptr);
+int fcg_memcpy_h2d(void* d_dst, const void* h_src, int64_t bytes);
+int fcg_memcpy_d2h(void* h_dst, const void* d_src, int64_t bytes);
+int fcg_memset_device(void* d_dst, int value, int64_t bytes);
+
+/* Per-kernel timing of the last evaluate on the context stream, measured with hipEvents
+ * (enable before the call).  names: "element", "assemble"; returns the count written. */
+int fcg_set_timing(fcg_ctx* ctx, int enable);
+int fcg_get_timing(const fcg_ctx* ctx, double* ms_element, double* ms_assemble);
+
+/* Sizes of what fcg_create built (for roofline bookkeeping). */
+typedef struct fcg_info {
+  int64_t n_ele, n_node, n_rows, n_cols, nnz;
+  int64_t n_incidences;     /* (element, owned local node) pairs */
+  int64_t scratch_bytes;    /* device scratch for element block-rows */
+  int64_t device_bytes;     /* total device memory held by the context */
+} fcg_info;
+int fcg_get_info(const fcg_ctx* ctx, fcg_info* info);
+
+/* ------------------------------------------------------------------------------------------
+ * Structured-box discretization builder: a restatement of 4C's GridGenerator
+ * (src/core/io/src/4C_io_gridgenerator.cpp:41-392), node ownership of Rebalance::build_graph
+ * (src/core/rebalance/src/4C_rebalance_graph_based.cpp:159-215), DofSet numbering
+ * (src/core/fem/src/dofset/4C_fem_dofset.cpp:343-351) and the Epetra graph after FillComplete.
+ * It produces exactly what a 4C rank would hand to fcg_create, for synthetic meshes.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct fcg_box {
+  int32_t celltype;        /* FCG_HEX8 / FCG_HEX27 */
+  int32_t interval[3];     /* INTERVALS */
+  double lower[3];         /* LOWER_BOUND */
+  double upper[3];         /* UPPER_BOUND */
+  double rotation[3];      /* ROTATION (degrees) */
+  int64_t first_node_gid;  /* node_gid_of_first_new_node */
+  double jitter;           /* interior-node jitter as a fraction of h (0 = none) */
+  uint64_t jitter_seed;    /* SplitMix64 seed */
+} fcg_box;
+
+typedef struct fcg_box_mesh fcg_box_mesh;
+
+/* Builds rank `rank` of `nranks` (PARTITION structured box split). */
+int fcg_box_mesh_create(const fcg_box* box, int rank, int nranks, fcg_box_mesh** out);
+int fcg_box_mesh_destroy(fcg_box_mesh* m);
+/* Fills a descriptor that points into the mesh's arrays (valid while the mesh lives). */
+int fcg_box_mesh_desc(const fcg_box_mesh* m, int kinematics, double youngs, double poisson,
+    int device, fcg_desc* out);
+/* Global numbering of the rank's maps: DOF GIDs of the row map [n_rows] and column map [n_cols],
+ * node GIDs of the column nodes [n_node], owner rank of each column node [n_node]. */
+int fcg_box_mesh_maps(const fcg_box_mesh* m, const int32_t** row_gid, const int32_t** col_gid,
+    const int64_t** node_gid, const int32_t** node_owner);
+/* Total number of elements (all ranks) and owned (row) elements of this rank. */
+int fcg_box_mesh_counts(const fcg_box_mesh* m, int64_t* n_ele_global, int64_t* n_ele_row);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FOURC_GPU_H */

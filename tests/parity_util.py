@@ -1,0 +1,60 @@
+"""Shared helpers for the parity tests: run the CPU oracle on a BoxMesh's discretization.
+TEST INFRASTRUCTURE ONLY."""
+
+import ctypes
+import importlib
+
+import numpy as np
+
+import oracle_lib as orc
+
+fcg = importlib.import_module("4c_amd").fcg
+
+
+def gid_maps(row_gid, col_gid):
+    max_gid = int(max(row_gid.max(initial=0), col_gid.max(initial=0)))
+    row_lid = np.full(max_gid + 1, -1, dtype=np.int32)
+    col_lid = np.full(max_gid + 1, -1, dtype=np.int32)
+    row_lid[row_gid] = np.arange(len(row_gid), dtype=np.int32)
+    col_lid[col_gid] = np.arange(len(col_gid), dtype=np.int32)
+    return row_lid, col_lid, max_gid
+
+
+def oracle_evaluate(mesh, kinem, E, nu, u_col, want_k=True, nworkers=1, min_node_gid=0):
+    """Oracle Discretization::evaluate on mesh's rank: returns (err, bad_ele, K_vals, fint).
+
+    The oracle evaluates the rank's column elements and assembles the rows the rank owns, in the
+    CSR pattern (rowptr/col_lid) and maps (row_gid/col_gid) of `mesh`.
+    """
+    lib = orc.load()
+    row_lid, col_lid, max_gid = gid_maps(mesh.row_gid, mesh.col_gid)
+    K = np.zeros(mesh.nnz) if want_k else None
+    f = np.zeros(mesh.n_rows)
+    csr = orc.OrcCsr()
+    csr.n_rows = mesh.n_rows
+    csr.rowptr = mesh.rowptr.ctypes.data_as(orc._i64p)
+    csr.col_lid = mesh.col_lid.ctypes.data_as(orc._i32p)
+    csr.vals = K.ctypes.data_as(orc._dp) if want_k else None
+    csr.row_lid_of_gid = row_lid.ctypes.data_as(orc._i32p)
+    csr.col_lid_of_gid = col_lid.ctypes.data_as(orc._i32p)
+    csr.max_gid = max_gid
+    ele_nodes = mesh.ele_nodes.astype(np.int64)
+    # owner: the mesh rank's owned nodes are split into `nworkers` contiguous chunks (z-slabs,
+    # since owned nodes are gid-ordered), each run as its own oracle "rank"; ghosts belong to none
+    owned = mesh.node_dof_row >= 0
+    owner = np.full(mesh.n_node, -1, dtype=np.int32)
+    idx = np.nonzero(owned)[0]
+    owner[idx] = (np.arange(len(idx)) * nworkers // max(len(idx), 1)).astype(np.int32)
+    bad = ctypes.c_int64(-1)
+    err = lib.orc_discretization_evaluate(
+        mesh.celltype, kinem, E, nu, mesh.n_ele, ele_nodes.ctypes.data_as(orc._i64p), mesh.n_node,
+        np.ascontiguousarray(mesh.node_x).ctypes.data_as(orc._dp),
+        mesh.node_gid.ctypes.data_as(orc._i64p), owner.ctypes.data_as(orc._i32p), min_node_gid,
+        nworkers, u_col.ctypes.data_as(orc._dp), ctypes.byref(csr), f.ctypes.data_as(orc._dp),
+        ctypes.byref(bad))
+    return err, bad.value, K, f
+
+
+def rel_err(a, b):
+    nb = np.linalg.norm(b)
+    return np.linalg.norm(a - b) / (nb if nb > 0 else 1.0)

