@@ -102,7 +102,7 @@ struct fcg_box_mesh {
   fcg_box box;
   int rank = 0, nranks = 1, npe = 8;
   int64_t n_ele_global = 0, n_ele_row = 0;
-  std::vector<int32_t> ele_nodes, ele_gid;
+  std::vector<int32_t> ele_nodes, ele_gid, ele_ijk;
   std::vector<double> node_x;
   std::vector<int64_t> node_gid;
   std::vector<int32_t> node_owner, node_dof_col, node_dof_row;
@@ -253,6 +253,14 @@ int fcg_box_mesh_create(const fcg_box* box, int rank, int nranks, fcg_box_mesh**
   // element connectivity in local column-node ids
   m->ele_nodes.resize(nce * npe);
   m->ele_gid.resize(nce);
+  m->ele_ijk.resize(3 * nce);
+  for (int64_t e = 0; e < nce; ++e)
+  {
+    // lattice position of the element (4C_io_gridgenerator.cpp:336-338)
+    m->ele_ijk[3 * e + 0] = int32_t(col_ele[e] % IX);
+    m->ele_ijk[3 * e + 1] = int32_t((col_ele[e] / IX) % IY);
+    m->ele_ijk[3 * e + 2] = int32_t(col_ele[e] / (IX * IY));
+  }
   for (int64_t e = 0; e < nce; ++e)
   {
     m->ele_gid[e] = int32_t(col_ele[e]);
@@ -348,6 +356,8 @@ int fcg_box_mesh_desc(const fcg_box_mesh* m, int kinematics, double youngs, doub
   o->node_dof_col = m->node_dof_col.data();
   o->node_dof_row = m->node_dof_row.data();
   o->node_dof_kcol = nullptr;
+  o->ele_ijk = m->ele_ijk.data();
+  o->path = FCG_PATH_AUTO;
   o->rowptr = m->rowptr.data();
   o->col_lid = m->col_lid.data();
   return FCG_OK;

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <atomic>
 #include <cstring>
 #include <mutex>
@@ -21,6 +22,7 @@
 #include <vector>
 
 #include "fcg_internal.hpp"
+#include "fcg_shape.hpp"
 
 namespace {
 
@@ -67,10 +69,182 @@ hipError_t upload(T** dst, const T* src, int64_t n, int64_t& bytes)
   return hipSuccess;
 }
 
+// Structured plan (fused hex8 kernel).  Verifies the lattice hint against the connectivity:
+// every element node must sit at lattice position ijk(e) + offset(a) consistently across
+// elements, no two elements/nodes may share a position, and every owned node row must hold
+// exactly the DOF triples of its existing lattice neighbours.
+struct StructHost {
+  int32_t lo[3] = {0, 0, 0}, n[3] = {0, 0, 0};    // owned-node box
+  int32_t elo[3] = {0, 0, 0}, en[3] = {0, 0, 0};  // column-element box
+  int32_t tiles_x = 0, tiles_y = 0, tiles_z = 0, seg = 0;
+  std::vector<int32_t> elem_at, rownode_at;
+  std::vector<uint16_t> nbr_pos;
+};
+
+const int kOff8[8][3] = {{0, 0, 0}, {1, 0, 0}, {1, 1, 0}, {0, 1, 0}, {0, 0, 1}, {1, 0, 1}, {1, 1, 1},
+    {0, 1, 1}};  // hex8 4C node order (4C_io_gridgenerator.cpp:371-379)
+
+bool build_structured_plan(const fcg_desc* d, const std::vector<int32_t>& rownodes,
+    const std::vector<int32_t>& row0, const int32_t* kcol, StructHost& P, std::string& why)
+{
+  if (d->celltype != FCG_HEX8 || !d->ele_ijk)
+  {
+    why = "no lattice hint, or not hex8";
+    return false;
+  }
+  if (d->n_ele == 0 || rownodes.empty())
+  {
+    why = "nothing to evaluate";
+    return false;
+  }
+  int64_t mn[3], mx[3];
+  for (int k = 0; k < 3; ++k)
+  {
+    mn[k] = INT32_MAX;
+    mx[k] = INT32_MIN;
+  }
+  for (int64_t e = 0; e < d->n_ele; ++e)
+    for (int k = 0; k < 3; ++k)
+    {
+      mn[k] = std::min<int64_t>(mn[k], d->ele_ijk[3 * e + k]);
+      mx[k] = std::max<int64_t>(mx[k], d->ele_ijk[3 * e + k]);
+    }
+  const int64_t EX = mx[0] - mn[0] + 1, EY = mx[1] - mn[1] + 1, EZ = mx[2] - mn[2] + 1;
+  if ((EX + 1) * (EY + 1) * (EZ + 1) > 8 * d->n_ele + 4096)
+  {
+    why = "element lattice box far larger than the element set";
+    return false;
+  }
+  P.elo[0] = int32_t(mn[0]); P.elo[1] = int32_t(mn[1]); P.elo[2] = int32_t(mn[2]);
+  P.en[0] = int32_t(EX); P.en[1] = int32_t(EY); P.en[2] = int32_t(EZ);
+  P.elem_at.assign(EX * EY * EZ, -1);
+  for (int64_t e = 0; e < d->n_ele; ++e)
+  {
+    const int64_t idx = ((d->ele_ijk[3 * e + 2] - mn[2]) * EY + (d->ele_ijk[3 * e + 1] - mn[1])) * EX +
+                        (d->ele_ijk[3 * e] - mn[0]);
+    if (P.elem_at[idx] != -1)
+    {
+      why = "two elements at one lattice position";
+      return false;
+    }
+    P.elem_at[idx] = int32_t(e);
+  }
+  // node lattice positions, relative to the element box origin, in [0, E+1)
+  const int64_t NXn = EX + 1, NYn = EY + 1, NZn = EZ + 1;
+  std::vector<int64_t> npos(d->n_node, -1);
+  for (int64_t e = 0; e < d->n_ele; ++e)
+  {
+    const int64_t ex = d->ele_ijk[3 * e] - mn[0], ey = d->ele_ijk[3 * e + 1] - mn[1],
+                  ez = d->ele_ijk[3 * e + 2] - mn[2];
+    for (int a = 0; a < 8; ++a)
+    {
+      const int64_t p = ((ez + kOff8[a][2]) * NYn + ey + kOff8[a][1]) * NXn + ex + kOff8[a][0];
+      const int32_t node = d->ele_nodes[8 * e + a];
+      if (npos[node] == -1)
+        npos[node] = p;
+      else if (npos[node] != p)
+      {
+        why = "connectivity does not match the lattice hint";
+        return false;
+      }
+    }
+  }
+  std::vector<int32_t> node_at(NXn * NYn * NZn, -1);
+  for (int64_t nd = 0; nd < d->n_node; ++nd)
+  {
+    if (npos[nd] < 0) continue;
+    if (node_at[npos[nd]] != -1)
+    {
+      why = "two nodes at one lattice position";
+      return false;
+    }
+    node_at[npos[nd]] = int32_t(nd);
+  }
+  // owned-node box
+  int64_t lo[3] = {INT64_MAX, INT64_MAX, INT64_MAX}, hi[3] = {-1, -1, -1};
+  for (int32_t nd : rownodes)
+  {
+    if (npos[nd] < 0)
+    {
+      why = "owned node outside every column element";
+      return false;
+    }
+    const int64_t q[3] = {npos[nd] % NXn, (npos[nd] / NXn) % NYn, npos[nd] / (NXn * NYn)};
+    for (int k = 0; k < 3; ++k)
+    {
+      lo[k] = std::min(lo[k], q[k]);
+      hi[k] = std::max(hi[k], q[k]);
+    }
+  }
+  for (int k = 0; k < 3; ++k)
+  {
+    P.lo[k] = int32_t(lo[k] + mn[k]);  // in the hint's lattice coordinates
+    P.n[k] = int32_t(hi[k] - lo[k] + 1);
+  }
+  P.rownode_at.assign(int64_t(P.n[0]) * P.n[1] * P.n[2], -1);
+  for (size_t r = 0; r < rownodes.size(); ++r)
+  {
+    const int64_t p = npos[rownodes[r]];
+    const int64_t q[3] = {p % NXn - lo[0], (p / NXn) % NYn - lo[1], p / (NXn * NYn) - lo[2]};
+    P.rownode_at[(q[2] * P.n[1] + q[1]) * P.n[0] + q[0]] = int32_t(r);
+  }
+  // neighbour column positions per owned node row
+  const int64_t nrn = int64_t(rownodes.size());
+  P.nbr_pos.assign(nrn * 27, 0xFFFF);
+  std::string err;
+  std::mutex err_m;
+  parallel_for(nrn, [&](int64_t r) {
+    const int64_t p = npos[rownodes[r]];
+    const int64_t i = p % NXn, jj = (p / NXn) % NYn, k = p / (NXn * NYn);
+    const int64_t s = d->rowptr[row0[r]];
+    const int64_t len = d->rowptr[row0[r] + 1] - s;
+    const int32_t* cols = d->col_lid + s;
+    int count = 0;
+    for (int t = 0; t < 27; ++t)
+    {
+      const int64_t x = i + t % 3 - 1, y = jj + (t / 3) % 3 - 1, z = k + t / 9 - 1;
+      if (x < 0 || x >= NXn || y < 0 || y >= NYn || z < 0 || z >= NZn) continue;
+      const int32_t m = node_at[(z * NYn + y) * NXn + x];
+      if (m < 0) continue;
+      const int32_t c = kcol[m];
+      const int32_t* it = std::lower_bound(cols, cols + len, c);
+      const int64_t pos = it - cols;
+      if (it == cols + len || *it != c || pos + 3 > len || cols[pos + 1] != c + 1 ||
+          cols[pos + 2] != c + 2)
+      {
+        std::lock_guard<std::mutex> lk(err_m);
+        err = "row lacks a lattice neighbour's DOF triple";
+        return;
+      }
+      P.nbr_pos[r * 27 + t] = uint16_t(pos);
+      ++count;
+    }
+    if (3 * count != len)
+    {
+      std::lock_guard<std::mutex> lk(err_m);
+      err = "row holds columns beyond the lattice neighbours";
+    }
+  });
+  if (!err.empty())
+  {
+    why = err;
+    return false;
+  }
+  // tiles: 4 x 4 node columns, z split into segments for >= ~8 workgroups per CU
+  P.tiles_x = (P.n[0] + 3) / 4;
+  P.tiles_y = (P.n[1] + 3) / 4;
+  const int64_t txy = int64_t(P.tiles_x) * P.tiles_y;
+  int64_t nseg = std::max<int64_t>(1, std::min<int64_t>(P.n[2], (2048 + txy - 1) / txy));
+  P.seg = int32_t((P.n[2] + nseg - 1) / nseg);
+  P.tiles_z = (P.n[2] + P.seg - 1) / P.seg;
+  return true;
+}
+
 void free_mesh(fcg::DeviceMesh& m)
 {
   void* ptrs[] = {m.ele_nodes, m.ele_gid, m.node_x, m.node_dof_col, m.inc_of, m.inc_ptr,
-      m.rownode_row0, m.inc_pos, m.rowptr, m.scratch, m.err};
+      m.rownode_row0, m.inc_pos, m.rowptr, m.scratch, m.err, m.elem_at, m.rownode_at, m.nbr_pos,
+      m.tables};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   m = fcg::DeviceMesh{};
@@ -184,9 +358,23 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
     return FCG_ERR_ARG;
   }
 
-  // --- incidences grouped by owned node
+  // --- structured (fused) plan when a verified lattice hint is present
+  StructHost sp;
+  std::string why;
+  bool structured = false;
+  if (d->path != FCG_PATH_GENERAL)
+  {
+    structured = build_structured_plan(d, rownodes, row0, kcol, sp, why);
+    if (!structured && d->path == FCG_PATH_STRUCTURED)
+    {
+      set_create_error("structured path requested but the lattice hint does not verify: " + why);
+      return FCG_ERR_ARG;
+    }
+  }
+
+  // --- incidences grouped by owned node (general path)
   std::vector<int64_t> inc_ptr(nrn + 1, 0);
-  for (int64_t i = 0; i < d->n_ele * npe; ++i)
+  for (int64_t i = 0; i < (structured ? 0 : d->n_ele * npe); ++i)
   {
     const int32_t rn = rn_of_node[d->ele_nodes[i]];
     if (rn >= 0) inc_ptr[rn + 1]++;
@@ -198,9 +386,10 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
     set_create_error("too many incidences for one context (> 2^31)");
     return FCG_ERR_ARG;
   }
-  std::vector<int32_t> inc_of(d->n_ele * npe, -1);
+  std::vector<int32_t> inc_of(structured ? 0 : d->n_ele * npe, -1);
   std::vector<int32_t> inc_ele(n_inc);
   std::vector<uint8_t> inc_a(n_inc);
+  if (!structured)
   {
     std::vector<int64_t> fill(inc_ptr.begin(), inc_ptr.end() - 1);
     for (int64_t e = 0; e < d->n_ele; ++e)
@@ -216,7 +405,7 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
   }
   // --- positions of every element node's DOF triple inside the row (stride fast path)
   std::vector<uint16_t> inc_pos(n_inc * npe);
-  parallel_for(nrn, [&](int64_t r) {
+  parallel_for(structured ? 0 : nrn, [&](int64_t r) {
     const int64_t s = d->rowptr[row0[r]];
     const int64_t len = d->rowptr[row0[r] + 1] - s;
     const int32_t* cols = d->col_lid + s;
@@ -291,13 +480,40 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
   chk(upload(&m.ele_gid, d->ele_gid ? d->ele_gid : eg.data(), d->n_ele, bytes));
   chk(upload(&m.node_x, d->node_x, d->n_node * 3, bytes));
   chk(upload(&m.node_dof_col, d->node_dof_col, d->n_node, bytes));
-  chk(upload(&m.inc_of, inc_of.data(), d->n_ele * npe, bytes));
-  chk(upload(&m.inc_ptr, inc_ptr.data(), nrn + 1, bytes));
   chk(upload(&m.rownode_row0, row0.data(), nrn, bytes));
-  chk(upload(&m.inc_pos, inc_pos.data(), n_inc * npe, bytes));
   chk(upload(&m.rowptr, d->rowptr, d->n_rows + 1, bytes));
-  chk(upload<double>(&m.scratch, nullptr, n_inc * fcg::record_doubles(npe), bytes));
   chk(upload<int32_t>(&m.err, nullptr, 2, bytes));
+  if (structured)
+  {
+    m.path = FCG_PATH_STRUCTURED;
+    m.tiles_x = sp.tiles_x;
+    m.tiles_y = sp.tiles_y;
+    m.tiles_z = sp.tiles_z;
+    m.seg_planes = sp.seg;
+    m.I0 = sp.lo[0]; m.J0 = sp.lo[1]; m.K0 = sp.lo[2];
+    m.NI = sp.n[0]; m.NJ = sp.n[1]; m.NK = sp.n[2];
+    m.EX0 = sp.elo[0]; m.EY0 = sp.elo[1]; m.EZ0 = sp.elo[2];
+    m.EX = sp.en[0]; m.EY = sp.en[1]; m.EZ = sp.en[2];
+    chk(upload(&m.elem_at, sp.elem_at.data(), int64_t(sp.elem_at.size()), bytes));
+    chk(upload(&m.rownode_at, sp.rownode_at.data(), int64_t(sp.rownode_at.size()), bytes));
+    chk(upload(&m.nbr_pos, sp.nbr_pos.data(), int64_t(sp.nbr_pos.size()), bytes));
+    std::vector<double> tab(8 * 8 * 3 * 2 + 8);
+    double xi[81], w[27], xn[81];
+    fcg::gauss_rule(fcg::kHex8, xi, w);
+    fcg::node_param_coords(fcg::kHex8, xn);
+    for (int g = 0; g < 8; ++g) fcg::shape_deriv(fcg::kHex8, &xi[3 * g], &tab[24 * g]);
+    for (int g = 0; g < 8; ++g) fcg::shape_deriv(fcg::kHex8, &xn[3 * g], &tab[192 + 24 * g]);
+    for (int g = 0; g < 8; ++g) tab[384 + g] = w[g];
+    chk(upload(&m.tables, tab.data(), int64_t(tab.size()), bytes));
+  }
+  else
+  {
+    m.path = FCG_PATH_GENERAL;
+    chk(upload(&m.inc_of, inc_of.data(), d->n_ele * npe, bytes));
+    chk(upload(&m.inc_ptr, inc_ptr.data(), nrn + 1, bytes));
+    chk(upload(&m.inc_pos, inc_pos.data(), n_inc * npe, bytes));
+    chk(upload<double>(&m.scratch, nullptr, n_inc * fcg::record_doubles(npe), bytes));
+  }
   for (auto& ev : ctx->timing.ev) chk(hipEventCreate(&ev));
   if (he != hipSuccess)
   {
@@ -344,10 +560,19 @@ int fcg_evaluate_device(fcg_ctx* ctx, int action, int mode, const double* d_u_co
   hipError_t he = hipMemcpyAsync(m.err, init, sizeof(init), hipMemcpyHostToDevice, s);
   auto& T = ctx->timing;
   if (T.enabled && he == hipSuccess) he = hipEventRecord(T.ev[0], s);
-  if (he == hipSuccess) he = fcg::launch_element(m, d_u_col, want_k, s);
-  if (T.enabled && he == hipSuccess) he = hipEventRecord(T.ev[1], s);
-  if (he == hipSuccess)
-    he = fcg::launch_assemble(m, want_k, mode == FCG_OVERWRITE, d_K_vals, d_fint_row, s);
+  if (m.path == FCG_PATH_STRUCTURED)
+  {
+    if (he == hipSuccess)
+      he = fcg::launch_fused_h8(m, d_u_col, want_k, mode == FCG_OVERWRITE, d_K_vals, d_fint_row, s);
+    if (T.enabled && he == hipSuccess) he = hipEventRecord(T.ev[1], s);
+  }
+  else
+  {
+    if (he == hipSuccess) he = fcg::launch_element(m, d_u_col, want_k, s);
+    if (T.enabled && he == hipSuccess) he = hipEventRecord(T.ev[1], s);
+    if (he == hipSuccess)
+      he = fcg::launch_assemble(m, want_k, mode == FCG_OVERWRITE, d_K_vals, d_fint_row, s);
+  }
   if (T.enabled && he == hipSuccess) he = hipEventRecord(T.ev[2], s);
   int32_t errv[2] = {0, INT32_MAX};
   if (he == hipSuccess) he = hipMemcpyAsync(errv, m.err, sizeof(errv), hipMemcpyDeviceToHost, s);
@@ -439,6 +664,7 @@ int fcg_get_info(const fcg_ctx* ctx, fcg_info* info)
   info->n_incidences = m.n_inc;
   info->scratch_bytes = m.n_inc * fcg::record_doubles(m.npe) * int64_t(sizeof(double));
   info->device_bytes = ctx->device_bytes;
+  info->path = m.path;
   return FCG_OK;
 }
 

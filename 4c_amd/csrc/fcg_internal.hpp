@@ -33,7 +33,21 @@ struct DeviceMesh {
   double* scratch = nullptr;        // [n_inc][record_doubles(npe)]
   int32_t* err = nullptr;           // [2]: code, min failing element index
   int32_t max_rowlen = 0;
+
+  // structured (fused z-sweep) plan, hex8 only
+  int path = FCG_PATH_GENERAL;
+  int32_t tiles_x = 0, tiles_y = 0, tiles_z = 0, seg_planes = 0;
+  int32_t I0 = 0, J0 = 0, K0 = 0, NI = 0, NJ = 0, NK = 0;  // owned-node lattice box
+  int32_t EX0 = 0, EY0 = 0, EZ0 = 0, EX = 0, EY = 0, EZ = 0;  // column-element lattice box
+  int32_t* elem_at = nullptr;       // [EZ][EY][EX] column element or -1
+  int32_t* rownode_at = nullptr;    // [NK][NJ][NI] row node or -1
+  uint16_t* nbr_pos = nullptr;      // [n_rownodes][27] column position of neighbour t, 0xFFFF absent
+  double* tables = nullptr;         // dN at GPs [192], dN at nodes [192], weights [8]
 };
+
+// Launches the fused hex8 kernel (element evaluation + LDS row accumulation + row flush).
+hipError_t launch_fused_h8(const DeviceMesh& m, const double* d_u_col, bool want_k,
+    bool overwrite, double* d_K, double* d_fint, hipStream_t stream);
 
 struct Timing {
   bool enabled = false;

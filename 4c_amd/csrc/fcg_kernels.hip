@@ -20,6 +20,7 @@
 
 #include <cstdio>
 
+#include "fcg_hex8_element.hpp"
 #include "fcg_internal.hpp"
 #include "fcg_shape.hpp"
 
@@ -486,46 +487,32 @@ __global__ __launch_bounds__(BLOCK) void element_kernel(ElementArgs A)
 }
 
 // ---------------------------------------------------------------------------------- hex8, 8 lanes/element
-// 32 elements per 256-thread workgroup, 8 lanes per element (lanes 8e..8e+7):
-//   phase 1: lane j handles Gauss point g = j: J, J^-1, fac, N_XYZ of all 8 nodes at g (-> LDS),
-//            strain / F and StVK stress at g; lane j also checks det J at node j.
-//   phase 2: lane j handles node row a = j: f_a and the symmetric pair blocks K_ab of a
-//            tournament schedule (a, a+1..a+3 mod 8, and a+4 for a < 4: 36 pairs over 8 lanes),
-//            writing K_ab into the record of incidence (e,a) and K_ab^T into (e,b).
+// General (unstructured) hex8 path: 32 elements per 256-thread workgroup, 8 lanes per element
+// (fcg_hex8_element.hpp); K_ab goes to the record of incidence (e,a), K_ab^T to (e,b).
 constexpr int H8_EPB = 32;  // elements per block
-
-template <int KIN>
-struct H8Shared {
-  double X[H8_EPB][8][3];
-  double U[H8_EPB][8][3];
-  double NX[H8_EPB][8][8][3];  // [e][g][node][d]
-  double fac[H8_EPB][8];
-  double S[H8_EPB][8][6];
-  double F[KIN ? H8_EPB : 1][8][9];
-  double dN[8][8][3];          // GP derivative table (copy of c_dN8_gp)
-  double dNn[8][8][3];         // nodal derivative table
-  int bad[H8_EPB];
-};
 
 template <int KIN>
 __global__ __launch_bounds__(256) void element_kernel_h8(ElementArgs A)
 {
   constexpr int REC = 9 * 8 + 3;
   constexpr int ROWLEN = 24;
-  __shared__ H8Shared<KIN> sh;
+  __shared__ H8Slot<KIN> slot[H8_EPB];
+  __shared__ double dN[8][8][3], dNn[8][8][3];
+  __shared__ int bad[H8_EPB];
   const int tid = threadIdx.x;
   const int le = tid >> 3;  // element slot in block
   const int j = tid & 7;    // lane within the element group
   for (int v = tid; v < 192; v += 256)
   {
-    (&sh.dN[0][0][0])[v] = c_dN8_gp[v];
-    (&sh.dNn[0][0][0])[v] = c_dN8_node[v];
+    (&dN[0][0][0])[v] = c_dN8_gp[v];
+    (&dNn[0][0][0])[v] = c_dN8_node[v];
   }
+  const StVK mat{A.lambda, A.mu, A.cdiag};
+  H8Slot<KIN>& s = slot[le];
   for (int64_t e0 = int64_t(blockIdx.x) * H8_EPB; e0 < A.n_ele; e0 += int64_t(gridDim.x) * H8_EPB)
   {
     const int64_t e = e0 + le;
     const bool active = e < A.n_ele;
-    // 0. gather node j of element e
     if (active)
     {
       const int node = A.ele_nodes[e * 8 + j];
@@ -533,242 +520,63 @@ __global__ __launch_bounds__(256) void element_kernel_h8(ElementArgs A)
 #pragma unroll
       for (int d = 0; d < 3; ++d)
       {
-        sh.X[le][j][d] = A.node_x[3 * int64_t(node) + d];
-        sh.U[le][j][d] = A.u_col[dof + d];
+        s.X[j][d] = A.node_x[3 * int64_t(node) + d];
+        s.U[j][d] = A.u_col[dof + d];
       }
     }
-    if (j == 0) sh.bad[le] = 0;
+    if (j == 0) bad[le] = 0;
     __syncthreads();
-    // 1. Gauss point g = j; nodal check at node j
     if (active)
     {
-      double J[9], Jn[9];
-#pragma unroll
-      for (int k = 0; k < 9; ++k) J[k] = Jn[k] = 0.0;
-#pragma unroll
-      for (int c = 0; c < 8; ++c)
-      {
-        const double x0 = sh.X[le][c][0], x1 = sh.X[le][c][1], x2 = sh.X[le][c][2];
-        const double d0 = sh.dN[j][c][0], d1 = sh.dN[j][c][1], d2 = sh.dN[j][c][2];
-        J[0] += d0 * x0; J[1] += d1 * x0; J[2] += d2 * x0;
-        J[3] += d0 * x1; J[4] += d1 * x1; J[5] += d2 * x1;
-        J[6] += d0 * x2; J[7] += d1 * x2; J[8] += d2 * x2;
-        const double n0 = sh.dNn[j][c][0], n1 = sh.dNn[j][c][1], n2 = sh.dNn[j][c][2];
-        Jn[0] += n0 * x0; Jn[1] += n1 * x0; Jn[2] += n2 * x0;
-        Jn[3] += n0 * x1; Jn[4] += n1 * x1; Jn[5] += n2 * x1;
-        Jn[6] += n0 * x2; Jn[7] += n1 * x2; Jn[8] += n2 * x2;
-      }
-      const double detn = invert3x3(Jn);
-      int bad = 0;
-      if (detn == 0.0) bad = 2;
-      else if (!(detn > 0)) bad = 1;
-      const double det = invert3x3(J);
-      if (det == 0.0) bad = 2;
-      if (bad) atomicMax(&sh.bad[le], bad);
-      const double fac = det * c_w8[j];
-      sh.fac[le][j] = fac;
-      double E[6] = {0, 0, 0, 0, 0, 0};
-      double F[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-      for (int c = 0; c < 8; ++c)
-      {
-        const double d0 = sh.dN[j][c][0], d1 = sh.dN[j][c][1], d2 = sh.dN[j][c][2];
-        const double n0 = J[0] * d0 + J[3] * d1 + J[6] * d2;
-        const double n1 = J[1] * d0 + J[4] * d1 + J[7] * d2;
-        const double n2 = J[2] * d0 + J[5] * d1 + J[8] * d2;
-        sh.NX[le][j][c][0] = n0;
-        sh.NX[le][j][c][1] = n1;
-        sh.NX[le][j][c][2] = n2;
-        const double u0 = sh.U[le][c][0], u1 = sh.U[le][c][1], u2 = sh.U[le][c][2];
-        if (KIN == 0)
-        {
-          E[0] += n0 * u0;
-          E[1] += n1 * u1;
-          E[2] += n2 * u2;
-          E[3] += n1 * u0 + n0 * u1;
-          E[4] += n2 * u1 + n1 * u2;
-          E[5] += n2 * u0 + n0 * u2;
-        }
-        else
-        {
-          // hex8: F = x N_XYZ^T from current coordinates (calc_lib.hpp:585-595)
-          const double q0 = sh.X[le][c][0] + u0, q1 = sh.X[le][c][1] + u1, q2 = sh.X[le][c][2] + u2;
-          F[0] += q0 * n0; F[1] += q1 * n0; F[2] += q2 * n0;
-          F[3] += q0 * n1; F[4] += q1 * n1; F[5] += q2 * n1;
-          F[6] += q0 * n2; F[7] += q1 * n2; F[8] += q2 * n2;
-        }
-      }
-      if (KIN == 1)
-      {
-        double Fi[9];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) Fi[k] = F[k];
-        if (invert3x3(Fi) == 0.0) atomicMax(&sh.bad[le], 2);
-        double C[9];
-#pragma unroll
-        for (int r = 0; r < 3; ++r)
-#pragma unroll
-          for (int s = 0; s < 3; ++s)
-            C[r + 3 * s] = F[3 * r] * F[3 * s] + F[3 * r + 1] * F[3 * s + 1] + F[3 * r + 2] * F[3 * s + 2];
-        E[0] = 0.5 * (C[0] - 1.0);
-        E[1] = 0.5 * (C[4] - 1.0);
-        E[2] = 0.5 * (C[8] - 1.0);
-        E[3] = C[3];
-        E[4] = C[7];
-        E[5] = C[2];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) sh.F[le][j][k] = F[k];
-      }
-      double* S = sh.S[le][j];
-      S[0] = A.cdiag * E[0] + A.lambda * E[1] + A.lambda * E[2];
-      S[1] = A.lambda * E[0] + A.cdiag * E[1] + A.lambda * E[2];
-      S[2] = A.lambda * E[0] + A.lambda * E[1] + A.cdiag * E[2];
-      S[3] = A.mu * E[3];
-      S[4] = A.mu * E[4];
-      S[5] = A.mu * E[5];
+      const int b = h8_stage_a<KIN>(j, s, dN, dNn, c_w8[j], mat);
+      if (b) atomicMax(&bad[le], b);
     }
     __syncthreads();
-    // 2. node row a = j
-    if (active && sh.bad[le] == 0)
+    if (active && bad[le] == 0)
     {
       const int a = j;
+      double K[5][9], f[3];
+      h8_stage_b<KIN>(a, s, mat, A.want_k != 0, K, f);
       const int32_t* inc = A.inc_of + e * 8;
-      const int npair = (a < 4) ? 5 : 4;  // (a,a), (a,a+1), (a,a+2), (a,a+3), (a,a+4) for a < 4
-      double G[5][9];
-      double H[5][6];
-      double geo[5];
-#pragma unroll
-      for (int p = 0; p < 5; ++p)
-      {
-#pragma unroll
-        for (int k = 0; k < 9; ++k) G[p][k] = 0.0;
-#pragma unroll
-        for (int k = 0; k < 6; ++k) H[p][k] = 0.0;
-        geo[p] = 0.0;
-      }
-      double f0 = 0.0, f1 = 0.0, f2 = 0.0;
-#pragma unroll 1
-      for (int g = 0; g < 8; ++g)
-      {
-        const double fc = sh.fac[le][g];
-        const double* S = sh.S[le][g];
-        const double a0 = sh.NX[le][g][a][0], a1 = sh.NX[le][g][a][1], a2 = sh.NX[le][g][a][2];
-        double t0 = S[0] * a0 + S[3] * a1 + S[5] * a2;
-        double t1 = S[3] * a0 + S[1] * a1 + S[4] * a2;
-        double t2 = S[5] * a0 + S[4] * a1 + S[2] * a2;
-        double pa0 = a0, pa1 = a1, pa2 = a2;  // F a for TotLag
-        const double* F = (KIN == 1) ? sh.F[le][g] : nullptr;
-        double M[6];
-        if (KIN == 1)
-        {
-          const double s0 = F[0] * t0 + F[3] * t1 + F[6] * t2;
-          const double s1 = F[1] * t0 + F[4] * t1 + F[7] * t2;
-          const double s2 = F[2] * t0 + F[5] * t1 + F[8] * t2;
-          t0 = s0;
-          t1 = s1;
-          t2 = s2;
-          pa0 = F[0] * a0 + F[3] * a1 + F[6] * a2;
-          pa1 = F[1] * a0 + F[4] * a1 + F[7] * a2;
-          pa2 = F[2] * a0 + F[5] * a1 + F[8] * a2;
-          M[0] = F[0] * F[0] + F[3] * F[3] + F[6] * F[6];
-          M[1] = F[1] * F[1] + F[4] * F[4] + F[7] * F[7];
-          M[2] = F[2] * F[2] + F[5] * F[5] + F[8] * F[8];
-          M[3] = F[0] * F[1] + F[3] * F[4] + F[6] * F[7];
-          M[4] = F[1] * F[2] + F[4] * F[5] + F[7] * F[8];
-          M[5] = F[2] * F[0] + F[5] * F[3] + F[8] * F[6];
-        }
-        f0 += fc * t0;
-        f1 += fc * t1;
-        f2 += fc * t2;
-        const double fa0 = fc * pa0, fa1 = fc * pa1, fa2 = fc * pa2;
-#pragma unroll
-        for (int p = 0; p < 5; ++p)
-        {
-          if (p >= npair) break;
-          const int b = (a + p) & 7;
-          const double b0 = sh.NX[le][g][b][0], b1 = sh.NX[le][g][b][1], b2 = sh.NX[le][g][b][2];
-          double q0 = b0, q1 = b1, q2 = b2;
-          if (KIN == 1)
-          {
-            q0 = F[0] * b0 + F[3] * b1 + F[6] * b2;
-            q1 = F[1] * b0 + F[4] * b1 + F[7] * b2;
-            q2 = F[2] * b0 + F[5] * b1 + F[8] * b2;
-          }
-          G[p][0] += fa0 * q0; G[p][3] += fa0 * q1; G[p][6] += fa0 * q2;
-          G[p][1] += fa1 * q0; G[p][4] += fa1 * q1; G[p][7] += fa1 * q2;
-          G[p][2] += fa2 * q0; G[p][5] += fa2 * q1; G[p][8] += fa2 * q2;
-          if (KIN == 1)
-          {
-            const double t = fc * (a0 * b0 + a1 * b1 + a2 * b2);
-#pragma unroll
-            for (int k = 0; k < 6; ++k) H[p][k] += t * M[k];
-            const double sb0 = S[0] * b0 + S[3] * b1 + S[5] * b2;
-            const double sb1 = S[3] * b0 + S[1] * b1 + S[4] * b2;
-            const double sb2 = S[5] * b0 + S[4] * b1 + S[2] * b2;
-            geo[p] += fc * (a0 * sb0 + a1 * sb1 + a2 * sb2);
-          }
-        }
-      }
       const int32_t ia = inc[a];
       if (ia >= 0)
       {
         double* rec = A.scratch + int64_t(ia) * REC + 72;
-        rec[0] = f0;
-        rec[1] = f1;
-        rec[2] = f2;
+        rec[0] = f[0];
+        rec[1] = f[1];
+        rec[2] = f[2];
       }
       if (A.want_k)
       {
-        const double lam = A.lambda, mu = A.mu;
+        const int npair = h8_npair(a);
 #pragma unroll
         for (int p = 0; p < 5; ++p)
         {
           if (p >= npair) break;
-          const int b = (a + p) & 7;
-          double K[9];
-#pragma unroll
-          for (int r = 0; r < 3; ++r)
-#pragma unroll
-            for (int s = 0; s < 3; ++s) K[r + 3 * s] = lam * G[p][r + 3 * s] + mu * G[p][s + 3 * r];
-          if (KIN == 0)
-          {
-            const double tr = mu * (G[p][0] + G[p][4] + G[p][8]);
-            K[0] += tr;
-            K[4] += tr;
-            K[8] += tr;
-          }
-          else
-          {
-            K[0] += mu * H[p][0] + geo[p];
-            K[4] += mu * H[p][1] + geo[p];
-            K[8] += mu * H[p][2] + geo[p];
-            K[1] += mu * H[p][3]; K[3] += mu * H[p][3];
-            K[5] += mu * H[p][4]; K[7] += mu * H[p][4];
-            K[2] += mu * H[p][5]; K[6] += mu * H[p][5];
-          }
+          const int bb = (a + p) & 7;
           if (ia >= 0)
           {
-            double* rec = A.scratch + int64_t(ia) * REC + 3 * b;
+            double* rec = A.scratch + int64_t(ia) * REC + 3 * bb;
 #pragma unroll
             for (int r = 0; r < 3; ++r)
 #pragma unroll
-              for (int s = 0; s < 3; ++s) rec[r * ROWLEN + s] = K[r + 3 * s];
+              for (int q = 0; q < 3; ++q) rec[r * ROWLEN + q] = K[p][r + 3 * q];
           }
-          const int32_t ib = inc[b];
+          const int32_t ib = inc[bb];
           if (p > 0 && ib >= 0)
           {
             double* rec = A.scratch + int64_t(ib) * REC + 3 * a;
 #pragma unroll
             for (int r = 0; r < 3; ++r)
 #pragma unroll
-              for (int s = 0; s < 3; ++s) rec[r * ROWLEN + s] = K[s + 3 * r];
+              for (int q = 0; q < 3; ++q) rec[r * ROWLEN + q] = K[p][q + 3 * r];
           }
         }
       }
     }
-    if (active && j == 0 && sh.bad[le])
+    if (active && j == 0 && bad[le])
     {
-      atomicMax(&A.err[0], sh.bad[le]);
+      atomicMax(&A.err[0], bad[le]);
       atomicMin(&A.err[1], int32_t(e));
     }
     __syncthreads();

@@ -17,6 +17,7 @@ HEX8, HEX27 = 0, 1
 LINEAR, TOTLAG = 0, 1
 CALC_NLNSTIFF, CALC_INTERNALFORCE = 0, 1
 ACCUMULATE, OVERWRITE = 0, 1
+PATH_AUTO, PATH_GENERAL, PATH_STRUCTURED = 0, 1, 2
 ABI_VERSION = 1
 
 STATUS = {0: "FCG_OK", 1: "FCG_ERR_NODAL_DETJ", 2: "FCG_ERR_SINGULAR", 3: "FCG_ERR_ARG",
@@ -34,7 +35,8 @@ class FcgDesc(ctypes.Structure):
                 ("n_ele", ctypes.c_int64), ("n_node", ctypes.c_int64), ("n_rows", ctypes.c_int64),
                 ("n_cols", ctypes.c_int64), ("ele_nodes", _i32p), ("ele_gid", _i32p),
                 ("node_x", _dp), ("node_dof_col", _i32p), ("node_dof_row", _i32p),
-                ("node_dof_kcol", _i32p), ("rowptr", _i64p), ("col_lid", _i32p)]
+                ("node_dof_kcol", _i32p), ("rowptr", _i64p), ("col_lid", _i32p),
+                ("ele_ijk", _i32p), ("path", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 class FcgBox(ctypes.Structure):
@@ -48,7 +50,8 @@ class FcgInfo(ctypes.Structure):
     _fields_ = [("n_ele", ctypes.c_int64), ("n_node", ctypes.c_int64), ("n_rows", ctypes.c_int64),
                 ("n_cols", ctypes.c_int64), ("nnz", ctypes.c_int64),
                 ("n_incidences", ctypes.c_int64), ("scratch_bytes", ctypes.c_int64),
-                ("device_bytes", ctypes.c_int64)]
+                ("device_bytes", ctypes.c_int64), ("path", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
 
 
 # every symbol declared in include/fourc_gpu.h
@@ -149,6 +152,7 @@ class BoxMesh:
 
         self.ele_nodes = view(d.ele_nodes, d.n_ele * self.npe, np.int32).reshape(-1, self.npe)
         self.ele_gid = view(d.ele_gid, d.n_ele, np.int32)
+        self.ele_ijk = view(d.ele_ijk, d.n_ele * 3, np.int32).reshape(-1, 3)
         self.node_x = view(d.node_x, d.n_node * 3, np.float64).reshape(-1, 3)
         self.node_dof_col = view(d.node_dof_col, d.n_node, np.int32)
         self.node_dof_row = view(d.node_dof_row, d.n_node, np.int32)
@@ -168,7 +172,7 @@ class BoxMesh:
         L.fcg_box_mesh_destroy(h)
         self._h = None
 
-    def desc(self, kinematics, youngs, poisson, device=0):
+    def desc(self, kinematics, youngs, poisson, device=0, path=PATH_AUTO):
         d = FcgDesc()
         d.abi_version = ABI_VERSION
         d.celltype = self.celltype
@@ -185,6 +189,8 @@ class BoxMesh:
         d.node_dof_kcol = None
         d.rowptr = _np_ptr(self.rowptr, _i64p)
         d.col_lid = _np_ptr(self.col_lid, _i32p)
+        d.ele_ijk = _np_ptr(self.ele_ijk, _i32p) if path != PATH_GENERAL else None
+        d.path = path
         return d
 
     def node_displacement(self, amplitude):
@@ -208,11 +214,12 @@ class Evaluator:
     """Device context (fcg_ctx): the MI355X replacement of Discretization::evaluate for SOLID
     hex8/hex27 + StVK.  Keeps 4C's error behaviour: a non-zero status raises FcgError."""
 
-    def __init__(self, desc_or_mesh, kinematics=LINEAR, youngs=210.0, poisson=0.3, device=0):
+    def __init__(self, desc_or_mesh, kinematics=LINEAR, youngs=210.0, poisson=0.3, device=0,
+                 path=PATH_AUTO):
         L = lib()
         if isinstance(desc_or_mesh, BoxMesh):
             self._mesh = desc_or_mesh
-            desc = desc_or_mesh.desc(kinematics, youngs, poisson, device)
+            desc = desc_or_mesh.desc(kinematics, youngs, poisson, device, path)
         else:
             self._mesh = None
             desc = desc_or_mesh

@@ -81,7 +81,18 @@ typedef struct fcg_desc {
                                   node_dof_col */
   const int64_t* rowptr;       /* [n_rows + 1] */
   const int32_t* col_lid;      /* [rowptr[n_rows]] */
+  /* Optional structured-lattice hint (GridGenerator meshes): [n_ele][3] element lattice
+   * position (ex, ey, ez) = (gid % nx, gid / nx % ny, gid / (nx ny)), 4C_io_gridgenerator.cpp:336-338.
+   * fcg_create verifies it against the connectivity and, for hex8, then uses the fused
+   * z-sweep kernel (no scratch round trip).  NULL = general (unstructured) path. */
+  const int32_t* ele_ijk;
+  int32_t path;                /* fcg_path: FCG_PATH_AUTO / _GENERAL / _STRUCTURED */
+  int32_t reserved;
 } fcg_desc;
+
+/* Evaluation paths.  AUTO picks STRUCTURED when the hint verifies, else GENERAL.  STRUCTURED
+ * fails fcg_create with FCG_ERR_ARG when the hint does not verify. */
+enum fcg_path { FCG_PATH_AUTO = 0, FCG_PATH_GENERAL = 1, FCG_PATH_STRUCTURED = 2 };
 
 typedef struct fcg_ctx fcg_ctx;
 
@@ -119,8 +130,9 @@ int fcg_memcpy_h2d(void* d_dst, const void* h_src, int64_t bytes);
 int fcg_memcpy_d2h(void* h_dst, const void* d_src, int64_t bytes);
 int fcg_memset_device(void* d_dst, int value, int64_t bytes);
 
-/* Per-kernel timing of the last evaluate on the context stream, measured with hipEvents
- * (enable before the call).  names: "element", "assemble"; returns the count written. */
+/* Per-kernel timing of the last evaluate on the launch stream, measured with hipEvents
+ * (enable before the call).  GENERAL path: element kernel, assemble kernel.  STRUCTURED path:
+ * the fused kernel in ms_element, 0 in ms_assemble.  Returns the number of kernels timed. */
 int fcg_set_timing(fcg_ctx* ctx, int enable);
 int fcg_get_timing(const fcg_ctx* ctx, double* ms_element, double* ms_assemble);
 
@@ -130,6 +142,8 @@ typedef struct fcg_info {
   int64_t n_incidences;     /* (element, owned local node) pairs */
   int64_t scratch_bytes;    /* device scratch for element block-rows */
   int64_t device_bytes;     /* total device memory held by the context */
+  int32_t path;             /* fcg_path actually used (GENERAL or STRUCTURED) */
+  int32_t reserved;
 } fcg_info;
 int fcg_get_info(const fcg_ctx* ctx, fcg_info* info);
 

@@ -32,9 +32,9 @@ def _dev():
 
 
 def _run_gpu(mesh, kinem, u_col, action=fcg.CALC_NLNSTIFF, mode=fcg.OVERWRITE, ev=None,
-             K0=None, f0=None):
+             K0=None, f0=None, path=fcg.PATH_AUTO):
     dev = _dev()
-    ev = ev or fcg.Evaluator(mesh, kinematics=kinem, youngs=E, poisson=NU, device=0)
+    ev = ev or fcg.Evaluator(mesh, kinematics=kinem, youngs=E, poisson=NU, device=0, path=path)
     u = torch.from_numpy(u_col).to(dev)
     f = torch.from_numpy(f0).to(dev) if f0 is not None else torch.zeros(mesh.n_rows, dtype=torch.float64, device=dev)
     K = None
@@ -67,8 +67,22 @@ def test_nlnstiff_matches_oracle(celltype, kinem, iv, amp):
     u = mesh.u_col(amp)
     err, _, Kr, fr = oracle_evaluate(mesh, kinem, E, NU, u)
     assert err == 0
-    Kg, fg, _ = _run_gpu(mesh, kinem, u)
+    Kg, fg, ev = _run_gpu(mesh, kinem, u)
+    # hex8 box meshes carry the lattice hint -> fused structured kernel; hex27 -> general path
+    assert ev.info.path == (fcg.PATH_STRUCTURED if celltype == fcg.HEX8 else fcg.PATH_GENERAL)
     _check(Kg, fg, Kr, fr)
+
+
+@pytest.mark.parametrize("kinem", [fcg.LINEAR, fcg.TOTLAG])
+@pytest.mark.parametrize("iv", [(10, 10, 10), (7, 5, 9), (1, 1, 1), (13, 3, 2)])
+def test_hex8_general_and_structured_paths_agree_with_oracle(kinem, iv):
+    mesh = fcg.BoxMesh(fcg.HEX8, iv, jitter=0.1, seed=7)
+    u = mesh.u_col(1e-3 if kinem == fcg.LINEAR else 5e-2)
+    _, _, Kr, fr = oracle_evaluate(mesh, kinem, E, NU, u)
+    for path in (fcg.PATH_GENERAL, fcg.PATH_STRUCTURED):
+        Kg, fg, ev = _run_gpu(mesh, kinem, u, path=path)
+        assert ev.info.path == path
+        _check(Kg, fg, Kr, fr)
 
 
 @pytest.mark.parametrize("celltype,kinem,iv,amp", CASES[:1] + CASES[3:])

@@ -137,3 +137,19 @@ def test_jitter_is_deterministic_and_interior_only():
     assert d.max() <= 0.1 * 0.25 + 1e-15 and d.max() > 0
     on_boundary = np.any((np.abs(c.node_x) < 1e-12) | (np.abs(c.node_x - 1) < 1e-12), axis=1)
     assert np.all(d[on_boundary] == 0)
+
+
+def test_structured_hint_is_verified_before_device_work():
+    """A wrong lattice hint with PATH_STRUCTURED is rejected (FCG_ERR_ARG) on the host; a valid
+    one passes verification and then needs the device (FCG_ERR_DEVICE here, no GPU)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: covered by the gpu tests")
+    m = fcg.BoxMesh(fcg.HEX8, (3, 4, 5))
+    with pytest.raises(fcg.FcgError) as ei:
+        fcg.Evaluator(m, path=fcg.PATH_STRUCTURED)
+    assert ei.value.code == 4
+    m.ele_ijk[[0, 1]] = m.ele_ijk[[1, 0]]  # swap two elements' lattice positions
+    with pytest.raises(fcg.FcgError) as ei:
+        fcg.Evaluator(m, path=fcg.PATH_STRUCTURED)
+    assert ei.value.code == 3 and "lattice" in str(ei.value)
