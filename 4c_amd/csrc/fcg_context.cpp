@@ -79,6 +79,9 @@ struct StructHost {
   int32_t tiles_x = 0, tiles_y = 0, tiles_z = 0, seg = 0;
   std::vector<int32_t> elem_at, rownode_at;
   std::vector<uint16_t> nbr_pos;
+  std::vector<double> lat_x;        // node coordinates on the column-node lattice
+  std::vector<int32_t> lat_dof;     // column LID of the node's first DOF, -1 = none
+  std::vector<uint32_t> plane_rec;  // [tiles_y][tiles_x][NK][PLANE_REC_WORDS]
 };
 
 const int kOff8[8][3] = {{0, 0, 0}, {1, 0, 0}, {1, 1, 0}, {0, 1, 0}, {0, 0, 1}, {1, 0, 1}, {1, 1, 1},
@@ -237,13 +240,51 @@ bool build_structured_plan(const fcg_desc* d, const std::vector<int32_t>& rownod
   int64_t nseg = std::max<int64_t>(1, std::min<int64_t>(P.n[2], (2048 + txy - 1) / txy));
   P.seg = int32_t((P.n[2] + nseg - 1) / nseg);
   P.tiles_z = (P.n[2] + P.seg - 1) / P.seg;
+  // lattice node tables (coordinates and DOF column LIDs, by lattice position)
+  P.lat_x.assign(3 * NXn * NYn * NZn, 0.0);
+  P.lat_dof.assign(NXn * NYn * NZn, -1);
+  for (int64_t nd = 0; nd < d->n_node; ++nd)
+  {
+    if (npos[nd] < 0) continue;
+    for (int k = 0; k < 3; ++k) P.lat_x[3 * npos[nd] + k] = d->node_x[3 * nd + k];
+    P.lat_dof[npos[nd]] = d->node_dof_col[nd];
+  }
+  // plane records: row bookkeeping of the 16 node columns of every tile, per node plane
+  const int64_t W = fcg::PLANE_REC_WORDS;
+  P.plane_rec.assign(int64_t(P.tiles_y) * P.tiles_x * P.n[2] * W, 0u);
+  parallel_for(int64_t(P.tiles_y) * P.tiles_x * P.n[2], [&](int64_t idx) {
+    const int64_t k = idx % P.n[2];
+    const int64_t t = idx / P.n[2];
+    const int64_t tx = t % P.tiles_x, ty = t / P.tiles_x;
+    uint32_t* rec = P.plane_rec.data() + idx * W;
+    uint16_t* np = reinterpret_cast<uint16_t*>(rec + 64);
+    for (int c = 0; c < 16; ++c)
+    {
+      const int64_t i = 4 * tx + c % 4, jj = 4 * ty + c / 4;
+      int32_t r = -1;
+      if (i < P.n[0] && jj < P.n[1]) r = P.rownode_at[(k * P.n[1] + jj) * P.n[0] + i];
+      if (r < 0)
+      {
+        rec[c] = 0xFFFFFFFFu;
+        for (int q = 0; q < 27; ++q) np[27 * c + q] = 0xFFFF;
+        continue;
+      }
+      const int64_t base = d->rowptr[row0[r]];
+      rec[c] = uint32_t(row0[r]);
+      rec[16 + c] = uint32_t(d->rowptr[row0[r] + 1] - base);
+      rec[32 + 2 * c] = uint32_t(uint64_t(base) & 0xFFFFFFFFu);
+      rec[32 + 2 * c + 1] = uint32_t(uint64_t(base) >> 32);
+      for (int q = 0; q < 27; ++q) np[27 * c + q] = P.nbr_pos[r * 27 + q];
+    }
+  });
   return true;
 }
 
 void free_mesh(fcg::DeviceMesh& m)
 {
   void* ptrs[] = {m.ele_nodes, m.ele_gid, m.node_x, m.node_dof_col, m.inc_of, m.inc_ptr,
-      m.rownode_row0, m.inc_pos, m.rowptr, m.scratch, m.err, m.elem_at, m.rownode_at, m.nbr_pos,
+      m.rownode_row0, m.inc_pos, m.rowptr, m.scratch, m.err, m.elem_at, m.lat_x, m.lat_dof,
+      m.plane_rec,
       m.tables};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -495,8 +536,9 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
     m.EX0 = sp.elo[0]; m.EY0 = sp.elo[1]; m.EZ0 = sp.elo[2];
     m.EX = sp.en[0]; m.EY = sp.en[1]; m.EZ = sp.en[2];
     chk(upload(&m.elem_at, sp.elem_at.data(), int64_t(sp.elem_at.size()), bytes));
-    chk(upload(&m.rownode_at, sp.rownode_at.data(), int64_t(sp.rownode_at.size()), bytes));
-    chk(upload(&m.nbr_pos, sp.nbr_pos.data(), int64_t(sp.nbr_pos.size()), bytes));
+    chk(upload(&m.lat_x, sp.lat_x.data(), int64_t(sp.lat_x.size()), bytes));
+    chk(upload(&m.lat_dof, sp.lat_dof.data(), int64_t(sp.lat_dof.size()), bytes));
+    chk(upload(&m.plane_rec, sp.plane_rec.data(), int64_t(sp.plane_rec.size()), bytes));
     std::vector<double> tab(8 * 8 * 3 * 2 + 8);
     double xi[81], w[27], xn[81];
     fcg::gauss_rule(fcg::kHex8, xi, w);

@@ -11,11 +11,14 @@
 //   3. node plane ez is now complete (its rows receive contributions only from layers ez-1 and
 //      ez): its 3 CSR rows per node are written once, coalesced (81 contiguous columns for an
 //      interior node), then the plane buffer is recycled for plane ez+2.
-// HBM traffic is therefore K and r written once plus X, u, connectivity read ~1.6 times
-// (halo recompute), instead of the general path's per-incidence scratch round trip.
+// Latency hiding at one workgroup per CU: the next layer's node coordinates/displacements and the
+// row bookkeeping of plane ez+2 (one 1152-byte record per tile and plane) are loaded into
+// registers while the current layer computes, and committed to LDS at the next layer boundary.
+// HBM traffic is therefore K and r written once plus X, u read ~1.6 times (halo recompute) and
+// ~37 bytes of plane bookkeeping per row node, instead of the general path's scratch round trip.
 //
 // Reference semantics kept: SparseMatrix::assemble's owned-rows-only sum (4C_linalg_sparsematrix.cpp:474)
-// and its column positions (resolved per node row into nbr_pos by fcg_create), Vector assemble
+// and its column positions (resolved per node row by fcg_create), Vector assemble
 // (4C_linalg_utils_sparse_algebra_assemble.cpp:72-92), element evaluation as in
 // 4C_solid_3D_ele_calc.cpp:110-240.
 #include <hip/hip_runtime.h>
@@ -32,6 +35,8 @@ constexpr int EXN = TX + 1, EYN = TY + 1;  // element columns per layer
 constexpr int NSLOT = EXN * EYN;           // 25 elements per layer
 constexpr int NCOL = TX * TY;              // 16 node columns
 constexpr int ROWIMG = 27 * 9;             // 27 neighbour blocks of 3x3
+// plane record (uint32 words): row0[16] | rowlen[16] | rbase[16] (int64) | npos[16][27] (uint16)
+constexpr int PR_ROW0 = 0, PR_LEN = 16, PR_BASE = 32, PR_NPOS = 64;
 
 // hex8 node offsets in 4C node order (4C_io_gridgenerator.cpp:371-379)
 __constant__ int c_ox[8] = {0, 1, 1, 0, 0, 1, 1, 0};
@@ -39,15 +44,11 @@ __constant__ int c_oy[8] = {0, 0, 1, 1, 0, 0, 1, 1};
 __constant__ int c_oz[8] = {0, 0, 0, 0, 1, 1, 1, 1};
 
 struct FusedArgs {
-  const int32_t* ele_nodes;
-  const double* node_x;
-  const int32_t* node_dof_col;
   const double* u_col;
-  const int32_t* elem_at;
-  const int32_t* rownode_at;
-  const uint16_t* nbr_pos;
-  const int32_t* rownode_row0;
-  const int64_t* rowptr;
+  const double* lat_x;       // [LZ][LY][LX][3] node coordinates on the column-node lattice
+  const int32_t* lat_dof;    // [LZ][LY][LX] column LID of the first DOF, -1 = no node
+  const int32_t* elem_at;    // [EZ][EY][EX] column element or -1
+  const uint32_t* plane_rec; // [tiles_y][tiles_x][NK][PLANE_REC_WORDS]
   const double* tables;
   double* K;
   double* fint;
@@ -55,7 +56,7 @@ struct FusedArgs {
   StVK mat;
   int32_t tiles_x, tiles_y, seg_planes;
   int32_t I0, J0, K0, NI, NJ, NK;
-  int32_t EX0, EY0, EZ0, EX, EY, EZ;
+  int32_t EX0, EY0, EZ0, EX, EY, EZ;  // element box; the node lattice box is EX+1 x EY+1 x EZ+1
 };
 
 template <int KIN>
@@ -63,15 +64,14 @@ struct FusedShared {
   H8Slot<KIN> slot[NSLOT];
   double row[2][NCOL][ROWIMG];
   double frow[2][NCOL][3];
-  int64_t rbase[2][NCOL];  // rowptr of the node's first DOF row
-  int32_t rowlen[2][NCOL];
-  int32_t rn[2][NCOL];     // row node id of column c in plane buffer, -1 = not ours
-  int32_t row0[2][NCOL];
+  uint32_t prec[3][PLANE_REC_WORDS];  // ring of plane records, plane p -> prec[(p + 3) % 3]
   double dN[8][8][3];
   double dNn[8][8][3];
   double w8[8];
   int bad[32];
 };
+
+__device__ inline int ring(int p) { return (p % 3 + 3) % 3; }
 
 template <int KIN, bool WANT_K, bool OVERWRITE>
 __global__ __launch_bounds__(256) void fused_h8_kernel(FusedArgs A)
@@ -87,6 +87,8 @@ __global__ __launch_bounds__(256) void fused_h8_kernel(FusedArgs A)
   const int i0 = A.I0 + TX * tx, j0 = A.J0 + TY * ty;
   const int kz0 = A.K0 + A.seg_planes * tz;
   const int kz1 = min(kz0 + A.seg_planes, A.K0 + A.NK);
+  const uint32_t* prec_tile = A.plane_rec + (int64_t(ty) * A.tiles_x + tx) * A.NK * PLANE_REC_WORDS;
+  const int64_t LX = A.EX + 1, LY = A.EY + 1;
 
   for (int v = tid; v < 192; v += 256)
   {
@@ -103,57 +105,92 @@ __global__ __launch_bounds__(256) void fused_h8_kernel(FusedArgs A)
   const int colour = (ex & 1) | ((ey & 1) << 1);
   const bool slot_used = s < NSLOT;
   const int ox = c_ox[j], oy = c_oy[j], oz = c_oz[j];
-  // the node column of this lane's node a = j (for accumulation), or -1 if outside the tile
   const int ca_x = ex + ox - i0, ca_y = ey + oy - j0;
   const int col_a = (ca_x >= 0 && ca_x < TX && ca_y >= 0 && ca_y < TY) ? ca_x + TX * ca_y : -1;
-  int lo = 0;  // plane buffer holding the lower node plane of the current layer
+  const bool exy_in = slot_used && ex >= A.EX0 && ex < A.EX0 + A.EX && ey >= A.EY0 && ey < A.EY0 + A.EY;
+  const int64_t lat_xy = exy_in ? (int64_t(ey - A.EY0 + oy) * LX + (ex - A.EX0 + ox)) : 0;
+
+  // --- loaders (issue only; values land in registers)
+  auto load_elem = [&](int lz, int& e, double* X, int& dof) {
+    e = -1;
+    dof = -1;
+    if (exy_in && lz >= A.EZ0 && lz < A.EZ0 + A.EZ)
+    {
+      e = A.elem_at[(int64_t(lz - A.EZ0) * A.EY + (ey - A.EY0)) * A.EX + (ex - A.EX0)];
+      const int64_t li = int64_t(lz - A.EZ0 + oz) * LX * LY + lat_xy;
+      dof = A.lat_dof[li];
+#pragma unroll
+      for (int d = 0; d < 3; ++d) X[d] = A.lat_x[3 * li + d];
+    }
+  };
+  auto load_rec = [&](int p, uint32_t* w) {
+    const bool in = p >= kz0 && p < kz1;
+    const uint32_t* src = prec_tile + int64_t(in ? p - A.K0 : 0) * PLANE_REC_WORDS;
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+    {
+      const int v = tid + 256 * k;
+      if (v < PLANE_REC_WORDS) w[k] = in ? src[v] : (v < PR_LEN ? 0xFFFFFFFFu : 0u);
+    }
+  };
+  auto store_rec = [&](int p, const uint32_t* w) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+    {
+      const int v = tid + 256 * k;
+      if (v < PLANE_REC_WORDS) sh.prec[ring(p)][v] = w[k];
+    }
+  };
+
+  // --- prologue: plane records of kz0-1 (empty) and kz0, elements of layer kz0-1
+  {
+    uint32_t w[2];
+    load_rec(kz0 - 1, w);
+    store_rec(kz0 - 1, w);
+    load_rec(kz0, w);
+    store_rec(kz0, w);
+  }
+  int e_cur, dof_cur;
+  double X_cur[3] = {0, 0, 0}, U_cur[3] = {0, 0, 0};
+  load_elem(kz0 - 1, e_cur, X_cur, dof_cur);
+  if (e_cur >= 0)
+#pragma unroll
+    for (int d = 0; d < 3; ++d) U_cur[d] = A.u_col[dof_cur + d];
+  int lo = 0;  // row-image buffer of the lower node plane
 
   for (int ez = kz0 - 1; ez < kz1; ++ez)
   {
-    // plane bookkeeping: buffers lo (plane ez) and 1-lo (plane ez+1)
-    if (tid < 2 * NCOL)
-    {
-      const int pl = tid / NCOL, c = tid % NCOL;
-      const int k = ez + pl;
-      const int i = i0 + c % TX, jj = j0 + c / TX;
-      int r = -1;
-      if (k >= kz0 && k < kz1 && i < A.I0 + A.NI && jj < A.J0 + A.NJ)
-        r = A.rownode_at[(int64_t(k - A.K0) * A.NJ + (jj - A.J0)) * A.NI + (i - A.I0)];
-      const int b = pl == 0 ? lo : 1 - lo;
-      sh.rn[b][c] = r;
-      if (r >= 0)
-      {
-        const int32_t r0 = A.rownode_row0[r];
-        sh.row0[b][c] = r0;
-        sh.rbase[b][c] = A.rowptr[r0];
-        sh.rowlen[b][c] = int32_t(A.rowptr[r0 + 1] - A.rowptr[r0]);
-      }
-    }
-    // element of this slot
-    int e = -1;
-    if (slot_used && ex >= A.EX0 && ex < A.EX0 + A.EX && ey >= A.EY0 && ey < A.EY0 + A.EY &&
-        ez >= A.EZ0 && ez < A.EZ0 + A.EZ)
-      e = A.elem_at[(int64_t(ez - A.EZ0) * A.EY + (ey - A.EY0)) * A.EX + (ex - A.EX0)];
+    // 1. commit this layer's element data
     H8Slot<KIN>& es = sh.slot[slot_used ? s : 0];  // unused slots never touch it (e < 0)
+    const int e = e_cur;
     if (e >= 0)
     {
-      const int node = A.ele_nodes[int64_t(e) * 8 + j];
-      const int dof = A.node_dof_col[node];
 #pragma unroll
       for (int d = 0; d < 3; ++d)
       {
-        es.X[j][d] = A.node_x[3 * int64_t(node) + d];
-        es.U[j][d] = A.u_col[dof + d];
+        es.X[j][d] = X_cur[d];
+        es.U[j][d] = U_cur[d];
       }
     }
     if (j == 0) sh.bad[s] = 0;
     __syncthreads();
+    // 2. prefetch: next layer's elements and plane ez+2's record
+    int e_nxt, dof_nxt;
+    double X_nxt[3] = {0, 0, 0}, U_nxt[3] = {0, 0, 0};
+    load_elem(ez + 1, e_nxt, X_nxt, dof_nxt);
+    uint32_t rec_nxt[2];
+    load_rec(ez + 2, rec_nxt);
+    // 3. Gauss-point stage
     if (e >= 0)
     {
       const int b = h8_stage_a<KIN>(j, es, sh.dN, sh.dNn, sh.w8[j], A.mat);
       if (b) atomicMax(&sh.bad[s], b);
     }
     __syncthreads();
+    if (e_nxt >= 0)
+#pragma unroll
+      for (int d = 0; d < 3; ++d) U_nxt[d] = A.u_col[dof_nxt + d];
+    // 4. node-row stage
     double K[5][9], f[3];
     const bool ok = e >= 0 && sh.bad[s] == 0;
     if (ok) h8_stage_b<KIN>(j, es, A.mat, WANT_K, K, f);
@@ -162,9 +199,12 @@ __global__ __launch_bounds__(256) void fused_h8_kernel(FusedArgs A)
       atomicMax(&A.err[0], sh.bad[s]);
       atomicMin(&A.err[1], e);
     }
-    // accumulate into the plane row images, one colour at a time
+    // 5. accumulate into the plane row images, one colour at a time
+    const uint32_t* rec_lo = sh.prec[ring(ez)];
+    const uint32_t* rec_hi = sh.prec[ring(ez + 1)];
     const int buf_a = oz == 0 ? lo : 1 - lo;
-    const bool own_a = ok && col_a >= 0 && sh.rn[buf_a][col_a] >= 0;
+    const uint32_t* rec_a = oz == 0 ? rec_lo : rec_hi;
+    const bool own_a = ok && col_a >= 0 && int32_t(rec_a[PR_ROW0 + col_a]) >= 0;
 #pragma unroll 1
     for (int c = 0; c < 4; ++c)
     {
@@ -201,7 +241,8 @@ __global__ __launch_bounds__(256) void fused_h8_kernel(FusedArgs A)
               {
                 const int col_b = cb_x + TX * cb_y;
                 const int buf_b = c_oz[b] == 0 ? lo : 1 - lo;
-                if (sh.rn[buf_b][col_b] >= 0)
+                const uint32_t* rec_b = c_oz[b] == 0 ? rec_lo : rec_hi;
+                if (int32_t(rec_b[PR_ROW0 + col_b]) >= 0)
                 {
                   double* blk = sh.row[buf_b][col_b] + 9 * ((1 - dz) * 9 + (1 - dy) * 3 + (1 - dx));
 #pragma unroll
@@ -216,9 +257,10 @@ __global__ __launch_bounds__(256) void fused_h8_kernel(FusedArgs A)
       }
       __syncthreads();
     }
-    // node plane ez is complete: write its rows once, then recycle the buffer
+    // 6. node plane ez is complete: write its rows once
     if (ez >= kz0)
     {
+      const uint16_t* npos = reinterpret_cast<const uint16_t*>(rec_lo + PR_NPOS);
       if (WANT_K)
       {
         for (int v = tid; v < NCOL * ROWIMG; v += 256)
@@ -229,11 +271,11 @@ __global__ __launch_bounds__(256) void fused_h8_kernel(FusedArgs A)
           const int rem2 = rem - 81 * r;
           const int t = rem2 / 3;
           const int q = rem2 - 3 * t;
-          const int node = sh.rn[lo][c];
-          if (node < 0) continue;
-          const uint16_t pos = A.nbr_pos[int64_t(node) * 27 + t];
+          if (int32_t(rec_lo[PR_ROW0 + c]) < 0) continue;
+          const uint16_t pos = npos[27 * c + t];
           if (pos == 0xFFFF) continue;
-          double* dst = A.K + sh.rbase[lo][c] + int64_t(r) * sh.rowlen[lo][c] + pos + q;
+          const int64_t base = int64_t(rec_lo[PR_BASE + 2 * c]) | (int64_t(rec_lo[PR_BASE + 2 * c + 1]) << 32);
+          double* dst = A.K + base + int64_t(r) * int32_t(rec_lo[PR_LEN + c]) + pos + q;
           const double val = sh.row[lo][c][9 * t + 3 * r + q];
           if (OVERWRITE)
             *dst = val;
@@ -244,10 +286,10 @@ __global__ __launch_bounds__(256) void fused_h8_kernel(FusedArgs A)
       if (tid < NCOL * 3)
       {
         const int c = tid / 3, r = tid - 3 * (tid / 3);
-        const int node = sh.rn[lo][c];
-        if (node >= 0)
+        const int32_t r0 = int32_t(rec_lo[PR_ROW0 + c]);
+        if (r0 >= 0)
         {
-          double* dst = A.fint + sh.row0[lo][c] + r;
+          double* dst = A.fint + r0 + r;
           if (OVERWRITE)
             *dst = sh.frow[lo][c][r];
           else
@@ -256,8 +298,18 @@ __global__ __launch_bounds__(256) void fused_h8_kernel(FusedArgs A)
       }
     }
     __syncthreads();
+    // 7. recycle: zero the lower row image, commit plane ez+2's record, roll registers
     for (int v = tid; v < NCOL * ROWIMG; v += 256) (&sh.row[lo][0][0])[v] = 0.0;
     if (tid < NCOL * 3) (&sh.frow[lo][0][0])[tid] = 0.0;
+    store_rec(ez + 2, rec_nxt);
+    e_cur = e_nxt;
+    dof_cur = dof_nxt;
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+    {
+      X_cur[d] = X_nxt[d];
+      U_cur[d] = U_nxt[d];
+    }
     lo = 1 - lo;
     __syncthreads();
   }
@@ -271,15 +323,11 @@ hipError_t launch_fused_h8(const DeviceMesh& m, const double* d_u_col, bool want
   const int64_t ntiles = int64_t(m.tiles_x) * m.tiles_y * m.tiles_z;
   if (ntiles == 0) return hipSuccess;
   FusedArgs a;
-  a.ele_nodes = m.ele_nodes;
-  a.node_x = m.node_x;
-  a.node_dof_col = m.node_dof_col;
   a.u_col = d_u_col;
+  a.lat_x = m.lat_x;
+  a.lat_dof = m.lat_dof;
   a.elem_at = m.elem_at;
-  a.rownode_at = m.rownode_at;
-  a.nbr_pos = m.nbr_pos;
-  a.rownode_row0 = m.rownode_row0;
-  a.rowptr = m.rowptr;
+  a.plane_rec = m.plane_rec;
   a.tables = m.tables;
   a.K = d_K;
   a.fint = d_fint;

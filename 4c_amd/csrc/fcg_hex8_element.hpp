@@ -24,6 +24,7 @@ struct H8Slot {
   double fac[8];
   double S[8][6];      // PK2, Voigt xx yy zz xy yz zx
   double F[KIN ? 8 : 1][9];
+  double pad[4];       // slot stride = 600 / 744 dwords: consecutive slots start in different banks
 };
 
 __device__ inline double h8_invert3x3(double* m)

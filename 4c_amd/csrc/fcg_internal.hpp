@@ -40,10 +40,15 @@ struct DeviceMesh {
   int32_t I0 = 0, J0 = 0, K0 = 0, NI = 0, NJ = 0, NK = 0;  // owned-node lattice box
   int32_t EX0 = 0, EY0 = 0, EZ0 = 0, EX = 0, EY = 0, EZ = 0;  // column-element lattice box
   int32_t* elem_at = nullptr;       // [EZ][EY][EX] column element or -1
-  int32_t* rownode_at = nullptr;    // [NK][NJ][NI] row node or -1
-  uint16_t* nbr_pos = nullptr;      // [n_rownodes][27] column position of neighbour t, 0xFFFF absent
+  double* lat_x = nullptr;          // [EZ+1][EY+1][EX+1][3] node coordinates on the lattice
+  int32_t* lat_dof = nullptr;       // [EZ+1][EY+1][EX+1] column LID of the node's first DOF or -1
+  uint32_t* plane_rec = nullptr;    // [tiles_y][tiles_x][NK][PLANE_REC_WORDS] row bookkeeping
   double* tables = nullptr;         // dN at GPs [192], dN at nodes [192], weights [8]
 };
+
+// One record per (tile, node plane): row0[16] | rowlen[16] | rbase[16] (int64) | npos[16][27]
+// (uint16, column position of lattice neighbour t inside the node's rows, 0xFFFF = absent).
+constexpr int PLANE_REC_WORDS = 288;
 
 // Launches the fused hex8 kernel (element evaluation + LDS row accumulation + row flush).
 hipError_t launch_fused_h8(const DeviceMesh& m, const double* d_u_col, bool want_k,
