@@ -4,13 +4,14 @@
 //
 // Per element layer ez (between node planes ez and ez+1):
 //   1. the 5 x 5 elements touching the tile's node columns (owned tile + one halo layer on the
-//      low x/y sides) are evaluated, 8 lanes per element (fcg_hex8_element.hpp);
-//   2. every lane adds its pair blocks K_ab / K_ab^T and f_a into LDS row images of the two node
-//      planes -- in four colour phases (ex & 1, ey & 1) so that no two elements of a phase share
-//      a node: plain read-add-write, fixed order, bitwise reproducible, no atomics;
+//      low x/y sides) are evaluated, 8 lanes per element (fcg_hex8_element.hpp); each element's
+//      36 pair blocks and 8 nodal forces are left in its (by then dead) LDS slot;
+//   2. owner-computes gather: every lane owns row-image entries (node column, plane, neighbour
+//      block, component) of the two node planes and adds the 1, 2 or 4 element contributions of
+//      this layer in a fixed element order -- no atomics, no colouring, bitwise reproducible;
 //   3. node plane ez is now complete (its rows receive contributions only from layers ez-1 and
 //      ez): its 3 CSR rows per node are written once, coalesced (81 contiguous columns for an
-//      interior node), then the plane buffer is recycled for plane ez+2.
+//      interior node), then the plane image is recycled for plane ez+2.
 // Latency hiding at one workgroup per CU: the next layer's node coordinates/displacements and the
 // row bookkeeping of plane ez+2 (one 1152-byte record per tile and plane) are loaded into
 // registers while the current layer computes, and committed to LDS at the next layer boundary.
@@ -38,10 +39,14 @@ constexpr int ROWIMG = 27 * 9;             // 27 neighbour blocks of 3x3
 // plane record (uint32 words): row0[16] | rowlen[16] | rbase[16] (int64) | npos[16][27] (uint16)
 constexpr int PR_ROW0 = 0, PR_LEN = 16, PR_BASE = 32, PR_NPOS = 64;
 
-// hex8 node offsets in 4C node order (4C_io_gridgenerator.cpp:371-379)
+// hex8 node offsets in 4C node order (4C_io_gridgenerator.cpp:371-379) and the inverse map
 __constant__ int c_ox[8] = {0, 1, 1, 0, 0, 1, 1, 0};
 __constant__ int c_oy[8] = {0, 0, 1, 1, 0, 0, 1, 1};
 __constant__ int c_oz[8] = {0, 0, 0, 0, 1, 1, 1, 1};
+__device__ inline int local_node(int ox, int oy, int oz)
+{
+  return 4 * oz + (oy ? (ox ? 2 : 3) : (ox ? 1 : 0));
+}
 
 struct FusedArgs {
   const double* u_col;
@@ -59,16 +64,27 @@ struct FusedArgs {
   int32_t EX0, EY0, EZ0, EX, EY, EZ;  // element box; the node lattice box is EX+1 x EY+1 x EZ+1
 };
 
+// LDS slot of one element: stage A/B working set, then (aliased) the stage B results
+template <int KIN>
+struct FusedSlot {
+  union {
+    H8Slot<KIN> s;
+    double Kp[8][5][9];  // lane a's pair blocks (a, (a+p)&7), column-major 3x3
+  } u;
+  double fe[8][3];
+};
+
 template <int KIN>
 struct FusedShared {
-  H8Slot<KIN> slot[NSLOT];
+  FusedSlot<KIN> slot[NSLOT];
   double row[2][NCOL][ROWIMG];
   double frow[2][NCOL][3];
-  uint32_t prec[3][PLANE_REC_WORDS];  // ring of plane records, plane p -> prec[(p + 3) % 3]
+  uint32_t prec[3][PLANE_REC_WORDS];  // ring of plane records, plane p -> prec[ring(p)]
   double dN[8][8][3];
   double dNn[8][8][3];
   double w8[8];
   int bad[32];
+  int ok[NSLOT];
 };
 
 __device__ inline int ring(int p) { return (p % 3 + 3) % 3; }
@@ -102,11 +118,8 @@ __global__ __launch_bounds__(256) void fused_h8_kernel(FusedArgs A)
   // element slot geometry (fixed over the sweep)
   const int sx = s % EXN, sy = s / EXN;
   const int ex = i0 - 1 + sx, ey = j0 - 1 + sy;
-  const int colour = (ex & 1) | ((ey & 1) << 1);
   const bool slot_used = s < NSLOT;
   const int ox = c_ox[j], oy = c_oy[j], oz = c_oz[j];
-  const int ca_x = ex + ox - i0, ca_y = ey + oy - j0;
-  const int col_a = (ca_x >= 0 && ca_x < TX && ca_y >= 0 && ca_y < TY) ? ca_x + TX * ca_y : -1;
   const bool exy_in = slot_used && ex >= A.EX0 && ex < A.EX0 + A.EX && ey >= A.EY0 && ey < A.EY0 + A.EY;
   const int64_t lat_xy = exy_in ? (int64_t(ey - A.EY0 + oy) * LX + (ex - A.EX0 + ox)) : 0;
 
@@ -161,7 +174,8 @@ __global__ __launch_bounds__(256) void fused_h8_kernel(FusedArgs A)
   for (int ez = kz0 - 1; ez < kz1; ++ez)
   {
     // 1. commit this layer's element data
-    H8Slot<KIN>& es = sh.slot[slot_used ? s : 0];  // unused slots never touch it (e < 0)
+    FusedSlot<KIN>& fs = sh.slot[slot_used ? s : 0];  // unused slots never touch it (e < 0)
+    H8Slot<KIN>& es = fs.u.s;
     const int e = e_cur;
     if (e >= 0)
     {
@@ -190,76 +204,107 @@ __global__ __launch_bounds__(256) void fused_h8_kernel(FusedArgs A)
     if (e_nxt >= 0)
 #pragma unroll
       for (int d = 0; d < 3; ++d) U_nxt[d] = A.u_col[dof_nxt + d];
-    // 4. node-row stage
-    double K[5][9], f[3];
-    const bool ok = e >= 0 && sh.bad[s] == 0;
-    if (ok) h8_stage_b<KIN>(j, es, A.mat, WANT_K, K, f);
-    if (e >= 0 && j == 0 && sh.bad[s])
+    // 4. node-row stage; results into the slot (aliases the dead stage-A data of this element)
     {
-      atomicMax(&A.err[0], sh.bad[s]);
-      atomicMin(&A.err[1], e);
-    }
-    // 5. accumulate into the plane row images, one colour at a time
-    const uint32_t* rec_lo = sh.prec[ring(ez)];
-    const uint32_t* rec_hi = sh.prec[ring(ez + 1)];
-    const int buf_a = oz == 0 ? lo : 1 - lo;
-    const uint32_t* rec_a = oz == 0 ? rec_lo : rec_hi;
-    const bool own_a = ok && col_a >= 0 && int32_t(rec_a[PR_ROW0 + col_a]) >= 0;
-#pragma unroll 1
-    for (int c = 0; c < 4; ++c)
-    {
-      if (ok && colour == c)
+      const bool ok = e >= 0 && sh.bad[s] == 0;
+      if (ok)
       {
-        if (own_a)
-        {
-          double* fr = sh.frow[buf_a][col_a];
-          fr[0] += f[0];
-          fr[1] += f[1];
-          fr[2] += f[2];
-        }
+        double K[5][9], f[3];
+        h8_stage_b<KIN>(j, es, A.mat, WANT_K, K, f);
+        // all 8 lanes of this element are in one wavefront and finished reading the slot
+        __builtin_amdgcn_wave_barrier();
+        fs.fe[j][0] = f[0];
+        fs.fe[j][1] = f[1];
+        fs.fe[j][2] = f[2];
         if (WANT_K)
         {
-          const int npair = h8_npair(j);
 #pragma unroll
           for (int p = 0; p < 5; ++p)
-          {
-            if (p >= npair) break;
-            const int b = (j + p) & 7;
-            const int dx = c_ox[b] - ox, dy = c_oy[b] - oy, dz = c_oz[b] - oz;
-            if (own_a)
-            {
-              double* blk = sh.row[buf_a][col_a] + 9 * ((dz + 1) * 9 + (dy + 1) * 3 + (dx + 1));
 #pragma unroll
-              for (int r = 0; r < 3; ++r)
-#pragma unroll
-                for (int q = 0; q < 3; ++q) blk[3 * r + q] += K[p][r + 3 * q];
-            }
-            if (p > 0)
-            {
-              const int cb_x = ca_x + dx, cb_y = ca_y + dy;
-              if (cb_x >= 0 && cb_x < TX && cb_y >= 0 && cb_y < TY)
-              {
-                const int col_b = cb_x + TX * cb_y;
-                const int buf_b = c_oz[b] == 0 ? lo : 1 - lo;
-                const uint32_t* rec_b = c_oz[b] == 0 ? rec_lo : rec_hi;
-                if (int32_t(rec_b[PR_ROW0 + col_b]) >= 0)
-                {
-                  double* blk = sh.row[buf_b][col_b] + 9 * ((1 - dz) * 9 + (1 - dy) * 3 + (1 - dx));
-#pragma unroll
-                  for (int r = 0; r < 3; ++r)
-#pragma unroll
-                    for (int q = 0; q < 3; ++q) blk[3 * r + q] += K[p][q + 3 * r];
-                }
-              }
-            }
-          }
+            for (int k = 0; k < 9; ++k) fs.u.Kp[j][p][k] = K[p][k];
         }
       }
-      __syncthreads();
+      if (slot_used && j == 0) sh.ok[s] = ok ? 1 : 0;
+      if (e >= 0 && j == 0 && sh.bad[s])
+      {
+        atomicMax(&A.err[0], sh.bad[s]);
+        atomicMin(&A.err[1], e);
+      }
     }
-    // 6. node plane ez is complete: write its rows once
+    __syncthreads();
+    // 5. owner-computes gather into the row images of planes ez (p = 0) and ez+1 (p = 1)
+    {
+      const uint32_t* rec_pl[2] = {sh.prec[ring(ez)], sh.prec[ring(ez + 1)]};
+      const int buf_pl[2] = {lo, 1 - lo};
+      // residual entries: 2 planes x 16 columns x 3
+      if (tid < 2 * NCOL * 3)
+      {
+        const int p = tid / (NCOL * 3);
+        const int rem = tid - p * NCOL * 3;
+        const int c = rem / 3, r = rem - 3 * (rem / 3);
+        if (int32_t(rec_pl[p][PR_ROW0 + c]) >= 0)
+        {
+          const int cx = c % TX, cy = c / TX;
+          double acc = 0.0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+          {
+            const int bx = k & 1, by = k >> 1;  // element (cx-1+bx, cy-1+by) in tile columns
+            const int sl = (cx + bx) + EXN * (cy + by);
+            if (sh.ok[sl]) acc += sh.slot[sl].fe[local_node(1 - bx, 1 - by, p)][r];
+          }
+          sh.frow[buf_pl[p]][c][r] += acc;
+        }
+      }
+      if (WANT_K)
+      {
+        // K entries: (p, c, t, k) with the neighbour in this layer's planes
+        for (int v = tid; v < 2 * NCOL * ROWIMG; v += 256)
+        {
+          const int p = v / (NCOL * ROWIMG);
+          const int rem = v - p * NCOL * ROWIMG;
+          const int c = rem / ROWIMG;
+          const int rem2 = rem - c * ROWIMG;
+          const int t = rem2 / 9;
+          const int kk = rem2 - 9 * t;
+          const int dz = t / 9 - 1;
+          const int pz = p + dz;
+          if (pz < 0 || pz > 1) continue;
+          if (int32_t(rec_pl[p][PR_ROW0 + c]) < 0) continue;
+          const int dy = (t / 3) % 3 - 1, dx = t % 3 - 1;
+          const int r = kk / 3, q = kk - 3 * (kk / 3);
+          const int cx = c % TX, cy = c / TX;
+          double acc = 0.0;
+          // elements of the layer holding node (cx, cy) and its neighbour (cx+dx, cy+dy):
+          // x offset bx in {0,1} relative to column cx-1 with both nodes inside
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+          {
+            const int bx = k & 1, by = k >> 1;
+            // element x index (tile-relative, column cx-1+bx): node at local ox = 1-bx,
+            // neighbour at ox + dx must be 0 or 1
+            const int oxa = 1 - bx, oya = 1 - by;
+            const int oxb = oxa + dx, oyb = oya + dy;
+            if (oxb < 0 || oxb > 1 || oyb < 0 || oyb > 1) continue;
+            const int sl = (cx + bx) + EXN * (cy + by);
+            if (!sh.ok[sl]) continue;
+            const int a = local_node(oxa, oya, p);
+            const int b = local_node(oxb, oyb, pz);
+            const int pp = (b - a) & 7;
+            if (pp <= 3 || (pp == 4 && a < 4))
+              acc += sh.slot[sl].u.Kp[a][pp][r + 3 * q];
+            else
+              acc += sh.slot[sl].u.Kp[b][(a - b) & 7][q + 3 * r];
+          }
+          sh.row[buf_pl[p]][c][9 * t + kk] += acc;
+        }
+      }
+    }
+    __syncthreads();
+    // 6. node plane ez is complete: write its rows once and clear the image
     if (ez >= kz0)
     {
+      const uint32_t* rec_lo = sh.prec[ring(ez)];
       const uint16_t* npos = reinterpret_cast<const uint16_t*>(rec_lo + PR_NPOS);
       if (WANT_K)
       {
@@ -271,12 +316,14 @@ __global__ __launch_bounds__(256) void fused_h8_kernel(FusedArgs A)
           const int rem2 = rem - 81 * r;
           const int t = rem2 / 3;
           const int q = rem2 - 3 * t;
+          double& img = sh.row[lo][c][9 * t + 3 * r + q];
+          const double val = img;
+          img = 0.0;
           if (int32_t(rec_lo[PR_ROW0 + c]) < 0) continue;
           const uint16_t pos = npos[27 * c + t];
           if (pos == 0xFFFF) continue;
           const int64_t base = int64_t(rec_lo[PR_BASE + 2 * c]) | (int64_t(rec_lo[PR_BASE + 2 * c + 1]) << 32);
           double* dst = A.K + base + int64_t(r) * int32_t(rec_lo[PR_LEN + c]) + pos + q;
-          const double val = sh.row[lo][c][9 * t + 3 * r + q];
           if (OVERWRITE)
             *dst = val;
           else
@@ -287,20 +334,24 @@ __global__ __launch_bounds__(256) void fused_h8_kernel(FusedArgs A)
       {
         const int c = tid / 3, r = tid - 3 * (tid / 3);
         const int32_t r0 = int32_t(rec_lo[PR_ROW0 + c]);
+        const double val = sh.frow[lo][c][r];
+        sh.frow[lo][c][r] = 0.0;
         if (r0 >= 0)
         {
           double* dst = A.fint + r0 + r;
           if (OVERWRITE)
-            *dst = sh.frow[lo][c][r];
+            *dst = val;
           else
-            *dst += sh.frow[lo][c][r];
+            *dst += val;
         }
       }
     }
-    __syncthreads();
-    // 7. recycle: zero the lower row image, commit plane ez+2's record, roll registers
-    for (int v = tid; v < NCOL * ROWIMG; v += 256) (&sh.row[lo][0][0])[v] = 0.0;
-    if (tid < NCOL * 3) (&sh.frow[lo][0][0])[tid] = 0.0;
+    else
+    {
+      for (int v = tid; v < NCOL * ROWIMG; v += 256) (&sh.row[lo][0][0])[v] = 0.0;
+      if (tid < NCOL * 3) (&sh.frow[lo][0][0])[tid] = 0.0;
+    }
+    // 7. commit plane ez+2's record (its ring slot held plane ez-1), roll registers
     store_rec(ez + 2, rec_nxt);
     e_cur = e_nxt;
     dof_cur = dof_nxt;
