@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <atomic>
 #include <cstring>
 #include <mutex>
@@ -285,7 +286,7 @@ void free_mesh(fcg::DeviceMesh& m)
   void* ptrs[] = {m.ele_nodes, m.ele_gid, m.node_x, m.node_dof_col, m.inc_of, m.inc_ptr,
       m.rownode_row0, m.inc_pos, m.rowptr, m.scratch, m.err, m.elem_at, m.lat_x, m.lat_dof,
       m.plane_rec,
-      m.tables};
+      m.tables, m.stamps};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   m = fcg::DeviceMesh{};
@@ -547,6 +548,16 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
     for (int g = 0; g < 8; ++g) fcg::shape_deriv(fcg::kHex8, &xn[3 * g], &tab[192 + 24 * g]);
     for (int g = 0; g < 8; ++g) tab[384 + g] = w[g];
     chk(upload(&m.tables, tab.data(), int64_t(tab.size()), bytes));
+    // diagnostics (tools/stamps.py): FCG_FUSED_ACC selects the accumulation variant,
+    // FCG_STAMPS=1 turns on the per-phase s_memtime counters
+    const char* acc = std::getenv("FCG_FUSED_ACC");
+    m.fused_acc = (acc && acc[0] == '1') ? 1 : 0;
+    const char* st = std::getenv("FCG_STAMPS");
+    if (st && st[0] == '1')
+    {
+      const unsigned long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      chk(upload(&m.stamps, zero, 8, bytes));
+    }
   }
   else
   {
@@ -692,6 +703,17 @@ int fcg_get_timing(const fcg_ctx* ctx, double* ms_element, double* ms_assemble)
   if (ms_element) *ms_element = ctx->timing.ms_element;
   if (ms_assemble) *ms_assemble = ctx->timing.ms_assemble;
   return 2;
+}
+
+int fcg_get_diagnostics(const fcg_ctx* ctx, uint64_t* out, int n)
+{
+  if (!ctx || !out || n < 0) return FCG_ERR_ARG;
+  const fcg::DeviceMesh& m = ctx->mesh;
+  unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (m.stamps && hipMemcpy(v, m.stamps, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess)
+    return FCG_ERR_DEVICE;
+  for (int i = 0; i < n && i < 8; ++i) out[i] = v[i];
+  return m.stamps ? 8 : 0;
 }
 
 int fcg_get_info(const fcg_ctx* ctx, fcg_info* info)

@@ -58,6 +58,7 @@ struct FusedArgs {
   double* K;
   double* fint;
   int32_t* err;
+  unsigned long long* stamps;  // diagnostic phase timers (NULL = off, the production setting)
   StVK mat;
   int32_t tiles_x, tiles_y, seg_planes;
   int32_t I0, J0, K0, NI, NJ, NK;
@@ -89,11 +90,24 @@ struct FusedShared {
 
 __device__ inline int ring(int p) { return (p % 3 + 3) % 3; }
 
-template <int KIN, bool WANT_K, bool OVERWRITE>
+// Diagnostic phase stamps: thread 0 of each workgroup adds the cycles of every phase (including
+// the barrier wait that ends it) into A.stamps[phase]; off (uniform branch, no s_memtime) when
+// A.stamps is NULL.
+#define FCG_STAMP(i)                                                                               \
+  if (A.stamps && tid == 0)                                                                        \
+  {                                                                                                \
+    const unsigned long long now = __builtin_amdgcn_s_memtime();                                  \
+    st_acc[i] += now - st_last;                                                                    \
+    st_last = now;                                                                                 \
+  }
+
+template <int KIN, bool WANT_K, bool OVERWRITE, int ACC>
 __global__ __launch_bounds__(256) void fused_h8_kernel(FusedArgs A)
 {
   __shared__ FusedShared<KIN> sh;
   const int tid = threadIdx.x;
+  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long st_last = A.stamps ? __builtin_amdgcn_s_memtime() : 0ull;
   const int s = tid >> 3;  // element slot
   const int j = tid & 7;   // lane in element group
   const int tile = blockIdx.x;
@@ -122,6 +136,10 @@ __global__ __launch_bounds__(256) void fused_h8_kernel(FusedArgs A)
   const int ox = c_ox[j], oy = c_oy[j], oz = c_oz[j];
   const bool exy_in = slot_used && ex >= A.EX0 && ex < A.EX0 + A.EX && ey >= A.EY0 && ey < A.EY0 + A.EY;
   const int64_t lat_xy = exy_in ? (int64_t(ey - A.EY0 + oy) * LX + (ex - A.EX0 + ox)) : 0;
+  // colour-phase accumulation (ACC 0): element colour and the tile column of this lane's node a
+  const int colour = (ex & 1) | ((ey & 1) << 1);
+  const int ca_x = ex + ox - i0, ca_y = ey + oy - j0;
+  const int col_a = (ca_x >= 0 && ca_x < TX && ca_y >= 0 && ca_y < TY) ? ca_x + TX * ca_y : -1;
 
   // --- loaders (issue only; values land in registers)
   auto load_elem = [&](int lz, int& e, double* X, int& dof) {
@@ -188,6 +206,7 @@ __global__ __launch_bounds__(256) void fused_h8_kernel(FusedArgs A)
     }
     if (j == 0) sh.bad[s] = 0;
     __syncthreads();
+    FCG_STAMP(0);
     // 2. prefetch: next layer's elements and plane ez+2's record
     int e_nxt, dof_nxt;
     double X_nxt[3] = {0, 0, 0}, U_nxt[3] = {0, 0, 0};
@@ -201,9 +220,82 @@ __global__ __launch_bounds__(256) void fused_h8_kernel(FusedArgs A)
       if (b) atomicMax(&sh.bad[s], b);
     }
     __syncthreads();
+    FCG_STAMP(1);
     if (e_nxt >= 0)
 #pragma unroll
       for (int d = 0; d < 3; ++d) U_nxt[d] = A.u_col[dof_nxt + d];
+    // 4./5. node-row stage and accumulation into the plane row images
+    if (ACC == 0)
+    {
+      double K[5][9], f[3];
+      const bool ok = e >= 0 && sh.bad[s] == 0;
+      if (ok) h8_stage_b<KIN>(j, es, A.mat, WANT_K, K, f);
+      if (e >= 0 && j == 0 && sh.bad[s])
+      {
+        atomicMax(&A.err[0], sh.bad[s]);
+        atomicMin(&A.err[1], e);
+      }
+      FCG_STAMP(2);
+      const uint32_t* rec_lo = sh.prec[ring(ez)];
+      const uint32_t* rec_hi = sh.prec[ring(ez + 1)];
+      const int buf_a = oz == 0 ? lo : 1 - lo;
+      const uint32_t* rec_a = oz == 0 ? rec_lo : rec_hi;
+      const bool own_a = ok && col_a >= 0 && int32_t(rec_a[PR_ROW0 + col_a]) >= 0;
+#pragma unroll 1
+      for (int c = 0; c < 4; ++c)
+      {
+        if (ok && colour == c)
+        {
+          if (own_a)
+          {
+            double* fr = sh.frow[buf_a][col_a];
+            fr[0] += f[0];
+            fr[1] += f[1];
+            fr[2] += f[2];
+          }
+          if (WANT_K)
+          {
+            const int npair = h8_npair(j);
+#pragma unroll
+            for (int p = 0; p < 5; ++p)
+            {
+              if (p >= npair) break;
+              const int b = (j + p) & 7;
+              const int dx = c_ox[b] - ox, dy = c_oy[b] - oy, dz = c_oz[b] - oz;
+              if (own_a)
+              {
+                double* blk = sh.row[buf_a][col_a] + 9 * ((dz + 1) * 9 + (dy + 1) * 3 + (dx + 1));
+#pragma unroll
+                for (int r = 0; r < 3; ++r)
+#pragma unroll
+                  for (int q = 0; q < 3; ++q) blk[3 * r + q] += K[p][r + 3 * q];
+              }
+              if (p > 0)
+              {
+                const int cb_x = ca_x + dx, cb_y = ca_y + dy;
+                if (cb_x >= 0 && cb_x < TX && cb_y >= 0 && cb_y < TY)
+                {
+                  const int col_b = cb_x + TX * cb_y;
+                  const int buf_b = c_oz[b] == 0 ? lo : 1 - lo;
+                  const uint32_t* rec_b = c_oz[b] == 0 ? rec_lo : rec_hi;
+                  if (int32_t(rec_b[PR_ROW0 + col_b]) >= 0)
+                  {
+                    double* blk = sh.row[buf_b][col_b] + 9 * ((1 - dz) * 9 + (1 - dy) * 3 + (1 - dx));
+#pragma unroll
+                    for (int r = 0; r < 3; ++r)
+#pragma unroll
+                      for (int q = 0; q < 3; ++q) blk[3 * r + q] += K[p][q + 3 * r];
+                  }
+                }
+              }
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    else
+    {
     // 4. node-row stage; results into the slot (aliases the dead stage-A data of this element)
     {
       const bool ok = e >= 0 && sh.bad[s] == 0;
@@ -231,7 +323,8 @@ __global__ __launch_bounds__(256) void fused_h8_kernel(FusedArgs A)
         atomicMin(&A.err[1], e);
       }
     }
-    __syncthreads();
+      __syncthreads();
+      FCG_STAMP(2);
     // 5. owner-computes gather into the row images of planes ez (p = 0) and ez+1 (p = 1)
     {
       const uint32_t* rec_pl[2] = {sh.prec[ring(ez)], sh.prec[ring(ez + 1)]};
@@ -301,6 +394,8 @@ __global__ __launch_bounds__(256) void fused_h8_kernel(FusedArgs A)
       }
     }
     __syncthreads();
+    }
+    FCG_STAMP(3);
     // 6. node plane ez is complete: write its rows once and clear the image
     if (ez >= kz0)
     {
@@ -363,6 +458,12 @@ __global__ __launch_bounds__(256) void fused_h8_kernel(FusedArgs A)
     }
     lo = 1 - lo;
     __syncthreads();
+    FCG_STAMP(4);
+  }
+  if (A.stamps && tid == 0)
+  {
+    for (int i = 0; i < 5; ++i) atomicAdd(&A.stamps[i], st_acc[i]);
+    atomicAdd(&A.stamps[5], 1ull);
   }
 }
 
@@ -383,6 +484,7 @@ hipError_t launch_fused_h8(const DeviceMesh& m, const double* d_u_col, bool want
   a.K = d_K;
   a.fint = d_fint;
   a.err = m.err;
+  a.stamps = m.stamps;
   a.mat = StVK{m.lambda, m.mu, m.cdiag};
   a.tiles_x = m.tiles_x;
   a.tiles_y = m.tiles_y;
@@ -391,15 +493,24 @@ hipError_t launch_fused_h8(const DeviceMesh& m, const double* d_u_col, bool want
   a.EX0 = m.EX0; a.EY0 = m.EY0; a.EZ0 = m.EZ0; a.EX = m.EX; a.EY = m.EY; a.EZ = m.EZ;
   const dim3 grid{static_cast<unsigned>(ntiles), 1, 1};
   const dim3 block{256, 1, 1};
-#define FCG_FUSED(KIN)                                                                             \
+#define FCG_FUSED3(KIN, ACC)                                                                       \
   if (want_k && overwrite)                                                                         \
-    hipLaunchKernelGGL((fused_h8_kernel<KIN, true, true>), grid, block, 0, stream, a);             \
+    hipLaunchKernelGGL((fused_h8_kernel<KIN, true, true, ACC>), grid, block, 0, stream, a);        \
   else if (want_k)                                                                                 \
-    hipLaunchKernelGGL((fused_h8_kernel<KIN, true, false>), grid, block, 0, stream, a);            \
+    hipLaunchKernelGGL((fused_h8_kernel<KIN, true, false, ACC>), grid, block, 0, stream, a);       \
   else if (overwrite)                                                                              \
-    hipLaunchKernelGGL((fused_h8_kernel<KIN, false, true>), grid, block, 0, stream, a);            \
+    hipLaunchKernelGGL((fused_h8_kernel<KIN, false, true, ACC>), grid, block, 0, stream, a);       \
   else                                                                                             \
-    hipLaunchKernelGGL((fused_h8_kernel<KIN, false, false>), grid, block, 0, stream, a);
+    hipLaunchKernelGGL((fused_h8_kernel<KIN, false, false, ACC>), grid, block, 0, stream, a);
+#define FCG_FUSED(KIN)                                                                             \
+  if (m.fused_acc == 0)                                                                            \
+  {                                                                                                \
+    FCG_FUSED3(KIN, 0)                                                                             \
+  }                                                                                                \
+  else                                                                                             \
+  {                                                                                                \
+    FCG_FUSED3(KIN, 1)                                                                             \
+  }
   if (m.kinem == 0)
   {
     FCG_FUSED(0)
@@ -408,6 +519,7 @@ hipError_t launch_fused_h8(const DeviceMesh& m, const double* d_u_col, bool want
   {
     FCG_FUSED(1)
   }
+#undef FCG_FUSED3
 #undef FCG_FUSED
   return hipGetLastError();
 }

@@ -44,6 +44,8 @@ struct DeviceMesh {
   int32_t* lat_dof = nullptr;       // [EZ+1][EY+1][EX+1] column LID of the node's first DOF or -1
   uint32_t* plane_rec = nullptr;    // [tiles_y][tiles_x][NK][PLANE_REC_WORDS] row bookkeeping
   double* tables = nullptr;         // dN at GPs [192], dN at nodes [192], weights [8]
+  int fused_acc = 0;                // 0: colour-phase accumulation, 1: owner-computes gather
+  unsigned long long* stamps = nullptr;  // diagnostic phase timers (FCG_STAMPS=1), else NULL
 };
 
 // One record per (tile, node plane): row0[16] | rowlen[16] | rbase[16] (int64) | npos[16][27]

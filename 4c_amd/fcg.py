@@ -58,6 +58,7 @@ class FcgInfo(ctypes.Structure):
 EXPORTS = ["fcg_create", "fcg_destroy", "fcg_last_error", "fcg_evaluate", "fcg_evaluate_device",
            "fcg_device_alloc", "fcg_device_free", "fcg_memcpy_h2d", "fcg_memcpy_d2h",
            "fcg_memset_device", "fcg_set_timing", "fcg_get_timing", "fcg_get_info",
+           "fcg_get_diagnostics",
            "fcg_box_mesh_create", "fcg_box_mesh_destroy", "fcg_box_mesh_desc", "fcg_box_mesh_maps",
            "fcg_box_mesh_counts"]
 
@@ -94,6 +95,7 @@ def lib():
     L.fcg_set_timing.argtypes = [vp, ctypes.c_int]
     L.fcg_get_timing.argtypes = [vp, _dp, _dp]
     L.fcg_get_info.argtypes = [vp, ctypes.POINTER(FcgInfo)]
+    L.fcg_get_diagnostics.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
     L.fcg_box_mesh_create.argtypes = [ctypes.POINTER(FcgBox), ctypes.c_int, ctypes.c_int,
                                       ctypes.POINTER(vp)]
     L.fcg_box_mesh_destroy.argtypes = [vp]
@@ -268,6 +270,12 @@ class Evaluator:
 
     def set_timing(self, enable):
         lib().fcg_set_timing(self._h, 1 if enable else 0)
+
+    def diagnostics(self):
+        """Per-phase cycle counters of the fused kernel (FCG_STAMPS=1 at creation), or None."""
+        buf = (ctypes.c_uint64 * 8)()
+        n = lib().fcg_get_diagnostics(self._h, buf, 8)
+        return list(buf) if n > 0 else None
 
     def timing(self):
         a, b = ctypes.c_double(), ctypes.c_double()

@@ -147,6 +147,12 @@ typedef struct fcg_info {
 } fcg_info;
 int fcg_get_info(const fcg_ctx* ctx, fcg_info* info);
 
+/* Diagnostics only: with FCG_STAMPS=1 in the environment at fcg_create, the fused kernel sums
+ * per-phase cycle counts (s_memtime, thread 0 of every workgroup) into 8 counters: commit,
+ * Gauss-point stage, node-row stage, accumulation, flush, workgroups (index 5).  Returns the number of
+ * counters (0 when off). */
+int fcg_get_diagnostics(const fcg_ctx* ctx, uint64_t* out, int n);
+
 /* ------------------------------------------------------------------------------------------
  * Structured-box discretization builder: a restatement of 4C's GridGenerator
  * (src/core/io/src/4C_io_gridgenerator.cpp:41-392), node ownership of Rebalance::build_graph
