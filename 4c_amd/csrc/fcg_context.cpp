@@ -70,7 +70,7 @@ hipError_t upload(T** dst, const T* src, int64_t n, int64_t& bytes)
   return hipSuccess;
 }
 
-// Structured plan (fused hex8 kernel).  Verifies the lattice hint against the connectivity:
+// Structured plan (hex8 row-block sweep kernel).  Verifies the lattice hint against the connectivity:
 // every element node must sit at lattice position ijk(e) + offset(a) consistently across
 // elements, no two elements/nodes may share a position, and every owned node row must hold
 // exactly the DOF triples of its existing lattice neighbours.
@@ -400,7 +400,7 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
     return FCG_ERR_ARG;
   }
 
-  // --- structured (fused) plan when a verified lattice hint is present
+  // --- structured (row-block sweep) plan when a verified lattice hint is present
   StructHost sp;
   std::string why;
   bool structured = false;
@@ -548,10 +548,7 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
     for (int g = 0; g < 8; ++g) fcg::shape_deriv(fcg::kHex8, &xn[3 * g], &tab[192 + 24 * g]);
     for (int g = 0; g < 8; ++g) tab[384 + g] = w[g];
     chk(upload(&m.tables, tab.data(), int64_t(tab.size()), bytes));
-    // diagnostics (tools/stamps.py): FCG_FUSED_ACC selects the accumulation variant,
-    // FCG_STAMPS=1 turns on the per-phase s_memtime counters
-    const char* acc = std::getenv("FCG_FUSED_ACC");
-    m.fused_acc = (acc && acc[0] == '1') ? 1 : 0;
+    // diagnostics (tools/stamps.py): FCG_STAMPS=1 turns on the per-phase s_memtime counters
     const char* st = std::getenv("FCG_STAMPS");
     if (st && st[0] == '1')
     {
@@ -616,7 +613,7 @@ int fcg_evaluate_device(fcg_ctx* ctx, int action, int mode, const double* d_u_co
   if (m.path == FCG_PATH_STRUCTURED)
   {
     if (he == hipSuccess)
-      he = fcg::launch_fused_h8(m, d_u_col, want_k, mode == FCG_OVERWRITE, d_K_vals, d_fint_row, s);
+      he = fcg::launch_sweep_h8(m, d_u_col, want_k, mode == FCG_OVERWRITE, d_K_vals, d_fint_row, s);
     if (T.enabled && he == hipSuccess) he = hipEventRecord(T.ev[1], s);
   }
   else

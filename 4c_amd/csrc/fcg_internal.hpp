@@ -34,7 +34,7 @@ struct DeviceMesh {
   int32_t* err = nullptr;           // [2]: code, min failing element index
   int32_t max_rowlen = 0;
 
-  // structured (fused z-sweep) plan, hex8 only
+  // structured (row-block sweep) plan, hex8 only
   int path = FCG_PATH_GENERAL;
   int32_t tiles_x = 0, tiles_y = 0, tiles_z = 0, seg_planes = 0;
   int32_t I0 = 0, J0 = 0, K0 = 0, NI = 0, NJ = 0, NK = 0;  // owned-node lattice box
@@ -44,7 +44,6 @@ struct DeviceMesh {
   int32_t* lat_dof = nullptr;       // [EZ+1][EY+1][EX+1] column LID of the node's first DOF or -1
   uint32_t* plane_rec = nullptr;    // [tiles_y][tiles_x][NK][PLANE_REC_WORDS] row bookkeeping
   double* tables = nullptr;         // dN at GPs [192], dN at nodes [192], weights [8]
-  int fused_acc = 0;                // 0: colour-phase accumulation, 1: owner-computes gather
   unsigned long long* stamps = nullptr;  // diagnostic phase timers (FCG_STAMPS=1), else NULL
 };
 
@@ -52,8 +51,8 @@ struct DeviceMesh {
 // (uint16, column position of lattice neighbour t inside the node's rows, 0xFFFF = absent).
 constexpr int PLANE_REC_WORDS = 288;
 
-// Launches the fused hex8 kernel (element evaluation + LDS row accumulation + row flush).
-hipError_t launch_fused_h8(const DeviceMesh& m, const double* d_u_col, bool want_k,
+// Launches the structured hex8 row-block sweep (element evaluation + assembly, fcg_sweep.hip).
+hipError_t launch_sweep_h8(const DeviceMesh& m, const double* d_u_col, bool want_k,
     bool overwrite, double* d_K, double* d_fint, hipStream_t stream);
 
 struct Timing {

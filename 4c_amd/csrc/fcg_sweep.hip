@@ -1,0 +1,630 @@
+// fcg_sweep.hip -- fused hex8 element evaluation + global assembly on structured (GridGenerator)
+// lattices: the row-block sweep.
+//
+// A workgroup owns a 4 x 4 column of row nodes over a z-segment of node planes and sweeps the
+// element layers bottom to top.  Per layer L (the elements between node planes L and L+1):
+//   A. one lane per (element, Gauss point) of the 5 x 5 elements touching the tile's node
+//      columns: J, J^-1, det J (and det J > 0 at node g), N_XYZ, strain or F, StVK stress
+//      (4C_solid_3D_ele_calc_lib.hpp:380-496, 579-676, 682-799; 4C_mat_stvenantkirchhoff.cpp:169-177).
+//      Into LDS go sqrt|fac| N_XYZ of the 8 nodes, for TotLag F and S, and the element's nodal
+//      forces f_a = sum_g fac F S N_XYZ_a (calc_lib.hpp:851-860, summed over the 8 Gauss-point
+//      lanes by a reduce-scatter);
+//   B. sixteen lanes per node column, four element visits each (fcg_visit_table.h): a lane sums
+//      over the elements holding both nodes of its blocks (A, B) and all Gauss points
+//        linear: G = sum fac a b^T,                 K_AB = lambda G + mu G^T + mu tr(G) I
+//        TotLag: G = sum fac (Fa)(Fb)^T, H = sum fac (a.b) F F^T, geo = sum fac a.S.b,
+//                K_AB = lambda G + mu G^T + mu H + geo I
+//      (= B_a^T C B_b + K_geo of calc_lib.hpp:872-927 for the isotropic C of fill_cmat) and
+//      writes the 3 x 3 block straight into its 3 CSR rows -- or keeps the lower-layer part of
+//      an in-plane block (dz = 0) in registers until the next layer adds the upper part.
+// Every entry of an owned row is written exactly once, by one lane, in a fixed summation order:
+// no atomics, no row image in LDS, bitwise reproducible.  Owned-rows-only assembly and column
+// positions follow SparseMatrix::assemble (4C_linalg_sparsematrix.cpp:474-543, positions resolved
+// per node row by fcg_create), the residual LinAlg::assemble (4C_linalg_utils_sparse_algebra_assemble.cpp:72-92).
+//
+// Latency hiding: two workgroups per CU (LDS 53 KB linear / 79 KB TotLag) plus, inside a
+// workgroup, register prefetch of the next node plane (coordinates, displacements) and plane
+// record while the current layer computes.
+#include <hip/hip_runtime.h>
+
+#include "fcg_hex8_element.hpp"
+#include "fcg_internal.hpp"
+#include "fcg_visit_table.h"
+
+namespace fcg {
+
+namespace {
+
+constexpr int TX = 4, TY = 4;              // node columns per tile
+constexpr int EXN = TX + 1, EYN = TY + 1;  // element columns per layer
+constexpr int NSLOT = EXN * EYN;           // 25 elements per layer
+constexpr int NXN = TX + 2;                // node columns per row of the node grid (6 x 6)
+constexpr int NNODE = NXN * (TY + 2);
+// plane record (uint32 words): row0[16] | rowlen[16] | rbase[16] (int64) | npos[16][27] (uint16)
+constexpr int PR_ROW0 = 0, PR_LEN = 16, PR_BASE = 32, PR_NPOS = 64;
+constexpr int SD = NSLOT * 8;  // nx stride of one dimension
+constexpr int SG = 3 * SD;     // nx stride of one Gauss point
+
+// hex8 node offsets in 4C node order (4C_io_gridgenerator.cpp:371-379)
+__device__ constexpr int node_ox(int n) { return ((n & 3) == 1 || (n & 3) == 2) ? 1 : 0; }
+__device__ constexpr int node_oy(int n) { return (n & 3) >= 2 ? 1 : 0; }
+__device__ constexpr int node_oz(int n) { return n >> 2; }
+
+struct SweepArgs {
+  const double* u_col;
+  const double* lat_x;       // [LZ][LY][LX][3] node coordinates on the column-node lattice
+  const int32_t* lat_dof;    // [LZ][LY][LX] column LID of the first DOF, -1 = no node
+  const int32_t* elem_at;    // [EZ][EY][EX] column element or -1
+  const uint32_t* plane_rec; // [tiles_y][tiles_x][NK][PLANE_REC_WORDS]
+  const double* tables;
+  double* K;
+  double* fint;
+  int32_t* err;
+  unsigned long long* stamps;  // diagnostic phase timers (NULL = off, the production setting)
+  StVK mat;
+  int32_t tiles_x, tiles_y, seg_planes;
+  int32_t I0, J0, K0, NI, NJ, NK;
+  int32_t EX0, EY0, EZ0, EX, EY, EZ;  // element box; the node lattice box is EX+1 x EY+1 x EZ+1
+};
+
+template <int KIN>
+struct SweepShared {
+  double nx[8][3][NSLOT][8];          // sqrt|fac| N_XYZ: [gp][dim][slot][node]
+  double gp[KIN ? 8 : 1][KIN ? NSLOT : 1][16];  // TotLag: F (column-major) | S (Voigt) | pad
+  double fe[NSLOT][8][3];             // nodal forces of the layer's elements
+  double node[2][NNODE][6];           // X | u of the 6 x 6 node columns, by plane parity
+  uint32_t prec[3][PLANE_REC_WORDS];  // plane records, ring by plane mod 3
+  double dN[8][8][3];
+  double dNn[8][8][3];
+  double w8[8];
+  uint32_t neg[NSLOT];  // bit g set: fac < 0 at Gauss point g
+};
+
+__device__ inline int ring(int p) { return (p % 3 + 3) % 3; }
+
+// Stage A for element slot s, Gauss point g of layer L (element e, -1 = none).  Written for a
+// small register footprint: node data stays in LDS and N_XYZ is recomputed where needed.
+template <int KIN>
+__device__ inline void sweep_stage_a(SweepShared<KIN>& sh, const SweepArgs& A, int s, int g,
+    int sx, int sy, int L, int e)
+{
+  const bool valid = e >= 0;
+  const double* nd[8];
+#pragma unroll
+  for (int n = 0; n < 8; ++n)
+    nd[n] = sh.node[(L + node_oz(n)) & 1][(sy + node_oy(n)) * NXN + sx + node_ox(n)];
+  double J[9], Jn[9];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) J[q] = Jn[q] = 0.0;
+#pragma unroll
+  for (int n = 0; n < 8; ++n)
+  {
+    const double x0 = nd[n][0], x1 = nd[n][1], x2 = nd[n][2];
+    const double d0 = sh.dN[g][n][0], d1 = sh.dN[g][n][1], d2 = sh.dN[g][n][2];
+    J[0] += d0 * x0; J[1] += d1 * x0; J[2] += d2 * x0;
+    J[3] += d0 * x1; J[4] += d1 * x1; J[5] += d2 * x1;
+    J[6] += d0 * x2; J[7] += d1 * x2; J[8] += d2 * x2;
+    const double n0 = sh.dNn[g][n][0], n1 = sh.dNn[g][n][1], n2 = sh.dNn[g][n][2];
+    Jn[0] += n0 * x0; Jn[1] += n1 * x0; Jn[2] += n2 * x0;
+    Jn[3] += n0 * x1; Jn[4] += n1 * x1; Jn[5] += n2 * x1;
+    Jn[6] += n0 * x2; Jn[7] += n1 * x2; Jn[8] += n2 * x2;
+  }
+  int bad = 0;
+  const double detn = h8_invert3x3(Jn);
+  if (detn == 0.0) bad = 2;
+  else if (!(detn > 0)) bad = 1;
+  const double det = h8_invert3x3(J);
+  if (det == 0.0) bad = 2;
+  const double fac = det * sh.w8[g];
+  const double sq = sqrt(fabs(fac));
+  // N_XYZ of node n (J now holds J^-1, column-major)
+  auto nxyz = [&](int n, double& n0, double& n1, double& n2) {
+    const double d0 = sh.dN[g][n][0], d1 = sh.dN[g][n][1], d2 = sh.dN[g][n][2];
+    n0 = J[0] * d0 + J[3] * d1 + J[6] * d2;
+    n1 = J[1] * d0 + J[4] * d1 + J[7] * d2;
+    n2 = J[2] * d0 + J[5] * d1 + J[8] * d2;
+  };
+  double E[6] = {0, 0, 0, 0, 0, 0};
+  double F[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int n = 0; n < 8; ++n)
+  {
+    double n0, n1, n2;
+    nxyz(n, n0, n1, n2);
+    sh.nx[g][0][s][n] = valid ? sq * n0 : 0.0;
+    sh.nx[g][1][s][n] = valid ? sq * n1 : 0.0;
+    sh.nx[g][2][s][n] = valid ? sq * n2 : 0.0;
+    const double u0 = nd[n][3], u1 = nd[n][4], u2 = nd[n][5];
+    if (KIN == 0)
+    {
+      E[0] += n0 * u0;
+      E[1] += n1 * u1;
+      E[2] += n2 * u2;
+      E[3] += n1 * u0 + n0 * u1;
+      E[4] += n2 * u1 + n1 * u2;
+      E[5] += n2 * u0 + n0 * u2;
+    }
+    else
+    {
+      // hex8: F = x N_XYZ^T from current coordinates (calc_lib.hpp:585-595)
+      const double q0 = nd[n][0] + u0, q1 = nd[n][1] + u1, q2 = nd[n][2] + u2;
+      F[0] += q0 * n0; F[1] += q1 * n0; F[2] += q2 * n0;
+      F[3] += q0 * n1; F[4] += q1 * n1; F[5] += q2 * n1;
+      F[6] += q0 * n2; F[7] += q1 * n2; F[8] += q2 * n2;
+    }
+  }
+  if (KIN == 1)
+  {
+    double Fi[9];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) Fi[q] = F[q];
+    if (h8_invert3x3(Fi) == 0.0) bad = 2;
+    double C[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        C[r + 3 * q] = F[3 * r] * F[3 * q] + F[3 * r + 1] * F[3 * q + 1] + F[3 * r + 2] * F[3 * q + 2];
+    E[0] = 0.5 * (C[0] - 1.0);
+    E[1] = 0.5 * (C[4] - 1.0);
+    E[2] = 0.5 * (C[8] - 1.0);
+    E[3] = C[3];
+    E[4] = C[7];
+    E[5] = C[2];
+  }
+  const StVK& m = A.mat;
+  double S[6];
+  S[0] = m.cdiag * E[0] + m.lambda * E[1] + m.lambda * E[2];
+  S[1] = m.lambda * E[0] + m.cdiag * E[1] + m.lambda * E[2];
+  S[2] = m.lambda * E[0] + m.lambda * E[1] + m.cdiag * E[2];
+  S[3] = m.mu * E[3];
+  S[4] = m.mu * E[4];
+  S[5] = m.mu * E[5];
+  if (KIN == 1)
+  {
+#pragma unroll
+    for (int q = 0; q < 9; ++q) sh.gp[KIN ? g : 0][KIN ? s : 0][q] = valid ? F[q] : 0.0;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) sh.gp[KIN ? g : 0][KIN ? s : 0][9 + q] = valid ? S[q] : 0.0;
+  }
+  if (valid && bad)
+  {
+    atomicMax(&A.err[0], bad);
+    atomicMin(&A.err[1], e);
+  }
+  const unsigned long long neg = __ballot(valid && fac < 0.0);
+  if (g == 0) sh.neg[s] = uint32_t((neg >> (threadIdx.x & 56)) & 0xFFull);
+
+  // nodal force contribution of this Gauss point, f_n = fac F S N_XYZ_n, reduce-scattered over
+  // the element's 8 Gauss-point lanes: lane g ends with node g's sum
+  auto fnode = [&](int n, double* out) {
+    double a0, a1, a2;
+    nxyz(n, a0, a1, a2);
+    double t0 = S[0] * a0 + S[3] * a1 + S[5] * a2;
+    double t1 = S[3] * a0 + S[1] * a1 + S[4] * a2;
+    double t2 = S[5] * a0 + S[4] * a1 + S[2] * a2;
+    if (KIN == 1)
+    {
+      const double s0 = F[0] * t0 + F[3] * t1 + F[6] * t2;
+      const double s1 = F[1] * t0 + F[4] * t1 + F[7] * t2;
+      const double s2 = F[2] * t0 + F[5] * t1 + F[8] * t2;
+      t0 = s0;
+      t1 = s1;
+      t2 = s2;
+    }
+    out[0] = fac * t0;
+    out[1] = fac * t1;
+    out[2] = fac * t2;
+  };
+  double w4[4][3], w2[2][3], w1[3];
+  const bool h4 = g & 4, h2 = g & 2, h1 = g & 1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+  {
+    double lo[3], hi[3];
+    fnode(i, lo);
+    fnode(i + 4, hi);
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+    {
+      const double mine = h4 ? hi[d] : lo[d];
+      const double other = h4 ? lo[d] : hi[d];
+      w4[i][d] = mine + __shfl_xor(other, 4);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+    {
+      const double mine = h2 ? w4[i + 2][d] : w4[i][d];
+      const double other = h2 ? w4[i][d] : w4[i + 2][d];
+      w2[i][d] = mine + __shfl_xor(other, 2);
+    }
+#pragma unroll
+  for (int d = 0; d < 3; ++d)
+  {
+    const double mine = h1 ? w2[1][d] : w2[0][d];
+    const double other = h1 ? w2[0][d] : w2[1][d];
+    w1[d] = mine + __shfl_xor(other, 1);
+  }
+#pragma unroll
+  for (int d = 0; d < 3; ++d) sh.fe[s][g][d] = valid ? w1[d] : 0.0;
+}
+
+// One element visit: accumulate the block (a, b) of element slot `slot` over its Gauss points.
+// Acc layout: G[9] (row-major, G[3r+q] = sum a'_r b'_q) then, for TotLag, H[6] and geo.
+template <int KIN, bool NEG>
+__device__ inline void sweep_visit(const SweepShared<KIN>& sh, int slot, int a, int b,
+    uint32_t nm, double* acc)
+{
+  const double* pa = &sh.nx[0][0][slot][a];
+  const double* pb = &sh.nx[0][0][slot][b];
+#pragma unroll
+  for (int g = 0; g < 8; ++g)
+  {
+    double a0 = pa[g * SG], a1 = pa[g * SG + SD], a2 = pa[g * SG + 2 * SD];
+    const double b0 = pb[g * SG], b1 = pb[g * SG + SD], b2 = pb[g * SG + 2 * SD];
+    if (NEG && ((nm >> g) & 1u))
+    {
+      a0 = -a0;
+      a1 = -a1;
+      a2 = -a2;
+    }
+    if (KIN == 0)
+    {
+      acc[0] += a0 * b0; acc[1] += a0 * b1; acc[2] += a0 * b2;
+      acc[3] += a1 * b0; acc[4] += a1 * b1; acc[5] += a1 * b2;
+      acc[6] += a2 * b0; acc[7] += a2 * b1; acc[8] += a2 * b2;
+    }
+    else
+    {
+      const double* P = sh.gp[KIN ? g : 0][KIN ? slot : 0];
+      const double F0 = P[0], F1 = P[1], F2 = P[2], F3 = P[3], F4 = P[4], F5 = P[5], F6 = P[6],
+                   F7 = P[7], F8 = P[8];
+      const double fa0 = F0 * a0 + F3 * a1 + F6 * a2;
+      const double fa1 = F1 * a0 + F4 * a1 + F7 * a2;
+      const double fa2 = F2 * a0 + F5 * a1 + F8 * a2;
+      const double fb0 = F0 * b0 + F3 * b1 + F6 * b2;
+      const double fb1 = F1 * b0 + F4 * b1 + F7 * b2;
+      const double fb2 = F2 * b0 + F5 * b1 + F8 * b2;
+      acc[0] += fa0 * fb0; acc[1] += fa0 * fb1; acc[2] += fa0 * fb2;
+      acc[3] += fa1 * fb0; acc[4] += fa1 * fb1; acc[5] += fa1 * fb2;
+      acc[6] += fa2 * fb0; acc[7] += fa2 * fb1; acc[8] += fa2 * fb2;
+      const double ab = a0 * b0 + a1 * b1 + a2 * b2;
+      acc[9] += ab * (F0 * F0 + F3 * F3 + F6 * F6);
+      acc[10] += ab * (F1 * F1 + F4 * F4 + F7 * F7);
+      acc[11] += ab * (F2 * F2 + F5 * F5 + F8 * F8);
+      acc[12] += ab * (F0 * F1 + F3 * F4 + F6 * F7);
+      acc[13] += ab * (F1 * F2 + F4 * F5 + F7 * F8);
+      acc[14] += ab * (F2 * F0 + F5 * F3 + F8 * F6);
+      const double S0 = P[9], S1 = P[10], S2 = P[11], S3 = P[12], S4 = P[13], S5 = P[14];
+      const double sb0 = S0 * b0 + S3 * b1 + S5 * b2;
+      const double sb1 = S3 * b0 + S1 * b1 + S4 * b2;
+      const double sb2 = S5 * b0 + S4 * b1 + S2 * b2;
+      acc[15] += a0 * sb0 + a1 * sb1 + a2 * sb2;
+    }
+  }
+}
+
+// Diagnostic phase stamps: thread 0 of each workgroup adds the cycles of every phase (including
+// the barrier wait that ends it) into A.stamps[phase]; off (uniform branch, no s_memtime) when
+// A.stamps is NULL.  Phases: 0 element stage (A), 1 visit stage (B); [5] counts workgroups.
+#define FCG_STAMP(i)                                                                               \
+  if (A.stamps && tid == 0)                                                                        \
+  {                                                                                                \
+    const unsigned long long now = __builtin_amdgcn_s_memtime();                                  \
+    st_acc[i] += now - st_last;                                                                    \
+    st_last = now;                                                                                 \
+  }
+
+template <int KIN, bool WANT_K, bool OVERWRITE>
+__global__ __launch_bounds__(256, 2) void sweep_h8_kernel(SweepArgs A)
+{
+  __shared__ SweepShared<KIN> sh;
+  constexpr int NACC = KIN ? 16 : 9;
+  const int tid = threadIdx.x;
+  unsigned long long st_acc[2] = {0, 0};
+  unsigned long long st_last = A.stamps ? __builtin_amdgcn_s_memtime() : 0ull;
+  const int tile = blockIdx.x;
+  const int tx = tile % A.tiles_x;
+  const int ty = (tile / A.tiles_x) % A.tiles_y;
+  const int tz = tile / (A.tiles_x * A.tiles_y);
+  const int i0 = A.I0 + TX * tx, j0 = A.J0 + TY * ty;
+  const int kz0 = A.K0 + A.seg_planes * tz;
+  const int kz1 = min(kz0 + A.seg_planes, A.K0 + A.NK);
+  const uint32_t* prec_tile = A.plane_rec + (int64_t(ty) * A.tiles_x + tx) * A.NK * PLANE_REC_WORDS;
+  const int64_t LX = A.EX + 1, LY = A.EY + 1;
+
+  for (int v = tid; v < 192; v += 256)
+  {
+    (&sh.dN[0][0][0])[v] = A.tables[v];
+    (&sh.dNn[0][0][0])[v] = A.tables[192 + v];
+  }
+  if (tid < 8) sh.w8[tid] = A.tables[384 + tid];
+
+  // stage-A lane: element slot s, Gauss point g
+  const int s = tid >> 3, g = tid & 7;
+  const bool a_lane = s < NSLOT;
+  const int sx = s % EXN, sy = s / EXN;
+  const int ex = i0 - 1 + sx, ey = j0 - 1 + sy;
+  const bool exy_in = a_lane && ex >= A.EX0 && ex < A.EX0 + A.EX && ey >= A.EY0 && ey < A.EY0 + A.EY;
+  auto load_elem = [&](int lz) -> int {
+    if (!exy_in || lz < A.EZ0 || lz >= A.EZ0 + A.EZ) return -1;
+    return A.elem_at[(int64_t(lz - A.EZ0) * A.EY + (ey - A.EY0)) * A.EX + (ex - A.EX0)];
+  };
+  // node-load lane: column ncol of the 6 x 6 node grid, component ncomp (X 0-2, u 3-5)
+  const bool n_lane = tid < NNODE * 6;
+  const int ncol = tid / 6, ncomp = tid - 6 * (tid / 6);
+  const int ni = i0 - 1 + ncol % NXN, nj = j0 - 1 + ncol / NXN;
+  const bool nxy_in =
+      n_lane && ni >= A.EX0 && ni <= A.EX0 + A.EX && nj >= A.EY0 && nj <= A.EY0 + A.EY;
+  const int64_t nlat_xy = nxy_in ? int64_t(nj - A.EY0) * LX + (ni - A.EX0) : 0;
+  auto load_node = [&](int P) -> double {
+    if (!nxy_in || P < A.EZ0 || P > A.EZ0 + A.EZ) return 0.0;
+    const int64_t li = int64_t(P - A.EZ0) * LX * LY + nlat_xy;
+    if (ncomp < 3) return A.lat_x[3 * li + ncomp];
+    const int dof = A.lat_dof[li];
+    return dof >= 0 ? A.u_col[dof + ncomp - 3] : 0.0;
+  };
+  auto load_rec = [&](int p, uint32_t* w) {
+    const bool in = p >= kz0 && p < kz1;
+    const uint32_t* src = prec_tile + int64_t(in ? p - A.K0 : 0) * PLANE_REC_WORDS;
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+    {
+      const int v = tid + 256 * k;
+      if (v < PLANE_REC_WORDS) w[k] = in ? src[v] : (v < PR_LEN ? 0xFFFFFFFFu : 0u);
+    }
+  };
+  auto store_rec = [&](int p, const uint32_t* w) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+    {
+      const int v = tid + 256 * k;
+      if (v < PLANE_REC_WORDS) sh.prec[ring(p)][v] = w[k];
+    }
+  };
+
+  // visit lane: node column c, task k
+  const int c = tid >> 4, k = tid & 15;
+  const int cx = c % TX, cy = c / TX;
+  uint32_t vis[4];
+#pragma unroll
+  for (int v = 0; v < 4; ++v) vis[v] = kVisit[k][v];
+
+  // --- prologue: node planes kz0-1, kz0 and their records; prefetch plane kz0+1
+  if (n_lane)
+  {
+    sh.node[(kz0 - 1) & 1][ncol][ncomp] = load_node(kz0 - 1);
+    sh.node[kz0 & 1][ncol][ncomp] = load_node(kz0);
+  }
+  {
+    uint32_t w[2];
+    load_rec(kz0 - 1, w);
+    store_rec(kz0 - 1, w);
+    load_rec(kz0, w);
+    store_rec(kz0, w);
+  }
+  double node_nxt = n_lane ? load_node(kz0 + 1) : 0.0;
+  uint32_t rec_nxt[2];
+  load_rec(kz0 + 1, rec_nxt);
+  int e_cur = load_elem(kz0 - 1);
+  double hold0[9], hold1[9], fhold[3];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) hold0[i] = hold1[i] = 0.0;
+  fhold[0] = fhold[1] = fhold[2] = 0.0;
+  __syncthreads();
+
+  for (int L = kz0 - 1; L < kz1; ++L)
+  {
+    const int e_nxt = load_elem(L + 1);
+    // A. element stage
+    if (a_lane) sweep_stage_a<KIN>(sh, A, s, g, sx, sy, L, e_cur);
+    __syncthreads();
+    FCG_STAMP(0);
+    // commit plane L+2 (nodes into plane L's parity slot, record into plane L-1's ring slot),
+    // then prefetch plane L+3
+    if (n_lane) sh.node[(L + 2) & 1][ncol][ncomp] = node_nxt;
+    store_rec(L + 2, rec_nxt);
+    node_nxt = n_lane ? load_node(L + 3) : 0.0;
+    load_rec(L + 3, rec_nxt);
+
+    // B. visit stage
+    const bool wl = L >= kz0, wl1 = L + 1 < kz1;
+    const uint32_t* recL = sh.prec[ring(L)];
+    const uint32_t* recL1 = sh.prec[ring(L + 1)];
+    // the self block's lower part lives in lane k1; lane k0 completes it
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+    {
+      const double t = __shfl_xor(hold0[i], 1);
+      if (k == 0) hold0[i] = t;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+    {
+      const double t = __shfl_xor(fhold[i], 1);
+      if (k == 0) fhold[i] = t;
+    }
+    if (WANT_K)
+    {
+      double acc[NACC];
+#pragma unroll
+      for (int i = 0; i < NACC; ++i) acc[i] = 0.0;
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+      {
+        const uint32_t w = vis[v];
+        const int q = w & 3, a = (w >> 2) & 7, b = (w >> 5) & 7, act = (w >> 8) & 7,
+                  t = (w >> 12) & 31;
+        const int slot = (cx + (q & 1)) + EXN * (cy + (q >> 1));
+        const uint32_t nm = sh.neg[slot];
+        if (nm == 0u)
+          sweep_visit<KIN, false>(sh, slot, a, b, nm, acc);
+        else
+          sweep_visit<KIN, true>(sh, slot, a, b, nm, acc);
+        if (act == kVisitActCont) continue;
+        // K_AB of the accumulated part
+        const double lam = A.mat.lambda, mu = A.mat.mu;
+        double Kb[9];
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+          for (int qq = 0; qq < 3; ++qq) Kb[3 * r + qq] = lam * acc[3 * r + qq] + mu * acc[3 * qq + r];
+        if (KIN == 0)
+        {
+          const double tr = mu * (acc[0] + acc[4] + acc[8]);
+          Kb[0] += tr;
+          Kb[4] += tr;
+          Kb[8] += tr;
+        }
+        else
+        {
+          Kb[0] += mu * acc[9] + acc[15];
+          Kb[4] += mu * acc[10] + acc[15];
+          Kb[8] += mu * acc[11] + acc[15];
+          Kb[1] += mu * acc[12]; Kb[3] += mu * acc[12];
+          Kb[5] += mu * acc[13]; Kb[7] += mu * acc[13];
+          Kb[2] += mu * acc[14]; Kb[6] += mu * acc[14];
+        }
+#pragma unroll
+        for (int i = 0; i < NACC; ++i) acc[i] = 0.0;
+        if (act == kVisitActHold0)
+        {
+#pragma unroll
+          for (int i = 0; i < 9; ++i) hold0[i] = Kb[i];
+          continue;
+        }
+        if (act == kVisitActHold1)
+        {
+#pragma unroll
+          for (int i = 0; i < 9; ++i) hold1[i] = Kb[i];
+          continue;
+        }
+        if (act == kVisitActWriteLH0)
+        {
+#pragma unroll
+          for (int i = 0; i < 9; ++i) Kb[i] = hold0[i] + Kb[i];
+        }
+        else if (act == kVisitActWriteLH1)
+        {
+#pragma unroll
+          for (int i = 0; i < 9; ++i) Kb[i] = hold1[i] + Kb[i];
+        }
+        const bool to_l1 = act == kVisitActWriteL1;
+        if (!(to_l1 ? wl1 : wl)) continue;
+        const uint32_t* rec = to_l1 ? recL1 : recL;
+        const int32_t row0 = int32_t(rec[PR_ROW0 + c]);
+        if (row0 < 0) continue;
+        const uint16_t pos = reinterpret_cast<const uint16_t*>(rec + PR_NPOS)[27 * c + t];
+        if (pos == 0xFFFF) continue;
+        const int64_t base = int64_t(rec[PR_BASE + 2 * c]) | (int64_t(rec[PR_BASE + 2 * c + 1]) << 32);
+        const int64_t len = int32_t(rec[PR_LEN + c]);
+        double* dst = A.K + base + pos;
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+          for (int qq = 0; qq < 3; ++qq)
+          {
+            if (OVERWRITE)
+              dst[r * len + qq] = Kb[3 * r + qq];
+            else
+              dst[r * len + qq] += Kb[3 * r + qq];
+          }
+      }
+    }
+    // nodal forces: lane k0 completes plane L's rows, lane k1 starts plane L+1's
+    if (k < 2)
+    {
+      double fs[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+      {
+        const int qx = q & 1, qy = q >> 1;
+        const int slot = (cx + qx) + EXN * (cy + qy);
+        // row node at local (1-qx, 1-qy, k): 4C order index
+        const int n = 4 * k + ((1 - qy) ? (1 - qx ? 2 : 3) : (1 - qx ? 1 : 0));
+#pragma unroll
+        for (int d = 0; d < 3; ++d) fs[d] += sh.fe[slot][n][d];
+      }
+      if (k == 1)
+      {
+#pragma unroll
+        for (int d = 0; d < 3; ++d) fhold[d] = fs[d];
+      }
+      else if (wl)
+      {
+        const int32_t row0 = int32_t(recL[PR_ROW0 + c]);
+        if (row0 >= 0)
+        {
+#pragma unroll
+          for (int d = 0; d < 3; ++d)
+          {
+            if (OVERWRITE)
+              A.fint[row0 + d] = fhold[d] + fs[d];
+            else
+              A.fint[row0 + d] += fhold[d] + fs[d];
+          }
+        }
+      }
+    }
+    e_cur = e_nxt;
+    __syncthreads();
+    FCG_STAMP(1);
+  }
+  if (A.stamps && tid == 0)
+  {
+    for (int i = 0; i < 2; ++i) atomicAdd(&A.stamps[i], st_acc[i]);
+    atomicAdd(&A.stamps[5], 1ull);
+  }
+}
+
+}  // namespace
+
+hipError_t launch_sweep_h8(const DeviceMesh& m, const double* d_u_col, bool want_k,
+    bool overwrite, double* d_K, double* d_fint, hipStream_t stream)
+{
+  const int64_t ntiles = int64_t(m.tiles_x) * m.tiles_y * m.tiles_z;
+  if (ntiles == 0) return hipSuccess;
+  SweepArgs a;
+  a.u_col = d_u_col;
+  a.lat_x = m.lat_x;
+  a.lat_dof = m.lat_dof;
+  a.elem_at = m.elem_at;
+  a.plane_rec = m.plane_rec;
+  a.tables = m.tables;
+  a.K = d_K;
+  a.fint = d_fint;
+  a.err = m.err;
+  a.stamps = m.stamps;
+  a.mat = StVK{m.lambda, m.mu, m.cdiag};
+  a.tiles_x = m.tiles_x;
+  a.tiles_y = m.tiles_y;
+  a.seg_planes = m.seg_planes;
+  a.I0 = m.I0; a.J0 = m.J0; a.K0 = m.K0; a.NI = m.NI; a.NJ = m.NJ; a.NK = m.NK;
+  a.EX0 = m.EX0; a.EY0 = m.EY0; a.EZ0 = m.EZ0; a.EX = m.EX; a.EY = m.EY; a.EZ = m.EZ;
+  const dim3 grid{static_cast<unsigned>(ntiles), 1, 1};
+  const dim3 block{256, 1, 1};
+#define FCG_SWEEP(KIN)                                                                             \
+  if (want_k && overwrite)                                                                         \
+    hipLaunchKernelGGL((sweep_h8_kernel<KIN, true, true>), grid, block, 0, stream, a);             \
+  else if (want_k)                                                                                 \
+    hipLaunchKernelGGL((sweep_h8_kernel<KIN, true, false>), grid, block, 0, stream, a);            \
+  else if (overwrite)                                                                              \
+    hipLaunchKernelGGL((sweep_h8_kernel<KIN, false, true>), grid, block, 0, stream, a);            \
+  else                                                                                             \
+    hipLaunchKernelGGL((sweep_h8_kernel<KIN, false, false>), grid, block, 0, stream, a);
+  if (m.kinem == 0)
+  {
+    FCG_SWEEP(0)
+  }
+  else
+  {
+    FCG_SWEEP(1)
+  }
+#undef FCG_SWEEP
+  return hipGetLastError();
+}
+
+}  // namespace fcg
