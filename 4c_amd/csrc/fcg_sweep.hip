@@ -6,9 +6,7 @@
 //   A. one lane per (element, Gauss point) of the 5 x 5 elements touching the tile's node
 //      columns: J, J^-1, det J (and det J > 0 at node g), N_XYZ, strain or F, StVK stress
 //      (4C_solid_3D_ele_calc_lib.hpp:380-496, 579-676, 682-799; 4C_mat_stvenantkirchhoff.cpp:169-177).
-//      Into LDS go sqrt|fac| N_XYZ of the 8 nodes, for TotLag F and S, and the element's nodal
-//      forces f_a = sum_g fac F S N_XYZ_a (calc_lib.hpp:851-860, summed over the 8 Gauss-point
-//      lanes by a reduce-scatter);
+//      Into LDS go sqrt|fac| N_XYZ of the 8 nodes and the stress (with F for TotLag);
 //   B. sixteen lanes per node column, four element visits each (fcg_visit_table.h): a lane sums
 //      over the elements holding both nodes of its blocks (A, B) and all Gauss points
 //        linear: G = sum fac a b^T,                 K_AB = lambda G + mu G^T + mu tr(G) I
@@ -17,6 +15,8 @@
 //      (= B_a^T C B_b + K_geo of calc_lib.hpp:872-927 for the isotropic C of fill_cmat) and
 //      writes the 3 x 3 block straight into its 3 CSR rows -- or keeps the lower-layer part of
 //      an in-plane block (dz = 0) in registers until the next layer adds the upper part.
+//      The residual rows f_A = sum fac F S N_XYZ_A (calc_lib.hpp:851-860) are summed the same way,
+//      16 lanes per column.
 // Every entry of an owned row is written exactly once, by one lane, in a fixed summation order:
 // no atomics, no row image in LDS, bitwise reproducible.  Owned-rows-only assembly and column
 // positions follow SparseMatrix::assemble (4C_linalg_sparsematrix.cpp:474-543, positions resolved
@@ -42,8 +42,15 @@ constexpr int NXN = TX + 2;                // node columns per row of the node g
 constexpr int NNODE = NXN * (TY + 2);
 // plane record (uint32 words): row0[16] | rowlen[16] | rbase[16] (int64) | npos[16][27] (uint16)
 constexpr int PR_ROW0 = 0, PR_LEN = 16, PR_BASE = 32, PR_NPOS = 64;
-constexpr int SD = NSLOT * 8;  // nx stride of one dimension
-constexpr int SG = 3 * SD;     // nx stride of one Gauss point
+// LDS image of sqrt|fac| N_XYZ: [dim][Gauss-point pair p][slot][node ^ swizzle][2], the two
+// Gauss points 2p, 2p+1 of a node side by side so that one ds_read_b128 fetches both.  The node
+// swizzle (p + 4 (slot & 1)) spreads the stage-A stores of an element's 8 lanes (and of the
+// 2 elements of a 16-lane store group) over distinct banks.
+__device__ constexpr int nx_sw(int p, int slot) { return (p + 4 * (slot & 1)) & 7; }
+__device__ constexpr int nx2i(int d, int p, int slot, int n)
+{
+  return (((d * 4 + p) * NSLOT + slot) * 8 + (n ^ nx_sw(p, slot))) * 2;
+}
 
 // hex8 node offsets in 4C node order (4C_io_gridgenerator.cpp:371-379)
 __device__ constexpr int node_ox(int n) { return ((n & 3) == 1 || (n & 3) == 2) ? 1 : 0; }
@@ -69,18 +76,38 @@ struct SweepArgs {
 
 template <int KIN>
 struct SweepShared {
-  double nx[8][3][NSLOT][8];          // sqrt|fac| N_XYZ: [gp][dim][slot][node]
-  double gp[KIN ? 8 : 1][KIN ? NSLOT : 1][16];  // TotLag: F (column-major) | S (Voigt) | pad
-  double fe[NSLOT][8][3];             // nodal forces of the layer's elements
+  alignas(16) double nx[3 * 4 * NSLOT * 8 * 2];  // sqrt|fac| N_XYZ, see nx2i()
+  // TotLag: F (column-major) | S (Voigt) | c = fac / sqrt|fac|;  linear: c S (Voigt) | pad
+  double gp[8][NSLOT][KIN ? 16 : 6];
   double node[2][NNODE][6];           // X | u of the 6 x 6 node columns, by plane parity
   uint32_t prec[3][PLANE_REC_WORDS];  // plane records, ring by plane mod 3
   double dN[8][8][3];
   double dNn[8][8][3];
   double w8[8];
   uint32_t neg[NSLOT];  // bit g set: fac < 0 at Gauss point g
+  // lower-layer parts of the in-plane blocks (dz = 0) of node plane L+1: [column][slot][3x3],
+  // slot = in-plane neighbour (dy+1)*3 + dx+1 (read, then rewritten, by the same lane) except for
+  // the self block, which lane k1 writes and lane k0 reads: slot 4 or 9 by plane parity
+  double hold[TX * TY][10][9];
+  double fhold[2][TX * TY][3];  // residual parts, by plane parity
 };
 
 __device__ inline int ring(int p) { return (p % 3 + 3) % 3; }
+
+// Cross-lane moves of a double by DPP (all lanes of the row active)
+constexpr int kDppXor1 = 0xB1;        // quad_perm [1,0,3,2]
+constexpr int kDppXor2 = 0x4E;        // quad_perm [2,3,0,1]
+constexpr int kDppHalfMirror = 0x141;  // lane i <-> 7-i within 8
+template <int CTRL>
+__device__ inline double dpp_f64(double v)
+{
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// 4C hex8 node index of the node at (ox, oy, oz) of an element (4C_io_gridgenerator.cpp:371-379)
+__device__ inline int node_at(int ox, int oy, int oz) { return 4 * oz + (oy ? (ox ? 2 : 3) : (ox ? 1 : 0)); }
 
 // Stage A for element slot s, Gauss point g of layer L (element e, -1 = none).  Written for a
 // small register footprint: node data stays in LDS and N_XYZ is recomputed where needed.
@@ -110,13 +137,17 @@ __device__ inline void sweep_stage_a(SweepShared<KIN>& sh, const SweepArgs& A, i
     Jn[6] += n0 * x2; Jn[7] += n1 * x2; Jn[8] += n2 * x2;
   }
   int bad = 0;
-  const double detn = h8_invert3x3(Jn);
+  // det J at node g only (same expansion as invert3x3's determinant)
+  const double detn = Jn[0] * (Jn[4] * Jn[8] - Jn[5] * Jn[7]) + Jn[3] * (Jn[2] * Jn[7] - Jn[1] * Jn[8]) +
+                      Jn[6] * (Jn[1] * Jn[5] - Jn[2] * Jn[4]);
   if (detn == 0.0) bad = 2;
   else if (!(detn > 0)) bad = 1;
   const double det = h8_invert3x3(J);
   if (det == 0.0) bad = 2;
   const double fac = det * sh.w8[g];
-  const double sq = sqrt(fabs(fac));
+  // missing element (outside the column set): all its LDS data become exact zeros
+  const double sq = valid ? sqrt(fabs(fac)) : 0.0;
+  const double cf = fac < 0.0 ? -sq : sq;  // fac / sqrt|fac|
   // N_XYZ of node n (J now holds J^-1, column-major)
   auto nxyz = [&](int n, double& n0, double& n1, double& n2) {
     const double d0 = sh.dN[g][n][0], d1 = sh.dN[g][n][1], d2 = sh.dN[g][n][2];
@@ -131,9 +162,9 @@ __device__ inline void sweep_stage_a(SweepShared<KIN>& sh, const SweepArgs& A, i
   {
     double n0, n1, n2;
     nxyz(n, n0, n1, n2);
-    sh.nx[g][0][s][n] = valid ? sq * n0 : 0.0;
-    sh.nx[g][1][s][n] = valid ? sq * n1 : 0.0;
-    sh.nx[g][2][s][n] = valid ? sq * n2 : 0.0;
+    sh.nx[nx2i(0, g >> 1, s, n) + (g & 1)] = sq * n0;
+    sh.nx[nx2i(1, g >> 1, s, n) + (g & 1)] = sq * n1;
+    sh.nx[nx2i(2, g >> 1, s, n) + (g & 1)] = sq * n2;
     const double u0 = nd[n][3], u1 = nd[n][4], u2 = nd[n][5];
     if (KIN == 0)
     {
@@ -180,12 +211,19 @@ __device__ inline void sweep_stage_a(SweepShared<KIN>& sh, const SweepArgs& A, i
   S[3] = m.mu * E[3];
   S[4] = m.mu * E[4];
   S[5] = m.mu * E[5];
+  double* P = sh.gp[g][s];
   if (KIN == 1)
   {
 #pragma unroll
-    for (int q = 0; q < 9; ++q) sh.gp[KIN ? g : 0][KIN ? s : 0][q] = valid ? F[q] : 0.0;
+    for (int q = 0; q < 9; ++q) P[q] = F[q];
 #pragma unroll
-    for (int q = 0; q < 6; ++q) sh.gp[KIN ? g : 0][KIN ? s : 0][9 + q] = valid ? S[q] : 0.0;
+    for (int q = 0; q < 6; ++q) P[9 + q] = S[q];
+    P[15] = cf;
+  }
+  else
+  {
+#pragma unroll
+    for (int q = 0; q < 6; ++q) P[q] = cf * S[q];
   }
   if (valid && bad)
   {
@@ -195,61 +233,6 @@ __device__ inline void sweep_stage_a(SweepShared<KIN>& sh, const SweepArgs& A, i
   const unsigned long long neg = __ballot(valid && fac < 0.0);
   if (g == 0) sh.neg[s] = uint32_t((neg >> (threadIdx.x & 56)) & 0xFFull);
 
-  // nodal force contribution of this Gauss point, f_n = fac F S N_XYZ_n, reduce-scattered over
-  // the element's 8 Gauss-point lanes: lane g ends with node g's sum
-  auto fnode = [&](int n, double* out) {
-    double a0, a1, a2;
-    nxyz(n, a0, a1, a2);
-    double t0 = S[0] * a0 + S[3] * a1 + S[5] * a2;
-    double t1 = S[3] * a0 + S[1] * a1 + S[4] * a2;
-    double t2 = S[5] * a0 + S[4] * a1 + S[2] * a2;
-    if (KIN == 1)
-    {
-      const double s0 = F[0] * t0 + F[3] * t1 + F[6] * t2;
-      const double s1 = F[1] * t0 + F[4] * t1 + F[7] * t2;
-      const double s2 = F[2] * t0 + F[5] * t1 + F[8] * t2;
-      t0 = s0;
-      t1 = s1;
-      t2 = s2;
-    }
-    out[0] = fac * t0;
-    out[1] = fac * t1;
-    out[2] = fac * t2;
-  };
-  double w4[4][3], w2[2][3], w1[3];
-  const bool h4 = g & 4, h2 = g & 2, h1 = g & 1;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-  {
-    double lo[3], hi[3];
-    fnode(i, lo);
-    fnode(i + 4, hi);
-#pragma unroll
-    for (int d = 0; d < 3; ++d)
-    {
-      const double mine = h4 ? hi[d] : lo[d];
-      const double other = h4 ? lo[d] : hi[d];
-      w4[i][d] = mine + __shfl_xor(other, 4);
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int d = 0; d < 3; ++d)
-    {
-      const double mine = h2 ? w4[i + 2][d] : w4[i][d];
-      const double other = h2 ? w4[i][d] : w4[i + 2][d];
-      w2[i][d] = mine + __shfl_xor(other, 2);
-    }
-#pragma unroll
-  for (int d = 0; d < 3; ++d)
-  {
-    const double mine = h1 ? w2[1][d] : w2[0][d];
-    const double other = h1 ? w2[0][d] : w2[1][d];
-    w1[d] = mine + __shfl_xor(other, 1);
-  }
-#pragma unroll
-  for (int d = 0; d < 3; ++d) sh.fe[s][g][d] = valid ? w1[d] : 0.0;
 }
 
 // One element visit: accumulate the block (a, b) of element slot `slot` over its Gauss points.
@@ -258,13 +241,7 @@ template <int KIN, bool NEG>
 __device__ inline void sweep_visit(const SweepShared<KIN>& sh, int slot, int a, int b,
     uint32_t nm, double* acc)
 {
-  const double* pa = &sh.nx[0][0][slot][a];
-  const double* pb = &sh.nx[0][0][slot][b];
-#pragma unroll
-  for (int g = 0; g < 8; ++g)
-  {
-    double a0 = pa[g * SG], a1 = pa[g * SG + SD], a2 = pa[g * SG + 2 * SD];
-    const double b0 = pb[g * SG], b1 = pb[g * SG + SD], b2 = pb[g * SG + 2 * SD];
+  auto gp_body = [&](int g, double a0, double a1, double a2, double b0, double b1, double b2) {
     if (NEG && ((nm >> g) & 1u))
     {
       a0 = -a0;
@@ -279,7 +256,7 @@ __device__ inline void sweep_visit(const SweepShared<KIN>& sh, int slot, int a, 
     }
     else
     {
-      const double* P = sh.gp[KIN ? g : 0][KIN ? slot : 0];
+      const double* P = sh.gp[g][slot];
       const double F0 = P[0], F1 = P[1], F2 = P[2], F3 = P[3], F4 = P[4], F5 = P[5], F6 = P[6],
                    F7 = P[7], F8 = P[8];
       const double fa0 = F0 * a0 + F3 * a1 + F6 * a2;
@@ -304,6 +281,18 @@ __device__ inline void sweep_visit(const SweepShared<KIN>& sh, int slot, int a, 
       const double sb2 = S5 * b0 + S4 * b1 + S2 * b2;
       acc[15] += a0 * sb0 + a1 * sb1 + a2 * sb2;
     }
+  };
+#pragma unroll
+  for (int p = 0; p < 4; ++p)
+  {
+    const double2 ax = *reinterpret_cast<const double2*>(&sh.nx[nx2i(0, p, slot, a)]);
+    const double2 ay = *reinterpret_cast<const double2*>(&sh.nx[nx2i(1, p, slot, a)]);
+    const double2 az = *reinterpret_cast<const double2*>(&sh.nx[nx2i(2, p, slot, a)]);
+    const double2 bx = *reinterpret_cast<const double2*>(&sh.nx[nx2i(0, p, slot, b)]);
+    const double2 by = *reinterpret_cast<const double2*>(&sh.nx[nx2i(1, p, slot, b)]);
+    const double2 bz = *reinterpret_cast<const double2*>(&sh.nx[nx2i(2, p, slot, b)]);
+    gp_body(2 * p, ax.x, ay.x, az.x, bx.x, by.x, bz.x);
+    gp_body(2 * p + 1, ax.y, ay.y, az.y, bx.y, by.y, bz.y);
   }
 }
 
@@ -319,7 +308,7 @@ __device__ inline void sweep_visit(const SweepShared<KIN>& sh, int slot, int a, 
   }
 
 template <int KIN, bool WANT_K, bool OVERWRITE>
-__global__ __launch_bounds__(256, 2) void sweep_h8_kernel(SweepArgs A)
+__global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
 {
   __shared__ SweepShared<KIN> sh;
   constexpr int NACC = KIN ? 16 : 9;
@@ -410,10 +399,6 @@ __global__ __launch_bounds__(256, 2) void sweep_h8_kernel(SweepArgs A)
   uint32_t rec_nxt[2];
   load_rec(kz0 + 1, rec_nxt);
   int e_cur = load_elem(kz0 - 1);
-  double hold0[9], hold1[9], fhold[3];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) hold0[i] = hold1[i] = 0.0;
-  fhold[0] = fhold[1] = fhold[2] = 0.0;
   __syncthreads();
 
   for (int L = kz0 - 1; L < kz1; ++L)
@@ -434,28 +419,15 @@ __global__ __launch_bounds__(256, 2) void sweep_h8_kernel(SweepArgs A)
     const bool wl = L >= kz0, wl1 = L + 1 < kz1;
     const uint32_t* recL = sh.prec[ring(L)];
     const uint32_t* recL1 = sh.prec[ring(L + 1)];
-    // the self block's lower part lives in lane k1; lane k0 completes it
-#pragma unroll
-    for (int i = 0; i < 9; ++i)
-    {
-      const double t = __shfl_xor(hold0[i], 1);
-      if (k == 0) hold0[i] = t;
-    }
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-    {
-      const double t = __shfl_xor(fhold[i], 1);
-      if (k == 0) fhold[i] = t;
-    }
     if (WANT_K)
     {
       double acc[NACC];
 #pragma unroll
       for (int i = 0; i < NACC; ++i) acc[i] = 0.0;
-#pragma unroll
+#pragma unroll 1
       for (int v = 0; v < 4; ++v)
       {
-        const uint32_t w = vis[v];
+        const uint32_t w = v == 0 ? vis[0] : v == 1 ? vis[1] : v == 2 ? vis[2] : vis[3];
         const int q = w & 3, a = (w >> 2) & 7, b = (w >> 5) & 7, act = (w >> 8) & 7,
                   t = (w >> 12) & 31;
         const int slot = (cx + (q & 1)) + EXN * (cy + (q >> 1));
@@ -490,27 +462,19 @@ __global__ __launch_bounds__(256, 2) void sweep_h8_kernel(SweepArgs A)
         }
 #pragma unroll
         for (int i = 0; i < NACC; ++i) acc[i] = 0.0;
-        if (act == kVisitActHold0)
+        // in-plane blocks: the lower-layer part waits in LDS for the next layer
+        if (act == kVisitActHold0 || act == kVisitActHold1)
         {
+          double* h = sh.hold[c][t == 13 && ((L + 1) & 1) ? 9 : t - 9];
 #pragma unroll
-          for (int i = 0; i < 9; ++i) hold0[i] = Kb[i];
+          for (int i = 0; i < 9; ++i) h[i] = Kb[i];
           continue;
         }
-        if (act == kVisitActHold1)
+        if (act == kVisitActWriteLH0 || act == kVisitActWriteLH1)
         {
+          const double* h = sh.hold[c][t == 13 && (L & 1) ? 9 : t - 9];
 #pragma unroll
-          for (int i = 0; i < 9; ++i) hold1[i] = Kb[i];
-          continue;
-        }
-        if (act == kVisitActWriteLH0)
-        {
-#pragma unroll
-          for (int i = 0; i < 9; ++i) Kb[i] = hold0[i] + Kb[i];
-        }
-        else if (act == kVisitActWriteLH1)
-        {
-#pragma unroll
-          for (int i = 0; i < 9; ++i) Kb[i] = hold1[i] + Kb[i];
+          for (int i = 0; i < 9; ++i) Kb[i] = h[i] + Kb[i];
         }
         const bool to_l1 = act == kVisitActWriteL1;
         if (!(to_l1 ? wl1 : wl)) continue;
@@ -534,26 +498,55 @@ __global__ __launch_bounds__(256, 2) void sweep_h8_kernel(SweepArgs A)
           }
       }
     }
-    // nodal forces: lane k0 completes plane L's rows, lane k1 starts plane L+1's
-    if (k < 2)
+    // nodal forces f_A = sum_e sum_g fac F S N_XYZ_A: lane k takes Gauss points 4h..4h+3
+    // (h = k & 1) of quadrant q = (k >> 1) & 3 for the row node on side k >> 3 (0: plane L, the
+    // elements' bottom node; 1: plane L+1, their top node); the 8 lanes of a side then sum by a
+    // butterfly (every lane ends with the same bits).  Lane 8 keeps plane L+1's part for the next
+    // layer, lane 0 completes and writes plane L's rows.
     {
-      double fs[3] = {0.0, 0.0, 0.0};
+      const int fside = k >> 3, fq = (k >> 1) & 3, fh = k & 1;
+      const int fqx = fq & 1, fqy = fq >> 1;
+      const int fslot = (cx + fqx) + EXN * (cy + fqy);
+      const int fn = node_at(1 - fqx, 1 - fqy, fside);
+      double f[3] = {0.0, 0.0, 0.0};
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+      for (int gg = 0; gg < 4; ++gg)
       {
-        const int qx = q & 1, qy = q >> 1;
-        const int slot = (cx + qx) + EXN * (cy + qy);
-        // row node at local (1-qx, 1-qy, k): 4C order index
-        const int n = 4 * k + ((1 - qy) ? (1 - qx ? 2 : 3) : (1 - qx ? 1 : 0));
-#pragma unroll
-        for (int d = 0; d < 3; ++d) fs[d] += sh.fe[slot][n][d];
+        const int gq = 4 * fh + gg;
+        const double a0 = sh.nx[nx2i(0, gq >> 1, fslot, fn) + (gq & 1)],
+                     a1 = sh.nx[nx2i(1, gq >> 1, fslot, fn) + (gq & 1)],
+                     a2 = sh.nx[nx2i(2, gq >> 1, fslot, fn) + (gq & 1)];
+        const double* P = sh.gp[gq][fslot];
+        if (KIN == 0)
+        {
+          f[0] += P[0] * a0 + P[3] * a1 + P[5] * a2;
+          f[1] += P[3] * a0 + P[1] * a1 + P[4] * a2;
+          f[2] += P[5] * a0 + P[4] * a1 + P[2] * a2;
+        }
+        else
+        {
+          const double t0 = P[9] * a0 + P[12] * a1 + P[14] * a2;
+          const double t1 = P[12] * a0 + P[10] * a1 + P[13] * a2;
+          const double t2 = P[14] * a0 + P[13] * a1 + P[11] * a2;
+          const double c = P[15];
+          f[0] += c * (P[0] * t0 + P[3] * t1 + P[6] * t2);
+          f[1] += c * (P[1] * t0 + P[4] * t1 + P[7] * t2);
+          f[2] += c * (P[2] * t0 + P[5] * t1 + P[8] * t2);
+        }
       }
-      if (k == 1)
+#pragma unroll
+      for (int d = 0; d < 3; ++d)
+      {
+        f[d] += dpp_f64<kDppXor1>(f[d]);
+        f[d] += dpp_f64<kDppXor2>(f[d]);
+        f[d] += dpp_f64<kDppHalfMirror>(f[d]);
+      }
+      if (k == 8)
       {
 #pragma unroll
-        for (int d = 0; d < 3; ++d) fhold[d] = fs[d];
+        for (int d = 0; d < 3; ++d) sh.fhold[(L + 1) & 1][c][d] = f[d];
       }
-      else if (wl)
+      else if (k == 0 && wl)
       {
         const int32_t row0 = int32_t(recL[PR_ROW0 + c]);
         if (row0 >= 0)
@@ -562,9 +555,9 @@ __global__ __launch_bounds__(256, 2) void sweep_h8_kernel(SweepArgs A)
           for (int d = 0; d < 3; ++d)
           {
             if (OVERWRITE)
-              A.fint[row0 + d] = fhold[d] + fs[d];
+              A.fint[row0 + d] = sh.fhold[L & 1][c][d] + f[d];
             else
-              A.fint[row0 + d] += fhold[d] + fs[d];
+              A.fint[row0 + d] += sh.fhold[L & 1][c][d] + f[d];
           }
         }
       }
