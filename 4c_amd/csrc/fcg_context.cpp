@@ -638,7 +638,7 @@ int fcg_evaluate_device(fcg_ctx* ctx, int action, int mode, const double* d_u_co
     (void)hipEventElapsedTime(&a, T.ev[0], T.ev[1]);
     (void)hipEventElapsedTime(&b, T.ev[1], T.ev[2]);
     T.ms_element = a;
-    T.ms_assemble = b;
+    T.ms_assemble = m.path == FCG_PATH_STRUCTURED ? 0.0 : b;  // one fused kernel
   }
   if (errv[0] != 0)
   {

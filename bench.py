@@ -221,7 +221,9 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "element_kernel + assemble_kernel (one evaluate)",
+            "kernel": ("sweep_h8_kernel (structured row-block sweep, one evaluate)"
+                       if ev.info.path == fcg.PATH_STRUCTURED
+                       else "element_kernel + assemble_kernel (one evaluate)"),
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

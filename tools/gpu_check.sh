@@ -18,4 +18,9 @@ export TMPDIR=/tmp
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline > "$GRAFT_REPO_ROOT/gpurun_out/bench_prof_$TAG.json" 2> "$GRAFT_REPO_ROOT/gpurun_out/bench_prof_$TAG.err"
 rc=$?
 echo "rocprof rc=$rc"
+if [ $rc -ne 0 ]; then exit $rc; fi
+# HBM traffic of the evaluate kernel (separate counter passes), for bench.py roofline.traffic
+bash "$GRAFT_REPO_ROOT/tools/pmc.sh" "pmc_$TAG" --n 100 --reps 3
+rc=$?
+echo "pmc rc=$rc"
 exit $rc
