@@ -82,7 +82,6 @@ struct SweepShared {
   double node[2][NNODE][6];           // X | u of the 6 x 6 node columns, by plane parity
   uint32_t prec[3][PLANE_REC_WORDS];  // plane records, ring by plane mod 3
   double dN[8][8][3];
-  double dNn[8][8][3];
   double w8[8];
   uint32_t neg[NSLOT];  // bit g set: fac < 0 at Gauss point g
   // lower-layer parts of the in-plane blocks (dz = 0) of node plane L+1: [column][slot][3x3],
@@ -120,9 +119,9 @@ __device__ inline void sweep_stage_a(SweepShared<KIN>& sh, const SweepArgs& A, i
 #pragma unroll
   for (int n = 0; n < 8; ++n)
     nd[n] = sh.node[(L + node_oz(n)) & 1][(sy + node_oy(n)) * NXN + sx + node_ox(n)];
-  double J[9], Jn[9];
+  double J[9];
 #pragma unroll
-  for (int q = 0; q < 9; ++q) J[q] = Jn[q] = 0.0;
+  for (int q = 0; q < 9; ++q) J[q] = 0.0;
 #pragma unroll
   for (int n = 0; n < 8; ++n)
   {
@@ -131,23 +130,43 @@ __device__ inline void sweep_stage_a(SweepShared<KIN>& sh, const SweepArgs& A, i
     J[0] += d0 * x0; J[1] += d1 * x0; J[2] += d2 * x0;
     J[3] += d0 * x1; J[4] += d1 * x1; J[5] += d2 * x1;
     J[6] += d0 * x2; J[7] += d1 * x2; J[8] += d2 * x2;
-    const double n0 = sh.dNn[g][n][0], n1 = sh.dNn[g][n][1], n2 = sh.dNn[g][n][2];
-    Jn[0] += n0 * x0; Jn[1] += n1 * x0; Jn[2] += n2 * x0;
-    Jn[3] += n0 * x1; Jn[4] += n1 * x1; Jn[5] += n2 * x1;
-    Jn[6] += n0 * x2; Jn[7] += n1 * x2; Jn[8] += n2 * x2;
   }
   int bad = 0;
-  // det J at node g only (same expansion as invert3x3's determinant)
-  const double detn = Jn[0] * (Jn[4] * Jn[8] - Jn[5] * Jn[7]) + Jn[3] * (Jn[2] * Jn[7] - Jn[1] * Jn[8]) +
-                      Jn[6] * (Jn[1] * Jn[5] - Jn[2] * Jn[4]);
-  if (detn == 0.0) bad = 2;
-  else if (!(detn > 0)) bad = 1;
+  // det J at node g (calc_lib.hpp:475-496): at a hex8 corner the shape derivatives are
+  // +-1/2 on the node and its neighbour along each parametric direction, so J's columns are
+  // half the three edge vectors through the node and det J = det(edges) / 8 (same sign).
+  {
+    const int ox = node_ox(g), oy = node_oy(g), oz = node_oz(g);
+    const double* zl = sh.node[L & 1][0];
+    const double* zh = sh.node[(L + 1) & 1][0];
+    const double* pz = oz ? zh : zl;
+    const int cxy = (sy + oy) * NXN + sx + ox;
+    const double* o = pz + 6 * cxy;
+    const double* ex_ = pz + 6 * (cxy + (ox ? -1 : 1));
+    const double* ey_ = pz + 6 * (cxy + (oy ? -NXN : NXN));
+    const double* ez_ = (oz ? zl : zh) + 6 * cxy;
+    // edge vectors oriented along +xi, +eta, +zeta
+    const double sgx = ox ? 1.0 : -1.0, sgy = oy ? 1.0 : -1.0, sgz = oz ? 1.0 : -1.0;
+    const double a0 = sgx * (o[0] - ex_[0]), a1 = sgx * (o[1] - ex_[1]), a2 = sgx * (o[2] - ex_[2]);
+    const double b0 = sgy * (o[0] - ey_[0]), b1 = sgy * (o[1] - ey_[1]), b2 = sgy * (o[2] - ey_[2]);
+    const double c0 = sgz * (o[0] - ez_[0]), c1 = sgz * (o[1] - ez_[1]), c2 = sgz * (o[2] - ez_[2]);
+    const double detn = a0 * (b1 * c2 - b2 * c1) + b0 * (c1 * a2 - c2 * a1) + c0 * (a1 * b2 - a2 * b1);
+    if (detn == 0.0) bad = 2;
+    else if (!(detn > 0)) bad = 1;
+  }
   const double det = h8_invert3x3(J);
   if (det == 0.0) bad = 2;
   const double fac = det * sh.w8[g];
   // missing element (outside the column set): all its LDS data become exact zeros
   const double sq = valid ? sqrt(fabs(fac)) : 0.0;
   const double cf = fac < 0.0 ? -sq : sq;  // fac / sqrt|fac|
+  if (KIN == 0)
+  {
+    // linear: scale J^-1 once; N_XYZ below is then sqrt|fac| N_XYZ, the strain sqrt|fac| E
+#pragma unroll
+    for (int q = 0; q < 9; ++q) J[q] *= sq;
+  }
+  const double ns = KIN == 0 ? 1.0 : sq;  // remaining scale of the stored N_XYZ
   // N_XYZ of node n (J now holds J^-1, column-major)
   auto nxyz = [&](int n, double& n0, double& n1, double& n2) {
     const double d0 = sh.dN[g][n][0], d1 = sh.dN[g][n][1], d2 = sh.dN[g][n][2];
@@ -162,9 +181,9 @@ __device__ inline void sweep_stage_a(SweepShared<KIN>& sh, const SweepArgs& A, i
   {
     double n0, n1, n2;
     nxyz(n, n0, n1, n2);
-    sh.nx[nx2i(0, g >> 1, s, n) + (g & 1)] = sq * n0;
-    sh.nx[nx2i(1, g >> 1, s, n) + (g & 1)] = sq * n1;
-    sh.nx[nx2i(2, g >> 1, s, n) + (g & 1)] = sq * n2;
+    sh.nx[nx2i(0, g >> 1, s, n) + (g & 1)] = KIN == 0 ? n0 : ns * n0;
+    sh.nx[nx2i(1, g >> 1, s, n) + (g & 1)] = KIN == 0 ? n1 : ns * n1;
+    sh.nx[nx2i(2, g >> 1, s, n) + (g & 1)] = KIN == 0 ? n2 : ns * n2;
     const double u0 = nd[n][3], u1 = nd[n][4], u2 = nd[n][5];
     if (KIN == 0)
     {
@@ -222,8 +241,9 @@ __device__ inline void sweep_stage_a(SweepShared<KIN>& sh, const SweepArgs& A, i
   }
   else
   {
+    // S was computed from sqrt|fac| E: c S = sign(fac) S(sqrt|fac| E)
 #pragma unroll
-    for (int q = 0; q < 6; ++q) P[q] = cf * S[q];
+    for (int q = 0; q < 6; ++q) P[q] = fac < 0.0 ? -S[q] : S[q];
   }
   if (valid && bad)
   {
@@ -328,7 +348,6 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
   for (int v = tid; v < 192; v += 256)
   {
     (&sh.dN[0][0][0])[v] = A.tables[v];
-    (&sh.dNn[0][0][0])[v] = A.tables[192 + v];
   }
   if (tid < 8) sh.w8[tid] = A.tables[384 + tid];
 
