@@ -286,7 +286,7 @@ void free_mesh(fcg::DeviceMesh& m)
   void* ptrs[] = {m.ele_nodes, m.ele_gid, m.node_x, m.node_dof_col, m.inc_of, m.inc_ptr,
       m.rownode_row0, m.inc_pos, m.rowptr, m.scratch, m.err, m.elem_at, m.lat_x, m.lat_dof,
       m.plane_rec,
-      m.tables, m.stamps};
+      m.tables, m.stamps, m.col_lid, m.diag_pos, m.pcg_work};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   m = fcg::DeviceMesh{};
@@ -524,6 +524,28 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
   chk(upload(&m.node_dof_col, d->node_dof_col, d->n_node, bytes));
   chk(upload(&m.rownode_row0, row0.data(), nrn, bytes));
   chk(upload(&m.rowptr, d->rowptr, d->n_rows + 1, bytes));
+  // operator support: column LIDs, diagonal positions (the Dirichlet rows and the Jacobi
+  // preconditioner need them) and whether the matrix column map is the row map (single rank)
+  {
+    std::vector<int64_t> diag(d->n_rows, -1);
+    bool square = d->n_rows == d->n_cols;
+    for (size_t r = 0; r < rownodes.size(); ++r)
+    {
+      const int32_t nd = rownodes[r];
+      if (kcol[nd] != row0[r]) square = false;
+      for (int dd = 0; dd < 3; ++dd)
+      {
+        const int64_t row = row0[r] + dd;
+        const int32_t* b = d->col_lid + d->rowptr[row];
+        const int32_t* e = d->col_lid + d->rowptr[row + 1];
+        const int32_t* it = std::lower_bound(b, e, kcol[nd] + dd);
+        if (it != e && *it == kcol[nd] + dd) diag[row] = d->rowptr[row] + (it - b);
+      }
+    }
+    m.square_local = square;
+    chk(upload(&m.col_lid, d->col_lid, m.nnz, bytes));
+    chk(upload(&m.diag_pos, diag.data(), d->n_rows, bytes));
+  }
   chk(upload<int32_t>(&m.err, nullptr, 2, bytes));
   if (structured)
   {

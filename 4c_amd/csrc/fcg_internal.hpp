@@ -45,6 +45,13 @@ struct DeviceMesh {
   uint32_t* plane_rec = nullptr;    // [tiles_y][tiles_x][NK][PLANE_REC_WORDS] row bookkeeping
   double* tables = nullptr;         // dN at GPs [192], dN at nodes [192], weights [8]
   unsigned long long* stamps = nullptr;  // diagnostic phase timers (FCG_STAMPS=1), else NULL
+
+  // operator / solver support (fcg_solver.hip)
+  int32_t* col_lid = nullptr;       // [nnz] CSR column LIDs (matrix column map)
+  int64_t* diag_pos = nullptr;      // [n_rows] position of the diagonal entry in K values, -1 = none
+  bool square_local = false;        // matrix column map == row map (single rank)
+  double* pcg_work = nullptr;       // PCG vectors and partial sums (allocated on first solve)
+  int64_t pcg_n = 0;
 };
 
 // One record per (tile, node plane): row0[16] | rowlen[16] | rbase[16] (int64) | npos[16][27]

@@ -102,4 +102,29 @@ inline void shape_deriv(int celltype, const double* xi, double* dN)
   }
 }
 
+// N[node] at xi (shape_function_3d, 4C_fem_general_utils_fem_shapefunctions.hpp:53-72,190-229).
+inline void shape_values(int celltype, const double* xi, double* N)
+{
+  if (celltype == kHex8)
+  {
+    for (int n = 0; n < 8; ++n)
+    {
+      double p[3];
+      for (int d = 0; d < 3; ++d) p[d] = 1.0 + (kHex27NodePos[n][d] == 0 ? -1.0 : 1.0) * xi[d];
+      N[n] = 0.125 * p[0] * p[1] * p[2];
+    }
+    return;
+  }
+  double L[3][3];
+  for (int d = 0; d < 3; ++d)
+  {
+    const double r = xi[d];
+    L[d][0] = 0.5 * r * (r - 1.0);
+    L[d][1] = 1.0 - r * r;
+    L[d][2] = 0.5 * r * (r + 1.0);
+  }
+  for (int n = 0; n < 27; ++n)
+    N[n] = L[0][kHex27NodePos[n][0]] * L[1][kHex27NodePos[n][1]] * L[2][kHex27NodePos[n][2]];
+}
+
 }  // namespace fcg

@@ -1,0 +1,393 @@
+// fcg_solver.hip -- what the Newton step around the assembly needs on the device (SURVEY §8f
+// rows 1-2): Dirichlet rows applied to the assembled tangent and residual, the CSR operator, and
+// a Jacobi-preconditioned conjugate-gradient solve, all on the HBM-resident K of the context.
+//
+//  * fcg_dirichlet_apply: Solid::Dbc::apply_dirichlet_to_local_system
+//    (4C_structure_new_dbc.cpp:221-262): residual entries of the DBC DOFs are set to zero
+//    (LinAlg::apply_dirichlet_to_system with zeros) after they were extracted as reaction forces
+//    (extract_freact), and the matrix rows become unit rows -- SparseMatrix::apply_dirichlet with
+//    diagonalblock = true (4C_linalg_sparsematrix.cpp:978-1097; the in-place branch, which keeps
+//    the graph, is what runs here; the explicit branch yields the same values).
+//  * fcg_spmv: y_row = K x_col (Epetra_CrsMatrix::Multiply on the local rows).
+//  * fcg_pcg_solve: K x = b for a single-rank system (column map = row map), x_0 = 0.  With unit
+//    DBC rows and zero DBC right-hand sides every iterate keeps x_D = 0, so CG on the row-modified
+//    matrix is CG on K_FF.  All reductions are block partials summed in a fixed order: the solve
+//    is bitwise reproducible.  (4C hands this system to Belos/MueLu through NOX,
+//    4C_solver_nonlin_nox_linearsystem.cpp:275-353; the preconditioner here is Jacobi.)
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "fcg_internal.hpp"
+
+namespace fcg {
+
+namespace {
+
+constexpr int kBlock = 256;
+
+// deterministic block sum (wave butterfly, then the waves in order); result valid in thread 0
+__device__ inline double block_sum(double v, double* sbuf)
+{
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) sbuf[w] = v;
+  __syncthreads();
+  double t = 0.0;
+  if (threadIdx.x == 0)
+    for (int i = 0; i < int(blockDim.x >> 6); ++i) t += sbuf[i];
+  __syncthreads();
+  return t;
+}
+
+// y = K x; optionally partial[blockIdx] = sum over the block's rows of d[row] * y[row]
+template <int LPR>
+__global__ __launch_bounds__(kBlock) void spmv_kernel(const int64_t* __restrict__ rowptr,
+    const int32_t* __restrict__ col, const double* __restrict__ vals, const double* __restrict__ x,
+    double* __restrict__ y, int64_t n_rows, const double* __restrict__ dotw, double* partial)
+{
+  __shared__ double sbuf[kBlock / 64];
+  const int64_t row = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / LPR;
+  const int lane = threadIdx.x % LPR;
+  double acc = 0.0;
+  if (row < n_rows)
+  {
+    const int64_t s = rowptr[row], e = rowptr[row + 1];
+    for (int64_t j = s + lane; j < e; j += LPR) acc += vals[j] * x[col[j]];
+  }
+#pragma unroll
+  for (int o = LPR / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, LPR);
+  double mine = 0.0;
+  if (row < n_rows && lane == 0)
+  {
+    y[row] = acc;
+    if (dotw) mine = dotw[row] * acc;
+  }
+  if (partial)
+  {
+    const double t = block_sum(mine, sbuf);
+    if (threadIdx.x == 0) partial[blockIdx.x] = t;
+  }
+}
+
+// Single-block reduction of n partials (fixed order) into sc[slot]; then the scalar recurrences
+// of the PCG step (op: 0 = store only, 1 = alpha = sc[RZ] / sum, 2 = beta = sum / sc[RZ], RZ = sum)
+enum { SC_RZ = 0, SC_PQ = 1, SC_RR = 2, SC_RZN = 3, SC_RR0 = 4, SC_BETA = 5, SC_ALPHA = 6, SC_N = 8 };
+__global__ __launch_bounds__(kBlock) void reduce_kernel(const double* __restrict__ partial,
+    int64_t n, double* sc, int slot, int op, const double* __restrict__ partial2, int slot2)
+{
+  __shared__ double sbuf[kBlock / 64];
+  double a = 0.0, b = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += kBlock)
+  {
+    a += partial[i];
+    if (partial2) b += partial2[i];
+  }
+  const double ta = block_sum(a, sbuf);
+  const double tb = partial2 ? block_sum(b, sbuf) : 0.0;
+  if (threadIdx.x != 0) return;
+  sc[slot] = ta;
+  if (partial2) sc[slot2] = tb;
+  if (op == 1) sc[SC_ALPHA] = sc[SC_PQ] != 0.0 ? sc[SC_RZ] / sc[SC_PQ] : 0.0;
+  if (op == 2)
+  {
+    sc[SC_BETA] = sc[SC_RZ] != 0.0 ? sc[SC_RZN] / sc[SC_RZ] : 0.0;
+    sc[SC_RZ] = sc[SC_RZN];
+  }
+  if (op == 3)
+  {
+    sc[SC_RZ] = ta;  // init: rz and rr (= rr0)
+    sc[SC_RR0] = tb;
+  }
+}
+
+// init: x = 0, r = b, z = dinv r, p = z; partials r.z, r.r
+__global__ __launch_bounds__(kBlock) void pcg_init_kernel(const double* __restrict__ b,
+    const double* __restrict__ dinv, double* x, double* r, double* z, double* p, int64_t n,
+    double* part_rz, double* part_rr)
+{
+  __shared__ double sbuf[kBlock / 64];
+  const int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  double rz = 0.0, rr = 0.0;
+  if (i < n)
+  {
+    const double ri = b[i], zi = dinv[i] * ri;
+    x[i] = 0.0;
+    r[i] = ri;
+    z[i] = zi;
+    p[i] = zi;
+    rz = ri * zi;
+    rr = ri * ri;
+  }
+  const double a = block_sum(rz, sbuf);
+  const double c = block_sum(rr, sbuf);
+  if (threadIdx.x == 0)
+  {
+    part_rz[blockIdx.x] = a;
+    part_rr[blockIdx.x] = c;
+  }
+}
+
+// x += alpha p, r -= alpha q, z = dinv r; partials r.z, r.r
+__global__ __launch_bounds__(kBlock) void pcg_update_kernel(const double* __restrict__ p,
+    const double* __restrict__ q, const double* __restrict__ dinv, double* x, double* r, double* z,
+    int64_t n, const double* sc, double* part_rz, double* part_rr)
+{
+  __shared__ double sbuf[kBlock / 64];
+  const double alpha = sc[SC_ALPHA];
+  const int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  double rz = 0.0, rr = 0.0;
+  if (i < n)
+  {
+    x[i] += alpha * p[i];
+    const double ri = r[i] - alpha * q[i];
+    const double zi = dinv[i] * ri;
+    r[i] = ri;
+    z[i] = zi;
+    rz = ri * zi;
+    rr = ri * ri;
+  }
+  const double a = block_sum(rz, sbuf);
+  const double c = block_sum(rr, sbuf);
+  if (threadIdx.x == 0)
+  {
+    part_rz[blockIdx.x] = a;
+    part_rr[blockIdx.x] = c;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void pcg_dir_kernel(const double* __restrict__ z, double* p,
+    int64_t n, const double* sc)
+{
+  const double beta = sc[SC_BETA];
+  const int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (i < n) p[i] = z[i] + beta * p[i];
+}
+
+__global__ __launch_bounds__(kBlock) void jacobi_kernel(const int64_t* __restrict__ diag_pos,
+    const double* __restrict__ K, double* dinv, int64_t n, int32_t* bad)
+{
+  const int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const int64_t dp = diag_pos[i];
+  const double d = dp >= 0 ? K[dp] : 0.0;
+  if (d == 0.0) atomicMax(bad, 1);
+  dinv[i] = d != 0.0 ? 1.0 / d : 0.0;
+}
+
+// Dirichlet rows: one wavefront per DBC row
+__global__ __launch_bounds__(kBlock) void dirichlet_kernel(const int64_t* __restrict__ rowptr,
+    const int64_t* __restrict__ diag_pos, const int32_t* __restrict__ rows, int64_t n_dbc,
+    int64_t n_rows, double* K, double* rhs, double* freact, int32_t* bad)
+{
+  const int64_t k = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (k >= n_dbc) return;
+  const int32_t row = rows[k];
+  if (row < 0 || row >= n_rows)
+  {
+    if (lane == 0) atomicMax(bad, 2);
+    return;
+  }
+  const int64_t dp = diag_pos[row];
+  if (dp < 0)
+  {
+    if (lane == 0) atomicMax(bad, 1);
+    return;
+  }
+  if (K)
+    for (int64_t j = rowptr[row] + lane; j < rowptr[row + 1]; j += 64) K[j] = j == dp ? 1.0 : 0.0;
+  if (lane == 0 && rhs)
+  {
+    if (freact) freact[row] = rhs[row];
+    rhs[row] = 0.0;
+  }
+}
+
+inline unsigned blocks_for(int64_t n, int per_block) { return unsigned((n + per_block - 1) / per_block); }
+
+hipError_t launch_spmv(const DeviceMesh& m, const double* K, const double* x, double* y,
+    const double* dotw, double* partial, hipStream_t s)
+{
+  if (m.n_rows == 0) return hipSuccess;
+  if (m.npe == 27)
+    hipLaunchKernelGGL((spmv_kernel<64>), dim3(blocks_for(m.n_rows * 64, kBlock)), dim3(kBlock), 0,
+        s, m.rowptr, m.col_lid, K, x, y, m.n_rows, dotw, partial);
+  else
+    hipLaunchKernelGGL((spmv_kernel<16>), dim3(blocks_for(m.n_rows * 16, kBlock)), dim3(kBlock), 0,
+        s, m.rowptr, m.col_lid, K, x, y, m.n_rows, dotw, partial);
+  return hipGetLastError();
+}
+
+int64_t spmv_blocks(const DeviceMesh& m)
+{
+  return blocks_for(m.n_rows * (m.npe == 27 ? 64 : 16), kBlock);
+}
+
+}  // namespace
+
+}  // namespace fcg
+
+extern "C" {
+
+int fcg_spmv(fcg_ctx* ctx, const double* d_K_vals, const double* d_x_col, double* d_y_row,
+    void* stream)
+{
+  if (!ctx || (ctx->mesh.n_rows > 0 && (!d_K_vals || !d_x_col || !d_y_row))) return FCG_ERR_ARG;
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  hipError_t he = fcg::launch_spmv(ctx->mesh, d_K_vals, d_x_col, d_y_row, nullptr, nullptr, s);
+  if (he == hipSuccess) he = hipStreamSynchronize(s);
+  if (he != hipSuccess)
+  {
+    ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
+    return FCG_ERR_DEVICE;
+  }
+  return FCG_OK;
+}
+
+int fcg_dirichlet_apply(fcg_ctx* ctx, int64_t n_dbc, const int32_t* d_rows, double* d_K_vals,
+    double* d_rhs_row, double* d_freact_row, void* stream)
+{
+  if (!ctx || n_dbc < 0 || (n_dbc > 0 && !d_rows)) return FCG_ERR_ARG;
+  if (n_dbc == 0) return FCG_OK;
+  fcg::DeviceMesh& m = ctx->mesh;
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  const int32_t zero = 0;
+  hipError_t he = hipMemcpyAsync(m.err, &zero, sizeof(zero), hipMemcpyHostToDevice, s);
+  if (he == hipSuccess)
+  {
+    hipLaunchKernelGGL(fcg::dirichlet_kernel, dim3(fcg::blocks_for(n_dbc * 64, fcg::kBlock)),
+        dim3(fcg::kBlock), 0, s, m.rowptr, m.diag_pos, d_rows, n_dbc, m.n_rows, d_K_vals, d_rhs_row,
+        d_freact_row, m.err);
+    he = hipGetLastError();
+  }
+  int32_t bad = 0;
+  if (he == hipSuccess) he = hipMemcpyAsync(&bad, m.err, sizeof(bad), hipMemcpyDeviceToHost, s);
+  if (he == hipSuccess) he = hipStreamSynchronize(s);
+  if (he != hipSuccess)
+  {
+    ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
+    return FCG_ERR_DEVICE;
+  }
+  if (bad)
+  {
+    ctx->last_error = bad == 2 ? "Dirichlet row LID out of range" : "Dirichlet row without a diagonal entry";
+    return FCG_ERR_ARG;
+  }
+  return FCG_OK;
+}
+
+int fcg_pcg_solve(fcg_ctx* ctx, const double* d_K_vals, const double* d_b_row, double* d_x_row,
+    double rtol, int max_iter, int* iterations, double* rel_residual, void* stream)
+{
+  if (!ctx || !(rtol >= 0.0) || max_iter < 0) return FCG_ERR_ARG;
+  fcg::DeviceMesh& m = ctx->mesh;
+  if (!m.square_local)
+  {
+    ctx->last_error = "fcg_pcg_solve needs a single-rank system (matrix column map = row map)";
+    return FCG_ERR_ARG;
+  }
+  const int64_t n = m.n_rows;
+  if (iterations) *iterations = 0;
+  if (rel_residual) *rel_residual = 0.0;
+  if (n == 0) return FCG_OK;
+  if (!d_K_vals || !d_b_row || !d_x_row) return FCG_ERR_ARG;
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  hipError_t he = hipSuccess;
+  const int64_t nb_vec = fcg::blocks_for(n, fcg::kBlock);
+  const int64_t nb_mv = fcg::spmv_blocks(m);
+  const int64_t nb = std::max(nb_vec, nb_mv);
+  if (!m.pcg_work || m.pcg_n != n)
+  {
+    if (m.pcg_work) (void)hipFree(m.pcg_work);
+    m.pcg_work = nullptr;
+    he = hipMalloc(reinterpret_cast<void**>(&m.pcg_work), sizeof(double) * (5 * n + 3 * nb + fcg::SC_N));
+    if (he != hipSuccess)
+    {
+      ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
+      return FCG_ERR_DEVICE;
+    }
+    m.pcg_n = n;
+  }
+  double* r = m.pcg_work;
+  double* z = r + n;
+  double* p = z + n;
+  double* q = p + n;
+  double* dinv = q + n;
+  double* pa = dinv + n;
+  double* pb = pa + nb;
+  double* pc = pb + nb;
+  double* sc = pc + nb;
+  const int32_t zero = 0;
+  he = hipMemcpyAsync(m.err, &zero, sizeof(zero), hipMemcpyHostToDevice, s);
+  if (he == hipSuccess)
+  {
+    hipLaunchKernelGGL(fcg::jacobi_kernel, dim3(nb_vec), dim3(fcg::kBlock), 0, s, m.diag_pos,
+        d_K_vals, dinv, n, m.err);
+    hipLaunchKernelGGL(fcg::pcg_init_kernel, dim3(nb_vec), dim3(fcg::kBlock), 0, s, d_b_row, dinv,
+        d_x_row, r, z, p, n, pa, pb);
+    hipLaunchKernelGGL(fcg::reduce_kernel, dim3(1), dim3(fcg::kBlock), 0, s, pa, nb_vec, sc,
+        int(fcg::SC_RZ), 3, pb, int(fcg::SC_RR));
+    he = hipGetLastError();
+  }
+  double hsc[fcg::SC_N] = {0};
+  int32_t bad = 0;
+  if (he == hipSuccess) he = hipMemcpyAsync(hsc, sc, sizeof(hsc), hipMemcpyDeviceToHost, s);
+  if (he == hipSuccess) he = hipMemcpyAsync(&bad, m.err, sizeof(bad), hipMemcpyDeviceToHost, s);
+  if (he == hipSuccess) he = hipStreamSynchronize(s);
+  if (he != hipSuccess)
+  {
+    ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
+    return FCG_ERR_DEVICE;
+  }
+  if (bad)
+  {
+    ctx->last_error = "zero or missing diagonal entry (Jacobi preconditioner)";
+    return FCG_ERR_SINGULAR;
+  }
+  const double rr0 = hsc[fcg::SC_RR0];
+  if (rr0 == 0.0) return FCG_OK;  // b = 0 -> x = 0
+  const double target = rtol * rtol * rr0;
+  int it = 0;
+  double rr = rr0;
+  const int check_every = 8;
+  while (it < max_iter && rr > target)
+  {
+    const int burst = std::min(check_every, max_iter - it);
+    for (int k = 0; k < burst; ++k)
+    {
+      he = fcg::launch_spmv(m, d_K_vals, p, q, p, pa, s);
+      if (he != hipSuccess) break;
+      hipLaunchKernelGGL(fcg::reduce_kernel, dim3(1), dim3(fcg::kBlock), 0, s, pa, nb_mv, sc,
+          int(fcg::SC_PQ), 1, nullptr, 0);
+      hipLaunchKernelGGL(fcg::pcg_update_kernel, dim3(nb_vec), dim3(fcg::kBlock), 0, s, p, q, dinv,
+          d_x_row, r, z, n, sc, pb, pc);
+      hipLaunchKernelGGL(fcg::reduce_kernel, dim3(1), dim3(fcg::kBlock), 0, s, pb, nb_vec, sc,
+          int(fcg::SC_RZN), 2, pc, int(fcg::SC_RR));
+      hipLaunchKernelGGL(fcg::pcg_dir_kernel, dim3(nb_vec), dim3(fcg::kBlock), 0, s, z, p, n, sc);
+      he = hipGetLastError();
+      if (he != hipSuccess) break;
+    }
+    if (he == hipSuccess) he = hipMemcpyAsync(hsc, sc, sizeof(hsc), hipMemcpyDeviceToHost, s);
+    if (he == hipSuccess) he = hipStreamSynchronize(s);
+    if (he != hipSuccess)
+    {
+      ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
+      return FCG_ERR_DEVICE;
+    }
+    it += burst;
+    rr = hsc[fcg::SC_RR];
+    if (!std::isfinite(rr)) break;
+  }
+  if (iterations) *iterations = it;
+  if (rel_residual) *rel_residual = std::sqrt(rr / rr0);
+  return FCG_OK;
+}
+
+}  // extern "C"

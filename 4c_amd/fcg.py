@@ -58,11 +58,13 @@ class FcgInfo(ctypes.Structure):
 EXPORTS = ["fcg_create", "fcg_destroy", "fcg_last_error", "fcg_evaluate", "fcg_evaluate_device",
            "fcg_device_alloc", "fcg_device_free", "fcg_memcpy_h2d", "fcg_memcpy_d2h",
            "fcg_memset_device", "fcg_set_timing", "fcg_get_timing", "fcg_get_info",
-           "fcg_get_diagnostics",
+           "fcg_get_diagnostics", "fcg_spmv", "fcg_dirichlet_apply", "fcg_pcg_solve",
+           "fcg_neumann_surface", "fcg_neumann_volume",
            "fcg_box_mesh_create", "fcg_box_mesh_destroy", "fcg_box_mesh_desc", "fcg_box_mesh_maps",
            "fcg_box_mesh_counts"]
 
 _lib = None
+FUNCT_FN = ctypes.CFUNCTYPE(ctypes.c_double, ctypes.c_int, _dp, ctypes.c_double, ctypes.c_void_p)
 
 
 class FcgError(RuntimeError):
@@ -96,6 +98,14 @@ def lib():
     L.fcg_get_timing.argtypes = [vp, _dp, _dp]
     L.fcg_get_info.argtypes = [vp, ctypes.POINTER(FcgInfo)]
     L.fcg_get_diagnostics.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
+    L.fcg_spmv.argtypes = [vp, vp, vp, vp, vp]
+    L.fcg_dirichlet_apply.argtypes = [vp, ctypes.c_int64, vp, vp, vp, vp, vp]
+    L.fcg_pcg_solve.argtypes = [vp, vp, vp, vp, ctypes.c_double, ctypes.c_int,
+                                ctypes.POINTER(ctypes.c_int), _dp, vp]
+    neu = [ctypes.c_int, ctypes.c_int64, _i32p, _dp, _i32p, _i32p, _dp, _i32p, FUNCT_FN,
+           ctypes.c_void_p, ctypes.c_double, _dp]
+    L.fcg_neumann_surface.argtypes = neu
+    L.fcg_neumann_volume.argtypes = neu
     L.fcg_box_mesh_create.argtypes = [ctypes.POINTER(FcgBox), ctypes.c_int, ctypes.c_int,
                                       ctypes.POINTER(vp)]
     L.fcg_box_mesh_destroy.argtypes = [vp]
@@ -110,6 +120,108 @@ def lib():
 
 def _np_ptr(a, t):
     return a.ctypes.data_as(t)
+
+
+class Discretization:
+    """Arrays of one rank's discretization as 4C holds them after FillComplete (the fcg_desc
+    contents), for meshes that are not GridGenerator boxes -- e.g. the reference's input files."""
+
+    def __init__(self, celltype, ele_nodes, node_x, node_dof_col, node_dof_row, rowptr, col_lid,
+                 n_cols=None, ele_gid=None):
+        self.celltype = celltype
+        self.npe = 8 if celltype == HEX8 else 27
+        self.ele_nodes = np.ascontiguousarray(ele_nodes, dtype=np.int32).reshape(-1, self.npe)
+        self.node_x = np.ascontiguousarray(node_x, dtype=np.float64).reshape(-1, 3)
+        self.node_dof_col = np.ascontiguousarray(node_dof_col, dtype=np.int32)
+        self.node_dof_row = np.ascontiguousarray(node_dof_row, dtype=np.int32)
+        self.rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)
+        self.col_lid = np.ascontiguousarray(col_lid, dtype=np.int32)
+        self.ele_gid = (np.ascontiguousarray(ele_gid, dtype=np.int32) if ele_gid is not None
+                        else np.arange(len(self.ele_nodes), dtype=np.int32))
+        self.n_ele, self.n_node = len(self.ele_nodes), len(self.node_x)
+        self.n_rows = len(self.rowptr) - 1
+        self.n_cols = int(n_cols) if n_cols is not None else self.n_rows
+        self.nnz = int(self.rowptr[-1])
+
+    @staticmethod
+    def from_elements(celltype, ele_nodes, node_x):
+        """Single-rank discretization: DOF LID = 3 * node + d, CSR graph of the element couplings."""
+        en = np.asarray(ele_nodes, dtype=np.int64)
+        n_node = len(node_x)
+        nbr = [set() for _ in range(n_node)]
+        for el in en:
+            for a in el:
+                nbr[a].update(int(b) for b in el)
+        rows, cols = [0], []
+        for a in range(n_node):
+            c = sorted(nbr[a])
+            cd = [3 * b + d for b in c for d in range(3)]
+            for _ in range(3):
+                cols.extend(cd)
+                rows.append(len(cols))
+        dof = 3 * np.arange(n_node, dtype=np.int32)
+        return Discretization(celltype, en, node_x, dof, dof, np.array(rows), np.array(cols))
+
+    def desc(self, kinematics, youngs, poisson, device=0, path=PATH_AUTO):
+        d = FcgDesc()
+        d.abi_version = ABI_VERSION
+        d.celltype = self.celltype
+        d.kinematics = kinematics
+        d.device = device
+        d.youngs = youngs
+        d.poisson = poisson
+        d.n_ele, d.n_node, d.n_rows, d.n_cols = self.n_ele, self.n_node, self.n_rows, self.n_cols
+        d.ele_nodes = _np_ptr(self.ele_nodes, _i32p)
+        d.ele_gid = _np_ptr(self.ele_gid, _i32p)
+        d.node_x = _np_ptr(self.node_x, _dp)
+        d.node_dof_col = _np_ptr(self.node_dof_col, _i32p)
+        d.node_dof_row = _np_ptr(self.node_dof_row, _i32p)
+        d.node_dof_kcol = None
+        d.rowptr = _np_ptr(self.rowptr, _i64p)
+        d.col_lid = _np_ptr(self.col_lid, _i32p)
+        d.ele_ijk = None
+        d.path = path
+        return d
+
+
+def _neumann(entry, celltype, conn, node_x, node_dof_row, onoff, val, funct, fn, time, fext):
+    """fcg_neumann_surface / fcg_neumann_volume into the numpy vector `fext` (+=)."""
+    conn = np.ascontiguousarray(conn, dtype=np.int32)
+    node_x = np.ascontiguousarray(node_x, dtype=np.float64)
+    node_dof_row = np.ascontiguousarray(node_dof_row, dtype=np.int32)
+    oo = np.ascontiguousarray(onoff, dtype=np.int32)
+    vv = np.ascontiguousarray(val, dtype=np.float64)
+    ff = np.ascontiguousarray(funct if funct is not None else [0, 0, 0], dtype=np.int32)
+    err = []
+
+    def cb(fid, x, t, _user):
+        try:
+            return float(fn(fid, (x[0], x[1], x[2]), t))
+        except Exception as e:  # surfaced after the call
+            err.append(e)
+            return 0.0
+
+    cfn = FUNCT_FN(cb) if fn is not None else FUNCT_FN()
+    n = conn.shape[0]
+    rc = getattr(lib(), entry)(celltype, n, _np_ptr(conn, _i32p), _np_ptr(node_x, _dp),
+                               _np_ptr(node_dof_row, _i32p), _np_ptr(oo, _i32p), _np_ptr(vv, _dp),
+                               _np_ptr(ff, _i32p), cfn, None, float(time), _np_ptr(fext, _dp))
+    if err:
+        raise err[0]
+    if rc != 0:
+        raise FcgError(rc, entry + " failed")
+
+
+def neumann_surface(celltype, face_nodes, node_x, node_dof_row, onoff, val, fext, funct=None,
+                    fn=None, time=1.0):
+    _neumann("fcg_neumann_surface", celltype, face_nodes, node_x, node_dof_row, onoff, val, funct,
+             fn, time, fext)
+
+
+def neumann_volume(celltype, ele_nodes, node_x, node_dof_row, onoff, val, fext, funct=None,
+                   fn=None, time=1.0):
+    _neumann("fcg_neumann_volume", celltype, ele_nodes, node_x, node_dof_row, onoff, val, funct,
+             fn, time, fext)
 
 
 def _tensor_ptr(t):
@@ -219,7 +331,7 @@ class Evaluator:
     def __init__(self, desc_or_mesh, kinematics=LINEAR, youngs=210.0, poisson=0.3, device=0,
                  path=PATH_AUTO):
         L = lib()
-        if isinstance(desc_or_mesh, BoxMesh):
+        if isinstance(desc_or_mesh, (BoxMesh, Discretization)):
             self._mesh = desc_or_mesh
             desc = desc_or_mesh.desc(kinematics, youngs, poisson, device, path)
         else:
@@ -267,6 +379,33 @@ class Evaluator:
                                        ctypes.byref(bad))
         if rc != 0:
             self._raise(rc, bad.value)
+
+    def _stream(self, stream):
+        return ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
+
+    def spmv(self, K_vals, x_col, y_row, stream=None):
+        rc = lib().fcg_spmv(self._h, _tensor_ptr(K_vals), _tensor_ptr(x_col), _tensor_ptr(y_row),
+                            self._stream(stream))
+        if rc != 0:
+            self._raise(rc, -1)
+
+    def dirichlet_apply(self, rows, K_vals=None, rhs=None, freact=None, stream=None):
+        """rows: int32 device tensor of DBC row LIDs."""
+        rc = lib().fcg_dirichlet_apply(self._h, int(rows.numel()), _tensor_ptr(rows),
+                                       _tensor_ptr(K_vals), _tensor_ptr(rhs), _tensor_ptr(freact),
+                                       self._stream(stream))
+        if rc != 0:
+            self._raise(rc, -1)
+
+    def pcg_solve(self, K_vals, b, x, rtol=1e-12, max_iter=10000, stream=None):
+        """K x = b (Jacobi PCG from x = 0); returns (iterations, relative residual)."""
+        it, rr = ctypes.c_int(0), ctypes.c_double(0.0)
+        rc = lib().fcg_pcg_solve(self._h, _tensor_ptr(K_vals), _tensor_ptr(b), _tensor_ptr(x),
+                                 float(rtol), int(max_iter), ctypes.byref(it), ctypes.byref(rr),
+                                 self._stream(stream))
+        if rc != 0:
+            self._raise(rc, -1)
+        return it.value, rr.value
 
     def set_timing(self, enable):
         lib().fcg_set_timing(self._h, 1 if enable else 0)

@@ -154,6 +154,41 @@ int fcg_get_info(const fcg_ctx* ctx, fcg_info* info);
 int fcg_get_diagnostics(const fcg_ctx* ctx, uint64_t* out, int n);
 
 /* ------------------------------------------------------------------------------------------
+ * Around the assembly: what one Newton step of Solid statics needs on the device
+ * (NOX full Newton, 4C_solver_nonlin_nox_linearsystem.cpp:275-353, with the structure's
+ * Dirichlet handling, 4C_structure_new_dbc.cpp:221-295).  All vectors are device-resident
+ * (owned DOF rows unless stated); `stream` as for fcg_evaluate_device; the calls return after
+ * the stream has drained.
+ * ---------------------------------------------------------------------------------------- */
+/* y_row = K x_col (Epetra_CrsMatrix::Multiply on the owned rows). */
+int fcg_spmv(fcg_ctx* ctx, const double* d_K_vals, const double* d_x_col, double* d_y_row,
+    void* stream);
+/* Dirichlet rows (row LIDs d_rows[n_dbc], device array): freact[row] = rhs[row] (if freact is not
+ * NULL, Solid::Dbc::extract_freact), rhs[row] = 0 (apply_dirichlet_to_system with zeros),
+ * K row -> unit row (SparseMatrix::apply_dirichlet, diagonalblock = true,
+ * 4C_linalg_sparsematrix.cpp:978-1097).  K or rhs may be NULL. */
+int fcg_dirichlet_apply(fcg_ctx* ctx, int64_t n_dbc, const int32_t* d_rows, double* d_K_vals,
+    double* d_rhs_row, double* d_freact_row, void* stream);
+/* K x = b by Jacobi-preconditioned CG from x = 0 until |r| <= rtol |b| or max_iter iterations;
+ * single-rank systems only (matrix column map = row map), else FCG_ERR_ARG.  Deterministic. */
+int fcg_pcg_solve(fcg_ctx* ctx, const double* d_K_vals, const double* d_b_row, double* d_x_row,
+    double rtol, int max_iter, int* iterations, double* rel_residual, void* stream);
+
+/* Neumann loads (host arrays; added into fext_row, owned rows only).  funct[d] > 0 selects a
+ * spatial function evaluated through `fn` at the reference position of each integration point
+ * (Core::Utils::FunctionOfSpaceTime::evaluate); funct may be NULL.
+ *   surface: live load on the material configuration, 4C_solid_3D_ele_surface_evaluate.cpp:262-320;
+ *            face_nodes[n_faces][4 (hex8 -> quad4) or 9 (hex27 -> quad9)] in 4C surface order
+ *   volume:  4C_solid_3D_ele_neumann_evaluator.cpp:45-110; ele_nodes[n_ele][8 or 27] */
+typedef double (*fcg_funct_fn)(int funct_id, const double* x, double time, void* user);
+int fcg_neumann_surface(int celltype, int64_t n_faces, const int32_t* face_nodes,
+    const double* node_x, const int32_t* node_dof_row, const int32_t* onoff, const double* val,
+    const int32_t* funct, fcg_funct_fn fn, void* user, double time, double* fext_row);
+int fcg_neumann_volume(int celltype, int64_t n_ele, const int32_t* ele_nodes, const double* node_x,
+    const int32_t* node_dof_row, const int32_t* onoff, const double* val, const int32_t* funct,
+    fcg_funct_fn fn, void* user, double time, double* fext_row);
+
+/* ------------------------------------------------------------------------------------------
  * Structured-box discretization builder: a restatement of 4C's GridGenerator
  * (src/core/io/src/4C_io_gridgenerator.cpp:41-392), node ownership of Rebalance::build_graph
  * (src/core/rebalance/src/4C_rebalance_graph_based.cpp:159-215), DofSet numbering
