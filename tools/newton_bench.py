@@ -1,0 +1,93 @@
+"""Newton-loop measurement on one GPU (BASELINE configs 1 and 3 shapes).
+
+Cantilever box [0,L]x[0,1]x[0,1] (x- face clamped, x+ face surface load), StVK E=210 nu=0.3,
+static full Newton through 4c_amd/newton.py: per iteration fcg_evaluate_device + Dirichlet +
+Jacobi PCG.  Prints one JSON line with per-phase times.
+usage: newton_bench.py --celltype hex8|hex27 --kinem linear|totlag --n N [--load L]"""
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+pkg = importlib.import_module("4c_amd")
+fcg, newton = pkg.fcg, importlib.import_module("4c_amd.newton")
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--celltype", default="hex8")
+ap.add_argument("--kinem", default="linear")
+ap.add_argument("--n", type=int, default=10)
+ap.add_argument("--length", type=float, default=10.0)
+ap.add_argument("--load", type=float, default=-1e-3)
+ap.add_argument("--lin-rtol", type=float, default=1e-10)
+ap.add_argument("--tol", type=float, default=1e-8)
+a = ap.parse_args()
+ct = fcg.HEX8 if a.celltype == "hex8" else fcg.HEX27
+kin = fcg.LINEAR if a.kinem == "linear" else fcg.TOTLAG
+t0 = time.perf_counter()
+mesh = fcg.BoxMesh(ct, (a.n, a.n, a.n), upper=(a.length, 1.0, 1.0))
+X = mesh.node_x
+dbc_nodes = np.nonzero(np.isclose(X[:, 0], 0.0) & (mesh.node_dof_row >= 0))[0]
+dbc = np.sort((mesh.node_dof_row[dbc_nodes][:, None] + np.arange(3)).ravel()).astype(np.int32)
+face = [1, 2, 6, 5] if ct == fcg.HEX8 else [1, 2, 6, 5, 9, 14, 17, 13, 22]
+faces = mesh.ele_nodes[mesh.ele_ijk[:, 0] == a.n - 1][:, face]
+fext = np.zeros(mesh.n_rows)
+fcg.neumann_surface(ct, faces, X, mesh.node_dof_row, [1, 1, 1], [0.0, 0.0, a.load], fext)
+ev = fcg.Evaluator(mesh, kinematics=kin, youngs=210.0, poisson=0.3)
+t_setup = time.perf_counter() - t0
+
+
+class Timed(newton.StaticNewton):
+    """StaticNewton with per-phase timing (synchronised wall clock)."""
+
+    def solve(self):
+        u = torch.zeros(self.n, dtype=torch.float64, device=self.dev)
+        self.history, ndu = [], float("inf")
+        for it in range(self.max_iter + 1):
+            torch.cuda.synchronize()
+            t_a = time.perf_counter()
+            self.ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u, self.fint, self.K)
+            torch.cuda.synchronize()
+            t_b = time.perf_counter()
+            torch.sub(self.fint, self.fext, out=self.r)
+            self.ev.dirichlet_apply(self.dbc, self.K, self.r, self.freact)
+            nr = float(torch.linalg.vector_norm(self.r))
+            t_c = time.perf_counter()
+            rec = {"iter": it, "norm_res": nr, "assembly_ms": 1e3 * (t_b - t_a),
+                   "dbc_ms": 1e3 * (t_c - t_b)}
+            if it > 0 and nr <= self.tol_res and ndu <= self.tol_inc:
+                self.history.append(rec)
+                return u
+            torch.neg(self.r, out=self.r)
+            li, lr = self.ev.pcg_solve(self.K, self.r, self.du, self.lin_rtol, self.lin_max_iter)
+            torch.cuda.synchronize()
+            t_d = time.perf_counter()
+            ndu = float(torch.linalg.vector_norm(self.du))
+            u += self.du
+            rec.update(solve_ms=1e3 * (t_d - t_c), pcg_iter=li, pcg_relres=lr, norm_inc=ndu)
+            self.history.append(rec)
+        return u
+
+
+nt = Timed(ev, fext, dbc, tol_res=a.tol * max(np.linalg.norm(fext), 1e-300), tol_inc=a.tol,
+           lin_rtol=a.lin_rtol)
+t1 = time.perf_counter()
+u = nt.solve()
+torch.cuda.synchronize()
+t_newton = time.perf_counter() - t1
+h = nt.history
+out = {"config": f"{a.celltype}-{a.kinem}-{a.n}^3-cantilever", "elements": mesh.n_ele,
+       "dofs": mesh.n_rows, "nnz": mesh.nnz, "setup_s": t_setup, "newton_s": t_newton,
+       "newton_iterations": len(h) - 1,
+       "assembly_ms_mean": float(np.mean([r["assembly_ms"] for r in h])),
+       "assembly_elem_per_s": mesh.n_ele / (1e-3 * float(np.median([r["assembly_ms"] for r in h]))),
+       "solve_ms_total": float(sum(r.get("solve_ms", 0.0) for r in h)),
+       "pcg_iterations": [r.get("pcg_iter") for r in h[:-1]],
+       "tip_uz": float(u[mesh.node_dof_row[np.argmax(X[:, 0] + X[:, 1] + X[:, 2])] + 2]),
+       "history": h}
+print(json.dumps(out))
