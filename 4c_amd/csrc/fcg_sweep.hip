@@ -84,10 +84,10 @@ struct SweepShared {
   double dN[8][8][3];
   double w8[8];
   uint32_t neg[NSLOT];  // bit g set: fac < 0 at Gauss point g
-  // lower-layer parts of the in-plane blocks (dz = 0) of node plane L+1: [column][slot][3x3],
-  // slot = in-plane neighbour (dy+1)*3 + dx+1 (read, then rewritten, by the same lane) except for
-  // the self block, which lane k1 writes and lane k0 reads: slot 4 or 9 by plane parity
-  double hold[TX * TY][10][9];
+  // lower-layer parts of the in-plane blocks (dz = 0) of node plane L+1, by plane parity (the
+  // D-side lane writes what the U-side lane of the next layer reads):
+  // [parity][column][in-plane neighbour (dy+1)*3 + dx+1][3x3]
+  double hold[2][TX * TY][9][9];
   double fhold[2][TX * TY][3];  // residual parts, by plane parity
 };
 
@@ -255,13 +255,15 @@ __device__ inline void sweep_stage_a(SweepShared<KIN>& sh, const SweepArgs& A, i
 
 }
 
-// One element visit: accumulate the block (a, b) of element slot `slot` over its Gauss points.
-// Acc layout: G[9] (row-major, G[3r+q] = sum a'_r b'_q) then, for TotLag, H[6] and geo.
+// One element visit: accumulate the blocks (a, b1) into acc1 and (a, b2) into acc2 over the
+// Gauss points of element slot `slot`.  Acc layout: G[9] (row-major, G[3r+q] = sum a'_r b'_q)
+// then, for TotLag, H[6] and geo.
 template <int KIN, bool NEG>
-__device__ inline void sweep_visit(const SweepShared<KIN>& sh, int slot, int a, int b,
-    uint32_t nm, double* acc)
+__device__ inline void sweep_visit(const SweepShared<KIN>& sh, int slot, int a, int b1, int b2,
+    uint32_t nm, double* acc1, double* acc2)
 {
-  auto gp_body = [&](int g, double a0, double a1, double a2, double b0, double b1, double b2) {
+  auto gp_body = [&](int g, double a0, double a1, double a2, double p0, double p1, double p2,
+                     double q0, double q1, double q2) {
     if (NEG && ((nm >> g) & 1u))
     {
       a0 = -a0;
@@ -270,36 +272,47 @@ __device__ inline void sweep_visit(const SweepShared<KIN>& sh, int slot, int a, 
     }
     if (KIN == 0)
     {
-      acc[0] += a0 * b0; acc[1] += a0 * b1; acc[2] += a0 * b2;
-      acc[3] += a1 * b0; acc[4] += a1 * b1; acc[5] += a1 * b2;
-      acc[6] += a2 * b0; acc[7] += a2 * b1; acc[8] += a2 * b2;
+      acc1[0] += a0 * p0; acc1[1] += a0 * p1; acc1[2] += a0 * p2;
+      acc1[3] += a1 * p0; acc1[4] += a1 * p1; acc1[5] += a1 * p2;
+      acc1[6] += a2 * p0; acc1[7] += a2 * p1; acc1[8] += a2 * p2;
+      acc2[0] += a0 * q0; acc2[1] += a0 * q1; acc2[2] += a0 * q2;
+      acc2[3] += a1 * q0; acc2[4] += a1 * q1; acc2[5] += a1 * q2;
+      acc2[6] += a2 * q0; acc2[7] += a2 * q1; acc2[8] += a2 * q2;
     }
     else
     {
       const double* P = sh.gp[g][slot];
       const double F0 = P[0], F1 = P[1], F2 = P[2], F3 = P[3], F4 = P[4], F5 = P[5], F6 = P[6],
                    F7 = P[7], F8 = P[8];
+      const double S0 = P[9], S1 = P[10], S2 = P[11], S3 = P[12], S4 = P[13], S5 = P[14];
       const double fa0 = F0 * a0 + F3 * a1 + F6 * a2;
       const double fa1 = F1 * a0 + F4 * a1 + F7 * a2;
       const double fa2 = F2 * a0 + F5 * a1 + F8 * a2;
-      const double fb0 = F0 * b0 + F3 * b1 + F6 * b2;
-      const double fb1 = F1 * b0 + F4 * b1 + F7 * b2;
-      const double fb2 = F2 * b0 + F5 * b1 + F8 * b2;
-      acc[0] += fa0 * fb0; acc[1] += fa0 * fb1; acc[2] += fa0 * fb2;
-      acc[3] += fa1 * fb0; acc[4] += fa1 * fb1; acc[5] += fa1 * fb2;
-      acc[6] += fa2 * fb0; acc[7] += fa2 * fb1; acc[8] += fa2 * fb2;
-      const double ab = a0 * b0 + a1 * b1 + a2 * b2;
-      acc[9] += ab * (F0 * F0 + F3 * F3 + F6 * F6);
-      acc[10] += ab * (F1 * F1 + F4 * F4 + F7 * F7);
-      acc[11] += ab * (F2 * F2 + F5 * F5 + F8 * F8);
-      acc[12] += ab * (F0 * F1 + F3 * F4 + F6 * F7);
-      acc[13] += ab * (F1 * F2 + F4 * F5 + F7 * F8);
-      acc[14] += ab * (F2 * F0 + F5 * F3 + F8 * F6);
-      const double S0 = P[9], S1 = P[10], S2 = P[11], S3 = P[12], S4 = P[13], S5 = P[14];
-      const double sb0 = S0 * b0 + S3 * b1 + S5 * b2;
-      const double sb1 = S3 * b0 + S1 * b1 + S4 * b2;
-      const double sb2 = S5 * b0 + S4 * b1 + S2 * b2;
-      acc[15] += a0 * sb0 + a1 * sb1 + a2 * sb2;
+      const double M0 = F0 * F0 + F3 * F3 + F6 * F6, M1 = F1 * F1 + F4 * F4 + F7 * F7,
+                   M2 = F2 * F2 + F5 * F5 + F8 * F8, M3 = F0 * F1 + F3 * F4 + F6 * F7,
+                   M4 = F1 * F2 + F4 * F5 + F7 * F8, M5 = F2 * F0 + F5 * F3 + F8 * F6;
+      // a.S (S symmetric): geo = (S a).b
+      const double sa0 = S0 * a0 + S3 * a1 + S5 * a2;
+      const double sa1 = S3 * a0 + S1 * a1 + S4 * a2;
+      const double sa2 = S5 * a0 + S4 * a1 + S2 * a2;
+      auto one = [&](double* acc, double b0, double bb1, double bb2) {
+        const double fb0 = F0 * b0 + F3 * bb1 + F6 * bb2;
+        const double fb1 = F1 * b0 + F4 * bb1 + F7 * bb2;
+        const double fb2 = F2 * b0 + F5 * bb1 + F8 * bb2;
+        acc[0] += fa0 * fb0; acc[1] += fa0 * fb1; acc[2] += fa0 * fb2;
+        acc[3] += fa1 * fb0; acc[4] += fa1 * fb1; acc[5] += fa1 * fb2;
+        acc[6] += fa2 * fb0; acc[7] += fa2 * fb1; acc[8] += fa2 * fb2;
+        const double ab = a0 * b0 + a1 * bb1 + a2 * bb2;
+        acc[9] += ab * M0;
+        acc[10] += ab * M1;
+        acc[11] += ab * M2;
+        acc[12] += ab * M3;
+        acc[13] += ab * M4;
+        acc[14] += ab * M5;
+        acc[15] += sa0 * b0 + sa1 * bb1 + sa2 * bb2;
+      };
+      one(acc1, p0, p1, p2);
+      one(acc2, q0, q1, q2);
     }
   };
 #pragma unroll
@@ -308,11 +321,41 @@ __device__ inline void sweep_visit(const SweepShared<KIN>& sh, int slot, int a, 
     const double2 ax = *reinterpret_cast<const double2*>(&sh.nx[nx2i(0, p, slot, a)]);
     const double2 ay = *reinterpret_cast<const double2*>(&sh.nx[nx2i(1, p, slot, a)]);
     const double2 az = *reinterpret_cast<const double2*>(&sh.nx[nx2i(2, p, slot, a)]);
-    const double2 bx = *reinterpret_cast<const double2*>(&sh.nx[nx2i(0, p, slot, b)]);
-    const double2 by = *reinterpret_cast<const double2*>(&sh.nx[nx2i(1, p, slot, b)]);
-    const double2 bz = *reinterpret_cast<const double2*>(&sh.nx[nx2i(2, p, slot, b)]);
-    gp_body(2 * p, ax.x, ay.x, az.x, bx.x, by.x, bz.x);
-    gp_body(2 * p + 1, ax.y, ay.y, az.y, bx.y, by.y, bz.y);
+    const double2 px = *reinterpret_cast<const double2*>(&sh.nx[nx2i(0, p, slot, b1)]);
+    const double2 py = *reinterpret_cast<const double2*>(&sh.nx[nx2i(1, p, slot, b1)]);
+    const double2 pz = *reinterpret_cast<const double2*>(&sh.nx[nx2i(2, p, slot, b1)]);
+    const double2 qx = *reinterpret_cast<const double2*>(&sh.nx[nx2i(0, p, slot, b2)]);
+    const double2 qy = *reinterpret_cast<const double2*>(&sh.nx[nx2i(1, p, slot, b2)]);
+    const double2 qz = *reinterpret_cast<const double2*>(&sh.nx[nx2i(2, p, slot, b2)]);
+    gp_body(2 * p, ax.x, ay.x, az.x, px.x, py.x, pz.x, qx.x, qy.x, qz.x);
+    gp_body(2 * p + 1, ax.y, ay.y, az.y, px.y, py.y, pz.y, qx.y, qy.y, qz.y);
+  }
+}
+
+// K_AB of an accumulated part (isotropic StVK)
+template <int KIN>
+__device__ inline void block_k(const StVK& m, const double* acc, double* Kb)
+{
+  const double lam = m.lambda, mu = m.mu;
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int q = 0; q < 3; ++q) Kb[3 * r + q] = lam * acc[3 * r + q] + mu * acc[3 * q + r];
+  if (KIN == 0)
+  {
+    const double tr = mu * (acc[0] + acc[4] + acc[8]);
+    Kb[0] += tr;
+    Kb[4] += tr;
+    Kb[8] += tr;
+  }
+  else
+  {
+    Kb[0] += mu * acc[9] + acc[15];
+    Kb[4] += mu * acc[10] + acc[15];
+    Kb[8] += mu * acc[11] + acc[15];
+    Kb[1] += mu * acc[12]; Kb[3] += mu * acc[12];
+    Kb[5] += mu * acc[13]; Kb[7] += mu * acc[13];
+    Kb[2] += mu * acc[14]; Kb[6] += mu * acc[14];
   }
 }
 
@@ -397,9 +440,7 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
   // visit lane: node column c, task k
   const int c = tid >> 4, k = tid & 15;
   const int cx = c % TX, cy = c / TX;
-  uint32_t vis[4];
-#pragma unroll
-  for (int v = 0; v < 4; ++v) vis[v] = kVisit[k][v];
+  const uint32_t vis0 = kVisit[k][0], vis1 = kVisit[k][1];
 
   // --- prologue: node planes kz0-1, kz0 and their records; prefetch plane kz0+1
   if (n_lane)
@@ -440,68 +481,28 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
     const uint32_t* recL1 = sh.prec[ring(L + 1)];
     if (WANT_K)
     {
-      double acc[NACC];
-#pragma unroll
-      for (int i = 0; i < NACC; ++i) acc[i] = 0.0;
-#pragma unroll 1
-      for (int v = 0; v < 4; ++v)
-      {
-        const uint32_t w = v == 0 ? vis[0] : v == 1 ? vis[1] : v == 2 ? vis[2] : vis[3];
-        const int q = w & 3, a = (w >> 2) & 7, b = (w >> 5) & 7, act = (w >> 8) & 7,
-                  t = (w >> 12) & 31;
-        const int slot = (cx + (q & 1)) + EXN * (cy + (q >> 1));
-        const uint32_t nm = sh.neg[slot];
-        if (nm == 0u)
-          sweep_visit<KIN, false>(sh, slot, a, b, nm, acc);
-        else
-          sweep_visit<KIN, true>(sh, slot, a, b, nm, acc);
-        if (act == kVisitActCont) continue;
-        // K_AB of the accumulated part
-        const double lam = A.mat.lambda, mu = A.mat.mu;
-        double Kb[9];
-#pragma unroll
-        for (int r = 0; r < 3; ++r)
-#pragma unroll
-          for (int qq = 0; qq < 3; ++qq) Kb[3 * r + qq] = lam * acc[3 * r + qq] + mu * acc[3 * qq + r];
-        if (KIN == 0)
+      // finished block t of this lane's column: hold it, or write it (plus the held part)
+      auto emit = [&](int act, int t, double* Kb) {
+        const int par = act == kActHold ? (L + 1) & 1 : L & 1;
+        double* h = sh.hold[par][c][t - 9];
+        if (act == kActHold)
         {
-          const double tr = mu * (acc[0] + acc[4] + acc[8]);
-          Kb[0] += tr;
-          Kb[4] += tr;
-          Kb[8] += tr;
-        }
-        else
-        {
-          Kb[0] += mu * acc[9] + acc[15];
-          Kb[4] += mu * acc[10] + acc[15];
-          Kb[8] += mu * acc[11] + acc[15];
-          Kb[1] += mu * acc[12]; Kb[3] += mu * acc[12];
-          Kb[5] += mu * acc[13]; Kb[7] += mu * acc[13];
-          Kb[2] += mu * acc[14]; Kb[6] += mu * acc[14];
-        }
-#pragma unroll
-        for (int i = 0; i < NACC; ++i) acc[i] = 0.0;
-        // in-plane blocks: the lower-layer part waits in LDS for the next layer
-        if (act == kVisitActHold0 || act == kVisitActHold1)
-        {
-          double* h = sh.hold[c][t == 13 && ((L + 1) & 1) ? 9 : t - 9];
 #pragma unroll
           for (int i = 0; i < 9; ++i) h[i] = Kb[i];
-          continue;
+          return;
         }
-        if (act == kVisitActWriteLH0 || act == kVisitActWriteLH1)
+        if (act == kActWriteLHold)
         {
-          const double* h = sh.hold[c][t == 13 && (L & 1) ? 9 : t - 9];
 #pragma unroll
           for (int i = 0; i < 9; ++i) Kb[i] = h[i] + Kb[i];
         }
-        const bool to_l1 = act == kVisitActWriteL1;
-        if (!(to_l1 ? wl1 : wl)) continue;
+        const bool to_l1 = act == kActWriteL1;
+        if (!(to_l1 ? wl1 : wl)) return;
         const uint32_t* rec = to_l1 ? recL1 : recL;
         const int32_t row0 = int32_t(rec[PR_ROW0 + c]);
-        if (row0 < 0) continue;
+        if (row0 < 0) return;
         const uint16_t pos = reinterpret_cast<const uint16_t*>(rec + PR_NPOS)[27 * c + t];
-        if (pos == 0xFFFF) continue;
+        if (pos == 0xFFFF) return;
         const int64_t base = int64_t(rec[PR_BASE + 2 * c]) | (int64_t(rec[PR_BASE + 2 * c + 1]) << 32);
         const int64_t len = int32_t(rec[PR_LEN + c]);
         double* dst = A.K + base + pos;
@@ -515,6 +516,42 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
             else
               dst[r * len + qq] += Kb[3 * r + qq];
           }
+      };
+      double acc1[NACC], acc2[NACC];
+#pragma unroll
+      for (int i = 0; i < NACC; ++i) acc1[i] = acc2[i] = 0.0;
+#pragma unroll 1
+      for (int v = 0; v < 2; ++v)
+      {
+        const uint32_t w = v == 0 ? vis0 : vis1;
+        const int q = w & 3, a = (w >> 2) & 7, b1 = (w >> 5) & 7, b2 = (w >> 8) & 7;
+        const int slot = (cx + (q & 1)) + EXN * (cy + (q >> 1));
+        const uint32_t nm = sh.neg[slot];
+        if (nm == 0u)
+          sweep_visit<KIN, false>(sh, slot, a, b1, b2, nm, acc1, acc2);
+        else
+          sweep_visit<KIN, true>(sh, slot, a, b1, b2, nm, acc1, acc2);
+        if ((w >> 24) & 1u)
+        {
+          double Kb[9];
+          block_k<KIN>(A.mat, acc2, Kb);
+#pragma unroll
+          for (int i = 0; i < NACC; ++i) acc2[i] = 0.0;
+          emit(int((w >> 21) & 7), int((w >> 16) & 31), Kb);
+        }
+      }
+      // acc1: the self block's two halves meet in lane r = 2 (order: qy = 1 half + qy = 0 half)
+      {
+        const int pair = int((vis1 >> 26) & 3);
+        double Kb[9];
+        block_k<KIN>(A.mat, acc1, Kb);
+#pragma unroll
+        for (int i = 0; i < 9; ++i)
+        {
+          const double o = dpp_f64<kDppXor1>(Kb[i]);
+          if (pair == kPairRecv) Kb[i] += o;
+        }
+        if (pair != kPairGive) emit(int((vis1 >> 21) & 7), int((vis1 >> 11) & 31), Kb);
       }
     }
     // nodal forces f_A = sum_e sum_g fac F S N_XYZ_A: lane k takes Gauss points 4h..4h+3
