@@ -53,12 +53,19 @@ class HaloImport:
         self.recv_counts = recv_counts.tolist()
         self.sendbuf = torch.empty(len(req), dtype=torch.float64, device=device)
         self.recvbuf = torch.empty(len(ghost), dtype=torch.float64, device=device)
+        # gloo moves host tensors only: stage device buffers through the host (tests/rehearsals)
+        self.staged = cpu.type != torch.device(device).type
         self.n_ghost = len(ghost)
 
     def __call__(self, u_row, u_col):
         u_col.index_copy_(0, self.own_col, u_row.index_select(0, self.own_row))
         torch.index_select(u_row, 0, self.send_row, out=self.sendbuf)
-        if self.world > 1:
+        if self.world > 1 and self.staged:
+            rb = torch.empty(self.n_ghost, dtype=torch.float64)
+            dist.all_to_all_single(rb, self.sendbuf.cpu(), output_split_sizes=self.recv_counts,
+                                   input_split_sizes=self.send_counts)
+            self.recvbuf.copy_(rb)
+        elif self.world > 1:
             dist.all_to_all_single(self.recvbuf, self.sendbuf,
                                    output_split_sizes=self.recv_counts,
                                    input_split_sizes=self.send_counts)
@@ -78,5 +85,10 @@ def residual_norm(f_row):
     """||f||_2 over all ranks (NOX norm, an Allreduce in the reference)."""
     s = torch.dot(f_row, f_row).reshape(1)
     if dist.is_initialized() and dist.get_world_size() > 1:
-        dist.all_reduce(s)
+        if dist.get_backend() == "gloo" and s.device.type != "cpu":
+            h = s.cpu()
+            dist.all_reduce(h)
+            s = h.to(s.device)
+        else:
+            dist.all_reduce(s)
     return torch.sqrt(s)

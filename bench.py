@@ -41,25 +41,43 @@ ALG_BYTES_PER_ELE = 2069.0
 ALG_FLOP_PER_ELE = 41.4e3
 
 
-def weak_interval(n, world):
-    """Global INTERVALS such that the GridGenerator box split gives every rank n^3 elements."""
-    iv = [n, n, n]
-    sub = [1, 1, 1]
-    w = world
-    f = 2
-    factors = []
+def _gridgen_subdivisions(iv, world):
+    """Processor grid of GridGenerator's box split (4C_io_gridgenerator.cpp:87-117): prime
+    factors, largest first, each to the direction with the largest interval per subdivision."""
+    factors, w, f = [], world, 2
     while w > 1:
         if w % f == 0:
             factors.append(f)
             w //= f
         else:
             f += 1
+    sub = [1, 1, 1]
     for fac in reversed(factors):
-        ratios = [iv[d] * 1.0 / sub[d] for d in range(3)]
-        d = int(np.argmax(ratios))  # first maximum, the reference's tie order
+        r = [iv[d] / sub[d] for d in range(3)]
+        d = 0 if (r[0] >= r[1] and r[0] >= r[2]) else (1 if r[1] >= r[2] else 2)
         sub[d] *= fac
-        iv[d] = n * sub[d]
-    return tuple(iv)
+    return sub
+
+
+def weak_interval(n, world):
+    """Global INTERVALS such that GridGenerator's own split gives every rank an n^3 box: the
+    processor grid as cubic as the prime factors allow (N=8 -> 2x2x2, i.e. config 4's 200^3),
+    checked against the reference's split rule; slabs along x otherwise."""
+    factors, w, f = [], world, 2
+    while w > 1:
+        if w % f == 0:
+            factors.append(f)
+            w //= f
+        else:
+            f += 1
+    p = [1, 1, 1]
+    for fac in reversed(factors):
+        d = int(np.argmin(p))
+        p[d] *= fac
+    iv = tuple(n * p[d] for d in range(3))
+    if _gridgen_subdivisions(iv, world) == p:
+        return iv
+    return (n * world, n, n)
 
 
 def cpu_baseline(n, kinem, threads):
@@ -108,7 +126,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--n", type=int, default=100, help="elements per direction per GPU")
+    ap.add_argument("--elems-per-dir", dest="n", type=int, default=100,
+                    help="elements per direction per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     args = ap.parse_args()
@@ -116,10 +135,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # FCG_DIST_BACKEND=gloo: rehearsal of the multi-rank flow with all ranks on the visible
+    # GPU(s) and the halo staged through the host; the real runs use RCCL ("nccl")
+    backend = os.environ.get("FCG_DIST_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     iv = weak_interval(args.n, world)
     t_setup = time.perf_counter()
@@ -167,7 +193,7 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     ev.set_timing(False)
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = elapsed.item()
