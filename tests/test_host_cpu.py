@@ -153,3 +153,20 @@ def test_structured_hint_is_verified_before_device_work():
     with pytest.raises(fcg.FcgError) as ei:
         fcg.Evaluator(m, path=fcg.PATH_STRUCTURED)
     assert ei.value.code == 3 and "lattice" in str(ei.value)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_bench_weak_scaling_boxes(world):
+    """bench.py's weak-scaling box: GridGenerator's own split gives every rank n^3 elements,
+    N=8 is config 4's cube (2x2x2)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    n = 3
+    iv = b.weak_interval(n, world)
+    if world == 8:
+        assert iv == (2 * n, 2 * n, 2 * n)
+    for r in range(world):
+        m = fcg.BoxMesh(fcg.HEX8, iv, rank=r, nranks=world)
+        assert m.n_ele_row == n ** 3
