@@ -100,6 +100,31 @@ int orc_discretization_evaluate(int celltype, int kinem, double E, double nu, in
     const int32_t* node_owner, int64_t min_node_gid, int nworkers, const double* u, orc_csr* K,
     double* fint, int64_t* bad_ele);
 
+/* ---------------------------------------------------------------------------------------
+ * Thermo-structure interaction, geometrically linear (BASELINE config 5).  Pinned against the
+ * RESULT DESCRIPTION of tsi_heatflux_monolithic.dat and tsi_heatflux_flexoutsurf_monolithic.dat
+ * (tests/test_oracle_known_answers.py).
+ * ------------------------------------------------------------------------------------- */
+/* stress-temperature modulus m = -(2 mu + 3 lambda) alpha_T (4C_mat_thermostvenantkirchhoff.cpp:331-369) */
+double orc_thermo_stvk_st_modulus(double E, double nu, double alpha);
+
+/* SOLIDSCATRA + ThermoStVenantKirchhoff, KINEM linear:
+ *   Ke, fe  struct_calc_nlnstiff with the "temperature" state (4C_solid_scatra_3D_ele_calc.cpp:272-403;
+ *           S = C E + m (T_gp - T0) (1,1,1,0,0,0), 4C_mat_thermostvenantkirchhoff.cpp:141-174)
+ *   Kst     struct_calc_stifftemp (4C_solid_scatra_3D_ele_calc.cpp:405-490): (3n x n)
+ * T: [n] nodal temperatures.  Matrices column-major, all outputs +=, NULL = skip. */
+int orc_tsi_solid_evaluate(int celltype, double E, double nu, double alpha, double T0,
+    const double* X, const double* u, const double* T, double* Ke, double* fe, double* Kst);
+
+/* Thermo::TemperImpl, geometrically linear TSI (4C_thermo_ele_impl.cpp):
+ *   Ktt, fT  calc_thermo_fintcond: linear_thermo_contribution (:802-891) + linear_disp_contribution
+ *            (:899-1043) with Fourier conductivity `conduct` and stress-temperature modulus m
+ *   Kts      calc_thermo_coupltang: linear_coupled_tang (:1046-1194), (n x 3n)
+ * v: [n][3] nodal velocities; timefac, timefac_d per :1094-1132 (statics: 1, 1/dt). */
+int orc_tsi_thermo_evaluate(int celltype, double conduct, double m, const double* X,
+    const double* T, const double* v, double timefac, double timefac_d, double* Ktt,
+    double* fT, double* Kts);
+
 #ifdef __cplusplus
 }
 #endif
