@@ -880,3 +880,189 @@ int orc_discretization_evaluate(int celltype, int kinem, double E, double nu, in
   if (bad_ele) *bad_ele = first_bad;
   return result;
 }
+
+/* =======================================================================================
+ * Thermo-structure interaction, geometrically linear (BASELINE config 5)
+ * ===================================================================================== */
+
+double orc_thermo_stvk_st_modulus(double E, double nu, double alpha)
+{
+  /* ThermoStVenantKirchhoff::st_modulus (4C_mat_thermostvenantkirchhoff.cpp:331-369) */
+  const double c1 = E / (1.0 + nu);
+  const double b1 = c1 * nu / (1.0 - 2.0 * nu);
+  const double mu = 0.5 * c1;
+  const double lambda = b1;
+  return (-1.0) * (2.0 * mu + 3.0 * lambda) * alpha;
+}
+
+/* linear B operator (evaluate_linear_strain_gradient, calc_lib.hpp:770-799; identical to the
+ * thermo element's calculate_boplin, 4C_thermo_ele_impl.cpp:2829-2869) */
+static void boplin(int n, const double* NX, double* Bop)
+{
+  memset(Bop, 0, sizeof(double) * 6 * 3 * n);
+#define B(r, c) Bop[(r) + 6 * (c)]
+#define NXYZ(d, i) NX[(d) + 3 * (i)]
+  for (int i = 0; i < n; ++i)
+  {
+    for (int d = 0; d < 3; ++d) B(d, 3 * i + d) = NXYZ(d, i);
+    B(3, 3 * i + 0) = NXYZ(1, i);
+    B(3, 3 * i + 1) = NXYZ(0, i);
+    B(4, 3 * i + 1) = NXYZ(2, i);
+    B(4, 3 * i + 2) = NXYZ(1, i);
+    B(5, 3 * i + 0) = NXYZ(2, i);
+    B(5, 3 * i + 2) = NXYZ(0, i);
+  }
+#undef B
+#undef NXYZ
+}
+
+/* Core::LinAlg::Matrix::dot (shape functions . nodal values), index order */
+static double dotn(const double* a, const double* b, int n)
+{
+  double s = 0.0;
+  for (int i = 0; i < n; ++i) s += a[i] * b[i];
+  return s;
+}
+
+int orc_tsi_solid_evaluate(int celltype, double E, double nu, double alpha, double T0,
+    const double* X, const double* u, const double* T, double* Ke, double* fe, double* Kst)
+{
+  if (celltype != ORC_HEX8 && celltype != ORC_HEX27) return ORC_ERR_ARG;
+  const int n = orc_num_nodes(celltype);
+  const int ndof = 3 * n;
+  const int ngp = orc_num_gp(celltype);
+  double xref[3 * MAXN], disp[3 * MAXN];
+  for (int i = 0; i < n; ++i)
+    for (int d = 0; d < 3; ++d)
+    {
+      xref[d + 3 * i] = X[3 * i + d];
+      disp[d + 3 * i] = u[3 * i + d];
+    }
+  /* struct_calc_stifftemp checks the nodal Jacobians (4C_solid_scatra_3D_ele_calc.cpp:441);
+   * struct_calc_nlnstiff of the solid-scatra element does not (:272-403). */
+  if (Kst)
+  {
+    double xin[3 * MAXN], dN[3 * MAXN];
+    orc_node_param_coords(celltype, xin);
+    for (int i = 0; i < n; ++i)
+    {
+      jac_map jm;
+      orc_shape_deriv1(celltype, &xin[3 * i], dN);
+      if (jacobian_mapping(n, dN, xref, &jm)) return ORC_ERR_SINGULAR;
+      if (!(jm.det > 0)) return ORC_ERR_NODAL_DETJ;
+    }
+  }
+  double cmat[36];
+  orc_stvk_cmat(E, nu, cmat); /* ThermoStVenantKirchhoff::setup_cmat (:308-326), constant E */
+  const double m = orc_thermo_stvk_st_modulus(E, nu, alpha);
+  double gxi[3 * 27], gw[27];
+  orc_gauss_points(celltype, gxi, gw);
+  for (int gp = 0; gp < ngp; ++gp)
+  {
+    double dN[3 * MAXN], N[MAXN];
+    orc_shape(celltype, &gxi[3 * gp], N);
+    orc_shape_deriv1(celltype, &gxi[3 * gp], dN);
+    jac_map jm;
+    if (jacobian_mapping(n, dN, xref, &jm)) return ORC_ERR_SINGULAR;
+    const double fac = jm.det * gw[gp];
+    double Bop[6 * MAXDOF];
+    boplin(n, jm.N_XYZ, Bop);
+    /* prepare_scalar_in_parameter_list("temperature"): T_gp = N . T
+     * (4C_solid_scatra_3D_ele_calc.cpp:172-182) */
+    const double Tgp = dotn(N, T, n);
+    if (fe || Ke)
+    {
+      double gl[6], pk2[6];
+      mm_nn(gl, 0.0, 1.0, Bop, disp, 6, ndof, 1, 0); /* evaluate_linear_gl_strain */
+      /* ThermoStVenantKirchhoff::evaluate (:141-174): S = C E, S_ii += m (T - T_ref) */
+      mm_nn(pk2, 0.0, 1.0, cmat, gl, 6, 6, 1, 0);
+      for (int i = 0; i < 3; ++i) pk2[i] += m * (Tgp - T0);
+      if (fe) mm_tn(fe, 1.0, fac, Bop, pk2, ndof, 6, 1, 1);
+      if (Ke)
+      {
+        double cb[6 * MAXDOF];
+        mm_nn(cb, 0.0, 1.0, cmat, Bop, 6, 6, ndof, 0);
+        mm_tn(Ke, 1.0, fac, Bop, cb, ndof, 6, ndof, 1);
+      }
+    }
+    if (Kst)
+    {
+      /* evaluate_d_stress_d_scalar (4C_mat_thermostvenantkirchhoff.cpp:250-295) with constant E:
+       * dS/dT = C_T E + (T - T0) ctemp_T + ctemp = (m, m, m, 0, 0, 0) */
+      double dSdT[6] = {m, m, m, 0.0, 0.0, 0.0};
+      /* k_dS = B^T dS/dT fac N^T (4C_solid_scatra_3D_ele_calc.cpp:472-487) */
+      double BdSdc[MAXDOF];
+      mm_tn(BdSdc, 0.0, fac, Bop, dSdT, ndof, 6, 1, 0);
+      for (int r = 0; r < ndof; ++r)
+        for (int c = 0; c < n; ++c) Kst[r + ndof * c] += BdSdc[r] * N[c];
+    }
+  }
+  return ORC_OK;
+}
+
+int orc_tsi_thermo_evaluate(int celltype, double conduct, double m, const double* X,
+    const double* T, const double* v, double timefac, double timefac_d, double* Ktt,
+    double* fT, double* Kts)
+{
+  if (celltype != ORC_HEX8 && celltype != ORC_HEX27) return ORC_ERR_ARG;
+  const int n = orc_num_nodes(celltype);
+  const int ndof = 3 * n;
+  const int ngp = orc_num_gp(celltype); /* DisTypeToOptGaussRule: hex_8point / hex_27point */
+  double xyze[3 * MAXN], evel[3 * MAXN];
+  for (int i = 0; i < n; ++i)
+    for (int d = 0; d < 3; ++d)
+    {
+      xyze[d + 3 * i] = X[3 * i + d];
+      evel[d + 3 * i] = v[3 * i + d];
+    }
+  double gxi[3 * 27], gw[27];
+  orc_gauss_points(celltype, gxi, gw);
+  double ctemp[6] = {m, m, m, 0.0, 0.0, 0.0}; /* setup_cthermo / fill_cthermo (:376-402) */
+  for (int gp = 0; gp < ngp; ++gp)
+  {
+    /* eval_shape_func_and_derivs_at_int_point (4C_thermo_ele_impl.cpp:2613-2671) */
+    double N[MAXN], deriv[3 * MAXN], xjm[9], derxy[3 * MAXN];
+    orc_shape(celltype, &gxi[3 * gp], N);
+    orc_shape_deriv1(celltype, &gxi[3 * gp], deriv);
+    mm_nt(xjm, 0.0, 1.0, deriv, xyze, 3, n, 3, 0);
+    const double det = invert3x3(xjm);
+    if (det < 1e-16) return det == 0.0 ? ORC_ERR_SINGULAR : ORC_ERR_NODAL_DETJ;
+    const double fac = gw[gp] * det;
+    mm_nn(derxy, 0.0, 1.0, xjm, deriv, 3, 3, n, 0);
+    const double NT = dotn(N, T, n); /* NT.multiply_tn(funct_, etempn_) */
+
+    /* linear_thermo_contribution (:802-891); Fourier: cmat = k I, heatflux = cmat gradT
+     * (4C_mat_fourier.cpp:147-192); the dercmat term vanishes for a constant conductivity */
+    if (fT || Ktt)
+    {
+      double gradtemp[3], heatflux[3], cm[9] = {conduct, 0, 0, 0, conduct, 0, 0, 0, conduct};
+      mm_nn(gradtemp, 0.0, 1.0, derxy, T, 3, n, 1, 0);
+      mm_nn(heatflux, 0.0, 1.0, cm, gradtemp, 3, 3, 1, 0);
+      if (fT) mm_tn(fT, 1.0, fac, derxy, heatflux, n, 3, 1, 1);
+      if (Ktt)
+      {
+        double aop[3 * MAXN];
+        mm_nn(aop, 0.0, 1.0, cm, derxy, 3, 3, n, 0);
+        mm_tn(Ktt, 1.0, fac, derxy, aop, n, 3, n, 1);
+      }
+      /* linear_disp_contribution (:899-1043): thermoelastic term with e' = B_L v */
+      double Bop[6 * MAXDOF], strainvel[6], Nctemp[6 * MAXN], ncBv[MAXN];
+      boplin(n, derxy, Bop);
+      mm_nn(strainvel, 0.0, 1.0, Bop, evel, 6, ndof, 1, 0);
+      mm_nt(Nctemp, 0.0, 1.0, N, ctemp, n, 1, 6, 0);
+      mm_nn(ncBv, 0.0, 1.0, Nctemp, strainvel, n, 6, 1, 0);
+      if (fT) mm_nn(fT, 1.0, -fac, ncBv, &NT, n, 1, 1, 1);
+      if (Ktt) mm_nt(Ktt, 1.0, -fac, ncBv, N, n, 1, n, 1);
+    }
+    /* linear_coupled_tang (:1046-1194): k_Td += -timefac fac timefac_d (N N.T ctemp^T) B_L */
+    if (Kts)
+    {
+      double Bop[6 * MAXDOF], NNT[MAXN], NNTC[6 * MAXN];
+      boplin(n, derxy, Bop);
+      mm_nn(NNT, 0.0, 1.0, N, &NT, n, 1, 1, 0);
+      mm_nt(NNTC, 0.0, 1.0, NNT, ctemp, n, 1, 6, 0);
+      mm_nn(Kts, 1.0, -timefac * fac * timefac_d, NNTC, Bop, n, 6, ndof, 1);
+    }
+  }
+  return ORC_OK;
+}

@@ -12,6 +12,8 @@ Sources (paths relative to /root/reference):
   tests/input_files/solid_ele_hex8_Standard_linear.dat   (registered tests/list_of_tests.cmake:1338)
   tests/input_files/solid_ele_hex27_Standard_linear.dat  (tests/list_of_tests.cmake:1311)
   tests/input_files/sohex27_patchtest_nl_cost_drt.dat    (tests/list_of_tests.cmake:1265)
+  tests/input_files/tsi_heatflux_monolithic.dat          (thermo-structure interaction, statics)
+  tests/input_files/tsi_heatflux_flexoutsurf_monolithic.dat
 """
 
 import json
@@ -113,12 +115,53 @@ def extract(fname):
             "functions": functs, "dynamic": dyn}
 
 
+def extract_tsi(fname):
+    """A monolithic TSI input: the structural data of extract() plus the thermo field's
+    conditions, the ThermoStVenantKirchhoff / Fourier constants, the TSI time stepping and the
+    THERMAL result lines."""
+    data = extract(fname)
+    s = sections(os.path.join(REF, fname))
+    mats = {}
+    for line in s["MATERIALS"]:
+        tok = line.split()
+        mats[tok[2]] = {tok[i]: tok[i + 1] for i in range(3, len(tok) - 1)}
+    st = mats["MAT_Struct_ThermoStVenantK"]
+    data["material"].update({"thexpans": float(st["THEXPANS"]), "inittemp": float(st["INITTEMP"]),
+                             "dens": float(st["DENS"])})
+    data["thermo_material"] = {"conduct": float(mats["MAT_Fourier"]["CONDUCT"]),
+                               "capa": float(mats["MAT_Fourier"]["CAPA"])}
+    for line in s["RESULT DESCRIPTION"]:
+        m = re.match(r"THERMAL DIS thermo NODE (\d+) QUANTITY temp VALUE\s+(\S+) TOLERANCE (\S+)", line)
+        if m:
+            data["results"].append({"node": int(m.group(1)), "dof": "temp",
+                                    "value": float(m.group(2)), "tol": float(m.group(3))})
+    tsi = {}
+    for line in s["TSI DYNAMIC"]:
+        tok = line.split()
+        if tok[0] in ("TIMESTEP", "NUMSTEP", "MAXTIME", "COUPALGO"):
+            tsi[tok[0]] = tok[1]
+    data["tsi_dynamic"] = tsi
+    thr = {}
+    for line in s["THERMAL DYNAMIC"]:
+        tok = line.split()
+        if tok[0] in ("DYNAMICTYPE", "INITIALFIELD", "INITFUNCNO"):
+            thr[tok[0]] = tok[1]
+    data["thermal_dynamic"] = thr
+    return data
+
+
 def main():
     if not os.path.isdir(REF):
         sys.exit("reference tree not present; fixtures are committed, nothing to do")
     for fname in ("solid_ele_hex8_Standard_linear.dat", "solid_ele_hex27_Standard_linear.dat",
                   "sohex27_patchtest_nl_cost_drt.dat"):
         data = extract(fname)
+        out = os.path.join(HERE, fname.replace(".dat", ".json"))
+        with open(out, "w") as f:
+            json.dump(data, f, indent=1, sort_keys=True)
+        print("wrote", out, len(data["nodes"]), "nodes", len(data["results"]), "results")
+    for fname in ("tsi_heatflux_monolithic.dat", "tsi_heatflux_flexoutsurf_monolithic.dat"):
+        data = extract_tsi(fname)
         out = os.path.join(HERE, fname.replace(".dat", ".json"))
         with open(out, "w") as f:
             json.dump(data, f, indent=1, sort_keys=True)

@@ -67,6 +67,11 @@ def load(path=None):
         ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int64, _i64p,
         ctypes.c_int64, _dp, _i64p, _i32p, ctypes.c_int64, ctypes.c_int, _dp,
         ctypes.POINTER(OrcCsr), _dp, _i64p]
+    lib.orc_thermo_stvk_st_modulus.argtypes = [ctypes.c_double] * 3
+    lib.orc_thermo_stvk_st_modulus.restype = ctypes.c_double
+    lib.orc_tsi_solid_evaluate.argtypes = [ctypes.c_int] + [ctypes.c_double] * 4 + [_dp] * 6
+    lib.orc_tsi_thermo_evaluate.argtypes = ([ctypes.c_int] + [ctypes.c_double] * 2 + [_dp] * 3 +
+                                            [ctypes.c_double] * 2 + [_dp] * 3)
     if path is None:
         _lib = lib
     return lib
@@ -164,3 +169,35 @@ def box_section(interval, nproc, rank):
     if lib.orc_box_section(ptr(iv, _i32p), nproc, rank, ptr(r, _i32p)) != 0:
         raise ValueError("cannot split nproc")
     return r
+
+
+def st_modulus(E, nu, alpha):
+    return load().orc_thermo_stvk_st_modulus(E, nu, alpha)
+
+
+def tsi_solid_evaluate(celltype, E, nu, alpha, T0, X, u, T, want=("K", "f", "Kst")):
+    """SOLIDSCATRA + ThermoStVenantKirchhoff (linear): returns (err, Ke, fe, Kst (3n x n))."""
+    lib = load()
+    n = 8 if celltype == HEX8 else 27
+    X = np.ascontiguousarray(X, dtype=np.float64).reshape(n, 3)
+    u = np.ascontiguousarray(u, dtype=np.float64).reshape(n, 3)
+    T = np.ascontiguousarray(T, dtype=np.float64).reshape(n)
+    Ke, fe, Kst = np.zeros(9 * n * n), np.zeros(3 * n), np.zeros(3 * n * n)
+    err = lib.orc_tsi_solid_evaluate(celltype, E, nu, alpha, T0, ptr(X, _dp), ptr(u, _dp), ptr(T, _dp),
+                                     ptr(Ke, _dp) if "K" in want else None,
+                                     ptr(fe, _dp) if "f" in want else None,
+                                     ptr(Kst, _dp) if "Kst" in want else None)
+    return err, Ke.reshape(3 * n, 3 * n).T.copy(), fe, Kst.reshape(n, 3 * n).T.copy()
+
+
+def tsi_thermo_evaluate(celltype, conduct, m, X, T, v, timefac, timefac_d):
+    """Thermo element, geometrically linear TSI: returns (err, Ktt (n x n), fT (n), Kts (n x 3n))."""
+    lib = load()
+    n = 8 if celltype == HEX8 else 27
+    X = np.ascontiguousarray(X, dtype=np.float64).reshape(n, 3)
+    T = np.ascontiguousarray(T, dtype=np.float64).reshape(n)
+    v = np.ascontiguousarray(v, dtype=np.float64).reshape(n, 3)
+    Ktt, fT, Kts = np.zeros(n * n), np.zeros(n), np.zeros(3 * n * n)
+    err = lib.orc_tsi_thermo_evaluate(celltype, conduct, m, ptr(X, _dp), ptr(T, _dp), ptr(v, _dp),
+                                      timefac, timefac_d, ptr(Ktt, _dp), ptr(fT, _dp), ptr(Kts, _dp))
+    return err, Ktt.reshape(n, n).T.copy(), fT, Kts.reshape(3 * n, n).T.copy()

@@ -7,6 +7,8 @@ tests/golden/make_fixtures.py or quoted below with their file:line):
   * tests/input_files/solid_ele_hex8_Standard_linear.dat  RESULT DESCRIPTION (1e-12)
   * tests/input_files/solid_ele_hex27_Standard_linear.dat RESULT DESCRIPTION (1e-12)
   * tests/input_files/sohex27_patchtest_nl_cost_drt.dat   RESULT DESCRIPTION (1e-9)
+  * tests/input_files/tsi_heatflux_monolithic.dat         RESULT DESCRIPTION (1e-9 disp, 1e-6 temp)
+  * tests/input_files/tsi_heatflux_flexoutsurf_monolithic.dat RESULT DESCRIPTION (1e-8)
 The result-test comparison is absolute (4C_utils_result_test.cpp:98).
 """
 
@@ -18,6 +20,7 @@ import pytest
 
 import oracle_lib as orc
 from fe_driver import Problem
+from tsi_driver import TsiProblem
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -147,3 +150,53 @@ def test_result_description(name):
     for r in fx["results"]:
         got = prob.disp(u, r["node"], r["dof"])
         assert abs(got - r["value"]) <= r["tol"], (r, got)
+
+
+# --------------------------------------------------------------------------- TSI (config 5)
+@pytest.mark.parametrize("name", ["tsi_heatflux_monolithic.json",
+                                  "tsi_heatflux_flexoutsurf_monolithic.json"])
+def test_tsi_result_description(name):
+    """Static monolithic TSI (both fields statics, KINEM linear, ThermoStVenantKirchhoff + Fourier)
+    through the oracle's SOLIDSCATRA and thermo element restatements."""
+    fx = load_fixture(name)
+    prob = TsiProblem(fx)
+    d, T = prob.solve()
+    for r in fx["results"]:
+        got = prob.result(d, T, r)
+        assert abs(got - r["value"]) <= r["tol"], (r, got)
+
+
+@pytest.mark.parametrize("celltype", [orc.HEX8, orc.HEX27])
+def test_tsi_tangent_blocks_are_derivatives(celltype):
+    """k_ST = d f_S / dT, k_TT = d f_T / dT and k_TS = (1/dt) d f_T / dV by central differences on a
+    distorted element (the blocks the GPU kernels reproduce)."""
+    rng = np.random.default_rng(5)
+    n = 8 if celltype == orc.HEX8 else 27
+    X = orc.node_param_coords(celltype) * np.array([1.0, 0.7, 1.3]) + 0.05 * rng.standard_normal((n, 3))
+    u = 1e-3 * rng.standard_normal((n, 3))
+    T = 300.0 + 20.0 * rng.standard_normal(n)
+    v = 1e-2 * rng.standard_normal((n, 3))
+    E, nu, alpha, T0, k, dt = 210.0, 0.3, 1.2e-5, 293.0, 52.0, 0.5
+    m = orc.st_modulus(E, nu, alpha)
+    assert np.isclose(m, -(2 * E / (2 * (1 + nu)) + 3 * E * nu / ((1 + nu) * (1 - 2 * nu))) * alpha)
+    _, _, _, Kst = orc.tsi_solid_evaluate(celltype, E, nu, alpha, T0, X, u, T)
+    _, Ktt, _, Kts = orc.tsi_thermo_evaluate(celltype, k, m, X, T, v, 1.0, 1.0 / dt)
+    h = 1e-3
+    for j in range(n):
+        e = np.zeros(n)
+        e[j] = h
+        fp = orc.tsi_solid_evaluate(celltype, E, nu, alpha, T0, X, u, T + e)[2]
+        fm = orc.tsi_solid_evaluate(celltype, E, nu, alpha, T0, X, u, T - e)[2]
+        np.testing.assert_allclose(Kst[:, j], (fp - fm) / (2 * h), rtol=1e-7, atol=1e-9 * abs(Kst).max())
+        gp = orc.tsi_thermo_evaluate(celltype, k, m, X, T + e, v, 1.0, 1.0 / dt)[2]
+        gm = orc.tsi_thermo_evaluate(celltype, k, m, X, T - e, v, 1.0, 1.0 / dt)[2]
+        np.testing.assert_allclose(Ktt[:, j], (gp - gm) / (2 * h), rtol=1e-7, atol=1e-9 * abs(Ktt).max())
+    hv = 1e-4
+    for j in range(3 * n):
+        e = np.zeros(3 * n)
+        e[j] = hv
+        gp = orc.tsi_thermo_evaluate(celltype, k, m, X, T, v + e.reshape(n, 3), 1.0, 1.0 / dt)[2]
+        gm = orc.tsi_thermo_evaluate(celltype, k, m, X, T, v - e.reshape(n, 3), 1.0, 1.0 / dt)[2]
+        # f_T is linear in v: the difference quotient is exact up to the rounding of f_T
+        np.testing.assert_allclose(Kts[:, j], (gp - gm) / (2 * hv) / dt, rtol=1e-6,
+                                   atol=1e-6 * abs(Kts).max())
