@@ -18,6 +18,8 @@ LINEAR, TOTLAG = 0, 1
 CALC_NLNSTIFF, CALC_INTERNALFORCE = 0, 1
 ACCUMULATE, OVERWRITE = 0, 1
 PATH_AUTO, PATH_GENERAL, PATH_STRUCTURED = 0, 1, 2
+TSI_STRUCT_FORCE, TSI_STIFFTEMP, TSI_THERMO_FINTCOND, TSI_COUPLTANG = 1, 2, 4, 8
+TSI_ALL = 15
 ABI_VERSION = 1
 
 STATUS = {0: "FCG_OK", 1: "FCG_ERR_NODAL_DETJ", 2: "FCG_ERR_SINGULAR", 3: "FCG_ERR_ARG",
@@ -54,12 +56,30 @@ class FcgInfo(ctypes.Structure):
                 ("reserved", ctypes.c_int32)]
 
 
+class FcgTsiDesc(ctypes.Structure):
+    _fields_ = [("abi_version", ctypes.c_int32), ("celltype", ctypes.c_int32),
+                ("device", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("youngs", ctypes.c_double), ("poisson", ctypes.c_double),
+                ("thexpans", ctypes.c_double), ("inittemp", ctypes.c_double),
+                ("conduct", ctypes.c_double),
+                ("n_ele", ctypes.c_int64), ("n_node", ctypes.c_int64),
+                ("n_rows_s", ctypes.c_int64), ("n_cols_s", ctypes.c_int64),
+                ("n_rows_t", ctypes.c_int64), ("n_cols_t", ctypes.c_int64),
+                ("ele_nodes", _i32p), ("ele_gid", _i32p), ("node_x", _dp),
+                ("node_dof_col_s", _i32p), ("node_dof_row_s", _i32p),
+                ("node_dof_col_t", _i32p), ("node_dof_row_t", _i32p),
+                ("rowptr_st", _i64p), ("col_st", _i32p),
+                ("rowptr_ts", _i64p), ("col_ts", _i32p),
+                ("rowptr_tt", _i64p), ("col_tt", _i32p)]
+
+
 # every symbol declared in include/fourc_gpu.h
 EXPORTS = ["fcg_create", "fcg_destroy", "fcg_last_error", "fcg_evaluate", "fcg_evaluate_device",
            "fcg_device_alloc", "fcg_device_free", "fcg_memcpy_h2d", "fcg_memcpy_d2h",
            "fcg_memset_device", "fcg_set_timing", "fcg_get_timing", "fcg_get_info",
            "fcg_get_diagnostics", "fcg_spmv", "fcg_dirichlet_apply", "fcg_pcg_solve",
            "fcg_neumann_surface", "fcg_neumann_volume",
+           "fcg_tsi_create", "fcg_tsi_destroy", "fcg_tsi_last_error", "fcg_tsi_evaluate_device",
            "fcg_box_mesh_create", "fcg_box_mesh_destroy", "fcg_box_mesh_desc", "fcg_box_mesh_maps",
            "fcg_box_mesh_counts"]
 
@@ -114,6 +134,12 @@ def lib():
     L.fcg_box_mesh_maps.argtypes = [vp, ctypes.POINTER(_i32p), ctypes.POINTER(_i32p),
                                     ctypes.POINTER(_i64p), ctypes.POINTER(_i32p)]
     L.fcg_box_mesh_counts.argtypes = [vp, _i64p, _i64p]
+    L.fcg_tsi_create.argtypes = [ctypes.POINTER(FcgTsiDesc), ctypes.POINTER(vp)]
+    L.fcg_tsi_destroy.argtypes = [vp]
+    L.fcg_tsi_last_error.argtypes = [vp]
+    L.fcg_tsi_last_error.restype = ctypes.c_char_p
+    L.fcg_tsi_evaluate_device.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_double,
+                                          ctypes.c_double, vp, vp, vp, vp, vp, vp, _i32p]
     _lib = L
     return L
 
@@ -420,3 +446,96 @@ class Evaluator:
         a, b = ctypes.c_double(), ctypes.c_double()
         lib().fcg_get_timing(self._h, ctypes.byref(a), ctypes.byref(b))
         return a.value, b.value
+
+
+class TsiGraph:
+    """The thermo field of a rank for TSI: one temperature DOF per node of the cloned thermo
+    discretization (same nodes, elements and owners as the structure; thermo DOF GIDs follow the
+    structural ones, 4C_fem_dofset.cpp:628-632) and the Epetra graphs of k_ST, k_TS and k_TT.
+    Derived from the structural node graph of `mesh` (BoxMesh or Discretization), whose DOF
+    column LIDs are 3 per node in node order."""
+
+    def __init__(self, mesh):
+        nn = mesh.n_node
+        self.node_dof_col_t = np.ascontiguousarray(mesh.node_dof_col // 3, dtype=np.int32)
+        self.node_dof_row_t = np.ascontiguousarray(
+            np.where(mesh.node_dof_row >= 0, mesh.node_dof_row // 3, -1), dtype=np.int32)
+        self.n_rows_t = int(mesh.n_rows) // 3
+        self.n_cols_t = int(mesh.n_cols) // 3
+        assert len(self.node_dof_col_t) == nn
+        rp = np.asarray(mesh.rowptr, dtype=np.int64)
+        cl = np.asarray(mesh.col_lid)
+        starts = rp[0:-1:3]                     # first structural row of every owned node
+        nnb = (rp[1::3] - rp[0:-1:3]) // 3      # neighbour nodes of the row
+        tot = int(nnb.sum())
+        self.rowptr_tt = np.concatenate([[0], np.cumsum(nnb)]).astype(np.int64)
+        off = np.arange(tot, dtype=np.int64) - np.repeat(self.rowptr_tt[:-1], nnb)
+        self.col_tt = np.ascontiguousarray(cl[np.repeat(starts, nnb) + 3 * off] // 3, dtype=np.int32)
+        # k_ST: 3 rows per node with the node's thermo columns
+        n3 = np.repeat(nnb, 3)
+        self.rowptr_st = np.concatenate([[0], np.cumsum(n3)]).astype(np.int64)
+        src = np.repeat(np.repeat(self.rowptr_tt[:-1], 3), n3)
+        off3 = np.arange(int(n3.sum()), dtype=np.int64) - np.repeat(self.rowptr_st[:-1], n3)
+        self.col_st = np.ascontiguousarray(self.col_tt[src + off3], dtype=np.int32)
+        # k_TS: one row per node with the node's structural columns (= its structural row)
+        self.rowptr_ts = np.concatenate([[0], np.cumsum(3 * nnb)]).astype(np.int64)
+        off_ts = np.arange(3 * tot, dtype=np.int64) - np.repeat(self.rowptr_ts[:-1], 3 * nnb)
+        self.col_ts = np.ascontiguousarray(cl[np.repeat(starts, 3 * nnb) + off_ts], dtype=np.int32)
+        self.nnz_st, self.nnz_ts, self.nnz_tt = len(self.col_st), len(self.col_ts), len(self.col_tt)
+
+
+class TsiEvaluator:
+    """Device context (fcg_tsi_ctx) for the temperature-dependent TSI blocks of one rank."""
+
+    def __init__(self, mesh, youngs, poisson, thexpans, inittemp, conduct, device=0, graph=None):
+        L = lib()
+        self.mesh = mesh
+        self.graph = g = graph or TsiGraph(mesh)
+        d = FcgTsiDesc()
+        d.abi_version = ABI_VERSION
+        d.celltype = mesh.celltype
+        d.device = device
+        d.youngs, d.poisson, d.thexpans = youngs, poisson, thexpans
+        d.inittemp, d.conduct = inittemp, conduct
+        d.n_ele, d.n_node = mesh.n_ele, mesh.n_node
+        d.n_rows_s, d.n_cols_s = mesh.n_rows, mesh.n_cols
+        d.n_rows_t, d.n_cols_t = g.n_rows_t, g.n_cols_t
+        d.ele_nodes = _np_ptr(mesh.ele_nodes, _i32p)
+        d.ele_gid = _np_ptr(mesh.ele_gid, _i32p)
+        d.node_x = _np_ptr(mesh.node_x, _dp)
+        d.node_dof_col_s = _np_ptr(mesh.node_dof_col, _i32p)
+        d.node_dof_row_s = _np_ptr(mesh.node_dof_row, _i32p)
+        d.node_dof_col_t = _np_ptr(g.node_dof_col_t, _i32p)
+        d.node_dof_row_t = _np_ptr(g.node_dof_row_t, _i32p)
+        d.rowptr_st, d.col_st = _np_ptr(g.rowptr_st, _i64p), _np_ptr(g.col_st, _i32p)
+        d.rowptr_ts, d.col_ts = _np_ptr(g.rowptr_ts, _i64p), _np_ptr(g.col_ts, _i32p)
+        d.rowptr_tt, d.col_tt = _np_ptr(g.rowptr_tt, _i64p), _np_ptr(g.col_tt, _i32p)
+        self.device = device
+        h = ctypes.c_void_p()
+        rc = L.fcg_tsi_create(ctypes.byref(d), ctypes.byref(h))
+        if rc != 0:
+            raise FcgError(rc, L.fcg_tsi_last_error(None).decode())
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().fcg_tsi_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def evaluate_device(self, parts, mode, v_col, T_col, timefac=1.0, timefac_d=1.0, fs=None,
+                        Kst=None, fT=None, Ktt=None, Kts=None, stream=None):
+        """Tensors: float64 on this device (v_col / T_col in the structural / thermo column maps)."""
+        bad = ctypes.c_int32(-1)
+        s = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
+        rc = lib().fcg_tsi_evaluate_device(self._h, parts, mode, _tensor_ptr(v_col),
+                                           _tensor_ptr(T_col), float(timefac), float(timefac_d),
+                                           _tensor_ptr(fs), _tensor_ptr(Kst), _tensor_ptr(fT),
+                                           _tensor_ptr(Ktt), _tensor_ptr(Kts), s, ctypes.byref(bad))
+        if rc != 0:
+            raise FcgError(rc, lib().fcg_tsi_last_error(self._h).decode(), bad.value)

@@ -189,6 +189,74 @@ int fcg_neumann_volume(int celltype, int64_t n_ele, const int32_t* ele_nodes, co
     fcg_funct_fn fn, void* user, double time, double* fext_row);
 
 /* ------------------------------------------------------------------------------------------
+ * Thermo-structure interaction (TSI), geometrically linear: the temperature-dependent blocks of
+ * 4C's monolithic TSI system (TSI::Monolithic, src/tsi/4C_tsi_monolithic.cpp:982-1005, 1694-1869)
+ * for SOLIDSCATRA hex8/hex27 elements with MAT_Struct_ThermoStVenantK (constant Young's modulus)
+ * and the cloned thermo elements with MAT_Fourier (constant conductivity).  The structural block
+ * k_SS and the mechanical part of f_S come from fcg_evaluate_device on an fcg_ctx of the same
+ * discretization (linear kinematics: k_SS does not depend on T).
+ *   FCG_TSI_STRUCT_FORCE     f_S += thermal-stress part  sum fac B^T m (T - T0) (1,1,1,0,0,0)
+ *                            (struct_calc_nlnstiff with the temperature state,
+ *                             4C_solid_scatra_3D_ele_calc.cpp:272-403; 4C_mat_thermostvenantkirchhoff.cpp:141-174)
+ *   FCG_TSI_STIFFTEMP        k_ST  (struct_calc_stifftemp, 4C_solid_scatra_3D_ele_calc.cpp:405-490,
+ *                            AssembleStrategy(0, 1, k_st), 4C_tsi_monolithic.cpp:1724-1732)
+ *   FCG_TSI_THERMO_FINTCOND  k_TT and f_T (calc_thermo_fintcond, 4C_thermo_ele_impl.cpp:802-1043)
+ *   FCG_TSI_COUPLTANG        k_TS  (calc_thermo_coupltang, 4C_thermo_ele_impl.cpp:1046-1194)
+ * ---------------------------------------------------------------------------------------- */
+enum fcg_tsi_part {
+  FCG_TSI_STRUCT_FORCE = 1,
+  FCG_TSI_STIFFTEMP = 2,
+  FCG_TSI_THERMO_FINTCOND = 4,
+  FCG_TSI_COUPLTANG = 8
+};
+
+/* One rank's view of both fields.  The thermo discretization is the structure's clone (same
+ * nodes, elements and owners); a node's thermo DOF is owned iff its structural DOFs are.  The
+ * graphs are those of the Epetra_CrsMatrix blocks after FillComplete, columns in the matrix
+ * column maps = the DOF column maps (node_dof_col_s / node_dof_col_t). */
+typedef struct fcg_tsi_desc {
+  int32_t abi_version;         /* FCG_ABI_VERSION */
+  int32_t celltype;            /* FCG_HEX8 / FCG_HEX27 */
+  int32_t device;
+  int32_t reserved;
+  double youngs, poisson;      /* MAT_Struct_ThermoStVenantK YOUNG (constant), NUE */
+  double thexpans;             /* THEXPANS (alpha_T) */
+  double inittemp;             /* INITTEMP (reference temperature of the thermal stress) */
+  double conduct;              /* MAT_Fourier CONDUCT (isotropic, constant) */
+  int64_t n_ele, n_node;       /* column elements / column nodes */
+  int64_t n_rows_s, n_cols_s;  /* structural DOF row / column map sizes */
+  int64_t n_rows_t, n_cols_t;  /* thermo DOF row / column map sizes */
+  const int32_t* ele_nodes;    /* [n_ele][8 or 27] column-node ids, 4C node order */
+  const int32_t* ele_gid;      /* [n_ele] (error reporting); may be NULL */
+  const double* node_x;        /* [n_node][3] */
+  const int32_t* node_dof_col_s, * node_dof_row_s;  /* first structural DOF: column LID, row LID or -1 */
+  const int32_t* node_dof_col_t, * node_dof_row_t;  /* thermo DOF: column LID, row LID or -1 */
+  const int64_t* rowptr_st; const int32_t* col_st;  /* k_ST: structural rows, thermo columns */
+  const int64_t* rowptr_ts; const int32_t* col_ts;  /* k_TS: thermo rows, structural columns */
+  const int64_t* rowptr_tt; const int32_t* col_tt;  /* k_TT */
+} fcg_tsi_desc;
+
+typedef struct fcg_tsi_ctx fcg_tsi_ctx;
+int fcg_tsi_create(const fcg_tsi_desc* desc, fcg_tsi_ctx** out);
+int fcg_tsi_destroy(fcg_tsi_ctx* ctx);
+const char* fcg_tsi_last_error(const fcg_tsi_ctx* ctx);
+/*
+ * Device-resident evaluation of the requested parts (bitmask of fcg_tsi_part):
+ *   d_v_col   structural velocity, DOF column map (statics: (D_{n+1} - D_n)/dt,
+ *             TSI::Algorithm::calc_velocity); needed for FCG_TSI_THERMO_FINTCOND
+ *   d_T_col   temperature, thermo DOF column map
+ *   timefac, timefac_d   k_TS = -timefac timefac_d (...) (4C_thermo_ele_impl.cpp:1094-1132;
+ *                        statics: 1 and 1/dt)
+ *   mode      applies to k_ST, k_TS, k_TT and f_T (OVERWRITE = zero + assemble); f_S always `+=`
+ *             (its mechanical part comes from fcg_evaluate_device)
+ * Error codes as fcg_evaluate_device (FCG_ERR_NODAL_DETJ also for the thermo element's
+ * det J < 1e-16, 4C_thermo_ele_impl.cpp:2663-2664).
+ */
+int fcg_tsi_evaluate_device(fcg_tsi_ctx* ctx, int parts, int mode, const double* d_v_col,
+    const double* d_T_col, double timefac, double timefac_d, double* d_fs_row, double* d_Kst,
+    double* d_fT_row, double* d_Ktt, double* d_Kts, void* stream, int32_t* bad_ele_gid);
+
+/* ------------------------------------------------------------------------------------------
  * Structured-box discretization builder: a restatement of 4C's GridGenerator
  * (src/core/io/src/4C_io_gridgenerator.cpp:41-392), node ownership of Rebalance::build_graph
  * (src/core/rebalance/src/4C_rebalance_graph_based.cpp:159-215), DofSet numbering
