@@ -101,6 +101,12 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} not built: run `make -C 4c_amd` (no CPU fallback exists)")
+    # One HIP runtime per process: when torch supplies the device buffers, its libamdhip64 must be
+    # the one the library binds to, so torch is loaded first (same soname -> shared).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     vp = ctypes.c_void_p
     L.fcg_create.argtypes = [ctypes.POINTER(FcgDesc), ctypes.POINTER(vp)]
