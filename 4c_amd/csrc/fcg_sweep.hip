@@ -22,9 +22,12 @@
 // positions follow SparseMatrix::assemble (4C_linalg_sparsematrix.cpp:474-543, positions resolved
 // per node row by fcg_create), the residual LinAlg::assemble (4C_linalg_utils_sparse_algebra_assemble.cpp:72-92).
 //
-// Latency hiding: two workgroups per CU (LDS 53 KB linear / 79 KB TotLag) plus, inside a
-// workgroup, register prefetch of the next node plane (coordinates, displacements) and plane
-// record while the current layer computes.
+// Linear kinematics: f_int = K u exactly (E = B u, f = sum fac B^T C B u), so the residual rows are
+// summed from the finished blocks, f_A += K_AB u_B, and stage A needs neither strains nor stresses.
+//
+// Latency hiding: two workgroups per CU for linear kinematics (LDS 59 KB), one for TotLag
+// (85 KB), plus, inside a workgroup, register prefetch of the next node plane (coordinates,
+// displacements) and plane record while the current layer computes.
 #include <hip/hip_runtime.h>
 
 #include "fcg_hex8_element.hpp"
@@ -77,18 +80,18 @@ struct SweepArgs {
 template <int KIN>
 struct SweepShared {
   alignas(16) double nx[3 * 4 * NSLOT * 8 * 2];  // sqrt|fac| N_XYZ, see nx2i()
-  // TotLag: F (column-major) | S (Voigt) | c = fac / sqrt|fac|;  linear: c S (Voigt) | pad
-  double gp[8][NSLOT][KIN ? 16 : 6];
-  double node[2][NNODE][6];           // X | u of the 6 x 6 node columns, by plane parity
+  // TotLag: F (column-major) | S (Voigt) | c = fac / sqrt|fac|  (linear kinematics: unused)
+  double gp[KIN ? 8 : 1][KIN ? NSLOT : 1][16];
+  double node[3][NNODE][6];           // X | u of the 6 x 6 node columns, ring by plane mod 3
   uint32_t prec[3][PLANE_REC_WORDS];  // plane records, ring by plane mod 3
   double dN[8][8][3];
   double w8[8];
   uint32_t neg[NSLOT];  // bit g set: fac < 0 at Gauss point g
-  // lower-layer parts of the in-plane blocks (dz = 0) of node plane L+1, by plane parity (the
-  // D-side lane writes what the U-side lane of the next layer reads):
-  // [parity][column][in-plane neighbour (dy+1)*3 + dx+1][3x3]
-  double hold[2][TX * TY][9][9];
-  double fhold[2][TX * TY][3];  // residual parts, by plane parity
+  // lower-layer parts of the in-plane blocks (dz = 0) of node plane L+1: written by the D-side
+  // lane k + 8, read by the U-side lane k of the next layer in the same instruction that precedes
+  // the next write (LDS operations of a wavefront complete in order): one buffer suffices.
+  // [column][in-plane neighbour (dy+1)*3 + dx+1][3x3]
+  double hold[TX * TY][9][9];
 };
 
 __device__ inline int ring(int p) { return (p % 3 + 3) % 3; }
@@ -97,6 +100,7 @@ __device__ inline int ring(int p) { return (p % 3 + 3) % 3; }
 constexpr int kDppXor1 = 0xB1;        // quad_perm [1,0,3,2]
 constexpr int kDppXor2 = 0x4E;        // quad_perm [2,3,0,1]
 constexpr int kDppHalfMirror = 0x141;  // lane i <-> 7-i within 8
+constexpr int kDppRowRor8 = 0x128;     // lane i <- lane i+8 (mod 16) within a row of 16
 template <int CTRL>
 __device__ inline double dpp_f64(double v)
 {
@@ -118,7 +122,7 @@ __device__ inline void sweep_stage_a(SweepShared<KIN>& sh, const SweepArgs& A, i
   const double* nd[8];
 #pragma unroll
   for (int n = 0; n < 8; ++n)
-    nd[n] = sh.node[(L + node_oz(n)) & 1][(sy + node_oy(n)) * NXN + sx + node_ox(n)];
+    nd[n] = sh.node[ring(L + node_oz(n))][(sy + node_oy(n)) * NXN + sx + node_ox(n)];
   double J[9];
 #pragma unroll
   for (int q = 0; q < 9; ++q) J[q] = 0.0;
@@ -137,8 +141,8 @@ __device__ inline void sweep_stage_a(SweepShared<KIN>& sh, const SweepArgs& A, i
   // half the three edge vectors through the node and det J = det(edges) / 8 (same sign).
   {
     const int ox = node_ox(g), oy = node_oy(g), oz = node_oz(g);
-    const double* zl = sh.node[L & 1][0];
-    const double* zh = sh.node[(L + 1) & 1][0];
+    const double* zl = sh.node[ring(L)][0];
+    const double* zh = sh.node[ring(L + 1)][0];
     const double* pz = oz ? zh : zl;
     const int cxy = (sy + oy) * NXN + sx + ox;
     const double* o = pz + 6 * cxy;
@@ -184,19 +188,10 @@ __device__ inline void sweep_stage_a(SweepShared<KIN>& sh, const SweepArgs& A, i
     sh.nx[nx2i(0, g >> 1, s, n) + (g & 1)] = KIN == 0 ? n0 : ns * n0;
     sh.nx[nx2i(1, g >> 1, s, n) + (g & 1)] = KIN == 0 ? n1 : ns * n1;
     sh.nx[nx2i(2, g >> 1, s, n) + (g & 1)] = KIN == 0 ? n2 : ns * n2;
-    const double u0 = nd[n][3], u1 = nd[n][4], u2 = nd[n][5];
-    if (KIN == 0)
-    {
-      E[0] += n0 * u0;
-      E[1] += n1 * u1;
-      E[2] += n2 * u2;
-      E[3] += n1 * u0 + n0 * u1;
-      E[4] += n2 * u1 + n1 * u2;
-      E[5] += n2 * u0 + n0 * u2;
-    }
-    else
+    if (KIN == 1)
     {
       // hex8: F = x N_XYZ^T from current coordinates (calc_lib.hpp:585-595)
+      const double u0 = nd[n][3], u1 = nd[n][4], u2 = nd[n][5];
       const double q0 = nd[n][0] + u0, q1 = nd[n][1] + u1, q2 = nd[n][2] + u2;
       F[0] += q0 * n0; F[1] += q1 * n0; F[2] += q2 * n0;
       F[3] += q0 * n1; F[4] += q1 * n1; F[5] += q2 * n1;
@@ -222,28 +217,22 @@ __device__ inline void sweep_stage_a(SweepShared<KIN>& sh, const SweepArgs& A, i
     E[4] = C[7];
     E[5] = C[2];
   }
-  const StVK& m = A.mat;
-  double S[6];
-  S[0] = m.cdiag * E[0] + m.lambda * E[1] + m.lambda * E[2];
-  S[1] = m.lambda * E[0] + m.cdiag * E[1] + m.lambda * E[2];
-  S[2] = m.lambda * E[0] + m.lambda * E[1] + m.cdiag * E[2];
-  S[3] = m.mu * E[3];
-  S[4] = m.mu * E[4];
-  S[5] = m.mu * E[5];
-  double* P = sh.gp[g][s];
   if (KIN == 1)
   {
+    const StVK& m = A.mat;
+    double S[6];
+    S[0] = m.cdiag * E[0] + m.lambda * E[1] + m.lambda * E[2];
+    S[1] = m.lambda * E[0] + m.cdiag * E[1] + m.lambda * E[2];
+    S[2] = m.lambda * E[0] + m.lambda * E[1] + m.cdiag * E[2];
+    S[3] = m.mu * E[3];
+    S[4] = m.mu * E[4];
+    S[5] = m.mu * E[5];
+    double* P = sh.gp[KIN ? g : 0][KIN ? s : 0];
 #pragma unroll
     for (int q = 0; q < 9; ++q) P[q] = F[q];
 #pragma unroll
     for (int q = 0; q < 6; ++q) P[9 + q] = S[q];
     P[15] = cf;
-  }
-  else
-  {
-    // S was computed from sqrt|fac| E: c S = sign(fac) S(sqrt|fac| E)
-#pragma unroll
-    for (int q = 0; q < 6; ++q) P[q] = fac < 0.0 ? -S[q] : S[q];
   }
   if (valid && bad)
   {
@@ -445,8 +434,8 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
   // --- prologue: node planes kz0-1, kz0 and their records; prefetch plane kz0+1
   if (n_lane)
   {
-    sh.node[(kz0 - 1) & 1][ncol][ncomp] = load_node(kz0 - 1);
-    sh.node[kz0 & 1][ncol][ncomp] = load_node(kz0);
+    sh.node[ring(kz0 - 1)][ncol][ncomp] = load_node(kz0 - 1);
+    sh.node[ring(kz0)][ncol][ncomp] = load_node(kz0);
   }
   {
     uint32_t w[2];
@@ -459,6 +448,8 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
   uint32_t rec_nxt[2];
   load_rec(kz0 + 1, rec_nxt);
   int e_cur = load_elem(kz0 - 1);
+  for (int v = tid; v < TX * TY * 81; v += 256) (&sh.hold[0][0][0])[v] = 0.0;
+  double fkeep[3] = {0.0, 0.0, 0.0};  // lane k = 8: D-side residual part of plane L+1's rows
   __syncthreads();
 
   for (int L = kz0 - 1; L < kz1; ++L)
@@ -468,9 +459,8 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
     if (a_lane) sweep_stage_a<KIN>(sh, A, s, g, sx, sy, L, e_cur);
     __syncthreads();
     FCG_STAMP(0);
-    // commit plane L+2 (nodes into plane L's parity slot, record into plane L-1's ring slot),
-    // then prefetch plane L+3
-    if (n_lane) sh.node[(L + 2) & 1][ncol][ncomp] = node_nxt;
+    // commit plane L+2 (nodes and record into plane L-1's ring slot), then prefetch plane L+3
+    if (n_lane) sh.node[ring(L + 2)][ncol][ncomp] = node_nxt;
     store_rec(L + 2, rec_nxt);
     node_nxt = n_lane ? load_node(L + 3) : 0.0;
     load_rec(L + 3, rec_nxt);
@@ -479,23 +469,45 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
     const bool wl = L >= kz0, wl1 = L + 1 < kz1;
     const uint32_t* recL = sh.prec[ring(L)];
     const uint32_t* recL1 = sh.prec[ring(L + 1)];
-    if (WANT_K)
+    // linear kinematics: this lane's share of f_A = sum_B K_AB u_B for the row node A of its side
+    // (plane L + (k >> 3))
+    double fpart[3] = {0.0, 0.0, 0.0};
+    if (WANT_K || KIN == 0)
     {
-      // finished block t of this lane's column: hold it, or write it (plus the held part)
+      // finished block t of this lane's column (this layer's elements): hold it, or write it plus
+      // the part held by lane k + 8 (same role, D side) since the previous layer
       auto emit = [&](int act, int t, double* Kb) {
-        const int par = act == kActHold ? (L + 1) & 1 : L & 1;
-        double* h = sh.hold[par][c][t - 9];
-        if (act == kActHold)
+        if (KIN == 0)
         {
+          const int dx = t % 3 - 1, dy = (t / 3) % 3 - 1, dz = t / 9 - 1;
+          const double* ub = &sh.node[ring(L + (k >> 3) + dz)][(cy + 1 + dy) * NXN + cx + 1 + dx][3];
+          const double u0 = ub[0], u1 = ub[1], u2 = ub[2];
 #pragma unroll
-          for (int i = 0; i < 9; ++i) h[i] = Kb[i];
-          return;
+          for (int r = 0; r < 3; ++r) fpart[r] += Kb[3 * r] * u0 + Kb[3 * r + 1] * u1 + Kb[3 * r + 2] * u2;
         }
-        if (act == kActWriteLHold)
+        // in-plane blocks: every lane of the pair reads the held entry first, then the holder
+        // (D side) stores this layer's part and the U side adds the part held since last layer
+        if (act == kActHold || act == kActWriteLHold)
         {
+          double* h = sh.hold[c][t - 9];
+          double held[9];
 #pragma unroll
-          for (int i = 0; i < 9; ++i) Kb[i] = h[i] + Kb[i];
+          for (int i = 0; i < 9; ++i) held[i] = h[i];
+          // all reads issue before any write (the compiler must not sink the U side's reads into
+          // its branch behind the D side's writes; the LDS executes a wavefront's ops in order)
+          __asm__ volatile("" ::: "memory");
+          if (act == kActHold)
+          {
+#pragma unroll
+            for (int i = 0; i < 9; ++i) h[i] = Kb[i];
+          }
+          else
+          {
+#pragma unroll
+            for (int i = 0; i < 9; ++i) Kb[i] = held[i] + Kb[i];
+          }
         }
+        if (act == kActHold || !WANT_K) return;
         const bool to_l1 = act == kActWriteL1;
         if (!(to_l1 ? wl1 : wl)) return;
         const uint32_t* rec = to_l1 ? recL1 : recL;
@@ -520,6 +532,7 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
       double acc1[NACC], acc2[NACC];
 #pragma unroll
       for (int i = 0; i < NACC; ++i) acc1[i] = acc2[i] = 0.0;
+      // the two element visits of this lane; acc2 is finished after a visit when flush2 is set
 #pragma unroll 1
       for (int v = 0; v < 2; ++v)
       {
@@ -554,53 +567,57 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
         if (pair != kPairGive) emit(int((vis1 >> 21) & 7), int((vis1 >> 11) & 31), Kb);
       }
     }
-    // nodal forces f_A = sum_e sum_g fac F S N_XYZ_A: lane k takes Gauss points 4h..4h+3
-    // (h = k & 1) of quadrant q = (k >> 1) & 3 for the row node on side k >> 3 (0: plane L, the
-    // elements' bottom node; 1: plane L+1, their top node); the 8 lanes of a side then sum by a
-    // butterfly (every lane ends with the same bits).  Lane 8 keeps plane L+1's part for the next
-    // layer, lane 0 completes and writes plane L's rows.
+    // residual rows of the column: the 8 lanes of a side sum their parts by a butterfly (every
+    // lane ends with the same bits); lane 8 keeps plane L+1's D-side part for the next layer, lane
+    // 0 adds the part lane 8 kept in the previous layer and writes plane L's rows.
     {
-      const int fside = k >> 3, fq = (k >> 1) & 3, fh = k & 1;
-      const int fqx = fq & 1, fqy = fq >> 1;
-      const int fslot = (cx + fqx) + EXN * (cy + fqy);
-      const int fn = node_at(1 - fqx, 1 - fqy, fside);
-      double f[3] = {0.0, 0.0, 0.0};
-#pragma unroll
-      for (int gg = 0; gg < 4; ++gg)
+      double f[3];
+      if (KIN == 0)
       {
-        const int gq = 4 * fh + gg;
-        const double a0 = sh.nx[nx2i(0, gq >> 1, fslot, fn) + (gq & 1)],
-                     a1 = sh.nx[nx2i(1, gq >> 1, fslot, fn) + (gq & 1)],
-                     a2 = sh.nx[nx2i(2, gq >> 1, fslot, fn) + (gq & 1)];
-        const double* P = sh.gp[gq][fslot];
-        if (KIN == 0)
+#pragma unroll
+        for (int d = 0; d < 3; ++d) f[d] = fpart[d];
+      }
+      else
+      {
+        // f_A = sum_e sum_g fac F S N_XYZ_A: lane k takes Gauss points 4h..4h+3 (h = k & 1) of
+        // quadrant q = (k >> 1) & 3 for the row node on side k >> 3 (0: plane L, the elements'
+        // bottom node; 1: plane L+1, their top node)
+        const int fside = k >> 3, fq = (k >> 1) & 3, fh = k & 1;
+        const int fqx = fq & 1, fqy = fq >> 1;
+        const int fslot = (cx + fqx) + EXN * (cy + fqy);
+        const int fn = node_at(1 - fqx, 1 - fqy, fside);
+#pragma unroll
+        for (int d = 0; d < 3; ++d) f[d] = 0.0;
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg)
         {
-          f[0] += P[0] * a0 + P[3] * a1 + P[5] * a2;
-          f[1] += P[3] * a0 + P[1] * a1 + P[4] * a2;
-          f[2] += P[5] * a0 + P[4] * a1 + P[2] * a2;
-        }
-        else
-        {
+          const int gq = 4 * fh + gg;
+          const double a0 = sh.nx[nx2i(0, gq >> 1, fslot, fn) + (gq & 1)],
+                       a1 = sh.nx[nx2i(1, gq >> 1, fslot, fn) + (gq & 1)],
+                       a2 = sh.nx[nx2i(2, gq >> 1, fslot, fn) + (gq & 1)];
+          const double* P = sh.gp[KIN ? gq : 0][KIN ? fslot : 0];
           const double t0 = P[9] * a0 + P[12] * a1 + P[14] * a2;
           const double t1 = P[12] * a0 + P[10] * a1 + P[13] * a2;
           const double t2 = P[14] * a0 + P[13] * a1 + P[11] * a2;
-          const double c = P[15];
-          f[0] += c * (P[0] * t0 + P[3] * t1 + P[6] * t2);
-          f[1] += c * (P[1] * t0 + P[4] * t1 + P[7] * t2);
-          f[2] += c * (P[2] * t0 + P[5] * t1 + P[8] * t2);
+          const double cc = P[15];
+          f[0] += cc * (P[0] * t0 + P[3] * t1 + P[6] * t2);
+          f[1] += cc * (P[1] * t0 + P[4] * t1 + P[7] * t2);
+          f[2] += cc * (P[2] * t0 + P[5] * t1 + P[8] * t2);
         }
       }
+      double fp[3];
 #pragma unroll
       for (int d = 0; d < 3; ++d)
       {
         f[d] += dpp_f64<kDppXor1>(f[d]);
         f[d] += dpp_f64<kDppXor2>(f[d]);
         f[d] += dpp_f64<kDppHalfMirror>(f[d]);
+        fp[d] = dpp_f64<kDppRowRor8>(fkeep[d]);
       }
       if (k == 8)
       {
 #pragma unroll
-        for (int d = 0; d < 3; ++d) sh.fhold[(L + 1) & 1][c][d] = f[d];
+        for (int d = 0; d < 3; ++d) fkeep[d] = f[d];
       }
       else if (k == 0 && wl)
       {
@@ -611,9 +628,9 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
           for (int d = 0; d < 3; ++d)
           {
             if (OVERWRITE)
-              A.fint[row0 + d] = sh.fhold[L & 1][c][d] + f[d];
+              A.fint[row0 + d] = fp[d] + f[d];
             else
-              A.fint[row0 + d] += sh.fhold[L & 1][c][d] + f[d];
+              A.fint[row0 + d] += fp[d] + f[d];
           }
         }
       }
