@@ -79,6 +79,7 @@ EXPORTS = ["fcg_create", "fcg_destroy", "fcg_last_error", "fcg_evaluate", "fcg_e
            "fcg_memset_device", "fcg_set_timing", "fcg_get_timing", "fcg_get_info",
            "fcg_get_diagnostics", "fcg_spmv", "fcg_dirichlet_apply", "fcg_pcg_solve",
            "fcg_neumann_surface", "fcg_neumann_volume",
+           "fcg_graph_build_device",
            "fcg_tsi_create", "fcg_tsi_destroy", "fcg_tsi_last_error", "fcg_tsi_evaluate_device",
            "fcg_box_mesh_create", "fcg_box_mesh_destroy", "fcg_box_mesh_desc", "fcg_box_mesh_maps",
            "fcg_box_mesh_counts"]
@@ -140,6 +141,9 @@ def lib():
     L.fcg_box_mesh_maps.argtypes = [vp, ctypes.POINTER(_i32p), ctypes.POINTER(_i32p),
                                     ctypes.POINTER(_i64p), ctypes.POINTER(_i32p)]
     L.fcg_box_mesh_counts.argtypes = [vp, _i64p, _i64p]
+    L.fcg_graph_build_device.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64, vp,
+                                         ctypes.c_int64, vp, vp, ctypes.c_int64, vp, vp,
+                                         ctypes.c_int64, _i64p, vp]
     L.fcg_tsi_create.argtypes = [ctypes.POINTER(FcgTsiDesc), ctypes.POINTER(vp)]
     L.fcg_tsi_destroy.argtypes = [vp]
     L.fcg_tsi_last_error.argtypes = [vp]
@@ -545,3 +549,25 @@ class TsiEvaluator:
                                            _tensor_ptr(Ktt), _tensor_ptr(Kts), s, ctypes.byref(bad))
         if rc != 0:
             raise FcgError(rc, lib().fcg_tsi_last_error(self._h).decode(), bad.value)
+
+
+def graph_build_device(celltype, ele_nodes, node_dof_col, node_dof_row, n_rows, device=0,
+                       stream=None):
+    """fcg_graph_build_device on torch tensors (int32, on `device`): returns (rowptr int64,
+    col_lid int32) device tensors -- the FillComplete graph of the rank's owned rows."""
+    import torch
+    dev = torch.device("cuda", device)
+    rowptr = torch.empty(int(n_rows) + 1, dtype=torch.int64, device=dev)
+    nnz = ctypes.c_int64(0)
+    s = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
+    args = (device, celltype, int(ele_nodes.numel() // (8 if celltype == HEX8 else 27)),
+            _tensor_ptr(ele_nodes), int(node_dof_col.numel()), _tensor_ptr(node_dof_col),
+            _tensor_ptr(node_dof_row), int(n_rows), _tensor_ptr(rowptr))
+    rc = lib().fcg_graph_build_device(*args, None, 0, ctypes.byref(nnz), s)
+    if rc != 0:
+        raise FcgError(rc, "fcg_graph_build_device (sizing) failed")
+    col = torch.empty(max(1, nnz.value), dtype=torch.int32, device=dev)
+    rc = lib().fcg_graph_build_device(*args, _tensor_ptr(col), nnz.value, ctypes.byref(nnz), s)
+    if rc != 0:
+        raise FcgError(rc, "fcg_graph_build_device failed")
+    return rowptr, col[:nnz.value]

@@ -189,6 +189,20 @@ int fcg_neumann_volume(int celltype, int64_t n_ele, const int32_t* ele_nodes, co
     fcg_funct_fn fn, void* user, double time, double* fext_row);
 
 /* ------------------------------------------------------------------------------------------
+ * The matrix graph on the device: what Epetra_CrsMatrix::FillComplete produces
+ * after 4C's first assembly through the unfilled path (4C_linalg_sparsematrix.cpp:578-611,
+ * 843-865): one row per owned DOF, columns = the DOFs of every node sharing an element with the
+ * row's node, sorted by column LID.  All arrays are device memory:
+ *   d_ele_nodes [n_ele][8|27] column-node ids; d_node_dof_col [n_node] column LID of the node's
+ *   first DOF; d_node_dof_row [n_node] row LID (a multiple of 3) or -1; n_rows = 3 x owned nodes.
+ * Fills d_rowptr [n_rows + 1] and *nnz; writes d_col_lid only when it is non-NULL and
+ * col_capacity >= *nnz (call once to size, allocate, call again).  At most 16 elements per node.
+ * ---------------------------------------------------------------------------------------- */
+int fcg_graph_build_device(int device, int celltype, int64_t n_ele, const int32_t* d_ele_nodes,
+    int64_t n_node, const int32_t* d_node_dof_col, const int32_t* d_node_dof_row, int64_t n_rows,
+    int64_t* d_rowptr, int32_t* d_col_lid, int64_t col_capacity, int64_t* nnz, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Thermo-structure interaction (TSI), geometrically linear: the temperature-dependent blocks of
  * 4C's monolithic TSI system (TSI::Monolithic, src/tsi/4C_tsi_monolithic.cpp:982-1005, 1694-1869)
  * for SOLIDSCATRA hex8/hex27 elements with MAT_Struct_ThermoStVenantK (constant Young's modulus)
