@@ -375,6 +375,129 @@ double orc_stvk_strain_energy(double E, double nu, const double* glstrain)
 }
 
 /* ---------------------------------------------------------------------------------------
+ * Mat::ElastHyper with one ELAST_CoupNeoHooke summand (isotropic, principal invariants):
+ * elast_hyper_evaluate (4C_mat_elasthyper_service.cpp:19-78) -> right Cauchy-Green (:80-88),
+ * Voigt inverse / principal invariants (4C_linalg_fixedsizematrix_voigt_notation.hpp:76-101,
+ * .cpp:188-207), CoupNeoHooke::add_derivatives_principal (4C_mat_elast_coupneohooke.cpp),
+ * calculate_gamma_delta (:413-432), elast_hyper_add_isotropic_stress_cmat (:162-215) with
+ * add_holzapfel_product (4C_linalg_fixedsizematrix_tensor_products.cpp:264-312).
+ * Strain-like Voigt vectors carry doubled shears; stress-like ones do not.
+ * ------------------------------------------------------------------------------------- */
+static const double voigt_unscale_strain[6] = {1.0, 1.0, 1.0, 0.5, 0.5, 0.5};
+static const double voigt_scale_strain[6] = {1.0, 1.0, 1.0, 2.0, 2.0, 2.0};
+
+static double voigt_triple(const double* v, int i, int j, int k)
+{
+  return v[i] * voigt_unscale_strain[i] * v[j] * voigt_unscale_strain[j] * v[k] *
+         voigt_unscale_strain[k];
+}
+
+static double voigt_det_strain(const double* v)
+{
+  return voigt_triple(v, 0, 1, 2) + 2 * voigt_triple(v, 3, 4, 5) - voigt_triple(v, 1, 5, 5) -
+         voigt_triple(v, 2, 3, 3) - voigt_triple(v, 0, 4, 4);
+}
+
+void orc_elasthyper_coupneohooke(double E, double nu, const double* glstrain, double* stress,
+    double* cmat)
+{
+  const double* us = voigt_unscale_strain;
+  const double* sc = voigt_scale_strain;
+  /* Mat::Elastic::PAR::CoupNeoHooke: c = E / (4 (1 + nu)), beta = nu / (1 - 2 nu) */
+  const double c = E / (4.0 * (1.0 + nu));
+  const double beta = nu / (1.0 - 2.0 * nu);
+  const double id2[6] = {1.0, 1.0, 1.0, 0.0, 0.0, 0.0};
+  double C[6], iC[6], prinv[3], dPI[3] = {0, 0, 0}, ddPII[6] = {0, 0, 0, 0, 0, 0};
+  /* C = 2 E + I (strain-like) */
+  for (int i = 0; i < 6; ++i) C[i] = 2.0 * glstrain[i];
+  for (int i = 0; i < 3; ++i) C[i] += 1.0;
+  /* VoigtUtils<strain>::inverse_tensor */
+  const double det = voigt_det_strain(C);
+  iC[0] = (C[1] * C[2] - us[4] * us[4] * C[4] * C[4]) / det * sc[0];
+  iC[1] = (C[0] * C[2] - us[5] * us[5] * C[5] * C[5]) / det * sc[1];
+  iC[2] = (C[0] * C[1] - us[3] * us[3] * C[3] * C[3]) / det * sc[2];
+  iC[3] = (us[5] * us[4] * C[5] * C[4] - us[3] * us[2] * C[3] * C[2]) / det * sc[3];
+  iC[4] = (us[3] * us[5] * C[3] * C[5] - us[0] * us[4] * C[0] * C[4]) / det * sc[4];
+  iC[5] = (us[3] * us[4] * C[3] * C[4] - us[5] * us[1] * C[5] * C[1]) / det * sc[5];
+  /* invariants_principal */
+  prinv[0] = C[0] + C[1] + C[2];
+  prinv[1] = 0.5 * (prinv[0] * prinv[0] - C[0] * C[0] - C[1] * C[1] - C[2] * C[2]) -
+             C[3] * C[3] * us[3] * us[3] - C[4] * C[4] * us[4] * us[4] - C[5] * C[5] * us[5] * us[5];
+  prinv[2] = voigt_det_strain(C);
+  /* CoupNeoHooke::add_derivatives_principal */
+  dPI[0] += c;
+  if (prinv[2] > 0)
+  {
+    const double p = exp(log(prinv[2]) * (-beta - 1.));
+    dPI[2] -= c * p;
+    ddPII[2] += c * (beta + 1.) * p / prinv[2];
+  }
+  else
+    dPI[2] = ddPII[2] = NAN;
+  /* calculate_gamma_delta (Holzapfel p. 216, 261) */
+  double gamma[3], delta[8];
+  gamma[0] = 2. * (dPI[0] + prinv[0] * dPI[1]);
+  gamma[1] = -2. * dPI[1];
+  gamma[2] = 2. * prinv[2] * dPI[2];
+  delta[0] = 4. * (ddPII[0] + 2. * prinv[0] * ddPII[5] + dPI[1] + prinv[0] * prinv[0] * ddPII[1]);
+  delta[1] = -4. * (ddPII[5] + prinv[0] * ddPII[1]);
+  delta[2] = 4. * (prinv[2] * ddPII[4] + prinv[0] * prinv[2] * ddPII[3]);
+  delta[3] = 4. * ddPII[1];
+  delta[4] = -4. * prinv[2] * ddPII[3];
+  delta[5] = 4. * (prinv[2] * dPI[2] + prinv[2] * prinv[2] * ddPII[2]);
+  delta[6] = -4. * prinv[2] * dPI[2];
+  delta[7] = -4. * dPI[1];
+  /* stress-like C and C^-1 */
+  double Cs[6], iCs[6];
+  for (int i = 0; i < 6; ++i)
+  {
+    Cs[i] = us[i] * C[i];
+    iCs[i] = us[i] * iC[i];
+  }
+  for (int i = 0; i < 6; ++i) stress[i] = 0.0;
+  for (int i = 0; i < 36; ++i) cmat[i] = 0.0;
+  for (int i = 0; i < 6; ++i) stress[i] = 1.0 * stress[i] + gamma[0] * id2[i];
+  for (int i = 0; i < 6; ++i) stress[i] = 1.0 * stress[i] + gamma[1] * Cs[i];
+  for (int i = 0; i < 6; ++i) stress[i] = 1.0 * stress[i] + gamma[2] * iCs[i];
+  mm_nt(cmat, 1.0, delta[0], id2, id2, 6, 1, 6, 1);
+  mm_nt(cmat, 1.0, delta[1], id2, Cs, 6, 1, 6, 1);
+  mm_nt(cmat, 1.0, delta[1], Cs, id2, 6, 1, 6, 1);
+  mm_nt(cmat, 1.0, delta[2], id2, iCs, 6, 1, 6, 1);
+  mm_nt(cmat, 1.0, delta[2], iCs, id2, 6, 1, 6, 1);
+  mm_nt(cmat, 1.0, delta[3], Cs, Cs, 6, 1, 6, 1);
+  mm_nt(cmat, 1.0, delta[4], Cs, iCs, 6, 1, 6, 1);
+  mm_nt(cmat, 1.0, delta[4], iCs, Cs, 6, 1, 6, 1);
+  mm_nt(cmat, 1.0, delta[5], iCs, iCs, 6, 1, 6, 1);
+  /* add_holzapfel_product(cmat, iC_stress, delta[6]) */
+  {
+    const double* v = iCs;
+    const double sc6 = delta[6];
+#define CM(i, j) cmat[(i) + 6 * (j)]
+    CM(0, 0) += sc6 * v[0] * v[0]; CM(0, 1) += sc6 * v[3] * v[3]; CM(0, 2) += sc6 * v[5] * v[5];
+    CM(0, 3) += sc6 * v[0] * v[3]; CM(0, 4) += sc6 * v[3] * v[5]; CM(0, 5) += sc6 * v[0] * v[5];
+    CM(1, 0) += sc6 * v[3] * v[3]; CM(1, 1) += sc6 * v[1] * v[1]; CM(1, 2) += sc6 * v[4] * v[4];
+    CM(1, 3) += sc6 * v[3] * v[1]; CM(1, 4) += sc6 * v[1] * v[4]; CM(1, 5) += sc6 * v[3] * v[4];
+    CM(2, 0) += sc6 * v[5] * v[5]; CM(2, 1) += sc6 * v[4] * v[4]; CM(2, 2) += sc6 * v[2] * v[2];
+    CM(2, 3) += sc6 * v[5] * v[4]; CM(2, 4) += sc6 * v[4] * v[2]; CM(2, 5) += sc6 * v[5] * v[2];
+    CM(3, 0) += sc6 * v[0] * v[3]; CM(3, 1) += sc6 * v[3] * v[1]; CM(3, 2) += sc6 * v[5] * v[4];
+    CM(3, 3) += sc6 * 0.5 * (v[0] * v[1] + v[3] * v[3]);
+    CM(3, 4) += sc6 * 0.5 * (v[3] * v[4] + v[5] * v[1]);
+    CM(3, 5) += sc6 * 0.5 * (v[0] * v[4] + v[5] * v[3]);
+    CM(4, 0) += sc6 * v[3] * v[5]; CM(4, 1) += sc6 * v[1] * v[4]; CM(4, 2) += sc6 * v[4] * v[2];
+    CM(4, 3) += sc6 * 0.5 * (v[3] * v[4] + v[5] * v[1]);
+    CM(4, 4) += sc6 * 0.5 * (v[1] * v[2] + v[4] * v[4]);
+    CM(4, 5) += sc6 * 0.5 * (v[3] * v[2] + v[4] * v[5]);
+    CM(5, 0) += sc6 * v[0] * v[5]; CM(5, 1) += sc6 * v[3] * v[4]; CM(5, 2) += sc6 * v[5] * v[2];
+    CM(5, 3) += sc6 * 0.5 * (v[0] * v[4] + v[5] * v[3]);
+    CM(5, 4) += sc6 * 0.5 * (v[3] * v[2] + v[4] * v[5]);
+    CM(5, 5) += sc6 * 0.5 * (v[0] * v[2] + v[5] * v[5]);
+    /* cmat.update(delta[7], id4sharp<stress, stress>, 1.0): diag 1 (normal), 0.5 (shear) */
+    for (int i = 0; i < 6; ++i) CM(i, i) = 1.0 * CM(i, i) + delta[7] * (i < 3 ? 1.0 : 0.5);
+#undef CM
+  }
+}
+
+/* ---------------------------------------------------------------------------------------
  * Element evaluation: SolidEleCalc::evaluate_nonlinear_force_stiffness_mass
  * (4C_solid_3D_ele_calc.cpp:110-240) with the helpers of 4C_solid_3D_ele_calc_lib.hpp.
  * ------------------------------------------------------------------------------------- */
@@ -400,6 +523,13 @@ static int jacobian_mapping(int n, const double* dN, const double* X, jac_map* j
 int orc_solid_evaluate(int celltype, int kinem, double E, double nu, const double* X,
     const double* u, double* Ke, double* fe)
 {
+  return orc_solid_evaluate_mat(celltype, kinem, ORC_MAT_STVK, E, nu, X, u, Ke, fe);
+}
+
+int orc_solid_evaluate_mat(int celltype, int kinem, int material, double E, double nu,
+    const double* X, const double* u, double* Ke, double* fe)
+{
+  if (material != ORC_MAT_STVK && material != ORC_MAT_NEOHOOKE) return ORC_ERR_ARG;
   if (celltype != ORC_HEX8 && celltype != ORC_HEX27) return ORC_ERR_ARG;
   const int n = orc_num_nodes(celltype);
   const int ndof = 3 * n;
@@ -515,9 +645,13 @@ int orc_solid_evaluate(int celltype, int kinem, double E, double nu, const doubl
 #undef FF
     }
 
-    /* So3Material::evaluate -> StVK: S = C . E (4C_mat_stvenantkirchhoff.cpp:169-177) */
+    /* So3Material::evaluate -> StVK: S = C . E (4C_mat_stvenantkirchhoff.cpp:169-177), or
+     * ElastHyper/CoupNeoHooke (cmat and S from the principal invariants of C = 2E + I) */
     double pk2[6];
-    mm_nn(pk2, 0.0, 1.0, cmat, gl, 6, 6, 1, 0);
+    if (material == ORC_MAT_NEOHOOKE)
+      orc_elasthyper_coupneohooke(E, nu, gl, pk2, cmat);
+    else
+      mm_nn(pk2, 0.0, 1.0, cmat, gl, 6, 6, 1, 0);
 
     /* add_internal_force_vector (calc_lib.hpp:851-860): f += fac * B^T S */
     if (fe) mm_tn(fe, 1.0, fac, Bop, pk2, ndof, 6, 1, 1);
@@ -804,6 +938,15 @@ int orc_discretization_evaluate(int celltype, int kinem, double E, double nu, in
     const int32_t* node_owner, int64_t min_node_gid, int nworkers, const double* u, orc_csr* K,
     double* fint, int64_t* bad_ele)
 {
+  return orc_discretization_evaluate_mat(celltype, kinem, ORC_MAT_STVK, E, nu, n_ele, ele_nodes,
+      n_nodes, node_x, node_gid, node_owner, min_node_gid, nworkers, u, K, fint, bad_ele);
+}
+
+int orc_discretization_evaluate_mat(int celltype, int kinem, int material, double E, double nu,
+    int64_t n_ele, const int64_t* ele_nodes, int64_t n_nodes, const double* node_x,
+    const int64_t* node_gid, const int32_t* node_owner, int64_t min_node_gid, int nworkers,
+    const double* u, orc_csr* K, double* fint, int64_t* bad_ele)
+{
   const int n = orc_num_nodes(celltype);
   const int ndof = 3 * n;
   int result = 0;
@@ -850,7 +993,7 @@ int orc_discretization_evaluate(int celltype, int kinem, double E, double nu, in
       const int want_k = K->vals != NULL;
       if (want_k) memset(Ke, 0, sizeof(double) * ndof * ndof);
       memset(fe, 0, sizeof(fe));
-      int err = orc_solid_evaluate(celltype, kinem, E, nu, X, ue, want_k ? Ke : NULL, fe);
+      int err = orc_solid_evaluate_mat(celltype, kinem, material, E, nu, X, ue, want_k ? Ke : NULL, fe);
       if (err)
       {
 #pragma omp critical

@@ -28,6 +28,8 @@ extern "C" {
 enum { ORC_HEX8 = 0, ORC_HEX27 = 1 };
 enum { ORC_LINEAR = 0, ORC_TOTLAG = 1 };
 enum { ORC_OK = 0, ORC_ERR_NODAL_DETJ = 1, ORC_ERR_SINGULAR = 2, ORC_ERR_ARG = 3 };
+/* MAT_Struct_StVenantKirchhoff / MAT_ElastHyper with one ELAST_CoupNeoHooke summand */
+enum { ORC_MAT_STVK = 0, ORC_MAT_NEOHOOKE = 1 };
 
 int orc_num_nodes(int celltype);
 int orc_num_gp(int celltype);
@@ -50,6 +52,11 @@ void orc_stvk_cmat(double E, double nu, double* cmat);
 void orc_stvk_evaluate(double E, double nu, const double* glstrain, double* stress, double* cmat);
 double orc_stvk_strain_energy(double E, double nu, const double* glstrain);
 
+/* ElastHyper + CoupNeoHooke (YOUNG E, NUE nu): PK2 stress and cmat (column-major 6x6) at the
+ * Green-Lagrange strain (strain-like Voigt), 4C_mat_elasthyper_service.cpp:19-215. */
+void orc_elasthyper_coupneohooke(double E, double nu, const double* glstrain, double* stress,
+    double* cmat);
+
 /* SolidEleCalc<celltype, Formulation>::evaluate_nonlinear_force_stiffness_mass
  * (4C_solid_3D_ele_calc.cpp:110-240) for DisplacementBased(LinearKinematics)Formulation + StVK.
  * X, u: [n][3] reference coordinates and displacements (node-major as lm).
@@ -58,6 +65,9 @@ double orc_stvk_strain_energy(double E, double nu, const double* glstrain);
  * (invert3x3 det == 0, 4C_linalg_fixedsizematrix.hpp:1394). */
 int orc_solid_evaluate(int celltype, int kinem, double E, double nu, const double* X,
     const double* u, double* Ke, double* fe);
+/* The same with the material chosen by ORC_MAT_* (E, nu are the summand's YOUNG, NUE). */
+int orc_solid_evaluate_mat(int celltype, int kinem, int material, double E, double nu,
+    const double* X, const double* u, double* Ke, double* fe);
 
 /* GridGenerator restatement (4C_io_gridgenerator.cpp). */
 void orc_hex_element_nodeids(int celltype, int64_t eleid, const int32_t* interval,
@@ -99,6 +109,10 @@ int orc_discretization_evaluate(int celltype, int kinem, double E, double nu, in
     const int64_t* ele_nodes, int64_t n_nodes, const double* node_x, const int64_t* node_gid,
     const int32_t* node_owner, int64_t min_node_gid, int nworkers, const double* u, orc_csr* K,
     double* fint, int64_t* bad_ele);
+int orc_discretization_evaluate_mat(int celltype, int kinem, int material, double E, double nu,
+    int64_t n_ele, const int64_t* ele_nodes, int64_t n_nodes, const double* node_x,
+    const int64_t* node_gid, const int32_t* node_owner, int64_t min_node_gid, int nworkers,
+    const double* u, orc_csr* K, double* fint, int64_t* bad_ele);
 
 /* ---------------------------------------------------------------------------------------
  * Thermo-structure interaction, geometrically linear (BASELINE config 5).  Pinned against the

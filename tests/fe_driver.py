@@ -71,6 +71,8 @@ class Problem:
         self.ndof = 3 * len(self.node_ids)
         self.E = fx["material"]["young"]
         self.nu = fx["material"]["nue"]
+        self.material = (orc.MAT_NEOHOOKE if fx["material"].get("type") == "elasthyper_coupneohooke"
+                         else orc.MAT_STVK)
         self.functs = {int(k): make_function(v) for k, v in fx.get("functions", {}).items()}
 
     def element_dofs(self, el):
@@ -87,7 +89,8 @@ class Problem:
             kin = orc.LINEAR if el["kinem"] == "linear" else orc.TOTLAG
             idx = self.element_dofs(el)
             Xe = self.X[[self.lid[n] for n in el["nodes"]]]
-            err, Ke, fe = orc.solid_evaluate(ct, kin, self.E, self.nu, Xe, u[idx])
+            err, Ke, fe = orc.solid_evaluate(ct, kin, self.E, self.nu, Xe, u[idx],
+                                             material=self.material)
             assert err == 0, err
             K[np.ix_(idx, idx)] += Ke
             f[idx] += fe
@@ -155,18 +158,24 @@ class Problem:
                             fixed.add(3 * self.lid[n] + d)
         return np.array(sorted(fixed), dtype=np.int64)
 
-    def solve_statics(self, t=1.0, tol=1e-13, maxiter=50):
+    def solve_statics(self, t=1.0, tol=1e-13, maxiter=50, nsteps=1, assemble=None):
+        """Full Newton per load step at t_k = k t / nsteps (the reference's TIMESTEP sequence for
+        large deformations); `assemble(u) -> (K, fint)` defaults to the oracle."""
+        assemble = assemble or self.assemble
         u = np.zeros(self.ndof)
         fixed = self.dirichlet_dofs()
         free = np.setdiff1d(np.arange(self.ndof), fixed)
-        fe = self.fext(t)
-        for _ in range(maxiter):
-            K, fint = self.assemble(u)
-            r = fint - fe
-            du = np.linalg.solve(K[np.ix_(free, free)], -r[free])
-            u[free] += du
-            if np.linalg.norm(du) < tol:
-                break
+        for k in range(1, nsteps + 1):
+            fe = self.fext(t * k / nsteps)
+            for _ in range(maxiter):
+                K, fint = assemble(u)
+                r = fint - fe
+                du = np.linalg.solve(K[np.ix_(free, free)], -r[free])
+                u[free] += du
+                if np.linalg.norm(du) < tol * max(1.0, np.linalg.norm(u)):
+                    break
+            else:
+                raise RuntimeError(f"Newton did not converge in load step {k}")
         return u
 
     def disp(self, u, node, dof):

@@ -12,6 +12,8 @@ Sources (paths relative to /root/reference):
   tests/input_files/solid_ele_hex8_Standard_linear.dat   (registered tests/list_of_tests.cmake:1338)
   tests/input_files/solid_ele_hex27_Standard_linear.dat  (tests/list_of_tests.cmake:1311)
   tests/input_files/sohex27_patchtest_nl_cost_drt.dat    (tests/list_of_tests.cmake:1265)
+  tests/input_files/solid_ele_hex8_Standard_eas_none_volume_neumann.dat (ElastHyper/CoupNeoHooke)
+  tests/input_files/solid_ele_hex27_Standard_volume_neumann.dat          (ElastHyper/CoupNeoHooke)
   tests/input_files/tsi_heatflux_monolithic.dat          (thermo-structure interaction, statics)
   tests/input_files/tsi_heatflux_flexoutsurf_monolithic.dat
 """
@@ -85,7 +87,15 @@ def extract(fname):
         elements.append({"id": int(tok[0]), "shape": shape, "nodes": [int(t) for t in tok[3 : 3 + nn]],
                          "kinem": kin})
     mat = s["MATERIALS"][0].split()
-    material = {"young": float(mat[mat.index("YOUNG") + 1]), "nue": float(mat[mat.index("NUE") + 1])}
+    if "MAT_ElastHyper" in mat:
+        # one ELAST_CoupNeoHooke summand (MATIDS)
+        summ = [l.split() for l in s["MATERIALS"] if "ELAST_CoupNeoHooke" in l]
+        assert len(summ) == 1 and mat[mat.index("NUMMAT") + 1] == "1"
+        sm = summ[0]
+        material = {"type": "elasthyper_coupneohooke", "young": float(sm[sm.index("YOUNG") + 1]),
+                    "nue": float(sm[sm.index("NUE") + 1])}
+    else:
+        material = {"young": float(mat[mat.index("YOUNG") + 1]), "nue": float(mat[mat.index("NUE") + 1])}
     results = []
     for line in s["RESULT DESCRIPTION"]:
         m = re.match(r"STRUCTURE DIS structure NODE (\d+) QUANTITY (\w+) VALUE\s+(\S+) TOLERANCE (\S+)", line)
@@ -154,7 +164,9 @@ def main():
     if not os.path.isdir(REF):
         sys.exit("reference tree not present; fixtures are committed, nothing to do")
     for fname in ("solid_ele_hex8_Standard_linear.dat", "solid_ele_hex27_Standard_linear.dat",
-                  "sohex27_patchtest_nl_cost_drt.dat"):
+                  "sohex27_patchtest_nl_cost_drt.dat",
+                  "solid_ele_hex8_Standard_eas_none_volume_neumann.dat",
+                  "solid_ele_hex27_Standard_volume_neumann.dat"):
         data = extract(fname)
         out = os.path.join(HERE, fname.replace(".dat", ".json"))
         with open(out, "w") as f:

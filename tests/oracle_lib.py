@@ -15,6 +15,7 @@ LIB_PATH = os.path.join(ORACLE_DIR, "_build", "liborc.so")
 
 HEX8, HEX27 = 0, 1
 LINEAR, TOTLAG = 0, 1
+MAT_STVK, MAT_NEOHOOKE = 0, 1
 
 _lib = None
 
@@ -63,6 +64,13 @@ def load(path=None):
     lib.orc_hex_element_nodeids.argtypes = [ctypes.c_int, ctypes.c_int64, _i32p, ctypes.c_int64, _i64p]
     lib.orc_lattice_node_coords.argtypes = [ctypes.c_int64, _i32p, ctypes.c_int64, _dp, _dp, _dp, _dp]
     lib.orc_box_section.argtypes = [_i32p, ctypes.c_int, ctypes.c_int, _i32p]
+    lib.orc_solid_evaluate_mat.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                           ctypes.c_double, _dp, _dp, _dp, _dp]
+    lib.orc_elasthyper_coupneohooke.argtypes = [ctypes.c_double, ctypes.c_double, _dp, _dp, _dp]
+    lib.orc_discretization_evaluate_mat.argtypes = [
+        ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int64,
+        _i64p, ctypes.c_int64, _dp, _i64p, _i32p, ctypes.c_int64, ctypes.c_int, _dp,
+        ctypes.POINTER(OrcCsr), _dp, _i64p]
     lib.orc_discretization_evaluate.argtypes = [
         ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int64, _i64p,
         ctypes.c_int64, _dp, _i64p, _i32p, ctypes.c_int64, ctypes.c_int, _dp,
@@ -128,7 +136,7 @@ def stvk_energy(E, nu, gl):
     return load().orc_stvk_strain_energy(E, nu, ptr(np.ascontiguousarray(gl, dtype=np.float64), _dp))
 
 
-def solid_evaluate(celltype, kinem, E, nu, X, u, want_k=True):
+def solid_evaluate(celltype, kinem, E, nu, X, u, want_k=True, material=MAT_STVK):
     """Returns (err, Ke (3n x 3n), fe (3n))."""
     lib = load()
     n = 8 if celltype == HEX8 else 27
@@ -136,8 +144,8 @@ def solid_evaluate(celltype, kinem, E, nu, X, u, want_k=True):
     u = np.ascontiguousarray(u, dtype=np.float64).reshape(n, 3)
     Ke = np.zeros(9 * n * n)
     fe = np.zeros(3 * n)
-    err = lib.orc_solid_evaluate(celltype, kinem, E, nu, ptr(X, _dp), ptr(u, _dp),
-                                 ptr(Ke, _dp) if want_k else None, ptr(fe, _dp))
+    err = lib.orc_solid_evaluate_mat(celltype, kinem, material, E, nu, ptr(X, _dp), ptr(u, _dp),
+                                     ptr(Ke, _dp) if want_k else None, ptr(fe, _dp))
     return err, Ke.reshape(3 * n, 3 * n).T.copy(), fe
 
 
@@ -201,3 +209,12 @@ def tsi_thermo_evaluate(celltype, conduct, m, X, T, v, timefac, timefac_d):
     err = lib.orc_tsi_thermo_evaluate(celltype, conduct, m, ptr(X, _dp), ptr(T, _dp), ptr(v, _dp),
                                       timefac, timefac_d, ptr(Ktt, _dp), ptr(fT, _dp), ptr(Kts, _dp))
     return err, Ktt.reshape(n, n).T.copy(), fT, Kts.reshape(3 * n, n).T.copy()
+
+
+def neohooke(E, nu, gl):
+    """ElastHyper/CoupNeoHooke: (S, cmat 6x6)."""
+    lib = load()
+    gl = np.ascontiguousarray(gl, dtype=np.float64)
+    S, c = np.zeros(6), np.zeros(36)
+    lib.orc_elasthyper_coupneohooke(E, nu, ptr(gl, _dp), ptr(S, _dp), ptr(c, _dp))
+    return S, c.reshape(6, 6).T

@@ -7,6 +7,8 @@ tests/golden/make_fixtures.py or quoted below with their file:line):
   * tests/input_files/solid_ele_hex8_Standard_linear.dat  RESULT DESCRIPTION (1e-12)
   * tests/input_files/solid_ele_hex27_Standard_linear.dat RESULT DESCRIPTION (1e-12)
   * tests/input_files/sohex27_patchtest_nl_cost_drt.dat   RESULT DESCRIPTION (1e-9)
+  * tests/input_files/solid_ele_hex8_Standard_eas_none_volume_neumann.dat, solid_ele_hex27_Standard_volume_neumann.dat
+    RESULT DESCRIPTION (ElastHyper/CoupNeoHooke, large deformation, 1e-12)
   * tests/input_files/tsi_heatflux_monolithic.dat         RESULT DESCRIPTION (1e-9 disp, 1e-6 temp)
   * tests/input_files/tsi_heatflux_flexoutsurf_monolithic.dat RESULT DESCRIPTION (1e-8)
 The result-test comparison is absolute (4C_utils_result_test.cpp:98).
@@ -138,7 +140,9 @@ def test_negative_nodal_jacobian_is_reported():
 # --------------------------------------------------------------------------- end-to-end
 @pytest.mark.parametrize("name", ["solid_ele_hex8_Standard_linear.json",
                                   "solid_ele_hex27_Standard_linear.json",
-                                  "sohex27_patchtest_nl_cost_drt.json"])
+                                  "sohex27_patchtest_nl_cost_drt.json",
+                                  "solid_ele_hex8_Standard_eas_none_volume_neumann.json",
+                                  "solid_ele_hex27_Standard_volume_neumann.json"])
 def test_result_description(name):
     fx = load_fixture(name)
     prob = Problem(fx)
@@ -146,7 +150,8 @@ def test_result_description(name):
     nstep = int(fx["dynamic"].get("NUMSTEP", 1))
     dt = float(fx["dynamic"].get("TIMESTEP", 1.0))
     t = min(t_end, nstep * dt)
-    u = prob.solve_statics(t=t)
+    # the reference's load steps (statics: each step converged from the previous one)
+    u = prob.solve_statics(t=t, nsteps=max(1, int(round(t / dt))))
     for r in fx["results"]:
         got = prob.disp(u, r["node"], r["dof"])
         assert abs(got - r["value"]) <= r["tol"], (r, got)
@@ -200,3 +205,23 @@ def test_tsi_tangent_blocks_are_derivatives(celltype):
         # f_T is linear in v: the difference quotient is exact up to the rounding of f_T
         np.testing.assert_allclose(Kts[:, j], (gp - gm) / (2 * hv) / dt, rtol=1e-6,
                                    atol=1e-6 * abs(Kts).max())
+
+
+# --------------------------------------------------------------------------- ElastHyper
+def test_neohooke_cmat_is_stress_derivative():
+    """cmat = dS/dE (strain-like Voigt: shear columns derive w.r.t. the engineering shear), S(0)=0,
+    and the small-strain limit is StVK's cmat for the same E, nu."""
+    E, nu = 10.0, 0.25
+    gl = np.array([0.05, -0.02, 0.03, 0.04, -0.01, 0.02])
+    S, C = orc.neohooke(E, nu, gl)
+    h = 1e-6
+    for j in range(6):
+        e = np.zeros(6)
+        e[j] = h
+        Sp, _ = orc.neohooke(E, nu, gl + e)
+        Sm, _ = orc.neohooke(E, nu, gl - e)
+        np.testing.assert_allclose(C[:, j], (Sp - Sm) / (2 * h), rtol=1e-6, atol=1e-8)
+    S0, C0 = orc.neohooke(E, nu, np.zeros(6))
+    np.testing.assert_allclose(S0, 0.0, atol=1e-14)
+    _, Cst = orc.stvk(E, nu, np.zeros(6))
+    np.testing.assert_allclose(C0, Cst, rtol=1e-12, atol=1e-12)
