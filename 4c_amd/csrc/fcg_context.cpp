@@ -324,6 +324,21 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
     set_create_error("Young's modulus must be > 0 and Poisson's ratio in [-1;0.5)");
     return FCG_ERR_ARG;
   }
+  if (d->material != FCG_MAT_STVK && d->material != FCG_MAT_ELASTHYPER_COUPNEOHOOKE)
+  {
+    set_create_error("unsupported material");
+    return FCG_ERR_ARG;
+  }
+  if (d->material == FCG_MAT_ELASTHYPER_COUPNEOHOOKE && d->kinematics != FCG_TOTLAG)
+  {
+    set_create_error("ElastHyper is supported with KINEM nonlinear (TotLag) only");
+    return FCG_ERR_ARG;
+  }
+  if (d->material != FCG_MAT_STVK && d->path == FCG_PATH_STRUCTURED)
+  {
+    set_create_error("the structured sweep implements StVenantKirchhoff only");
+    return FCG_ERR_ARG;
+  }
   if (d->n_ele < 0 || d->n_node < 0 || d->n_rows < 0 || d->n_cols < 0 ||
       (d->n_ele > 0 && (!d->ele_nodes || !d->node_x || !d->node_dof_col || !d->node_dof_row)) ||
       (d->n_rows > 0 && (!d->rowptr || !d->col_lid)) || d->n_ele >= (int64_t(1) << 31))
@@ -404,7 +419,7 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
   StructHost sp;
   std::string why;
   bool structured = false;
-  if (d->path != FCG_PATH_GENERAL)
+  if (d->path != FCG_PATH_GENERAL && d->material == FCG_MAT_STVK)
   {
     structured = build_structured_plan(d, rownodes, row0, kcol, sp, why);
     if (!structured && d->path == FCG_PATH_STRUCTURED)
@@ -507,6 +522,10 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
   m.cdiag = mfac * (1.0 - nu);
   m.lambda = mfac * nu;
   m.mu = mfac * 0.5 * (1.0 - 2.0 * nu);
+  // Mat::Elastic::PAR::CoupNeoHooke (4C_mat_elast_coupneohooke.cpp): c, beta
+  m.material = d->material;
+  m.nh_c = d->youngs / (4.0 * (1.0 + nu));
+  m.nh_beta = nu / (1.0 - 2.0 * nu);
   std::vector<int32_t> eg;
   if (!d->ele_gid)
   {

@@ -20,6 +20,8 @@ struct DeviceMesh {
   int64_t n_ele = 0, n_node = 0, n_rows = 0, n_cols = 0, nnz = 0;
   int64_t n_rownodes = 0, n_inc = 0;
   double lambda = 0, mu = 0, cdiag = 0;  // StVK: C_00 = cdiag, C_01 = lambda, C_33 = mu
+  int material = FCG_MAT_STVK;
+  double nh_c = 0, nh_beta = 0;          // ElastHyper/CoupNeoHooke constants
 
   int32_t* ele_nodes = nullptr;     // [n_ele][npe]
   int32_t* ele_gid = nullptr;       // [n_ele]

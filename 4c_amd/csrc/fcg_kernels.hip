@@ -126,7 +126,7 @@ __device__ inline void jacobian(const double* __restrict__ dN, const double* __r
   }
 }
 
-template <int NPE, int KIN>
+template <int NPE, int KIN, int MAT = 0>
 struct ElementShared {
   static constexpr int NGP = NPE;
   double X[3 * NPE];
@@ -138,8 +138,96 @@ struct ElementShared {
   double S[NGP * 6];                      // PK2 stress, Voigt xx yy zz xy yz zx
   double F[KIN ? NGP * 9 : 1];
   double M[KIN ? NGP * 6 : 1];            // F F^T (sym)
+  double Cm[MAT ? NGP * 36 : 1];          // ElastHyper: cmat (column-major 6x6) per Gauss point
   int bad;
 };
+
+// Mat::ElastHyper with one ELAST_CoupNeoHooke summand: S and cmat from the principal invariants
+// of C = 2E + I (4C_mat_elasthyper_service.cpp:19-215, 4C_mat_elast_coupneohooke.cpp,
+// calculate_gamma_delta :413-432, add_holzapfel_product
+// 4C_linalg_fixedsizematrix_tensor_products.cpp:264-312).  E in strain-like Voigt notation.
+__device__ inline void neohooke_stress_cmat(double c, double beta, const double* E, double* S,
+    double* cm)
+{
+  double C[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) C[i] = 2.0 * E[i];
+  C[0] += 1.0;
+  C[1] += 1.0;
+  C[2] += 1.0;
+  // determinant and inverse in strain-like Voigt notation (shear entries carry 2x)
+  const double c3 = 0.5 * C[3], c4 = 0.5 * C[4], c5 = 0.5 * C[5];
+  const double det = C[0] * C[1] * C[2] + 2 * c3 * c4 * c5 - C[1] * c5 * c5 - C[2] * c3 * c3 -
+                     C[0] * c4 * c4;
+  double iC[6];
+  iC[0] = (C[1] * C[2] - c4 * c4) / det;
+  iC[1] = (C[0] * C[2] - c5 * c5) / det;
+  iC[2] = (C[0] * C[1] - c3 * c3) / det;
+  iC[3] = (c5 * c4 - c3 * C[2]) / det;  // stress-like (tensor) components
+  iC[4] = (c3 * c5 - C[0] * c4) / det;
+  iC[5] = (c3 * c4 - c5 * C[1]) / det;
+  const double I1 = C[0] + C[1] + C[2];
+  const double I3 = det;
+  // CoupNeoHooke::add_derivatives_principal: dPI = (c, 0, -c I3^(-beta-1)), ddPII(2)
+  double dP2 = NAN, ddP2 = NAN;
+  if (I3 > 0)
+  {
+    const double p = exp(log(I3) * (-beta - 1.));
+    dP2 = -c * p;
+    ddP2 = c * (beta + 1.) * p / I3;
+  }
+  const double g0 = 2. * c, g2 = 2. * I3 * dP2;
+  const double d5 = 4. * (I3 * dP2 + I3 * I3 * ddP2), d6 = -4. * I3 * dP2;
+  (void)I1;
+  // S = g0 I + g2 C^-1 (stress-like)
+  S[0] = g0 + g2 * iC[0];
+  S[1] = g0 + g2 * iC[1];
+  S[2] = g0 + g2 * iC[2];
+  S[3] = g2 * iC[3];
+  S[4] = g2 * iC[4];
+  S[5] = g2 * iC[5];
+  // cmat = d5 C^-1 (x) C^-1 + d6 (C^-1 odot C^-1)  (the other delta vanish for CoupNeoHooke)
+  const double* v = iC;
+#define CM(i, j) cm[(i) + 6 * (j)]
+#pragma unroll
+  for (int j = 0; j < 6; ++j)
+#pragma unroll
+    for (int i = 0; i < 6; ++i) CM(i, j) = d5 * v[i] * v[j];
+  CM(0, 0) += d6 * v[0] * v[0]; CM(0, 1) += d6 * v[3] * v[3]; CM(0, 2) += d6 * v[5] * v[5];
+  CM(0, 3) += d6 * v[0] * v[3]; CM(0, 4) += d6 * v[3] * v[5]; CM(0, 5) += d6 * v[0] * v[5];
+  CM(1, 0) += d6 * v[3] * v[3]; CM(1, 1) += d6 * v[1] * v[1]; CM(1, 2) += d6 * v[4] * v[4];
+  CM(1, 3) += d6 * v[3] * v[1]; CM(1, 4) += d6 * v[1] * v[4]; CM(1, 5) += d6 * v[3] * v[4];
+  CM(2, 0) += d6 * v[5] * v[5]; CM(2, 1) += d6 * v[4] * v[4]; CM(2, 2) += d6 * v[2] * v[2];
+  CM(2, 3) += d6 * v[5] * v[4]; CM(2, 4) += d6 * v[4] * v[2]; CM(2, 5) += d6 * v[5] * v[2];
+  CM(3, 0) += d6 * v[0] * v[3]; CM(3, 1) += d6 * v[3] * v[1]; CM(3, 2) += d6 * v[5] * v[4];
+  CM(3, 3) += d6 * 0.5 * (v[0] * v[1] + v[3] * v[3]);
+  CM(3, 4) += d6 * 0.5 * (v[3] * v[4] + v[5] * v[1]);
+  CM(3, 5) += d6 * 0.5 * (v[0] * v[4] + v[5] * v[3]);
+  CM(4, 0) += d6 * v[3] * v[5]; CM(4, 1) += d6 * v[1] * v[4]; CM(4, 2) += d6 * v[4] * v[2];
+  CM(4, 3) += d6 * 0.5 * (v[3] * v[4] + v[5] * v[1]);
+  CM(4, 4) += d6 * 0.5 * (v[1] * v[2] + v[4] * v[4]);
+  CM(4, 5) += d6 * 0.5 * (v[3] * v[2] + v[4] * v[5]);
+  CM(5, 0) += d6 * v[0] * v[5]; CM(5, 1) += d6 * v[3] * v[4]; CM(5, 2) += d6 * v[5] * v[2];
+  CM(5, 3) += d6 * 0.5 * (v[0] * v[4] + v[5] * v[3]);
+  CM(5, 4) += d6 * 0.5 * (v[3] * v[2] + v[4] * v[5]);
+  CM(5, 5) += d6 * 0.5 * (v[0] * v[2] + v[5] * v[5]);
+#undef CM
+}
+
+// B_NL of node n (evaluate_strain_gradient, calc_lib.hpp:708-760): B[r][e], F column-major
+__device__ inline void strain_gradient(const double* F, const double* nx, double (*B)[3])
+{
+#pragma unroll
+  for (int e = 0; e < 3; ++e)
+  {
+    B[0][e] = F[e] * nx[0];
+    B[1][e] = F[e + 3] * nx[1];
+    B[2][e] = F[e + 6] * nx[2];
+    B[3][e] = F[e] * nx[1] + F[e + 3] * nx[0];
+    B[4][e] = F[e + 3] * nx[2] + F[e + 6] * nx[1];
+    B[5][e] = F[e + 6] * nx[0] + F[e] * nx[2];
+  }
+}
 
 struct ElementArgs {
   int64_t n_ele;
@@ -151,11 +239,12 @@ struct ElementArgs {
   double* scratch;
   int32_t* err;
   double lambda, mu, cdiag;
+  double nh_c, nh_beta;  // ElastHyper/CoupNeoHooke: c = E / (4 (1 + nu)), beta = nu / (1 - 2 nu)
   int want_k;
 };
 
 // ---------------------------------------------------------------------------------- element
-template <int NPE, int KIN, int BLOCK>
+template <int NPE, int KIN, int BLOCK, int MAT = 0>
 __global__ __launch_bounds__(BLOCK) void element_kernel(ElementArgs A)
 {
   constexpr int NGP = NPE;
@@ -163,7 +252,7 @@ __global__ __launch_bounds__(BLOCK) void element_kernel(ElementArgs A)
   constexpr int NPAIR = SYM ? NPE * (NPE + 1) / 2 : NPE * NPE;
   constexpr int REC = 9 * NPE + 3;
   constexpr int ROWLEN = 3 * NPE;
-  __shared__ ElementShared<NPE, KIN> sh;
+  __shared__ ElementShared<NPE, KIN, MAT> sh;
   const int tid = threadIdx.x;
   const double* dNgp = Tables<NPE>::dNgp();
   const double* dNnode = Tables<NPE>::dNnode();
@@ -306,14 +395,19 @@ __global__ __launch_bounds__(BLOCK) void element_kernel(ElementArgs A)
         Ms[4] = F[1] * F[2] + F[4] * F[5] + F[7] * F[8];
         Ms[5] = F[2] * F[0] + F[5] * F[3] + F[8] * F[6];
       }
-      // So3Material::evaluate -> S = C E (4C_mat_stvenantkirchhoff.cpp:169-177)
+      // So3Material::evaluate -> S = C E (4C_mat_stvenantkirchhoff.cpp:169-177), or ElastHyper
       double* S = sh.S + 6 * g;
-      S[0] = A.cdiag * E[0] + A.lambda * E[1] + A.lambda * E[2];
-      S[1] = A.lambda * E[0] + A.cdiag * E[1] + A.lambda * E[2];
-      S[2] = A.lambda * E[0] + A.lambda * E[1] + A.cdiag * E[2];
-      S[3] = A.mu * E[3];
-      S[4] = A.mu * E[4];
-      S[5] = A.mu * E[5];
+      if (MAT == 1)
+        neohooke_stress_cmat(A.nh_c, A.nh_beta, E, S, sh.Cm + 36 * (MAT ? g : 0));
+      else
+      {
+        S[0] = A.cdiag * E[0] + A.lambda * E[1] + A.lambda * E[2];
+        S[1] = A.lambda * E[0] + A.cdiag * E[1] + A.lambda * E[2];
+        S[2] = A.lambda * E[0] + A.lambda * E[1] + A.cdiag * E[2];
+        S[3] = A.mu * E[3];
+        S[4] = A.mu * E[4];
+        S[5] = A.mu * E[5];
+      }
     }
     __syncthreads();
     if (KIN == 1)
@@ -410,7 +504,44 @@ __global__ __launch_bounds__(BLOCK) void element_kernel(ElementArgs A)
           const double fc = sh.fac[g];
           const double* na = sh.NX + 3 * (NPE * g + a);
           const double* nb = sh.NX + 3 * (NPE * g + b);
-          if (KIN == 0)
+          if (MAT == 1)
+          {
+            // general material: K_ab += fac (B_a^T cmat B_b + (a.S.b) I)  (calc_lib.hpp:872-927);
+            // G holds B_a^T cmat B_b (row-major i, j), geo the geometric part
+            const double* F = sh.F + 9 * g;
+            const double* cm = sh.Cm + 36 * (MAT ? g : 0);
+            double Ba[6][3], Bb[6][3];
+            strain_gradient(F, na, Ba);
+            strain_gradient(F, nb, Bb);
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+            {
+              double cb[6];
+#pragma unroll
+              for (int r = 0; r < 6; ++r)
+              {
+                double t = 0.0;
+#pragma unroll
+                for (int q = 0; q < 6; ++q) t += cm[r + 6 * q] * Bb[q][j];
+                cb[r] = fc * t;
+              }
+#pragma unroll
+              for (int i = 0; i < 3; ++i)
+              {
+                double t = 0.0;
+#pragma unroll
+                for (int r = 0; r < 6; ++r) t += Ba[r][i] * cb[r];
+                G[i + 3 * j] += t;
+              }
+            }
+            const double* S = sh.S + 6 * g;
+            const double c0 = nb[0], c1 = nb[1], c2 = nb[2];
+            const double sb0 = S[0] * c0 + S[3] * c1 + S[5] * c2;
+            const double sb1 = S[3] * c0 + S[1] * c1 + S[4] * c2;
+            const double sb2 = S[5] * c0 + S[4] * c1 + S[2] * c2;
+            geo += fc * (na[0] * sb0 + na[1] * sb1 + na[2] * sb2);
+          }
+          else if (KIN == 0)
           {
             const double fa0 = fc * na[0], fa1 = fc * na[1], fa2 = fc * na[2];
             const double b0 = nb[0], b1 = nb[1], b2 = nb[2];
@@ -444,11 +575,25 @@ __global__ __launch_bounds__(BLOCK) void element_kernel(ElementArgs A)
         // K_ij = lambda G_ij + mu G_ji + mu H_ij + geo delta_ij (TotLag)
         double K[9];
         const double lam = A.lambda, mu = A.mu;
+        if (MAT == 1)
+        {
 #pragma unroll
-        for (int i = 0; i < 3; ++i)
+          for (int i = 0; i < 9; ++i) K[i] = G[i];
+          K[0] += geo;
+          K[4] += geo;
+          K[8] += geo;
+        }
+        else
+        {
 #pragma unroll
-          for (int j = 0; j < 3; ++j) K[i + 3 * j] = lam * G[i + 3 * j] + mu * G[j + 3 * i];
-        if (KIN == 0)
+          for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) K[i + 3 * j] = lam * G[i + 3 * j] + mu * G[j + 3 * i];
+        }
+        if (MAT == 1)
+        {
+        }
+        else if (KIN == 0)
         {
           const double tr = mu * (G[0] + G[4] + G[8]);
           K[0] += tr;
@@ -711,6 +856,19 @@ hipError_t launch_element(const DeviceMesh& m, const double* d_u_col, bool want_
   a.mu = m.mu;
   a.cdiag = m.cdiag;
   a.want_k = want_k ? 1 : 0;
+  a.nh_c = m.nh_c;
+  a.nh_beta = m.nh_beta;
+  if (m.material == FCG_MAT_ELASTHYPER_COUPNEOHOOKE)
+  {
+    // general constitutive tangent: one workgroup per element (TotLag only, checked at create)
+    if (m.npe == 8)
+      hipLaunchKernelGGL((element_kernel<8, 1, 64, 1>), dim3(grid_for(m.n_ele, 256 * 32)), dim3(64),
+          0, stream, a);
+    else
+      hipLaunchKernelGGL((element_kernel<27, 1, 256, 1>), dim3(grid_for(m.n_ele, 256 * 8)),
+          dim3(256), 0, stream, a);
+    return hipGetLastError();
+  }
   if (m.npe == 8)
   {
     const int grid = grid_for((m.n_ele + H8_EPB - 1) / H8_EPB, 256 * 16);

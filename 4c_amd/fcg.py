@@ -18,6 +18,7 @@ LINEAR, TOTLAG = 0, 1
 CALC_NLNSTIFF, CALC_INTERNALFORCE = 0, 1
 ACCUMULATE, OVERWRITE = 0, 1
 PATH_AUTO, PATH_GENERAL, PATH_STRUCTURED = 0, 1, 2
+MAT_STVK, MAT_ELASTHYPER_COUPNEOHOOKE = 0, 1
 TSI_STRUCT_FORCE, TSI_STIFFTEMP, TSI_THERMO_FINTCOND, TSI_COUPLTANG = 1, 2, 4, 8
 TSI_ALL = 15
 ABI_VERSION = 1
@@ -38,7 +39,7 @@ class FcgDesc(ctypes.Structure):
                 ("n_cols", ctypes.c_int64), ("ele_nodes", _i32p), ("ele_gid", _i32p),
                 ("node_x", _dp), ("node_dof_col", _i32p), ("node_dof_row", _i32p),
                 ("node_dof_kcol", _i32p), ("rowptr", _i64p), ("col_lid", _i32p),
-                ("ele_ijk", _i32p), ("path", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("ele_ijk", _i32p), ("path", ctypes.c_int32), ("material", ctypes.c_int32)]
 
 
 class FcgBox(ctypes.Structure):
@@ -198,7 +199,7 @@ class Discretization:
         dof = 3 * np.arange(n_node, dtype=np.int32)
         return Discretization(celltype, en, node_x, dof, dof, np.array(rows), np.array(cols))
 
-    def desc(self, kinematics, youngs, poisson, device=0, path=PATH_AUTO):
+    def desc(self, kinematics, youngs, poisson, device=0, path=PATH_AUTO, material=MAT_STVK):
         d = FcgDesc()
         d.abi_version = ABI_VERSION
         d.celltype = self.celltype
@@ -217,6 +218,7 @@ class Discretization:
         d.col_lid = _np_ptr(self.col_lid, _i32p)
         d.ele_ijk = None
         d.path = path
+        d.material = material
         return d
 
 
@@ -322,7 +324,7 @@ class BoxMesh:
         L.fcg_box_mesh_destroy(h)
         self._h = None
 
-    def desc(self, kinematics, youngs, poisson, device=0, path=PATH_AUTO):
+    def desc(self, kinematics, youngs, poisson, device=0, path=PATH_AUTO, material=MAT_STVK):
         d = FcgDesc()
         d.abi_version = ABI_VERSION
         d.celltype = self.celltype
@@ -341,6 +343,7 @@ class BoxMesh:
         d.col_lid = _np_ptr(self.col_lid, _i32p)
         d.ele_ijk = _np_ptr(self.ele_ijk, _i32p) if path != PATH_GENERAL else None
         d.path = path
+        d.material = material
         return d
 
     def node_displacement(self, amplitude):
@@ -365,11 +368,11 @@ class Evaluator:
     hex8/hex27 + StVK.  Keeps 4C's error behaviour: a non-zero status raises FcgError."""
 
     def __init__(self, desc_or_mesh, kinematics=LINEAR, youngs=210.0, poisson=0.3, device=0,
-                 path=PATH_AUTO):
+                 path=PATH_AUTO, material=MAT_STVK):
         L = lib()
         if isinstance(desc_or_mesh, (BoxMesh, Discretization)):
             self._mesh = desc_or_mesh
-            desc = desc_or_mesh.desc(kinematics, youngs, poisson, device, path)
+            desc = desc_or_mesh.desc(kinematics, youngs, poisson, device, path, material)
         else:
             self._mesh = None
             desc = desc_or_mesh

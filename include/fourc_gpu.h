@@ -87,8 +87,14 @@ typedef struct fcg_desc {
    * z-sweep kernel (no scratch round trip).  NULL = general (unstructured) path. */
   const int32_t* ele_ijk;
   int32_t path;                /* fcg_path: FCG_PATH_AUTO / _GENERAL / _STRUCTURED */
-  int32_t reserved;
+  int32_t material;            /* fcg_material (0 = StVenantKirchhoff) */
 } fcg_desc;
+
+/* Materials.  FCG_MAT_STVK: MAT_Struct_StVenantKirchhoff YOUNG NUE (4C_mat_stvenantkirchhoff.cpp).
+ * FCG_MAT_ELASTHYPER_COUPNEOHOOKE: MAT_ElastHyper with one ELAST_CoupNeoHooke summand, youngs /
+ * poisson = the summand's YOUNG / NUE (4C_mat_elasthyper_service.cpp:19-215,
+ * 4C_mat_elast_coupneohooke.cpp); FCG_TOTLAG only, general (unstructured) kernels. */
+enum fcg_material { FCG_MAT_STVK = 0, FCG_MAT_ELASTHYPER_COUPNEOHOOKE = 1 };
 
 /* Evaluation paths.  AUTO picks STRUCTURED when the hint verifies, else GENERAL.  STRUCTURED
  * fails fcg_create with FCG_ERR_ARG when the hint does not verify. */

@@ -20,7 +20,8 @@ def gid_maps(row_gid, col_gid):
     return row_lid, col_lid, max_gid
 
 
-def oracle_evaluate(mesh, kinem, E, nu, u_col, want_k=True, nworkers=1, min_node_gid=0):
+def oracle_evaluate(mesh, kinem, E, nu, u_col, want_k=True, nworkers=1, min_node_gid=0,
+                    material=orc.MAT_STVK):
     """Oracle Discretization::evaluate on mesh's rank: returns (err, bad_ele, K_vals, fint).
 
     The oracle evaluates the rank's column elements and assembles the rows the rank owns, in the
@@ -46,8 +47,8 @@ def oracle_evaluate(mesh, kinem, E, nu, u_col, want_k=True, nworkers=1, min_node
     idx = np.nonzero(owned)[0]
     owner[idx] = (np.arange(len(idx)) * nworkers // max(len(idx), 1)).astype(np.int32)
     bad = ctypes.c_int64(-1)
-    err = lib.orc_discretization_evaluate(
-        mesh.celltype, kinem, E, nu, mesh.n_ele, ele_nodes.ctypes.data_as(orc._i64p), mesh.n_node,
+    err = lib.orc_discretization_evaluate_mat(
+        mesh.celltype, kinem, material, E, nu, mesh.n_ele, ele_nodes.ctypes.data_as(orc._i64p), mesh.n_node,
         np.ascontiguousarray(mesh.node_x).ctypes.data_as(orc._dp),
         mesh.node_gid.ctypes.data_as(orc._i64p), owner.ctypes.data_as(orc._i32p), min_node_gid,
         nworkers, u_col.ctypes.data_as(orc._dp), ctypes.byref(csr), f.ctypes.data_as(orc._dp),

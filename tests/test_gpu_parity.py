@@ -183,3 +183,23 @@ def test_full_size_linear_properties():
     err, _, Kr, fr = oracle_evaluate(mesh, fcg.LINEAR, E, NU, u, nworkers=16)
     assert err == 0
     _check(K.cpu().numpy(), f.cpu().numpy(), Kr, fr)
+
+
+# ------------------------------------------------------------------ ElastHyper / CoupNeoHooke
+NH = fcg.MAT_ELASTHYPER_COUPNEOHOOKE
+
+
+@pytest.mark.parametrize("celltype,iv", [(fcg.HEX8, (4, 3, 3)), (fcg.HEX27, (2, 2, 1))])
+def test_neohooke_matches_oracle(celltype, iv):
+    import oracle_lib as orc
+    _dev()
+    mesh = fcg.BoxMesh(celltype, iv, jitter=0.1 if celltype == fcg.HEX8 else 0.02, seed=9)
+    u = mesh.u_col(5e-2)
+    err, _, Kr, fr = oracle_evaluate(mesh, fcg.TOTLAG, 10.0, 0.25, u, material=orc.MAT_NEOHOOKE)
+    assert err == 0
+    ev = fcg.Evaluator(mesh, kinematics=fcg.TOTLAG, youngs=10.0, poisson=0.25, material=NH)
+    assert ev.info.path == fcg.PATH_GENERAL
+    Kg, fg, _ = _run_gpu(mesh, fcg.TOTLAG, u, ev=ev)
+    _check(Kg, fg, Kr, fr)
+    _, fi, _ = _run_gpu(mesh, fcg.TOTLAG, u, action=fcg.CALC_INTERNALFORCE, ev=ev)
+    assert rel_err(fi, fr) <= 1e-10

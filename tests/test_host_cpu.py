@@ -170,3 +170,14 @@ def test_bench_weak_scaling_boxes(world):
     for r in range(world):
         m = fcg.BoxMesh(fcg.HEX8, iv, rank=r, nranks=world)
         assert m.n_ele_row == n ** 3
+
+
+def test_neohooke_needs_totlag_and_general_path():
+    m = fcg.BoxMesh(fcg.HEX8, (1, 1, 1))
+    with pytest.raises(fcg.FcgError) as ei:
+        fcg.Evaluator(m, kinematics=fcg.LINEAR, material=fcg.MAT_ELASTHYPER_COUPNEOHOOKE)
+    assert ei.value.code == 3
+    with pytest.raises(fcg.FcgError) as ei:
+        fcg.Evaluator(m, kinematics=fcg.TOTLAG, path=fcg.PATH_STRUCTURED,
+                      material=fcg.MAT_ELASTHYPER_COUPNEOHOOKE)
+    assert ei.value.code == 3

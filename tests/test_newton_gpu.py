@@ -147,3 +147,32 @@ def test_spmv_dirichlet_pcg_against_scipy():
     sol2 = torch.empty_like(rhs)
     ev.pcg_solve(K, rhs, sol2, rtol=1e-14, max_iter=5000)
     assert torch.equal(sol, sol2)
+
+
+@pytest.mark.parametrize("name", ["solid_ele_hex8_Standard_eas_none_volume_neumann.json",
+                                  "solid_ele_hex27_Standard_volume_neumann.json"])
+def test_neohooke_result_description_on_device(name):
+    """ElastHyper/CoupNeoHooke, large deformation (|u| ~ 2.9), the reference's two load steps;
+    every tangent and residual from the library, Newton solved on the host."""
+    dev = _dev()
+    fx = json.load(open(os.path.join(GOLD, name)))
+    prob = fp.problem(fx)
+    dis = fp.discretization(prob)
+    ev = fcg.Evaluator(dis, kinematics=fcg.TOTLAG, youngs=prob.E, poisson=prob.nu,
+                       material=fcg.MAT_ELASTHYPER_COUPNEOHOOKE)
+
+    def assemble(u):
+        f = torch.zeros(dis.n_rows, dtype=torch.float64, device=dev)
+        K = torch.zeros(dis.nnz, dtype=torch.float64, device=dev)
+        ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, torch.from_numpy(u).to(dev), f, K)
+        D = np.zeros((dis.n_rows, dis.n_cols))
+        rows = np.repeat(np.arange(dis.n_rows), np.diff(dis.rowptr))
+        D[rows, dis.col_lid] = K.cpu().numpy()
+        return D, f.cpu().numpy()
+
+    t = fp.end_time(fx)
+    dt = float(fx["dynamic"]["TIMESTEP"])
+    u = prob.solve_statics(t=t, nsteps=int(round(t / dt)), assemble=assemble)
+    for r in fx["results"]:
+        got = prob.disp(u, r["node"], r["dof"])
+        assert abs(got - r["value"]) <= r["tol"], (r, got)
