@@ -17,6 +17,7 @@ ap.add_argument("--kinem", default="linear")
 ap.add_argument("--n", type=int, default=50)
 ap.add_argument("--path", default="auto")
 ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--material", default="stvk", choices=["stvk", "neohooke"])
 a = ap.parse_args()
 ct = fcg.HEX8 if a.celltype == "hex8" else fcg.HEX27
 kin = fcg.LINEAR if a.kinem == "linear" else fcg.TOTLAG
@@ -24,7 +25,8 @@ path = {"auto": fcg.PATH_AUTO, "general": fcg.PATH_GENERAL}[a.path]
 t0 = time.perf_counter()
 m = fcg.BoxMesh(ct, (a.n, a.n, a.n), jitter=0.1 if ct == fcg.HEX8 else 0.02)
 t1 = time.perf_counter()
-ev = fcg.Evaluator(m, kinematics=kin, path=path)
+mat = fcg.MAT_STVK if a.material == "stvk" else fcg.MAT_ELASTHYPER_COUPNEOHOOKE
+ev = fcg.Evaluator(m, kinematics=kin, path=path, material=mat)
 t2 = time.perf_counter()
 dev = torch.device("cuda:0")
 u = torch.from_numpy(m.u_col(1e-3 if kin == fcg.LINEAR else 5e-2)).to(dev)
@@ -36,7 +38,7 @@ for _ in range(a.reps):
     ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u, f, K)
     ts.append(ev.timing())
 ms = sorted(x[0] + x[1] for x in ts)[len(ts) // 2]
-print(json.dumps({"config": f"{a.celltype}-{a.kinem}-{a.n}^3", "path": int(ev.info.path),
+print(json.dumps({"config": f"{a.celltype}-{a.kinem}-{a.material}-{a.n}^3", "path": int(ev.info.path),
                   "elements": m.n_ele, "nnz": m.nnz, "ms_evaluate": ms,
                   "ms_element": sorted(ts)[len(ts) // 2][0], "ms_assemble": sorted(ts)[len(ts) // 2][1],
                   "elem_per_s": m.n_ele / (ms * 1e-3), "mesh_s": t1 - t0, "create_s": t2 - t1,
