@@ -64,6 +64,21 @@ constexpr int PLANE_REC_WORDS = 288;
 hipError_t launch_sweep_h8(const DeviceMesh& m, const double* d_u_col, bool want_k,
     bool overwrite, double* d_K, double* d_fint, hipStream_t stream);
 
+// Fused TSI blocks of the structured sweep (fcg_tsi_evaluate_fused): linear kinematics, StVK,
+// node-consistent thermo numbering (thermo LID = structural LID / 3, see fcg_tsi.hip).
+struct SweepTsi {
+  const double* v_col = nullptr;
+  const double* T_col = nullptr;
+  const double* Ngp = nullptr;  // shape values at the hex8 Gauss points [8][8]
+  double* Kst = nullptr;
+  double* Kts = nullptr;
+  double* Ktt = nullptr;
+  double* fT = nullptr;
+  double m = 0, T0 = 0, conduct = 0, kts = 0;  // kts = -timefac timefac_d
+};
+hipError_t launch_sweep_h8_tsi(const DeviceMesh& m, const double* d_u_col, bool overwrite,
+    double* d_K, double* d_fint, const SweepTsi& t, hipStream_t stream);
+
 struct Timing {
   bool enabled = false;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};

@@ -72,26 +72,43 @@ struct SweepArgs {
   int32_t* err;
   unsigned long long* stamps;  // diagnostic phase timers (NULL = off, the production setting)
   StVK mat;
+  // fused TSI blocks (TSI instantiation only): v, T by column LID (thermo LID = structural / 3),
+  // shape values at the Gauss points [8][8], the k_ST / k_TS / k_TT values and f_T by row LID
+  const double* v_col;
+  const double* T_col;
+  const double* Ngp;
+  double* Kst;
+  double* Kts;
+  double* Ktt;
+  double* fT;
+  double tsi_m, tsi_T0, tsi_k, tsi_kts;  // m, T_0, Fourier k, -timefac timefac_d
   int32_t tiles_x, tiles_y, seg_planes;
   int32_t I0, J0, K0, NI, NJ, NK;
   int32_t EX0, EY0, EZ0, EX, EY, EZ;  // element box; the node lattice box is EX+1 x EY+1 x EZ+1
 };
 
-template <int KIN>
+// node data per lattice column: X | u, and for TSI v | T
+template <bool TSI>
+constexpr int node_comps() { return TSI ? 10 : 6; }
+
+template <int KIN, bool TSI>
 struct SweepShared {
   alignas(16) double nx[3 * 4 * NSLOT * 8 * 2];  // sqrt|fac| N_XYZ, see nx2i()
   // TotLag: F (column-major) | S (Voigt) | c = fac / sqrt|fac|  (linear kinematics: unused)
   double gp[KIN ? 8 : 1][KIN ? NSLOT : 1][16];
-  double node[3][NNODE][6];           // X | u of the 6 x 6 node columns, ring by plane mod 3
+  // TSI: c = fac / sqrt|fac| | T_g | m c sqrt|fac| tr(B_L v)_g = m fac tr(e')_g | pad
+  alignas(16) double tg[TSI ? 8 : 1][TSI ? NSLOT : 1][4];
+  double node[3][NNODE][node_comps<TSI>()];  // node columns of the 6 x 6 grid, ring by plane mod 3
   uint32_t prec[3][PLANE_REC_WORDS];  // plane records, ring by plane mod 3
   double dN[8][8][3];
+  double Ng[TSI ? 8 : 1][8];  // TSI: shape values N_n at Gauss point g
   double w8[8];
   uint32_t neg[NSLOT];  // bit g set: fac < 0 at Gauss point g
   // lower-layer parts of the in-plane blocks (dz = 0) of node plane L+1: written by the D-side
   // lane k + 8, read by the U-side lane k of the next layer in the same instruction that precedes
   // the next write (LDS operations of a wavefront complete in order): one buffer suffices.
-  // [column][in-plane neighbour (dy+1)*3 + dx+1][3x3]
-  double hold[TX * TY][9][9];
+  // [column][in-plane neighbour (dy+1)*3 + dx+1][3x3 | TSI: k_ST 3 | k_TS 3 | k_TT 1]
+  double hold[TX * TY][9][TSI ? 16 : 9];
 };
 
 __device__ inline int ring(int p) { return (p % 3 + 3) % 3; }
@@ -114,10 +131,11 @@ __device__ inline int node_at(int ox, int oy, int oz) { return 4 * oz + (oy ? (o
 
 // Stage A for element slot s, Gauss point g of layer L (element e, -1 = none).  Written for a
 // small register footprint: node data stays in LDS and N_XYZ is recomputed where needed.
-template <int KIN>
-__device__ inline void sweep_stage_a(SweepShared<KIN>& sh, const SweepArgs& A, int s, int g,
+template <int KIN, bool TSI>
+__device__ inline void sweep_stage_a(SweepShared<KIN, TSI>& sh, const SweepArgs& A, int s, int g,
     int sx, int sy, int L, int e)
 {
+  constexpr int NC = node_comps<TSI>();
   const bool valid = e >= 0;
   const double* nd[8];
 #pragma unroll
@@ -145,10 +163,10 @@ __device__ inline void sweep_stage_a(SweepShared<KIN>& sh, const SweepArgs& A, i
     const double* zh = sh.node[ring(L + 1)][0];
     const double* pz = oz ? zh : zl;
     const int cxy = (sy + oy) * NXN + sx + ox;
-    const double* o = pz + 6 * cxy;
-    const double* ex_ = pz + 6 * (cxy + (ox ? -1 : 1));
-    const double* ey_ = pz + 6 * (cxy + (oy ? -NXN : NXN));
-    const double* ez_ = (oz ? zl : zh) + 6 * cxy;
+    const double* o = pz + NC * cxy;
+    const double* ex_ = pz + NC * (cxy + (ox ? -1 : 1));
+    const double* ey_ = pz + NC * (cxy + (oy ? -NXN : NXN));
+    const double* ez_ = (oz ? zl : zh) + NC * cxy;
     // edge vectors oriented along +xi, +eta, +zeta
     const double sgx = ox ? 1.0 : -1.0, sgy = oy ? 1.0 : -1.0, sgz = oz ? 1.0 : -1.0;
     const double a0 = sgx * (o[0] - ex_[0]), a1 = sgx * (o[1] - ex_[1]), a2 = sgx * (o[2] - ex_[2]);
@@ -160,6 +178,8 @@ __device__ inline void sweep_stage_a(SweepShared<KIN>& sh, const SweepArgs& A, i
   }
   const double det = h8_invert3x3(J);
   if (det == 0.0) bad = 2;
+  // the thermo element's check (4C_thermo_ele_impl.cpp:2663-2664)
+  else if (TSI && det < 1e-16 && bad == 0) bad = 1;
   const double fac = det * sh.w8[g];
   // missing element (outside the column set): all its LDS data become exact zeros
   const double sq = valid ? sqrt(fabs(fac)) : 0.0;
@@ -180,11 +200,17 @@ __device__ inline void sweep_stage_a(SweepShared<KIN>& sh, const SweepArgs& A, i
   };
   double E[6] = {0, 0, 0, 0, 0, 0};
   double F[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  double Tg = 0.0, trv = 0.0;  // TSI: T_g = N.T, sqrt|fac| tr(B_L v)
 #pragma unroll
   for (int n = 0; n < 8; ++n)
   {
     double n0, n1, n2;
     nxyz(n, n0, n1, n2);
+    if (TSI)
+    {
+      trv += n0 * nd[n][6] + n1 * nd[n][7] + n2 * nd[n][8];
+      Tg += sh.Ng[TSI ? g : 0][n] * nd[n][9];
+    }
     sh.nx[nx2i(0, g >> 1, s, n) + (g & 1)] = KIN == 0 ? n0 : ns * n0;
     sh.nx[nx2i(1, g >> 1, s, n) + (g & 1)] = KIN == 0 ? n1 : ns * n1;
     sh.nx[nx2i(2, g >> 1, s, n) + (g & 1)] = KIN == 0 ? n2 : ns * n2;
@@ -234,6 +260,13 @@ __device__ inline void sweep_stage_a(SweepShared<KIN>& sh, const SweepArgs& A, i
     for (int q = 0; q < 6; ++q) P[9 + q] = S[q];
     P[15] = cf;
   }
+  if (TSI)
+  {
+    double* t = sh.tg[TSI ? g : 0][TSI ? s : 0];
+    t[0] = cf;
+    t[1] = Tg;
+    t[2] = A.tsi_m * cf * trv;
+  }
   if (valid && bad)
   {
     atomicMax(&A.err[0], bad);
@@ -246,13 +279,29 @@ __device__ inline void sweep_stage_a(SweepShared<KIN>& sh, const SweepArgs& A, i
 
 // One element visit: accumulate the blocks (a, b1) into acc1 and (a, b2) into acc2 over the
 // Gauss points of element slot `slot`.  Acc layout: G[9] (row-major, G[3r+q] = sum a'_r b'_q)
-// then, for TotLag, H[6] and geo.
-template <int KIN, bool NEG>
-__device__ inline void sweep_visit(const SweepShared<KIN>& sh, int slot, int a, int b1, int b2,
+// then, for TotLag, H[6] and geo; for TSI (linear) sum c N_b a[3], sum c N_a T_g b[3] and
+// sum m fac tr(e') N_a N_b (the factors m, -timefac timefac_d and k enter in tsi_block).
+template <int KIN, bool NEG, bool TSI>
+__device__ inline void sweep_visit(const SweepShared<KIN, TSI>& sh, int slot, int a, int b1, int b2,
     uint32_t nm, double* acc1, double* acc2)
 {
   auto gp_body = [&](int g, double a0, double a1, double a2, double p0, double p1, double p2,
                      double q0, double q1, double q2) {
+    if (TSI)
+    {
+      // unflipped sqrt|fac| N_XYZ times c = fac / sqrt|fac| gives fac N_XYZ
+      const double* t = sh.tg[TSI ? g : 0][TSI ? slot : 0];
+      const double cf = t[0], Tg = t[1], qq = t[2];
+      const double Na = sh.Ng[TSI ? g : 0][a], N1 = sh.Ng[TSI ? g : 0][b1],
+                   N2 = sh.Ng[TSI ? g : 0][b2];
+      const double c1 = cf * N1, c2 = cf * N2, ct = cf * Na * Tg, qa = qq * Na;
+      acc1[9] += c1 * a0; acc1[10] += c1 * a1; acc1[11] += c1 * a2;
+      acc2[9] += c2 * a0; acc2[10] += c2 * a1; acc2[11] += c2 * a2;
+      acc1[12] += ct * p0; acc1[13] += ct * p1; acc1[14] += ct * p2;
+      acc2[12] += ct * q0; acc2[13] += ct * q1; acc2[14] += ct * q2;
+      acc1[15] += qa * N1;
+      acc2[15] += qa * N2;
+    }
     if (NEG && ((nm >> g) & 1u))
     {
       a0 = -a0;
@@ -321,6 +370,19 @@ __device__ inline void sweep_visit(const SweepShared<KIN>& sh, int slot, int a, 
   }
 }
 
+// TSI blocks of an accumulated (linear) part: k_ST(A,B) [3] | k_TS(A,B) [3] | k_TT(A,B)
+__device__ inline void tsi_block(const SweepArgs& A, const double* acc, double* Tv)
+{
+  const double m = A.tsi_m, mk = A.tsi_m * A.tsi_kts;
+  Tv[0] = m * acc[9];
+  Tv[1] = m * acc[10];
+  Tv[2] = m * acc[11];
+  Tv[3] = mk * acc[12];
+  Tv[4] = mk * acc[13];
+  Tv[5] = mk * acc[14];
+  Tv[6] = A.tsi_k * (acc[0] + acc[4] + acc[8]) - acc[15];
+}
+
 // K_AB of an accumulated part (isotropic StVK)
 template <int KIN>
 __device__ inline void block_k(const StVK& m, const double* acc, double* Kb)
@@ -359,11 +421,15 @@ __device__ inline void block_k(const StVK& m, const double* acc, double* Kb)
     st_last = now;                                                                                 \
   }
 
-template <int KIN, bool WANT_K, bool OVERWRITE>
+template <int KIN, bool WANT_K, bool OVERWRITE, bool TSI>
 __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
 {
-  __shared__ SweepShared<KIN> sh;
-  constexpr int NACC = KIN ? 16 : 9;
+  static_assert(!TSI || (KIN == 0 && WANT_K), "TSI is geometrically linear, full tangent");
+  __shared__ SweepShared<KIN, TSI> sh;
+  constexpr int NACC = (KIN || TSI) ? 16 : 9;
+  constexpr int NC = node_comps<TSI>();
+  constexpr int NLD = (NNODE * NC + 255) / 256;  // node-load items per lane
+  constexpr int NF = TSI ? 4 : 3;                // residual rows per node: f_S (3) | f_T
   const int tid = threadIdx.x;
   unsigned long long st_acc[2] = {0, 0};
   unsigned long long st_last = A.stamps ? __builtin_amdgcn_s_memtime() : 0ull;
@@ -382,6 +448,7 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
     (&sh.dN[0][0][0])[v] = A.tables[v];
   }
   if (tid < 8) sh.w8[tid] = A.tables[384 + tid];
+  if (TSI && tid < 64) (&sh.Ng[0][0])[tid] = A.Ngp[tid];
 
   // stage-A lane: element slot s, Gauss point g
   const int s = tid >> 3, g = tid & 7;
@@ -393,19 +460,32 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
     if (!exy_in || lz < A.EZ0 || lz >= A.EZ0 + A.EZ) return -1;
     return A.elem_at[(int64_t(lz - A.EZ0) * A.EY + (ey - A.EY0)) * A.EX + (ex - A.EX0)];
   };
-  // node-load lane: column ncol of the 6 x 6 node grid, component ncomp (X 0-2, u 3-5)
-  const bool n_lane = tid < NNODE * 6;
-  const int ncol = tid / 6, ncomp = tid - 6 * (tid / 6);
-  const int ni = i0 - 1 + ncol % NXN, nj = j0 - 1 + ncol / NXN;
-  const bool nxy_in =
-      n_lane && ni >= A.EX0 && ni <= A.EX0 + A.EX && nj >= A.EY0 && nj <= A.EY0 + A.EY;
-  const int64_t nlat_xy = nxy_in ? int64_t(nj - A.EY0) * LX + (ni - A.EX0) : 0;
-  auto load_node = [&](int P) -> double {
-    if (!nxy_in || P < A.EZ0 || P > A.EZ0 + A.EZ) return 0.0;
-    const int64_t li = int64_t(P - A.EZ0) * LX * LY + nlat_xy;
-    if (ncomp < 3) return A.lat_x[3 * li + ncomp];
+  // node-load items tid + 256 j: column ncol of the 6 x 6 node grid, component ncomp
+  // (X 0-2, u 3-5; TSI: v 6-8, T 9)
+  bool n_lane[NLD], nxy_in[NLD];
+  int ncol[NLD], ncomp[NLD];
+  int64_t nlat_xy[NLD];
+#pragma unroll
+  for (int j = 0; j < NLD; ++j)
+  {
+    const int v = tid + 256 * j;
+    n_lane[j] = v < NNODE * NC;
+    ncol[j] = v / NC;
+    ncomp[j] = v - NC * (v / NC);
+    const int ni = i0 - 1 + ncol[j] % NXN, nj = j0 - 1 + ncol[j] / NXN;
+    nxy_in[j] = n_lane[j] && ni >= A.EX0 && ni <= A.EX0 + A.EX && nj >= A.EY0 && nj <= A.EY0 + A.EY;
+    nlat_xy[j] = nxy_in[j] ? int64_t(nj - A.EY0) * LX + (ni - A.EX0) : 0;
+  }
+  auto load_node = [&](int j, int P) -> double {
+    if (!nxy_in[j] || P < A.EZ0 || P > A.EZ0 + A.EZ) return 0.0;
+    const int64_t li = int64_t(P - A.EZ0) * LX * LY + nlat_xy[j];
+    const int cp = ncomp[j];
+    if (cp < 3) return A.lat_x[3 * li + cp];
     const int dof = A.lat_dof[li];
-    return dof >= 0 ? A.u_col[dof + ncomp - 3] : 0.0;
+    if (dof < 0) return 0.0;
+    if (!TSI || cp < 6) return A.u_col[dof + cp - 3];
+    if (cp < 9) return A.v_col[dof + cp - 6];
+    return A.T_col[dof / 3];
   };
   auto load_rec = [&](int p, uint32_t* w) {
     const bool in = p >= kz0 && p < kz1;
@@ -432,11 +512,13 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
   const uint32_t vis0 = kVisit[k][0], vis1 = kVisit[k][1];
 
   // --- prologue: node planes kz0-1, kz0 and their records; prefetch plane kz0+1
-  if (n_lane)
-  {
-    sh.node[ring(kz0 - 1)][ncol][ncomp] = load_node(kz0 - 1);
-    sh.node[ring(kz0)][ncol][ncomp] = load_node(kz0);
-  }
+#pragma unroll
+  for (int j = 0; j < NLD; ++j)
+    if (n_lane[j])
+    {
+      sh.node[ring(kz0 - 1)][ncol[j]][ncomp[j]] = load_node(j, kz0 - 1);
+      sh.node[ring(kz0)][ncol[j]][ncomp[j]] = load_node(j, kz0);
+    }
   {
     uint32_t w[2];
     load_rec(kz0 - 1, w);
@@ -444,25 +526,32 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
     load_rec(kz0, w);
     store_rec(kz0, w);
   }
-  double node_nxt = n_lane ? load_node(kz0 + 1) : 0.0;
+  double node_nxt[NLD];
+#pragma unroll
+  for (int j = 0; j < NLD; ++j) node_nxt[j] = n_lane[j] ? load_node(j, kz0 + 1) : 0.0;
   uint32_t rec_nxt[2];
   load_rec(kz0 + 1, rec_nxt);
   int e_cur = load_elem(kz0 - 1);
-  for (int v = tid; v < TX * TY * 81; v += 256) (&sh.hold[0][0][0])[v] = 0.0;
-  double fkeep[3] = {0.0, 0.0, 0.0};  // lane k = 8: D-side residual part of plane L+1's rows
+  for (int v = tid; v < int(sizeof(sh.hold) / sizeof(double)); v += 256) (&sh.hold[0][0][0])[v] = 0.0;
+  double fkeep[NF];  // lane k = 8: D-side residual part of plane L+1's rows
+#pragma unroll
+  for (int d = 0; d < NF; ++d) fkeep[d] = 0.0;
   __syncthreads();
 
   for (int L = kz0 - 1; L < kz1; ++L)
   {
     const int e_nxt = load_elem(L + 1);
     // A. element stage
-    if (a_lane) sweep_stage_a<KIN>(sh, A, s, g, sx, sy, L, e_cur);
+    if (a_lane) sweep_stage_a<KIN, TSI>(sh, A, s, g, sx, sy, L, e_cur);
     __syncthreads();
     FCG_STAMP(0);
     // commit plane L+2 (nodes and record into plane L-1's ring slot), then prefetch plane L+3
-    if (n_lane) sh.node[ring(L + 2)][ncol][ncomp] = node_nxt;
+#pragma unroll
+    for (int j = 0; j < NLD; ++j)
+      if (n_lane[j]) sh.node[ring(L + 2)][ncol[j]][ncomp[j]] = node_nxt[j];
     store_rec(L + 2, rec_nxt);
-    node_nxt = n_lane ? load_node(L + 3) : 0.0;
+#pragma unroll
+    for (int j = 0; j < NLD; ++j) node_nxt[j] = n_lane[j] ? load_node(j, L + 3) : 0.0;
     load_rec(L + 3, rec_nxt);
 
     // B. visit stage
@@ -471,12 +560,15 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
     const uint32_t* recL1 = sh.prec[ring(L + 1)];
     // linear kinematics: this lane's share of f_A = sum_B K_AB u_B for the row node A of its side
     // (plane L + (k >> 3))
-    double fpart[3] = {0.0, 0.0, 0.0};
+    double fpart[NF];
+#pragma unroll
+    for (int d = 0; d < NF; ++d) fpart[d] = 0.0;
     if (WANT_K || KIN == 0)
     {
       // finished block t of this lane's column (this layer's elements): hold it, or write it plus
-      // the part held by lane k + 8 (same role, D side) since the previous layer
-      auto emit = [&](int act, int t, double* Kb) {
+      // the part held by lane k + 8 (same role, D side) since the previous layer.  TSI: Tv holds
+      // the block's k_ST / k_TS / k_TT entries (tsi_block), treated the same way.
+      auto emit = [&](int act, int t, double* Kb, double* Tv) {
         if (KIN == 0)
         {
           const int dx = t % 3 - 1, dy = (t / 3) % 3 - 1, dz = t / 9 - 1;
@@ -484,15 +576,25 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
           const double u0 = ub[0], u1 = ub[1], u2 = ub[2];
 #pragma unroll
           for (int r = 0; r < 3; ++r) fpart[r] += Kb[3 * r] * u0 + Kb[3 * r + 1] * u1 + Kb[3 * r + 2] * u2;
+          if (TSI)
+          {
+            // f_S += k_ST (T - T_0) (partition of unity), f_T = k_TT T (exact for linear TSI)
+            const double TB = ub[6];
+            const double dT = TB - A.tsi_T0;
+#pragma unroll
+            for (int r = 0; r < 3; ++r) fpart[r] += Tv[r] * dT;
+            fpart[NF - 1] += Tv[6] * TB;
+          }
         }
         // in-plane blocks: every lane of the pair reads the held entry first, then the holder
         // (D side) stores this layer's part and the U side adds the part held since last layer
         if (act == kActHold || act == kActWriteLHold)
         {
+          constexpr int NH = TSI ? 16 : 9;
           double* h = sh.hold[c][t - 9];
-          double held[9];
+          double held[NH];
 #pragma unroll
-          for (int i = 0; i < 9; ++i) held[i] = h[i];
+          for (int i = 0; i < NH; ++i) held[i] = h[i];
           // all reads issue before any write (the compiler must not sink the U side's reads into
           // its branch behind the D side's writes; the LDS executes a wavefront's ops in order)
           __asm__ volatile("" ::: "memory");
@@ -500,11 +602,17 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
           {
 #pragma unroll
             for (int i = 0; i < 9; ++i) h[i] = Kb[i];
+            if (TSI)
+#pragma unroll
+              for (int i = 0; i < 7; ++i) h[9 + i] = Tv[i];
           }
           else
           {
 #pragma unroll
             for (int i = 0; i < 9; ++i) Kb[i] = held[i] + Kb[i];
+            if (TSI)
+#pragma unroll
+              for (int i = 0; i < 7; ++i) Tv[i] = held[9 + i] + Tv[i];
           }
         }
         if (act == kActHold || !WANT_K) return;
@@ -528,6 +636,34 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
             else
               dst[r * len + qq] += Kb[3 * r + qq];
           }
+        if (TSI)
+        {
+          // node-consistent block graphs (checked by fcg_tsi_evaluate_fused): the k_ST rows of the
+          // node start at base / 3 (length len / 3), its k_TS row at base / 3, its k_TT row at
+          // base / 9; the neighbour's thermo column sits at pos / 3, its displacements at pos
+          const int64_t bst = base / 3, lst = len / 3, pst = pos / 3;
+#pragma unroll
+          for (int r = 0; r < 3; ++r)
+          {
+            double* d1 = A.Kst + bst + r * lst + pst;
+            double* d2 = A.Kts + bst + pos + r;
+            if (OVERWRITE)
+            {
+              *d1 = Tv[r];
+              *d2 = Tv[3 + r];
+            }
+            else
+            {
+              *d1 += Tv[r];
+              *d2 += Tv[3 + r];
+            }
+          }
+          double* d3 = A.Ktt + base / 9 + pst;
+          if (OVERWRITE)
+            *d3 = Tv[6];
+          else
+            *d3 += Tv[6];
+        }
       };
       double acc1[NACC], acc2[NACC];
 #pragma unroll
@@ -541,22 +677,23 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
         const int slot = (cx + (q & 1)) + EXN * (cy + (q >> 1));
         const uint32_t nm = sh.neg[slot];
         if (nm == 0u)
-          sweep_visit<KIN, false>(sh, slot, a, b1, b2, nm, acc1, acc2);
+          sweep_visit<KIN, false, TSI>(sh, slot, a, b1, b2, nm, acc1, acc2);
         else
-          sweep_visit<KIN, true>(sh, slot, a, b1, b2, nm, acc1, acc2);
+          sweep_visit<KIN, true, TSI>(sh, slot, a, b1, b2, nm, acc1, acc2);
         if ((w >> 24) & 1u)
         {
-          double Kb[9];
+          double Kb[9], Tv[7];
           block_k<KIN>(A.mat, acc2, Kb);
+          if (TSI) tsi_block(A, acc2, Tv);
 #pragma unroll
           for (int i = 0; i < NACC; ++i) acc2[i] = 0.0;
-          emit(int((w >> 21) & 7), int((w >> 16) & 31), Kb);
+          emit(int((w >> 21) & 7), int((w >> 16) & 31), Kb, Tv);
         }
       }
       // acc1: the self block's two halves meet in lane r = 2 (order: qy = 1 half + qy = 0 half)
       {
         const int pair = int((vis1 >> 26) & 3);
-        double Kb[9];
+        double Kb[9], Tv[7];
         block_k<KIN>(A.mat, acc1, Kb);
 #pragma unroll
         for (int i = 0; i < 9; ++i)
@@ -564,18 +701,28 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
           const double o = dpp_f64<kDppXor1>(Kb[i]);
           if (pair == kPairRecv) Kb[i] += o;
         }
-        if (pair != kPairGive) emit(int((vis1 >> 21) & 7), int((vis1 >> 11) & 31), Kb);
+        if (TSI)
+        {
+          tsi_block(A, acc1, Tv);
+#pragma unroll
+          for (int i = 0; i < 7; ++i)
+          {
+            const double o = dpp_f64<kDppXor1>(Tv[i]);
+            if (pair == kPairRecv) Tv[i] += o;
+          }
+        }
+        if (pair != kPairGive) emit(int((vis1 >> 21) & 7), int((vis1 >> 11) & 31), Kb, Tv);
       }
     }
     // residual rows of the column: the 8 lanes of a side sum their parts by a butterfly (every
     // lane ends with the same bits); lane 8 keeps plane L+1's D-side part for the next layer, lane
     // 0 adds the part lane 8 kept in the previous layer and writes plane L's rows.
     {
-      double f[3];
+      double f[NF];
       if (KIN == 0)
       {
 #pragma unroll
-        for (int d = 0; d < 3; ++d) f[d] = fpart[d];
+        for (int d = 0; d < NF; ++d) f[d] = fpart[d];
       }
       else
       {
@@ -605,9 +752,9 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
           f[2] += cc * (P[2] * t0 + P[5] * t1 + P[8] * t2);
         }
       }
-      double fp[3];
+      double fp[NF];
 #pragma unroll
-      for (int d = 0; d < 3; ++d)
+      for (int d = 0; d < NF; ++d)
       {
         f[d] += dpp_f64<kDppXor1>(f[d]);
         f[d] += dpp_f64<kDppXor2>(f[d]);
@@ -617,7 +764,7 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
       if (k == 8)
       {
 #pragma unroll
-        for (int d = 0; d < 3; ++d) fkeep[d] = f[d];
+        for (int d = 0; d < NF; ++d) fkeep[d] = f[d];
       }
       else if (k == 0 && wl)
       {
@@ -631,6 +778,14 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
               A.fint[row0 + d] = fp[d] + f[d];
             else
               A.fint[row0 + d] += fp[d] + f[d];
+          }
+          if (TSI)
+          {
+            // thermo row of the node = first structural row / 3 (checked at the fused call)
+            if (OVERWRITE)
+              A.fT[row0 / 3] = fp[NF - 1] + f[NF - 1];
+            else
+              A.fT[row0 / 3] += fp[NF - 1] + f[NF - 1];
           }
         }
       }
@@ -648,12 +803,10 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
 
 }  // namespace
 
-hipError_t launch_sweep_h8(const DeviceMesh& m, const double* d_u_col, bool want_k,
-    bool overwrite, double* d_K, double* d_fint, hipStream_t stream)
+namespace {
+SweepArgs sweep_args(const DeviceMesh& m, const double* d_u_col, double* d_K, double* d_fint)
 {
-  const int64_t ntiles = int64_t(m.tiles_x) * m.tiles_y * m.tiles_z;
-  if (ntiles == 0) return hipSuccess;
-  SweepArgs a;
+  SweepArgs a{};
   a.u_col = d_u_col;
   a.lat_x = m.lat_x;
   a.lat_dof = m.lat_dof;
@@ -670,17 +823,27 @@ hipError_t launch_sweep_h8(const DeviceMesh& m, const double* d_u_col, bool want
   a.seg_planes = m.seg_planes;
   a.I0 = m.I0; a.J0 = m.J0; a.K0 = m.K0; a.NI = m.NI; a.NJ = m.NJ; a.NK = m.NK;
   a.EX0 = m.EX0; a.EY0 = m.EY0; a.EZ0 = m.EZ0; a.EX = m.EX; a.EY = m.EY; a.EZ = m.EZ;
+  return a;
+}
+}  // namespace
+
+hipError_t launch_sweep_h8(const DeviceMesh& m, const double* d_u_col, bool want_k,
+    bool overwrite, double* d_K, double* d_fint, hipStream_t stream)
+{
+  const int64_t ntiles = int64_t(m.tiles_x) * m.tiles_y * m.tiles_z;
+  if (ntiles == 0) return hipSuccess;
+  const SweepArgs a = sweep_args(m, d_u_col, d_K, d_fint);
   const dim3 grid{static_cast<unsigned>(ntiles), 1, 1};
   const dim3 block{256, 1, 1};
 #define FCG_SWEEP(KIN)                                                                             \
   if (want_k && overwrite)                                                                         \
-    hipLaunchKernelGGL((sweep_h8_kernel<KIN, true, true>), grid, block, 0, stream, a);             \
+    hipLaunchKernelGGL((sweep_h8_kernel<KIN, true, true, false>), grid, block, 0, stream, a);      \
   else if (want_k)                                                                                 \
-    hipLaunchKernelGGL((sweep_h8_kernel<KIN, true, false>), grid, block, 0, stream, a);            \
+    hipLaunchKernelGGL((sweep_h8_kernel<KIN, true, false, false>), grid, block, 0, stream, a);     \
   else if (overwrite)                                                                              \
-    hipLaunchKernelGGL((sweep_h8_kernel<KIN, false, true>), grid, block, 0, stream, a);            \
+    hipLaunchKernelGGL((sweep_h8_kernel<KIN, false, true, false>), grid, block, 0, stream, a);     \
   else                                                                                             \
-    hipLaunchKernelGGL((sweep_h8_kernel<KIN, false, false>), grid, block, 0, stream, a);
+    hipLaunchKernelGGL((sweep_h8_kernel<KIN, false, false, false>), grid, block, 0, stream, a);
   if (m.kinem == 0)
   {
     FCG_SWEEP(0)
@@ -690,6 +853,32 @@ hipError_t launch_sweep_h8(const DeviceMesh& m, const double* d_u_col, bool want
     FCG_SWEEP(1)
   }
 #undef FCG_SWEEP
+  return hipGetLastError();
+}
+
+hipError_t launch_sweep_h8_tsi(const DeviceMesh& m, const double* d_u_col, bool overwrite,
+    double* d_K, double* d_fint, const SweepTsi& t, hipStream_t stream)
+{
+  const int64_t ntiles = int64_t(m.tiles_x) * m.tiles_y * m.tiles_z;
+  if (ntiles == 0) return hipSuccess;
+  SweepArgs a = sweep_args(m, d_u_col, d_K, d_fint);
+  a.v_col = t.v_col;
+  a.T_col = t.T_col;
+  a.Ngp = t.Ngp;
+  a.Kst = t.Kst;
+  a.Kts = t.Kts;
+  a.Ktt = t.Ktt;
+  a.fT = t.fT;
+  a.tsi_m = t.m;
+  a.tsi_T0 = t.T0;
+  a.tsi_k = t.conduct;
+  a.tsi_kts = t.kts;
+  const dim3 grid{static_cast<unsigned>(ntiles), 1, 1};
+  const dim3 block{256, 1, 1};
+  if (overwrite)
+    hipLaunchKernelGGL((sweep_h8_kernel<0, true, true, true>), grid, block, 0, stream, a);
+  else
+    hipLaunchKernelGGL((sweep_h8_kernel<0, true, false, true>), grid, block, 0, stream, a);
   return hipGetLastError();
 }
 

@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <climits>
 #include <cstring>
 #include <mutex>
@@ -72,6 +73,12 @@ struct TsiDevice {
   double* tables = nullptr;      // dN at GPs [npe][npe][3] | N at GPs [npe][npe] | dN at nodes | w
   double* scratch = nullptr;     // [n_inc][tsi_rec(npe)]
   int32_t* err = nullptr;        // [2]
+  // fused path (fcg_tsi_evaluate_fused): node-consistent numbering verified at create, the
+  // structural context it was last verified against, the k_TT graph on the device for that check
+  bool fusable = false;
+  double lambda = 0, mu = 0;
+  int32_t* col_tt = nullptr;
+  const void* fused_with = nullptr;
 };
 
 template <int NPE>
@@ -393,6 +400,50 @@ hipError_t upload(T** dst, const T* src, int64_t n, int64_t& bytes)
   return hipMemset(*dst, 0, sizeof(T) * n);
 }
 
+// The structural context of a fused call describes the same mesh with the node graph of the TSI
+// context: same elements, node coordinates and column DOFs, K rows = the 3 x 3 expansion of the k_TT rows.
+struct FusedCheckArgs {
+  int64_t n_node, n_ele8, n_rows_s;
+  const int32_t* s_dof_col;
+  const int32_t* t_dof_col_s;
+  const int32_t* s_ele;
+  const int32_t* t_ele;
+  const double* s_x;
+  const double* t_x;
+  const int64_t* rp_ss;
+  const int32_t* col_ss;
+  const int64_t* rp_tt;
+  const int32_t* col_tt;
+  int32_t* flag;
+};
+
+__global__ __launch_bounds__(256) void tsi_fused_check_kernel(FusedCheckArgs A)
+{
+  const int64_t i0 = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t st = int64_t(gridDim.x) * blockDim.x;
+  int bad = 0;
+  for (int64_t i = i0; i < A.n_node; i += st)
+    if (A.s_dof_col[i] != A.t_dof_col_s[i] || A.s_x[3 * i] != A.t_x[3 * i] ||
+        A.s_x[3 * i + 1] != A.t_x[3 * i + 1] || A.s_x[3 * i + 2] != A.t_x[3 * i + 2])
+      bad = 1;
+  for (int64_t i = i0; i < A.n_ele8; i += st)
+    if (A.s_ele[i] != A.t_ele[i]) bad = 1;
+  for (int64_t r = i0; r < A.n_rows_s; r += st)
+  {
+    const int64_t t = r / 3, d = r - 3 * t;
+    const int64_t b = A.rp_tt[t], lt = A.rp_tt[t + 1] - b;
+    const int64_t rb = A.rp_ss[r];
+    if (rb != 9 * b + 3 * d * lt || A.rp_ss[r + 1] - rb != 3 * lt)
+    {
+      bad = 1;
+      continue;
+    }
+    for (int64_t j = 0; j < 3 * lt; ++j)
+      if (A.col_ss[rb + j] != 3 * A.col_tt[b + j / 3] + int32_t(j % 3)) bad = 1;
+  }
+  if (bad) atomicOr(A.flag, 1);
+}
+
 std::mutex g_tsi_err_mutex;
 std::string g_tsi_create_error;
 
@@ -431,7 +482,7 @@ int fcg_tsi_destroy(fcg_tsi_ctx* ctx)
   fcg::TsiDevice& d = ctx->d;
   void* ptrs[] = {d.ele_nodes, d.ele_gid, d.node_x, d.dof_col_s, d.dof_col_t, d.inc_of, d.inc_ptr,
       d.rn_srow, d.rn_trow, d.pos_st, d.pos_ts, d.pos_tt, d.rowptr_st, d.rowptr_ts, d.rowptr_tt,
-      d.tables, d.scratch, d.err};
+      d.tables, d.scratch, d.err, d.col_tt};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -597,6 +648,26 @@ int fcg_tsi_create(const fcg_tsi_desc* D, fcg_tsi_ctx** out)
     }
   }
 
+  // node-consistent numbering (what fcg_tsi_evaluate_fused requires): thermo DOF LIDs are the
+  // structural ones / 3 and the three block graphs are expansions of one node graph (the k_TT graph)
+  bool fusable = npe == 8 && D->n_rows_s == 3 * D->n_rows_t && D->n_cols_s == 3 * D->n_cols_t;
+  for (int64_t n = 0; fusable && n < D->n_node; ++n)
+    fusable = D->node_dof_col_s[n] == 3 * D->node_dof_col_t[n] &&
+              D->node_dof_row_s[n] == (D->node_dof_row_t[n] < 0 ? D->node_dof_row_s[n] : 3 * D->node_dof_row_t[n]);
+  for (int64_t t = 0; fusable && t < D->n_rows_t; ++t)
+  {
+    const int64_t b = D->rowptr_tt[t], lt = D->rowptr_tt[t + 1] - b;
+    fusable = D->rowptr_ts[t] == 3 * b && D->rowptr_ts[t + 1] - D->rowptr_ts[t] == 3 * lt;
+    for (int d = 0; fusable && d < 3; ++d)
+      fusable = D->rowptr_st[3 * t + d] == 3 * b + d * lt &&
+                std::memcmp(D->col_st + D->rowptr_st[3 * t + d], D->col_tt + b, sizeof(int32_t) * lt) == 0;
+    for (int64_t j = 0; fusable && j < 3 * lt; ++j)
+      fusable = D->col_ts[3 * b + j] == 3 * D->col_tt[b + j / 3] + int32_t(j % 3);
+  }
+  if (fusable && D->n_rows_t > 0)
+    fusable = D->rowptr_st[D->n_rows_s] == 3 * D->rowptr_tt[D->n_rows_t] &&
+              D->rowptr_ts[D->n_rows_t] == 3 * D->rowptr_tt[D->n_rows_t];
+
   auto* ctx = new fcg_tsi_ctx();
   ctx->device = D->device;
   hipError_t he = hipSetDevice(D->device);
@@ -626,7 +697,10 @@ int fcg_tsi_create(const fcg_tsi_desc* D, fcg_tsi_ctx** out)
     const double b1 = c1 * D->poisson / (1.0 - 2.0 * D->poisson);
     const double mu = 0.5 * c1, lambda = b1;
     d.m = (-1.0) * (2.0 * mu + 3.0 * lambda) * D->thexpans;
+    d.lambda = lambda;
+    d.mu = mu;
   }
+  d.fusable = fusable;
   d.T0 = D->inittemp;
   d.conduct = D->conduct;
   std::vector<int32_t> eg;
@@ -659,6 +733,7 @@ int fcg_tsi_create(const fcg_tsi_desc* D, fcg_tsi_ctx** out)
   chk(upload(&d.tables, tab.data(), int64_t(tab.size()), bytes));
   chk(upload<double>(&d.scratch, nullptr, n_inc * fcg::tsi_rec(npe), bytes));
   chk(upload<int32_t>(&d.err, nullptr, 2, bytes));
+  if (fusable) chk(upload(&d.col_tt, D->col_tt, d.nnz_tt, bytes));
   if (he != hipSuccess)
   {
     set_tsi_create_error(std::string("HIP allocation/copy failed: ") + hipGetErrorString(he));
@@ -757,6 +832,120 @@ int fcg_tsi_evaluate_device(fcg_tsi_ctx* ctx, int parts, int mode, const double*
     int32_t gid = -1;
     if (errv[1] >= 0 && errv[1] < d.n_ele)
       (void)hipMemcpy(&gid, d.ele_gid + errv[1], sizeof(int32_t), hipMemcpyDeviceToHost);
+    if (bad_ele_gid) *bad_ele_gid = gid;
+    ctx->last_error = errv[0] == FCG_ERR_NODAL_DETJ
+                          ? "non-positive jacobian determinant in element " + std::to_string(gid)
+                          : "singular 3x3 matrix in element " + std::to_string(gid);
+    return errv[0];
+  }
+  return FCG_OK;
+}
+
+int fcg_tsi_evaluate_fused(fcg_ctx* sctx, fcg_tsi_ctx* ctx, int mode, const double* d_u_col,
+    const double* d_v_col, const double* d_T_col, double timefac, double timefac_d,
+    double* d_fs_row, double* d_Kss, double* d_Kst, double* d_fT_row, double* d_Ktt,
+    double* d_Kts, void* stream_ptr, int32_t* bad_ele_gid)
+{
+  if (!ctx) return FCG_ERR_ARG;
+  if (!sctx)
+  {
+    ctx->last_error = "no structural context";
+    return FCG_ERR_ARG;
+  }
+  fcg::TsiDevice& d = ctx->d;
+  const fcg::DeviceMesh& m = sctx->mesh;
+  auto rel_eq = [](double a, double b) { return std::fabs(a - b) <= 1e-14 * std::fabs(b); };
+  if (m.path != FCG_PATH_STRUCTURED || m.kinem != 0 || m.material != FCG_MAT_STVK || m.npe != 8 ||
+      !d.fusable || sctx->device != ctx->device || m.n_node != d.n_node || m.n_ele != d.n_ele ||
+      m.n_rows != d.n_rows_s || m.n_cols != d.n_cols_s || m.nnz != 9 * d.nnz_tt ||
+      !rel_eq(m.lambda, d.lambda) || !rel_eq(m.mu, d.mu))
+  {
+    ctx->last_error =
+        "fused TSI needs a structured hex8 StVK context with linear kinematics, the TSI material's "
+        "E and nu, and node-consistent thermo numbering (thermo LID = structural LID / 3)";
+    return FCG_ERR_ARG;
+  }
+  if ((mode != FCG_ACCUMULATE && mode != FCG_OVERWRITE) ||
+      (d.n_ele > 0 && (!d_u_col || !d_v_col || !d_T_col)) ||
+      (d.n_rows_s > 0 && (!d_fs_row || !d_Kss || !d_Kst || !d_fT_row || !d_Ktt || !d_Kts)))
+  {
+    ctx->last_error = "invalid fused TSI evaluate arguments";
+    return FCG_ERR_ARG;
+  }
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = stream_ptr ? static_cast<hipStream_t>(stream_ptr) : ctx->stream;
+  hipError_t he = hipSuccess;
+  if (d.fused_with != static_cast<const void*>(sctx))
+  {
+    fcg::FusedCheckArgs c;
+    c.n_node = d.n_node;
+    c.n_ele8 = d.n_ele * 8;
+    c.n_rows_s = d.n_rows_s;
+    c.s_dof_col = m.node_dof_col;
+    c.t_dof_col_s = d.dof_col_s;
+    c.s_ele = m.ele_nodes;
+    c.t_ele = d.ele_nodes;
+    c.s_x = m.node_x;
+    c.t_x = d.node_x;
+    c.rp_ss = m.rowptr;
+    c.col_ss = m.col_lid;
+    c.rp_tt = d.rowptr_tt;
+    c.col_tt = d.col_tt;
+    c.flag = d.err;
+    int32_t flag = 0;
+    he = hipMemcpyAsync(d.err, &flag, sizeof(flag), hipMemcpyHostToDevice, s);
+    if (he == hipSuccess)
+    {
+      const int64_t work = std::max(std::max(d.n_node, d.n_ele * 8), d.n_rows_s);
+      hipLaunchKernelGGL(fcg::tsi_fused_check_kernel, dim3(fcg::grid_for((work + 255) / 256, 4096)),
+          dim3(256), 0, s, c);
+      he = hipGetLastError();
+    }
+    if (he == hipSuccess) he = hipMemcpyAsync(&flag, d.err, sizeof(flag), hipMemcpyDeviceToHost, s);
+    if (he == hipSuccess) he = hipStreamSynchronize(s);
+    if (he != hipSuccess)
+    {
+      ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
+      return FCG_ERR_DEVICE;
+    }
+    if (flag)
+    {
+      ctx->last_error = "structural context and TSI context do not share the mesh and node graph";
+      return FCG_ERR_ARG;
+    }
+    d.fused_with = sctx;
+  }
+  const int32_t init[2] = {0, INT32_MAX};
+  he = hipMemcpyAsync(m.err, init, sizeof(init), hipMemcpyHostToDevice, s);
+  if (he == hipSuccess)
+  {
+    fcg::SweepTsi t;
+    t.v_col = d_v_col;
+    t.T_col = d_T_col;
+    t.Ngp = d.tables + 8 * 8 * 3;
+    t.Kst = d_Kst;
+    t.Kts = d_Kts;
+    t.Ktt = d_Ktt;
+    t.fT = d_fT_row;
+    t.m = d.m;
+    t.T0 = d.T0;
+    t.conduct = d.conduct;
+    t.kts = -timefac * timefac_d;  // linear_coupled_tang (4C_thermo_ele_impl.cpp:1189)
+    he = fcg::launch_sweep_h8_tsi(m, d_u_col, mode == FCG_OVERWRITE, d_Kss, d_fs_row, t, s);
+  }
+  int32_t errv[2] = {0, INT32_MAX};
+  if (he == hipSuccess) he = hipMemcpyAsync(errv, m.err, sizeof(errv), hipMemcpyDeviceToHost, s);
+  if (he == hipSuccess) he = hipStreamSynchronize(s);
+  if (he != hipSuccess)
+  {
+    ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
+    return FCG_ERR_DEVICE;
+  }
+  if (errv[0] != 0)
+  {
+    int32_t gid = -1;
+    if (errv[1] >= 0 && errv[1] < m.n_ele)
+      (void)hipMemcpy(&gid, m.ele_gid + errv[1], sizeof(int32_t), hipMemcpyDeviceToHost);
     if (bad_ele_gid) *bad_ele_gid = gid;
     ctx->last_error = errv[0] == FCG_ERR_NODAL_DETJ
                           ? "non-positive jacobian determinant in element " + std::to_string(gid)

@@ -82,6 +82,7 @@ EXPORTS = ["fcg_create", "fcg_destroy", "fcg_last_error", "fcg_evaluate", "fcg_e
            "fcg_neumann_surface", "fcg_neumann_volume",
            "fcg_graph_build_device",
            "fcg_tsi_create", "fcg_tsi_destroy", "fcg_tsi_last_error", "fcg_tsi_evaluate_device",
+           "fcg_tsi_evaluate_fused",
            "fcg_box_mesh_create", "fcg_box_mesh_destroy", "fcg_box_mesh_desc", "fcg_box_mesh_maps",
            "fcg_box_mesh_counts"]
 
@@ -151,6 +152,8 @@ def lib():
     L.fcg_tsi_last_error.restype = ctypes.c_char_p
     L.fcg_tsi_evaluate_device.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_double,
                                           ctypes.c_double, vp, vp, vp, vp, vp, vp, _i32p]
+    L.fcg_tsi_evaluate_fused.argtypes = [vp, vp, ctypes.c_int, vp, vp, vp, ctypes.c_double,
+                                         ctypes.c_double, vp, vp, vp, vp, vp, vp, vp, _i32p]
     _lib = L
     return L
 
@@ -550,6 +553,20 @@ class TsiEvaluator:
                                            _tensor_ptr(T_col), float(timefac), float(timefac_d),
                                            _tensor_ptr(fs), _tensor_ptr(Kst), _tensor_ptr(fT),
                                            _tensor_ptr(Ktt), _tensor_ptr(Kts), s, ctypes.byref(bad))
+        if rc != 0:
+            raise FcgError(rc, lib().fcg_tsi_last_error(self._h).decode(), bad.value)
+
+    def evaluate_fused(self, struct_ev, mode, u_col, v_col, T_col, timefac=1.0, timefac_d=1.0,
+                       fs=None, Kss=None, Kst=None, fT=None, Ktt=None, Kts=None, stream=None):
+        """fcg_tsi_evaluate_fused: the whole monolithic tangent (K_SS, k_ST, k_TS, k_TT) and both
+        residuals in one sweep; `struct_ev` is the structured linear StVK Evaluator of the mesh."""
+        bad = ctypes.c_int32(-1)
+        s = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
+        rc = lib().fcg_tsi_evaluate_fused(struct_ev._h, self._h, mode, _tensor_ptr(u_col),
+                                          _tensor_ptr(v_col), _tensor_ptr(T_col), float(timefac),
+                                          float(timefac_d), _tensor_ptr(fs), _tensor_ptr(Kss),
+                                          _tensor_ptr(Kst), _tensor_ptr(fT), _tensor_ptr(Ktt),
+                                          _tensor_ptr(Kts), s, ctypes.byref(bad))
         if rc != 0:
             raise FcgError(rc, lib().fcg_tsi_last_error(self._h).decode(), bad.value)
 

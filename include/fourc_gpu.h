@@ -275,6 +275,25 @@ const char* fcg_tsi_last_error(const fcg_tsi_ctx* ctx);
 int fcg_tsi_evaluate_device(fcg_tsi_ctx* ctx, int parts, int mode, const double* d_v_col,
     const double* d_T_col, double timefac, double timefac_d, double* d_fs_row, double* d_Kst,
     double* d_fT_row, double* d_Ktt, double* d_Kts, void* stream, int32_t* bad_ele_gid);
+/*
+ * The whole monolithic TSI tangent and both residuals in ONE pass of the structured hex8 sweep:
+ * what fcg_evaluate_device(sctx, FCG_ACTION_NLNSTIFF, mode, d_u_col, d_fs_row, d_Kss) followed by
+ * fcg_tsi_evaluate_device(ctx, all parts, mode, ...) computes (TSI::Monolithic::evaluate,
+ * 4C_tsi_monolithic.cpp: apply_str_coupl_matrix / apply_thr_coupl_matrix_conv_heat plus the two
+ * field evaluates), with each element's Gauss-point work done once for all five blocks.
+ *   sctx   structured (FCG_PATH_STRUCTURED) hex8, FCG_LINEAR, FCG_MAT_STVK with the TSI material's
+ *          E and nu, on the same mesh, elements and column DOFs as ctx
+ *   ctx    node-consistent thermo numbering: thermo LID = structural LID / 3 in the row and
+ *          column maps, k_ST / k_TS / k_TT rows the node graph's expansions (what 4C's cloned
+ *          thermo discretization with one DOF per node yields)
+ *   mode   applies to all outputs (f_S is the full residual: K u + thermal stress part)
+ * Returns FCG_ERR_ARG (last_error says why) when the contexts do not qualify; the first call
+ * with a structural context checks mesh and graph identity on the device.
+ */
+int fcg_tsi_evaluate_fused(fcg_ctx* sctx, fcg_tsi_ctx* ctx, int mode, const double* d_u_col,
+    const double* d_v_col, const double* d_T_col, double timefac, double timefac_d,
+    double* d_fs_row, double* d_Kss, double* d_Kst, double* d_fT_row, double* d_Ktt,
+    double* d_Kts, void* stream, int32_t* bad_ele_gid);
 
 /* ------------------------------------------------------------------------------------------
  * Structured-box discretization builder: a restatement of 4C's GridGenerator

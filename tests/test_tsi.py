@@ -276,3 +276,118 @@ def test_tsi_result_description_on_device(name):
     for r in fx["results"]:
         got = prob.result(d, T, r)
         assert abs(got - r["value"]) <= r["tol"], (r, got)
+
+
+# ------------------------------------------------------------- fused structured sweep (config 5)
+def _gpu_fused(mesh, tev, ev, u, v, Tn, mode=fcg.OVERWRITE, init=None):
+    torch, dev = _dev()
+    g = tev.graph
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).to(dev)
+    out = {k: torch.full((n,), float("nan"), dtype=torch.float64, device=dev)
+           for k, n in (("Kss", mesh.nnz), ("fs", mesh.n_rows), ("Kst", g.nnz_st),
+                        ("Kts", g.nnz_ts), ("Ktt", g.nnz_tt), ("fT", g.n_rows_t))}
+    if init is not None:
+        for k in out:
+            out[k] = t(init[k])
+    tev.evaluate_fused(ev, mode, t(u), t(v), t(Tn), 1.0, 1.0 / DT, **out)
+    torch.cuda.synchronize()
+    return {k: x.cpu().numpy() for k, x in out.items()}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("iv,rank,nranks,jitter", [((5, 4, 3), 0, 1, 0.1), ((9, 6, 5), 0, 1, 0.0),
+                                                    ((6, 5, 4), 1, 2, 0.1), ((8, 8, 8), 5, 8, 0.05)])
+def test_tsi_fused_matches_oracle_and_separate_path(iv, rank, nranks, jitter):
+    _dev()
+    mesh = fcg.BoxMesh(fcg.HEX8, iv, jitter=jitter, seed=3, rank=rank, nranks=nranks)
+    u, v, Tn = _fields(mesh)
+    ev = fcg.Evaluator(mesh, kinematics=fcg.LINEAR, youngs=E, poisson=NU, path=fcg.PATH_STRUCTURED)
+    tev = fcg.TsiEvaluator(mesh, E, NU, ALPHA, T0, COND)
+    g = tev.graph
+    r = _gpu_fused(mesh, tev, ev, u, v, Tn)
+    for k, x in r.items():
+        assert np.all(np.isfinite(x)), k
+    Kss, Kst, Kts, Ktt, fs, fT = _oracle_blocks(mesh, g, u, v, Tn)
+    for name, D, rp, cl in (("Kss", Kss, mesh.rowptr, mesh.col_lid),
+                            ("Kst", Kst, g.rowptr_st, g.col_st), ("Kts", Kts, g.rowptr_ts, g.col_ts),
+                            ("Ktt", Ktt, g.rowptr_tt, g.col_tt)):
+        ref = _csr_vals(D, rp, cl)
+        assert _rel(r[name], ref) <= 1e-12, (name, _rel(r[name], ref))
+        assert np.abs(r[name] - ref).max() <= 1e-12 * np.abs(ref).max(), name
+    assert _rel(r["fs"], fs) <= 1e-10, _rel(r["fs"], fs)
+    assert _rel(r["fT"], fT) <= 1e-10, _rel(r["fT"], fT)
+    # the two-kernel device path gives the same numbers (to rounding)
+    sep = _gpu_all(mesh, tev, ev, u, v, Tn)
+    for k in r:
+        tol = 1e-11 if k in ("fs", "fT") else 1e-13
+        assert np.abs(r[k] - sep[k]).max() <= tol * max(np.abs(sep[k]).max(), 1e-300), k
+
+
+@pytest.mark.gpu
+def test_tsi_fused_accumulate_and_reproducible():
+    _dev()
+    mesh = fcg.BoxMesh(fcg.HEX8, (6, 5, 4), jitter=0.1)
+    u, v, Tn = _fields(mesh)
+    ev = fcg.Evaluator(mesh, kinematics=fcg.LINEAR, youngs=E, poisson=NU, path=fcg.PATH_STRUCTURED)
+    tev = fcg.TsiEvaluator(mesh, E, NU, ALPHA, T0, COND)
+    a = _gpu_fused(mesh, tev, ev, u, v, Tn)
+    b = _gpu_fused(mesh, tev, ev, u, v, Tn)
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
+    rng = np.random.default_rng(2)
+    init = {k: rng.standard_normal(len(x)) for k, x in a.items()}
+    c = _gpu_fused(mesh, tev, ev, u, v, Tn, mode=fcg.ACCUMULATE, init=init)
+    for k in init:
+        np.testing.assert_allclose(c[k], init[k] + a[k], rtol=0, atol=1e-12 * np.abs(a[k]).max())
+
+
+@pytest.mark.gpu
+def test_tsi_fused_rejects_unqualified_contexts():
+    _dev()
+    mesh = fcg.BoxMesh(fcg.HEX8, (3, 3, 3))
+    u, v, Tn = _fields(mesh)
+    tev = fcg.TsiEvaluator(mesh, E, NU, ALPHA, T0, COND)
+    for ev in (fcg.Evaluator(mesh, kinematics=fcg.LINEAR, youngs=E, poisson=NU, path=fcg.PATH_GENERAL),
+               fcg.Evaluator(mesh, kinematics=fcg.TOTLAG, youngs=E, poisson=NU),
+               fcg.Evaluator(mesh, kinematics=fcg.LINEAR, youngs=2 * E, poisson=NU)):
+        with pytest.raises(fcg.FcgError) as ei:
+            _gpu_fused(mesh, tev, ev, u, v, Tn)
+        assert ei.value.code == 3
+    # a structural context of another mesh fails the device identity check
+    other = fcg.BoxMesh(fcg.HEX8, (3, 3, 3), jitter=0.1)
+    ev = fcg.Evaluator(other, kinematics=fcg.LINEAR, youngs=E, poisson=NU, path=fcg.PATH_STRUCTURED)
+    with pytest.raises(fcg.FcgError) as ei:
+        _gpu_fused(mesh, tev, ev, u, v, Tn)
+    assert ei.value.code == 3 and "do not share" in str(ei.value)
+    hex27 = fcg.BoxMesh(fcg.HEX27, (1, 1, 1))
+    with pytest.raises(fcg.FcgError) as ei:
+        _gpu_fused(hex27, fcg.TsiEvaluator(hex27, E, NU, ALPHA, T0, COND),
+                   fcg.Evaluator(hex27, kinematics=fcg.LINEAR, youngs=E, poisson=NU),
+                   *_fields(hex27))
+    assert ei.value.code == 3
+
+
+@pytest.mark.gpu
+def test_tsi_fused_full_size_properties():
+    """Config 5 at 100^3 hex8 (1M elements): fused and two-kernel paths agree; f_T = K_TT T and
+    f_S = K_SS u + K_ST (T - T_0) hold through the library's SpMV."""
+    torch, dev = _dev()
+    mesh = fcg.BoxMesh(fcg.HEX8, (100, 100, 100))
+    u, v, Tn = _fields(mesh)
+    ev = fcg.Evaluator(mesh, kinematics=fcg.LINEAR, youngs=E, poisson=NU, path=fcg.PATH_STRUCTURED)
+    tev = fcg.TsiEvaluator(mesh, E, NU, ALPHA, T0, COND)
+    g = tev.graph
+    r = _gpu_fused(mesh, tev, ev, u, v, Tn)
+    sep = _gpu_all(mesh, tev, ev, u, v, Tn)
+    for k in r:
+        # residuals: the fused pass sums f_T = K_TT T (T ~ 300 against rows summing to ~0), the
+        # two-kernel path k grad T -- equal to the residual tolerance, not to the last bits
+        tol = 1e-11 if k in ("fs", "fT") else 1e-13
+        assert np.abs(r[k] - sep[k]).max() <= tol * np.abs(sep[k]).max(), k
+    # CSR products on the host (scipy) for the size-independent identities
+    sp = pytest.importorskip("scipy.sparse")
+    Ktt = sp.csr_matrix((r["Ktt"], g.col_tt, g.rowptr_tt), shape=(g.n_rows_t, g.n_cols_t))
+    Kss = sp.csr_matrix((r["Kss"], mesh.col_lid, mesh.rowptr), shape=(mesh.n_rows, mesh.n_cols))
+    Kst = sp.csr_matrix((r["Kst"], g.col_st, g.rowptr_st), shape=(mesh.n_rows, g.n_cols_t))
+    assert _rel(Ktt @ Tn, r["fT"]) <= 1e-12
+    assert _rel(Kss @ u + Kst @ (Tn - T0), r["fs"]) <= 1e-12
