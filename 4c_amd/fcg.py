@@ -162,6 +162,47 @@ def _np_ptr(a, t):
     return a.ctypes.data_as(t)
 
 
+def lattice_ijk(ele_nodes):
+    """Element lattice positions (ex, ey, ez) of a hex8 mesh whose elements stack like a
+    GridGenerator box: neighbours share whole faces in 4C node order (+x: nodes 1 2 6 5 of the
+    element are 0 3 7 4 of the neighbour; +y: 3 2 6 7 -> 0 1 5 4; +z: 4 5 6 7 -> 0 1 2 3).
+    Returns an int32 [n_ele][3] array (minimum 0), or None if the mesh is not such a lattice --
+    the fcg_desc.ele_ijk hint, which fcg_create verifies again."""
+    en = np.asarray(ele_nodes, dtype=np.int64).reshape(-1, 8)
+    n = len(en)
+    if n == 0:
+        return None
+    dirs = (((1, 2, 6, 5), (0, 3, 7, 4), (1, 0, 0)), ((3, 2, 6, 7), (0, 1, 5, 4), (0, 1, 0)),
+            ((4, 5, 6, 7), (0, 1, 2, 3), (0, 0, 1)))
+    maps = []
+    for hi, lo, _ in dirs:
+        mhi = {tuple(r): e for e, r in enumerate(en[:, list(hi)].tolist())}
+        mlo = {tuple(r): e for e, r in enumerate(en[:, list(lo)].tolist())}
+        maps.append((mhi, mlo))
+    ijk = np.full((n, 3), np.iinfo(np.int64).min, dtype=np.int64)
+    ijk[0] = 0
+    stack = [0]
+    while stack:
+        e = stack.pop()
+        for (hi, lo, off), (mhi, mlo) in zip(dirs, maps):
+            for nb, sgn in ((mlo.get(tuple(en[e, list(hi)].tolist())), 1),
+                            (mhi.get(tuple(en[e, list(lo)].tolist())), -1)):
+                if nb is None:
+                    continue
+                want = ijk[e] + sgn * np.asarray(off)
+                if ijk[nb, 0] == np.iinfo(np.int64).min:
+                    ijk[nb] = want
+                    stack.append(nb)
+                elif not np.array_equal(ijk[nb], want):
+                    return None
+    if (ijk[:, 0] == np.iinfo(np.int64).min).any():
+        return None
+    ijk -= ijk.min(axis=0)
+    if len(np.unique(ijk, axis=0)) != n or ijk.max() >= 2 ** 31:
+        return None
+    return np.ascontiguousarray(ijk, dtype=np.int32)
+
+
 class Discretization:
     """Arrays of one rank's discretization as 4C holds them after FillComplete (the fcg_desc
     contents), for meshes that are not GridGenerator boxes -- e.g. the reference's input files."""
@@ -182,10 +223,12 @@ class Discretization:
         self.n_rows = len(self.rowptr) - 1
         self.n_cols = int(n_cols) if n_cols is not None else self.n_rows
         self.nnz = int(self.rowptr[-1])
+        self.ele_ijk = None  # optional structured-lattice hint (lattice_ijk)
 
     @staticmethod
-    def from_elements(celltype, ele_nodes, node_x):
-        """Single-rank discretization: DOF LID = 3 * node + d, CSR graph of the element couplings."""
+    def from_elements(celltype, ele_nodes, node_x, lattice=False):
+        """Single-rank discretization: DOF LID = 3 * node + d, CSR graph of the element couplings.
+        lattice=True attaches the structured-lattice hint (hex8 meshes stacked like a box)."""
         en = np.asarray(ele_nodes, dtype=np.int64)
         n_node = len(node_x)
         nbr = [set() for _ in range(n_node)]
@@ -200,7 +243,10 @@ class Discretization:
                 cols.extend(cd)
                 rows.append(len(cols))
         dof = 3 * np.arange(n_node, dtype=np.int32)
-        return Discretization(celltype, en, node_x, dof, dof, np.array(rows), np.array(cols))
+        dis = Discretization(celltype, en, node_x, dof, dof, np.array(rows), np.array(cols))
+        if lattice and celltype == HEX8:
+            dis.ele_ijk = lattice_ijk(en)
+        return dis
 
     def desc(self, kinematics, youngs, poisson, device=0, path=PATH_AUTO, material=MAT_STVK):
         d = FcgDesc()
@@ -219,7 +265,8 @@ class Discretization:
         d.node_dof_kcol = None
         d.rowptr = _np_ptr(self.rowptr, _i64p)
         d.col_lid = _np_ptr(self.col_lid, _i32p)
-        d.ele_ijk = None
+        d.ele_ijk = (_np_ptr(self.ele_ijk, _i32p)
+                     if self.ele_ijk is not None and path != PATH_GENERAL else None)
         d.path = path
         d.material = material
         return d

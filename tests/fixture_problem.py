@@ -22,10 +22,10 @@ def kinematics_of(fx):
     return fcg.LINEAR if k.pop() == "linear" else fcg.TOTLAG
 
 
-def discretization(prob):
+def discretization(prob, lattice=False):
     ct = celltype_of(prob.fx)
     en = [[prob.lid[n] for n in el["nodes"]] for el in prob.fx["elements"]]
-    return fcg.Discretization.from_elements(ct, en, prob.X)
+    return fcg.Discretization.from_elements(ct, en, prob.X, lattice=lattice)
 
 
 def fext(prob, t):

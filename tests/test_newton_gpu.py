@@ -52,6 +52,23 @@ def test_result_description_on_device(name):
         assert abs(got - r["value"]) <= r["tol"], (r, got, nt.history)
 
 
+def test_result_description_structured_sweep():
+    """The reference's hex8 known answer through the structured row-block sweep (lattice hint)."""
+    _dev()
+    fx = json.load(open(os.path.join(GOLD, "solid_ele_hex8_Standard_linear.json")))
+    prob = fp.problem(fx)
+    dis = fp.discretization(prob, lattice=True)
+    ev = fcg.Evaluator(dis, kinematics=fcg.LINEAR, youngs=prob.E, poisson=prob.nu,
+                       path=fcg.PATH_STRUCTURED)
+    assert ev.info.path == fcg.PATH_STRUCTURED
+    nt = newton.StaticNewton(ev, fp.fext(prob, fp.end_time(fx)), prob.dirichlet_dofs(),
+                             tol_res=1e-11, tol_inc=1e-12)
+    u = nt.solve().cpu().numpy()
+    for r in fx["results"]:
+        got = u[3 * prob.lid[r["node"]] + r["dof"]]
+        assert abs(got - r["value"]) <= r["tol"], (r, got, nt.history)
+
+
 def _cantilever(iv=(10, 10, 10), upper=(10.0, 1.0, 1.0)):
     mesh = fcg.BoxMesh(fcg.HEX8, iv, upper=upper)
     # x- face: all DOFs fixed; x+ face: surface load (0, 0, -1e-3) (SURVEY §8d config 1)

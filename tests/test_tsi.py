@@ -51,6 +51,24 @@ def test_tsi_graph_is_the_node_graph(celltype, iv, nranks):
         assert list(g.col_ts[g.rowptr_ts[tr]:g.rowptr_ts[tr + 1]]) == cols_s
 
 
+@pytest.mark.parametrize("iv,rank,nranks", [((4, 3, 5), 1, 3), ((2, 2, 2), 0, 1), ((7, 1, 1), 0, 1)])
+def test_lattice_ijk_recovers_box_positions(iv, rank, nranks):
+    m = fcg.BoxMesh(fcg.HEX8, iv, rank=rank, nranks=nranks)
+    ijk = fcg.lattice_ijk(m.ele_nodes)
+    assert np.array_equal(ijk, m.ele_ijk - m.ele_ijk.min(axis=0))
+    en = m.ele_nodes.copy()
+    en[len(en) // 2] = np.roll(en[len(en) // 2], 1)  # one element with a rotated node order
+    assert fcg.lattice_ijk(en) is None or len(en) == 1
+
+
+def test_lattice_ijk_on_reference_tsi_meshes():
+    for name, n in (("tsi_heatflux_monolithic.json", (1, 1, 3)),
+                    ("tsi_heatflux_flexoutsurf_monolithic.json", (2, 2, 3))):
+        prob = TsiProblem(json.load(open(os.path.join(GOLD, name))))
+        ijk = fcg.lattice_ijk(prob.elements)
+        assert ijk is not None and tuple(ijk.max(axis=0) + 1) == n
+
+
 def test_tsi_create_without_gpu_fails_loudly():
     import torch
     if torch.cuda.is_available():
@@ -234,11 +252,15 @@ def test_tsi_multirank_rows_equal_global():
                     assert abs(a[c] - b[c]) <= 1e-12 * np.abs(ra["Kst"]).max()
 
 
-def _library_assembler(prob):
-    """tsi_driver assemble callback with every block from the device library."""
+def _library_assembler(prob, fused=False):
+    """tsi_driver assemble callback with every block from the device library (fused: one
+    structured sweep pass, fcg_tsi_evaluate_fused)."""
     torch, dev = _dev()
-    dis = fcg.Discretization.from_elements(prob.celltype, prob.elements, prob.X)
-    ev = fcg.Evaluator(dis, kinematics=fcg.LINEAR, youngs=prob.E, poisson=prob.nu)
+    dis = fcg.Discretization.from_elements(prob.celltype, prob.elements, prob.X, lattice=fused)
+    if fused:
+        assert dis.ele_ijk is not None, "reference mesh is not a lattice"
+    ev = fcg.Evaluator(dis, kinematics=fcg.LINEAR, youngs=prob.E, poisson=prob.nu,
+                       path=fcg.PATH_STRUCTURED if fused else fcg.PATH_AUTO)
     tev = fcg.TsiEvaluator(dis, prob.E, prob.nu, prob.alpha, prob.T0, prob.conduct)
     g = tev.graph
 
@@ -252,10 +274,14 @@ def _library_assembler(prob):
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).to(dev)
         fs = torch.zeros(dis.n_rows, dtype=torch.float64, device=dev)
         Kss = torch.zeros(dis.nnz, dtype=torch.float64, device=dev)
-        ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, t(d), fs, Kss)
         o = {k: torch.zeros(n, dtype=torch.float64, device=dev)
              for k, n in (("Kst", g.nnz_st), ("Kts", g.nnz_ts), ("Ktt", g.nnz_tt), ("fT", g.n_rows_t))}
-        tev.evaluate_device(fcg.TSI_ALL, fcg.OVERWRITE, t(v), t(T), 1.0, 1.0 / prob.dt, fs=fs, **o)
+        if fused:
+            tev.evaluate_fused(ev, fcg.OVERWRITE, t(d), t(v), t(T), 1.0, 1.0 / prob.dt, fs=fs,
+                               Kss=Kss, **o)
+        else:
+            ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, t(d), fs, Kss)
+            tev.evaluate_device(fcg.TSI_ALL, fcg.OVERWRITE, t(v), t(T), 1.0, 1.0 / prob.dt, fs=fs, **o)
         o = {k: x.cpu().numpy() for k, x in o.items()}
         ns, nn = prob.ns, prob.nn
         return (dense(Kss.cpu().numpy(), dis.rowptr, dis.col_lid, (ns, ns)),
@@ -266,13 +292,14 @@ def _library_assembler(prob):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("name", ["tsi_heatflux_monolithic.json",
                                   "tsi_heatflux_flexoutsurf_monolithic.json"])
-def test_tsi_result_description_on_device(name):
+def test_tsi_result_description_on_device(name, fused):
     _dev()
     fx = json.load(open(os.path.join(GOLD, name)))
     prob = TsiProblem(fx)
-    d, T = prob.solve(assemble=_library_assembler(prob))
+    d, T = prob.solve(assemble=_library_assembler(prob, fused=fused))
     for r in fx["results"]:
         got = prob.result(d, T, r)
         assert abs(got - r["value"]) <= r["tol"], (r, got)
