@@ -281,12 +281,136 @@ bool build_structured_plan(const fcg_desc* d, const std::vector<int32_t>& rownod
   return true;
 }
 
+// Colour-ordered direct assembly plan (hex27 on a verified lattice).  Element e at lattice
+// position (ex, ey, ez) gets colour (ex & 1) + 2 (ey & 1) + 4 (ez & 1); two elements of one colour
+// share no node, so the eight colour launches write disjoint rows.  The elements holding both
+// nodes a, b of e form the product over the axes of {e} or {e, e -+ 1} (the latter when a and b
+// both lie on e's lower / upper face along that axis); the first of them in colour order is the
+// even one along every such axis, or e itself when the odd/even partner does not exist.  Bits of
+// ft[e]: 2d = e comes first along axis d for pairs on its lower face, 2d+1 = on its upper face.
+// The hint must place every element node at 2 ijk(e) + position(a) consistently (unique nodes
+// and positions), which makes lattice neighbours share exactly their face nodes.
+struct ColorHost {
+  std::vector<int32_t> col_ele;
+  std::vector<uint8_t> ft;
+  int64_t color_ptr[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+};
+
+bool build_colored_plan(const fcg_desc* d, ColorHost& P, std::string& why)
+{
+  if (d->celltype != FCG_HEX27 || !d->ele_ijk)
+  {
+    why = "no lattice hint, or not hex27";
+    return false;
+  }
+  if (d->n_ele == 0)
+  {
+    why = "nothing to evaluate";
+    return false;
+  }
+  int64_t mn[3], mx[3];
+  for (int k = 0; k < 3; ++k)
+  {
+    mn[k] = INT32_MAX;
+    mx[k] = INT32_MIN;
+  }
+  for (int64_t e = 0; e < d->n_ele; ++e)
+    for (int k = 0; k < 3; ++k)
+    {
+      mn[k] = std::min<int64_t>(mn[k], d->ele_ijk[3 * e + k]);
+      mx[k] = std::max<int64_t>(mx[k], d->ele_ijk[3 * e + k]);
+    }
+  const int64_t EX = mx[0] - mn[0] + 1, EY = mx[1] - mn[1] + 1, EZ = mx[2] - mn[2] + 1;
+  if (EX * EY * EZ > 8 * d->n_ele + 4096)
+  {
+    why = "element lattice box far larger than the element set";
+    return false;
+  }
+  std::vector<int32_t> elem_at(EX * EY * EZ, -1);
+  for (int64_t e = 0; e < d->n_ele; ++e)
+  {
+    const int64_t idx = ((d->ele_ijk[3 * e + 2] - mn[2]) * EY + (d->ele_ijk[3 * e + 1] - mn[1])) * EX +
+                        (d->ele_ijk[3 * e] - mn[0]);
+    if (elem_at[idx] != -1)
+    {
+      why = "two elements at one lattice position";
+      return false;
+    }
+    elem_at[idx] = int32_t(e);
+  }
+  // node positions on the (2E+1)^3 lattice of the element box
+  const int64_t NXn = 2 * EX + 1, NYn = 2 * EY + 1;
+  std::vector<int64_t> npos(d->n_node, -1);
+  for (int64_t e = 0; e < d->n_ele; ++e)
+  {
+    const int64_t ex = d->ele_ijk[3 * e] - mn[0], ey = d->ele_ijk[3 * e + 1] - mn[1],
+                  ez = d->ele_ijk[3 * e + 2] - mn[2];
+    for (int a = 0; a < 27; ++a)
+    {
+      const int64_t p = ((2 * ez + fcg::kHex27NodePos[a][2]) * NYn + 2 * ey + fcg::kHex27NodePos[a][1]) *
+                            NXn + 2 * ex + fcg::kHex27NodePos[a][0];
+      const int32_t node = d->ele_nodes[27 * e + a];
+      if (npos[node] == -1)
+        npos[node] = p;
+      else if (npos[node] != p)
+      {
+        why = "connectivity does not match the lattice hint";
+        return false;
+      }
+    }
+  }
+  {
+    std::vector<int64_t> sorted;
+    sorted.reserve(d->n_node);
+    for (int64_t nd = 0; nd < d->n_node; ++nd)
+      if (npos[nd] >= 0) sorted.push_back(npos[nd]);
+    std::sort(sorted.begin(), sorted.end());
+    if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end())
+    {
+      why = "two nodes at one lattice position";
+      return false;
+    }
+  }
+  P.ft.assign(d->n_ele, 0);
+  std::vector<int64_t> cnt(8, 0);
+  std::vector<uint8_t> color(d->n_ele);
+  for (int64_t e = 0; e < d->n_ele; ++e)
+  {
+    const int64_t c[3] = {d->ele_ijk[3 * e] - mn[0], d->ele_ijk[3 * e + 1] - mn[1],
+        d->ele_ijk[3 * e + 2] - mn[2]};
+    uint8_t bits = 0, col = 0;
+    for (int k = 0; k < 3; ++k)
+    {
+      const bool even = (d->ele_ijk[3 * e + k] & 1) == 0;
+      int64_t lo[3] = {c[0], c[1], c[2]}, hi[3] = {c[0], c[1], c[2]};
+      lo[k] -= 1;
+      hi[k] += 1;
+      auto exists = [&](const int64_t* q) {
+        if (q[0] < 0 || q[1] < 0 || q[2] < 0 || q[0] >= EX || q[1] >= EY || q[2] >= EZ) return false;
+        return elem_at[(q[2] * EY + q[1]) * EX + q[0]] >= 0;
+      };
+      if (even || !exists(lo)) bits |= uint8_t(1u << (2 * k));
+      if (even || !exists(hi)) bits |= uint8_t(1u << (2 * k + 1));
+      if (!even) col |= uint8_t(1u << k);
+    }
+    P.ft[e] = bits;
+    color[e] = col;
+    cnt[col]++;
+  }
+  P.color_ptr[0] = 0;
+  for (int c = 0; c < 8; ++c) P.color_ptr[c + 1] = P.color_ptr[c] + cnt[c];
+  P.col_ele.resize(d->n_ele);
+  std::vector<int64_t> fill(P.color_ptr, P.color_ptr + 8);
+  for (int64_t e = 0; e < d->n_ele; ++e) P.col_ele[fill[color[e]]++] = int32_t(e);
+  return true;
+}
+
 void free_mesh(fcg::DeviceMesh& m)
 {
   void* ptrs[] = {m.ele_nodes, m.ele_gid, m.node_x, m.node_dof_col, m.inc_of, m.inc_ptr,
       m.rownode_row0, m.inc_pos, m.rowptr, m.scratch, m.err, m.elem_at, m.lat_x, m.lat_dof,
       m.plane_rec,
-      m.tables, m.stamps, m.col_lid, m.diag_pos, m.pcg_work};
+      m.tables, m.stamps, m.col_lid, m.diag_pos, m.pcg_work, m.col_ele, m.ele_ft, m.inc_row0};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   m = fcg::DeviceMesh{};
@@ -334,7 +458,7 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
     set_create_error("ElastHyper is supported with KINEM nonlinear (TotLag) only");
     return FCG_ERR_ARG;
   }
-  if (d->material != FCG_MAT_STVK && d->path == FCG_PATH_STRUCTURED)
+  if (d->material != FCG_MAT_STVK && d->path == FCG_PATH_STRUCTURED && d->celltype == FCG_HEX8)
   {
     set_create_error("the structured sweep implements StVenantKirchhoff only");
     return FCG_ERR_ARG;
@@ -422,11 +546,32 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
   if (d->path != FCG_PATH_GENERAL && d->material == FCG_MAT_STVK)
   {
     structured = build_structured_plan(d, rownodes, row0, kcol, sp, why);
-    if (!structured && d->path == FCG_PATH_STRUCTURED)
+    if (!structured && d->path == FCG_PATH_STRUCTURED && d->celltype == FCG_HEX8)
     {
       set_create_error("structured path requested but the lattice hint does not verify: " + why);
       return FCG_ERR_ARG;
     }
+  }
+  // --- colour-ordered direct assembly (hex27 on a verified lattice, any material)
+  ColorHost cp;
+  bool colored = false;
+  // AUTO keeps hex27 on the general path: it measured faster (hex27 40^3 on one MI355X: 4.2 vs
+  // 5.2 ms linear, 4.8 vs 6.6 ms TotLag -- the colour launches write K in 72-byte runs that share
+  // cache lines with other colours' runs); the colour-ordered path needs no scratch (1M hex27:
+  // 53 GB less device memory) and is taken when requested.
+  if ((d->path == FCG_PATH_STRUCTURED || d->path == FCG_PATH_COLORED) && d->celltype == FCG_HEX27)
+  {
+    colored = build_colored_plan(d, cp, why);
+    if (!colored)
+    {
+      set_create_error("lattice path requested but the lattice hint does not verify: " + why);
+      return FCG_ERR_ARG;
+    }
+  }
+  if (d->path == FCG_PATH_COLORED && d->celltype != FCG_HEX27)
+  {
+    set_create_error("the colour-ordered path is implemented for hex27");
+    return FCG_ERR_ARG;
   }
 
   // --- incidences grouped by owned node (general path)
@@ -446,6 +591,7 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
   std::vector<int32_t> inc_of(structured ? 0 : d->n_ele * npe, -1);
   std::vector<int32_t> inc_ele(n_inc);
   std::vector<uint8_t> inc_a(n_inc);
+  std::vector<int32_t> inc_row0(colored ? n_inc : 0);
   if (!structured)
   {
     std::vector<int64_t> fill(inc_ptr.begin(), inc_ptr.end() - 1);
@@ -458,6 +604,7 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
         inc_of[e * npe + a] = int32_t(k);
         inc_ele[k] = int32_t(e);
         inc_a[k] = uint8_t(a);
+        if (colored) inc_row0[k] = row0[rn];
       }
   }
   // --- positions of every element node's DOF triple inside the row (stride fast path)
@@ -597,6 +744,16 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
       chk(upload(&m.stamps, zero, 8, bytes));
     }
   }
+  else if (colored)
+  {
+    m.path = FCG_PATH_COLORED;
+    chk(upload(&m.inc_of, inc_of.data(), d->n_ele * npe, bytes));
+    chk(upload(&m.inc_pos, inc_pos.data(), n_inc * npe, bytes));
+    chk(upload(&m.inc_row0, inc_row0.data(), n_inc, bytes));
+    chk(upload(&m.col_ele, cp.col_ele.data(), d->n_ele, bytes));
+    chk(upload(&m.ele_ft, cp.ft.data(), d->n_ele, bytes));
+    for (int c = 0; c < 9; ++c) m.color_ptr[c] = cp.color_ptr[c];
+  }
   else
   {
     m.path = FCG_PATH_GENERAL;
@@ -657,6 +814,13 @@ int fcg_evaluate_device(fcg_ctx* ctx, int action, int mode, const double* d_u_co
       he = fcg::launch_sweep_h8(m, d_u_col, want_k, mode == FCG_OVERWRITE, d_K_vals, d_fint_row, s);
     if (T.enabled && he == hipSuccess) he = hipEventRecord(T.ev[1], s);
   }
+  else if (m.path == FCG_PATH_COLORED)
+  {
+    if (he == hipSuccess)
+      he = fcg::launch_element_colored(m, d_u_col, want_k, mode == FCG_OVERWRITE, d_K_vals,
+          d_fint_row, s);
+    if (T.enabled && he == hipSuccess) he = hipEventRecord(T.ev[1], s);
+  }
   else
   {
     if (he == hipSuccess) he = fcg::launch_element(m, d_u_col, want_k, s);
@@ -679,7 +843,7 @@ int fcg_evaluate_device(fcg_ctx* ctx, int action, int mode, const double* d_u_co
     (void)hipEventElapsedTime(&a, T.ev[0], T.ev[1]);
     (void)hipEventElapsedTime(&b, T.ev[1], T.ev[2]);
     T.ms_element = a;
-    T.ms_assemble = m.path == FCG_PATH_STRUCTURED ? 0.0 : b;  // one fused kernel
+    T.ms_assemble = m.path == FCG_PATH_GENERAL ? b : 0.0;  // fused: evaluate + assembly in ms_element
   }
   if (errv[0] != 0)
   {
@@ -764,7 +928,7 @@ int fcg_get_info(const fcg_ctx* ctx, fcg_info* info)
   info->n_cols = m.n_cols;
   info->nnz = m.nnz;
   info->n_incidences = m.n_inc;
-  info->scratch_bytes = m.n_inc * fcg::record_doubles(m.npe) * int64_t(sizeof(double));
+  info->scratch_bytes = m.scratch ? m.n_inc * fcg::record_doubles(m.npe) * int64_t(sizeof(double)) : 0;
   info->device_bytes = ctx->device_bytes;
   info->path = m.path;
   return FCG_OK;

@@ -36,6 +36,12 @@ struct DeviceMesh {
   int32_t* err = nullptr;           // [2]: code, min failing element index
   int32_t max_rowlen = 0;
 
+  // colour-ordered direct assembly (hex27 on a verified lattice, FCG_PATH_COLORED)
+  int32_t* col_ele = nullptr;       // [n_ele] elements sorted by colour (lattice parity), then index
+  int64_t color_ptr[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // col_ele range of colour c
+  uint8_t* ele_ft = nullptr;        // [n_ele] first-touch bits (see fcg_kernels.hip)
+  int32_t* inc_row0 = nullptr;      // [n_inc] row LID of the incidence's node
+
   // structured (row-block sweep) plan, hex8 only
   int path = FCG_PATH_GENERAL;
   int32_t tiles_x = 0, tiles_y = 0, tiles_z = 0, seg_planes = 0;
@@ -88,6 +94,10 @@ struct Timing {
 void upload_constant_tables(int celltype);  // GP / nodal derivative tables -> __constant__
 hipError_t launch_element(const DeviceMesh& m, const double* d_u_col, bool want_k,
     hipStream_t stream);
+// Colour-ordered direct assembly (FCG_PATH_COLORED): eight element launches, one per colour,
+// each adding (or, first in colour order, writing) its blocks straight into the CSR rows.
+hipError_t launch_element_colored(const DeviceMesh& m, const double* d_u_col, bool want_k,
+    bool overwrite, double* d_K, double* d_fint, hipStream_t stream);
 hipError_t launch_assemble(const DeviceMesh& m, bool want_k, bool overwrite, double* d_K,
     double* d_fint, hipStream_t stream);
 

@@ -34,6 +34,13 @@ __constant__ double c_dN27_gp[27 * 27 * 3];
 __constant__ double c_dN27_node[27 * 27 * 3];
 __constant__ double c_w27[27];
 __constant__ uint16_t c_pairs27[378];          // symmetric pairs a <= b, packed a | b << 8
+__constant__ uint8_t c_loc27[27];              // hex27 node lattice offsets, x | y << 2 | z << 4
+__constant__ uint8_t c_latnode27[27];          // hex27 node at lattice offset x + 3 y + 9 z
+__device__ inline int lat27(int a)
+{
+  const int l = c_loc27[a];
+  return (l & 3) + 3 * ((l >> 2) & 3) + 9 * (l >> 4);
+}
 
 template <int NPE> struct Tables;
 template <> struct Tables<8> {
@@ -78,6 +85,14 @@ void upload_constant_tables(int /*celltype*/)
   for (int a = 0; a < 27; ++a)
     for (int b = a; b < 27; ++b) pairs[p++] = uint16_t(a | (b << 8));
   (void)hipMemcpyToSymbol(HIP_SYMBOL(c_pairs27), pairs, sizeof(pairs));
+  uint8_t loc[27];
+  for (int a = 0; a < 27; ++a)
+    loc[a] = uint8_t(kHex27NodePos[a][0] | (kHex27NodePos[a][1] << 2) | (kHex27NodePos[a][2] << 4));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(c_loc27), loc, sizeof(loc));
+  uint8_t latnode[27];
+  for (int a = 0; a < 27; ++a)
+    latnode[kHex27NodePos[a][0] + 3 * kHex27NodePos[a][1] + 9 * kHex27NodePos[a][2]] = uint8_t(a);
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(c_latnode27), latnode, sizeof(latnode));
   done = true;
 }
 
@@ -131,8 +146,15 @@ struct ElementShared {
   static constexpr int NGP = NPE;
   double X[3 * NPE];
   double U[3 * NPE];
-  double NX[NGP * NPE * 3];               // [g][c][d]
-  double P[KIN ? NGP * NPE * 3 : 1];      // F * N_XYZ_c  (TotLag)
+  union {
+    struct {
+      double NX[NGP * NPE * 3];           // [g][c][d]
+      double P[KIN ? NGP * NPE * 3 : 1];  // F * N_XYZ_c  (TotLag)
+    };
+    // colour-ordered direct assembly: the element's blocks a <= b (c_pairs27 order, 3 x 3
+    // column-major), written once N_XYZ and P are no longer read
+    double KS[NPE == 27 ? 378 * 9 : 1];
+  };
   double invJ[NGP * 9];
   double fac[NGP];
   double S[NGP * 6];                      // PK2 stress, Voigt xx yy zz xy yz zx
@@ -140,6 +162,14 @@ struct ElementShared {
   double M[KIN ? NGP * 6 : 1];            // F F^T (sym)
   double Cm[MAT ? NGP * 36 : 1];          // ElastHyper: cmat (column-major 6x6) per Gauss point
   int bad;
+  // colour-ordered direct assembly: per local node its incidence (-1 = row not owned), the CSR
+  // offset and length of its rows, and the column position of every element node in them
+  int32_t inc[NPE];
+  int32_t rlen[NPE];
+  int64_t rbase[NPE];
+  uint16_t ipos[NPE * NPE];
+  uint8_t loc[NPE];      // hex27 lattice offsets of the nodes (c_loc27)
+  uint8_t latnode[NPE];  // node at lattice offset (c_latnode27)
 };
 
 // Mat::ElastHyper with one ELAST_CoupNeoHooke summand: S and cmat from the principal invariants
@@ -241,11 +271,39 @@ struct ElementArgs {
   double lambda, mu, cdiag;
   double nh_c, nh_beta;  // ElastHyper/CoupNeoHooke: c = E / (4 (1 + nu)), beta = nu / (1 - 2 nu)
   int want_k;
+  // colour-ordered direct assembly (ASM != 0): elements col_ele[e_begin, e_end) of one colour
+  const int32_t* col_ele;
+  int64_t e_begin, e_end;
+  const uint8_t* ele_ft;
+  const int32_t* inc_row0;
+  const uint16_t* inc_pos;
+  const int64_t* rowptr;
+  double* K;
+  double* fint;
 };
 
+// Colour-ordered direct assembly: is element e (first-touch bits ft, see build_colored_plan in
+// fcg_context.cpp) the first, in colour order, of the elements holding both hex27 nodes a and b?
+// Along an axis where both nodes lie on e's lower (upper) face the lower (upper) neighbour holds
+// them too; e comes first there iff bit 2d (2d+1) of ft is set.  Along every other axis e is alone.
+__device__ inline bool first_touch27(const uint8_t* loc, uint32_t ft, int a, int b)
+{
+  const uint32_t la = loc[a], lb = loc[b];
+  bool first = true;
+#pragma unroll
+  for (int d = 0; d < 3; ++d)
+  {
+    const uint32_t x = (la >> (2 * d)) & 3u, y = (lb >> (2 * d)) & 3u;
+    if (x == y && x != 1u) first = first && ((ft >> (2 * d + (x == 2u ? 1 : 0))) & 1u);
+  }
+  return first;
+}
+
 // ---------------------------------------------------------------------------------- element
-template <int NPE, int KIN, int BLOCK, int MAT = 0>
-__global__ __launch_bounds__(BLOCK) void element_kernel(ElementArgs A)
+// ASM: 0 = block rows into the incidence scratch (general path, assemble_kernel sums them);
+// 1 / 2 = colour-ordered direct assembly, ACCUMULATE / OVERWRITE (hex27 lattice path).
+template <int NPE, int KIN, int BLOCK, int MAT = 0, int ASM = 0>
+__global__ __launch_bounds__(BLOCK, (NPE == 27 && MAT == 0) ? 3 : 1) void element_kernel(ElementArgs A)
 {
   constexpr int NGP = NPE;
   constexpr bool SYM = (NPE == 27);             // hex27: compute a<=b and mirror
@@ -258,8 +316,11 @@ __global__ __launch_bounds__(BLOCK) void element_kernel(ElementArgs A)
   const double* dNnode = Tables<NPE>::dNnode();
   const double* wgp = Tables<NPE>::w();
 
-  for (int64_t e = blockIdx.x; e < A.n_ele; e += gridDim.x)
+  const int64_t n_it = ASM ? A.e_end - A.e_begin : A.n_ele;
+  for (int64_t it = blockIdx.x; it < n_it; it += gridDim.x)
   {
+    const int64_t e = ASM ? int64_t(A.col_ele[A.e_begin + it]) : it;
+    const uint32_t ft = ASM ? uint32_t(A.ele_ft[e]) : 0u;
     const int32_t* en = A.ele_nodes + e * NPE;
     // 1. gather reference coordinates and displacements (evaluate_element_nodes, calc_lib.hpp:180-203)
     for (int v = tid; v < 3 * NPE; v += BLOCK)
@@ -268,6 +329,27 @@ __global__ __launch_bounds__(BLOCK) void element_kernel(ElementArgs A)
       const int node = en[a];
       sh.X[v] = A.node_x[3 * int64_t(node) + d];
       sh.U[v] = A.u_col[A.node_dof_col[node] + d];
+    }
+    if (ASM)
+    {
+      for (int v = tid; v < NPE * NPE; v += BLOCK)
+      {
+        const int a = v / NPE;
+        const int32_t ia = A.inc_of[e * NPE + a];
+        sh.ipos[v] = ia >= 0 ? A.inc_pos[int64_t(ia) * NPE + (v - NPE * a)] : uint16_t(0);
+        if (v - NPE * a == 0)
+        {
+          sh.loc[a] = c_loc27[a];
+          sh.latnode[a] = c_latnode27[a];
+          sh.inc[a] = ia;
+          if (ia >= 0)
+          {
+            const int32_t r0 = A.inc_row0[ia];
+            sh.rbase[a] = A.rowptr[r0];
+            sh.rlen[a] = int32_t(A.rowptr[r0 + 1] - A.rowptr[r0]);
+          }
+        }
+      }
     }
     if (tid == 0) sh.bad = 0;
     __syncthreads();
@@ -467,148 +549,235 @@ __global__ __launch_bounds__(BLOCK) void element_kernel(ElementArgs A)
           f[1] += fc * t[1];
           f[2] += fc * t[2];
         }
-        double* rec = A.scratch + int64_t(ia) * REC + 9 * NPE;
-        rec[0] = f[0];
-        rec[1] = f[1];
-        rec[2] = f[2];
+        if (ASM)
+        {
+          double* dst = A.fint + A.inc_row0[ia];
+          if (ASM == 2 && first_touch27(sh.loc, ft, a, a))
+          {
+            dst[0] = f[0];
+            dst[1] = f[1];
+            dst[2] = f[2];
+          }
+          else
+          {
+            dst[0] += f[0];
+            dst[1] += f[1];
+            dst[2] += f[2];
+          }
+        }
+        else
+        {
+          double* rec = A.scratch + int64_t(ia) * REC + 9 * NPE;
+          rec[0] = f[0];
+          rec[1] = f[1];
+          rec[2] = f[2];
+        }
       }
     }
 
     // 6. element stiffness blocks K_ab (add_elastic/geometric_stiffness_matrix, calc_lib.hpp:872-927)
-    if (A.want_k)
+    auto pair_block = [&](int a, int b, double* K) {
+      double G[9];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) G[k] = 0.0;
+      double H[6] = {0, 0, 0, 0, 0, 0};
+      double geo = 0.0;
+      for (int g = 0; g < NGP; ++g)
+      {
+        const double fc = sh.fac[g];
+        const double* na = sh.NX + 3 * (NPE * g + a);
+        const double* nb = sh.NX + 3 * (NPE * g + b);
+        if (MAT == 1)
+        {
+          // general material: K_ab += fac (B_a^T cmat B_b + (a.S.b) I)  (calc_lib.hpp:872-927);
+          // G holds B_a^T cmat B_b (row-major i, j), geo the geometric part
+          const double* F = sh.F + 9 * g;
+          const double* cm = sh.Cm + 36 * (MAT ? g : 0);
+          double Ba[6][3], Bb[6][3];
+          strain_gradient(F, na, Ba);
+          strain_gradient(F, nb, Bb);
+#pragma unroll
+          for (int j = 0; j < 3; ++j)
+          {
+            double cb[6];
+#pragma unroll
+            for (int r = 0; r < 6; ++r)
+            {
+              double t = 0.0;
+#pragma unroll
+              for (int q = 0; q < 6; ++q) t += cm[r + 6 * q] * Bb[q][j];
+              cb[r] = fc * t;
+            }
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+            {
+              double t = 0.0;
+#pragma unroll
+              for (int r = 0; r < 6; ++r) t += Ba[r][i] * cb[r];
+              G[i + 3 * j] += t;
+            }
+          }
+          const double* S = sh.S + 6 * g;
+          const double c0 = nb[0], c1 = nb[1], c2 = nb[2];
+          const double sb0 = S[0] * c0 + S[3] * c1 + S[5] * c2;
+          const double sb1 = S[3] * c0 + S[1] * c1 + S[4] * c2;
+          const double sb2 = S[5] * c0 + S[4] * c1 + S[2] * c2;
+          geo += fc * (na[0] * sb0 + na[1] * sb1 + na[2] * sb2);
+        }
+        else if (KIN == 0)
+        {
+          const double fa0 = fc * na[0], fa1 = fc * na[1], fa2 = fc * na[2];
+          const double b0 = nb[0], b1 = nb[1], b2 = nb[2];
+          G[0] += fa0 * b0; G[3] += fa0 * b1; G[6] += fa0 * b2;
+          G[1] += fa1 * b0; G[4] += fa1 * b1; G[7] += fa1 * b2;
+          G[2] += fa2 * b0; G[5] += fa2 * b1; G[8] += fa2 * b2;
+        }
+        else
+        {
+          const double* pa = sh.P + 3 * (NPE * g + a);
+          const double* pb = sh.P + 3 * (NPE * g + b);
+          const double fa0 = fc * pa[0], fa1 = fc * pa[1], fa2 = fc * pa[2];
+          const double b0 = pb[0], b1 = pb[1], b2 = pb[2];
+          G[0] += fa0 * b0; G[3] += fa0 * b1; G[6] += fa0 * b2;
+          G[1] += fa1 * b0; G[4] += fa1 * b1; G[7] += fa1 * b2;
+          G[2] += fa2 * b0; G[5] += fa2 * b1; G[8] += fa2 * b2;
+          const double a0 = na[0], a1 = na[1], a2 = na[2];
+          const double c0 = nb[0], c1 = nb[1], c2 = nb[2];
+          const double t = fc * (a0 * c0 + a1 * c1 + a2 * c2);
+          const double* M = sh.M + 6 * g;
+#pragma unroll
+          for (int k = 0; k < 6; ++k) H[k] += t * M[k];
+          const double* S = sh.S + 6 * g;
+          const double sb0 = S[0] * c0 + S[3] * c1 + S[5] * c2;
+          const double sb1 = S[3] * c0 + S[1] * c1 + S[4] * c2;
+          const double sb2 = S[5] * c0 + S[4] * c1 + S[2] * c2;
+          geo += fc * (a0 * sb0 + a1 * sb1 + a2 * sb2);
+        }
+      }
+      // K_ij = lambda G_ij + mu G_ji + mu tr(G) delta_ij      (linear)
+      // K_ij = lambda G_ij + mu G_ji + mu H_ij + geo delta_ij (TotLag)
+      const double lam = A.lambda, mu = A.mu;
+      if (MAT == 1)
+      {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) K[i] = G[i];
+        K[0] += geo;
+        K[4] += geo;
+        K[8] += geo;
+      }
+      else
+      {
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) K[i + 3 * j] = lam * G[i + 3 * j] + mu * G[j + 3 * i];
+      }
+      if (MAT == 1)
+      {
+      }
+      else if (KIN == 0)
+      {
+        const double tr = mu * (G[0] + G[4] + G[8]);
+        K[0] += tr;
+        K[4] += tr;
+        K[8] += tr;
+      }
+      else
+      {
+        K[0] += mu * H[0] + geo;
+        K[4] += mu * H[1] + geo;
+        K[8] += mu * H[2] + geo;
+        K[1] += mu * H[3]; K[3] += mu * H[3];
+        K[5] += mu * H[4]; K[7] += mu * H[4];
+        K[2] += mu * H[5]; K[6] += mu * H[5];
+      }
+    };
+    auto pair_of = [&](int p, int& a, int& b) {
+      if (SYM)
+      {
+        const uint16_t pr = c_pairs27[p];
+        a = pr & 0xff;
+        b = pr >> 8;
+      }
+      else
+      {
+        a = p / NPE;
+        b = p - NPE * (p / NPE);
+      }
+    };
+    if constexpr (ASM != 0)
+    {
+      if (A.want_k)
+      {
+      static_assert(NPE == 27, "colour-ordered direct assembly is the hex27 path");
+      // blocks a <= b into registers, then (after every thread's last N_XYZ / P read) into the
+      // LDS image KS; then the element's 81 rows leave in runs of contiguous columns (element
+      // nodes in lattice order) -- written by the first element of the colour order that holds
+      // both nodes, added to by the others
+      double Kq[2][9];
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+      {
+        const int p = tid + BLOCK * q;
+        if (p < NPAIR)
+        {
+          int a, b;
+          pair_of(p, a, b);
+          if (sh.inc[a] >= 0 || sh.inc[b] >= 0) pair_block(a, b, Kq[q]);
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+      {
+        const int p = tid + BLOCK * q;
+        if (p < NPAIR)
+#pragma unroll
+          for (int k = 0; k < 9; ++k) sh.KS[9 * p + k] = Kq[q][k];
+      }
+      __syncthreads();
+      constexpr int NV = 9;  // entries in flight per thread: all loads before the stores
+      for (int v0 = 0; v0 < NPE * 243; v0 += NV * BLOCK)
+      {
+        uint32_t slot[NV];  // local row node | offset inside its rows << 5; 0xFFFFFFFF = none
+        double val[NV];
+#pragma unroll
+        for (int k = 0; k < NV; ++k)
+        {
+          const int v = v0 + tid + BLOCK * k;
+          slot[k] = 0xFFFFFFFFu;
+          val[k] = 0.0;
+          if (v >= NPE * 243) continue;
+          const int a = v / 243;
+          if (sh.inc[a] < 0) continue;
+          const int r = v - 243 * a;
+          const int i = r / 81, c = r - 81 * (r / 81);
+          const int b = sh.latnode[c / 3], j = c - 3 * (c / 3);
+          const uint32_t o = uint32_t(i * sh.rlen[a] + sh.ipos[NPE * a + b] + j);
+          slot[k] = uint32_t(a) | (o << 5);
+          const int lo = a < b ? a : b, hi = a < b ? b : a;
+          const int pidx = 27 * lo - (lo * (lo - 1)) / 2 + hi - lo;
+          val[k] = sh.KS[9 * pidx + (a <= b ? i + 3 * j : j + 3 * i)];
+          if (!(ASM == 2 && first_touch27(sh.loc, ft, a, b))) val[k] += A.K[sh.rbase[a] + o];
+        }
+#pragma unroll
+        for (int k = 0; k < NV; ++k)
+          if (slot[k] != 0xFFFFFFFFu)
+            __builtin_nontemporal_store(val[k], A.K + sh.rbase[slot[k] & 31u] + (slot[k] >> 5));
+      }
+      }
+    }
+    else if (A.want_k)
     {
       for (int p = tid; p < NPAIR; p += BLOCK)
       {
         int a, b;
-        if (SYM)
-        {
-          const uint16_t pr = c_pairs27[p];
-          a = pr & 0xff;
-          b = pr >> 8;
-        }
-        else
-        {
-          a = p / NPE;
-          b = p - NPE * (p / NPE);
-        }
+        pair_of(p, a, b);
         const int32_t ia = inc[a];
         const int32_t ib = inc[b];
         if (ia < 0 && (!SYM || ib < 0)) continue;
-        double G[9];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) G[k] = 0.0;
-        double H[6] = {0, 0, 0, 0, 0, 0};
-        double geo = 0.0;
-        for (int g = 0; g < NGP; ++g)
-        {
-          const double fc = sh.fac[g];
-          const double* na = sh.NX + 3 * (NPE * g + a);
-          const double* nb = sh.NX + 3 * (NPE * g + b);
-          if (MAT == 1)
-          {
-            // general material: K_ab += fac (B_a^T cmat B_b + (a.S.b) I)  (calc_lib.hpp:872-927);
-            // G holds B_a^T cmat B_b (row-major i, j), geo the geometric part
-            const double* F = sh.F + 9 * g;
-            const double* cm = sh.Cm + 36 * (MAT ? g : 0);
-            double Ba[6][3], Bb[6][3];
-            strain_gradient(F, na, Ba);
-            strain_gradient(F, nb, Bb);
-#pragma unroll
-            for (int j = 0; j < 3; ++j)
-            {
-              double cb[6];
-#pragma unroll
-              for (int r = 0; r < 6; ++r)
-              {
-                double t = 0.0;
-#pragma unroll
-                for (int q = 0; q < 6; ++q) t += cm[r + 6 * q] * Bb[q][j];
-                cb[r] = fc * t;
-              }
-#pragma unroll
-              for (int i = 0; i < 3; ++i)
-              {
-                double t = 0.0;
-#pragma unroll
-                for (int r = 0; r < 6; ++r) t += Ba[r][i] * cb[r];
-                G[i + 3 * j] += t;
-              }
-            }
-            const double* S = sh.S + 6 * g;
-            const double c0 = nb[0], c1 = nb[1], c2 = nb[2];
-            const double sb0 = S[0] * c0 + S[3] * c1 + S[5] * c2;
-            const double sb1 = S[3] * c0 + S[1] * c1 + S[4] * c2;
-            const double sb2 = S[5] * c0 + S[4] * c1 + S[2] * c2;
-            geo += fc * (na[0] * sb0 + na[1] * sb1 + na[2] * sb2);
-          }
-          else if (KIN == 0)
-          {
-            const double fa0 = fc * na[0], fa1 = fc * na[1], fa2 = fc * na[2];
-            const double b0 = nb[0], b1 = nb[1], b2 = nb[2];
-            G[0] += fa0 * b0; G[3] += fa0 * b1; G[6] += fa0 * b2;
-            G[1] += fa1 * b0; G[4] += fa1 * b1; G[7] += fa1 * b2;
-            G[2] += fa2 * b0; G[5] += fa2 * b1; G[8] += fa2 * b2;
-          }
-          else
-          {
-            const double* pa = sh.P + 3 * (NPE * g + a);
-            const double* pb = sh.P + 3 * (NPE * g + b);
-            const double fa0 = fc * pa[0], fa1 = fc * pa[1], fa2 = fc * pa[2];
-            const double b0 = pb[0], b1 = pb[1], b2 = pb[2];
-            G[0] += fa0 * b0; G[3] += fa0 * b1; G[6] += fa0 * b2;
-            G[1] += fa1 * b0; G[4] += fa1 * b1; G[7] += fa1 * b2;
-            G[2] += fa2 * b0; G[5] += fa2 * b1; G[8] += fa2 * b2;
-            const double a0 = na[0], a1 = na[1], a2 = na[2];
-            const double c0 = nb[0], c1 = nb[1], c2 = nb[2];
-            const double t = fc * (a0 * c0 + a1 * c1 + a2 * c2);
-            const double* M = sh.M + 6 * g;
-#pragma unroll
-            for (int k = 0; k < 6; ++k) H[k] += t * M[k];
-            const double* S = sh.S + 6 * g;
-            const double sb0 = S[0] * c0 + S[3] * c1 + S[5] * c2;
-            const double sb1 = S[3] * c0 + S[1] * c1 + S[4] * c2;
-            const double sb2 = S[5] * c0 + S[4] * c1 + S[2] * c2;
-            geo += fc * (a0 * sb0 + a1 * sb1 + a2 * sb2);
-          }
-        }
-        // K_ij = lambda G_ij + mu G_ji + mu tr(G) delta_ij      (linear)
-        // K_ij = lambda G_ij + mu G_ji + mu H_ij + geo delta_ij (TotLag)
         double K[9];
-        const double lam = A.lambda, mu = A.mu;
-        if (MAT == 1)
-        {
-#pragma unroll
-          for (int i = 0; i < 9; ++i) K[i] = G[i];
-          K[0] += geo;
-          K[4] += geo;
-          K[8] += geo;
-        }
-        else
-        {
-#pragma unroll
-          for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int j = 0; j < 3; ++j) K[i + 3 * j] = lam * G[i + 3 * j] + mu * G[j + 3 * i];
-        }
-        if (MAT == 1)
-        {
-        }
-        else if (KIN == 0)
-        {
-          const double tr = mu * (G[0] + G[4] + G[8]);
-          K[0] += tr;
-          K[4] += tr;
-          K[8] += tr;
-        }
-        else
-        {
-          K[0] += mu * H[0] + geo;
-          K[4] += mu * H[1] + geo;
-          K[8] += mu * H[2] + geo;
-          K[1] += mu * H[3]; K[3] += mu * H[3];
-          K[5] += mu * H[4]; K[7] += mu * H[4];
-          K[2] += mu * H[5]; K[6] += mu * H[5];
-        }
+        pair_block(a, b, K);
         if (ia >= 0)
         {
           double* rec = A.scratch + int64_t(ia) * REC + 3 * b;
@@ -843,7 +1012,7 @@ static int grid_for(int64_t work, int cap)
 hipError_t launch_element(const DeviceMesh& m, const double* d_u_col, bool want_k, hipStream_t stream)
 {
   if (m.n_ele == 0) return hipSuccess;
-  ElementArgs a;
+  ElementArgs a{};
   a.n_ele = m.n_ele;
   a.ele_nodes = m.ele_nodes;
   a.node_x = m.node_x;
@@ -886,6 +1055,62 @@ hipError_t launch_element(const DeviceMesh& m, const double* d_u_col, bool want_
       hipLaunchKernelGGL((element_kernel<27, 1, 256>), dim3(grid), dim3(256), 0, stream, a);
   }
   return hipGetLastError();
+}
+
+hipError_t launch_element_colored(const DeviceMesh& m, const double* d_u_col, bool want_k,
+    bool overwrite, double* d_K, double* d_fint, hipStream_t stream)
+{
+  if (m.n_ele == 0 || m.npe != 27) return m.n_ele == 0 ? hipSuccess : hipErrorInvalidValue;
+  ElementArgs a{};
+  a.n_ele = m.n_ele;
+  a.ele_nodes = m.ele_nodes;
+  a.node_x = m.node_x;
+  a.node_dof_col = m.node_dof_col;
+  a.u_col = d_u_col;
+  a.inc_of = m.inc_of;
+  a.scratch = nullptr;
+  a.err = m.err;
+  a.lambda = m.lambda;
+  a.mu = m.mu;
+  a.cdiag = m.cdiag;
+  a.want_k = want_k ? 1 : 0;
+  a.nh_c = m.nh_c;
+  a.nh_beta = m.nh_beta;
+  a.col_ele = m.col_ele;
+  a.ele_ft = m.ele_ft;
+  a.inc_row0 = m.inc_row0;
+  a.inc_pos = m.inc_pos;
+  a.rowptr = m.rowptr;
+  a.K = d_K;
+  a.fint = d_fint;
+  for (int c = 0; c < 8; ++c)
+  {
+    a.e_begin = m.color_ptr[c];
+    a.e_end = m.color_ptr[c + 1];
+    if (a.e_end == a.e_begin) continue;
+    const dim3 grid(grid_for(a.e_end - a.e_begin, 256 * 8)), block(256);
+#define FCG_COL(KIN, MAT)                                                                          \
+  if (overwrite)                                                                                   \
+    hipLaunchKernelGGL((element_kernel<27, KIN, 256, MAT, 2>), grid, block, 0, stream, a);         \
+  else                                                                                             \
+    hipLaunchKernelGGL((element_kernel<27, KIN, 256, MAT, 1>), grid, block, 0, stream, a);
+    if (m.material == FCG_MAT_ELASTHYPER_COUPNEOHOOKE)
+    {
+      FCG_COL(1, 1)
+    }
+    else if (m.kinem == 0)
+    {
+      FCG_COL(0, 0)
+    }
+    else
+    {
+      FCG_COL(1, 0)
+    }
+#undef FCG_COL
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_assemble(const DeviceMesh& m, bool want_k, bool overwrite, double* d_K,

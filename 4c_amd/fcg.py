@@ -17,7 +17,7 @@ HEX8, HEX27 = 0, 1
 LINEAR, TOTLAG = 0, 1
 CALC_NLNSTIFF, CALC_INTERNALFORCE = 0, 1
 ACCUMULATE, OVERWRITE = 0, 1
-PATH_AUTO, PATH_GENERAL, PATH_STRUCTURED = 0, 1, 2
+PATH_AUTO, PATH_GENERAL, PATH_STRUCTURED, PATH_COLORED = 0, 1, 2, 3
 MAT_STVK, MAT_ELASTHYPER_COUPNEOHOOKE = 0, 1
 TSI_STRUCT_FORCE, TSI_STIFFTEMP, TSI_THERMO_FINTCOND, TSI_COUPLTANG = 1, 2, 4, 8
 TSI_ALL = 15

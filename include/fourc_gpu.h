@@ -83,8 +83,9 @@ typedef struct fcg_desc {
   const int32_t* col_lid;      /* [rowptr[n_rows]] */
   /* Optional structured-lattice hint (GridGenerator meshes): [n_ele][3] element lattice
    * position (ex, ey, ez) = (gid % nx, gid / nx % ny, gid / (nx ny)), 4C_io_gridgenerator.cpp:336-338.
-   * fcg_create verifies it against the connectivity and, for hex8, then uses the fused
-   * z-sweep kernel (no scratch round trip).  NULL = general (unstructured) path. */
+   * fcg_create verifies it against the connectivity and then uses the fused z-sweep kernel
+   * (hex8) or the colour-ordered direct assembly (hex27) -- no scratch round trip either way.
+   * NULL = general (unstructured) path. */
   const int32_t* ele_ijk;
   int32_t path;                /* fcg_path: FCG_PATH_AUTO / _GENERAL / _STRUCTURED */
   int32_t material;            /* fcg_material (0 = StVenantKirchhoff) */
@@ -96,9 +97,14 @@ typedef struct fcg_desc {
  * 4C_mat_elast_coupneohooke.cpp); FCG_TOTLAG only, general (unstructured) kernels. */
 enum fcg_material { FCG_MAT_STVK = 0, FCG_MAT_ELASTHYPER_COUPNEOHOOKE = 1 };
 
-/* Evaluation paths.  AUTO picks STRUCTURED when the hint verifies, else GENERAL.  STRUCTURED
- * fails fcg_create with FCG_ERR_ARG when the hint does not verify. */
-enum fcg_path { FCG_PATH_AUTO = 0, FCG_PATH_GENERAL = 1, FCG_PATH_STRUCTURED = 2 };
+/* Evaluation paths.  AUTO picks the hex8 row-block sweep (FCG_PATH_STRUCTURED) when the lattice
+ * hint verifies, else GENERAL.  STRUCTURED requests the lattice path and fails fcg_create with
+ * FCG_ERR_ARG when the hint does not verify: for hex8 the fused row-block sweep, for hex27 the
+ * colour-ordered direct assembly (reported as FCG_PATH_COLORED: eight launches, one per
+ * element-parity colour; each element adds its blocks straight into the CSR rows, the first
+ * colour to reach a matrix entry writes it -- no scratch records, no atomics, fixed order).
+ * COLORED requests the latter explicitly (hex27 only). */
+enum fcg_path { FCG_PATH_AUTO = 0, FCG_PATH_GENERAL = 1, FCG_PATH_STRUCTURED = 2, FCG_PATH_COLORED = 3 };
 
 typedef struct fcg_ctx fcg_ctx;
 
@@ -148,7 +154,7 @@ typedef struct fcg_info {
   int64_t n_incidences;     /* (element, owned local node) pairs */
   int64_t scratch_bytes;    /* device scratch for element block-rows */
   int64_t device_bytes;     /* total device memory held by the context */
-  int32_t path;             /* fcg_path actually used (GENERAL or STRUCTURED) */
+  int32_t path;             /* fcg_path actually used (GENERAL, STRUCTURED or COLORED) */
   int32_t reserved;
 } fcg_info;
 int fcg_get_info(const fcg_ctx* ctx, fcg_info* info);

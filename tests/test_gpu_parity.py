@@ -68,7 +68,8 @@ def test_nlnstiff_matches_oracle(celltype, kinem, iv, amp):
     err, _, Kr, fr = oracle_evaluate(mesh, kinem, E, NU, u)
     assert err == 0
     Kg, fg, ev = _run_gpu(mesh, kinem, u)
-    # hex8 box meshes carry the lattice hint -> fused structured kernel; hex27 -> general path
+    # box meshes carry the lattice hint -> hex8: fused structured sweep; hex27: general path
+    # (the colour-ordered path is tested below)
     assert ev.info.path == (fcg.PATH_STRUCTURED if celltype == fcg.HEX8 else fcg.PATH_GENERAL)
     _check(Kg, fg, Kr, fr)
 
@@ -197,9 +198,73 @@ def test_neohooke_matches_oracle(celltype, iv):
     u = mesh.u_col(5e-2)
     err, _, Kr, fr = oracle_evaluate(mesh, fcg.TOTLAG, 10.0, 0.25, u, material=orc.MAT_NEOHOOKE)
     assert err == 0
-    ev = fcg.Evaluator(mesh, kinematics=fcg.TOTLAG, youngs=10.0, poisson=0.25, material=NH)
-    assert ev.info.path == fcg.PATH_GENERAL
-    Kg, fg, _ = _run_gpu(mesh, fcg.TOTLAG, u, ev=ev)
-    _check(Kg, fg, Kr, fr)
-    _, fi, _ = _run_gpu(mesh, fcg.TOTLAG, u, action=fcg.CALC_INTERNALFORCE, ev=ev)
+    for path in (fcg.PATH_GENERAL, fcg.PATH_COLORED):
+        if path == fcg.PATH_COLORED and celltype != fcg.HEX27:
+            continue
+        ev = fcg.Evaluator(mesh, kinematics=fcg.TOTLAG, youngs=10.0, poisson=0.25, material=NH,
+                           path=path)
+        assert ev.info.path == path
+        Kg, fg, _ = _run_gpu(mesh, fcg.TOTLAG, u, ev=ev)
+        _check(Kg, fg, Kr, fr)
+        _, fi, _ = _run_gpu(mesh, fcg.TOTLAG, u, action=fcg.CALC_INTERNALFORCE, ev=ev)
+        assert rel_err(fi, fr) <= 1e-10
+
+
+# ------------------------------------------------------------------ hex27 colour-ordered path
+@pytest.mark.parametrize("kinem", [fcg.LINEAR, fcg.TOTLAG])
+@pytest.mark.parametrize("iv", [(1, 1, 1), (2, 3, 4), (5, 1, 2), (4, 4, 4)])
+def test_hex27_colored_and_general_paths_agree_with_oracle(kinem, iv):
+    """Every entry of an owned row is written by the first element of the colour order that holds
+    both nodes (K starts as NaN, so a missed entry shows), the others add: same K and f as the
+    oracle and as the scratch + row-gather path."""
+    mesh = fcg.BoxMesh(fcg.HEX27, iv, jitter=0.02, seed=11)
+    u = mesh.u_col(1e-3 if kinem == fcg.LINEAR else 5e-2)
+    _, _, Kr, fr = oracle_evaluate(mesh, kinem, E, NU, u)
+    for path in (fcg.PATH_GENERAL, fcg.PATH_STRUCTURED):
+        Kg, fg, ev = _run_gpu(mesh, kinem, u, path=path)
+        assert ev.info.path == (fcg.PATH_GENERAL if path == fcg.PATH_GENERAL else fcg.PATH_COLORED)
+        _check(Kg, fg, Kr, fr)
+    _, fi, _ = _run_gpu(mesh, kinem, u, action=fcg.CALC_INTERNALFORCE, ev=ev)
     assert rel_err(fi, fr) <= 1e-10
+
+
+def test_hex27_colored_accumulate_and_reproducible():
+    mesh = fcg.BoxMesh(fcg.HEX27, (3, 3, 2), jitter=0.02)
+    u = mesh.u_col(5e-2)
+    rng = np.random.default_rng(1)
+    K0 = rng.standard_normal(mesh.nnz)
+    f0 = rng.standard_normal(mesh.n_rows)
+    Ka, fa, ev = _run_gpu(mesh, fcg.TOTLAG, u, mode=fcg.ACCUMULATE, K0=K0.copy(), f0=f0.copy(),
+                          path=fcg.PATH_COLORED)
+    assert ev.info.path == fcg.PATH_COLORED
+    K1, f1, _ = _run_gpu(mesh, fcg.TOTLAG, u, ev=ev)
+    K2, f2, _ = _run_gpu(mesh, fcg.TOTLAG, u, ev=ev)
+    assert np.array_equal(K1, K2) and np.array_equal(f1, f2)
+    np.testing.assert_allclose(Ka, K0 + K1, rtol=0, atol=1e-13 * np.abs(K1).max())
+    np.testing.assert_allclose(fa, f0 + f1, rtol=0, atol=1e-13 * np.abs(f1).max())
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 8])
+def test_hex27_colored_multirank_rows_equal_global(nranks):
+    """Box ranks (owned + ghost elements): the colour rule sees missing neighbours at the rank
+    boundary only for rows the rank does not own; the union of owned rows equals the global K, f."""
+    iv = (4, 3, 3)
+    glob = fcg.BoxMesh(fcg.HEX27, iv, jitter=0.02)
+    ug = glob.u_col(5e-2)
+    Kg, fg, _ = _run_gpu(glob, fcg.TOTLAG, ug)
+    grow = {int(g): i for i, g in enumerate(glob.row_gid)}
+    gcol = {int(g): i for i, g in enumerate(glob.col_gid)}
+    for r in range(nranks):
+        m = fcg.BoxMesh(fcg.HEX27, iv, jitter=0.02, rank=r, nranks=nranks)
+        u = np.array([ug[gcol[int(g)]] for g in m.col_gid])
+        K, f, ev = _run_gpu(m, fcg.TOTLAG, u, path=fcg.PATH_COLORED)
+        assert ev.info.path == fcg.PATH_COLORED
+        gi = np.array([grow[int(g)] for g in m.row_gid])
+        np.testing.assert_allclose(f, fg[gi], rtol=0, atol=1e-12 * np.abs(fg).max())
+        for i in range(m.n_rows):
+            cols = m.col_gid[m.col_lid[m.rowptr[i]:m.rowptr[i + 1]]]
+            gcols = glob.col_gid[glob.col_lid[glob.rowptr[gi[i]]:glob.rowptr[gi[i] + 1]]]
+            assert np.array_equal(np.sort(cols), np.sort(gcols))
+            mine = K[m.rowptr[i]:m.rowptr[i + 1]][np.argsort(cols)]
+            ref = Kg[glob.rowptr[gi[i]]:glob.rowptr[gi[i] + 1]][np.argsort(gcols)]
+            np.testing.assert_allclose(mine, ref, rtol=0, atol=1e-12 * np.abs(Kg).max())

@@ -139,13 +139,15 @@ def test_jitter_is_deterministic_and_interior_only():
     assert np.all(d[on_boundary] == 0)
 
 
-def test_structured_hint_is_verified_before_device_work():
+@pytest.mark.parametrize("celltype", [fcg.HEX8, fcg.HEX27])
+def test_structured_hint_is_verified_before_device_work(celltype):
     """A wrong lattice hint with PATH_STRUCTURED is rejected (FCG_ERR_ARG) on the host; a valid
-    one passes verification and then needs the device (FCG_ERR_DEVICE here, no GPU)."""
+    one passes verification and then needs the device (FCG_ERR_DEVICE here, no GPU).  hex8: the
+    row-block sweep's plan; hex27: the colour-ordered direct assembly's plan."""
     import torch
     if torch.cuda.is_available():
         pytest.skip("GPU present: covered by the gpu tests")
-    m = fcg.BoxMesh(fcg.HEX8, (3, 4, 5))
+    m = fcg.BoxMesh(celltype, (3, 4, 5) if celltype == fcg.HEX8 else (2, 3, 2))
     with pytest.raises(fcg.FcgError) as ei:
         fcg.Evaluator(m, path=fcg.PATH_STRUCTURED)
     assert ei.value.code == 4

@@ -18,10 +18,11 @@ ap.add_argument("--n", type=int, default=50)
 ap.add_argument("--path", default="auto")
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--material", default="stvk", choices=["stvk", "neohooke"])
+ap.add_argument("--action", default="nlnstiff", choices=["nlnstiff", "internalforce"])
 a = ap.parse_args()
 ct = fcg.HEX8 if a.celltype == "hex8" else fcg.HEX27
 kin = fcg.LINEAR if a.kinem == "linear" else fcg.TOTLAG
-path = {"auto": fcg.PATH_AUTO, "general": fcg.PATH_GENERAL}[a.path]
+path = {"auto": fcg.PATH_AUTO, "general": fcg.PATH_GENERAL, "structured": fcg.PATH_STRUCTURED}[a.path]
 t0 = time.perf_counter()
 m = fcg.BoxMesh(ct, (a.n, a.n, a.n), jitter=0.1 if ct == fcg.HEX8 else 0.02)
 t1 = time.perf_counter()
@@ -32,13 +33,14 @@ dev = torch.device("cuda:0")
 u = torch.from_numpy(m.u_col(1e-3 if kin == fcg.LINEAR else 5e-2)).to(dev)
 f = torch.zeros(m.n_rows, dtype=torch.float64, device=dev)
 K = torch.zeros(m.nnz, dtype=torch.float64, device=dev)
+act = fcg.CALC_NLNSTIFF if a.action == "nlnstiff" else fcg.CALC_INTERNALFORCE
 ev.set_timing(True)
 ts = []
 for _ in range(a.reps):
-    ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u, f, K)
+    ev.evaluate_device(act, fcg.OVERWRITE, u, f, K)
     ts.append(ev.timing())
 ms = sorted(x[0] + x[1] for x in ts)[len(ts) // 2]
-print(json.dumps({"config": f"{a.celltype}-{a.kinem}-{a.material}-{a.n}^3", "path": int(ev.info.path),
+print(json.dumps({"config": f"{a.celltype}-{a.kinem}-{a.material}-{a.n}^3-{a.action}", "path": int(ev.info.path),
                   "elements": m.n_ele, "nnz": m.nnz, "ms_evaluate": ms,
                   "ms_element": sorted(ts)[len(ts) // 2][0], "ms_assemble": sorted(ts)[len(ts) // 2][1],
                   "elem_per_s": m.n_ele / (ms * 1e-3), "mesh_s": t1 - t0, "create_s": t2 - t1,

@@ -26,6 +26,8 @@ ap.add_argument("--length", type=float, default=10.0)
 ap.add_argument("--load", type=float, default=-1e-3)
 ap.add_argument("--lin-rtol", type=float, default=1e-10)
 ap.add_argument("--tol", type=float, default=1e-8)
+ap.add_argument("--path", default="auto", choices=["auto", "general", "structured"])
+ap.add_argument("--lin-max-iter", type=int, default=100000)
 a = ap.parse_args()
 ct = fcg.HEX8 if a.celltype == "hex8" else fcg.HEX27
 kin = fcg.LINEAR if a.kinem == "linear" else fcg.TOTLAG
@@ -38,7 +40,9 @@ face = [1, 2, 6, 5] if ct == fcg.HEX8 else [1, 2, 6, 5, 9, 14, 17, 13, 22]
 faces = mesh.ele_nodes[mesh.ele_ijk[:, 0] == a.n - 1][:, face]
 fext = np.zeros(mesh.n_rows)
 fcg.neumann_surface(ct, faces, X, mesh.node_dof_row, [1, 1, 1], [0.0, 0.0, a.load], fext)
-ev = fcg.Evaluator(mesh, kinematics=kin, youngs=210.0, poisson=0.3)
+path = {"auto": fcg.PATH_AUTO, "general": fcg.PATH_GENERAL, "structured": fcg.PATH_STRUCTURED}[a.path]
+print(f"mesh {time.perf_counter() - t0:.1f} s: {mesh.n_ele} elements, {mesh.nnz} nonzeros", file=sys.stderr, flush=True)
+ev = fcg.Evaluator(mesh, kinematics=kin, youngs=210.0, poisson=0.3, path=path)
 t_setup = time.perf_counter() - t0
 
 
@@ -64,17 +68,29 @@ class Timed(newton.StaticNewton):
                 self.history.append(rec)
                 return u
             torch.neg(self.r, out=self.r)
-            li, lr = self.ev.pcg_solve(self.K, self.r, self.du, self.lin_rtol, self.lin_max_iter)
+            # heartbeat while the (blocking) PCG runs: the GPU box treats 3 silent minutes as a hang
+            import threading
+            done = threading.Event()
+            hb = threading.Thread(target=lambda: [print(f"  pcg running ({it})", file=sys.stderr,
+                                                        flush=True) for _ in iter(lambda: done.wait(30), True)])
+            hb.start()
+            try:
+                li, lr = self.ev.pcg_solve(self.K, self.r, self.du, self.lin_rtol, self.lin_max_iter)
+            finally:
+                done.set()
+                hb.join()
             torch.cuda.synchronize()
             t_d = time.perf_counter()
             ndu = float(torch.linalg.vector_norm(self.du))
             u += self.du
             rec.update(solve_ms=1e3 * (t_d - t_c), pcg_iter=li, pcg_relres=lr, norm_inc=ndu)
             self.history.append(rec)
+            print(json.dumps(rec), file=sys.stderr, flush=True)
         return u
 
 
-nt = Timed(ev, fext, dbc, tol_res=a.tol * max(np.linalg.norm(fext), 1e-300), tol_inc=a.tol,
+print(f"setup {t_setup:.1f} s", file=sys.stderr, flush=True)
+nt = Timed(ev, fext, dbc, lin_max_iter=a.lin_max_iter, tol_res=a.tol * max(np.linalg.norm(fext), 1e-300), tol_inc=a.tol,
            lin_rtol=a.lin_rtol)
 t1 = time.perf_counter()
 u = nt.solve()

@@ -19,7 +19,7 @@ a = ap.parse_args()
 ct = fcg.HEX8 if a.celltype == "hex8" else fcg.HEX27
 kin = fcg.LINEAR if a.kinem == "linear" else fcg.TOTLAG
 path = {"auto": fcg.PATH_AUTO, "general": fcg.PATH_GENERAL, "structured": fcg.PATH_STRUCTURED}[a.path]
-m = fcg.BoxMesh(ct, (a.n, a.n, a.n), jitter=0.1)
+m = fcg.BoxMesh(ct, (a.n, a.n, a.n), jitter=0.1 if ct == fcg.HEX8 else 0.02)
 ev = fcg.Evaluator(m, kinematics=kin, path=path)
 dev = torch.device("cuda:0")
 u = torch.from_numpy(m.u_col(1e-3 if kin == fcg.LINEAR else 5e-2)).to(dev)
