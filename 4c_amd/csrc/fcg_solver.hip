@@ -13,7 +13,9 @@
 //    DBC rows and zero DBC right-hand sides every iterate keeps x_D = 0, so CG on the row-modified
 //    matrix is CG on K_FF.  All reductions are block partials summed in a fixed order: the solve
 //    is bitwise reproducible.  (4C hands this system to Belos/MueLu through NOX,
-//    4C_solver_nonlin_nox_linearsystem.cpp:275-353; the preconditioner here is Jacobi.)
+//    4C_solver_nonlin_nox_linearsystem.cpp:275-353; the preconditioner here is block Jacobi on
+//    the 3 x 3 nodal diagonal blocks -- Ifpack's point-block relaxation with the DOF triples of a
+//    node as blocks.)
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -43,28 +45,53 @@ __device__ inline double block_sum(double v, double* sbuf)
   return t;
 }
 
-// y = K x; optionally partial[blockIdx] = sum over the block's rows of d[row] * y[row]
-template <int LPR>
-__global__ __launch_bounds__(kBlock) void spmv_kernel(const int64_t* __restrict__ rowptr,
-    const int32_t* __restrict__ col, const double* __restrict__ vals, const double* __restrict__ x,
-    double* __restrict__ y, int64_t n_rows, const double* __restrict__ dotw, double* partial)
+// y = K x by node rows: the 3 rows of an owned node share one column pattern made of DOF triples
+// (checked by fcg_create), so LPN lanes walk the node's neighbour triples -- one column index,
+// x[c..c+2] and the 3 x 3 block of the 3 rows per triple -- instead of one index per matrix entry.
+// Row-major sums in a fixed lane order: deterministic.  Optionally
+// partial[blockIdx] = sum over the block's rows of dotw[row] * y[row].
+template <int LPN>
+__global__ __launch_bounds__(kBlock) void spmv_node_kernel(const int64_t* __restrict__ rowptr,
+    const int32_t* __restrict__ row0_of, const int32_t* __restrict__ col,
+    const double* __restrict__ vals, const double* __restrict__ x, double* __restrict__ y,
+    int64_t n_nodes, const double* __restrict__ dotw, double* partial)
 {
   __shared__ double sbuf[kBlock / 64];
-  const int64_t row = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / LPR;
-  const int lane = threadIdx.x % LPR;
-  double acc = 0.0;
-  if (row < n_rows)
+  const int64_t node = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / LPN;
+  const int lane = threadIdx.x % LPN;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+  int32_t row0 = 0;
+  if (node < n_nodes)
   {
-    const int64_t s = rowptr[row], e = rowptr[row + 1];
-    for (int64_t j = s + lane; j < e; j += LPR) acc += vals[j] * x[col[j]];
+    row0 = row0_of[node];
+    const int64_t s = rowptr[row0];
+    const int64_t len = rowptr[row0 + 1] - s;
+    const double* v0 = vals + s;
+    const double* v1 = v0 + len;
+    const double* v2 = v1 + len;
+    for (int64_t k = 3 * lane; k < len; k += 3 * LPN)
+    {
+      const int32_t c = col[s + k];
+      const double x0 = x[c], x1 = x[c + 1], x2 = x[c + 2];
+      a0 += v0[k] * x0 + v0[k + 1] * x1 + v0[k + 2] * x2;
+      a1 += v1[k] * x0 + v1[k + 1] * x1 + v1[k + 2] * x2;
+      a2 += v2[k] * x0 + v2[k + 1] * x1 + v2[k + 2] * x2;
+    }
   }
 #pragma unroll
-  for (int o = LPR / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, LPR);
-  double mine = 0.0;
-  if (row < n_rows && lane == 0)
+  for (int o = LPN / 2; o >= 1; o >>= 1)
   {
-    y[row] = acc;
-    if (dotw) mine = dotw[row] * acc;
+    a0 += __shfl_xor(a0, o, LPN);
+    a1 += __shfl_xor(a1, o, LPN);
+    a2 += __shfl_xor(a2, o, LPN);
+  }
+  double mine = 0.0;
+  if (node < n_nodes && lane == 0)
+  {
+    y[row0] = a0;
+    y[row0 + 1] = a1;
+    y[row0 + 2] = a2;
+    if (dotw) mine = dotw[row0] * a0 + dotw[row0 + 1] * a1 + dotw[row0 + 2] * a2;
   }
   if (partial)
   {
@@ -104,23 +131,42 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(const double* __restrict
   }
 }
 
-// init: x = 0, r = b, z = dinv r, p = z; partials r.z, r.r
-__global__ __launch_bounds__(kBlock) void pcg_init_kernel(const double* __restrict__ b,
-    const double* __restrict__ dinv, double* x, double* r, double* z, double* p, int64_t n,
-    double* part_rz, double* part_rr)
+// Block-Jacobi preconditioner: z_A = D_AA^-1 r_A with D_AA the 3 x 3 diagonal block of owned node
+// A (its rows' entries in the node's own DOF columns).  A Dirichlet row of the block is a unit row,
+// so z keeps zeros on constrained DOFs and the preconditioner restricted to the free DOFs is the
+// symmetric positive definite free part of the block.  One thread per owned node.
+__device__ inline void bj_apply(const double* __restrict__ Dinv, const double* r, double* z)
+{
+  z[0] = Dinv[0] * r[0] + Dinv[1] * r[1] + Dinv[2] * r[2];
+  z[1] = Dinv[3] * r[0] + Dinv[4] * r[1] + Dinv[5] * r[2];
+  z[2] = Dinv[6] * r[0] + Dinv[7] * r[1] + Dinv[8] * r[2];
+}
+
+// init: x = 0, r = b, z = D^-1 r, p = z; partials r.z, r.r
+__global__ __launch_bounds__(kBlock) void pcg_init_kernel(const int32_t* __restrict__ row0_of,
+    const double* __restrict__ b, const double* __restrict__ dinv, double* x, double* r, double* z,
+    double* p, int64_t n_nodes, double* part_rz, double* part_rr)
 {
   __shared__ double sbuf[kBlock / 64];
-  const int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  const int64_t k = int64_t(blockIdx.x) * kBlock + threadIdx.x;
   double rz = 0.0, rr = 0.0;
-  if (i < n)
+  if (k < n_nodes)
   {
-    const double ri = b[i], zi = dinv[i] * ri;
-    x[i] = 0.0;
-    r[i] = ri;
-    z[i] = zi;
-    p[i] = zi;
-    rz = ri * zi;
-    rr = ri * ri;
+    const int32_t i = row0_of[k];
+    double ri[3], zi[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) ri[d] = b[i + d];
+    bj_apply(dinv + 9 * k, ri, zi);
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+    {
+      x[i + d] = 0.0;
+      r[i + d] = ri[d];
+      z[i + d] = zi[d];
+      p[i + d] = zi[d];
+      rz += ri[d] * zi[d];
+      rr += ri[d] * ri[d];
+    }
   }
   const double a = block_sum(rz, sbuf);
   const double c = block_sum(rr, sbuf);
@@ -131,24 +177,35 @@ __global__ __launch_bounds__(kBlock) void pcg_init_kernel(const double* __restri
   }
 }
 
-// x += alpha p, r -= alpha q, z = dinv r; partials r.z, r.r
-__global__ __launch_bounds__(kBlock) void pcg_update_kernel(const double* __restrict__ p,
-    const double* __restrict__ q, const double* __restrict__ dinv, double* x, double* r, double* z,
-    int64_t n, const double* sc, double* part_rz, double* part_rr)
+// x += alpha p, r -= alpha q, z = D^-1 r; partials r.z, r.r
+__global__ __launch_bounds__(kBlock) void pcg_update_kernel(const int32_t* __restrict__ row0_of,
+    const double* __restrict__ p, const double* __restrict__ q, const double* __restrict__ dinv,
+    double* x, double* r, double* z, int64_t n_nodes, const double* sc, double* part_rz,
+    double* part_rr)
 {
   __shared__ double sbuf[kBlock / 64];
   const double alpha = sc[SC_ALPHA];
-  const int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  const int64_t k = int64_t(blockIdx.x) * kBlock + threadIdx.x;
   double rz = 0.0, rr = 0.0;
-  if (i < n)
+  if (k < n_nodes)
   {
-    x[i] += alpha * p[i];
-    const double ri = r[i] - alpha * q[i];
-    const double zi = dinv[i] * ri;
-    r[i] = ri;
-    z[i] = zi;
-    rz = ri * zi;
-    rr = ri * ri;
+    const int32_t i = row0_of[k];
+    double ri[3], zi[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+    {
+      x[i + d] += alpha * p[i + d];
+      ri[d] = r[i + d] - alpha * q[i + d];
+    }
+    bj_apply(dinv + 9 * k, ri, zi);
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+    {
+      r[i + d] = ri[d];
+      z[i + d] = zi[d];
+      rz += ri[d] * zi[d];
+      rr += ri[d] * ri[d];
+    }
   }
   const double a = block_sum(rz, sbuf);
   const double c = block_sum(rr, sbuf);
@@ -167,15 +224,47 @@ __global__ __launch_bounds__(kBlock) void pcg_dir_kernel(const double* __restric
   if (i < n) p[i] = z[i] + beta * p[i];
 }
 
-__global__ __launch_bounds__(kBlock) void jacobi_kernel(const int64_t* __restrict__ diag_pos,
-    const double* __restrict__ K, double* dinv, int64_t n, int32_t* bad)
+// D_AA^-1 per owned node: the block's row d sits in row row0 + d at the columns of the node's own
+// DOF triple, which starts at the diagonal entry's position minus d
+__global__ __launch_bounds__(kBlock) void block_jacobi_kernel(const int32_t* __restrict__ row0_of,
+    const int64_t* __restrict__ diag_pos, const double* __restrict__ K, double* dinv,
+    int64_t n_nodes, int32_t* bad)
 {
-  const int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x;
-  if (i >= n) return;
-  const int64_t dp = diag_pos[i];
-  const double d = dp >= 0 ? K[dp] : 0.0;
-  if (d == 0.0) atomicMax(bad, 1);
-  dinv[i] = d != 0.0 ? 1.0 / d : 0.0;
+  const int64_t k = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (k >= n_nodes) return;
+  const int32_t i = row0_of[k];
+  double m[9];  // column-major, as invert3x3 of the element kernels
+  bool ok = true;
+#pragma unroll
+  for (int d = 0; d < 3; ++d)
+  {
+    const int64_t dp = diag_pos[i + d];
+    ok = ok && dp >= 0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) m[d + 3 * c] = dp >= 0 ? K[dp - d + c] : 0.0;
+  }
+  const double c00 = m[4] * m[8] - m[7] * m[5], c01 = m[7] * m[2] - m[1] * m[8],
+               c02 = m[1] * m[5] - m[4] * m[2];
+  const double det = m[0] * c00 + m[3] * c01 + m[6] * c02;
+  double* o = dinv + 9 * k;  // row-major inverse
+  if (!ok || det == 0.0 || !(det == det))
+  {
+    atomicMax(bad, 1);
+#pragma unroll
+    for (int q = 0; q < 9; ++q) o[q] = 0.0;
+    return;
+  }
+  const double id = 1.0 / det;
+  // inverse (row-major): inv(r, c) = cofactor(c, r) / det
+  o[0] = c00 * id;
+  o[1] = (m[6] * m[5] - m[3] * m[8]) * id;
+  o[2] = (m[3] * m[7] - m[6] * m[4]) * id;
+  o[3] = c01 * id;
+  o[4] = (m[0] * m[8] - m[6] * m[2]) * id;
+  o[5] = (m[6] * m[1] - m[0] * m[7]) * id;
+  o[6] = c02 * id;
+  o[7] = (m[3] * m[2] - m[0] * m[5]) * id;
+  o[8] = (m[0] * m[4] - m[3] * m[1]) * id;
 }
 
 // Dirichlet rows: one wavefront per DBC row
@@ -213,18 +302,21 @@ hipError_t launch_spmv(const DeviceMesh& m, const double* K, const double* x, do
     const double* dotw, double* partial, hipStream_t s)
 {
   if (m.n_rows == 0) return hipSuccess;
+  // node rows (every owned row belongs to a node triple, fcg_create checks the pattern)
   if (m.npe == 27)
-    hipLaunchKernelGGL((spmv_kernel<64>), dim3(blocks_for(m.n_rows * 64, kBlock)), dim3(kBlock), 0,
-        s, m.rowptr, m.col_lid, K, x, y, m.n_rows, dotw, partial);
+    hipLaunchKernelGGL((spmv_node_kernel<64>), dim3(blocks_for(m.n_rownodes * 64, kBlock)),
+        dim3(kBlock), 0, s, m.rowptr, m.rownode_row0, m.col_lid, K, x, y, m.n_rownodes, dotw,
+        partial);
   else
-    hipLaunchKernelGGL((spmv_kernel<16>), dim3(blocks_for(m.n_rows * 16, kBlock)), dim3(kBlock), 0,
-        s, m.rowptr, m.col_lid, K, x, y, m.n_rows, dotw, partial);
+    hipLaunchKernelGGL((spmv_node_kernel<16>), dim3(blocks_for(m.n_rownodes * 16, kBlock)),
+        dim3(kBlock), 0, s, m.rowptr, m.rownode_row0, m.col_lid, K, x, y, m.n_rownodes, dotw,
+        partial);
   return hipGetLastError();
 }
 
 int64_t spmv_blocks(const DeviceMesh& m)
 {
-  return blocks_for(m.n_rows * (m.npe == 27 ? 64 : 16), kBlock);
+  return blocks_for(m.n_rownodes * (m.npe == 27 ? 64 : 16), kBlock);
 }
 
 }  // namespace
@@ -300,14 +392,21 @@ int fcg_pcg_solve(fcg_ctx* ctx, const double* d_K_vals, const double* d_b_row, d
   (void)hipSetDevice(ctx->device);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   hipError_t he = hipSuccess;
+  const int64_t nn = m.n_rownodes;
+  if (3 * nn != n)
+  {
+    ctx->last_error = "fcg_pcg_solve: every owned row must belong to an owned node's DOF triple";
+    return FCG_ERR_ARG;
+  }
   const int64_t nb_vec = fcg::blocks_for(n, fcg::kBlock);
+  const int64_t nb_node = fcg::blocks_for(nn, fcg::kBlock);
   const int64_t nb_mv = fcg::spmv_blocks(m);
-  const int64_t nb = std::max(nb_vec, nb_mv);
+  const int64_t nb = std::max(nb_node, nb_mv);
   if (!m.pcg_work || m.pcg_n != n)
   {
     if (m.pcg_work) (void)hipFree(m.pcg_work);
     m.pcg_work = nullptr;
-    he = hipMalloc(reinterpret_cast<void**>(&m.pcg_work), sizeof(double) * (5 * n + 3 * nb + fcg::SC_N));
+    he = hipMalloc(reinterpret_cast<void**>(&m.pcg_work), sizeof(double) * (7 * n + 3 * nb + fcg::SC_N));
     if (he != hipSuccess)
     {
       ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
@@ -320,7 +419,7 @@ int fcg_pcg_solve(fcg_ctx* ctx, const double* d_K_vals, const double* d_b_row, d
   double* p = z + n;
   double* q = p + n;
   double* dinv = q + n;
-  double* pa = dinv + n;
+  double* pa = dinv + 3 * n;  // dinv: 9 doubles per owned node
   double* pb = pa + nb;
   double* pc = pb + nb;
   double* sc = pc + nb;
@@ -328,11 +427,11 @@ int fcg_pcg_solve(fcg_ctx* ctx, const double* d_K_vals, const double* d_b_row, d
   he = hipMemcpyAsync(m.err, &zero, sizeof(zero), hipMemcpyHostToDevice, s);
   if (he == hipSuccess)
   {
-    hipLaunchKernelGGL(fcg::jacobi_kernel, dim3(nb_vec), dim3(fcg::kBlock), 0, s, m.diag_pos,
-        d_K_vals, dinv, n, m.err);
-    hipLaunchKernelGGL(fcg::pcg_init_kernel, dim3(nb_vec), dim3(fcg::kBlock), 0, s, d_b_row, dinv,
-        d_x_row, r, z, p, n, pa, pb);
-    hipLaunchKernelGGL(fcg::reduce_kernel, dim3(1), dim3(fcg::kBlock), 0, s, pa, nb_vec, sc,
+    hipLaunchKernelGGL(fcg::block_jacobi_kernel, dim3(nb_node), dim3(fcg::kBlock), 0, s,
+        m.rownode_row0, m.diag_pos, d_K_vals, dinv, nn, m.err);
+    hipLaunchKernelGGL(fcg::pcg_init_kernel, dim3(nb_node), dim3(fcg::kBlock), 0, s, m.rownode_row0,
+        d_b_row, dinv, d_x_row, r, z, p, nn, pa, pb);
+    hipLaunchKernelGGL(fcg::reduce_kernel, dim3(1), dim3(fcg::kBlock), 0, s, pa, nb_node, sc,
         int(fcg::SC_RZ), 3, pb, int(fcg::SC_RR));
     he = hipGetLastError();
   }
@@ -348,7 +447,7 @@ int fcg_pcg_solve(fcg_ctx* ctx, const double* d_K_vals, const double* d_b_row, d
   }
   if (bad)
   {
-    ctx->last_error = "zero or missing diagonal entry (Jacobi preconditioner)";
+    ctx->last_error = "singular or missing diagonal node block (block-Jacobi preconditioner)";
     return FCG_ERR_SINGULAR;
   }
   const double rr0 = hsc[fcg::SC_RR0];
@@ -366,9 +465,9 @@ int fcg_pcg_solve(fcg_ctx* ctx, const double* d_K_vals, const double* d_b_row, d
       if (he != hipSuccess) break;
       hipLaunchKernelGGL(fcg::reduce_kernel, dim3(1), dim3(fcg::kBlock), 0, s, pa, nb_mv, sc,
           int(fcg::SC_PQ), 1, nullptr, 0);
-      hipLaunchKernelGGL(fcg::pcg_update_kernel, dim3(nb_vec), dim3(fcg::kBlock), 0, s, p, q, dinv,
-          d_x_row, r, z, n, sc, pb, pc);
-      hipLaunchKernelGGL(fcg::reduce_kernel, dim3(1), dim3(fcg::kBlock), 0, s, pb, nb_vec, sc,
+      hipLaunchKernelGGL(fcg::pcg_update_kernel, dim3(nb_node), dim3(fcg::kBlock), 0, s,
+          m.rownode_row0, p, q, dinv, d_x_row, r, z, nn, sc, pb, pc);
+      hipLaunchKernelGGL(fcg::reduce_kernel, dim3(1), dim3(fcg::kBlock), 0, s, pb, nb_node, sc,
           int(fcg::SC_RZN), 2, pc, int(fcg::SC_RR));
       hipLaunchKernelGGL(fcg::pcg_dir_kernel, dim3(nb_vec), dim3(fcg::kBlock), 0, s, z, p, n, sc);
       he = hipGetLastError();

@@ -487,7 +487,7 @@ class Evaluator:
             self._raise(rc, -1)
 
     def pcg_solve(self, K_vals, b, x, rtol=1e-12, max_iter=10000, stream=None):
-        """K x = b (Jacobi PCG from x = 0); returns (iterations, relative residual)."""
+        """K x = b (block-Jacobi PCG from x = 0); returns (iterations, relative residual)."""
         it, rr = ctypes.c_int(0), ctypes.c_double(0.0)
         rc = lib().fcg_pcg_solve(self._h, _tensor_ptr(K_vals), _tensor_ptr(b), _tensor_ptr(x),
                                  float(rtol), int(max_iter), ctypes.byref(it), ctypes.byref(rr),

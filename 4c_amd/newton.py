@@ -7,7 +7,7 @@ Mirrors the static step of 4C's structure_new time integrator with a NOX full Ne
   Dirichlet on r (reaction forces kept) and K                       fcg_dirichlet_apply,
                                                                     4C_structure_new_dbc.cpp:221-262
   convergence: |r|_2 <= tol_res and |du|_2 <= tol_inc (NOX normF / normUpdate tests, combined "And")
-  K du = -r                                                         fcg_pcg_solve (Jacobi PCG)
+  K du = -r                                                         fcg_pcg_solve (block-Jacobi PCG)
   u += du
 Homogeneous Dirichlet conditions (the increments of the constrained DOFs are zero); single rank
 (the PCG needs the matrix column map to be the row map).  u, f, K, f_ext and the work vectors stay

@@ -181,7 +181,7 @@ int fcg_spmv(fcg_ctx* ctx, const double* d_K_vals, const double* d_x_col, double
  * 4C_linalg_sparsematrix.cpp:978-1097).  K or rhs may be NULL. */
 int fcg_dirichlet_apply(fcg_ctx* ctx, int64_t n_dbc, const int32_t* d_rows, double* d_K_vals,
     double* d_rhs_row, double* d_freact_row, void* stream);
-/* K x = b by Jacobi-preconditioned CG from x = 0 until |r| <= rtol |b| or max_iter iterations;
+/* K x = b by CG preconditioned with the inverse 3x3 nodal diagonal blocks (block Jacobi) from x = 0 until |r| <= rtol |b| or max_iter iterations;
  * single-rank systems only (matrix column map = row map), else FCG_ERR_ARG.  Deterministic. */
 int fcg_pcg_solve(fcg_ctx* ctx, const double* d_K_vals, const double* d_b_row, double* d_x_row,
     double rtol, int max_iter, int* iterations, double* rel_residual, void* stream);

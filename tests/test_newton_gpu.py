@@ -1,4 +1,4 @@
-"""The Newton path on the device: Dirichlet rows, CSR operator, Jacobi PCG
+"""The Newton path on the device: Dirichlet rows, CSR operator, block-Jacobi PCG
 and the static Newton driver (4c_amd/newton.py), against
   * the reference's own RESULT DESCRIPTION values (the three known-answer inputs the oracle is
     pinned on) -- assembled, constrained and solved entirely through the library;

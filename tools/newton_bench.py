@@ -2,7 +2,7 @@
 
 Cantilever box [0,L]x[0,1]x[0,1] (x- face clamped, x+ face surface load), StVK E=210 nu=0.3,
 static full Newton through 4c_amd/newton.py: per iteration fcg_evaluate_device + Dirichlet +
-Jacobi PCG.  Prints one JSON line with per-phase times.
+block-Jacobi PCG.  Prints one JSON line with per-phase times.
 usage: newton_bench.py --celltype hex8|hex27 --kinem linear|totlag --n N [--load L]"""
 import argparse
 import importlib
