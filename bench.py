@@ -84,16 +84,7 @@ def cpu_baseline(n, kinem, threads):
     """Oracle (4C-faithful restatement, oracle/) on the host cores: reference MPI semantics with
     `threads` workers as ranks, each assembling its own rows.  Bounded sample: one evaluation of
     the full n^3 mesh (about 10-30 s of CPU work in total)."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_lib
-    import parity_util
-    import tempfile
-    out = os.path.join(tempfile.gettempdir(), f"liborc_native_{os.getpid()}.so")
-    flags = ["-march=native"]
-    oracle_lib.build(force=True, extra_flags=flags, out=out)
-    oracle_lib._lib = None
-    oracle_lib.load(out)
-    oracle_lib._lib = oracle_lib.load(out)
+    parity_util = _oracle_native()
     mesh = fcg.BoxMesh(fcg.HEX8, (n, n, n), jitter=0.1, seed=20251015)
     u = mesh.u_col(1e-3)
     # single-core rate on a small slab, then all-core on the full mesh
@@ -121,6 +112,80 @@ def cpu_baseline(n, kinem, threads):
     }
 
 
+# SURVEY.md §8d algorithmic figures for hex27 TotLag K + r (per element)
+ALG_BYTES_PER_ELE_H27 = 37695.0
+ALG_FLOP_PER_ELE_H27_TOTLAG = 2.59e6
+
+
+def _oracle_native():
+    """The oracle (oracle/) compiled -O3 -march=native for the host cores (CPU baseline leg only)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+    import tempfile
+    out = os.path.join(tempfile.gettempdir(), f"liborc_native_{os.getpid()}.so")
+    if oracle_lib._lib is None or getattr(oracle_lib, "_native_out", None) != out:
+        oracle_lib.build(force=True, extra_flags=["-march=native"], out=out)
+        oracle_lib._lib = None
+        oracle_lib._lib = oracle_lib.load(out)
+        oracle_lib._native_out = out
+    import parity_util
+    return parity_util
+
+
+def hex27_secondary(dev, n, steps, threads, with_cpu):
+    """BASELINE config 3's element (hex27, StVK, TotLag, state A = 5e-2) on one GPU: K + r
+    assembly rate on an n^3 box (the per-element rate is flat from 40^3 up; the 1M-element Newton
+    loop itself is tools/newton_bench.py, profiles/r01_config3_hex27_1M_totlag_newton.json), the
+    FP64 and HBM fractions with SURVEY §8d's per-element figures, and the oracle beside it."""
+    mesh = fcg.BoxMesh(fcg.HEX27, (n, n, n), jitter=0.02, seed=20251015)
+    ev = fcg.Evaluator(mesh, kinematics=fcg.TOTLAG, youngs=210.0, poisson=0.3, device=dev.index)
+    u_h = mesh.u_col(5e-2)
+    u = torch.from_numpy(u_h).to(dev)
+    f = torch.zeros(mesh.n_rows, dtype=torch.float64, device=dev)
+    K = torch.zeros(mesh.nnz, dtype=torch.float64, device=dev)
+    for _ in range(2):
+        ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u, f, K)
+    ev.set_timing(True)
+    ts = []
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u, f, K)
+        ts.append(ev.timing())
+    torch.cuda.synchronize(dev)
+    wall = (time.perf_counter() - t0) / steps
+    ms_kern = float(np.mean([a + b for a, b in ts]))
+    flops = ALG_FLOP_PER_ELE_H27_TOTLAG * mesh.n_ele / (ms_kern * 1e-3) / 1e12
+    gbs = ALG_BYTES_PER_ELE_H27 * mesh.n_ele / (ms_kern * 1e-3) / 1e9
+    out = {
+        "workload": f"hex27-totlag-{n}^3", "baseline_config": "BASELINE.json configs[2] element",
+        "value": mesh.n_ele / wall, "unit": "element-evaluations/s", "ms_per_step": 1e3 * wall,
+        "elements": mesh.n_ele, "nnz": mesh.nnz, "path": "general (element_kernel + assemble_kernel)",
+        "roofline": {"bound": "mfma", "achieved": flops, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                     "frac": flops / FP64_PEAK_TFS, "alg_flop_per_element": ALG_FLOP_PER_ELE_H27_TOTLAG,
+                     "hbm_achieved_gbs": gbs, "hbm_frac": gbs / HBM_PEAK_GBS,
+                     "alg_bytes_per_element": ALG_BYTES_PER_ELE_H27,
+                     "ms_element_kernel": float(np.mean([a for a, _ in ts])),
+                     "ms_assemble_kernel": float(np.mean([b for _, b in ts]))},
+    }
+    ev.close()
+    del K, f, u
+    if with_cpu:
+        pu = _oracle_native()
+        small = fcg.BoxMesh(fcg.HEX27, (n, n, max(2, n // 10)), jitter=0.02, seed=20251015)
+        us = small.u_col(5e-2)
+        t = time.perf_counter()
+        err, _, _, _ = pu.oracle_evaluate(small, fcg.TOTLAG, 210.0, 0.3, us, nworkers=threads)
+        tn = time.perf_counter() - t
+        assert err == 0
+        out["cpu_baseline"] = {"value": small.n_ele / tn, "unit": "element-evaluations/s",
+                               "cores": threads, "kind": "port",
+                               "sample": f"one struct_calc_nlnstiff evaluation (K + r) of a "
+                                         f"{n}x{n}x{max(2, n // 10)} hex27 TotLag slab, "
+                                         f"{threads} threads as ranks"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -130,6 +195,8 @@ def main():
                     help="elements per direction per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-hex27", action="store_true", help="skip the hex27 (config 3) line")
+    ap.add_argument("--hex27-n", type=int, default=40)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -273,6 +340,14 @@ def main():
             out["cpu_baseline"] = cpu_baseline(args.n, fcg.LINEAR, args.cpu_threads)
         except Exception as e:  # report, never hide
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
+    if rank == 0 and world == 1 and not args.no_hex27:
+        del K, f, u_col, u_row
+        ev.close()
+        try:
+            out["secondary"] = [hex27_secondary(dev, args.hex27_n, max(3, min(args.steps, 10)),
+                                                args.cpu_threads, not args.no_cpu_baseline)]
+        except Exception as e:  # report, never hide
+            out["secondary"] = [{"workload": "hex27-totlag", "error": repr(e)}]
     if rank == 0:
         print(json.dumps(out))
     if world > 1:
