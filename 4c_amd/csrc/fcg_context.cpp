@@ -762,6 +762,16 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
     chk(upload(&m.inc_pos, inc_pos.data(), n_inc * npe, bytes));
     chk(upload<double>(&m.scratch, nullptr, n_inc * fcg::record_doubles(npe), bytes));
   }
+  if (!structured)
+  {
+    // diagnostics: per-phase s_memtime counters of the element kernel (tools/stamps.py)
+    const char* st = std::getenv("FCG_STAMPS");
+    if (st && st[0] == '1')
+    {
+      const unsigned long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      chk(upload(&m.stamps, zero, 8, bytes));
+    }
+  }
   for (auto& ev : ctx->timing.ev) chk(hipEventCreate(&ev));
   if (he != hipSuccess)
   {

@@ -36,6 +36,17 @@ __constant__ double c_w27[27];
 __constant__ uint16_t c_pairs27[378];          // symmetric pairs a <= b, packed a | b << 8
 __constant__ uint8_t c_loc27[27];              // hex27 node lattice offsets, x | y << 2 | z << 4
 __constant__ uint8_t c_latnode27[27];          // hex27 node at lattice offset x + 3 y + 9 z
+__constant__ double c_L27gp[3][3];             // L_i(xi_p) of the 1D quadratic Lagrange factors
+__constant__ double c_dL27gp[3][3];            // L_i'(xi_p), xi_p = -a, 0, a (hex_27point)
+__constant__ double c_dL27nd[3][3];            // L_i'(x_p), x_p = -1, 0, 1 (the nodes)
+// hex27 node lattice offsets (4C order, 4C_io_gridgenerator.cpp:348-369) for compile-time use
+struct Hex27Pos {
+  static constexpr int p[27][3] = {{0, 0, 0}, {2, 0, 0}, {2, 2, 0}, {0, 2, 0}, {0, 0, 2}, {2, 0, 2},
+      {2, 2, 2}, {0, 2, 2}, {1, 0, 0}, {2, 1, 0}, {1, 2, 0}, {0, 1, 0}, {0, 0, 1}, {2, 0, 1},
+      {2, 2, 1}, {0, 2, 1}, {1, 0, 2}, {2, 1, 2}, {1, 2, 2}, {0, 1, 2}, {1, 1, 0}, {1, 0, 1},
+      {2, 1, 1}, {1, 2, 1}, {0, 1, 1}, {1, 1, 2}, {1, 1, 1}};
+};
+#define kPos27 Hex27Pos::p
 __device__ inline int lat27(int a)
 {
   const int l = c_loc27[a];
@@ -93,6 +104,30 @@ void upload_constant_tables(int /*celltype*/)
   for (int a = 0; a < 27; ++a)
     latnode[kHex27NodePos[a][0] + 3 * kHex27NodePos[a][1] + 9 * kHex27NodePos[a][2]] = uint8_t(a);
   (void)hipMemcpyToSymbol(HIP_SYMBOL(c_latnode27), latnode, sizeof(latnode));
+  {
+    // 1D factors, evaluated as in shape_deriv (fcg_shape.hpp)
+    double xg[27 * 3], wg[27];
+    gauss_rule(kHex27, xg, wg);
+    const double xs[3] = {xg[3 * 0], xg[3 * 8], xg[3 * 1]};  // -a, 0, a (nodes 0, 8, 1 along xi)
+    const double xn[3] = {-1.0, 0.0, 1.0};
+    double L[3][3], dL[3][3], dLn[3][3];
+    for (int p = 0; p < 3; ++p)
+    {
+      const double r = xs[p], t = xn[p];
+      L[p][0] = 0.5 * r * (r - 1.0);
+      L[p][1] = 1.0 - r * r;
+      L[p][2] = 0.5 * r * (r + 1.0);
+      dL[p][0] = r - 0.5;
+      dL[p][1] = -2.0 * r;
+      dL[p][2] = r + 0.5;
+      dLn[p][0] = t - 0.5;
+      dLn[p][1] = -2.0 * t;
+      dLn[p][2] = t + 0.5;
+    }
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_L27gp), L, sizeof(L));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_dL27gp), dL, sizeof(dL));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_dL27nd), dLn, sizeof(dLn));
+  }
   done = true;
 }
 
@@ -151,10 +186,14 @@ struct ElementShared {
       double NX[NGP * NPE * 3];           // [g][c][d]
       double P[KIN ? NGP * NPE * 3 : 1];  // F * N_XYZ_c  (TotLag)
     };
-    // colour-ordered direct assembly: the element's blocks a <= b (c_pairs27 order, 3 x 3
+    // TotLag hex27, colour-ordered path: the element's blocks a <= b (c_pairs27 order, 3 x 3
     // column-major), written once N_XYZ and P are no longer read
-    double KS[NPE == 27 ? 378 * 9 : 1];
+    double KSu[(NPE == 27 && KIN) ? 378 * 9 : 1];
   };
+  // linear hex27: the same image in its own space (24 + 27 KB still allow 3 workgroups per CU),
+  // written by the pair threads directly
+  double KSs[(NPE == 27 && !KIN) ? 378 * 9 : 1];
+  __device__ double* ks() { return KIN ? KSu : KSs; }
   double invJ[NGP * 9];
   double fac[NGP];
   double S[NGP * 6];                      // PK2 stress, Voigt xx yy zz xy yz zx
@@ -170,6 +209,8 @@ struct ElementShared {
   uint16_t ipos[NPE * NPE];
   uint8_t loc[NPE];      // hex27 lattice offsets of the nodes (c_loc27)
   uint8_t latnode[NPE];  // node at lattice offset (c_latnode27)
+  // hex27 1D quadratic Lagrange factors: L_i and L_i' at the 3 Gauss abscissae, L_i' at -1, 0, 1
+  double L1[3][3], dL1[3][3], dLn[3][3];
 };
 
 // Mat::ElastHyper with one ELAST_CoupNeoHooke summand: S and cmat from the principal invariants
@@ -271,6 +312,7 @@ struct ElementArgs {
   double lambda, mu, cdiag;
   double nh_c, nh_beta;  // ElastHyper/CoupNeoHooke: c = E / (4 (1 + nu)), beta = nu / (1 - 2 nu)
   int want_k;
+  unsigned long long* stamps;  // diagnostic phase timers (NULL = off)
   // colour-ordered direct assembly (ASM != 0): elements col_ele[e_begin, e_end) of one colour
   const int32_t* col_ele;
   int64_t e_begin, e_end;
@@ -316,6 +358,22 @@ __global__ __launch_bounds__(BLOCK, (NPE == 27 && MAT == 0) ? 3 : 1) void elemen
   const double* dNnode = Tables<NPE>::dNnode();
   const double* wgp = Tables<NPE>::w();
 
+  // diagnostic phase timers (library built with -DFCG_ELEMENT_STAMPS, run with FCG_STAMPS=1):
+  // wave-uniform s_memtime deltas, summed per workgroup; compiled out of the production library
+  // (the counters would cost registers)
+#ifdef FCG_ELEMENT_STAMPS
+  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long st_last = A.stamps ? __builtin_amdgcn_s_memtime() : 0ull;
+#define EL_STAMP(i)                                                                                \
+  if (A.stamps)                                                                                    \
+  {                                                                                                \
+    const unsigned long long now = __builtin_amdgcn_s_memtime();                                  \
+    st_acc[i] += now - st_last;                                                                    \
+    st_last = now;                                                                                 \
+  }
+#else
+#define EL_STAMP(i)
+#endif
   const int64_t n_it = ASM ? A.e_end - A.e_begin : A.n_ele;
   for (int64_t it = blockIdx.x; it < n_it; it += gridDim.x)
   {
@@ -329,6 +387,18 @@ __global__ __launch_bounds__(BLOCK, (NPE == 27 && MAT == 0) ? 3 : 1) void elemen
       const int node = en[a];
       sh.X[v] = A.node_x[3 * int64_t(node) + d];
       sh.U[v] = A.u_col[A.node_dof_col[node] + d];
+    }
+    if (NPE == 27 && !ASM && tid < NPE)
+    {
+      sh.inc[tid] = A.inc_of[e * NPE + tid];
+      sh.loc[tid] = c_loc27[tid];
+      sh.latnode[tid] = c_latnode27[tid];
+    }
+    if (NPE == 27 && tid < 9)
+    {
+      (&sh.L1[0][0])[tid] = (&c_L27gp[0][0])[tid];
+      (&sh.dL1[0][0])[tid] = (&c_dL27gp[0][0])[tid];
+      (&sh.dLn[0][0])[tid] = (&c_dL27nd[0][0])[tid];
     }
     if (ASM)
     {
@@ -353,9 +423,76 @@ __global__ __launch_bounds__(BLOCK, (NPE == 27 && MAT == 0) ? 3 : 1) void elemen
     }
     if (tid == 0) sh.bad = 0;
     __syncthreads();
+    EL_STAMP(0);
 
     // 2. nodal det J > 0 check (calc_lib.hpp:475-496) and GP Jacobian inverses (calc_lib.hpp:435-448)
-    if (tid < NPE)
+    if (NPE == 27 && tid < NPE + NGP)
+    {
+      // hex27 shape functions are products of 1D quadratic Lagrange factors (the tables of
+      // upload_constant_tables are built the same way), so dN comes from 9 + 9 factors instead of
+      // 81 table loads; at a node the factors are Kronecker deltas and J reduces to the 3 nodes on
+      // each parametric line through it
+      const bool at_node = tid < NPE;
+      const int g = at_node ? tid : tid - NPE;
+      const uint32_t l = sh.loc[g];
+      const int p = l & 3, q = (l >> 2) & 3, r = l >> 4;
+      double J[9];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) J[k] = 0.0;
+      if (at_node)
+      {
+#pragma unroll
+        for (int m = 0; m < 3; ++m)
+        {
+          const double* x0 = sh.X + 3 * sh.latnode[m + 3 * q + 9 * r];
+          const double* x1 = sh.X + 3 * sh.latnode[p + 3 * m + 9 * r];
+          const double* x2 = sh.X + 3 * sh.latnode[p + 3 * q + 9 * m];
+          const double d0 = sh.dLn[p][m], d1 = sh.dLn[q][m], d2 = sh.dLn[r][m];
+#pragma unroll
+          for (int c = 0; c < 3; ++c)
+          {
+            J[3 * c + 0] += d0 * x0[c];
+            J[3 * c + 1] += d1 * x1[c];
+            J[3 * c + 2] += d2 * x2[c];
+          }
+        }
+        const double det = invert3x3(J);
+        if (det == 0.0) atomicMax(&sh.bad, 2);
+        else if (!(det > 0)) atomicMax(&sh.bad, 1);
+      }
+      else
+      {
+        double Lx[3], Ly[3], Lz[3], dx[3], dy[3], dz[3];
+#pragma unroll
+        for (int m = 0; m < 3; ++m)
+        {
+          Lx[m] = sh.L1[p][m]; dx[m] = sh.dL1[p][m];
+          Ly[m] = sh.L1[q][m]; dy[m] = sh.dL1[q][m];
+          Lz[m] = sh.L1[r][m]; dz[m] = sh.dL1[r][m];
+        }
+#pragma unroll
+        for (int c = 0; c < 27; ++c)
+        {
+          const int i = kPos27[c][0], j = kPos27[c][1], k = kPos27[c][2];
+          const double d0 = Ly[j] * Lz[k] * dx[i];
+          const double d1 = Lx[i] * Lz[k] * dy[j];
+          const double d2 = Lx[i] * Ly[j] * dz[k];
+          const double x0 = sh.X[3 * c + 0], x1 = sh.X[3 * c + 1], x2 = sh.X[3 * c + 2];
+          J[0] += d0 * x0; J[1] += d1 * x0; J[2] += d2 * x0;
+          J[3] += d0 * x1; J[4] += d1 * x1; J[5] += d2 * x1;
+          J[6] += d0 * x2; J[7] += d1 * x2; J[8] += d2 * x2;
+        }
+        const double det = invert3x3(J);
+        if (det == 0.0) atomicMax(&sh.bad, 2);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) sh.invJ[9 * g + k] = J[k];
+        sh.fac[g] = det * wgp[g];
+      }
+    }
+    else if (NPE == 27)
+    {
+    }
+    else if (tid < NPE)
     {
       double J[9];
       jacobian<NPE>(dNnode + 3 * NPE * tid, sh.X, J);
@@ -375,6 +512,7 @@ __global__ __launch_bounds__(BLOCK, (NPE == 27 && MAT == 0) ? 3 : 1) void elemen
       sh.fac[g] = det * wgp[g];
     }
     __syncthreads();
+    EL_STAMP(1);
     if (sh.bad)
     {
       if (tid == 0)
@@ -397,6 +535,7 @@ __global__ __launch_bounds__(BLOCK, (NPE == 27 && MAT == 0) ? 3 : 1) void elemen
       for (int i = 0; i < 3; ++i) sh.NX[3 * v + i] = iJ[i] * d0 + iJ[i + 3] * d1 + iJ[i + 6] * d2;
     }
     __syncthreads();
+    EL_STAMP(2);
 
     // 4. strains and StVK stress per Gauss point
     if (tid < NGP)
@@ -492,6 +631,7 @@ __global__ __launch_bounds__(BLOCK, (NPE == 27 && MAT == 0) ? 3 : 1) void elemen
       }
     }
     __syncthreads();
+    EL_STAMP(3);
     if (KIN == 1)
     {
       if (sh.bad)
@@ -514,6 +654,7 @@ __global__ __launch_bounds__(BLOCK, (NPE == 27 && MAT == 0) ? 3 : 1) void elemen
         for (int i = 0; i < 3; ++i) sh.P[3 * v + i] = F[i] * n0 + F[i + 3] * n1 + F[i + 6] * n2;
       }
       __syncthreads();
+      EL_STAMP(4);
     }
 
     const int32_t* inc = A.inc_of + e * NPE;
@@ -705,37 +846,66 @@ __global__ __launch_bounds__(BLOCK, (NPE == 27 && MAT == 0) ? 3 : 1) void elemen
         b = p - NPE * (p / NPE);
       }
     };
-    if constexpr (ASM != 0)
+    if constexpr (NPE == 27 && (KIN == 0 || ASM != 0))
     {
       if (A.want_k)
       {
-      static_assert(NPE == 27, "colour-ordered direct assembly is the hex27 path");
       // blocks a <= b into registers, then (after every thread's last N_XYZ / P read) into the
-      // LDS image KS; then the element's 81 rows leave in runs of contiguous columns (element
-      // nodes in lattice order) -- written by the first element of the colour order that holds
-      // both nodes, added to by the others
-      double Kq[2][9];
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
+      // LDS image KS; then the element's owned block rows leave coalesced: general path (ASM 0)
+      // as contiguous incidence records [3][27 nodes][3] of the scratch; colour-ordered path as
+      // runs of contiguous CSR columns (element nodes in lattice order) -- written by the first
+      // element of the colour order that holds both nodes, added to by the others
+      double* KS = sh.ks();
+      if constexpr (KIN == 0)
       {
-        const int p = tid + BLOCK * q;
-        if (p < NPAIR)
+        for (int p = tid; p < NPAIR; p += BLOCK)
         {
           int a, b;
           pair_of(p, a, b);
-          if (sh.inc[a] >= 0 || sh.inc[b] >= 0) pair_block(a, b, Kq[q]);
+          if (sh.inc[a] >= 0 || sh.inc[b] >= 0) pair_block(a, b, KS + 9 * p);
+        }
+      }
+      else
+      {
+        double Kq[2][9];
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+        {
+          const int p = tid + BLOCK * q;
+          if (p < NPAIR)
+          {
+            int a, b;
+            pair_of(p, a, b);
+            if (sh.inc[a] >= 0 || sh.inc[b] >= 0) pair_block(a, b, Kq[q]);
+          }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+        {
+          const int p = tid + BLOCK * q;
+          if (p < NPAIR)
+#pragma unroll
+            for (int k = 0; k < 9; ++k) KS[9 * p + k] = Kq[q][k];
         }
       }
       __syncthreads();
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
+      if constexpr (ASM == 0)
       {
-        const int p = tid + BLOCK * q;
-        if (p < NPAIR)
-#pragma unroll
-          for (int k = 0; k < 9; ++k) sh.KS[9 * p + k] = Kq[q][k];
+        for (int v = tid; v < NPE * 243; v += BLOCK)
+        {
+          const int a = v / 243;
+          if (sh.inc[a] < 0) continue;
+          const int r = v - 243 * a;
+          const int i = r / 81, c = r - 81 * (r / 81);
+          const int b = c / 3, j = c - 3 * (c / 3);
+          const int lo = a < b ? a : b, hi = a < b ? b : a;
+          const int pidx = 27 * lo - (lo * (lo - 1)) / 2 + hi - lo;
+          A.scratch[int64_t(sh.inc[a]) * REC + r] = KS[9 * pidx + (a <= b ? i + 3 * j : j + 3 * i)];
+        }
       }
-      __syncthreads();
+      else
+      {
       constexpr int NV = 9;  // entries in flight per thread: all loads before the stores
       for (int v0 = 0; v0 < NPE * 243; v0 += NV * BLOCK)
       {
@@ -757,13 +927,14 @@ __global__ __launch_bounds__(BLOCK, (NPE == 27 && MAT == 0) ? 3 : 1) void elemen
           slot[k] = uint32_t(a) | (o << 5);
           const int lo = a < b ? a : b, hi = a < b ? b : a;
           const int pidx = 27 * lo - (lo * (lo - 1)) / 2 + hi - lo;
-          val[k] = sh.KS[9 * pidx + (a <= b ? i + 3 * j : j + 3 * i)];
+          val[k] = KS[9 * pidx + (a <= b ? i + 3 * j : j + 3 * i)];
           if (!(ASM == 2 && first_touch27(sh.loc, ft, a, b))) val[k] += A.K[sh.rbase[a] + o];
         }
 #pragma unroll
         for (int k = 0; k < NV; ++k)
           if (slot[k] != 0xFFFFFFFFu)
             __builtin_nontemporal_store(val[k], A.K + sh.rbase[slot[k] & 31u] + (slot[k] >> 5));
+      }
       }
       }
     }
@@ -797,7 +968,17 @@ __global__ __launch_bounds__(BLOCK, (NPE == 27 && MAT == 0) ? 3 : 1) void elemen
       }
     }
     __syncthreads();
+    EL_STAMP(5);
   }
+#ifdef FCG_ELEMENT_STAMPS
+  if (A.stamps && tid == 0)
+  {
+    for (int i = 0; i < 6; ++i) atomicAdd(&A.stamps[i], st_acc[i]);
+    atomicAdd(&A.stamps[6], (unsigned long long)((n_it - blockIdx.x + gridDim.x - 1) / gridDim.x));
+    atomicAdd(&A.stamps[7], 1ull);
+  }
+#endif
+#undef EL_STAMP
 }
 
 // ---------------------------------------------------------------------------------- hex8, 8 lanes/element
@@ -1025,6 +1206,7 @@ hipError_t launch_element(const DeviceMesh& m, const double* d_u_col, bool want_
   a.mu = m.mu;
   a.cdiag = m.cdiag;
   a.want_k = want_k ? 1 : 0;
+  a.stamps = m.stamps;
   a.nh_c = m.nh_c;
   a.nh_beta = m.nh_beta;
   if (m.material == FCG_MAT_ELASTHYPER_COUPNEOHOOKE)
@@ -1074,6 +1256,7 @@ hipError_t launch_element_colored(const DeviceMesh& m, const double* d_u_col, bo
   a.mu = m.mu;
   a.cdiag = m.cdiag;
   a.want_k = want_k ? 1 : 0;
+  a.stamps = m.stamps;
   a.nh_c = m.nh_c;
   a.nh_beta = m.nh_beta;
   a.col_ele = m.col_ele;

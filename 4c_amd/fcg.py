@@ -12,6 +12,9 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "lib", "libfourc_gpu.so")
+# diagnostics only: FCG_LIB=diag loads the phase-stamp build (make -C 4c_amd diag)
+if os.environ.get("FCG_LIB") == "diag":
+    LIB_PATH = os.path.join(PKG_DIR, "lib", "libfourc_gpu_diag.so")
 
 HEX8, HEX27 = 0, 1
 LINEAR, TOTLAG = 0, 1
