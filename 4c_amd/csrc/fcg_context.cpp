@@ -89,7 +89,7 @@ const int kOff8[8][3] = {{0, 0, 0}, {1, 0, 0}, {1, 1, 0}, {0, 1, 0}, {0, 0, 1}, 
     {0, 1, 1}};  // hex8 4C node order (4C_io_gridgenerator.cpp:371-379)
 
 bool build_structured_plan(const fcg_desc* d, const std::vector<int32_t>& rownodes,
-    const std::vector<int32_t>& row0, const int32_t* kcol, StructHost& P, std::string& why)
+    const std::vector<int32_t>& row0, const int32_t* kcol, int cus, StructHost& P, std::string& why)
 {
   if (d->celltype != FCG_HEX8 || !d->ele_ijk)
   {
@@ -234,11 +234,29 @@ bool build_structured_plan(const fcg_desc* d, const std::vector<int32_t>& rownod
     why = err;
     return false;
   }
-  // tiles: 4 x 4 node columns, z split into segments for >= ~8 workgroups per CU
+  // tiles: 4 x 4 node columns, z split into segments.  The workgroups are alike, so the sweep
+  // runs in rounds of `slots` resident workgroups (CUs x workgroups per CU: 2 for the linear /
+  // TSI sweep, 1 for TotLag, LDS-bound); a segment of s planes costs s + 1 element layers (it
+  // starts one layer early).  Pick the segment count with the least rounds x layers -- e.g. 100^3
+  // linear on 256 CUs: 3 segments of 34 planes, 2,028 workgroups in 4 full rounds, where a fixed
+  // ">= 2,048 workgroups" rule gave 4 segments, 2,704 workgroups and a 28 %-full sixth round.
   P.tiles_x = (P.n[0] + 3) / 4;
   P.tiles_y = (P.n[1] + 3) / 4;
   const int64_t txy = int64_t(P.tiles_x) * P.tiles_y;
-  int64_t nseg = std::max<int64_t>(1, std::min<int64_t>(P.n[2], (2048 + txy - 1) / txy));
+  const int64_t slots = int64_t(std::max(1, cus)) * (d->kinematics == FCG_TOTLAG ? 1 : 2);
+  int64_t nseg = 1;
+  double best = 0.0;
+  for (int64_t k = 1; k <= std::min<int64_t>(P.n[2], 64); ++k)
+  {
+    const int64_t segk = (P.n[2] + k - 1) / k;
+    const int64_t wgs = txy * ((P.n[2] + segk - 1) / segk);
+    const double cost = double((wgs + slots - 1) / slots) * double(segk + 1);
+    if (k == 1 || cost < best)
+    {
+      best = cost;
+      nseg = k;
+    }
+  }
   P.seg = int32_t((P.n[2] + nseg - 1) / nseg);
   P.tiles_z = (P.n[2] + P.seg - 1) / P.seg;
   // lattice node tables (coordinates and DOF column LIDs, by lattice position)
@@ -545,7 +563,15 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
   bool structured = false;
   if (d->path != FCG_PATH_GENERAL && d->material == FCG_MAT_STVK)
   {
-    structured = build_structured_plan(d, rownodes, row0, kcol, sp, why);
+    // compute units of the target device (the segment count depends on it; 256 when the device
+    // cannot be queried, e.g. plan checks on a host without GPU)
+    int cus = 256;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, d->device) == hipSuccess && prop.multiProcessorCount > 0)
+      cus = prop.multiProcessorCount;
+    else
+      (void)hipGetLastError();
+    structured = build_structured_plan(d, rownodes, row0, kcol, cus, sp, why);
     if (!structured && d->path == FCG_PATH_STRUCTURED && d->celltype == FCG_HEX8)
     {
       set_create_error("structured path requested but the lattice hint does not verify: " + why);
