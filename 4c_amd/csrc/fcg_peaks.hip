@@ -1,0 +1,133 @@
+// fcg_peaks.hip -- on-box re-measurement of the two peaks SURVEY §8d prices the assembly against
+// (HBM bandwidth, FP64 throughput): a STREAM triad over HBM-resident arrays, an FP64 VALU FMA loop
+// and an FP64 MFMA loop (v_mfma_f64_16x16x4_f64), each timed with hipEvents over repeated
+// launches that fill every CU.  bench.py reports these beside the spec peaks it divides by.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "fourc_gpu.h"
+
+namespace {
+
+__global__ __launch_bounds__(256) void triad_kernel(const double* __restrict__ b,
+    const double* __restrict__ c, double* __restrict__ a, double s, int64_t n)
+{
+  // two 16-byte pieces per lane per step, one wave-contiguous 1 KiB block apart
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x * 4;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x * 4 + 2 * threadIdx.x; i < n; i += stride)
+  {
+    const double2 b0 = *reinterpret_cast<const double2*>(b + i);
+    const double2 c0 = *reinterpret_cast<const double2*>(c + i);
+    const double2 b1 = *reinterpret_cast<const double2*>(b + i + 2 * blockDim.x);
+    const double2 c1 = *reinterpret_cast<const double2*>(c + i + 2 * blockDim.x);
+    *reinterpret_cast<double2*>(a + i) = make_double2(b0.x + s * c0.x, b0.y + s * c0.y);
+    *reinterpret_cast<double2*>(a + i + 2 * blockDim.x) = make_double2(b1.x + s * c1.x, b1.y + s * c1.y);
+  }
+}
+
+// NCH independent FMA chains per lane; the result is stored so nothing is dead code
+constexpr int NCH = 16;
+__global__ __launch_bounds__(256) void fma_kernel(double* out, int iters, double x)
+{
+  double v[NCH];
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) v[k] = x + k + threadIdx.x;
+  const double m = 0.999999, c = 1e-7;
+  for (int i = 0; i < iters; ++i)
+  {
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) v[k] = fma(v[k], m, c);
+  }
+  double s = 0.0;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) s += v[k];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+// NACC independent accumulators of v_mfma_f64_16x16x4_f64 per wave (2 * 16 * 16 * 4 flop each)
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+constexpr int NACC = 8;
+__global__ __launch_bounds__(256) void mfma_kernel(double* out, int iters, double x)
+{
+  f64x4 acc[NACC];
+#pragma unroll
+  for (int k = 0; k < NACC; ++k) acc[k] = f64x4{0.0, 0.0, 0.0, 0.0};
+  const double a = x + threadIdx.x * 1e-3, b = 1.0 - threadIdx.x * 1e-4;
+  for (int i = 0; i < iters; ++i)
+  {
+#pragma unroll
+    for (int k = 0; k < NACC; ++k)
+      acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[k], 0, 0, 0);
+  }
+  double s = 0.0;
+#pragma unroll
+  for (int k = 0; k < NACC; ++k) s += acc[k][0] + acc[k][1] + acc[k][2] + acc[k][3];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+template <class F>
+float time_ms(hipStream_t s, int reps, F launch)
+{
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  launch();  // warm-up
+  (void)hipEventRecord(e0, s);
+  for (int r = 0; r < reps; ++r) launch();
+  (void)hipEventRecord(e1, s);
+  (void)hipEventSynchronize(e1);
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return ms / reps;
+}
+
+}  // namespace
+
+extern "C" int fcg_measure_peaks(int device, double* hbm_triad_gbs, double* fp64_valu_tflops,
+    double* fp64_mfma_tflops)
+{
+  if (hipSetDevice(device) != hipSuccess) return FCG_ERR_DEVICE;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return FCG_ERR_DEVICE;
+  const int cus = std::max(1, prop.multiProcessorCount);
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return FCG_ERR_DEVICE;
+  int rc = FCG_OK;
+  // triad over 3 x 1 GiB (far beyond the 256 MB Infinity Cache)
+  const int64_t n = int64_t(1) << 27;
+  double *a = nullptr, *b = nullptr, *c = nullptr, *out = nullptr;
+  const int grid_v = cus * 8, iters = 4096;
+  if (hipMalloc(&a, n * 8) != hipSuccess || hipMalloc(&b, n * 8) != hipSuccess ||
+      hipMalloc(&c, n * 8) != hipSuccess || hipMalloc(&out, int64_t(grid_v) * 256 * 8) != hipSuccess)
+    rc = FCG_ERR_DEVICE;
+  if (rc == FCG_OK)
+  {
+    (void)hipMemsetAsync(b, 0, n * 8, s);
+    (void)hipMemsetAsync(c, 0, n * 8, s);
+    const float ms = time_ms(s, 10, [&] {
+      hipLaunchKernelGGL(triad_kernel, dim3(cus * 32), dim3(256), 0, s, b, c, a, 3.0, n);
+    });
+    if (hbm_triad_gbs) *hbm_triad_gbs = 3.0 * 8.0 * double(n) / (ms * 1e-3) / 1e9;
+    const float mv = time_ms(s, 5, [&] {
+      hipLaunchKernelGGL(fma_kernel, dim3(grid_v), dim3(256), 0, s, out, iters, 1.0);
+    });
+    if (fp64_valu_tflops)
+      *fp64_valu_tflops = 2.0 * NCH * double(iters) * grid_v * 256 / (mv * 1e-3) / 1e12;
+    const float mm = time_ms(s, 5, [&] {
+      hipLaunchKernelGGL(mfma_kernel, dim3(grid_v), dim3(256), 0, s, out, iters / NACC, 1.0);
+    });
+    // per wave and instruction: 16 x 16 x 4 multiply-adds
+    if (fp64_mfma_tflops)
+      *fp64_mfma_tflops =
+          2.0 * 1024.0 * NACC * double(iters / NACC) * grid_v * 4 / (mm * 1e-3) / 1e12;
+    if (hipStreamSynchronize(s) != hipSuccess || hipGetLastError() != hipSuccess) rc = FCG_ERR_DEVICE;
+  }
+  for (double* p : {a, b, c, out})
+    if (p) (void)hipFree(p);
+  (void)hipStreamDestroy(s);
+  return rc;
+}

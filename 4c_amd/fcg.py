@@ -81,7 +81,8 @@ class FcgTsiDesc(ctypes.Structure):
 EXPORTS = ["fcg_create", "fcg_destroy", "fcg_last_error", "fcg_evaluate", "fcg_evaluate_device",
            "fcg_device_alloc", "fcg_device_free", "fcg_memcpy_h2d", "fcg_memcpy_d2h",
            "fcg_memset_device", "fcg_set_timing", "fcg_get_timing", "fcg_get_info",
-           "fcg_get_diagnostics", "fcg_spmv", "fcg_dirichlet_apply", "fcg_pcg_solve",
+           "fcg_get_diagnostics", "fcg_measure_peaks", "fcg_spmv", "fcg_dirichlet_apply",
+           "fcg_pcg_solve",
            "fcg_neumann_surface", "fcg_neumann_volume",
            "fcg_graph_build_device",
            "fcg_tsi_create", "fcg_tsi_destroy", "fcg_tsi_last_error", "fcg_tsi_evaluate_device",
@@ -131,6 +132,7 @@ def lib():
     L.fcg_get_info.argtypes = [vp, ctypes.POINTER(FcgInfo)]
     L.fcg_get_diagnostics.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
     L.fcg_spmv.argtypes = [vp, vp, vp, vp, vp]
+    L.fcg_measure_peaks.argtypes = [ctypes.c_int, _dp, _dp, _dp]
     L.fcg_dirichlet_apply.argtypes = [vp, ctypes.c_int64, vp, vp, vp, vp, vp]
     L.fcg_pcg_solve.argtypes = [vp, vp, vp, vp, ctypes.c_double, ctypes.c_int,
                                 ctypes.POINTER(ctypes.c_int), _dp, vp]
@@ -641,3 +643,12 @@ def graph_build_device(celltype, ele_nodes, node_dof_col, node_dof_row, n_rows, 
     if rc != 0:
         raise FcgError(rc, "fcg_graph_build_device failed")
     return rowptr, col[:nnz.value]
+
+
+def measure_peaks(device=0):
+    """fcg_measure_peaks: (STREAM-triad GB/s, FP64 VALU TFLOP/s, FP64 MFMA TFLOP/s) on `device`."""
+    a, b, c = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+    rc = lib().fcg_measure_peaks(int(device), ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+    if rc != 0:
+        raise FcgError(rc, "fcg_measure_peaks failed")
+    return a.value, b.value, c.value

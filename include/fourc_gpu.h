@@ -159,6 +159,12 @@ typedef struct fcg_info {
 } fcg_info;
 int fcg_get_info(const fcg_ctx* ctx, fcg_info* info);
 
+/* On-box peaks for the roofline (SURVEY §8d asks to re-measure the spec figures): STREAM triad
+ * bandwidth over 3 x 1 GiB HBM arrays (GB/s), FP64 VALU FMA and FP64 MFMA (v_mfma_f64_16x16x4_f64)
+ * throughput (TFLOP/s), each on every CU of `device`.  Outputs may be NULL. */
+int fcg_measure_peaks(int device, double* hbm_triad_gbs, double* fp64_valu_tflops,
+    double* fp64_mfma_tflops);
+
 /* Diagnostics only: with FCG_STAMPS=1 in the environment at fcg_create, the fused kernel sums
  * per-phase cycle counts (s_memtime, thread 0 of every workgroup) into 8 counters: commit,
  * Gauss-point stage, node-row stage, accumulation, flush, workgroups (index 5).  Returns the number of
