@@ -1090,6 +1090,100 @@ struct AssembleArgs {
   double* fint;
 };
 
+// hex27 rows: one wavefront per owned row node as assemble_kernel, the incidence records read as
+// 16-byte pieces, two records in flight before their sums enter the LDS row image (each
+// record adds to distinct columns and a wavefront's LDS operations execute in order: no barrier
+// between records).  Summation order per entry = incidence order, as in assemble_kernel.
+template <bool WANT_K, bool OVERWRITE>
+__global__ __launch_bounds__(64) void assemble27_kernel(AssembleArgs A)
+{
+  constexpr int NPE = 27, REC = 9 * NPE + 3, NB = 2;
+  constexpr int NV2 = 2;  // double2 pieces per lane and record: 122 pieces of the 243 entries
+  __shared__ double acc[WANT_K ? 3 * 375 : 1];
+  const int lane = threadIdx.x;
+  for (int64_t r = blockIdx.x; r < A.n_rownodes; r += gridDim.x)
+  {
+    const int32_t row0 = A.rownode_row0[r];
+    const int64_t base = A.rowptr[row0];
+    const int rowlen = int(A.rowptr[row0 + 1] - base);
+    if (WANT_K)
+      for (int v = lane; v < 3 * rowlen; v += 64) acc[v] = 0.0;
+    double f = 0.0;
+    const int64_t k0 = A.inc_ptr[r], k1 = A.inc_ptr[r + 1];
+    for (int64_t kb = k0; kb < k1; kb += NB)
+    {
+      double2 val[NB][NV2];
+      int dst[NB][NV2][2];
+      double fv[NB];
+#pragma unroll
+      for (int q = 0; q < NB; ++q)
+      {
+        const int64_t k = kb + q;
+        fv[q] = 0.0;
+#pragma unroll
+        for (int s = 0; s < NV2; ++s)
+        {
+          val[q][s] = make_double2(0.0, 0.0);
+          dst[q][s][0] = dst[q][s][1] = -1;
+        }
+        if (k >= k1) continue;
+        const double* src = A.scratch + k * REC;
+        if (lane < 3) fv[q] = src[243 + lane];
+        if (!WANT_K) continue;
+        const uint16_t* pos = A.inc_pos + k * NPE;
+#pragma unroll
+        for (int s = 0; s < NV2; ++s)
+        {
+          const int v2 = lane + 64 * s;
+          if (v2 >= 122) continue;
+          val[q][s] = *reinterpret_cast<const double2*>(src + 2 * v2);
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+          {
+            const int d = 2 * v2 + h;
+            if (d >= 243) continue;
+            const int i = d / 81, rem = d - 81 * (d / 81);
+            const int b = rem / 3, j = rem - 3 * (rem / 3);
+            dst[q][s][h] = i * rowlen + pos[b] + j;
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < NB; ++q)
+      {
+        f += fv[q];
+        if (WANT_K)
+#pragma unroll
+          for (int s = 0; s < NV2; ++s)
+          {
+            if (dst[q][s][0] >= 0) acc[dst[q][s][0]] += val[q][s].x;
+            if (dst[q][s][1] >= 0) acc[dst[q][s][1]] += val[q][s].y;
+          }
+      }
+    }
+    __syncthreads();
+    if (WANT_K)
+    {
+      double* out = A.K + base;  // the node's 3 rows are contiguous (checked at setup)
+      for (int v = lane; v < 3 * rowlen; v += 64)
+      {
+        if (OVERWRITE)
+          out[v] = acc[v];
+        else
+          out[v] += acc[v];
+      }
+    }
+    if (lane < 3)
+    {
+      if (OVERWRITE)
+        A.fint[row0 + lane] = f;
+      else
+        A.fint[row0 + lane] += f;
+    }
+    __syncthreads();
+  }
+}
+
 template <int NPE, bool WANT_K, bool OVERWRITE>
 __global__ __launch_bounds__(64) void assemble_kernel(AssembleArgs A)
 {
@@ -1325,7 +1419,14 @@ hipError_t launch_assemble(const DeviceMesh& m, bool want_k, bool overwrite, dou
   }
   else
   {
-    FCG_ASM(27)
+    if (want_k && overwrite)
+      hipLaunchKernelGGL((assemble27_kernel<true, true>), dim3(grid), dim3(64), 0, stream, a);
+    else if (want_k)
+      hipLaunchKernelGGL((assemble27_kernel<true, false>), dim3(grid), dim3(64), 0, stream, a);
+    else if (overwrite)
+      hipLaunchKernelGGL((assemble27_kernel<false, true>), dim3(grid), dim3(64), 0, stream, a);
+    else
+      hipLaunchKernelGGL((assemble27_kernel<false, false>), dim3(grid), dim3(64), 0, stream, a);
   }
 #undef FCG_ASM
   return hipGetLastError();
