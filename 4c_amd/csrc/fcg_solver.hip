@@ -18,6 +18,7 @@
 //    node as blocks.)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <string>
 #include <vector>
@@ -57,41 +58,46 @@ __global__ __launch_bounds__(kBlock) void spmv_node_kernel(const int64_t* __rest
     int64_t n_nodes, const double* __restrict__ dotw, double* partial)
 {
   __shared__ double sbuf[kBlock / 64];
-  const int64_t node = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / LPN;
   const int lane = threadIdx.x % LPN;
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-  int32_t row0 = 0;
-  if (node < n_nodes)
-  {
-    row0 = row0_of[node];
-    const int64_t s = rowptr[row0];
-    const int64_t len = rowptr[row0 + 1] - s;
-    const double* v0 = vals + s;
-    const double* v1 = v0 + len;
-    const double* v2 = v1 + len;
-    for (int64_t k = 3 * lane; k < len; k += 3 * LPN)
-    {
-      const int32_t c = col[s + k];
-      const double x0 = x[c], x1 = x[c + 1], x2 = x[c + 2];
-      a0 += v0[k] * x0 + v0[k + 1] * x1 + v0[k + 2] * x2;
-      a1 += v1[k] * x0 + v1[k + 1] * x1 + v1[k + 2] * x2;
-      a2 += v2[k] * x0 + v2[k + 1] * x1 + v2[k + 2] * x2;
-    }
-  }
-#pragma unroll
-  for (int o = LPN / 2; o >= 1; o >>= 1)
-  {
-    a0 += __shfl_xor(a0, o, LPN);
-    a1 += __shfl_xor(a1, o, LPN);
-    a2 += __shfl_xor(a2, o, LPN);
-  }
+  const int64_t step = int64_t(gridDim.x) * (kBlock / LPN);
   double mine = 0.0;
-  if (node < n_nodes && lane == 0)
+  // grid-stride over the nodes: a bounded number of blocks keeps the dot partials few
+  for (int64_t node = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / LPN; node - (threadIdx.x / LPN) <
+       n_nodes; node += step)
   {
-    y[row0] = a0;
-    y[row0 + 1] = a1;
-    y[row0 + 2] = a2;
-    if (dotw) mine = dotw[row0] * a0 + dotw[row0 + 1] * a1 + dotw[row0 + 2] * a2;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+    int32_t row0 = 0;
+    if (node < n_nodes)
+    {
+      row0 = row0_of[node];
+      const int64_t s = rowptr[row0];
+      const int64_t len = rowptr[row0 + 1] - s;
+      const double* v0 = vals + s;
+      const double* v1 = v0 + len;
+      const double* v2 = v1 + len;
+      for (int64_t k = 3 * lane; k < len; k += 3 * LPN)
+      {
+        const int32_t c = col[s + k];
+        const double x0 = x[c], x1 = x[c + 1], x2 = x[c + 2];
+        a0 += v0[k] * x0 + v0[k + 1] * x1 + v0[k + 2] * x2;
+        a1 += v1[k] * x0 + v1[k + 1] * x1 + v1[k + 2] * x2;
+        a2 += v2[k] * x0 + v2[k + 1] * x1 + v2[k + 2] * x2;
+      }
+    }
+#pragma unroll
+    for (int o = LPN / 2; o >= 1; o >>= 1)
+    {
+      a0 += __shfl_xor(a0, o, LPN);
+      a1 += __shfl_xor(a1, o, LPN);
+      a2 += __shfl_xor(a2, o, LPN);
+    }
+    if (node < n_nodes && lane == 0)
+    {
+      y[row0] = a0;
+      y[row0 + 1] = a1;
+      y[row0 + 2] = a2;
+      if (dotw) mine += dotw[row0] * a0 + dotw[row0 + 1] * a1 + dotw[row0 + 2] * a2;
+    }
   }
   if (partial)
   {
@@ -148,9 +154,9 @@ __global__ __launch_bounds__(kBlock) void pcg_init_kernel(const int32_t* __restr
     double* p, int64_t n_nodes, double* part_rz, double* part_rr)
 {
   __shared__ double sbuf[kBlock / 64];
-  const int64_t k = int64_t(blockIdx.x) * kBlock + threadIdx.x;
   double rz = 0.0, rr = 0.0;
-  if (k < n_nodes)
+  for (int64_t k = int64_t(blockIdx.x) * kBlock + threadIdx.x; k < n_nodes;
+       k += int64_t(gridDim.x) * kBlock)
   {
     const int32_t i = row0_of[k];
     double ri[3], zi[3];
@@ -185,9 +191,9 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(const int32_t* __res
 {
   __shared__ double sbuf[kBlock / 64];
   const double alpha = sc[SC_ALPHA];
-  const int64_t k = int64_t(blockIdx.x) * kBlock + threadIdx.x;
   double rz = 0.0, rr = 0.0;
-  if (k < n_nodes)
+  for (int64_t k = int64_t(blockIdx.x) * kBlock + threadIdx.x; k < n_nodes;
+       k += int64_t(gridDim.x) * kBlock)
   {
     const int32_t i = row0_of[k];
     double ri[3], zi[3];
@@ -297,6 +303,31 @@ __global__ __launch_bounds__(kBlock) void dirichlet_kernel(const int64_t* __rest
 }
 
 inline unsigned blocks_for(int64_t n, int per_block) { return unsigned((n + per_block - 1) / per_block); }
+// grid-stride kernels with dot partials: at most this many blocks (16 per CU of a 256-CU part),
+// so the single-block reductions of the partials stay short
+constexpr int64_t kMaxBlocks = 4096;
+inline unsigned capped_blocks(int64_t n, int per_block)
+{
+  return unsigned(std::min<int64_t>(kMaxBlocks, std::max<int64_t>(1, (n + per_block - 1) / per_block)));
+}
+
+// one node per LPN lanes; with dot partials the grid is capped (grid-stride) so they stay few
+inline unsigned spmv_grid(const DeviceMesh& m, int lpn, bool partials)
+{
+  return partials ? capped_blocks(m.n_rownodes * lpn, kBlock) : blocks_for(m.n_rownodes * lpn, kBlock);
+}
+
+// partial[blockIdx] = sum over the block's rows of p . q (grid-stride, fixed assignment)
+__global__ __launch_bounds__(kBlock) void dot_kernel(const double* __restrict__ p,
+    const double* __restrict__ q, int64_t n, double* partial)
+{
+  __shared__ double sbuf[kBlock / 64];
+  double t = 0.0;
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock)
+    t += p[i] * q[i];
+  const double b = block_sum(t, sbuf);
+  if (threadIdx.x == 0) partial[blockIdx.x] = b;
+}
 
 hipError_t launch_spmv(const DeviceMesh& m, const double* K, const double* x, double* y,
     const double* dotw, double* partial, hipStream_t s)
@@ -304,20 +335,16 @@ hipError_t launch_spmv(const DeviceMesh& m, const double* K, const double* x, do
   if (m.n_rows == 0) return hipSuccess;
   // node rows (every owned row belongs to a node triple, fcg_create checks the pattern)
   if (m.npe == 27)
-    hipLaunchKernelGGL((spmv_node_kernel<64>), dim3(blocks_for(m.n_rownodes * 64, kBlock)),
+    hipLaunchKernelGGL((spmv_node_kernel<64>), dim3(spmv_grid(m, 64, partial != nullptr)),
         dim3(kBlock), 0, s, m.rowptr, m.rownode_row0, m.col_lid, K, x, y, m.n_rownodes, dotw,
         partial);
   else
-    hipLaunchKernelGGL((spmv_node_kernel<16>), dim3(blocks_for(m.n_rownodes * 16, kBlock)),
+    hipLaunchKernelGGL((spmv_node_kernel<16>), dim3(spmv_grid(m, 16, partial != nullptr)),
         dim3(kBlock), 0, s, m.rowptr, m.rownode_row0, m.col_lid, K, x, y, m.n_rownodes, dotw,
         partial);
   return hipGetLastError();
 }
 
-int64_t spmv_blocks(const DeviceMesh& m)
-{
-  return blocks_for(m.n_rownodes * (m.npe == 27 ? 64 : 16), kBlock);
-}
 
 }  // namespace
 
@@ -399,9 +426,9 @@ int fcg_pcg_solve(fcg_ctx* ctx, const double* d_K_vals, const double* d_b_row, d
     return FCG_ERR_ARG;
   }
   const int64_t nb_vec = fcg::blocks_for(n, fcg::kBlock);
-  const int64_t nb_node = fcg::blocks_for(nn, fcg::kBlock);
-  const int64_t nb_mv = fcg::spmv_blocks(m);
-  const int64_t nb = std::max(nb_node, nb_mv);
+  const int64_t nb_node = fcg::capped_blocks(nn, fcg::kBlock);
+  const int64_t nb_dot = fcg::capped_blocks(n, fcg::kBlock);
+  const int64_t nb = std::max(nb_node, nb_dot);
   if (!m.pcg_work || m.pcg_n != n)
   {
     if (m.pcg_work) (void)hipFree(m.pcg_work);
@@ -427,7 +454,7 @@ int fcg_pcg_solve(fcg_ctx* ctx, const double* d_K_vals, const double* d_b_row, d
   he = hipMemcpyAsync(m.err, &zero, sizeof(zero), hipMemcpyHostToDevice, s);
   if (he == hipSuccess)
   {
-    hipLaunchKernelGGL(fcg::block_jacobi_kernel, dim3(nb_node), dim3(fcg::kBlock), 0, s,
+    hipLaunchKernelGGL(fcg::block_jacobi_kernel, dim3(fcg::blocks_for(nn, fcg::kBlock)), dim3(fcg::kBlock), 0, s,
         m.rownode_row0, m.diag_pos, d_K_vals, dinv, nn, m.err);
     hipLaunchKernelGGL(fcg::pcg_init_kernel, dim3(nb_node), dim3(fcg::kBlock), 0, s, m.rownode_row0,
         d_b_row, dinv, d_x_row, r, z, p, nn, pa, pb);
@@ -461,9 +488,11 @@ int fcg_pcg_solve(fcg_ctx* ctx, const double* d_K_vals, const double* d_b_row, d
     const int burst = std::min(check_every, max_iter - it);
     for (int k = 0; k < burst; ++k)
     {
-      he = fcg::launch_spmv(m, d_K_vals, p, q, p, pa, s);
+      // q = K p (full-width grid), then p . q over a capped grid of block partials
+      he = fcg::launch_spmv(m, d_K_vals, p, q, nullptr, nullptr, s);
       if (he != hipSuccess) break;
-      hipLaunchKernelGGL(fcg::reduce_kernel, dim3(1), dim3(fcg::kBlock), 0, s, pa, nb_mv, sc,
+      hipLaunchKernelGGL(fcg::dot_kernel, dim3(nb_dot), dim3(fcg::kBlock), 0, s, p, q, n, pa);
+      hipLaunchKernelGGL(fcg::reduce_kernel, dim3(1), dim3(fcg::kBlock), 0, s, pa, nb_dot, sc,
           int(fcg::SC_PQ), 1, nullptr, 0);
       hipLaunchKernelGGL(fcg::pcg_update_kernel, dim3(nb_node), dim3(fcg::kBlock), 0, s,
           m.rownode_row0, p, q, dinv, d_x_row, r, z, nn, sc, pb, pc);
