@@ -431,6 +431,7 @@ void free_mesh(fcg::DeviceMesh& m)
       m.tables, m.stamps, m.col_lid, m.diag_pos, m.pcg_work, m.col_ele, m.ele_ft, m.inc_row0};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  if (m.err_host) (void)hipHostFree(m.err_host);
   m = fcg::DeviceMesh{};
 }
 
@@ -739,6 +740,8 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
     chk(upload(&m.diag_pos, diag.data(), d->n_rows, bytes));
   }
   chk(upload<int32_t>(&m.err, nullptr, 2, bytes));
+  if (he == hipSuccess) he = hipHostMalloc(reinterpret_cast<void**>(&m.err_host), 2 * sizeof(int32_t),
+      hipHostMallocDefault);
   if (structured)
   {
     m.path = FCG_PATH_STRUCTURED;
@@ -841,7 +844,8 @@ int fcg_evaluate_device(fcg_ctx* ctx, int action, int mode, const double* d_u_co
   (void)hipSetDevice(ctx->device);
   hipStream_t s = stream_ptr ? static_cast<hipStream_t>(stream_ptr) : ctx->stream;
   const int32_t init[2] = {0, INT32_MAX};
-  hipError_t he = hipMemcpyAsync(m.err, init, sizeof(init), hipMemcpyHostToDevice, s);
+  hipError_t he = hipSuccess;
+  if (!m.err_clean) he = hipMemcpyAsync(m.err, init, sizeof(init), hipMemcpyHostToDevice, s);
   auto& T = ctx->timing;
   if (T.enabled && he == hipSuccess) he = hipEventRecord(T.ev[0], s);
   if (m.path == FCG_PATH_STRUCTURED)
@@ -865,14 +869,16 @@ int fcg_evaluate_device(fcg_ctx* ctx, int action, int mode, const double* d_u_co
       he = fcg::launch_assemble(m, want_k, mode == FCG_OVERWRITE, d_K_vals, d_fint_row, s);
   }
   if (T.enabled && he == hipSuccess) he = hipEventRecord(T.ev[2], s);
-  int32_t errv[2] = {0, INT32_MAX};
-  if (he == hipSuccess) he = hipMemcpyAsync(errv, m.err, sizeof(errv), hipMemcpyDeviceToHost, s);
+  int32_t* errv = m.err_host;
+  if (he == hipSuccess) he = hipMemcpyAsync(errv, m.err, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, s);
   if (he == hipSuccess) he = hipStreamSynchronize(s);
   if (he != hipSuccess)
   {
+    m.err_clean = false;
     ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
     return FCG_ERR_DEVICE;
   }
+  m.err_clean = errv[0] == 0;  // no failing element: err still {0, INT32_MAX}
   if (T.enabled)
   {
     float a = 0.f, b = 0.f;

@@ -34,6 +34,11 @@ struct DeviceMesh {
   int64_t* rowptr = nullptr;        // [n_rows+1]
   double* scratch = nullptr;        // [n_inc][record_doubles(npe)]
   int32_t* err = nullptr;           // [2]: code, min failing element index
+  // evaluate's error-flag protocol: err holds {0, INT32_MAX} between calls while err_clean is set
+  // (no per-call re-initialisation); whatever else writes err clears err_clean.  The flags come
+  // back through the pinned err_host (a DMA, not a staged pageable copy).
+  int32_t* err_host = nullptr;      // [2], pinned host memory
+  bool err_clean = false;
   int32_t max_rowlen = 0;
 
   // colour-ordered direct assembly (hex27 on a verified lattice, FCG_PATH_COLORED)

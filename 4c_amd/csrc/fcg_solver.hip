@@ -377,6 +377,7 @@ int fcg_dirichlet_apply(fcg_ctx* ctx, int64_t n_dbc, const int32_t* d_rows, doub
   (void)hipSetDevice(ctx->device);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   const int32_t zero = 0;
+  m.err_clean = false;  // err[0] becomes this call's flag
   hipError_t he = hipMemcpyAsync(m.err, &zero, sizeof(zero), hipMemcpyHostToDevice, s);
   if (he == hipSuccess)
   {
@@ -451,6 +452,7 @@ int fcg_pcg_solve(fcg_ctx* ctx, const double* d_K_vals, const double* d_b_row, d
   double* pc = pb + nb;
   double* sc = pc + nb;
   const int32_t zero = 0;
+  m.err_clean = false;  // err[0] becomes this call's flag
   he = hipMemcpyAsync(m.err, &zero, sizeof(zero), hipMemcpyHostToDevice, s);
   if (he == hipSuccess)
   {

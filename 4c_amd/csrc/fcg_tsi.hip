@@ -916,6 +916,7 @@ int fcg_tsi_evaluate_fused(fcg_ctx* sctx, fcg_tsi_ctx* ctx, int mode, const doub
     d.fused_with = sctx;
   }
   const int32_t init[2] = {0, INT32_MAX};
+  sctx->mesh.err_clean = false;  // the fused sweep reports through the structural context's flags
   he = hipMemcpyAsync(m.err, init, sizeof(init), hipMemcpyHostToDevice, s);
   if (he == hipSuccess)
   {
