@@ -7,12 +7,15 @@ Mirrors the static step of 4C's structure_new time integrator with a NOX full Ne
   Dirichlet on r (reaction forces kept) and K                       fcg_dirichlet_apply,
                                                                     4C_structure_new_dbc.cpp:221-262
   convergence: |r|_2 <= tol_res and |du|_2 <= tol_inc (NOX normF / normUpdate tests, combined "And")
-  K du = -r                                                         fcg_pcg_solve (block-Jacobi PCG)
+  K du = -r                                                         fcg_pcg_solve (block-Jacobi PCG),
+                                                                    relative tolerance from ForcingTerm
   u += du
 Homogeneous Dirichlet conditions (the increments of the constrained DOFs are zero); single rank
 (the PCG needs the matrix column map to be the row map).  u, f, K, f_ext and the work vectors stay
 in HBM; torch only supplies the device buffers and the vector updates.
 """
+
+import math
 
 import numpy as np
 import torch
@@ -20,9 +23,59 @@ import torch
 from . import fcg
 
 
+class ForcingTerm:
+    """Relative tolerance of each Newton step's linear solve: the "STRUCT NOX/Direction/Newton"
+    forcing-term parameters of 4C (4C_inpar_solver_nonlin.cpp:48-71: "Forcing Term Method"
+    Constant | Type 1 | Type 2, initial 0.1, minimum 1e-6, maximum 0.01, alpha 1.5, gamma 0.9),
+    which 4C hands to Trilinos NOX (sha 06db4c85, not vendored).  NOX's
+    Direction::Utils::InexactNewton::computeForcingTerm is the Eisenstat-Walker choice
+    (SIAM J. Sci. Comput. 17, 1996), restated here:
+      Constant: eta = the linear solver's own tolerance, every step;
+      step 0:   eta = initial (no clamp);
+      Type 1:   eta = |‖F_k‖ - ‖F_{k-1} + J_{k-1} d_{k-1}‖| / ‖F_{k-1}‖,
+                raised to eta_{k-1}^((1+√5)/2) when that exceeds 0.1;
+      Type 2:   eta = gamma (‖F_k‖ / ‖F_{k-1}‖)^alpha, raised to gamma eta_{k-1}^alpha when that
+                exceeds 0.1;
+    then (Types 1, 2) clamped to [minimum, maximum].  Parity: unpinned (no reference test uses
+    Types 1/2); the converged displacement does not depend on eta (the Newton tests on |r| and
+    |du| decide), which tests/test_newton_gpu.py checks against the Constant method."""
+
+    METHODS = ("Constant", "Type 1", "Type 2")
+
+    def __init__(self, method="Constant", constant=1e-13, initial=0.1, minimum=1e-6,
+                 maximum=0.01, alpha=1.5, gamma=0.9):
+        if method not in self.METHODS:
+            raise ValueError(f"Forcing Term Method must be one of {self.METHODS}, not {method!r}")
+        self.method, self.constant = method, constant
+        self.initial, self.minimum, self.maximum = initial, minimum, maximum
+        self.alpha, self.gamma = alpha, gamma
+        self.eta = None
+
+    def compute(self, niter, normf, normoldf=None, normpredf=None):
+        """eta for the linear solve of Newton step `niter`: normf = ‖F_k‖, normoldf = ‖F_{k-1}‖,
+        normpredf = ‖F_{k-1} + J_{k-1} d_{k-1}‖ (the previous linear residual; Type 1 only)."""
+        if self.method == "Constant":
+            self.eta = self.constant
+        elif niter == 0:
+            self.eta = self.initial
+        else:
+            eta_km1 = self.eta
+            if self.method == "Type 1":
+                eta = abs(normf - normpredf) / normoldf
+                safe = eta_km1 ** ((1.0 + math.sqrt(5.0)) / 2.0)
+            else:
+                eta = self.gamma * (normf / normoldf) ** self.alpha
+                safe = self.gamma * eta_km1 ** self.alpha
+            if safe > 0.1:
+                eta = max(eta, safe)
+            self.eta = min(max(eta, self.minimum), self.maximum)
+        return self.eta
+
+
 class StaticNewton:
     def __init__(self, evaluator, fext_row, dbc_rows, tol_res=1e-10, tol_inc=1e-10, max_iter=20,
-                 lin_rtol=1e-13, lin_max_iter=100000):
+                 lin_rtol=1e-13, lin_max_iter=100000, forcing=None):
+        """forcing: ForcingTerm (None: Constant at lin_rtol)."""
         info = evaluator.info
         self.ev = evaluator
         self.dev = torch.device("cuda", evaluator.device)
@@ -40,6 +93,7 @@ class StaticNewton:
         self.freact = torch.zeros(self.n, **f64)
         self.tol_res, self.tol_inc, self.max_iter = tol_res, tol_inc, max_iter
         self.lin_rtol, self.lin_max_iter = lin_rtol, lin_max_iter
+        self.forcing = forcing if forcing is not None else ForcingTerm("Constant", constant=lin_rtol)
         self.history = []
 
     def solve(self, u0=None):
@@ -48,6 +102,7 @@ class StaticNewton:
              else torch.as_tensor(u0, dtype=torch.float64).to(self.dev).clone())
         self.history = []
         ndu = float("inf")
+        nr_old = lin_abs = None
         for it in range(self.max_iter + 1):
             self.ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u, self.fint, self.K)
             torch.sub(self.fint, self.fext, out=self.r)
@@ -58,9 +113,10 @@ class StaticNewton:
                 self.history.append(rec)
                 return u
             torch.neg(self.r, out=self.r)
-            lin_it, lin_res = self.ev.pcg_solve(self.K, self.r, self.du, self.lin_rtol,
-                                                self.lin_max_iter)
-            rec.update(lin_iter=lin_it, lin_relres=lin_res)
+            eta = self.forcing.compute(it, nr, nr_old, lin_abs)
+            lin_it, lin_res = self.ev.pcg_solve(self.K, self.r, self.du, eta, self.lin_max_iter)
+            nr_old, lin_abs = nr, lin_res * nr  # ‖F_k + J_k d_k‖ (full step, no line search)
+            rec.update(lin_iter=lin_it, lin_relres=lin_res, eta=eta)
             self.history.append(rec)
             ndu = float(torch.linalg.vector_norm(self.du))
             u += self.du

@@ -126,6 +126,26 @@ def test_totlag_newton_structured():
     assert rel_err(u, ref) <= 1e-8, (rel_err(u, ref), nt.history)
 
 
+@pytest.mark.parametrize("method", ["Type 1", "Type 2"])
+def test_inexact_newton_forcing_term_same_solution(method):
+    """NOX forcing terms (newton.ForcingTerm): looser early linear solves, same converged u."""
+    _dev()
+    mesh, dbc, fext = _cantilever(iv=(6, 3, 3), upper=(6.0, 1.0, 1.0))
+    fext *= 2e3
+    ev = fcg.Evaluator(mesh, kinematics=fcg.TOTLAG, youngs=E, poisson=NU)
+    exact = newton.StaticNewton(ev, fext, dbc, tol_res=1e-10, tol_inc=1e-10, lin_rtol=1e-14)
+    u_ref = exact.solve().cpu().numpy()
+    nt = newton.StaticNewton(ev, fext, dbc, tol_res=1e-10, tol_inc=1e-10, max_iter=40,
+                             forcing=newton.ForcingTerm(method))
+    u = nt.solve().cpu().numpy()
+    assert rel_err(u, u_ref) <= 1e-9, (rel_err(u, u_ref), nt.history)
+    etas = [h["eta"] for h in nt.history if "eta" in h]
+    assert etas[0] == 0.1 and all(1e-6 <= e <= 0.01 for e in etas[1:]), etas
+    lin = sum(h["lin_iter"] for h in nt.history if "lin_iter" in h)
+    lin_exact = sum(h["lin_iter"] for h in exact.history if "lin_iter" in h)
+    assert lin < lin_exact, (lin, lin_exact)
+
+
 def test_spmv_dirichlet_pcg_against_scipy():
     dev = _dev()
     mesh = fcg.BoxMesh(fcg.HEX8, (8, 6, 5), jitter=0.1)

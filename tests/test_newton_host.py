@@ -40,3 +40,29 @@ def test_fixture_csr_covers_element_couplings(name):
     for r in range(dis.n_rows):
         c = dis.col_lid[dis.rowptr[r]:dis.rowptr[r + 1]]
         assert np.all(np.diff(c) > 0)
+
+
+def test_forcing_term_sequence():
+    """newton.ForcingTerm against hand-evaluated Eisenstat-Walker steps (NOX InexactNewton)."""
+    import importlib
+    import math
+    newton = importlib.import_module("4c_amd.newton")
+    ft = newton.ForcingTerm("Constant", constant=1e-8)
+    assert ft.compute(0, 1.0) == 1e-8 and ft.compute(3, 1e-3, 1e-2, 1e-4) == 1e-8
+    t2 = newton.ForcingTerm("Type 2")
+    assert t2.compute(0, 1.0) == 0.1                            # initial, unclamped
+    # 0.9 (0.5)^1.5 = 0.318; safeguard 0.9 * 0.1^1.5 = 0.028 < 0.1; clamp to max 0.01
+    assert t2.compute(1, 0.5, 1.0) == 0.01
+    # 0.9 (1e-3)^1.5 = 2.85e-5; safeguard 0.9 * 0.01^1.5 = 9e-4 < 0.1 -> 2.85e-5
+    assert math.isclose(t2.compute(2, 1e-3, 1.0), 0.9 * 1e-3 ** 1.5, rel_tol=1e-15)
+    assert t2.compute(3, 1e-9, 1.0) == 1e-6                     # clamp to min
+    big = newton.ForcingTerm("Type 2", maximum=0.9)
+    big.compute(0, 1.0)
+    big.eta = 0.8                                               # safeguard 0.9 * 0.8^1.5 = 0.644 > 0.1
+    assert math.isclose(big.compute(1, 1e-4, 1.0), 0.9 * 0.8 ** 1.5, rel_tol=1e-15)
+    t1 = newton.ForcingTerm("Type 1")
+    assert t1.compute(0, 2.0) == 0.1
+    # |0.5 - 0.498| / 2 = 1e-3; safeguard 0.1^1.618 = 0.024 < 0.1
+    assert math.isclose(t1.compute(1, 0.5, 2.0, 0.498), 1e-3, rel_tol=1e-12)
+    with pytest.raises(ValueError):
+        newton.ForcingTerm("Type 3")

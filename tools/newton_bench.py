@@ -28,6 +28,8 @@ ap.add_argument("--lin-rtol", type=float, default=1e-10)
 ap.add_argument("--tol", type=float, default=1e-8)
 ap.add_argument("--path", default="auto", choices=["auto", "general", "structured"])
 ap.add_argument("--lin-max-iter", type=int, default=100000)
+ap.add_argument("--forcing", default="Constant", choices=["Constant", "Type 1", "Type 2"],
+                help="NOX forcing-term method (Constant = --lin-rtol every step)")
 a = ap.parse_args()
 ct = fcg.HEX8 if a.celltype == "hex8" else fcg.HEX27
 kin = fcg.LINEAR if a.kinem == "linear" else fcg.TOTLAG
@@ -52,6 +54,7 @@ class Timed(newton.StaticNewton):
     def solve(self):
         u = torch.zeros(self.n, dtype=torch.float64, device=self.dev)
         self.history, ndu = [], float("inf")
+        nr_old = lin_abs = None
         for it in range(self.max_iter + 1):
             torch.cuda.synchronize()
             t_a = time.perf_counter()
@@ -75,7 +78,9 @@ class Timed(newton.StaticNewton):
                                                         flush=True) for _ in iter(lambda: done.wait(30), True)])
             hb.start()
             try:
-                li, lr = self.ev.pcg_solve(self.K, self.r, self.du, self.lin_rtol, self.lin_max_iter)
+                eta = self.forcing.compute(it, nr, nr_old, lin_abs)
+                li, lr = self.ev.pcg_solve(self.K, self.r, self.du, eta, self.lin_max_iter)
+                nr_old, lin_abs = nr, lr * nr
             finally:
                 done.set()
                 hb.join()
@@ -83,7 +88,7 @@ class Timed(newton.StaticNewton):
             t_d = time.perf_counter()
             ndu = float(torch.linalg.vector_norm(self.du))
             u += self.du
-            rec.update(solve_ms=1e3 * (t_d - t_c), pcg_iter=li, pcg_relres=lr, norm_inc=ndu)
+            rec.update(solve_ms=1e3 * (t_d - t_c), pcg_iter=li, pcg_relres=lr, eta=eta, norm_inc=ndu)
             self.history.append(rec)
             print(json.dumps(rec), file=sys.stderr, flush=True)
         return u
@@ -91,13 +96,14 @@ class Timed(newton.StaticNewton):
 
 print(f"setup {t_setup:.1f} s", file=sys.stderr, flush=True)
 nt = Timed(ev, fext, dbc, lin_max_iter=a.lin_max_iter, tol_res=a.tol * max(np.linalg.norm(fext), 1e-300), tol_inc=a.tol,
-           lin_rtol=a.lin_rtol)
+           lin_rtol=a.lin_rtol, max_iter=40,
+           forcing=newton.ForcingTerm(a.forcing, constant=a.lin_rtol))
 t1 = time.perf_counter()
 u = nt.solve()
 torch.cuda.synchronize()
 t_newton = time.perf_counter() - t1
 h = nt.history
-out = {"config": f"{a.celltype}-{a.kinem}-{a.n}^3-cantilever", "elements": mesh.n_ele,
+out = {"config": f"{a.celltype}-{a.kinem}-{a.n}^3-cantilever", "forcing": a.forcing, "elements": mesh.n_ele,
        "dofs": mesh.n_rows, "nnz": mesh.nnz, "setup_s": t_setup, "newton_s": t_newton,
        "newton_iterations": len(h) - 1,
        "assembly_ms_mean": float(np.mean([r["assembly_ms"] for r in h])),
