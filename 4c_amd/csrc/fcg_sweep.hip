@@ -479,17 +479,26 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
     nxy_in[j] = n_lane[j] && ni >= A.EX0 && ni <= A.EX0 + A.EX && nj >= A.EY0 && nj <= A.EY0 + A.EY;
     nlat_xy[j] = nxy_in[j] ? int64_t(nj - A.EY0) * LX + (ni - A.EX0) : 0;
   }
-  auto load_node = [&](int j, int P) -> double {
-    if (!nxy_in[j] || P < A.EZ0 || P > A.EZ0 + A.EZ) return 0.0;
-    const int64_t li = int64_t(P - A.EZ0) * LX * LY + nlat_xy[j];
+  // node loads in two steps, so that no load waits on another inside a layer: the DOF of a plane
+  // is fetched one layer before its values (load_dof), the values (load_val) are issued before
+  // stage A and consumed after it -- the wait for them then also covers the previous layer's K
+  // stores (gfx9 counts stores in vmcnt), which stage A has had time to retire.
+  auto node_li = [&](int j, int P) -> int64_t { return int64_t(P - A.EZ0) * LX * LY + nlat_xy[j]; };
+  auto node_in = [&](int j, int P) -> bool { return nxy_in[j] && P >= A.EZ0 && P <= A.EZ0 + A.EZ; };
+  auto load_dof = [&](int j, int P) -> int32_t {
+    if (!node_in(j, P) || ncomp[j] < 3) return -1;
+    return A.lat_dof[node_li(j, P)];
+  };
+  auto load_val = [&](int j, int P, int32_t dof) -> double {
+    if (!node_in(j, P)) return 0.0;
     const int cp = ncomp[j];
-    if (cp < 3) return A.lat_x[3 * li + cp];
-    const int dof = A.lat_dof[li];
+    if (cp < 3) return A.lat_x[3 * node_li(j, P) + cp];
     if (dof < 0) return 0.0;
     if (!TSI || cp < 6) return A.u_col[dof + cp - 3];
     if (cp < 9) return A.v_col[dof + cp - 6];
     return A.T_col[dof / 3];
   };
+  auto load_node = [&](int j, int P) -> double { return load_val(j, P, load_dof(j, P)); };
   auto load_rec = [&](int p, uint32_t* w) {
     const bool in = p >= kz0 && p < kz1;
     const uint32_t* src = prec_tile + int64_t(in ? p - A.K0 : 0) * PLANE_REC_WORDS;
@@ -529,33 +538,45 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
     load_rec(kz0, w);
     store_rec(kz0, w);
   }
-  double node_nxt[NLD];
+  int32_t dof_nxt[NLD];  // DOF of plane L+2's node-load items at the top of layer L
 #pragma unroll
-  for (int j = 0; j < NLD; ++j) node_nxt[j] = n_lane[j] ? load_node(j, kz0 + 1) : 0.0;
-  uint32_t rec_nxt[2];
-  load_rec(kz0 + 1, rec_nxt);
+  for (int j = 0; j < NLD; ++j) dof_nxt[j] = n_lane[j] ? load_dof(j, kz0 + 1) : -1;
   int e_cur = load_elem(kz0 - 1);
   for (int v = tid; v < int(sizeof(sh.hold) / sizeof(double)); v += 256) (&sh.hold[0][0][0])[v] = 0.0;
   double fkeep[NF];  // lane k = 8: D-side residual part of plane L+1's rows
 #pragma unroll
   for (int d = 0; d < NF; ++d) fkeep[d] = 0.0;
+  // the prologue's loads land here, so that the compiler's wait bookkeeping does not carry them
+  // into the loop (where the first use of e_cur would otherwise wait for every load in flight)
+  __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
 
   for (int L = kz0 - 1; L < kz1; ++L)
   {
+    // issue the loads of plane L+2 (values, record), plane L+3's DOFs and layer L+1's element
     const int e_nxt = load_elem(L + 1);
+    double node_nxt[NLD];
+    int32_t dof_nn[NLD];
+#pragma unroll
+    for (int j = 0; j < NLD; ++j)
+    {
+      node_nxt[j] = n_lane[j] ? load_val(j, L + 2, dof_nxt[j]) : 0.0;
+      dof_nn[j] = n_lane[j] ? load_dof(j, L + 3) : -1;
+    }
+    uint32_t rec_nxt[2];
+    load_rec(L + 2, rec_nxt);
     // A. element stage
     if (a_lane) sweep_stage_a<KIN, TSI>(sh, A, s, g, sx, sy, L, e_cur);
     __syncthreads();
     FCG_STAMP(0);
-    // commit plane L+2 (nodes and record into plane L-1's ring slot), then prefetch plane L+3
+    // commit plane L+2 (nodes and record into plane L-1's ring slot)
 #pragma unroll
     for (int j = 0; j < NLD; ++j)
+    {
       if (n_lane[j]) sh.node[ring(L + 2)][ncol[j]][ncomp[j]] = node_nxt[j];
+      dof_nxt[j] = dof_nn[j];
+    }
     store_rec(L + 2, rec_nxt);
-#pragma unroll
-    for (int j = 0; j < NLD; ++j) node_nxt[j] = n_lane[j] ? load_node(j, L + 3) : 0.0;
-    load_rec(L + 3, rec_nxt);
 
     // B. visit stage
     const bool wl = L >= kz0, wl1 = L + 1 < kz1;
