@@ -670,7 +670,7 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
   fcg_ctx* ctx = new fcg_ctx();
   ctx->device = d->device;
   hipError_t he = hipSetDevice(d->device);
-  if (he == hipSuccess) he = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  if (he == hipSuccess) he = hipStreamCreateWithFlags(&ctx->stream, hipStreamDefault);  // ordered with the null stream (torch's default)
   if (he != hipSuccess)
   {
     set_create_error(std::string("HIP: ") + hipGetErrorString(he));

@@ -302,6 +302,55 @@ __global__ __launch_bounds__(kBlock) void dirichlet_kernel(const int64_t* __rest
   }
 }
 
+// z = scale D^-1 r (+ z if accumulate) per owned node: the smoother step of the multigrid
+// preconditioner (4c_amd/multigrid.py)
+__global__ __launch_bounds__(kBlock) void bj_apply_kernel(const int32_t* __restrict__ row0_of,
+    const double* __restrict__ dinv, const double* __restrict__ r, double* z, int64_t n_nodes,
+    double scale, int accumulate)
+{
+  const int64_t k = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (k >= n_nodes) return;
+  const int32_t i = row0_of[k];
+  double ri[3], zi[3];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) ri[d] = r[i + d];
+  bj_apply(dinv + 9 * k, ri, zi);
+#pragma unroll
+  for (int d = 0; d < 3; ++d) z[i + d] = (accumulate ? z[i + d] : 0.0) + scale * zi[d];
+}
+
+// Node-block transfer between two discretizations of one box (multigrid prolongation and its
+// transpose): y[dst_row0[o] + d] = (accumulate ? y : 0) + sum_j w[j] x[src_row0[j] + d] over
+// j in [ptr[o], ptr[o+1]), d = 0..2.  Fixed summation order: deterministic.
+__global__ __launch_bounds__(kBlock) void node_transfer_kernel(const int64_t* __restrict__ ptr,
+    const int32_t* __restrict__ src_row0, const double* __restrict__ w,
+    const int32_t* __restrict__ dst_row0, const double* __restrict__ x, double* y, int64_t n_out,
+    int accumulate)
+{
+  const int64_t o = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (o >= n_out) return;
+  const int32_t dr = dst_row0[o];
+  if (dr < 0) return;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+  for (int64_t j = ptr[o]; j < ptr[o + 1]; ++j)
+  {
+    const int32_t sr = src_row0[j];
+    const double wj = w[j];
+    a0 += wj * x[sr];
+    a1 += wj * x[sr + 1];
+    a2 += wj * x[sr + 2];
+  }
+  if (accumulate)
+  {
+    a0 += y[dr];
+    a1 += y[dr + 1];
+    a2 += y[dr + 2];
+  }
+  y[dr] = a0;
+  y[dr + 1] = a1;
+  y[dr + 2] = a2;
+}
+
 inline unsigned blocks_for(int64_t n, int per_block) { return unsigned((n + per_block - 1) / per_block); }
 // grid-stride kernels with dot partials: at most this many blocks (16 per CU of a 256-CU part),
 // so the single-block reductions of the partials stay short
@@ -518,6 +567,77 @@ int fcg_pcg_solve(fcg_ctx* ctx, const double* d_K_vals, const double* d_b_row, d
   if (iterations) *iterations = it;
   if (rel_residual) *rel_residual = std::sqrt(rr / rr0);
   return FCG_OK;
+}
+
+int fcg_block_jacobi_setup(fcg_ctx* ctx, const double* d_K_vals, double* d_dinv, void* stream)
+{
+  if (!ctx || !d_K_vals || !d_dinv) return FCG_ERR_ARG;
+  fcg::DeviceMesh& m = ctx->mesh;
+  const int64_t nn = m.n_rownodes;
+  if (3 * nn != m.n_rows)
+  {
+    ctx->last_error = "fcg_block_jacobi_setup: every owned row must belong to an owned node's DOF triple";
+    return FCG_ERR_ARG;
+  }
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  const int32_t zero = 0;
+  int32_t bad = 0;
+  m.err_clean = false;
+  hipError_t he = hipMemcpyAsync(m.err, &zero, sizeof(zero), hipMemcpyHostToDevice, s);
+  if (he == hipSuccess && nn > 0)
+  {
+    hipLaunchKernelGGL(fcg::block_jacobi_kernel, dim3(fcg::blocks_for(nn, fcg::kBlock)), dim3(fcg::kBlock), 0, s,
+        m.rownode_row0, m.diag_pos, d_K_vals, d_dinv, nn, m.err);
+    he = hipGetLastError();
+  }
+  if (he == hipSuccess) he = hipMemcpyAsync(&bad, m.err, sizeof(bad), hipMemcpyDeviceToHost, s);
+  if (he == hipSuccess) he = hipStreamSynchronize(s);
+  if (he != hipSuccess)
+  {
+    ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
+    return FCG_ERR_DEVICE;
+  }
+  if (bad)
+  {
+    ctx->last_error = "singular or missing diagonal node block (block-Jacobi preconditioner)";
+    return FCG_ERR_SINGULAR;
+  }
+  return FCG_OK;
+}
+
+int fcg_block_jacobi_apply(fcg_ctx* ctx, const double* d_dinv, const double* d_r_row, double* d_z_row,
+    double scale, int accumulate, void* stream)
+{
+  if (!ctx || !d_dinv || !d_r_row || !d_z_row) return FCG_ERR_ARG;
+  fcg::DeviceMesh& m = ctx->mesh;
+  const int64_t nn = m.n_rownodes;
+  if (nn == 0) return FCG_OK;
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  hipLaunchKernelGGL(fcg::bj_apply_kernel, dim3(fcg::blocks_for(nn, fcg::kBlock)), dim3(fcg::kBlock), 0, s,
+      m.rownode_row0, d_dinv, d_r_row, d_z_row, nn, scale, accumulate);
+  const hipError_t he = hipGetLastError();
+  if (he != hipSuccess)
+  {
+    ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
+    return FCG_ERR_DEVICE;
+  }
+  return FCG_OK;
+}
+
+int fcg_node_transfer(int device, int64_t n_out, const int64_t* d_ptr, const int32_t* d_src_row0,
+    const double* d_w, const int32_t* d_dst_row0, const double* d_x, double* d_y, int accumulate,
+    void* stream)
+{
+  if (n_out < 0 || (n_out > 0 && (!d_ptr || !d_src_row0 || !d_w || !d_dst_row0 || !d_x || !d_y)))
+    return FCG_ERR_ARG;
+  if (n_out == 0) return FCG_OK;
+  if (hipSetDevice(device) != hipSuccess) return FCG_ERR_DEVICE;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(fcg::node_transfer_kernel, dim3(fcg::blocks_for(n_out, fcg::kBlock)), dim3(fcg::kBlock), 0, s,
+      d_ptr, d_src_row0, d_w, d_dst_row0, d_x, d_y, n_out, accumulate);
+  return hipGetLastError() == hipSuccess ? FCG_OK : FCG_ERR_DEVICE;
 }
 
 }  // extern "C"

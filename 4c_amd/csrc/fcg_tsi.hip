@@ -671,7 +671,7 @@ int fcg_tsi_create(const fcg_tsi_desc* D, fcg_tsi_ctx** out)
   auto* ctx = new fcg_tsi_ctx();
   ctx->device = D->device;
   hipError_t he = hipSetDevice(D->device);
-  if (he == hipSuccess) he = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  if (he == hipSuccess) he = hipStreamCreateWithFlags(&ctx->stream, hipStreamDefault);  // ordered with the null stream (torch's default)
   if (he != hipSuccess)
   {
     set_tsi_create_error(std::string("HIP: ") + hipGetErrorString(he));

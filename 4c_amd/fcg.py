@@ -12,9 +12,10 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "lib", "libfourc_gpu.so")
-# diagnostics only: FCG_LIB=diag loads the phase-stamp build (make -C 4c_amd diag)
-if os.environ.get("FCG_LIB") == "diag":
-    LIB_PATH = os.path.join(PKG_DIR, "lib", "libfourc_gpu_diag.so")
+# diagnostics / A-B timing only: FCG_LIB=<name> loads lib/libfourc_gpu_<name>.so instead
+# (diag = the phase-stamp build, make -C 4c_amd diag)
+if os.environ.get("FCG_LIB"):
+    LIB_PATH = os.path.join(PKG_DIR, "lib", "libfourc_gpu_%s.so" % os.environ["FCG_LIB"])
 
 HEX8, HEX27 = 0, 1
 LINEAR, TOTLAG = 0, 1
@@ -136,6 +137,10 @@ def lib():
     L.fcg_dirichlet_apply.argtypes = [vp, ctypes.c_int64, vp, vp, vp, vp, vp]
     L.fcg_pcg_solve.argtypes = [vp, vp, vp, vp, ctypes.c_double, ctypes.c_int,
                                 ctypes.POINTER(ctypes.c_int), _dp, vp]
+    L.fcg_block_jacobi_setup.argtypes = [vp, vp, vp, vp]
+    L.fcg_block_jacobi_apply.argtypes = [vp, vp, vp, vp, ctypes.c_double, ctypes.c_int, vp]
+    L.fcg_node_transfer.argtypes = [ctypes.c_int, ctypes.c_int64, vp, vp, vp, vp, vp, vp,
+                                    ctypes.c_int, vp]
     neu = [ctypes.c_int, ctypes.c_int64, _i32p, _dp, _i32p, _i32p, _dp, _i32p, FUNCT_FN,
            ctypes.c_void_p, ctypes.c_double, _dp]
     L.fcg_neumann_surface.argtypes = neu
@@ -161,6 +166,16 @@ def lib():
                                          ctypes.c_double, vp, vp, vp, vp, vp, vp, vp, _i32p]
     _lib = L
     return L
+
+
+def _torch_stream(stream):
+    """The HIP stream of a library call on torch tensors: the given torch stream, else torch's
+    current stream -- never the context's own (non-blocking) stream, which is not ordered with
+    the torch work that produced or consumes the buffers."""
+    import torch
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return ctypes.c_void_p(stream.cuda_stream)
 
 
 def _np_ptr(a, t):
@@ -467,7 +482,7 @@ class Evaluator:
     def evaluate_device(self, action, mode, u_col, fint_row, K_vals=None, stream=None):
         """Device-resident path; tensors are float64 torch tensors on this device."""
         bad = ctypes.c_int32(-1)
-        s = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
+        s = _torch_stream(stream)
         rc = lib().fcg_evaluate_device(self._h, action, mode, _tensor_ptr(u_col),
                                        _tensor_ptr(fint_row), _tensor_ptr(K_vals), s,
                                        ctypes.byref(bad))
@@ -475,7 +490,7 @@ class Evaluator:
             self._raise(rc, bad.value)
 
     def _stream(self, stream):
-        return ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
+        return _torch_stream(stream)
 
     def spmv(self, K_vals, x_col, y_row, stream=None):
         rc = lib().fcg_spmv(self._h, _tensor_ptr(K_vals), _tensor_ptr(x_col), _tensor_ptr(y_row),
@@ -600,7 +615,7 @@ class TsiEvaluator:
                         Kst=None, fT=None, Ktt=None, Kts=None, stream=None):
         """Tensors: float64 on this device (v_col / T_col in the structural / thermo column maps)."""
         bad = ctypes.c_int32(-1)
-        s = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
+        s = _torch_stream(stream)
         rc = lib().fcg_tsi_evaluate_device(self._h, parts, mode, _tensor_ptr(v_col),
                                            _tensor_ptr(T_col), float(timefac), float(timefac_d),
                                            _tensor_ptr(fs), _tensor_ptr(Kst), _tensor_ptr(fT),
@@ -613,7 +628,7 @@ class TsiEvaluator:
         """fcg_tsi_evaluate_fused: the whole monolithic tangent (K_SS, k_ST, k_TS, k_TT) and both
         residuals in one sweep; `struct_ev` is the structured linear StVK Evaluator of the mesh."""
         bad = ctypes.c_int32(-1)
-        s = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
+        s = _torch_stream(stream)
         rc = lib().fcg_tsi_evaluate_fused(struct_ev._h, self._h, mode, _tensor_ptr(u_col),
                                           _tensor_ptr(v_col), _tensor_ptr(T_col), float(timefac),
                                           float(timefac_d), _tensor_ptr(fs), _tensor_ptr(Kss),
@@ -631,7 +646,7 @@ def graph_build_device(celltype, ele_nodes, node_dof_col, node_dof_row, n_rows, 
     dev = torch.device("cuda", device)
     rowptr = torch.empty(int(n_rows) + 1, dtype=torch.int64, device=dev)
     nnz = ctypes.c_int64(0)
-    s = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
+    s = _torch_stream(stream)
     args = (device, celltype, int(ele_nodes.numel() // (8 if celltype == HEX8 else 27)),
             _tensor_ptr(ele_nodes), int(node_dof_col.numel()), _tensor_ptr(node_dof_col),
             _tensor_ptr(node_dof_row), int(n_rows), _tensor_ptr(rowptr))

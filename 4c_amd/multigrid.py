@@ -1,0 +1,344 @@
+"""Geometric multigrid preconditioner for the Newton solve on GridGenerator boxes (SURVEY §8f
+row 2: "GPU CG with a Jacobi/AMG preconditioner").
+
+4C hands the linearised system to Belos with a MueLu (smoothed-aggregation AMG) preconditioner
+(4C_solver_nonlin_nox_linearsystem.cpp:275-353, 4C_linear_solver_preconditioner_muelu.cpp).
+MueLu is not vendored and builds its hierarchy from the matrix graph; on the structured boxes of
+the BASELINE configs the hierarchy is known in advance, so it is built geometrically instead:
+
+  level 0   the tangent K being solved (hex27 or hex8, any kinematics, Dirichlet unit rows)
+  level 1   hex27 -> hex8 on the same elements (p-coarsening), if level 0 is hex27
+  level l+1 hex8 n -> hex8 n/2 (h-coarsening) while n stays even and >= min_intervals
+
+Coarse operators are rediscretised: linear-elastic StVK hex8 assembled by the library's own
+evaluate (for affine boxes and linear kinematics this is exactly the Galerkin product P^T K P,
+the quadrature being exact for the trilinear subspace).  Transfers are the nodal interpolation of
+a trilinear field (weights 1 or 1/2 per direction) and its transpose, applied by
+fcg_node_transfer.  Smoother: Chebyshev polynomial in D^-1 K with D the 3x3 nodal diagonal blocks
+(Ifpack2's Chebyshev with point-block diagonal; eigenvalue ratio and boost as Ifpack2's defaults),
+the same polynomial before and after the coarse correction.  Coarsest level: block-Jacobi PCG to a
+loose tolerance -- a nonlinear preconditioner, so the outer iteration is flexible CG
+(Polak-Ribiere beta).  Every level's K, the work vectors and the transfer tables stay in HBM;
+torch supplies the buffers and the vector updates (axpy, dot), the library the operator, the
+smoother's block-diagonal solve and the transfers.
+"""
+
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+from . import fcg
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def node_lattice(mesh):
+    """(i, j, k) of every node on the mesh's own node lattice (GridGenerator node GIDs,
+    4C_io_gridgenerator.cpp:283-291: gid = (ez NY + ey) NX + ex on the 2n+1 lattice; hex8 nodes
+    sit at its even points)."""
+    iv = [int(mesh.box.interval[d]) for d in range(3)]
+    NX, NY = 2 * iv[0] + 1, 2 * iv[1] + 1
+    g = mesh.node_gid - int(mesh.box.first_node_gid)
+    ijk = np.stack([g % NX, (g // NX) % NY, g // (NX * NY)], axis=1)
+    if mesh.celltype == fcg.HEX8:
+        ijk //= 2
+    return ijk
+
+
+def transfer_tables(fine, coarse):
+    """Prolongation fine <- coarse (trilinear nodal interpolation) and its transpose, as
+    node-block tables for fcg_node_transfer: (ptr, src_row0, w, dst_row0) each."""
+    fl, cl = node_lattice(fine), node_lattice(coarse)
+    cdim = cl.max(axis=0) + 1
+    if not np.array_equal(fl.max(axis=0), 2 * (cdim - 1)):
+        raise ValueError("fine lattice is not the 2:1 refinement of the coarse one")
+    crow = np.full(tuple(cdim), -1, dtype=np.int64)
+    crow[cl[:, 0], cl[:, 1], cl[:, 2]] = coarse.node_dof_row
+    nf = len(fl)
+    lo, hi, wl, wh = [], [], [], []
+    for d in range(3):
+        f = fl[:, d]
+        odd = (f & 1).astype(bool)
+        lo.append(f // 2)
+        hi.append(np.where(odd, f // 2 + 1, f // 2))
+        wl.append(np.where(odd, 0.5, 1.0))
+        wh.append(np.where(odd, 0.5, 0.0))
+    fidx, cidx, w = [], [], []
+    for cx in range(2):
+        for cy in range(2):
+            for cz in range(2):
+                wx = wh[0] if cx else wl[0]
+                wy = wh[1] if cy else wl[1]
+                wz = wh[2] if cz else wl[2]
+                ww = wx * wy * wz
+                m = ww > 0
+                ix = (hi[0] if cx else lo[0])[m]
+                iy = (hi[1] if cy else lo[1])[m]
+                iz = (hi[2] if cz else lo[2])[m]
+                fidx.append(np.nonzero(m)[0])
+                cidx.append(crow[ix, iy, iz])
+                w.append(ww[m])
+    fidx, cidx, w = np.concatenate(fidx), np.concatenate(cidx), np.concatenate(w)
+    if (cidx < 0).any():
+        raise ValueError("coarse node missing from the coarse mesh")
+    frow = fine.node_dof_row.astype(np.int64)
+
+    def table(out_idx, out_row, src_row, n_out):
+        order = np.lexsort((src_row, out_idx))
+        ptr = np.zeros(n_out + 1, dtype=np.int64)
+        np.add.at(ptr, out_idx + 1, 1)
+        return (np.cumsum(ptr), src_row[order].astype(np.int32), w[order].copy(),
+                out_row.astype(np.int32))
+
+    # prolongation: out = fine nodes, sources = coarse rows
+    P = table(fidx, frow, cidx, nf)
+    # restriction (transpose): out = coarse nodes (numbered by the coarse mesh's node index)
+    cl_of_entry = np.empty(len(cidx), dtype=np.int64)
+    # coarse node index of every entry: invert crow (row0 -> node) through a dense map
+    row2node = np.full(int(coarse.node_dof_row.max()) + 1, -1, dtype=np.int64)
+    row2node[coarse.node_dof_row] = np.arange(len(cl))
+    cl_of_entry[:] = row2node[cidx]
+    R = table(cl_of_entry, coarse.node_dof_row.astype(np.int64), frow[fidx], len(cl))
+    return P, R
+
+
+class _Transfer:
+    def __init__(self, tab, device):
+        ptr, src, w, dst = tab
+        self.n_out = len(dst)
+        self.ptr = torch.from_numpy(ptr).to(device)
+        self.src = torch.from_numpy(src).to(device)
+        self.w = torch.from_numpy(w).to(device)
+        self.dst = torch.from_numpy(dst).to(device)
+        self.device = device.index or 0
+
+    def __call__(self, x, y, accumulate):
+        rc = fcg.lib().fcg_node_transfer(
+            self.device, ctypes.c_int64(self.n_out), _ptr(self.ptr), _ptr(self.src), _ptr(self.w),
+            _ptr(self.dst), _ptr(x), _ptr(y), 1 if accumulate else 0,
+            ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream))
+        if rc != 0:
+            raise fcg.FcgError(rc, "fcg_node_transfer failed")
+
+
+class _Level:
+    def __init__(self, mesh, ev, K, dbc_rows, device):
+        self.mesh, self.ev, self.K = mesh, ev, K
+        self.n = mesh.n_rows
+        self.dev = device
+        f64 = dict(dtype=torch.float64, device=device)
+        self.dinv = torch.empty(9 * (self.n // 3), **f64)
+        self.mask = torch.ones(self.n, **f64)
+        if len(dbc_rows):
+            self.mask[torch.as_tensor(np.asarray(dbc_rows, dtype=np.int64), device=device)] = 0.0
+        self.x, self.b, self.r, self.d, self.z = (torch.zeros(self.n, **f64) for _ in range(5))
+        self.lmax = None
+
+    def stream(self):
+        return torch.cuda.current_stream(self.dev)
+
+    def setup_diag(self):
+        rc = fcg.lib().fcg_block_jacobi_setup(self.ev._h, _ptr(self.K), _ptr(self.dinv),
+                                              ctypes.c_void_p(self.stream().cuda_stream))
+        if rc != 0:
+            self.ev._raise(rc, -1)
+
+    def apply_dinv(self, r, z, scale=1.0, accumulate=False):
+        rc = fcg.lib().fcg_block_jacobi_apply(self.ev._h, _ptr(self.dinv), _ptr(r), _ptr(z),
+                                              ctypes.c_double(scale), 1 if accumulate else 0,
+                                              ctypes.c_void_p(self.stream().cuda_stream))
+        if rc != 0:
+            self.ev._raise(rc, -1)
+
+    def spmv(self, x, y):
+        self.ev.spmv(self.K, x, y, stream=self.stream())
+
+    def estimate_lmax(self, iters=20, seed=20251015):
+        """Largest eigenvalue of D^-1 K from the Lanczos tridiagonal of a short block-Jacobi PCG
+        run on a random right-hand side (the CG estimate of hypre / AmgX Chebyshev smoothers;
+        power iteration converges from below too slowly on these spectra)."""
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        b = (torch.rand(self.n, generator=g, dtype=torch.float64) - 0.5).to(self.dev) * self.mask
+        r = b.clone()
+        z, q = self.z, self.r
+        self.apply_dinv(r, z)
+        p = z.clone()
+        rz = float(torch.dot(r, z))
+        alphas, betas = [], []
+        for _ in range(iters):
+            self.spmv(p, q)
+            pq = float(torch.dot(p, q))
+            if not pq > 0.0:
+                if not alphas:
+                    raise FloatingPointError(
+                        f"Lanczos estimate: p.Kp = {pq} on level with {self.n} rows (r.z = {rz}, "
+                        f"|p| = {float(torch.linalg.vector_norm(p))}, |Kp| = {float(torch.linalg.vector_norm(q))})")
+                break
+            alpha = rz / pq
+            r.add_(q, alpha=-alpha)
+            self.apply_dinv(r, z)
+            rz_n = float(torch.dot(r, z))
+            alphas.append(alpha)
+            if not rz_n > 0.0:
+                break
+            betas.append(rz_n / rz)
+            p.mul_(rz_n / rz).add_(z)
+            rz = rz_n
+        k = len(alphas)
+        T = np.zeros((k, k))
+        for i in range(k):
+            T[i, i] = 1.0 / alphas[i] + (betas[i - 1] / alphas[i - 1] if i > 0 else 0.0)
+            if i + 1 < k:
+                T[i, i + 1] = T[i + 1, i] = np.sqrt(betas[i]) / alphas[i]
+        self.lmax = float(np.linalg.eigvalsh(T)[-1])
+
+
+class Multigrid:
+    """Flexible-CG solver preconditioned by a geometric multigrid V-cycle (see module doc).
+
+    fine_mesh / fine_ev: the discretisation being solved (BoxMesh + Evaluator, single rank);
+    dbc_nodes(mesh) -> bool mask of the clamped nodes of a mesh of the same box (all 3 DOFs)."""
+
+    def __init__(self, fine_mesh, fine_ev, dbc_nodes, youngs, poisson, nu=2, min_intervals=4,
+                 max_levels=8, ratio=20.0, boost=1.1, coarse_rtol=1e-2, coarse_max_iter=2000):
+        dev = torch.device("cuda", fine_ev.device)
+        self.dev, self.nu, self.ratio, self.boost = dev, nu, ratio, boost
+        self.coarse_rtol, self.coarse_max_iter = coarse_rtol, coarse_max_iter
+        self.trace = bool(os.environ.get("FCG_MG_TRACE"))  # per-iteration residuals to stderr
+        box = fine_mesh.box
+        iv = [int(box.interval[d]) for d in range(3)]
+        lower = [box.lower[d] for d in range(3)]
+        upper = [box.upper[d] for d in range(3)]
+        rot = [box.rotation[d] for d in range(3)]
+        f64 = dict(dtype=torch.float64, device=dev)
+
+        def dbc_rows(mesh):
+            nodes = np.nonzero(dbc_nodes(mesh) & (mesh.node_dof_row >= 0))[0]
+            return np.sort((mesh.node_dof_row[nodes][:, None] + np.arange(3)).ravel()).astype(np.int32)
+
+        self.levels = [_Level(fine_mesh, fine_ev, None, dbc_rows(fine_mesh), dev)]
+        self.P, self.R = [], []
+        meshes = []
+        if fine_mesh.celltype == fcg.HEX27:
+            meshes.append(tuple(iv))
+        n = list(iv)
+        while len(meshes) + 1 < max_levels and all(v % 2 == 0 and v // 2 >= min_intervals for v in n):
+            n = [v // 2 for v in n]
+            meshes.append(tuple(n))
+        prev = fine_mesh
+        for ivc in meshes:
+            m = fcg.BoxMesh(fcg.HEX8, ivc, lower=lower, upper=upper, rotation=rot,
+                            first_node_gid=int(box.first_node_gid))
+            ev = fcg.Evaluator(m, kinematics=fcg.LINEAR, youngs=youngs, poisson=poisson,
+                               device=fine_ev.device)
+            K = torch.zeros(m.nnz, **f64)
+            u0 = torch.zeros(m.n_cols, **f64)
+            f0 = torch.zeros(m.n_rows, **f64)
+            ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u0, f0, K)
+            rows = dbc_rows(m)
+            ev.dirichlet_apply(torch.as_tensor(rows, device=dev), K)
+            lvl = _Level(m, ev, K, rows, dev)
+            lvl.setup_diag()
+            P, R = transfer_tables(prev, m)
+            self.P.append(_Transfer(P, dev))
+            self.R.append(_Transfer(R, dev))
+            self.levels.append(lvl)
+            prev = m
+        for lvl in self.levels[1:-1]:
+            lvl.estimate_lmax()
+
+    def describe(self):
+        return [{"celltype": "hex27" if l.mesh.celltype == fcg.HEX27 else "hex8",
+                 "intervals": [int(l.mesh.box.interval[d]) for d in range(3)], "dofs": l.n,
+                 "lmax": l.lmax} for l in self.levels]
+
+    # -- smoother ---------------------------------------------------------------------------
+    def _cheb(self, lvl, b, x, x_zero):
+        lmax = self.boost * lvl.lmax
+        lmin = lmax / self.ratio
+        theta, delta = 0.5 * (lmax + lmin), 0.5 * (lmax - lmin)
+        sigma = theta / delta
+        rho = 1.0 / sigma
+        r, d = lvl.r, lvl.d
+        if x_zero:
+            lvl.apply_dinv(b, d, 1.0 / theta)
+            x.copy_(d)
+        else:
+            lvl.spmv(x, r)
+            torch.sub(b, r, out=r)
+            lvl.apply_dinv(r, d, 1.0 / theta)
+            x.add_(d)
+        for _ in range(self.nu - 1):
+            lvl.spmv(x, r)
+            torch.sub(b, r, out=r)
+            rho_n = 1.0 / (2.0 * sigma - rho)
+            d.mul_(rho_n * rho)
+            lvl.apply_dinv(r, d, 2.0 * rho_n / delta, accumulate=True)
+            x.add_(d)
+            rho = rho_n
+
+    def _vcycle(self, l, b, x):
+        lvl = self.levels[l]
+        if l == len(self.levels) - 1:
+            lvl.ev.pcg_solve(lvl.K, b, x, self.coarse_rtol, self.coarse_max_iter,
+                             stream=torch.cuda.current_stream(self.dev))
+            return
+        self._cheb(lvl, b, x, x_zero=True)
+        lvl.spmv(x, lvl.r)
+        torch.sub(b, lvl.r, out=lvl.r)
+        c = self.levels[l + 1]
+        self.R[l](lvl.r, c.b, accumulate=False)
+        c.b.mul_(c.mask)
+        self._vcycle(l + 1, c.b, c.x)
+        self.P[l](c.x, x, accumulate=True)
+        x.mul_(lvl.mask)
+        self._cheb(lvl, b, x, x_zero=False)
+
+    # -- outer solve ------------------------------------------------------------------------
+    def solve(self, K, b, x, rtol, max_iter=1000):
+        """K x = b from x = 0 by flexible CG; returns (iterations, relative residual)."""
+        f0 = self.levels[0]
+        f0.K = K
+        f0.setup_diag()
+        f0.estimate_lmax()  # the tangent changes every Newton iteration
+        if self.trace:
+            print(f"  multigrid levels: {self.describe()}", file=sys.stderr, flush=True)
+        bn = float(torch.linalg.vector_norm(b))
+        x.zero_()
+        if bn == 0.0:
+            return 0, 0.0
+        r = b.clone()
+        z = torch.zeros_like(b)
+        q = torch.empty_like(b)
+        self._vcycle(0, r, z)
+        p = z.clone()
+        rz = float(torch.dot(r, z))
+        rn = bn
+        it = 0
+        while it < max_iter:
+            it += 1
+            f0.spmv(p, q)
+            alpha = rz / float(torch.dot(p, q))
+            x.add_(p, alpha=alpha)
+            r_old = r.clone()  # z . r_old enters the Polak-Ribiere beta
+            r.add_(q, alpha=-alpha)
+            rn = float(torch.linalg.vector_norm(r))
+            if not np.isfinite(rn):
+                raise FloatingPointError("multigrid FCG diverged (non-finite residual)")
+            if rn <= rtol * bn:
+                break
+            z = torch.zeros_like(b)
+            self._vcycle(0, r, z)
+            rz_new = float(torch.dot(r, z))
+            beta = (rz_new - float(torch.dot(z, r_old))) / rz
+            if self.trace:
+                print(f"  fcg {it}: |r|/|b| {rn / bn:.3e} rz {rz_new:.3e} beta {beta:.3e} "
+                      f"alpha {alpha:.3e}", file=sys.stderr, flush=True)
+            p.mul_(beta).add_(z)
+            rz = rz_new
+        return it, rn / bn

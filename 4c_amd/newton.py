@@ -74,8 +74,10 @@ class ForcingTerm:
 
 class StaticNewton:
     def __init__(self, evaluator, fext_row, dbc_rows, tol_res=1e-10, tol_inc=1e-10, max_iter=20,
-                 lin_rtol=1e-13, lin_max_iter=100000, forcing=None):
-        """forcing: ForcingTerm (None: Constant at lin_rtol)."""
+                 lin_rtol=1e-13, lin_max_iter=100000, forcing=None, linear_solver=None):
+        """forcing: ForcingTerm (None: Constant at lin_rtol).  linear_solver: an object with
+        solve(K, b, x, rtol, max_iter) -> (iterations, relative residual), e.g.
+        multigrid.Multigrid (None: the library's block-Jacobi PCG)."""
         info = evaluator.info
         self.ev = evaluator
         self.dev = torch.device("cuda", evaluator.device)
@@ -94,7 +96,14 @@ class StaticNewton:
         self.tol_res, self.tol_inc, self.max_iter = tol_res, tol_inc, max_iter
         self.lin_rtol, self.lin_max_iter = lin_rtol, lin_max_iter
         self.forcing = forcing if forcing is not None else ForcingTerm("Constant", constant=lin_rtol)
+        self.linear_solver = linear_solver
         self.history = []
+
+    def linear_solve(self, b, x, rtol):
+        """K x = b to |r| <= rtol |b| from x = 0; returns (iterations, relative residual)."""
+        if self.linear_solver is not None:
+            return self.linear_solver.solve(self.K, b, x, rtol, self.lin_max_iter)
+        return self.ev.pcg_solve(self.K, b, x, rtol, self.lin_max_iter)
 
     def solve(self, u0=None):
         """Returns the converged displacement (row map, device tensor); raises if not converged."""
@@ -114,7 +123,7 @@ class StaticNewton:
                 return u
             torch.neg(self.r, out=self.r)
             eta = self.forcing.compute(it, nr, nr_old, lin_abs)
-            lin_it, lin_res = self.ev.pcg_solve(self.K, self.r, self.du, eta, self.lin_max_iter)
+            lin_it, lin_res = self.linear_solve(self.r, self.du, eta)
             nr_old, lin_abs = nr, lin_res * nr  # ‖F_k + J_k d_k‖ (full step, no line search)
             rec.update(lin_iter=lin_it, lin_relres=lin_res, eta=eta)
             self.history.append(rec)

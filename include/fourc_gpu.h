@@ -191,6 +191,19 @@ int fcg_dirichlet_apply(fcg_ctx* ctx, int64_t n_dbc, const int32_t* d_rows, doub
  * single-rank systems only (matrix column map = row map), else FCG_ERR_ARG.  Deterministic. */
 int fcg_pcg_solve(fcg_ctx* ctx, const double* d_K_vals, const double* d_b_row, double* d_x_row,
     double rtol, int max_iter, int* iterations, double* rel_residual, void* stream);
+/* Pieces of the geometric multigrid preconditioner (4c_amd/multigrid.py; the MueLu
+ * preconditioner 4C hands to Belos, 4C_linear_solver_preconditioner_muelu.cpp, restated for
+ * structured boxes).  d_dinv: 9 doubles per owned node (row-major inverse 3x3 nodal diagonal
+ * blocks of K, FCG_ERR_SINGULAR if one is singular).  apply: z = scale D^-1 r (+ z if accumulate).
+ * fcg_node_transfer: y[dst_row0[o] + d] = (accumulate ? y : 0) + sum_{j in [ptr[o], ptr[o+1])}
+ * w[j] x[src_row0[j] + d] for d = 0..2 and dst_row0[o] >= 0 (all device arrays; stream may be
+ * NULL = the null stream).  Asynchronous on `stream` except fcg_block_jacobi_setup. */
+int fcg_block_jacobi_setup(fcg_ctx* ctx, const double* d_K_vals, double* d_dinv, void* stream);
+int fcg_block_jacobi_apply(fcg_ctx* ctx, const double* d_dinv, const double* d_r_row, double* d_z_row,
+    double scale, int accumulate, void* stream);
+int fcg_node_transfer(int device, int64_t n_out, const int64_t* d_ptr, const int32_t* d_src_row0,
+    const double* d_w, const int32_t* d_dst_row0, const double* d_x, double* d_y, int accumulate,
+    void* stream);
 
 /* Neumann loads (host arrays; added into fext_row, owned rows only).  funct[d] > 0 selects a
  * spatial function evaluated through `fn` at the reference position of each integration point

@@ -30,6 +30,11 @@ ap.add_argument("--path", default="auto", choices=["auto", "general", "structure
 ap.add_argument("--lin-max-iter", type=int, default=100000)
 ap.add_argument("--forcing", default="Constant", choices=["Constant", "Type 1", "Type 2"],
                 help="NOX forcing-term method (Constant = --lin-rtol every step)")
+ap.add_argument("--mg", action="store_true",
+                help="geometric multigrid preconditioned flexible CG (4c_amd/multigrid.py)")
+ap.add_argument("--mg-nu", type=int, default=2, help="Chebyshev degree of the MG smoother")
+ap.add_argument("--mg-coarse-rtol", type=float, default=1e-2)
+ap.add_argument("--mg-ratio", type=float, default=20.0)
 a = ap.parse_args()
 ct = fcg.HEX8 if a.celltype == "hex8" else fcg.HEX27
 kin = fcg.LINEAR if a.kinem == "linear" else fcg.TOTLAG
@@ -79,7 +84,7 @@ class Timed(newton.StaticNewton):
             hb.start()
             try:
                 eta = self.forcing.compute(it, nr, nr_old, lin_abs)
-                li, lr = self.ev.pcg_solve(self.K, self.r, self.du, eta, self.lin_max_iter)
+                li, lr = self.linear_solve(self.r, self.du, eta)
                 nr_old, lin_abs = nr, lr * nr
             finally:
                 done.set()
@@ -94,16 +99,27 @@ class Timed(newton.StaticNewton):
         return u
 
 
+mg = None
+if a.mg:
+    t_mg = time.perf_counter()
+    mg = importlib.import_module("4c_amd.multigrid").Multigrid(
+        mesh, ev, lambda m: np.isclose(m.node_x[:, 0], 0.0), 210.0, 0.3, nu=a.mg_nu,
+        coarse_rtol=a.mg_coarse_rtol, ratio=a.mg_ratio)
+    print(f"multigrid setup {time.perf_counter() - t_mg:.1f} s: {json.dumps(mg.describe())}",
+          file=sys.stderr, flush=True)
+    t_setup = time.perf_counter() - t0
 print(f"setup {t_setup:.1f} s", file=sys.stderr, flush=True)
 nt = Timed(ev, fext, dbc, lin_max_iter=a.lin_max_iter, tol_res=a.tol * max(np.linalg.norm(fext), 1e-300), tol_inc=a.tol,
            lin_rtol=a.lin_rtol, max_iter=40,
-           forcing=newton.ForcingTerm(a.forcing, constant=a.lin_rtol))
+           forcing=newton.ForcingTerm(a.forcing, constant=a.lin_rtol), linear_solver=mg)
 t1 = time.perf_counter()
 u = nt.solve()
 torch.cuda.synchronize()
 t_newton = time.perf_counter() - t1
 h = nt.history
-out = {"config": f"{a.celltype}-{a.kinem}-{a.n}^3-cantilever", "forcing": a.forcing, "elements": mesh.n_ele,
+out = {"config": f"{a.celltype}-{a.kinem}-{a.n}^3-cantilever", "forcing": a.forcing,
+       "linear_solver": (f"multigrid-FCG (Chebyshev {a.mg_nu})" if a.mg else "block-Jacobi PCG"),
+       "mg_levels": mg.describe() if mg else None, "elements": mesh.n_ele,
        "dofs": mesh.n_rows, "nnz": mesh.nnz, "setup_s": t_setup, "newton_s": t_newton,
        "newton_iterations": len(h) - 1,
        "assembly_ms_mean": float(np.mean([r["assembly_ms"] for r in h])),
