@@ -83,7 +83,7 @@ EXPORTS = ["fcg_create", "fcg_destroy", "fcg_last_error", "fcg_evaluate", "fcg_e
            "fcg_device_alloc", "fcg_device_free", "fcg_memcpy_h2d", "fcg_memcpy_d2h",
            "fcg_memset_device", "fcg_set_timing", "fcg_get_timing", "fcg_get_info",
            "fcg_get_diagnostics", "fcg_measure_peaks", "fcg_spmv", "fcg_dirichlet_apply",
-           "fcg_pcg_solve",
+           "fcg_pcg_solve", "fcg_block_jacobi_setup", "fcg_block_jacobi_apply", "fcg_node_transfer",
            "fcg_neumann_surface", "fcg_neumann_volume",
            "fcg_graph_build_device",
            "fcg_tsi_create", "fcg_tsi_destroy", "fcg_tsi_last_error", "fcg_tsi_evaluate_device",
