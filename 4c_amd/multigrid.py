@@ -158,7 +158,7 @@ class _Level:
     def spmv(self, x, y):
         self.ev.spmv(self.K, x, y, stream=self.stream())
 
-    def estimate_lmax(self, iters=20, seed=20251015):
+    def estimate_lmax(self, iters=10, seed=20251015):
         """Largest eigenvalue of D^-1 K from the Lanczos tridiagonal of a short block-Jacobi PCG
         run on a random right-hand side (the CG estimate of hypre / AmgX Chebyshev smoothers;
         power iteration converges from below too slowly on these spectra)."""
