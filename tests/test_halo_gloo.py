@@ -31,6 +31,7 @@ def _worker(rank, world, port, q):
         m = fcg.BoxMesh(fcg.HEX8, iv, rank=rank, nranks=world)
         owner = halo.col_owner_of(m)
         imp = halo.HaloImport(m.row_gid, m.col_gid, owner, rank, world, torch.device("cpu"))
+        assert imp.contiguous  # BoxMesh column maps: owned prefix + ghosts by (owner, gid)
         u_row = torch.tensor([ug[gmap[int(g)]] for g in m.row_gid], dtype=torch.float64)
         u_col = torch.full((m.n_cols,), float("nan"), dtype=torch.float64)
         imp(u_row, u_col)
