@@ -112,6 +112,32 @@ def cpu_baseline(n, kinem, threads):
     }
 
 
+def newton_secondary(n, timeout_s=900):
+    """BASELINE config 3: StVK TotLag on the 1M-hex27 cube (x- clamped, traction -1 in z on x+),
+    full static Newton on this GPU (fcg_evaluate_device + Dirichlet + multigrid-preconditioned
+    flexible CG, 4c_amd/newton.py + multigrid.py), run by tools/newton_bench.py in a child process
+    so that its ~60 GB of device buffers are released when it ends."""
+    cmd = [sys.executable, os.path.join(ROOT, "tools", "newton_bench.py"), "--celltype", "hex27",
+           "--kinem", "totlag", "--n", str(n), "--length", "1", "--load", "-1", "--mg"]
+    t = time.perf_counter()
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s)
+    wall = time.perf_counter() - t
+    if p.returncode != 0:
+        return {"workload": f"hex27-totlag-{n}^3-newton", "error": p.stderr[-2000:]}
+    d = json.loads(p.stdout.strip().splitlines()[-1])
+    return {
+        "workload": f"hex27-totlag-{n}^3-full-newton",
+        "baseline_config": "BASELINE.json configs[2] (StVK, 1M hex27, full Newton loop on 1 MI355X)",
+        "value": d["newton_s"], "unit": "s (Newton loop, setup excluded)", "higher_is_better": False,
+        "newton_iterations": d["newton_iterations"], "linear_iterations": d["pcg_iterations"],
+        "linear_solver": d["linear_solver"], "forcing": d["forcing"],
+        "norm_res": [h["norm_res"] for h in d["history"]],
+        "assembly_ms_mean": d["assembly_ms_mean"], "assembly_elem_per_s": d["assembly_elem_per_s"],
+        "solve_ms_total": d["solve_ms_total"], "setup_s": d["setup_s"], "wall_s": wall,
+        "elements": d["elements"], "dofs": d["dofs"], "nnz": d["nnz"], "tip_uz": d["tip_uz"],
+    }
+
+
 # SURVEY.md §8d algorithmic figures for hex27 TotLag K + r (per element)
 ALG_BYTES_PER_ELE_H27 = 37695.0
 ALG_FLOP_PER_ELE_H27_TOTLAG = 2.59e6
@@ -269,6 +295,8 @@ def main():
     ap.add_argument("--no-hex27", action="store_true", help="skip the hex27 (config 3) line")
     ap.add_argument("--no-tsi", action="store_true", help="skip the TSI (config 5) line")
     ap.add_argument("--hex27-n", type=int, default=40)
+    ap.add_argument("--no-newton", action="store_true", help="skip the config-3 Newton line")
+    ap.add_argument("--newton-n", type=int, default=100)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -437,6 +465,12 @@ def main():
                                              args.cpu_threads, not args.no_cpu_baseline))
         except Exception as e:  # report, never hide
             secondary.append({"workload": "hex27-totlag", "error": repr(e)})
+    if rank == 0 and world == 1 and not args.no_newton:
+        torch.cuda.empty_cache()
+        try:
+            secondary.append(newton_secondary(args.newton_n))
+        except Exception as e:  # report, never hide
+            secondary.append({"workload": "hex27-totlag-newton", "error": repr(e)})
     if secondary:
         out["secondary"] = secondary
     if rank == 0:
