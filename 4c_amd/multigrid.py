@@ -198,6 +198,10 @@ class _Level:
         self.lmax = float(np.linalg.eigvalsh(T)[-1])
 
 
+class _Indefinite(Exception):
+    """The V-cycle returned a non-descent direction (r . z <= 0): smoother bound too low."""
+
+
 class Multigrid:
     """Flexible-CG solver preconditioned by a geometric multigrid V-cycle (see module doc).
 
@@ -305,7 +309,18 @@ class Multigrid:
         f0 = self.levels[0]
         f0.K = K
         f0.setup_diag()
-        f0.estimate_lmax()  # the tangent changes every Newton iteration
+        # lambda_max of D^-1 K barely moves between Newton iterations: estimated on the first
+        # solve and kept; a solve that meets an indefinite preconditioned step re-estimates and
+        # restarts (below)
+        if f0.lmax is None:
+            f0.estimate_lmax()
+        try:
+            return self._fcg(f0, b, x, rtol, max_iter)
+        except _Indefinite:
+            f0.estimate_lmax()
+            return self._fcg(f0, b, x, rtol, max_iter)
+
+    def _fcg(self, f0, b, x, rtol, max_iter):
         if self.trace:
             print(f"  multigrid levels: {self.describe()}", file=sys.stderr, flush=True)
         bn = float(torch.linalg.vector_norm(b))
@@ -318,6 +333,8 @@ class Multigrid:
         self._vcycle(0, r, z)
         p = z.clone()
         rz = float(torch.dot(r, z))
+        if not rz > 0.0:
+            raise _Indefinite()
         rn = bn
         it = 0
         while it < max_iter:
@@ -335,6 +352,8 @@ class Multigrid:
             z = torch.zeros_like(b)
             self._vcycle(0, r, z)
             rz_new = float(torch.dot(r, z))
+            if not rz_new > 0.0:
+                raise _Indefinite()
             beta = (rz_new - float(torch.dot(z, r_old))) / rz
             if self.trace:
                 print(f"  fcg {it}: |r|/|b| {rn / bn:.3e} rz {rz_new:.3e} beta {beta:.3e} "
