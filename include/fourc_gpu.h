@@ -129,8 +129,10 @@ int fcg_evaluate(fcg_ctx* ctx, int action, const double* u_col, double* fint_row
 /*
  * The same on device-resident buffers (HBM) for a GPU-resident Newton loop.
  *   mode    fcg_mode (ACCUMULATE = +=, OVERWRITE = zero + assemble fused)
- *   stream  hipStream_t to run on (NULL = the context's own stream); the call returns after the
- *           stream has drained (matching the synchronous Newton loop of the reference).
+ *   stream  hipStream_t to run on (NULL = the context's own stream, a blocking stream: ordered
+ *           with the null stream, so work the caller queued there -- e.g. torch's default
+ *           stream filling d_u_col -- completes first); the call returns after the stream has
+ *           drained (matching the synchronous Newton loop of the reference).
  */
 int fcg_evaluate_device(fcg_ctx* ctx, int action, int mode, const double* d_u_col,
     double* d_fint_row, double* d_K_vals, void* stream, int32_t* bad_ele_gid);
@@ -197,7 +199,8 @@ int fcg_pcg_solve(fcg_ctx* ctx, const double* d_K_vals, const double* d_b_row, d
  * blocks of K, FCG_ERR_SINGULAR if one is singular).  apply: z = scale D^-1 r (+ z if accumulate).
  * fcg_node_transfer: y[dst_row0[o] + d] = (accumulate ? y : 0) + sum_{j in [ptr[o], ptr[o+1])}
  * w[j] x[src_row0[j] + d] for d = 0..2 and dst_row0[o] >= 0 (all device arrays; stream may be
- * NULL = the null stream).  Asynchronous on `stream` except fcg_block_jacobi_setup. */
+ * NULL: the context's stream for the ctx calls, the null stream for fcg_node_transfer).
+ * Asynchronous on `stream` except fcg_block_jacobi_setup, which returns after it drained. */
 int fcg_block_jacobi_setup(fcg_ctx* ctx, const double* d_K_vals, double* d_dinv, void* stream);
 int fcg_block_jacobi_apply(fcg_ctx* ctx, const double* d_dinv, const double* d_r_row, double* d_z_row,
     double scale, int accumulate, void* stream);
