@@ -210,12 +210,24 @@ class Multigrid:
 
     def __init__(self, fine_mesh, fine_ev, dbc_nodes, youngs, poisson, nu=2, min_intervals=4,
                  max_levels=8, ratio=20.0, boost=1.1, coarse_rtol=1e-2, coarse_max_iter=2000):
+        box = getattr(fine_mesh, "box", None)
+        if box is None or getattr(fine_mesh, "nranks", 1) != 1:
+            raise ValueError("Multigrid needs a single-rank GridGenerator box (fcg.BoxMesh)")
+        iv = [int(box.interval[d]) for d in range(3)]
+        meshes = []  # intervals of the hex8 coarse levels
+        if fine_mesh.celltype == fcg.HEX27:
+            meshes.append(tuple(iv))
+        n = list(iv)
+        while len(meshes) + 1 < max_levels and all(v % 2 == 0 and v // 2 >= min_intervals for v in n):
+            n = [v // 2 for v in n]
+            meshes.append(tuple(n))
+        if not meshes:
+            raise ValueError(f"no coarse level for intervals {iv}: hex8 boxes need even intervals "
+                             f"with n/2 >= min_intervals ({min_intervals})")
         dev = torch.device("cuda", fine_ev.device)
         self.dev, self.nu, self.ratio, self.boost = dev, nu, ratio, boost
         self.coarse_rtol, self.coarse_max_iter = coarse_rtol, coarse_max_iter
         self.trace = bool(os.environ.get("FCG_MG_TRACE"))  # per-iteration residuals to stderr
-        box = fine_mesh.box
-        iv = [int(box.interval[d]) for d in range(3)]
         lower = [box.lower[d] for d in range(3)]
         upper = [box.upper[d] for d in range(3)]
         rot = [box.rotation[d] for d in range(3)]
@@ -227,13 +239,6 @@ class Multigrid:
 
         self.levels = [_Level(fine_mesh, fine_ev, None, dbc_rows(fine_mesh), dev)]
         self.P, self.R = [], []
-        meshes = []
-        if fine_mesh.celltype == fcg.HEX27:
-            meshes.append(tuple(iv))
-        n = list(iv)
-        while len(meshes) + 1 < max_levels and all(v % 2 == 0 and v // 2 >= min_intervals for v in n):
-            n = [v // 2 for v in n]
-            meshes.append(tuple(n))
         prev = fine_mesh
         for ivc in meshes:
             m = fcg.BoxMesh(fcg.HEX8, ivc, lower=lower, upper=upper, rotation=rot,

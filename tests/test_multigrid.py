@@ -59,6 +59,14 @@ def test_transfer_tables_host(k):
     assert np.allclose(np.add.reduceat(w, ptr[:-1]), 1.0)
 
 
+def test_multigrid_rejects_meshes_without_a_hierarchy():
+    m = fcg.BoxMesh(fcg.HEX8, (3, 3, 3))
+    with pytest.raises(ValueError):
+        mgm.Multigrid(m, None, lambda mm: np.zeros(mm.n_node, bool), E, NU)
+    with pytest.raises(ValueError):
+        mgm.Multigrid(object(), None, None, E, NU)
+
+
 def _dev():
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
