@@ -287,7 +287,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--elems-per-dir", dest="n", type=int, default=100,
                     help="elements per direction per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -341,24 +341,36 @@ def main():
         ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u_col, f, K, stream=stream)
         return halo.residual_norm(f)
 
+    # SURVEY §8d asks for the spec peaks re-measured on the box; measured here, on every rank's
+    # GPU before its warm-up, so that the timed steps start on a GPU already at its working
+    # clocks (the reported peaks are rank 0's)
+    try:
+        peaks = fcg.measure_peaks(dev.index)
+    except Exception as e:  # report, never hide
+        peaks = e
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    ev.set_timing(True)
-    t_el, t_as = [], []
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        a, b = ev.timing()
-        t_el.append(a)
-        t_as.append(b)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
+    # the kernel's own duration (hipEvents on its launch stream) from a second pass of the same
+    # steps, so that the event records and queries stay out of the wall-clock window above
+    ev.set_timing(True)
+    t_el, t_as = [], []
+    for _ in range(args.steps):
+        step()
+        a, b = ev.timing()
+        t_el.append(a)
+        t_as.append(b)
+    torch.cuda.synchronize(dev)
     ev.set_timing(False)
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
     if world > 1:
@@ -444,7 +456,9 @@ def main():
     # `peak` stays the spec figure, the fractions against the measured ones are reported beside
     if rank == 0:
         try:
-            triad, valu, mfma = fcg.measure_peaks(dev.index)
+            if isinstance(peaks, Exception):
+                raise peaks
+            triad, valu, mfma = peaks
             fp64_meas = max(valu, mfma)
             out["roofline"]["measured_peaks"] = {
                 "hbm_triad_gbs": triad, "fp64_valu_tflops": valu, "fp64_mfma_tflops": mfma,
