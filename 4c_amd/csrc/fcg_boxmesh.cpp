@@ -101,7 +101,8 @@ void parallel_for(int64_t n, F f)
 struct fcg_box_mesh {
   fcg_box box;
   int rank = 0, nranks = 1, npe = 8;
-  int64_t n_ele_global = 0, n_ele_row = 0;
+  int64_t n_ele_global = 0, n_ele_row = 0, n_owned_rows = 0;
+  int flags = 0;
   std::vector<int32_t> ele_nodes, ele_gid, ele_ijk;
   std::vector<double> node_x;
   std::vector<int64_t> node_gid;
@@ -115,6 +116,13 @@ extern "C" {
 
 int fcg_box_mesh_create(const fcg_box* box, int rank, int nranks, fcg_box_mesh** out)
 {
+  return fcg_box_mesh_create_ex(box, rank, nranks, FCG_BOX_GHOSTED, out);
+}
+
+int fcg_box_mesh_create_ex(const fcg_box* box, int rank, int nranks, int flags, fcg_box_mesh** out)
+{
+  if (flags != FCG_BOX_GHOSTED && flags != FCG_BOX_STRICT) return FCG_ERR_ARG;
+  const bool strict = flags == FCG_BOX_STRICT;
   if (!box || !out || nranks < 1 || rank < 0 || rank >= nranks) return FCG_ERR_ARG;
   *out = nullptr;
   for (int d = 0; d < 3; ++d)
@@ -127,6 +135,7 @@ int fcg_box_mesh_create(const fcg_box* box, int rank, int nranks, fcg_box_mesh**
   m->box = *box;
   m->rank = rank;
   m->nranks = nranks;
+  m->flags = flags;
   const bool h27 = box->celltype == FCG_HEX27;
   const int npe = h27 ? 27 : 8;
   m->npe = npe;
@@ -154,19 +163,19 @@ int fcg_box_mesh_create(const fcg_box* box, int rank, int nranks, fcg_box_mesh**
       {2, 0, 1}, {2, 2, 1}, {0, 2, 1}, {1, 0, 2}, {2, 1, 2}, {1, 2, 2}, {0, 1, 2}, {1, 1, 0},
       {1, 0, 1}, {2, 1, 1}, {1, 2, 1}, {0, 1, 1}, {1, 1, 2}, {1, 1, 1}};
 
-  // column elements: candidates in the section grown by one layer
+  // column elements: candidates in the section grown by one layer (strict: the section itself)
   int64_t clo[3], chi[3];
   for (int d = 0; d < 3; ++d)
   {
-    clo[d] = std::max<int64_t>(0, my.lo[d] - 1);
-    chi[d] = std::min<int64_t>(box->interval[d], my.hi[d] + 1);
+    clo[d] = strict ? my.lo[d] : std::max<int64_t>(0, my.lo[d] - 1);
+    chi[d] = strict ? my.hi[d] : std::min<int64_t>(box->interval[d], my.hi[d] + 1);
   }
   std::vector<int64_t> col_ele;
   for (int64_t ez = clo[2]; ez < chi[2]; ++ez)
     for (int64_t ey = clo[1]; ey < chi[1]; ++ey)
       for (int64_t ex = clo[0]; ex < chi[0]; ++ex)
       {
-        bool has = false;
+        bool has = strict;
         for (int a = 0; a < npe && !has; ++a)
           has = owner_of(2 * ex + off27[a][0], 2 * ey + off27[a][1], 2 * ez + off27[a][2]) == rank;
         if (has) col_ele.push_back((ez * IY + ey) * IX + ex);
@@ -217,6 +226,7 @@ int fcg_box_mesh_create(const fcg_box* box, int rank, int nranks, fcg_box_mesh**
     m->node_owner[i] = own[n];
     m->node_dof_col[i] = int32_t(3 * i);
     if (own[n] == rank) m->node_dof_row[i] = int32_t(3 * n_owned++);
+    else if (strict) m->node_dof_row[i] = int32_t(3 * i);  // extended row (owned nodes come first)
     // coordinates (4C_io_gridgenerator.cpp:283-317)
     const int64_t ii = L % NX, jj = (L / NX) % NY, kk = L / (NX * NY);
     const int64_t lidx[3] = {ii, jj, kk};
@@ -271,8 +281,11 @@ int fcg_box_mesh_create(const fcg_box* box, int rank, int nranks, fcg_box_mesh**
       m->ele_nodes[e * npe + a] = newid[n];
     }
   }
+  m->n_owned_rows = 3 * n_owned;
+  // rows: the owned nodes, plus (strict) the extended rows of every other touched node
+  const int64_t n_rn = strict ? ncn : n_owned;
   // dof gids of the maps
-  m->row_gid.resize(3 * n_owned);
+  m->row_gid.resize(3 * n_rn);
   m->col_gid.resize(3 * ncn);
   for (int64_t i = 0; i < ncn; ++i)
   {
@@ -281,27 +294,27 @@ int fcg_box_mesh_create(const fcg_box* box, int rank, int nranks, fcg_box_mesh**
     if (m->node_dof_row[i] >= 0)
       for (int d = 0; d < 3; ++d) m->row_gid[m->node_dof_row[i] + d] = int32_t(dof0 + d);
   }
-  // graph: owned node -> incident column elements -> neighbour nodes
-  std::vector<int64_t> adj_ptr(n_owned + 1, 0);
+  // graph: row node -> incident column elements -> neighbour nodes
+  std::vector<int64_t> adj_ptr(n_rn + 1, 0);
   for (int64_t i = 0; i < nce * npe; ++i)
   {
     const int32_t n = m->ele_nodes[i];
-    if (n < n_owned) adj_ptr[n + 1]++;  // owned nodes are the first n_owned local ids
+    if (n < n_rn) adj_ptr[n + 1]++;  // row nodes are the first n_rn local ids
   }
-  for (int64_t n = 0; n < n_owned; ++n) adj_ptr[n + 1] += adj_ptr[n];
-  std::vector<int32_t> adj(adj_ptr[n_owned]);
+  for (int64_t n = 0; n < n_rn; ++n) adj_ptr[n + 1] += adj_ptr[n];
+  std::vector<int32_t> adj(adj_ptr[n_rn]);
   {
     std::vector<int64_t> fill(adj_ptr.begin(), adj_ptr.end() - 1);
     for (int64_t e = 0; e < nce; ++e)
       for (int a = 0; a < npe; ++a)
       {
         const int32_t n = m->ele_nodes[e * npe + a];
-        if (n < n_owned) adj[fill[n]++] = int32_t(e);
+        if (n < n_rn) adj[fill[n]++] = int32_t(e);
       }
   }
-  std::vector<int32_t> nnb(n_owned);
-  std::vector<std::vector<int32_t>> nb(n_owned);
-  parallel_for(n_owned, [&](int64_t n) {
+  std::vector<int32_t> nnb(n_rn);
+  std::vector<std::vector<int32_t>> nb(n_rn);
+  parallel_for(n_rn, [&](int64_t n) {
     std::vector<int32_t>& v = nb[n];
     v.reserve(8 * npe);
     for (int64_t k = adj_ptr[n]; k < adj_ptr[n + 1]; ++k)
@@ -310,12 +323,12 @@ int fcg_box_mesh_create(const fcg_box* box, int rank, int nranks, fcg_box_mesh**
     v.erase(std::unique(v.begin(), v.end()), v.end());
     nnb[n] = int32_t(v.size());
   });
-  m->rowptr.resize(3 * n_owned + 1);
+  m->rowptr.resize(3 * n_rn + 1);
   m->rowptr[0] = 0;
-  for (int64_t n = 0; n < n_owned; ++n)
+  for (int64_t n = 0; n < n_rn; ++n)
     for (int d = 0; d < 3; ++d) m->rowptr[3 * n + d + 1] = m->rowptr[3 * n + d] + 3 * int64_t(nnb[n]);
-  m->col_lid.resize(m->rowptr[3 * n_owned]);
-  parallel_for(n_owned, [&](int64_t n) {
+  m->col_lid.resize(m->rowptr[3 * n_rn]);
+  parallel_for(n_rn, [&](int64_t n) {
     const std::vector<int32_t>& v = nb[n];
     for (int d = 0; d < 3; ++d)
     {
@@ -379,6 +392,13 @@ int fcg_box_mesh_counts(const fcg_box_mesh* m, int64_t* n_ele_global, int64_t* n
   if (!m) return FCG_ERR_ARG;
   if (n_ele_global) *n_ele_global = m->n_ele_global;
   if (n_ele_row) *n_ele_row = m->n_ele_row;
+  return FCG_OK;
+}
+
+int fcg_box_mesh_owned_rows(const fcg_box_mesh* m, int64_t* n_owned_rows)
+{
+  if (!m || !n_owned_rows) return FCG_ERR_ARG;
+  *n_owned_rows = m->n_owned_rows;
   return FCG_OK;
 }
 

@@ -823,9 +823,141 @@ int fcg_destroy(fcg_ctx* ctx)
   if (ctx->h_u) (void)hipFree(ctx->h_u);
   if (ctx->h_f) (void)hipFree(ctx->h_f);
   if (ctx->h_k) (void)hipFree(ctx->h_k);
+  fcg::staging_free(ctx->staging);
   delete ctx;
   return FCG_OK;
 }
+
+}  // extern "C"
+
+namespace {
+
+// The error flags of the evaluates queued since the last check (4C's throws).
+int report_error(fcg_ctx* ctx, int32_t* bad_ele_gid)
+{
+  fcg::DeviceMesh& m = ctx->mesh;
+  const int32_t* errv = m.err_host;
+  m.err_clean = errv[0] == 0;  // no failing element: err still {0, INT32_MAX}
+  if (errv[0] == 0) return FCG_OK;
+  int32_t gid = -1;
+  if (errv[1] >= 0 && errv[1] < m.n_ele)
+    (void)hipMemcpy(&gid, m.ele_gid + errv[1], sizeof(int32_t), hipMemcpyDeviceToHost);
+  if (bad_ele_gid) *bad_ele_gid = gid;
+  ctx->last_error = errv[0] == FCG_ERR_NODAL_DETJ
+                        ? "determinant of jacobian <= 0 at one node of element " + std::to_string(gid)
+                        : "singular 3x3 matrix in element " + std::to_string(gid);
+  return errv[0];
+}
+
+void read_timing(fcg::Timing& T)
+{
+  if (!T.pending) return;
+  T.pending = false;
+  float a = 0.f, b = 0.f;
+  if (hipEventSynchronize(T.ev[2]) != hipSuccess) return;
+  (void)hipEventElapsedTime(&a, T.ev[0], T.ev[1]);
+  (void)hipEventElapsedTime(&b, T.ev[1], T.ev[2]);
+  T.ms_element = a;
+  T.ms_assemble = T.path == FCG_PATH_GENERAL ? b : 0.0;  // fused: evaluate + assembly in ms_element
+}
+
+}  // namespace
+
+namespace fcg {
+
+hipError_t staged_copy(HostStaging& st, int device, void* dst, const void* src, int64_t bytes,
+    bool to_device)
+{
+  if (bytes <= 0) return hipSuccess;
+  if (st.threads <= 0)
+    return hipMemcpy(dst, src, bytes, to_device ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost);
+  hipError_t he = hipSuccess;
+  if (!st.stream)
+  {
+    st.chunk = int64_t(32) << 20;  // bytes per chunk
+    he = hipStreamCreateWithFlags(&st.stream, hipStreamNonBlocking);
+    for (int b = 0; b < 2 && he == hipSuccess; ++b)
+    {
+      he = hipHostMalloc(reinterpret_cast<void**>(&st.pin[b]), st.chunk);
+      if (he == hipSuccess) he = hipEventCreateWithFlags(&st.ev[b], hipEventDisableTiming);
+    }
+    if (he != hipSuccess) return he;
+  }
+  (void)device;
+  const int64_t n_chunks = (bytes + st.chunk - 1) / st.chunk;
+  auto host_copy = [&](char* d, const char* s, int64_t len) {
+    const int nt = int(std::min<int64_t>(st.threads, std::max<int64_t>(1, len >> 22)));
+    if (nt <= 1)
+    {
+      std::memcpy(d, s, len);
+      return;
+    }
+    std::vector<std::thread> th;
+    const int64_t part = (len + nt - 1) / nt;
+    for (int t = 0; t < nt; ++t)
+    {
+      const int64_t a = t * part, e = std::min(len, a + part);
+      if (a < e) th.emplace_back([=]() { std::memcpy(d + a, s + a, e - a); });
+    }
+    for (auto& x : th) x.join();
+  };
+  char* D = static_cast<char*>(dst);
+  const char* S = static_cast<const char*>(src);
+  if (to_device)
+  {
+    // host copy of chunk i into pin[i % 2] overlaps the DMA of chunk i - 1
+    for (int64_t i = 0; i < n_chunks && he == hipSuccess; ++i)
+    {
+      const int b = int(i & 1);
+      const int64_t off = i * st.chunk, len = std::min(st.chunk, bytes - off);
+      if (i >= 2) he = hipEventSynchronize(st.ev[b]);  // the DMA that last read pin[b] is done
+      if (he != hipSuccess) break;
+      host_copy(reinterpret_cast<char*>(st.pin[b]), S + off, len);
+      he = hipMemcpyAsync(D + off, st.pin[b], len, hipMemcpyHostToDevice, st.stream);
+      if (he == hipSuccess) he = hipEventRecord(st.ev[b], st.stream);
+    }
+  }
+  else
+  {
+    // DMA of chunk i + 1 overlaps the host copy of chunk i
+    auto issue = [&](int64_t i) {
+      const int b = int(i & 1);
+      const int64_t off = i * st.chunk, len = std::min(st.chunk, bytes - off);
+      hipError_t e = hipMemcpyAsync(st.pin[b], S + off, len, hipMemcpyDeviceToHost, st.stream);
+      if (e == hipSuccess) e = hipEventRecord(st.ev[b], st.stream);
+      return e;
+    };
+    he = issue(0);
+    for (int64_t i = 0; i < n_chunks && he == hipSuccess; ++i)
+    {
+      const int b = int(i & 1);
+      he = hipEventSynchronize(st.ev[b]);
+      if (he == hipSuccess && i + 1 < n_chunks) he = issue(i + 1);
+      if (he != hipSuccess) break;
+      const int64_t off = i * st.chunk, len = std::min(st.chunk, bytes - off);
+      host_copy(D + off, reinterpret_cast<const char*>(st.pin[b]), len);
+    }
+  }
+  if (he == hipSuccess) he = hipStreamSynchronize(st.stream);
+  return he;
+}
+
+void staging_free(HostStaging& st)
+{
+  for (int b = 0; b < 2; ++b)
+  {
+    if (st.pin[b]) (void)hipHostFree(st.pin[b]);
+    if (st.ev[b]) (void)hipEventDestroy(st.ev[b]);
+    st.pin[b] = nullptr;
+    st.ev[b] = nullptr;
+  }
+  if (st.stream) (void)hipStreamDestroy(st.stream);
+  st.stream = nullptr;
+}
+
+}  // namespace fcg
+
+extern "C" {
 
 int fcg_evaluate_device(fcg_ctx* ctx, int action, int mode, const double* d_u_col,
     double* d_fint_row, double* d_K_vals, void* stream_ptr, int32_t* bad_ele_gid)
@@ -845,7 +977,13 @@ int fcg_evaluate_device(fcg_ctx* ctx, int action, int mode, const double* d_u_co
   hipStream_t s = stream_ptr ? static_cast<hipStream_t>(stream_ptr) : ctx->stream;
   const int32_t init[2] = {0, INT32_MAX};
   hipError_t he = hipSuccess;
-  if (!m.err_clean) he = hipMemcpyAsync(m.err, init, sizeof(init), hipMemcpyHostToDevice, s);
+  // a pending evaluate on another stream must have written its flags first
+  if (ctx->pending && ctx->pending_stream != s) he = hipStreamSynchronize(ctx->pending_stream);
+  if (he == hipSuccess && !m.err_clean)
+  {
+    he = hipMemcpyAsync(m.err, init, sizeof(init), hipMemcpyHostToDevice, s);
+    m.err_clean = true;  // re-initialised in stream order
+  }
   auto& T = ctx->timing;
   if (T.enabled && he == hipSuccess) he = hipEventRecord(T.ev[0], s);
   if (m.path == FCG_PATH_STRUCTURED)
@@ -868,35 +1006,111 @@ int fcg_evaluate_device(fcg_ctx* ctx, int action, int mode, const double* d_u_co
     if (he == hipSuccess)
       he = fcg::launch_assemble(m, want_k, mode == FCG_OVERWRITE, d_K_vals, d_fint_row, s);
   }
-  if (T.enabled && he == hipSuccess) he = hipEventRecord(T.ev[2], s);
-  int32_t* errv = m.err_host;
-  if (he == hipSuccess) he = hipMemcpyAsync(errv, m.err, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, s);
+  if (T.enabled && he == hipSuccess)
+  {
+    he = hipEventRecord(T.ev[2], s);
+    T.pending = true;
+    T.path = m.path;
+  }
+  if (he == hipSuccess)
+    he = hipMemcpyAsync(m.err_host, m.err, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, s);
+  if (he == hipSuccess && ctx->async)
+  {
+    ctx->pending = true;
+    ctx->pending_stream = s;
+    return FCG_OK;  // fcg_check_error reports what the queued work finds
+  }
   if (he == hipSuccess) he = hipStreamSynchronize(s);
   if (he != hipSuccess)
   {
     m.err_clean = false;
+    ctx->pending = false;
     ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
     return FCG_ERR_DEVICE;
   }
-  m.err_clean = errv[0] == 0;  // no failing element: err still {0, INT32_MAX}
-  if (T.enabled)
+  ctx->pending = false;
+  read_timing(T);
+  return report_error(ctx, bad_ele_gid);
+}
+
+int fcg_set_async(fcg_ctx* ctx, int enable)
+{
+  if (!ctx) return FCG_ERR_ARG;
+  if (!enable && ctx->pending)
   {
-    float a = 0.f, b = 0.f;
-    (void)hipEventElapsedTime(&a, T.ev[0], T.ev[1]);
-    (void)hipEventElapsedTime(&b, T.ev[1], T.ev[2]);
-    T.ms_element = a;
-    T.ms_assemble = m.path == FCG_PATH_GENERAL ? b : 0.0;  // fused: evaluate + assembly in ms_element
+    const int rc = fcg_check_error(ctx, nullptr);
+    ctx->async = false;
+    return rc;
   }
-  if (errv[0] != 0)
+  ctx->async = enable != 0;
+  return FCG_OK;
+}
+
+int fcg_check_error(fcg_ctx* ctx, int32_t* bad_ele_gid)
+{
+  if (!ctx) return FCG_ERR_ARG;
+  if (!ctx->pending) return FCG_OK;
+  (void)hipSetDevice(ctx->device);
+  ctx->pending = false;
+  if (hipStreamSynchronize(ctx->pending_stream) != hipSuccess)
   {
-    int32_t gid = -1;
-    if (errv[1] >= 0 && errv[1] < m.n_ele)
-      (void)hipMemcpy(&gid, m.ele_gid + errv[1], sizeof(int32_t), hipMemcpyDeviceToHost);
-    if (bad_ele_gid) *bad_ele_gid = gid;
-    ctx->last_error = errv[0] == FCG_ERR_NODAL_DETJ
-                          ? "determinant of jacobian <= 0 at one node of element " + std::to_string(gid)
-                          : "singular 3x3 matrix in element " + std::to_string(gid);
-    return errv[0];
+    ctx->mesh.err_clean = false;
+    ctx->last_error = "HIP: stream failed";
+    return FCG_ERR_DEVICE;
+  }
+  return report_error(ctx, bad_ele_gid);
+}
+
+int fcg_evaluate_host(fcg_ctx* ctx, int action, int mode, const double* u_col, double* fint_row,
+    double* K_vals, int32_t* bad_ele_gid)
+{
+  if (!ctx) return FCG_ERR_ARG;
+  fcg::DeviceMesh& m = ctx->mesh;
+  const bool want_k = (action == FCG_CALC_NLNSTIFF) && K_vals;
+  if ((action != FCG_CALC_NLNSTIFF && action != FCG_CALC_INTERNALFORCE) ||
+      (mode != FCG_ACCUMULATE && mode != FCG_OVERWRITE) || (m.n_cols && !u_col) ||
+      (m.n_rows && !fint_row))
+  {
+    ctx->last_error = "invalid evaluate arguments";
+    return FCG_ERR_ARG;
+  }
+  (void)hipSetDevice(ctx->device);
+  if (ctx->pending)
+  {
+    const int rc = fcg_check_error(ctx, bad_ele_gid);
+    if (rc != FCG_OK) return rc;
+  }
+  static const char* thr = std::getenv("FCG_HOST_COPY_THREADS");
+  ctx->staging.threads = thr ? std::atoi(thr) : 8;
+  hipError_t he = hipSuccess;
+  if (!ctx->h_u && m.n_cols) he = hipMalloc(&ctx->h_u, sizeof(double) * m.n_cols);
+  if (he == hipSuccess && !ctx->h_f && m.n_rows) he = hipMalloc(&ctx->h_f, sizeof(double) * m.n_rows);
+  if (he == hipSuccess && want_k && !ctx->h_k && m.nnz) he = hipMalloc(&ctx->h_k, sizeof(double) * m.nnz);
+  const bool acc = mode == FCG_ACCUMULATE;
+  if (he == hipSuccess)
+    he = fcg::staged_copy(ctx->staging, ctx->device, ctx->h_u, u_col, sizeof(double) * m.n_cols, true);
+  if (he == hipSuccess && acc)
+    he = fcg::staged_copy(ctx->staging, ctx->device, ctx->h_f, fint_row, sizeof(double) * m.n_rows, true);
+  if (he == hipSuccess && acc && want_k)
+    he = fcg::staged_copy(ctx->staging, ctx->device, ctx->h_k, K_vals, sizeof(double) * m.nnz, true);
+  if (he != hipSuccess)
+  {
+    ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
+    return FCG_ERR_DEVICE;
+  }
+  const bool was_async = ctx->async;
+  ctx->async = false;
+  const int rc = fcg_evaluate_device(ctx, want_k ? FCG_CALC_NLNSTIFF : FCG_CALC_INTERNALFORCE, mode,
+      ctx->h_u, ctx->h_f, ctx->h_k, nullptr, bad_ele_gid);
+  ctx->async = was_async;
+  if (rc != FCG_OK) return rc;
+  he = fcg::staged_copy(ctx->staging, ctx->device, fint_row, ctx->h_f, sizeof(double) * m.n_rows, false);
+  if (he == hipSuccess && want_k)
+    he = fcg::staged_copy(ctx->staging, ctx->device, K_vals, ctx->h_k, sizeof(double) * m.nnz, false);
+  if (he != hipSuccess)
+  {
+    ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
+    return FCG_ERR_DEVICE;
   }
   return FCG_OK;
 }
@@ -904,34 +1118,7 @@ int fcg_evaluate_device(fcg_ctx* ctx, int action, int mode, const double* d_u_co
 int fcg_evaluate(fcg_ctx* ctx, int action, const double* u_col, double* fint_row, double* K_vals,
     int32_t* bad_ele_gid)
 {
-  if (!ctx) return FCG_ERR_ARG;
-  fcg::DeviceMesh& m = ctx->mesh;
-  const bool want_k = (action == FCG_CALC_NLNSTIFF) && K_vals;
-  (void)hipSetDevice(ctx->device);
-  hipError_t he = hipSuccess;
-  if (!ctx->h_u && m.n_cols) he = hipMalloc(&ctx->h_u, sizeof(double) * m.n_cols);
-  if (he == hipSuccess && !ctx->h_f && m.n_rows) he = hipMalloc(&ctx->h_f, sizeof(double) * m.n_rows);
-  if (he == hipSuccess && want_k && !ctx->h_k && m.nnz) he = hipMalloc(&ctx->h_k, sizeof(double) * m.nnz);
-  if (he == hipSuccess && m.n_cols) he = hipMemcpy(ctx->h_u, u_col, sizeof(double) * m.n_cols, hipMemcpyHostToDevice);
-  if (he == hipSuccess && m.n_rows) he = hipMemcpy(ctx->h_f, fint_row, sizeof(double) * m.n_rows, hipMemcpyHostToDevice);
-  if (he == hipSuccess && want_k && m.nnz) he = hipMemcpy(ctx->h_k, K_vals, sizeof(double) * m.nnz, hipMemcpyHostToDevice);
-  if (he != hipSuccess)
-  {
-    ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
-    return FCG_ERR_DEVICE;
-  }
-  const int rc = fcg_evaluate_device(ctx, want_k ? FCG_CALC_NLNSTIFF : FCG_CALC_INTERNALFORCE,
-      FCG_ACCUMULATE, ctx->h_u, ctx->h_f, ctx->h_k, nullptr, bad_ele_gid);
-  if (rc != FCG_OK) return rc;
-  if (m.n_rows) he = hipMemcpy(fint_row, ctx->h_f, sizeof(double) * m.n_rows, hipMemcpyDeviceToHost);
-  if (he == hipSuccess && want_k && m.nnz)
-    he = hipMemcpy(K_vals, ctx->h_k, sizeof(double) * m.nnz, hipMemcpyDeviceToHost);
-  if (he != hipSuccess)
-  {
-    ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
-    return FCG_ERR_DEVICE;
-  }
-  return FCG_OK;
+  return fcg_evaluate_host(ctx, action, FCG_ACCUMULATE, u_col, fint_row, K_vals, bad_ele_gid);
 }
 
 int fcg_set_timing(fcg_ctx* ctx, int enable)
@@ -944,6 +1131,7 @@ int fcg_set_timing(fcg_ctx* ctx, int enable)
 int fcg_get_timing(const fcg_ctx* ctx, double* ms_element, double* ms_assemble)
 {
   if (!ctx) return FCG_ERR_ARG;
+  read_timing(const_cast<fcg_ctx*>(ctx)->timing);
   if (ms_element) *ms_element = ctx->timing.ms_element;
   if (ms_assemble) *ms_assemble = ctx->timing.ms_assemble;
   return 2;

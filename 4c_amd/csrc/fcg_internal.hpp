@@ -92,9 +92,25 @@ hipError_t launch_sweep_h8_tsi(const DeviceMesh& m, const double* d_u_col, bool 
 
 struct Timing {
   bool enabled = false;
+  bool pending = false;  // events recorded, durations not read yet (async evaluate)
+  int path = 0;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
   double ms_element = 0.0, ms_assemble = 0.0;
 };
+
+// Host <-> device copies of the host-buffer entry points through pinned staging chunks: the DMA
+// of one chunk overlaps the host-side copy of the previous one (threads > 0), or one pageable
+// hipMemcpy (threads == 0).
+struct HostStaging {
+  double* pin[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  hipStream_t stream = nullptr;
+  int64_t chunk = 0;  // doubles per chunk
+  int threads = 8;
+};
+hipError_t staged_copy(HostStaging& st, int device, void* dst, const void* src, int64_t bytes,
+    bool to_device);
+void staging_free(HostStaging& st);
 
 void upload_constant_tables(int celltype);  // GP / nodal derivative tables -> __constant__
 hipError_t launch_element(const DeviceMesh& m, const double* d_u_col, bool want_k,
@@ -115,8 +131,13 @@ struct fcg_ctx {
   fcg::Timing timing;
   std::string last_error;
   int64_t device_bytes = 0;
-  // staging buffers for the host-pointer entry point
+  // device buffers of the host-pointer entry points
   double* h_u = nullptr;
   double* h_f = nullptr;
   double* h_k = nullptr;
+  fcg::HostStaging staging;
+  // deferred error check (fcg_set_async)
+  bool async = false;
+  bool pending = false;
+  hipStream_t pending_stream = nullptr;
 };

@@ -61,6 +61,28 @@ class FcgInfo(ctypes.Structure):
                 ("reserved", ctypes.c_int32)]
 
 
+class FcgImportPlan(ctypes.Structure):
+    _fields_ = [("nranks", ctypes.c_int32), ("rank", ctypes.c_int32),
+                ("n_rows", ctypes.c_int64), ("n_cols", ctypes.c_int64),
+                ("n_same", ctypes.c_int64), ("n_permute", ctypes.c_int64),
+                ("permute_from", _i32p), ("permute_to", _i32p),
+                ("send_counts", _i64p), ("send_row", _i32p),
+                ("recv_counts", _i64p), ("recv_col", _i32p)]
+
+
+class FcgSharedPlan(ctypes.Structure):
+    _fields_ = [("nranks", ctypes.c_int32), ("rank", ctypes.c_int32),
+                ("n_global", ctypes.c_int64), ("n_local", ctypes.c_int64),
+                ("n_owned", ctypes.c_int64), ("row", _i32p), ("pos", _i64p)]
+
+
+# fcg_alltoallv_fn: (send_buf, send_counts, recv_buf, recv_counts, item_bytes, user) -> int
+ALLTOALLV_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, _i64p, ctypes.c_void_p, _i64p,
+                                ctypes.c_int64, ctypes.c_void_p)
+FCG_OP_SUM, FCG_OP_MAX = 0, 1
+BOX_GHOSTED, BOX_STRICT = 0, 1
+
+
 class FcgTsiDesc(ctypes.Structure):
     _fields_ = [("abi_version", ctypes.c_int32), ("celltype", ctypes.c_int32),
                 ("device", ctypes.c_int32), ("reserved", ctypes.c_int32),
@@ -89,7 +111,13 @@ EXPORTS = ["fcg_create", "fcg_destroy", "fcg_last_error", "fcg_evaluate", "fcg_e
            "fcg_tsi_create", "fcg_tsi_destroy", "fcg_tsi_last_error", "fcg_tsi_evaluate_device",
            "fcg_tsi_evaluate_fused",
            "fcg_box_mesh_create", "fcg_box_mesh_destroy", "fcg_box_mesh_desc", "fcg_box_mesh_maps",
-           "fcg_box_mesh_counts"]
+           "fcg_box_mesh_counts", "fcg_box_mesh_create_ex", "fcg_box_mesh_owned_rows",
+           "fcg_comm_unique_id", "fcg_comm_create", "fcg_comm_destroy", "fcg_comm_allreduce",
+           "fcg_comm_alltoallv", "fcg_import_plan_build", "fcg_plan_free", "fcg_halo_create",
+           "fcg_halo_destroy", "fcg_halo_import", "fcg_halo_pack", "fcg_halo_unpack",
+           "fcg_shared_plan_build", "fcg_shared_create", "fcg_shared_destroy", "fcg_shared_reduce",
+           "fcg_shared_pack", "fcg_shared_unpack", "fcg_norm2", "fcg_set_async", "fcg_check_error",
+           "fcg_evaluate_host"]
 
 _lib = None
 FUNCT_FN = ctypes.CFUNCTYPE(ctypes.c_double, ctypes.c_int, _dp, ctypes.c_double, ctypes.c_void_p)
@@ -153,6 +181,36 @@ def lib():
     L.fcg_box_mesh_maps.argtypes = [vp, ctypes.POINTER(_i32p), ctypes.POINTER(_i32p),
                                     ctypes.POINTER(_i64p), ctypes.POINTER(_i32p)]
     L.fcg_box_mesh_counts.argtypes = [vp, _i64p, _i64p]
+    L.fcg_box_mesh_create_ex.argtypes = [ctypes.POINTER(FcgBox), ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, ctypes.POINTER(vp)]
+    L.fcg_box_mesh_owned_rows.argtypes = [vp, _i64p]
+    L.fcg_comm_unique_id.argtypes = [vp]
+    L.fcg_comm_create.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
+    L.fcg_comm_destroy.argtypes = [vp]
+    L.fcg_comm_allreduce.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_int, vp]
+    L.fcg_comm_alltoallv.argtypes = [vp, _i64p, vp, _i64p, ctypes.c_int64, vp]
+    L.fcg_import_plan_build.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64, _i32p,
+                                        ctypes.c_int64, _i32p, _i32p, ALLTOALLV_FN, vp,
+                                        ctypes.POINTER(FcgImportPlan), ctypes.POINTER(vp)]
+    L.fcg_plan_free.argtypes = [vp]
+    L.fcg_plan_free.restype = None
+    L.fcg_halo_create.argtypes = [ctypes.POINTER(FcgImportPlan), ctypes.c_int, ctypes.POINTER(vp)]
+    L.fcg_halo_destroy.argtypes = [vp]
+    L.fcg_halo_import.argtypes = [vp, vp, vp, vp, vp]
+    L.fcg_halo_pack.argtypes = [vp, vp, vp, vp, vp]
+    L.fcg_halo_unpack.argtypes = [vp, vp, vp, vp]
+    L.fcg_shared_plan_build.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64, _i32p,
+                                        ctypes.c_int64, _i32p, _i32p, ALLTOALLV_FN, vp,
+                                        ctypes.POINTER(FcgSharedPlan), ctypes.POINTER(vp)]
+    L.fcg_shared_create.argtypes = [ctypes.POINTER(FcgSharedPlan), ctypes.c_int, ctypes.POINTER(vp)]
+    L.fcg_shared_destroy.argtypes = [vp]
+    L.fcg_shared_reduce.argtypes = [vp, vp, vp, vp]
+    L.fcg_shared_pack.argtypes = [vp, vp, vp, vp]
+    L.fcg_shared_unpack.argtypes = [vp, vp, vp, vp]
+    L.fcg_norm2.argtypes = [vp, vp, ctypes.c_int64, vp, _dp]
+    L.fcg_set_async.argtypes = [vp, ctypes.c_int]
+    L.fcg_check_error.argtypes = [vp, _i32p]
+    L.fcg_evaluate_host.argtypes = [vp, ctypes.c_int, ctypes.c_int, _dp, _dp, _dp, _i32p]
     L.fcg_graph_build_device.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64, vp,
                                          ctypes.c_int64, vp, vp, ctypes.c_int64, vp, vp,
                                          ctypes.c_int64, _i64p, vp]
@@ -168,13 +226,14 @@ def lib():
     return L
 
 
-def _torch_stream(stream):
+def _torch_stream(stream, device=None):
     """The HIP stream of a library call on torch tensors: the given torch stream, else torch's
-    current stream -- never the context's own (non-blocking) stream, which is not ordered with
-    the torch work that produced or consumes the buffers."""
+    current stream of `device` (the context's device, not whichever device is current) -- never
+    the context's own stream, which is not ordered with the torch work that produced or consumes
+    the buffers."""
     import torch
     if stream is None:
-        stream = torch.cuda.current_stream()
+        stream = torch.cuda.current_stream(device)
     return ctypes.c_void_p(stream.cuda_stream)
 
 
@@ -341,7 +400,9 @@ class BoxMesh:
 
     def __init__(self, celltype, interval, lower=(0.0, 0.0, 0.0), upper=(1.0, 1.0, 1.0),
                  rotation=(0.0, 0.0, 0.0), first_node_gid=0, jitter=0.0, seed=20251015,
-                 rank=0, nranks=1):
+                 rank=0, nranks=1, strict=False):
+        """strict=True: FCG_BOX_STRICT (row elements only, extended rows for the non-owned
+        nodes they touch after the n_owned_rows owned rows)."""
         L = lib()
         box = FcgBox()
         box.celltype = celltype
@@ -357,8 +418,10 @@ class BoxMesh:
         self.celltype = celltype
         self.npe = 8 if celltype == HEX8 else 27
         self.rank, self.nranks = rank, nranks
+        self.strict = bool(strict)
         h = ctypes.c_void_p()
-        rc = L.fcg_box_mesh_create(ctypes.byref(box), rank, nranks, ctypes.byref(h))
+        rc = L.fcg_box_mesh_create_ex(ctypes.byref(box), rank, nranks,
+                                      BOX_STRICT if strict else BOX_GHOSTED, ctypes.byref(h))
         if rc != 0:
             raise FcgError(rc, "fcg_box_mesh_create failed")
         self._h = h
@@ -390,6 +453,9 @@ class BoxMesh:
         ng_, nr_ = ctypes.c_int64(), ctypes.c_int64()
         L.fcg_box_mesh_counts(h, ctypes.byref(ng_), ctypes.byref(nr_))
         self.n_ele_global, self.n_ele_row = ng_.value, nr_.value
+        no_ = ctypes.c_int64()
+        L.fcg_box_mesh_owned_rows(h, ctypes.byref(no_))
+        self.n_owned_rows = no_.value
         # the builder's arrays are copied; release the native mesh
         L.fcg_box_mesh_destroy(h)
         self._h = None
@@ -479,10 +545,32 @@ class Evaluator:
         if rc != 0:
             self._raise(rc, bad.value)
 
+    def evaluate_host(self, action, mode, u_col, fint_row, K_vals=None):
+        """fcg_evaluate_host: host (numpy) buffers; mode OVERWRITE fuses the caller's zero()."""
+        bad = ctypes.c_int32(-1)
+        rc = lib().fcg_evaluate_host(self._h, action, mode, _np_ptr(u_col, _dp),
+                                     _np_ptr(fint_row, _dp),
+                                     _np_ptr(K_vals, _dp) if K_vals is not None else None,
+                                     ctypes.byref(bad))
+        if rc != 0:
+            self._raise(rc, bad.value)
+
+    def set_async(self, enable):
+        """fcg_set_async: evaluate_device returns once queued; check_error reports failures."""
+        rc = lib().fcg_set_async(self._h, 1 if enable else 0)
+        if rc != 0:
+            self._raise(rc, -1)
+
+    def check_error(self):
+        bad = ctypes.c_int32(-1)
+        rc = lib().fcg_check_error(self._h, ctypes.byref(bad))
+        if rc != 0:
+            self._raise(rc, bad.value)
+
     def evaluate_device(self, action, mode, u_col, fint_row, K_vals=None, stream=None):
         """Device-resident path; tensors are float64 torch tensors on this device."""
         bad = ctypes.c_int32(-1)
-        s = _torch_stream(stream)
+        s = _torch_stream(stream, self.device)
         rc = lib().fcg_evaluate_device(self._h, action, mode, _tensor_ptr(u_col),
                                        _tensor_ptr(fint_row), _tensor_ptr(K_vals), s,
                                        ctypes.byref(bad))
@@ -490,7 +578,7 @@ class Evaluator:
             self._raise(rc, bad.value)
 
     def _stream(self, stream):
-        return _torch_stream(stream)
+        return _torch_stream(stream, self.device)
 
     def spmv(self, K_vals, x_col, y_row, stream=None):
         rc = lib().fcg_spmv(self._h, _tensor_ptr(K_vals), _tensor_ptr(x_col), _tensor_ptr(y_row),
@@ -615,7 +703,7 @@ class TsiEvaluator:
                         Kst=None, fT=None, Ktt=None, Kts=None, stream=None):
         """Tensors: float64 on this device (v_col / T_col in the structural / thermo column maps)."""
         bad = ctypes.c_int32(-1)
-        s = _torch_stream(stream)
+        s = _torch_stream(stream, self.device)
         rc = lib().fcg_tsi_evaluate_device(self._h, parts, mode, _tensor_ptr(v_col),
                                            _tensor_ptr(T_col), float(timefac), float(timefac_d),
                                            _tensor_ptr(fs), _tensor_ptr(Kst), _tensor_ptr(fT),
@@ -628,7 +716,7 @@ class TsiEvaluator:
         """fcg_tsi_evaluate_fused: the whole monolithic tangent (K_SS, k_ST, k_TS, k_TT) and both
         residuals in one sweep; `struct_ev` is the structured linear StVK Evaluator of the mesh."""
         bad = ctypes.c_int32(-1)
-        s = _torch_stream(stream)
+        s = _torch_stream(stream, self.device)
         rc = lib().fcg_tsi_evaluate_fused(struct_ev._h, self._h, mode, _tensor_ptr(u_col),
                                           _tensor_ptr(v_col), _tensor_ptr(T_col), float(timefac),
                                           float(timefac_d), _tensor_ptr(fs), _tensor_ptr(Kss),
@@ -646,7 +734,7 @@ def graph_build_device(celltype, ele_nodes, node_dof_col, node_dof_row, n_rows, 
     dev = torch.device("cuda", device)
     rowptr = torch.empty(int(n_rows) + 1, dtype=torch.int64, device=dev)
     nnz = ctypes.c_int64(0)
-    s = _torch_stream(stream)
+    s = _torch_stream(stream, device)
     args = (device, celltype, int(ele_nodes.numel() // (8 if celltype == HEX8 else 27)),
             _tensor_ptr(ele_nodes), int(node_dof_col.numel()), _tensor_ptr(node_dof_col),
             _tensor_ptr(node_dof_row), int(n_rows), _tensor_ptr(rowptr))

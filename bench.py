@@ -101,15 +101,53 @@ def cpu_baseline(n, kinem, threads):
         model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
     except Exception:
         model = platform.processor()
+    topo = cpu_topology()
+    phys = topo.get("physical_cores") or threads
     return {
         "value": mesh.n_ele / tn, "unit": "element-evaluations/s", "cores": threads,
         "kind": "port",
         "sample": f"one struct_calc_nlnstiff evaluation of the full {n}^3 hex8 mesh "
-                  f"({mesh.n_ele} elements, K+r assembled), {threads} threads as ranks; "
-                  f"single-core {small.n_ele / t1:.4g} elem/s on {small.n_ele} elements",
+                  f"({mesh.n_ele} elements, K+r assembled), {threads} threads as ranks (the CPU "
+                  f"share granted to this process); single-core {small.n_ele / t1:.4g} elem/s on "
+                  f"{small.n_ele} elements",
         "wall_s": tn, "single_core_value": small.n_ele / t1, "cpu_model": model,
+        "topology": topo,
+        # not measured: the single-core rate times every physical core of the host (what a full
+        # MPI run of the reference could reach at perfect scaling)
+        "all_physical_cores_extrapolated": small.n_ele / t1 * phys,
         "compiler": "gcc -O3 -march=native -fopenmp",
     }
+
+
+def cpu_threads(requested):
+    """Threads of the CPU baseline: the CPU share this process may use (the affinity mask; on the
+    GPU box the harness grants 16 CPUs per GPU and exports OMP_NUM_THREADS accordingly)."""
+    if requested > 0:
+        return requested
+    share = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(share, omp) if omp > 0 else share)
+
+
+def cpu_topology():
+    """nproc, physical cores and SMT state of the host (lscpu semantics from /sys)."""
+    out = {"nproc_affinity": len(os.sched_getaffinity(0)), "logical_cpus": os.cpu_count()}
+    try:
+        cores = set()
+        base = "/sys/devices/system/cpu"
+        for d in os.listdir(base):
+            if d.startswith("cpu") and d[3:].isdigit():
+                try:
+                    pk = open(f"{base}/{d}/topology/physical_package_id").read().strip()
+                    co = open(f"{base}/{d}/topology/core_id").read().strip()
+                    cores.add((pk, co))
+                except OSError:
+                    pass
+        out["physical_cores"] = len(cores) or None
+        out["smt_active"] = open(f"{base}/smt/active").read().strip() == "1"
+    except OSError:
+        pass
+    return out
 
 
 def newton_secondary(n, timeout_s=900):
@@ -255,8 +293,7 @@ def tsi_secondary(dev, rank, world, steps, n=126):
         except Exception as e:
             err = e
     t = time.perf_counter() - t0
-    res = torch.tensor([t, 1.0 if err is not None else 0.0], dtype=torch.float64,
-                       device=dev if world == 1 or dist.get_backend() == "nccl" else "cpu")
+    res = torch.tensor([t, 1.0 if err is not None else 0.0], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(res, op=dist.ReduceOp.MAX)
     if err is not None or res[1].item() != 0.0:
@@ -283,6 +320,123 @@ def tsi_secondary(dev, rank, world, steps, n=126):
     return out
 
 
+def _ctl_max(x, world):
+    """Max over ranks of a host float (the control plane: gloo on the CPU)."""
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.item()
+
+
+def _bcast_id(world):
+    """rank 0's RCCL id to every rank over the gloo control plane."""
+    def f(b):
+        box = [b]
+        if world > 1:
+            dist.broadcast_object_list(box, src=0)
+        return box[0]
+    return f
+
+
+def optionb_secondary(dev, rank, world, n, steps, staged):
+    """SURVEY §8e option B, north_star's "RCCL all-reduce over xGMI of the shared-DOF residual":
+    strict element partition (every rank only its GridGenerator box, no ghost layer; FCG_BOX_STRICT)
+    -> set_state import of the interface displacements -> struct_calc_internalforce of the rank's
+    elements into owned + extended rows -> fcg_shared_reduce (ncclAllReduce of the compact
+    interface buffer, positions by (owner, GID)) -> the residual norm over the ranks."""
+    comm = None
+    try:
+        iv = weak_interval(n, world)
+        m = fcg.BoxMesh(fcg.HEX8, iv, upper=(iv[0] / n, iv[1] / n, iv[2] / n), jitter=0.1,
+                        seed=20251015, rank=rank, nranks=world, strict=True)
+        comm = None if staged else halo.Comm(rank, world, dev.index, _bcast_id(world))
+        xchg = halo.gloo_exchange() if staged else comm.exchange
+        n_own = m.n_owned_rows
+        plan = halo.ImportPlan(rank, world, m.row_gid[:n_own], m.col_gid, halo.col_owner_of(m), xchg)
+        h = halo.Halo(plan, dev.index)
+        sp = halo.SharedPlan.of_mesh(m, xchg)
+        sh = halo.Shared(sp, dev.index)
+        ev = fcg.Evaluator(m, kinematics=fcg.LINEAR, youngs=210.0, poisson=0.3, device=dev.index)
+        ev.set_async(True)
+        u_h = m.u_col(1e-3)
+        u_row = torch.from_numpy(np.ascontiguousarray(u_h[:n_own])).to(dev)  # row LID == col LID
+        u_col = torch.zeros(m.n_cols, dtype=torch.float64, device=dev)
+        f = torch.zeros(m.n_rows, dtype=torch.float64, device=dev)
+        stream = torch.cuda.current_stream(dev)
+
+        def step():
+            if staged:
+                h.import_staged(u_row, u_col, stream)
+            else:
+                h.import_(comm, u_row, u_col, stream)
+            ev.evaluate_device(fcg.CALC_INTERNALFORCE, fcg.OVERWRITE, u_col, f, stream=stream)
+            if staged:
+                sh.reduce_staged(f, stream)
+                nrm = halo.residual_norm(f[:n_own], None, stream)
+            else:
+                sh.reduce(comm, f, stream)
+                nrm = halo.residual_norm(f[:n_own], comm, stream)
+            ev.check_error()
+            return nrm
+
+        for _ in range(5):
+            step()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            nrm = step()
+        torch.cuda.synchronize(dev)
+        wall = _ctl_max((time.perf_counter() - t0) / steps, world)
+        out = {"workload": f"hex8-linear-{n}^3-per-gpu strict partition, internal force + shared-DOF "
+                           f"all-reduce (option B)",
+               "baseline_config": "BASELINE.json configs[3] (RCCL shared-DOF all-reduce)",
+               "value": m.n_ele_global / wall, "unit": "element-evaluations/s (residual only)",
+               "ms_per_step": 1e3 * wall, "elements_global": m.n_ele_global,
+               "elements_evaluated_rank0": m.n_ele, "interface_dofs_global": sp.n_global,
+               "allreduce_bytes": 8 * sp.n_global, "residual_norm": nrm,
+               "transport": "host-staged gloo" if staged else "RCCL (fcg_halo_import + fcg_shared_reduce)"}
+        for o in (sh, h, ev):
+            o.close()
+        return out
+    except Exception as e:  # report, never hide
+        return {"workload": "option-B shared-DOF all-reduce", "error": repr(e)}
+    finally:
+        if comm is not None:
+            comm.close()
+
+
+def host_secondary(dev, n, steps):
+    """The 4C drop-in on host (Epetra-shaped) storage: fcg_evaluate_host with u, f and K in host
+    memory, PCIe transfers included (pinned staging chunks, DMA overlapped with the host copy).
+    OVERWRITE = the caller's SparseMatrix::zero() fused (K and f only written back); ACCUMULATE =
+    fcg_evaluate's += (K and f also uploaded)."""
+    try:
+        mesh = fcg.BoxMesh(fcg.HEX8, (n, n, n), jitter=0.1, seed=20251015)
+        ev = fcg.Evaluator(mesh, kinematics=fcg.LINEAR, youngs=210.0, poisson=0.3, device=dev.index)
+        u = mesh.u_col(1e-3)
+        K = np.zeros(mesh.nnz)
+        f = np.zeros(mesh.n_rows)
+        out = {"workload": f"hex8-linear-{n}^3 on host buffers (fcg_evaluate_host, PCIe-inclusive)",
+               "baseline_config": "BASELINE.json configs[1] through the 4C host boundary",
+               "unit": "element-evaluations/s", "K_bytes": 8 * mesh.nnz}
+        for name, mode in (("overwrite", fcg.OVERWRITE), ("accumulate", fcg.ACCUMULATE)):
+            ev.evaluate_host(fcg.CALC_NLNSTIFF, mode, u, f, K)  # first call: staging buffers
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                ev.evaluate_host(fcg.CALC_NLNSTIFF, mode, u, f, K)
+            wall = (time.perf_counter() - t0) / steps
+            out[name] = {"value": mesh.n_ele / wall, "ms_per_step": 1e3 * wall,
+                         "pcie_gbs": (8 * mesh.nnz * (1 if mode == fcg.OVERWRITE else 2)) / wall / 1e9}
+        out["value"] = out["overwrite"]["value"]
+        ev.close()
+        return out
+    except Exception as e:  # report, never hide
+        return {"workload": "host-buffer drop-in", "error": repr(e)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -291,28 +445,33 @@ def main():
     ap.add_argument("--elems-per-dir", dest="n", type=int, default=100,
                     help="elements per direction per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0: the CPU share of this process)")
     ap.add_argument("--no-hex27", action="store_true", help="skip the hex27 (config 3) line")
     ap.add_argument("--no-tsi", action="store_true", help="skip the TSI (config 5) line")
     ap.add_argument("--hex27-n", type=int, default=40)
     ap.add_argument("--no-newton", action="store_true", help="skip the config-3 Newton line")
     ap.add_argument("--newton-n", type=int, default=100)
+    ap.add_argument("--no-optionb", action="store_true", help="skip the option-B (shared-DOF) line")
+    ap.add_argument("--no-host", action="store_true", help="skip the host-buffer drop-in line")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # FCG_DIST_BACKEND=gloo: rehearsal of the multi-rank flow with all ranks on the visible
-    # GPU(s) and the halo staged through the host; the real runs use RCCL ("nccl")
-    backend = os.environ.get("FCG_DIST_BACKEND", "nccl")
-    local = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
+    # data path: the library's RCCL communicator (halo import, norms); the control plane (RCCL id,
+    # barriers, max over ranks) is gloo on the CPU.  FCG_DIST_BACKEND=gloo rehearses the multi-rank
+    # flow with several ranks on one GPU (RCCL refuses that): halo staged through the host.
+    staged = os.environ.get("FCG_DIST_BACKEND", "rccl") == "gloo"
+    local = local % max(1, torch.cuda.device_count()) if staged else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    comm = None
     if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
+        os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+        dist.init_process_group("gloo")
+        if not staged:
+            comm = halo.Comm(rank, world, local, _bcast_id(world))
 
     iv = weak_interval(args.n, world)
     t_setup = time.perf_counter()
@@ -330,16 +489,31 @@ def main():
     K = torch.zeros(mesh.nnz, dtype=torch.float64, device=dev)
     imp = None
     if world > 1:
-        imp = halo.HaloImport(mesh.row_gid, mesh.col_gid, halo.col_owner_of(mesh), rank, world, dev)
+        plan = halo.ImportPlan(rank, world, mesh.row_gid, mesh.col_gid, halo.col_owner_of(mesh),
+                               halo.gloo_exchange() if staged else comm.exchange)
+        imp = halo.Halo(plan, local)
     else:
         u_col.copy_(torch.from_numpy(u_col_h).to(dev))
     stream = torch.cuda.current_stream(dev)
+    # evaluate returns once queued; 4C's throws are collected after the norm (one drain per step)
+    ev.set_async(True)
 
     def step():
         if imp is not None:
-            imp(u_row, u_col)
+            if staged:
+                imp.import_staged(u_row, u_col, stream)
+            else:
+                imp.import_(comm, u_row, u_col, stream)
         ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u_col, f, K, stream=stream)
-        return halo.residual_norm(f)
+        if staged and world > 1:
+            loc = halo.residual_norm(f, None, stream)
+            t = torch.tensor([loc * loc], dtype=torch.float64)
+            dist.all_reduce(t)
+            nrm = float(np.sqrt(t.item()))
+        else:
+            nrm = halo.residual_norm(f, comm, stream)
+        ev.check_error()
+        return nrm
 
     # SURVEY §8d asks for the spec peaks re-measured on the box; measured here, on every rank's
     # GPU before its warm-up, so that the timed steps start on a GPU already at its working
@@ -356,7 +530,7 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        nrm = step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -372,10 +546,7 @@ def main():
         t_as.append(b)
     torch.cuda.synchronize(dev)
     ev.set_timing(False)
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed = elapsed.item()
+    elapsed = _ctl_max(t1 - t0, world)
     ms_step = 1e3 * elapsed / args.steps
     n_ele_global = mesh.n_ele_global
     value = n_ele_global / (elapsed / args.steps)
@@ -420,36 +591,41 @@ def main():
             "nnz_rank0": mesh.nnz,
             "material": "StVenantKirchhoff E=210 nu=0.3",
             "assembly": "zero+assemble fused (FCG_OVERWRITE), owned rows, no atomics",
-            "parallelism": f"element partition x{world} (GridGenerator box split, ghost layer, "
-                           f"RCCL halo all-to-all)" if world > 1 else "single GPU",
+            "parallelism": (f"element partition x{world} (GridGenerator box split, ghost layer; "
+                            f"set_state import by fcg_halo_import = RCCL grouped send/recv, "
+                            f"residual norm by fcg_norm2 = RCCL all-reduce)" if not staged else
+                            f"element partition x{world}, host-staged gloo rehearsal")
+                           if world > 1 else "single GPU",
             "setup_s_rank0": t_setup,
         },
-        # the K + r assembly is FP64-compute bound (41.4 kflop vs 2,069 B per hex8
-        # element = 20 flop/B against a ridge of 9.8 flop/B), so the bounding roofline is the FP64
-        # (vector = matrix) peak; the HBM fraction of the same launch is reported beside it.
+        # The bounding roofline of the launch: SURVEY.md §8d prices the K + r assembly FP64-bound
+        # (41.4 kflop vs 2,069 B per hex8 element), but the kernel runs the isotropic (lambda, mu)
+        # contraction, a fraction of those flops, on the VALU (no MFMA), and its floor in practice
+        # is writing K once: so the reported bound is HBM (algorithmic bytes / kernel time vs the
+        # 8 TB/s spec), and the FP64 fraction by SURVEY's flop count is kept beside it.
         "roofline": {
-            "bound": "mfma",
+            "bound": "hbm",
             "kernel": ("sweep_h8_kernel (structured row-block sweep, one evaluate)"
                        if ev.info.path == fcg.PATH_STRUCTURED
                        else "element_kernel + assemble_kernel (one evaluate)"),
-            "achieved": flops,
-            "peak": FP64_PEAK_TFS,
-            "unit": "TFLOP/s",
-            "frac": flops / FP64_PEAK_TFS,
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
-            "alg_flop_per_element": ALG_FLOP_PER_ELE,
             "alg_bytes_per_element": ALG_BYTES_PER_ELE,
-            "hbm_achieved_gbs": achieved,
-            "hbm_peak_gbs": HBM_PEAK_GBS,
-            "hbm_frac": achieved / HBM_PEAK_GBS,
+            "elements_per_launch": n_row_ele,
             "ms_element_kernel": ms_el,
             "ms_assemble_kernel": ms_as,
+            "fp64_valu": {"achieved_tflops_by_survey_count": flops, "peak_tflops": FP64_PEAK_TFS,
+                          "frac": flops / FP64_PEAK_TFS, "alg_flop_per_element": ALG_FLOP_PER_ELE,
+                          "note": "SURVEY §8d flop count; the isotropic contraction executes fewer"},
         },
         "assembly_wall_ms": ms_step,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            out["cpu_baseline"] = cpu_baseline(args.n, fcg.LINEAR, args.cpu_threads)
+            out["cpu_baseline"] = cpu_baseline(args.n, fcg.LINEAR, cpu_threads(args.cpu_threads))
         except Exception as e:  # report, never hide
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
     # the spec peaks re-measured on this box (STREAM triad, FP64 VALU, FP64 MFMA);
@@ -462,21 +638,30 @@ def main():
             fp64_meas = max(valu, mfma)
             out["roofline"]["measured_peaks"] = {
                 "hbm_triad_gbs": triad, "fp64_valu_tflops": valu, "fp64_mfma_tflops": mfma,
-                "frac_vs_measured_fp64": flops / fp64_meas if fp64_meas > 0 else None,
-                "hbm_frac_vs_triad": achieved / triad if triad > 0 else None}
+                "hbm_frac_vs_triad": achieved / triad if triad > 0 else None,
+                "fp64_frac_vs_measured": flops / fp64_meas if fp64_meas > 0 else None}
         except Exception as e:  # report, never hide
             out["roofline"]["measured_peaks"] = {"error": repr(e)}
+    out["residual_norm"] = nrm
     # the other BASELINE configs' kernels, measured after the primary line's buffers are freed
+    if imp is not None:
+        imp.close()
     del K, f, u_col, u_row, imp
     ev.close()
     torch.cuda.empty_cache()
     secondary = []
+    if not args.no_optionb:
+        secondary.append(optionb_secondary(dev, rank, world, args.n, max(3, min(args.steps, 10)),
+                                           staged))
+        torch.cuda.empty_cache()
     if not args.no_tsi:
         secondary.append(tsi_secondary(dev, rank, world, max(3, min(args.steps, 10))))
+    if rank == 0 and world == 1 and not args.no_host:
+        secondary.append(host_secondary(dev, args.n, 3))
     if rank == 0 and world == 1 and not args.no_hex27:
         try:
             secondary.append(hex27_secondary(dev, args.hex27_n, max(3, min(args.steps, 10)),
-                                             args.cpu_threads, not args.no_cpu_baseline))
+                                             cpu_threads(args.cpu_threads), not args.no_cpu_baseline))
         except Exception as e:  # report, never hide
             secondary.append({"workload": "hex27-totlag", "error": repr(e)})
     if rank == 0 and world == 1 and not args.no_newton:
@@ -489,6 +674,8 @@ def main():
         out["secondary"] = secondary
     if rank == 0:
         print(json.dumps(out))
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -355,6 +355,136 @@ int fcg_box_mesh_maps(const fcg_box_mesh* m, const int32_t** row_gid, const int3
     const int64_t** node_gid, const int32_t** node_owner);
 /* Total number of elements (all ranks) and owned (row) elements of this rank. */
 int fcg_box_mesh_counts(const fcg_box_mesh* m, int64_t* n_ele_global, int64_t* n_ele_row);
+/* fcg_box_mesh_create with options.  FCG_BOX_STRICT: strict element partition (SURVEY §8e option
+ * B): the rank holds only its row elements (no ghost layer); every node those elements touch gets a
+ * row -- the owned DOF rows first (LIDs [0, n_owned_rows), as without the flag), then one extended
+ * row triple per touched node owned by another rank, so the row map equals the column map.  The
+ * extended rows collect the rank's partial sums for the interface DOFs, which fcg_shared_reduce
+ * completes.  fcg_box_mesh_maps' row_gid then lists the extended rows' GIDs after the owned ones. */
+enum fcg_box_flags { FCG_BOX_GHOSTED = 0, FCG_BOX_STRICT = 1 };
+int fcg_box_mesh_create_ex(const fcg_box* box, int rank, int nranks, int flags, fcg_box_mesh** out);
+/* Owned DOF rows of the rank (= n_rows without FCG_BOX_STRICT). */
+int fcg_box_mesh_owned_rows(const fcg_box_mesh* m, int64_t* n_owned_rows);
+
+/* ------------------------------------------------------------------------------------------
+ * Multi-GPU: one rank per GPU, elements partitioned like GridGenerator's box split.
+ * The collectives on 4C's path map onto RCCL over xGMI:
+ *   Discretization::set_state's row -> column Epetra_Import (4C_fem_discretization.cpp:542-548)
+ *       -> fcg_halo_import: grouped ncclSend / ncclRecv of the ghost DOFs with the neighbours;
+ *   Core::Communication::sum_all (4C_comm_mpi_utils.hpp:294-306) on the shared-DOF residual of a
+ *       strict element partition -> fcg_shared_reduce: ncclAllReduce of a compact interface buffer;
+ *   the NOX residual norm (Epetra Norm2 -> MPI_Allreduce) -> fcg_norm2.
+ * Plans are built on the host from the maps a 4C rank holds, with one host exchange callback
+ * (fcg_alltoallv_fn: an MPI_Alltoallv wrapper in 4C, fcg_comm_alltoallv over RCCL); a host that
+ * moves the bytes itself (MPI, host-staged) uses the pack / unpack halves instead of the RCCL
+ * entry points.  All device calls are asynchronous on `stream` unless stated.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct fcg_comm fcg_comm;
+#define FCG_COMM_ID_BYTES 128
+enum fcg_op { FCG_OP_SUM = 0, FCG_OP_MAX = 1 };
+/* Rank 0 makes the id (ncclGetUniqueId); the host broadcasts its FCG_COMM_ID_BYTES bytes. */
+int fcg_comm_unique_id(void* id);
+/* Collective over nranks: one RCCL communicator per rank, on HIP device `device`. */
+int fcg_comm_create(const void* id, int nranks, int rank, int device, fcg_comm** out);
+int fcg_comm_destroy(fcg_comm* comm);
+/* In-place all-reduce of n doubles in device memory (ncclAllReduce). */
+int fcg_comm_allreduce(fcg_comm* comm, double* d_buf, int64_t n, int op, void* stream);
+
+/* Host exchange with MPI_Alltoallv semantics: this rank sends send_counts[p] items of item_bytes
+ * bytes to every rank p (packed in rank order in send_buf) and receives recv_counts[p] items from
+ * every p (packed in rank order in recv_buf).  Returns 0 on success. */
+typedef int (*fcg_alltoallv_fn)(const void* send_buf, const int64_t* send_counts, void* recv_buf,
+    const int64_t* recv_counts, int64_t item_bytes, void* user);
+/* An fcg_alltoallv_fn over RCCL (user = the fcg_comm*); host buffers, blocking. */
+int fcg_comm_alltoallv(const void* send_buf, const int64_t* send_counts, void* recv_buf,
+    const int64_t* recv_counts, int64_t item_bytes, void* comm);
+
+/* The row -> column import of one rank (what Epetra_Import(colmap, rowmap) holds: NumSameIDs,
+ * PermuteFromLIDs / PermuteToLIDs, ExportLIDs / ExportPIDs, RemoteLIDs), peers in rank order. */
+typedef struct fcg_import_plan {
+  int32_t nranks, rank;
+  int64_t n_rows, n_cols;
+  int64_t n_same;               /* columns [0, n_same) take rows [0, n_same) */
+  int64_t n_permute;
+  const int32_t* permute_from;  /* [n_permute] row LIDs */
+  const int32_t* permute_to;    /* [n_permute] column LIDs */
+  const int64_t* send_counts;   /* [nranks] values this rank sends to every peer */
+  const int32_t* send_row;      /* [sum send_counts] row LIDs, grouped by peer in rank order */
+  const int64_t* recv_counts;   /* [nranks] values received from every peer */
+  const int32_t* recv_col;      /* [sum recv_counts] column LIDs, grouped by peer in rank order */
+} fcg_import_plan;
+/* Builds the plan from the rank's maps (collective, two exchanges through xchg): row_gid [n_rows]
+ * owned DOF GIDs; col_gid [n_cols] column DOF GIDs with their owners col_owner [n_cols] (4C:
+ * node->owner()).  *out points into *storage, released by fcg_plan_free. */
+int fcg_import_plan_build(int rank, int nranks, int64_t n_rows, const int32_t* row_gid,
+    int64_t n_cols, const int32_t* col_gid, const int32_t* col_owner, fcg_alltoallv_fn xchg,
+    void* user, fcg_import_plan* out, void** storage);
+void fcg_plan_free(void* storage);
+
+typedef struct fcg_halo fcg_halo;
+/* Device copy of an import plan (the plan's arrays are copied). */
+int fcg_halo_create(const fcg_import_plan* plan, int device, fcg_halo** out);
+int fcg_halo_destroy(fcg_halo* h);
+/* set_state: d_u_col = import of d_u_row, the ghost values over RCCL (grouped send / recv; peers
+ * whose ghost columns are contiguous receive straight into d_u_col). */
+int fcg_halo_import(fcg_halo* h, fcg_comm* comm, const double* d_u_row, double* d_u_col,
+    void* stream);
+/* Host-transport halves: pack copies the owned columns and writes the values every peer needs into
+ * d_send [sum send_counts] (plan order); after the host moved d_send to the peers' d_recv
+ * [sum recv_counts], unpack scatters d_recv into the ghost columns. */
+int fcg_halo_pack(fcg_halo* h, const double* d_u_row, double* d_u_col, double* d_send, void* stream);
+int fcg_halo_unpack(fcg_halo* h, const double* d_recv, double* d_u_col, void* stream);
+
+/* Shared-DOF reduction of a strict element partition (FCG_BOX_STRICT layout: owned rows
+ * [0, n_owned), extended rows n_owned + k for the non-owned DOFs ext_gid[k] the rank's elements
+ * touch, owned by ext_owner[k]).  The interface = every DOF some rank holds as an extended row;
+ * it is numbered globally by (owner rank, GID), so all ranks share one all-reduce buffer of
+ * n_global doubles. */
+typedef struct fcg_shared_plan {
+  int32_t nranks, rank;
+  int64_t n_global;             /* interface DOFs over all ranks (all-reduce length) */
+  int64_t n_local;              /* interface entries of this rank */
+  int64_t n_owned;              /* the first n_owned entries are owned rows: they get the sums */
+  const int32_t* row;           /* [n_local] row LIDs (owned, then extended) */
+  const int64_t* pos;           /* [n_local] position in the all-reduce buffer */
+} fcg_shared_plan;
+int fcg_shared_plan_build(int rank, int nranks, int64_t n_owned_rows, const int32_t* owned_gid,
+    int64_t n_ext_rows, const int32_t* ext_gid, const int32_t* ext_owner, fcg_alltoallv_fn xchg,
+    void* user, fcg_shared_plan* out, void** storage);
+
+typedef struct fcg_shared fcg_shared;
+int fcg_shared_create(const fcg_shared_plan* plan, int device, fcg_shared** out);
+int fcg_shared_destroy(fcg_shared* s);
+/* d_f [n_owned_rows + n_ext_rows] holds this rank's partial sums (an FCG_CALC_INTERNALFORCE
+ * evaluate of its row elements); afterwards the owned interface rows hold the global sums
+ * (pack -> ncclAllReduce(sum) -> unpack).  Rows away from the interface are already complete. */
+int fcg_shared_reduce(fcg_shared* s, fcg_comm* comm, double* d_f, void* stream);
+/* Host-transport halves: d_buf [n_global] = zero + this rank's interface partials; the host sums
+ * d_buf over the ranks (MPI_Allreduce); unpack writes the sums into the owned interface rows. */
+int fcg_shared_pack(fcg_shared* s, const double* d_f, double* d_buf, void* stream);
+int fcg_shared_unpack(fcg_shared* s, const double* d_buf, double* d_f, void* stream);
+
+/* ||x||_2 over all ranks (comm may be NULL: this rank only); fixed-order partial sums, blocking. */
+int fcg_norm2(fcg_comm* comm, const double* d_x, int64_t n, void* stream, double* out);
+
+/* ------------------------------------------------------------------------------------------
+ * Deferred error check.  With fcg_set_async(ctx, 1), fcg_evaluate_device returns once the work is
+ * queued on the stream (no drain, no host round trip per call); 4C's throws (FCG_ERR_NODAL_DETJ,
+ * FCG_ERR_SINGULAR) are then reported by fcg_check_error, which waits for the queued evaluates
+ * and returns the first failure since the last check (sticky until checked).
+ * ---------------------------------------------------------------------------------------- */
+int fcg_set_async(fcg_ctx* ctx, int enable);
+int fcg_check_error(fcg_ctx* ctx, int32_t* bad_ele_gid);
+
+/* ------------------------------------------------------------------------------------------
+ * Host-buffer evaluate with the matrix lifecycle of the caller: mode FCG_OVERWRITE fuses the
+ * caller's SparseMatrix::zero() (4C re-creates the values from the saved graph right before the
+ * evaluate, 4C_linalg_sparsematrix.cpp:353-378, 4C_structure_new_model_evaluator_structure.cpp:
+ * 143-151): K_vals and fint_row are only written, never read, which halves the PCIe traffic.
+ * FCG_ACCUMULATE is fcg_evaluate (+=).  Blocking.
+ * ---------------------------------------------------------------------------------------- */
+int fcg_evaluate_host(fcg_ctx* ctx, int action, int mode, const double* u_col, double* fint_row,
+    double* K_vals, int32_t* bad_ele_gid);
 
 #ifdef __cplusplus
 }

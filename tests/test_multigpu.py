@@ -1,0 +1,246 @@
+"""GPU tests of the multi-GPU data path through the C ABI.
+
+RCCL refuses two ranks on one device, so on a one-GPU box:
+* the RCCL entry points run on a one-rank communicator: fcg_halo_import with an explicit plan
+  whose peer is the rank itself (grouped ncclSend / ncclRecv loopback, contiguous and scattered
+  ghost blocks), fcg_comm_allreduce, fcg_norm2 and fcg_shared_reduce;
+* the multi-rank steps run as two processes on the GPU with the library's pack / unpack halves
+  around a host-staged gloo transport, and are compared with the CPU oracle:
+  option A (ghost layer: halo import + evaluate, owned rows == the global rows) and option B
+  (strict element partition: evaluate + shared-DOF all-reduce, owned rows == the global f_int).
+"""
+
+import importlib
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+torch = pytest.importorskip("torch")
+fcg = importlib.import_module("4c_amd").fcg
+halo = importlib.import_module("4c_amd.halo")
+
+pytestmark = pytest.mark.gpu
+
+E, NU = 210.0, 0.3
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+def _comm1():
+    return halo.Comm(0, 1, 0, lambda b: b)
+
+
+@pytest.mark.parametrize("contiguous", [True, False])
+def test_rccl_loopback_halo_import(contiguous):
+    dev = _dev()
+    comm = _comm1()
+    rng = np.random.default_rng(3)
+    n_rows, k = 200, 57
+    n_cols = n_rows + k + 5
+    perm_to = np.arange(n_rows, n_rows + 5)
+    perm_from = rng.choice(n_rows, 5, replace=False)
+    send_row = rng.choice(n_rows, k, replace=False)
+    recv_col = np.arange(n_rows + 5, n_cols)
+    if not contiguous:
+        recv_col = rng.permutation(recv_col)
+    plan = halo.ImportPlan.from_arrays(0, 1, n_rows, n_cols, n_rows, perm_from, perm_to, [k],
+                                       send_row, [k], recv_col)
+    h = halo.Halo(plan, 0)
+    u_row = torch.from_numpy(rng.standard_normal(n_rows)).to(dev)
+    u_col = torch.full((n_cols,), float("nan"), dtype=torch.float64, device=dev)
+    for _ in range(3):  # repeated imports reuse the library's buffers
+        h.import_(comm, u_row, u_col)
+    torch.cuda.synchronize()
+    ur = u_row.cpu().numpy()
+    expect = np.empty(n_cols)
+    expect[:n_rows] = ur
+    expect[perm_to] = ur[perm_from]
+    expect[recv_col] = ur[send_row]
+    assert np.array_equal(u_col.cpu().numpy(), expect)
+    h.close()
+    comm.close()
+
+
+def test_rccl_allreduce_norm_and_shared_single_rank():
+    dev = _dev()
+    comm = _comm1()
+    x = torch.from_numpy(np.random.default_rng(4).standard_normal(1_000_003)).to(dev)
+    y = x.clone()
+    comm.allreduce(y)
+    comm.allreduce(y, op=fcg.FCG_OP_MAX)
+    torch.cuda.synchronize()
+    assert torch.equal(x, y)
+    ref = float(np.linalg.norm(x.cpu().numpy()))
+    for c in (comm, None):
+        n = halo.residual_norm(x, c)
+        assert abs(n - ref) <= 1e-13 * ref
+        assert n == halo.residual_norm(x, c)  # fixed summation order: bitwise repeatable
+    # shared reduce on one rank: the owned interface rows get the buffer values back
+    f = torch.from_numpy(np.arange(10, dtype=np.float64)).to(dev)
+    sp = halo.SharedPlan.from_arrays(0, 1, 6, 3, [1, 4, 7, 0, 2, 9], [5, 0, 2, 1, 3, 4])
+    s = halo.Shared(sp, 0)
+    s.reduce(comm, f)
+    torch.cuda.synchronize()
+    assert np.array_equal(f.cpu().numpy(), np.arange(10, dtype=np.float64))
+    s.close()
+    comm.close()
+
+
+def test_async_evaluate_defers_errors():
+    """fcg_set_async: the failing evaluate returns at once; fcg_check_error reports 4C's throw
+    with the element GID, and the context recovers for the next evaluate."""
+    dev = _dev()
+    mesh = fcg.BoxMesh(fcg.HEX8, (2, 2, 2))
+    good = fcg.BoxMesh(fcg.HEX8, (2, 2, 2))
+    mesh.node_x[:, 0] *= -1.0
+    ev = fcg.Evaluator(mesh, kinematics=fcg.LINEAR, youngs=E, poisson=NU)
+    ev.set_async(True)
+    u = torch.zeros(mesh.n_cols, dtype=torch.float64, device=dev)
+    f = torch.zeros(mesh.n_rows, dtype=torch.float64, device=dev)
+    K = torch.zeros(mesh.nnz, dtype=torch.float64, device=dev)
+    ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u, f, K)  # queued, no error yet
+    ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u, f, K)  # sticky until checked
+    with pytest.raises(fcg.FcgError) as ei:
+        ev.check_error()
+    assert ei.value.code == 1 and ei.value.bad_ele_gid == 0
+    ev.check_error()  # nothing pending any more
+    ev2 = fcg.Evaluator(good, kinematics=fcg.LINEAR, youngs=E, poisson=NU)
+    ev2.set_async(True)
+    ev2.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u, f, K)
+    ev2.check_error()
+    ev2.set_async(False)
+
+
+@pytest.mark.parametrize("threads", ["8", "0"])
+def test_host_overwrite_entry_point(threads):
+    """fcg_evaluate_host(OVERWRITE): the caller's zero() fused -- garbage in K and f is
+    overwritten, the result equals the oracle; ACCUMULATE adds (fcg_evaluate)."""
+    from parity_util import oracle_evaluate, rel_err
+    _dev()
+    os.environ["FCG_HOST_COPY_THREADS"] = threads
+    mesh = fcg.BoxMesh(fcg.HEX8, (12, 10, 9), jitter=0.1)
+    u = mesh.u_col(1e-3)
+    ev = fcg.Evaluator(mesh, kinematics=fcg.LINEAR, youngs=E, poisson=NU)
+    K = np.full(mesh.nnz, 7.0)
+    f = np.full(mesh.n_rows, -3.0)
+    ev.evaluate_host(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u, f, K)
+    _, _, Kr, fr = oracle_evaluate(mesh, fcg.LINEAR, E, NU, u)
+    assert rel_err(f, fr) <= 1e-10 and rel_err(K, Kr) <= 1e-12
+    ev.evaluate_host(fcg.CALC_NLNSTIFF, fcg.ACCUMULATE, u, f, K)
+    assert rel_err(f, 2 * fr) <= 1e-10 and rel_err(K, 2 * Kr) <= 1e-12
+
+
+# ------------------------------------------------------------------ two ranks, host-staged
+def _worker(rank, world, port, q, option, celltype, kinem, path):
+    try:
+        for p in (ROOT, os.path.join(ROOT, "tests")):
+            if p not in sys.path:
+                sys.path.insert(0, p)
+        import torch.distributed as dist
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from parity_util import oracle_evaluate, rel_err
+        dev = torch.device("cuda:0")
+        iv = (8, 6, 5) if celltype == fcg.HEX8 else (3, 3, 2)
+        amp = 1e-3 if kinem == fcg.LINEAR else 5e-2
+        glob = fcg.BoxMesh(celltype, iv, jitter=0.1 if celltype == fcg.HEX8 else 0.02, seed=5)
+        ug = glob.u_col(amp)
+        gcol = {int(g): i for i, g in enumerate(glob.col_gid)}
+        strict = option == "B"
+        m = fcg.BoxMesh(celltype, iv, jitter=0.1 if celltype == fcg.HEX8 else 0.02, seed=5,
+                        rank=rank, nranks=world, strict=strict)
+        n_own = m.n_owned_rows
+        plan = halo.ImportPlan(rank, world, m.row_gid[:n_own], m.col_gid, halo.col_owner_of(m),
+                               halo.gloo_exchange())
+        h = halo.Halo(plan, 0)
+        u_row = torch.from_numpy(np.array([ug[gcol[int(g)]] for g in m.row_gid[:n_own]])).to(dev)
+        u_col = torch.full((m.n_cols,), float("nan"), dtype=torch.float64, device=dev)
+        h.import_staged(u_row, u_col)
+        torch.cuda.synchronize()
+        u_exp = np.array([ug[gcol[int(g)]] for g in m.col_gid])
+        ok = bool(np.array_equal(u_col.cpu().numpy(), u_exp))
+        ev = fcg.Evaluator(m, kinematics=kinem, youngs=E, poisson=NU, device=0, path=path)
+        ev.set_async(True)
+        f = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+        out = {"path": ev.info.path}
+        if option == "A":
+            K = torch.full((m.nnz,), float("nan"), dtype=torch.float64, device=dev)
+            ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u_col, f, K)
+            ev.check_error()
+            _, _, Kr, fr = oracle_evaluate(m, kinem, E, NU, u_exp)
+            Kg = K.cpu().numpy()
+            out["dK"] = float(rel_err(Kg, Kr))
+            out["dKmax"] = float(np.abs(Kg - Kr).max() / np.abs(Kr).max())
+            out["df"] = float(rel_err(f.cpu().numpy(), fr))
+            fg_own = fr
+        else:
+            ev.evaluate_device(fcg.CALC_INTERNALFORCE, fcg.OVERWRITE, u_col, f)
+            ev.check_error()
+            sh = halo.Shared(halo.SharedPlan.of_mesh(m, halo.gloo_exchange()), 0)
+            sh.reduce_staged(f)
+            torch.cuda.synchronize()
+            _, _, _, fgl = oracle_evaluate(glob, kinem, E, NU, ug, want_k=False)
+            grow = {int(g): i for i, g in enumerate(glob.row_gid)}
+            fg_own = fgl[[grow[int(g)] for g in m.row_gid[:n_own]]]
+            out["df"] = float(rel_err(f[:n_own].cpu().numpy(), fg_own))
+            out["n_global"] = sh.n_global
+        # residual norm over the ranks (fcg_norm2 locally, the sum of squares through gloo)
+        loc = halo.residual_norm(f[:n_own])
+        t = torch.tensor([loc * loc], dtype=torch.float64)
+        dist.all_reduce(t)
+        ref = torch.tensor([float(np.dot(fg_own, fg_own))], dtype=torch.float64)
+        dist.all_reduce(ref)
+        out["dnorm"] = abs(np.sqrt(t.item()) - np.sqrt(ref.item())) / np.sqrt(ref.item())
+        q.put((rank, ok, out))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, traceback.format_exc() + repr(e), {}))
+
+
+def _spawn(world, args):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29600 + os.getpid() % 1000 + world
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    return res
+
+
+@pytest.mark.parametrize("celltype,kinem,path", [
+    (fcg.HEX8, fcg.LINEAR, fcg.PATH_AUTO), (fcg.HEX8, fcg.TOTLAG, fcg.PATH_GENERAL),
+    (fcg.HEX27, fcg.TOTLAG, fcg.PATH_AUTO)])
+def test_two_ranks_option_a_halo_evaluate(celltype, kinem, path):
+    _dev()
+    for rank, ok, out in _spawn(2, ("A", celltype, kinem, path)):
+        assert ok is True, (rank, ok)
+        assert out["df"] <= 1e-10 and out["dK"] <= 1e-12 and out["dKmax"] <= 1e-12, (rank, out)
+        assert out["dnorm"] <= 1e-10
+
+
+@pytest.mark.parametrize("celltype,kinem,path", [
+    (fcg.HEX8, fcg.LINEAR, fcg.PATH_AUTO), (fcg.HEX8, fcg.LINEAR, fcg.PATH_GENERAL),
+    (fcg.HEX8, fcg.TOTLAG, fcg.PATH_AUTO), (fcg.HEX27, fcg.LINEAR, fcg.PATH_GENERAL)])
+def test_two_ranks_option_b_shared_allreduce(celltype, kinem, path):
+    _dev()
+    res = _spawn(2, ("B", celltype, kinem, path))
+    assert res[0][2].get("n_global") == res[1][2].get("n_global") and res[0][2]["n_global"] > 0
+    for rank, ok, out in res:
+        assert ok is True, (rank, ok)
+        if celltype == fcg.HEX8 and path == fcg.PATH_AUTO:
+            assert out["path"] == fcg.PATH_STRUCTURED  # strict ranks keep the fused sweep
+        assert out["df"] <= 1e-10, (rank, out)
+        assert out["dnorm"] <= 1e-10
