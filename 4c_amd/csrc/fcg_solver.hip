@@ -108,7 +108,7 @@ __global__ __launch_bounds__(kBlock) void spmv_node_kernel(const int64_t* __rest
 
 // Single-block reduction of n partials (fixed order) into sc[slot]; then the scalar recurrences
 // of the PCG step (op: 0 = store only, 1 = alpha = sc[RZ] / sum, 2 = beta = sum / sc[RZ], RZ = sum)
-enum { SC_RZ = 0, SC_PQ = 1, SC_RR = 2, SC_RZN = 3, SC_RR0 = 4, SC_BETA = 5, SC_ALPHA = 6, SC_N = 8 };
+enum { SC_RZ = 0, SC_PQ = 1, SC_RR = 2, SC_RZN = 3, SC_RR0 = 4, SC_BETA = 5, SC_ALPHA = 6, SC_BAD = 7, SC_N = 8 };
 __global__ __launch_bounds__(kBlock) void reduce_kernel(const double* __restrict__ partial,
     int64_t n, double* sc, int slot, int op, const double* __restrict__ partial2, int slot2)
 {
@@ -124,7 +124,13 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(const double* __restrict
   if (threadIdx.x != 0) return;
   sc[slot] = ta;
   if (partial2) sc[slot2] = tb;
-  if (op == 1) sc[SC_ALPHA] = sc[SC_PQ] != 0.0 ? sc[SC_RZ] / sc[SC_PQ] : 0.0;
+  if (op == 1)
+  {
+    // CG breakdown: p.Kp must be positive for an SPD operator (NaN fails the test too) unless the
+    // iteration already converged exactly (r = 0 -> z = p = 0 within a burst)
+    if (!(sc[SC_PQ] > 0.0) && sc[SC_RZ] != 0.0) sc[SC_BAD] = 1.0;
+    sc[SC_ALPHA] = sc[SC_PQ] > 0.0 ? sc[SC_RZ] / sc[SC_PQ] : 0.0;
+  }
   if (op == 2)
   {
     sc[SC_BETA] = sc[SC_RZ] != 0.0 ? sc[SC_RZN] / sc[SC_RZ] : 0.0;
@@ -134,6 +140,7 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(const double* __restrict
   {
     sc[SC_RZ] = ta;  // init: rz and rr (= rr0)
     sc[SC_RR0] = tb;
+    sc[SC_BAD] = 0.0;
   }
 }
 
@@ -297,7 +304,7 @@ __global__ __launch_bounds__(kBlock) void dirichlet_kernel(const int64_t* __rest
     for (int64_t j = rowptr[row] + lane; j < rowptr[row + 1]; j += 64) K[j] = j == dp ? 1.0 : 0.0;
   if (lane == 0 && rhs)
   {
-    if (freact) freact[row] = rhs[row];
+    if (freact) freact[row] = -rhs[row];  // extract_freact: freact().scale(-1.0), 4C_structure_new_dbc.cpp:389-394
     rhs[row] = 0.0;
   }
 }
@@ -529,6 +536,11 @@ int fcg_pcg_solve(fcg_ctx* ctx, const double* d_K_vals, const double* d_b_row, d
     return FCG_ERR_SINGULAR;
   }
   const double rr0 = hsc[fcg::SC_RR0];
+  if (!std::isfinite(rr0) || !std::isfinite(hsc[fcg::SC_RZ]))
+  {
+    ctx->last_error = "fcg_pcg_solve: non-finite right-hand side or preconditioned residual";
+    return FCG_ERR_SINGULAR;
+  }
   if (rr0 == 0.0) return FCG_OK;  // b = 0 -> x = 0
   const double target = rtol * rtol * rr0;
   int it = 0;
@@ -562,7 +574,15 @@ int fcg_pcg_solve(fcg_ctx* ctx, const double* d_K_vals, const double* d_b_row, d
     }
     it += burst;
     rr = hsc[fcg::SC_RR];
-    if (!std::isfinite(rr)) break;
+    if (!std::isfinite(rr) || hsc[fcg::SC_BAD] != 0.0)
+    {
+      if (iterations) *iterations = it;
+      if (rel_residual) *rel_residual = std::sqrt(rr / rr0);
+      ctx->last_error = !std::isfinite(rr)
+                            ? "fcg_pcg_solve: non-finite residual (diverged)"
+                            : "fcg_pcg_solve: breakdown, p.Kp <= 0 (matrix not positive definite)";
+      return FCG_ERR_SINGULAR;
+    }
   }
   if (iterations) *iterations = it;
   if (rel_residual) *rel_residual = std::sqrt(rr / rr0);

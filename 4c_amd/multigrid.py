@@ -129,6 +129,7 @@ class _Transfer:
 class _Level:
     def __init__(self, mesh, ev, K, dbc_rows, device):
         self.mesh, self.ev, self.K = mesh, ev, K
+        self.rows = np.asarray(dbc_rows, dtype=np.int32)
         self.n = mesh.n_rows
         self.dev = device
         f64 = dict(dtype=torch.float64, device=device)
@@ -200,6 +201,11 @@ class _Level:
 
 class _Indefinite(Exception):
     """The V-cycle returned a non-descent direction (r . z <= 0): smoother bound too low."""
+
+
+class MultigridError(RuntimeError):
+    """The preconditioned solve failed twice: with the kept lambda_max estimate and again with a
+    fresh one (indefinite V-cycle, or no convergence to the requested tolerance)."""
 
 
 class Multigrid:
@@ -309,21 +315,43 @@ class Multigrid:
         self._cheb(lvl, b, x, x_zero=False)
 
     # -- outer solve ------------------------------------------------------------------------
+    def check_dirichlet(self, dbc_rows):
+        """The fine level's mask (from dbc_nodes) must constrain exactly the Newton's Dirichlet
+        rows, else prolongation leaves values on constrained rows that the unit rows never
+        correct; raises ValueError when the two sets differ."""
+        mine = np.sort(self.levels[0].rows)
+        theirs = np.sort(np.asarray(dbc_rows, dtype=np.int32))
+        if not np.array_equal(mine, theirs):
+            raise ValueError(f"multigrid Dirichlet rows ({len(mine)}) differ from the system's "
+                             f"({len(theirs)}): pass a dbc_nodes mask with the same nodes and all "
+                             f"three DOFs constrained")
+
     def solve(self, K, b, x, rtol, max_iter=1000):
-        """K x = b from x = 0 by flexible CG; returns (iterations, relative residual)."""
+        """K x = b from x = 0 by flexible CG; returns (iterations, relative residual).
+
+        lambda_max of D^-1 K barely moves between Newton iterations: it is estimated on the first
+        solve and kept.  A solve that meets an indefinite preconditioned step, or ends above rtol
+        (a stale, too low estimate lets the Chebyshev smoother amplify modes without r.z turning
+        negative), re-estimates lambda_max and restarts once; a second failure raises
+        MultigridError."""
         f0 = self.levels[0]
         f0.K = K
         f0.setup_diag()
-        # lambda_max of D^-1 K barely moves between Newton iterations: estimated on the first
-        # solve and kept; a solve that meets an indefinite preconditioned step re-estimates and
-        # restarts (below)
         if f0.lmax is None:
             f0.estimate_lmax()
-        try:
-            return self._fcg(f0, b, x, rtol, max_iter)
-        except _Indefinite:
-            f0.estimate_lmax()
-            return self._fcg(f0, b, x, rtol, max_iter)
+        why = None
+        for attempt in range(2):
+            if attempt:
+                f0.estimate_lmax()
+            try:
+                it, rel = self._fcg(f0, b, x, rtol, max_iter)
+            except (_Indefinite, FloatingPointError) as e:
+                why = repr(e) or "indefinite V-cycle"
+                continue
+            if rel <= rtol:
+                return it, rel
+            why = f"relative residual {rel:.3e} > {rtol:.3e} after {it} iterations"
+        raise MultigridError(f"multigrid FCG failed after a lambda_max re-estimate: {why}")
 
     def _fcg(self, f0, b, x, rtol, max_iter):
         if self.trace:

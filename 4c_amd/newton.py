@@ -97,6 +97,8 @@ class StaticNewton:
         self.lin_rtol, self.lin_max_iter = lin_rtol, lin_max_iter
         self.forcing = forcing if forcing is not None else ForcingTerm("Constant", constant=lin_rtol)
         self.linear_solver = linear_solver
+        if linear_solver is not None and hasattr(linear_solver, "check_dirichlet"):
+            linear_solver.check_dirichlet(dbc_rows)
         self.history = []
 
     def linear_solve(self, b, x, rtol):
@@ -124,6 +126,10 @@ class StaticNewton:
             torch.neg(self.r, out=self.r)
             eta = self.forcing.compute(it, nr, nr_old, lin_abs)
             lin_it, lin_res = self.linear_solve(self.r, self.du, eta)
+            if not lin_res <= eta:
+                raise RuntimeError(f"linear solve of Newton step {it} stopped at relative residual "
+                                   f"{lin_res:.3e} above the forcing tolerance {eta:.3e} "
+                                   f"({lin_it} iterations)")
             nr_old, lin_abs = nr, lin_res * nr  # ‖F_k + J_k d_k‖ (full step, no line search)
             rec.update(lin_iter=lin_it, lin_relres=lin_res, eta=eta)
             self.history.append(rec)

@@ -163,6 +163,8 @@ def newton_secondary(n, timeout_s=900):
     if p.returncode != 0:
         return {"workload": f"hex27-totlag-{n}^3-newton", "error": p.stderr[-2000:]}
     d = json.loads(p.stdout.strip().splitlines()[-1])
+    if not d.get("converged"):
+        return {"workload": f"hex27-totlag-{n}^3-newton", "error": "Newton did not converge"}
     return {
         "workload": f"hex27-totlag-{n}^3-full-newton",
         "baseline_config": "BASELINE.json configs[2] (StVK, 1M hex27, full Newton loop on 1 MI355X)",
@@ -173,6 +175,7 @@ def newton_secondary(n, timeout_s=900):
         "assembly_ms_mean": d["assembly_ms_mean"], "assembly_elem_per_s": d["assembly_elem_per_s"],
         "solve_ms_total": d["solve_ms_total"], "setup_s": d["setup_s"], "wall_s": wall,
         "elements": d["elements"], "dofs": d["dofs"], "nnz": d["nnz"], "tip_uz": d["tip_uz"],
+        "tangent_symmetry_rel": d.get("tangent_symmetry_rel"),
     }
 
 

@@ -183,8 +183,8 @@ int fcg_get_diagnostics(const fcg_ctx* ctx, uint64_t* out, int n);
 /* y_row = K x_col (Epetra_CrsMatrix::Multiply on the owned rows). */
 int fcg_spmv(fcg_ctx* ctx, const double* d_K_vals, const double* d_x_col, double* d_y_row,
     void* stream);
-/* Dirichlet rows (row LIDs d_rows[n_dbc], device array): freact[row] = rhs[row] (if freact is not
- * NULL, Solid::Dbc::extract_freact), rhs[row] = 0 (apply_dirichlet_to_system with zeros),
+/* Dirichlet rows (row LIDs d_rows[n_dbc], device array): freact[row] = -rhs[row] (if freact is not
+ * NULL, Solid::Dbc::extract_freact: with rhs = F = f_int - f_ext the reaction is f_ext - f_int), rhs[row] = 0 (apply_dirichlet_to_system with zeros),
  * K row -> unit row (SparseMatrix::apply_dirichlet, diagonalblock = true,
  * 4C_linalg_sparsematrix.cpp:978-1097).  K or rhs may be NULL. */
 int fcg_dirichlet_apply(fcg_ctx* ctx, int64_t n_dbc, const int32_t* d_rows, double* d_K_vals,

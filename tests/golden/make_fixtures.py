@@ -16,6 +16,12 @@ Sources (paths relative to /root/reference):
   tests/input_files/solid_ele_hex27_Standard_volume_neumann.dat          (ElastHyper/CoupNeoHooke)
   tests/input_files/tsi_heatflux_monolithic.dat          (thermo-structure interaction, statics)
   tests/input_files/tsi_heatflux_flexoutsurf_monolithic.dat
+  tests/input_files/patch_test_cube_linear_test_react.dat     (reaction forces, list_of_tests.cmake:978)
+  tests/input_files/patch_test_cube_h27_linear_test_react.dat (reaction forces, list_of_tests.cmake:982)
+  tests/input_files/error_analytical_beam_cantilever_end_surface_load_with_poissons_effect.dat
+      + its .csv (L2 error against the analytical solution, list_of_tests.cmake:509)
+  tests/input_files/sohex8_disp_altgeogeneration.dat     (STRUCTURE DOMAIN = GridGenerator,
+                                                          list_of_tests.cmake:1268, NP 2)
 """
 
 import json
@@ -96,12 +102,7 @@ def extract(fname):
                     "nue": float(sm[sm.index("NUE") + 1])}
     else:
         material = {"young": float(mat[mat.index("YOUNG") + 1]), "nue": float(mat[mat.index("NUE") + 1])}
-    results = []
-    for line in s["RESULT DESCRIPTION"]:
-        m = re.match(r"STRUCTURE DIS structure NODE (\d+) QUANTITY (\w+) VALUE\s+(\S+) TOLERANCE (\S+)", line)
-        if m and m.group(2) in ("dispx", "dispy", "dispz"):
-            results.append({"node": int(m.group(1)), "dof": "xyz".index(m.group(2)[-1]),
-                            "value": float(m.group(3)), "tol": float(m.group(4))})
+    results, reactions, reaction_ops = parse_results(s)
     conds = {}
     for key in s:
         if key.startswith("DESIGN") and key.endswith("CONDITIONS"):
@@ -111,18 +112,102 @@ def extract(fname):
                       ("DSURF-NODE TOPOLOGY", "DSURFACE"), ("DVOL-NODE TOPOLOGY", "DVOL")):
         if key in s:
             topo[kind] = topology(s[key], kind)
-    functs = {}
-    for key in s:
-        if key.startswith("FUNCT"):
-            functs[key[5:]] = s[key][0].split("SYMBOLIC_FUNCTION_OF_SPACE_TIME")[1].strip()
+    functs, comps = parse_functions(s)
     dyn = {}
     for line in s["STRUCTURAL DYNAMIC"]:
         tok = line.split()
         if tok[0] in ("TIMESTEP", "NUMSTEP", "MAXTIME", "DYNAMICTYPE"):
             dyn[tok[0]] = tok[1]
-    return {"source": "tests/input_files/" + fname, "nodes": nodes, "elements": elements,
-            "material": material, "results": results, "conditions": conds, "topology": topo,
-            "functions": functs, "dynamic": dyn}
+    out = {"source": "tests/input_files/" + fname, "nodes": nodes, "elements": elements,
+           "material": material, "results": results, "conditions": conds, "topology": topo,
+           "functions": functs, "dynamic": dyn}
+    if reactions:
+        out["reactions"] = reactions
+    if reaction_ops:
+        out["reaction_ops"] = reaction_ops
+    if comps:
+        out["function_components"] = comps
+    return out
+
+
+def parse_results(s):
+    """RESULT DESCRIPTION: nodal displacements, nodal reactions and the OP (sum/min/max) lines over
+    condition node sets (4C_structure_new_resulttest.cpp)."""
+    results, reactions, ops = [], [], []
+    for line in s["RESULT DESCRIPTION"]:
+        m = re.match(r"STRUCTURE DIS structure NODE (\d+) QUANTITY (\w+) VALUE\s+(\S+) TOLERANCE (\S+)", line)
+        if m and m.group(2) in ("dispx", "dispy", "dispz"):
+            results.append({"node": int(m.group(1)), "dof": "xyz".index(m.group(2)[-1]),
+                            "value": float(m.group(3)), "tol": float(m.group(4))})
+        elif m and m.group(2) in ("reactx", "reacty", "reactz"):
+            reactions.append({"node": int(m.group(1)), "dof": "xyz".index(m.group(2)[-1]),
+                              "value": float(m.group(3)), "tol": float(m.group(4))})
+        m = re.match(r"STRUCTURE DIS structure (SURFACE|LINE) (\d+) OP (\w+) QUANTITY (react[xyz]) "
+                     r"VALUE\s+(\S+) TOLERANCE (\S+)", line)
+        if m:
+            ops.append({"set": {"SURFACE": "DSURFACE", "LINE": "DLINE"}[m.group(1)],
+                        "entity": int(m.group(2)), "op": m.group(3), "dof": "xyz".index(m.group(4)[-1]),
+                        "value": float(m.group(5)), "tol": float(m.group(6))})
+    return results, reactions, ops
+
+
+def parse_functions(s):
+    functs, comps = {}, {}
+    for key in s:
+        if key.startswith("FUNCT"):
+            lines = s[key]
+            if len(lines) > 1 and lines[0].startswith("COMPONENT"):
+                comps[key[5:]] = [l.split("SYMBOLIC_FUNCTION_OF_SPACE_TIME")[1].strip() for l in lines]
+            else:
+                functs[key[5:]] = lines[0].split("SYMBOLIC_FUNCTION_OF_SPACE_TIME")[1].strip()
+    return functs, comps
+
+
+def extract_domain(fname):
+    """A STRUCTURE DOMAIN input (GridGenerator box, 4C_io_meshreader.cpp:448-500): box bounds,
+    intervals, element line, CORNER / SIDE node sets, conditions and results."""
+    s = sections(os.path.join(REF, fname))
+    dom = {}
+    for line in s["STRUCTURE DOMAIN"]:
+        tok = line.split()
+        if tok[0] in ("LOWER_BOUND", "UPPER_BOUND"):
+            dom[tok[0].lower()] = [float(t) for t in tok[1:4]]
+        elif tok[0] == "INTERVALS":
+            dom["intervals"] = [int(t) for t in tok[1:4]]
+        elif tok[0] == "ELEMENTS":
+            dom["shape"] = tok[2]
+            dom["kinem"] = tok[tok.index("KINEM") + 1]
+        elif tok[0] == "PARTITION":
+            dom["partition"] = tok[1]
+        elif tok[0] == "ROTATION":
+            dom["rotation"] = [float(t) for t in tok[1:4]]
+    mat = s["MATERIALS"][0].split()
+    material = {"young": float(mat[mat.index("YOUNG") + 1]), "nue": float(mat[mat.index("NUE") + 1])}
+    results, reactions, _ = parse_results(s)
+    conds = {}
+    for key in s:
+        if key.startswith("DESIGN") and key.endswith("CONDITIONS"):
+            conds[key] = [parse_condition(l) for l in s[key]]
+    geo = []
+    for key in ("DNODE-NODE TOPOLOGY", "DLINE-NODE TOPOLOGY", "DSURF-NODE TOPOLOGY"):
+        for line in s.get(key, []):
+            tok = line.split()
+            # CORNER structure x- y- z- DNODE 1 / SIDE structure x- DSURFACE 1
+            geo.append({"kind": tok[0], "spec": tok[2:-2], "set": tok[-2], "entity": int(tok[-1])})
+    dyn = {}
+    for line in s["STRUCTURAL DYNAMIC"]:
+        tok = line.split()
+        if tok[0] in ("TIMESTEP", "NUMSTEP", "MAXTIME", "DYNAMICTYPE", "MAXITER"):
+            dyn[tok[0]] = tok[1]
+    return {"source": "tests/input_files/" + fname, "domain": dom, "material": material,
+            "results": results, "conditions": conds, "geometry_sets": geo, "dynamic": dyn}
+
+
+def extract_csv(fname):
+    """A CSV_COMPARISON reference file: header + rows (data)."""
+    with open(os.path.join(REF, fname)) as f:
+        rows = [l.strip().split(",") for l in f if l.strip()]
+    return {"columns": rows[0], "rows": [[float(v) for v in r] for r in rows[1:]]}
 
 
 def extract_tsi(fname):
@@ -172,6 +257,23 @@ def main():
         with open(out, "w") as f:
             json.dump(data, f, indent=1, sort_keys=True)
         print("wrote", out, len(data["nodes"]), "nodes", len(data["results"]), "results")
+    for fname in ("patch_test_cube_linear_test_react.dat", "patch_test_cube_h27_linear_test_react.dat",
+                  "error_analytical_beam_cantilever_end_surface_load_with_poissons_effect.dat"):
+        data = extract(fname)
+        csv = fname.replace(".dat", ".csv")
+        if os.path.exists(os.path.join(REF, csv)):
+            data["csv_reference"] = extract_csv(csv)
+            data["csv_tolerance"] = {"rtol": 1e-10, "atol": 1e-12}  # list_of_tests.cmake:509
+        out = os.path.join(HERE, fname.replace(".dat", ".json"))
+        with open(out, "w") as f:
+            json.dump(data, f, indent=1, sort_keys=True)
+        print("wrote", out, len(data["nodes"]), "nodes", len(data["results"]), "results")
+    data = extract_domain("sohex8_disp_altgeogeneration.dat")
+    data["np"] = 2  # list_of_tests.cmake:1268
+    out = os.path.join(HERE, "sohex8_disp_altgeogeneration.json")
+    with open(out, "w") as f:
+        json.dump(data, f, indent=1, sort_keys=True)
+    print("wrote", out, data["domain"])
     for fname in ("tsi_heatflux_monolithic.dat", "tsi_heatflux_flexoutsurf_monolithic.dat"):
         data = extract_tsi(fname)
         out = os.path.join(HERE, fname.replace(".dat", ".json"))

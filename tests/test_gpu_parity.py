@@ -268,3 +268,78 @@ def test_hex27_colored_multirank_rows_equal_global(nranks):
             mine = K[m.rowptr[i]:m.rowptr[i + 1]][np.argsort(cols)]
             ref = Kg[glob.rowptr[gi[i]]:glob.rowptr[gi[i] + 1]][np.argsort(gcols)]
             np.testing.assert_allclose(mine, ref, rtol=0, atol=1e-12 * np.abs(Kg).max())
+
+
+# ------------------------------------------------------------------ error paths (4C's throws)
+# A hex27 element (coordinates x 1/8) whose 27 nodal Jacobian determinants are positive but whose
+# Jacobian at the centre Gauss point (0, 0, 0) is exactly singular: invert3x3 throws
+# "determinant of 3x3 matrix is zero" (4C_linalg_fixedsizematrix.hpp:1394) after the nodal check
+# passed (calc_lib.hpp:475-496).  Found by a search over quarter-grid perturbations of the unit
+# hex27 with the z-face centre difference forced into the span of the x- and y-face differences;
+# every product at the centre point is exact, so det J == 0.0 on any summation order.
+SINGULAR_HEX27_X4 = [  # x 1/8
+    [-32, -32, -32], [36, -28, -32], [32, 32, -32], [-30, 28, -36], [-32, -32, 32], [32, -32, 32],
+    [32, 32, 30], [-36, 34, 30], [0, -32, -32], [36, 4, -30], [0, 32, -32], [-32, 0, -32],
+    [-26, -38, 6], [26, -38, 4], [32, 32, 0], [-32, 32, 0], [0, -32, 32], [32, 0, 32], [0, 32, 32],
+    [-32, 0, 32], [0, 0, -32], [2, -36, 2], [26, 0, 2], [0, 32, 0], [-32, 0, 0], [1, -34, -31],
+    [0, 0, 0]]
+
+
+def _singular_hex27_mesh(n_before):
+    """n_before regular hex27 elements, then the singular one (element GID n_before + 100)."""
+    X = [np.array(SINGULAR_HEX27_X4, dtype=float) / 8.0]
+    en = [np.arange(27)]
+    for k in range(n_before):  # regular cubes, apart from each other
+        X.append(4.0 * orc_par27() + 20.0 * (k + 1))
+        en.append(np.arange(27) + 27 * (k + 1))
+    dis = fcg.Discretization.from_elements(fcg.HEX27, np.array(en[1:] + en[:1]), np.vstack(X))
+    dis.ele_gid = np.arange(100, 100 + dis.n_ele, dtype=np.int32)
+    return dis
+
+
+def orc_par27():
+    import oracle_lib as orc
+    return orc.node_param_coords(orc.HEX27)
+
+
+@pytest.mark.parametrize("n_before", [0, 3])
+def test_singular_gauss_point_jacobian_reports_element(n_before):
+    import oracle_lib as orc
+    X = np.array(SINGULAR_HEX27_X4, dtype=float) / 8.0
+    assert orc.solid_evaluate(orc.HEX27, orc.LINEAR, E, NU, X, np.zeros((27, 3)))[0] == 2
+    _dev()
+    dis = _singular_hex27_mesh(n_before)
+    for kinem in (fcg.LINEAR, fcg.TOTLAG):
+        with pytest.raises(fcg.FcgError) as ei:
+            _run_gpu(dis, kinem, np.zeros(dis.n_cols), path=fcg.PATH_GENERAL)
+        assert ei.value.code == 2 and ei.value.bad_ele_gid == 100 + n_before
+
+
+@pytest.mark.parametrize("celltype,path", [(fcg.HEX8, fcg.PATH_GENERAL), (fcg.HEX27, fcg.PATH_GENERAL),
+                                           (fcg.HEX27, fcg.PATH_COLORED)])
+def test_negative_nodal_jacobian_all_paths(celltype, path):
+    """calc_lib.hpp:492-494 on the general and colour-ordered paths (the structured hex8 sweep is
+    test_negative_jacobian_reports_element): one inverted element in the middle of a box is
+    reported by its GID, and the next evaluate of a valid state succeeds again."""
+    _dev()
+    mesh = fcg.BoxMesh(celltype, (3, 2, 2))
+    bad = 4  # element gid 4 = lattice (1, 1, 0)
+    nodes = mesh.ele_nodes[list(mesh.ele_gid).index(bad)]
+    good_x = mesh.node_x.copy()
+    # pull the element's interior / top nodes through its bottom face (det J < 0 at its nodes)
+    npe = 8 if celltype == fcg.HEX8 else 27
+    top = nodes[4:8] if npe == 8 else nodes[[4, 5, 6, 7, 16, 17, 18, 19, 25]]
+    mesh.node_x[top, 2] -= 1.5 * (mesh.node_x[top, 2].max() - mesh.node_x[nodes, 2].min())
+    kinem = fcg.LINEAR
+    # expected: the lowest GID among the elements the oracle rejects (the move also inverts
+    # neighbours sharing the moved nodes); the reference throws on the first one it evaluates
+    import oracle_lib as orc
+    rejected = [int(g) for g, en in zip(mesh.ele_gid, mesh.ele_nodes)
+                if orc.solid_evaluate(celltype, kinem, E, NU, mesh.node_x[en], np.zeros((npe, 3)),
+                                      want_k=False)[0] == 1]
+    assert bad in rejected
+    with pytest.raises(fcg.FcgError) as ei:
+        _run_gpu(mesh, kinem, np.zeros(mesh.n_cols), path=path)
+    assert ei.value.code == 1 and ei.value.bad_ele_gid == min(rejected), (ei.value, rejected)
+    mesh.node_x[:] = good_x
+    _run_gpu(mesh, kinem, mesh.u_col(1e-3), path=path)

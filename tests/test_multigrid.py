@@ -160,3 +160,49 @@ def test_newton_multigrid_matches_pcg(ct, n, kin, load, length, jitter, tol):
     assert len(lv) >= 2
     assert np.linalg.norm(u1 - u0) <= 100 * tol * np.linalg.norm(u0)
     assert it1 * 3 < it0, (it0, it1)
+
+
+@pytest.mark.gpu
+def test_stale_lmax_restarts_and_dirichlet_mismatch_raises():
+    """a too-low kept lambda_max estimate is re-estimated and the solve restarted (the
+    restart path), and a multigrid mask that disagrees with the Newton's Dirichlet rows is refused."""
+    torch, dev = _dev()
+    mesh, clamp, dbc, fext = _cantilever(fcg.HEX8, 8, fcg.LINEAR, -1e-2)
+    ev = fcg.Evaluator(mesh, kinematics=fcg.LINEAR, youngs=E, poisson=NU)
+    mg = mgm.Multigrid(mesh, ev, clamp, E, NU, min_intervals=2)
+    with pytest.raises(ValueError):
+        newton.StaticNewton(ev, fext, dbc[3:], linear_solver=mg)
+    nt = newton.StaticNewton(ev, fext, dbc, tol_res=1e-10 * np.linalg.norm(fext), tol_inc=1e-9,
+                             lin_rtol=1e-12, linear_solver=mg)
+    u_ref = nt.solve().cpu().numpy()
+    good = mg.levels[0].lmax
+    mg.levels[0].lmax = 1e-3 * good  # stale and far too low
+    u = nt.solve().cpu().numpy()
+    assert mg.levels[0].lmax > 0.5 * good  # re-estimated
+    assert np.linalg.norm(u - u_ref) <= 1e-8 * np.linalg.norm(u_ref)
+
+
+@pytest.mark.gpu
+def test_pcg_reports_breakdown_and_nonfinite():
+    """fcg_pcg_solve returns FCG_ERR_SINGULAR for a non-finite system or a
+    p.Kp <= 0 breakdown instead of FCG_OK with NaN."""
+    torch, dev = _dev()
+    mesh, clamp, dbc, fext = _cantilever(fcg.HEX8, 4, fcg.LINEAR, -1e-2)
+    ev = fcg.Evaluator(mesh, kinematics=fcg.LINEAR, youngs=E, poisson=NU)
+    f64 = dict(dtype=torch.float64, device=dev)
+    K = torch.zeros(mesh.nnz, **f64)
+    ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, torch.zeros(mesh.n_cols, **f64),
+                       torch.zeros(mesh.n_rows, **f64), K)
+    ev.dirichlet_apply(torch.from_numpy(dbc).to(dev), K)
+    b = torch.from_numpy(fext).to(dev)
+    x = torch.empty_like(b)
+    bn = b.clone()
+    bn[5] = float("nan")
+    with pytest.raises(fcg.FcgError) as ei:
+        ev.pcg_solve(K, bn, x)
+    assert ei.value.code == 2
+    with pytest.raises(fcg.FcgError) as ei:
+        ev.pcg_solve(-K, b, x)  # negative definite: p.Kp < 0 on the first step
+    assert ei.value.code == 2
+    it, rr = ev.pcg_solve(K, b, x, rtol=1e-12)
+    assert rr <= 1e-12

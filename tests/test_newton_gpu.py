@@ -172,7 +172,7 @@ def test_spmv_dirichlet_pcg_against_scipy():
     assert np.all(Kd[isd & (mesh.col_lid == rows)] == 1.0)
     assert np.all(Kd[isd & (mesh.col_lid != rows)] == 0.0)
     assert np.array_equal(Kd[~isd], Kh[~isd])
-    assert np.array_equal(freact.cpu().numpy()[dbc], rhs_h[dbc])
+    assert np.array_equal(freact.cpu().numpy()[dbc], -rhs_h[dbc])  # extract_freact scales by -1
     assert np.all(rhs.cpu().numpy()[dbc] == 0.0)
     sol = torch.empty_like(rhs)
     it, rr = ev.pcg_solve(K, rhs, sol, rtol=1e-14, max_iter=5000)
@@ -213,3 +213,72 @@ def test_neohooke_result_description_on_device(name):
     for r in fx["results"]:
         got = prob.disp(u, r["node"], r["dof"])
         assert abs(got - r["value"]) <= r["tol"], (r, got)
+
+
+# ------------------------------------------------- reactions, analytical error, DOMAIN (device)
+import known_answers as ka  # noqa: E402
+
+
+@pytest.mark.parametrize("name", ["patch_test_cube_linear_test_react.json",
+                                  "patch_test_cube_h27_linear_test_react.json"])
+def test_reaction_forces_on_device(name):
+    """Reaction forces of patch_test_cube_*_linear_test_react.dat (1e-13) from the library alone:
+    StaticNewton's final evaluate + fcg_dirichlet_apply (extract_freact's -F at the DBC rows)."""
+    _dev()
+    fx = json.load(open(os.path.join(GOLD, name)))
+    prob = fp.problem(fx)
+    dis = fp.discretization(prob)
+    ev = fcg.Evaluator(dis, kinematics=fp.kinematics_of(fx), youngs=prob.E, poisson=prob.nu)
+    nt = newton.StaticNewton(ev, fp.fext(prob, 1.0), prob.dirichlet_dofs(), tol_res=1e-12,
+                             tol_inc=1e-13, lin_rtol=1e-14)
+    u = nt.solve().cpu().numpy()
+    for r in fx["results"]:
+        assert abs(u[3 * prob.lid[r["node"]] + r["dof"]] - r["value"]) <= r["tol"], r
+    assert ka.check_reactions(fx, prob, nt.freact.cpu().numpy()) == []
+
+
+@pytest.mark.parametrize("lattice", [False, True])
+def test_analytical_error_cantilever_on_device(lattice):
+    """error_analytical_beam_cantilever_end_surface_load_with_poissons_effect.dat through the
+    library (general path, and the structured sweep via the lattice hint the beam admits): the
+    RESULT DESCRIPTION (1e-10) and the L2-error CSV (rtol 1e-10, atol 1e-12)."""
+    _dev()
+    fx = json.load(open(os.path.join(GOLD,
+                    "error_analytical_beam_cantilever_end_surface_load_with_poissons_effect.json")))
+    prob = fp.problem(fx)
+    dis = fp.discretization(prob, lattice=lattice)
+    ev = fcg.Evaluator(dis, kinematics=fcg.LINEAR, youngs=prob.E, poisson=prob.nu,
+                       path=fcg.PATH_STRUCTURED if lattice else fcg.PATH_GENERAL)
+    assert ev.info.path == (fcg.PATH_STRUCTURED if lattice else fcg.PATH_GENERAL)
+    nt = newton.StaticNewton(ev, fp.fext(prob, 1.0), prob.dirichlet_dofs(), tol_res=1e-12,
+                             tol_inc=1e-12, lin_rtol=1e-14)
+    u = nt.solve().cpu().numpy()
+    for r in fx["results"]:
+        assert abs(u[3 * prob.lid[r["node"]] + r["dof"]] - r["value"]) <= r["tol"], r
+    ref = dict(zip(fx["csv_reference"]["columns"], fx["csv_reference"]["rows"][0]))
+    tol = fx["csv_tolerance"]
+    for k, v in zip(("displacement_error_l2_norm", "displacement_integral", "reference_volume"),
+                    ka.analytical_error(fx, prob, u)):
+        assert abs(v - ref[k]) <= tol["atol"] + tol["rtol"] * abs(ref[k]), (k, v, ref[k])
+
+
+@pytest.mark.parametrize("nranks", [1, 2])
+def test_domain_altgeogeneration_on_device(nranks):
+    """sohex8_disp_altgeogeneration.dat (STRUCTURE DOMAIN, NP 2 in the reference): the box of
+    fcg_box_mesh_create at 1 and 2 ranks, every rank's owned K rows from its own context on the
+    device (structured sweep), gathered by DOF GID; NODE 49 (GID 48) dispx = 4.0 at 1e-14."""
+    dev = _dev()
+    fx = json.load(open(os.path.join(GOLD, "sohex8_disp_altgeogeneration.json")))
+    meshes = ka.domain_meshes(fx, nranks)
+    E, nu = fx["material"]["young"], fx["material"]["nue"]
+
+    def assemble(m, u):
+        ev = fcg.Evaluator(m, kinematics=fcg.TOTLAG, youngs=E, poisson=nu)
+        assert ev.info.path == fcg.PATH_STRUCTURED
+        f = torch.zeros(m.n_rows, dtype=torch.float64, device=dev)
+        K = torch.full((m.nnz,), float("nan"), dtype=torch.float64, device=dev)
+        ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, torch.from_numpy(u).to(dev), f, K)
+        return K.cpu().numpy(), f.cpu().numpy()
+
+    u = ka.domain_solve(fx, meshes, assemble)
+    assert ka.check_domain_results(fx, u) == []

@@ -225,3 +225,70 @@ def test_neohooke_cmat_is_stress_derivative():
     np.testing.assert_allclose(S0, 0.0, atol=1e-14)
     _, Cst = orc.stvk(E, nu, np.zeros(6))
     np.testing.assert_allclose(C0, Cst, rtol=1e-12, atol=1e-12)
+
+
+# --------------------------------------------------------------------------- reactions, error, DOMAIN
+import known_answers as ka  # noqa: E402
+
+
+@pytest.mark.parametrize("name", ["patch_test_cube_linear_test_react.json",
+                                  "patch_test_cube_h27_linear_test_react.json"])
+def test_reaction_forces(name):
+    """tests/input_files/patch_test_cube_*_linear_test_react.dat: displacements and the reaction
+    forces (the reference's only direct pin on the assembled residual at Dirichlet rows), 1e-13."""
+    fx = load_fixture(name)
+    prob = Problem(fx)
+    u = prob.solve_statics(t=1.0)
+    for r in fx["results"]:
+        assert abs(prob.disp(u, r["node"], r["dof"]) - r["value"]) <= r["tol"], r
+    fr = ka.reactions(prob, u)
+    assert ka.check_reactions(fx, prob, fr) == []
+    assert len(fx["reactions"]) >= 4
+
+
+def test_analytical_error_cantilever():
+    """error_analytical_beam_cantilever_end_surface_load_with_poissons_effect.dat: the end-load
+    cantilever (10 hex8, ten load steps), its RESULT DESCRIPTION (1e-10) and the L2-error CSV
+    (CSV_COMPARISON_TOL_R 1e-10, _A 1e-12, list_of_tests.cmake:509)."""
+    fx = load_fixture("error_analytical_beam_cantilever_end_surface_load_with_poissons_effect.json")
+    prob = Problem(fx)
+    u = prob.solve_statics(t=1.0, nsteps=10)
+    for r in fx["results"]:
+        assert abs(prob.disp(u, r["node"], r["dof"]) - r["value"]) <= r["tol"], r
+    got = ka.analytical_error(fx, prob, u)
+    ref = dict(zip(fx["csv_reference"]["columns"], fx["csv_reference"]["rows"][0]))
+    tol = fx["csv_tolerance"]
+    for k, v in zip(("displacement_error_l2_norm", "displacement_integral", "reference_volume"), got):
+        assert abs(v - ref[k]) <= tol["atol"] + tol["rtol"] * abs(ref[k]), (k, v, ref[k])
+
+
+@pytest.mark.parametrize("nranks", [1, 2])
+def test_domain_altgeogeneration(nranks):
+    """sohex8_disp_altgeogeneration.dat: STRUCTURE DOMAIN 3x3x3 hex8 TotLag on [0,4]^3 built by the
+    GridGenerator restatement (fcg_box_mesh_create) at NP 1 and NP 2 (the reference runs NP 2),
+    assembled by the oracle rank by rank; NODE 49 (GID 48, the corner (4,4,0) of the 7^3 lattice)
+    dispx = 4.0 at 1e-14."""
+    from parity_util import oracle_evaluate
+    fx = load_fixture("sohex8_disp_altgeogeneration.json")
+    meshes = ka.domain_meshes(fx, nranks)
+    g48 = [m.node_x[list(m.node_gid).index(48)] for m in meshes if 48 in m.node_gid]
+    np.testing.assert_allclose(g48[0], [4.0, 4.0, 0.0], atol=1e-14)
+    E, nu = fx["material"]["young"], fx["material"]["nue"]
+
+    def assemble(m, u):
+        err, _, K, f = oracle_evaluate(m, orc.TOTLAG, E, nu, u)
+        assert err == 0
+        return K, f
+
+    u = ka.domain_solve(fx, meshes, assemble)
+    assert ka.check_domain_results(fx, u) == []
+
+
+def test_singular_gauss_point_jacobian_oracle():
+    """The hex27 element of tests/test_gpu_parity.py::SINGULAR_HEX27_X4 passes the nodal check
+    (calc_lib.hpp:475-496) and hits det J == 0 at the centre Gauss point: invert3x3's throw
+    (4C_linalg_fixedsizematrix.hpp:1394), error code 2."""
+    from test_gpu_parity import SINGULAR_HEX27_X4
+    X = np.array(SINGULAR_HEX27_X4, dtype=float) / 8.0
+    for kin in (orc.LINEAR, orc.TOTLAG):
+        assert orc.solid_evaluate(orc.HEX27, kin, 210.0, 0.3, X, np.zeros((27, 3)))[0] == 2

@@ -96,7 +96,9 @@ class Timed(newton.StaticNewton):
             rec.update(solve_ms=1e3 * (t_d - t_c), pcg_iter=li, pcg_relres=lr, eta=eta, norm_inc=ndu)
             self.history.append(rec)
             print(json.dumps(rec), file=sys.stderr, flush=True)
-        return u
+        # as StaticNewton: an unconverged loop is an error, never a timing
+        raise RuntimeError(f"Newton did not converge in {self.max_iter} iterations: "
+                           f"{self.history[-3:]}")
 
 
 mg = None
@@ -117,7 +119,21 @@ u = nt.solve()
 torch.cuda.synchronize()
 t_newton = time.perf_counter() - t1
 h = nt.history
+# the tangent at the solution (before Dirichlet rows) is symmetric for StVK: x.(K y) == y.(K x)
+ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u, nt.fint, nt.K)
+gen = torch.Generator(device="cpu").manual_seed(7)
+xv = torch.randn(mesh.n_rows, generator=gen, dtype=torch.float64).to(u.device)
+yv = torch.randn(mesh.n_rows, generator=gen, dtype=torch.float64).to(u.device)
+Kx, Ky = torch.empty_like(xv), torch.empty_like(yv)
+ev.spmv(nt.K, xv, Kx)
+ev.spmv(nt.K, yv, Ky)
+sym = abs(float(torch.dot(xv, Ky)) - float(torch.dot(yv, Kx))) / float(
+    torch.linalg.vector_norm(xv) * torch.linalg.vector_norm(Ky))
+r_final = float(torch.linalg.vector_norm(nt.fint - nt.fext)) / max(np.linalg.norm(fext), 1e-300)
+del xv, yv, Kx, Ky
 out = {"config": f"{a.celltype}-{a.kinem}-{a.n}^3-cantilever", "forcing": a.forcing,
+       "converged": True, "tangent_symmetry_rel": sym,
+       "residual_rel_incl_dbc_rows": r_final,
        "linear_solver": (f"multigrid-FCG (Chebyshev {a.mg_nu})" if a.mg else "block-Jacobi PCG"),
        "mg_levels": mg.describe() if mg else None, "elements": mesh.n_ele,
        "dofs": mesh.n_rows, "nnz": mesh.nnz, "setup_s": t_setup, "newton_s": t_newton,
