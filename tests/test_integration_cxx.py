@@ -1,0 +1,37 @@
+"""The INTEGRATION.md C++ binding, compiled (tests/cxx/integration_4c.cpp, built by
+__graft_entry__.build() / `make -C tests/cxx`) and run: on the CPU it must build, link against
+libfourc_gpu.so and report fcg_create's device error cleanly; on the GPU every rank of a 2-rank
+GridGenerator box evaluates through fcg_evaluate and through the C++ facade
+(fourc_gpu::Discretization::evaluate with a ParameterList action) and matches the oracle."""
+
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CXX = os.path.join(ROOT, "tests", "cxx")
+BIN = os.path.join(CXX, "_build", "integration_4c")
+
+
+def _binary():
+    if not os.path.exists(BIN):
+        subprocess.run(["make", "-s", "-C", CXX], check=True)
+    return BIN
+
+
+def test_integration_builds_and_reports_missing_device():
+    torch = pytest.importorskip("torch")
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present: the device run is the gpu test")
+    p = subprocess.run([_binary(), "--expect-no-device"], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "PASS" in p.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [["6", "5", "4", "2"], ["9", "7", "8", "3"], ["5", "5", "5", "1"]])
+def test_integration_on_device(args):
+    p = subprocess.run([_binary()] + args, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "PASS" in p.stdout, p.stdout
