@@ -48,7 +48,18 @@ class Comm:
             uid = bcast_id(None)
         ctypes.memmove(buf, uid, 128)
         h = ctypes.c_void_p()
-        rc = L.fcg_comm_create(buf, world, rank, device, ctypes.byref(h))
+        # RCCL prints its version banner on stdout at init: send it to stderr, so that a host's
+        # stdout (bench.py's one JSON line) stays clean
+        import os
+        import sys
+        sys.stdout.flush()
+        saved = os.dup(1)
+        try:
+            os.dup2(2, 1)
+            rc = L.fcg_comm_create(buf, world, rank, device, ctypes.byref(h))
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
         if rc != 0:
             raise fcg.FcgError(rc, "fcg_comm_create (ncclCommInitRank) failed")
         self._h, self.rank, self.world, self.device = h, rank, world, device

@@ -253,7 +253,29 @@ def hex27_secondary(dev, n, steps, threads, with_cpu):
     return out
 
 
-def tsi_secondary(dev, rank, world, steps, n=126):
+def tsi_cpu_baseline(n, nz, threads):
+    """The oracle's TSI::Monolithic element loop (orc_tsi_discretization_evaluate: the four
+    blocks and both residuals, owned rows, `threads` workers as ranks) on an n x n x nz slab of the
+    config-5 box, timed on the host cores."""
+    pu = _oracle_native()
+    E, NU, ALPHA, T0, COND, DT = 210.0, 0.3, 1.2e-5, 293.0, 52.0, 0.5
+    m = fcg.BoxMesh(fcg.HEX8, (n, n, nz), upper=(1.0, 1.0, nz / n), jitter=0.1, seed=20251015)
+    g = fcg.TsiGraph(m)
+    X = m.node_x
+    Tn = T0 + 50.0 * np.sin(2 * np.pi * X[:, 0]) * np.cos(np.pi * X[:, 1])
+    t = time.perf_counter()
+    err = pu.oracle_tsi_evaluate(m, g, E, NU, ALPHA, T0, COND, 1.0, 1.0 / DT, m.u_col(1e-3),
+                                 m.u_col(1e-2), Tn, nworkers=threads)[0]
+    tn = time.perf_counter() - t
+    assert err == 0
+    return {"value": m.n_ele / tn, "unit": "element-evaluations/s (two-field tangent)",
+            "cores": threads, "kind": "port",
+            "sample": f"one TSI two-field tangent (K_SS, k_ST, k_TS, k_TT, f_S, f_T) of a {n}x{n}x{nz} "
+                      f"slab of the 126^3 box ({m.n_ele} elements), {threads} threads as ranks",
+            "wall_s": tn}
+
+
+def tsi_secondary(dev, rank, world, steps, n=126, cpu_threads_=0):
     """BASELINE config 5: the monolithic TSI two-field tangent (K_SS, k_ST, k_TS, k_TT, f_S, f_T;
     hex8, geometrically linear ThermoStVenantKirchhoff + Fourier) of a 126^3 = 2M-element box,
     strong-scaled: every rank assembles its GridGenerator share (owned rows, ghost layer, no
@@ -320,6 +342,11 @@ def tsi_secondary(dev, rank, world, steps, n=126):
            "cpu_baseline": None}
     for o in (tev, ev):
         o.close()
+    if cpu_threads_ and rank == 0 and world == 1:
+        try:
+            out["cpu_baseline"] = tsi_cpu_baseline(n, 16, cpu_threads_)
+        except Exception as e:  # report, never hide
+            out["cpu_baseline"] = {"value": None, "error": repr(e)}
     return out
 
 
@@ -658,7 +685,9 @@ def main():
                                            staged))
         torch.cuda.empty_cache()
     if not args.no_tsi:
-        secondary.append(tsi_secondary(dev, rank, world, max(3, min(args.steps, 10))))
+        secondary.append(tsi_secondary(dev, rank, world, max(3, min(args.steps, 10)),
+                                       cpu_threads_=0 if args.no_cpu_baseline
+                                       else cpu_threads(args.cpu_threads)))
     if rank == 0 and world == 1 and not args.no_host:
         secondary.append(host_secondary(dev, args.n, 3))
     if rank == 0 and world == 1 and not args.no_hex27:

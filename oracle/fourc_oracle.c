@@ -839,9 +839,17 @@ static int* lower_bound_int(int* first, int* last, int value)
 int orc_sparse_assemble(orc_csr* A, int myrank, int numnode, const int* lmstride, int lcoldim,
     const double* Aele, const int* lmrow, const int* lmrowowner, const int* lmcol)
 {
-  /* SparseMatrix::assemble, Filled() branch (4C_linalg_sparsematrix.cpp:444-576).
-   * Aele is column-major with leading dimension lrowdim. */
-  const int lrowdim = lcoldim;
+  return orc_sparse_assemble_rect(A, myrank, numnode, lmstride, lcoldim, lcoldim, Aele, lmrow,
+      lmrowowner, lmcol);
+}
+
+int orc_sparse_assemble_rect(orc_csr* A, int myrank, int numnode, const int* lmstride, int lrowdim,
+    int lcoldim, const double* Aele, const int* lmrow, const int* lmrowowner, const int* lmcol)
+{
+  /* SparseMatrix::assemble, Filled() branch (4C_linalg_sparsematrix.cpp:444-576): lrowdim rows x
+   * lcoldim columns (rectangular for TSI's coupling blocks, AssembleStrategy(0, 1, k_st));
+   * numnode / lmstride describe the column nodes.  Aele is column-major with leading dimension
+   * lrowdim. */
   int localcol[MAXDOF];
   for (int lcol = 0; lcol < lcoldim; ++lcol)
   {
@@ -1208,4 +1216,103 @@ int orc_tsi_thermo_evaluate(int celltype, double conduct, double m, const double
     }
   }
   return ORC_OK;
+}
+
+/* TSI::Monolithic's four element evaluates per element and their assembly (owned rows, the
+ * reference's MPI semantics with `nworkers` ranks as threads, as orc_discretization_evaluate):
+ * struct_calc_nlnstiff with the temperature state -> K_ss, f_s; struct_calc_stifftemp -> K_st
+ * (AssembleStrategy(0, 1, k_st), 4C_tsi_monolithic.cpp:1694-1767); calc_thermo_fintcond -> K_tt,
+ * f_t; calc_thermo_coupltang -> K_ts (:1773-1869).  Structural DOF gid 3 (node gid - min) + d,
+ * thermo DOF gid node gid - min (one DOF per node; only the maps of the four CSRs use them). */
+int orc_tsi_discretization_evaluate(int celltype, double E, double nu, double alpha, double T0,
+    double conduct, double timefac, double timefac_d, int64_t n_ele, const int64_t* ele_nodes,
+    const double* node_x, const int64_t* node_gid, const int32_t* node_owner, int64_t min_node_gid,
+    int nworkers, const double* u, const double* v, const double* T, orc_csr* Kss, orc_csr* Kst,
+    orc_csr* Kts, orc_csr* Ktt, double* fs, double* ft, int64_t* bad_ele)
+{
+  const int n = orc_num_nodes(celltype);
+  const int ndof = 3 * n;
+  const double m = orc_thermo_stvk_st_modulus(E, nu, alpha);
+  int result = 0;
+  int64_t first_bad = -1;
+  if (nworkers < 1) nworkers = 1;
+#pragma omp parallel for num_threads(nworkers) schedule(static, 1)
+  for (int w = 0; w < nworkers; ++w)
+  {
+    double* Ke = (double*)malloc(sizeof(double) * ndof * ndof);
+    double* Kst_e = (double*)malloc(sizeof(double) * ndof * n);
+    double* Kts_e = (double*)malloc(sizeof(double) * ndof * n);
+    double* Ktt_e = (double*)malloc(sizeof(double) * n * n);
+    double fe[MAXDOF], fte[MAXN], X[3 * MAXN], ue[3 * MAXN], ve[3 * MAXN], Te[MAXN];
+    int lm[MAXDOF], lmowner[MAXDOF], lmstride[MAXN], lmt[MAXN], lmtowner[MAXN], lmtstride[MAXN];
+    for (int64_t e = 0; e < n_ele; ++e)
+    {
+      const int64_t* en = ele_nodes + (int64_t)n * e;
+      int touches = 0;
+      for (int a = 0; a < n; ++a)
+        if (node_owner[en[a]] == w)
+        {
+          touches = 1;
+          break;
+        }
+      if (!touches) continue;
+      for (int a = 0; a < n; ++a)
+      {
+        const int64_t nd = en[a];
+        const int g = (int)(node_gid[nd] - min_node_gid);
+        for (int d = 0; d < 3; ++d)
+        {
+          lm[3 * a + d] = 3 * g + d;
+          lmowner[3 * a + d] = node_owner[nd];
+          X[3 * a + d] = node_x[3 * nd + d];
+          ue[3 * a + d] = u[Kss->col_lid_of_gid[3 * g + d]];
+          ve[3 * a + d] = v[Kss->col_lid_of_gid[3 * g + d]];
+        }
+        lmt[a] = g;
+        lmtowner[a] = node_owner[nd];
+        Te[a] = T[Ktt->col_lid_of_gid[g]];
+        lmstride[a] = 3;
+        lmtstride[a] = 1;
+      }
+      memset(Ke, 0, sizeof(double) * ndof * ndof);
+      memset(Kst_e, 0, sizeof(double) * ndof * n);
+      memset(Kts_e, 0, sizeof(double) * ndof * n);
+      memset(Ktt_e, 0, sizeof(double) * n * n);
+      memset(fe, 0, sizeof(fe));
+      memset(fte, 0, sizeof(fte));
+      int err = orc_tsi_solid_evaluate(celltype, E, nu, alpha, T0, X, ue, Te, Ke, fe, Kst_e);
+      if (!err) err = orc_tsi_thermo_evaluate(celltype, conduct, m, X, Te, ve, timefac, timefac_d,
+                    Ktt_e, fte, Kts_e);
+      if (err)
+      {
+#pragma omp critical
+        {
+          if (!result || e < first_bad)
+          {
+            result = err;
+            first_bad = e;
+          }
+        }
+        break;
+      }
+      int rc = orc_sparse_assemble_rect(Kss, w, n, lmstride, ndof, ndof, Ke, lm, lmowner, lm);
+      if (!rc) rc = orc_sparse_assemble_rect(Kst, w, n, lmtstride, ndof, n, Kst_e, lm, lmowner, lmt);
+      if (!rc) rc = orc_sparse_assemble_rect(Kts, w, n, lmstride, n, ndof, Kts_e, lmt, lmtowner, lm);
+      if (!rc) rc = orc_sparse_assemble_rect(Ktt, w, n, lmtstride, n, n, Ktt_e, lmt, lmtowner, lmt);
+      if (!rc) rc = orc_vector_assemble(fs, Kss->row_lid_of_gid, Kss->max_gid, ndof, fe, lm, lmowner, w);
+      if (!rc) rc = orc_vector_assemble(ft, Ktt->row_lid_of_gid, Ktt->max_gid, n, fte, lmt, lmtowner, w);
+      if (rc)
+      {
+#pragma omp critical
+        result = ORC_ERR_ARG;
+        break;
+      }
+    }
+    free(Ke);
+    free(Kst_e);
+    free(Kts_e);
+    free(Ktt_e);
+  }
+  if (bad_ele) *bad_ele = first_bad;
+  return result;
 }

@@ -91,6 +91,11 @@ typedef struct orc_csr {
 int orc_sparse_assemble(orc_csr* A, int myrank, int nnode, const int* lmstride, int ndof,
     const double* Aele, const int* lmrow, const int* lmrowowner, const int* lmcol);
 
+/* The same for lrowdim x lcoldim element matrices (TSI coupling blocks); numnode / lmstride
+ * describe the column nodes. */
+int orc_sparse_assemble_rect(orc_csr* A, int myrank, int numnode, const int* lmstride, int lrowdim,
+    int lcoldim, const double* Aele, const int* lmrow, const int* lmrowowner, const int* lmcol);
+
 /* LinAlg::assemble(Vector&, ...) (4C_linalg_utils_sparse_algebra_assemble.cpp:72-92). */
 int orc_vector_assemble(double* V, const int32_t* lid_of_gid, int64_t max_gid, int ndof,
     const double* Vele, const int* lm, const int* lmowner, int myrank);
@@ -138,6 +143,15 @@ int orc_tsi_solid_evaluate(int celltype, double E, double nu, double alpha, doub
 int orc_tsi_thermo_evaluate(int celltype, double conduct, double m, const double* X,
     const double* T, const double* v, double timefac, double timefac_d, double* Ktt,
     double* fT, double* Kts);
+
+/* All four TSI blocks and both residuals of a mesh, assembled rank by rank (owned rows) like
+ * orc_discretization_evaluate.  u, v: structural column vectors (Kss's column map); T: thermo
+ * column vector (Ktt's column map). */
+int orc_tsi_discretization_evaluate(int celltype, double E, double nu, double alpha, double T0,
+    double conduct, double timefac, double timefac_d, int64_t n_ele, const int64_t* ele_nodes,
+    const double* node_x, const int64_t* node_gid, const int32_t* node_owner, int64_t min_node_gid,
+    int nworkers, const double* u, const double* v, const double* T, orc_csr* Kss, orc_csr* Kst,
+    orc_csr* Kts, orc_csr* Ktt, double* fs, double* ft, int64_t* bad_ele);
 
 #ifdef __cplusplus
 }

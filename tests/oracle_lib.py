@@ -75,6 +75,10 @@ def load(path=None):
         ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int64, _i64p,
         ctypes.c_int64, _dp, _i64p, _i32p, ctypes.c_int64, ctypes.c_int, _dp,
         ctypes.POINTER(OrcCsr), _dp, _i64p]
+    lib.orc_tsi_discretization_evaluate.argtypes = (
+        [ctypes.c_int] + [ctypes.c_double] * 7 + [ctypes.c_int64, _i64p, _dp, _i64p, _i32p,
+                                                 ctypes.c_int64, ctypes.c_int, _dp, _dp, _dp]
+        + [ctypes.POINTER(OrcCsr)] * 4 + [_dp, _dp, _i64p])
     lib.orc_thermo_stvk_st_modulus.argtypes = [ctypes.c_double] * 3
     lib.orc_thermo_stvk_st_modulus.restype = ctypes.c_double
     lib.orc_tsi_solid_evaluate.argtypes = [ctypes.c_int] + [ctypes.c_double] * 4 + [_dp] * 6

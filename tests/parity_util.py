@@ -59,3 +59,53 @@ def oracle_evaluate(mesh, kinem, E, nu, u_col, want_k=True, nworkers=1, min_node
 def rel_err(a, b):
     nb = np.linalg.norm(b)
     return np.linalg.norm(a - b) / (nb if nb > 0 else 1.0)
+
+
+def _csr(n_rows, rowptr, cols, vals, row_gid, col_gid):
+    row_lid, col_lid, max_gid = gid_maps(np.asarray(row_gid), np.asarray(col_gid))
+    c = orc.OrcCsr()
+    c.n_rows = n_rows
+    c.rowptr = rowptr.ctypes.data_as(orc._i64p)
+    c.col_lid = cols.ctypes.data_as(orc._i32p)
+    c.vals = vals.ctypes.data_as(orc._dp)
+    c.row_lid_of_gid = row_lid.ctypes.data_as(orc._i32p)
+    c.col_lid_of_gid = col_lid.ctypes.data_as(orc._i32p)
+    c.max_gid = max_gid
+    return c, (row_lid, col_lid)
+
+
+def oracle_tsi_evaluate(mesh, g, E, nu, alpha, T0, conduct, timefac, timefac_d, u_col, v_col,
+                        T_node, nworkers=1, min_node_gid=0):
+    """Oracle TSI::Monolithic element loop (orc_tsi_discretization_evaluate) on a BoxMesh rank and
+    its TsiGraph: returns (err, Kss, Kst, Kts, Ktt values in the graphs' CSR order, f_s, f_t).
+    T_node: nodal temperatures (node order of the mesh)."""
+    lib = orc.load()
+    row_s, col_s = mesh.row_gid, mesh.col_gid
+    # thermo maps: one DOF per node, gid = structural gid / 3 (node order kept)
+    row_t, col_t = row_s[::3] // 3, col_s[::3] // 3
+    vals = [np.zeros(mesh.nnz), np.zeros(g.nnz_st), np.zeros(g.nnz_ts), np.zeros(g.nnz_tt)]
+    keep = []
+    css, k1 = _csr(mesh.n_rows, mesh.rowptr, mesh.col_lid, vals[0], row_s, col_s)
+    cst, k2 = _csr(mesh.n_rows, g.rowptr_st, g.col_st, vals[1], row_s, col_t)
+    cts, k3 = _csr(g.n_rows_t, g.rowptr_ts, g.col_ts, vals[2], row_t, col_s)
+    ctt, k4 = _csr(g.n_rows_t, g.rowptr_tt, g.col_tt, vals[3], row_t, col_t)
+    keep += [k1, k2, k3, k4]
+    T_col = np.zeros(g.n_cols_t)
+    T_col[g.node_dof_col_t] = T_node
+    fs, ft = np.zeros(mesh.n_rows), np.zeros(g.n_rows_t)
+    owned = mesh.node_dof_row >= 0
+    owner = np.full(mesh.n_node, -1, dtype=np.int32)
+    idx = np.nonzero(owned)[0]
+    owner[idx] = (np.arange(len(idx)) * nworkers // max(len(idx), 1)).astype(np.int32)
+    en = mesh.ele_nodes.astype(np.int64)
+    bad = ctypes.c_int64(-1)
+    u_col = np.ascontiguousarray(u_col, dtype=np.float64)
+    v_col = np.ascontiguousarray(v_col, dtype=np.float64)
+    err = lib.orc_tsi_discretization_evaluate(
+        mesh.celltype, E, nu, alpha, T0, conduct, timefac, timefac_d, mesh.n_ele,
+        en.ctypes.data_as(orc._i64p), np.ascontiguousarray(mesh.node_x).ctypes.data_as(orc._dp),
+        mesh.node_gid.ctypes.data_as(orc._i64p), owner.ctypes.data_as(orc._i32p), min_node_gid,
+        nworkers, u_col.ctypes.data_as(orc._dp), v_col.ctypes.data_as(orc._dp),
+        T_col.ctypes.data_as(orc._dp), ctypes.byref(css), ctypes.byref(cst), ctypes.byref(cts),
+        ctypes.byref(ctt), fs.ctypes.data_as(orc._dp), ft.ctypes.data_as(orc._dp), ctypes.byref(bad))
+    return (err,) + tuple(vals) + (fs, ft)

@@ -418,3 +418,24 @@ def test_tsi_fused_full_size_properties():
     Kst = sp.csr_matrix((r["Kst"], g.col_st, g.rowptr_st), shape=(mesh.n_rows, g.n_cols_t))
     assert _rel(Ktt @ Tn, r["fT"]) <= 1e-12
     assert _rel(Kss @ u + Kst @ (Tn - T0), r["fs"]) <= 1e-12
+
+
+
+@pytest.mark.parametrize("nranks,nworkers", [(1, 1), (1, 4), (2, 3)])
+def test_oracle_tsi_discretization_loop(nranks, nworkers):
+    """orc_tsi_discretization_evaluate (the C loop the TSI CPU baseline times) equals the
+    per-element Python assembly of the same oracle element routines."""
+    from parity_util import oracle_tsi_evaluate
+    for r in range(nranks):
+        mesh = fcg.BoxMesh(fcg.HEX8, (4, 3, 3), jitter=0.1, rank=r, nranks=nranks)
+        g = fcg.TsiGraph(mesh)
+        u, v, Tn = _fields(mesh)
+        ref = _oracle_blocks(mesh, g, u, v, Tn)
+        err, Kss, Kst, Kts, Ktt, fs, fT = oracle_tsi_evaluate(mesh, g, E, NU, ALPHA, T0, COND, 1.0,
+                                                              1.0 / DT, u, v, Tn, nworkers=nworkers)
+        assert err == 0
+        for got, (D, rp, cl) in zip((Kss, Kst, Kts, Ktt),
+                                    ((ref[0], mesh.rowptr, mesh.col_lid), (ref[1], g.rowptr_st, g.col_st),
+                                     (ref[2], g.rowptr_ts, g.col_ts), (ref[3], g.rowptr_tt, g.col_tt))):
+            assert _rel(got, _csr_vals(D, rp, cl)) <= 1e-13
+        assert _rel(fs, ref[4]) <= 1e-13 and _rel(fT, ref[5]) <= 1e-13
