@@ -425,7 +425,8 @@ bool build_colored_plan(const fcg_desc* d, ColorHost& P, std::string& why)
 
 void free_mesh(fcg::DeviceMesh& m)
 {
-  void* ptrs[] = {m.ele_nodes, m.ele_gid, m.node_x, m.node_dof_col, m.inc_of, m.inc_ptr,
+  void* ptrs[] = {m.rec_ptr, m.rec_row0, m.rec_meta, m.rec_ele, m.rec_a, m.rec_tmap, m.ele_x,
+      m.ele_dof, m.ele_nodes, m.ele_gid, m.node_x, m.node_dof_col, m.inc_of, m.inc_ptr,
       m.rownode_row0, m.inc_pos, m.rowptr, m.scratch, m.err, m.elem_at, m.lat_x, m.lat_dof,
       m.plane_rec,
       m.tables, m.stamps, m.col_lid, m.diag_pos, m.pcg_work, m.col_ele, m.ele_ft, m.inc_row0};
@@ -562,7 +563,7 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
   StructHost sp;
   std::string why;
   bool structured = false;
-  if (d->path != FCG_PATH_GENERAL && d->material == FCG_MAT_STVK)
+  if (d->path != FCG_PATH_GENERAL && d->path != FCG_PATH_GATHER && d->material == FCG_MAT_STVK)
   {
     // compute units of the target device (the segment count depends on it; 256 when the device
     // cannot be queried, e.g. plan checks on a host without GPU)
@@ -600,6 +601,14 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
     set_create_error("the colour-ordered path is implemented for hex27");
     return FCG_ERR_ARG;
   }
+  // --- node-row gather: hex8 StVK meshes without a verified lattice (AUTO), or on request
+  if (d->path == FCG_PATH_GATHER && (d->celltype != FCG_HEX8 || d->material != FCG_MAT_STVK))
+  {
+    set_create_error("the gather path is implemented for hex8 with StVenantKirchhoff");
+    return FCG_ERR_ARG;
+  }
+  bool gather = !structured && d->celltype == FCG_HEX8 && d->material == FCG_MAT_STVK &&
+                (d->path == FCG_PATH_GATHER || d->path == FCG_PATH_AUTO);
 
   // --- incidences grouped by owned node (general path)
   std::vector<int64_t> inc_ptr(nrn + 1, 0);
@@ -663,6 +672,16 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
   if (!err.empty())
   {
     set_create_error(err);
+    return FCG_ERR_ARG;
+  }
+  // the gather path addresses a row by node triples (one byte each): every element node's columns
+  // must start a triple of the row, which holds when the row is made of node DOF triples only
+  if (gather)
+    for (int64_t i = 0; i < n_inc * npe && gather; ++i)
+      if (inc_pos[i] % 3 != 0) gather = false;
+  if (!gather && d->path == FCG_PATH_GATHER)
+  {
+    set_create_error("gather path: a row holds columns that are not node DOF triples");
     return FCG_ERR_ARG;
   }
 
@@ -782,6 +801,71 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
     chk(upload(&m.col_ele, cp.col_ele.data(), d->n_ele, bytes));
     chk(upload(&m.ele_ft, cp.ft.data(), d->n_ele, bytes));
     for (int c = 0; c < 9; ++c) m.color_ptr[c] = cp.color_ptr[c];
+  }
+  else if (gather)
+  {
+    m.path = FCG_PATH_GATHER;
+    // records of <= 8 incidences per row node (a node without elements keeps one empty record,
+    // which zeroes its rows under OVERWRITE)
+    std::vector<int64_t> rec_ptr(nrn + 1, 0);
+    for (int64_t r = 0; r < nrn; ++r)
+      rec_ptr[r + 1] = rec_ptr[r] + std::max<int64_t>(1, (inc_ptr[r + 1] - inc_ptr[r] + 7) / 8);
+    const int64_t n_rec = rec_ptr[nrn];
+    m.n_rec = n_rec;
+    std::vector<int32_t> rec_row0(n_rec), rec_meta(n_rec), rec_ele(n_rec * 8, -1);
+    std::vector<uint8_t> rec_a(n_rec * 8, 0);
+    std::vector<uint32_t> rec_tmap(n_rec * 32, 0x88888888u);
+    parallel_for(nrn, [&](int64_t r) {
+      const int64_t nr = rec_ptr[r + 1] - rec_ptr[r];
+      for (int64_t i = 0; i < nr; ++i)
+      {
+        const int64_t R = rec_ptr[r] + i;
+        const int64_t k0 = inc_ptr[r] + 8 * i;
+        const int ns = int(std::min<int64_t>(8, std::max<int64_t>(0, inc_ptr[r + 1] - k0)));
+        rec_row0[R] = row0[r];
+        rec_meta[R] = ns | (i == 0 ? 16 : 0) | (i == nr - 1 ? 32 : 0);
+        // per column triple t of the rows: which element node of slot s lands there (nibble s;
+        // 8 = none) -- stage 4 of the kernel sums a triple's blocks in slot (element) order
+        for (int s = 0; s < ns; ++s)
+        {
+          rec_ele[R * 8 + s] = inc_ele[k0 + s];
+          rec_a[R * 8 + s] = inc_a[k0 + s];
+          for (int b = 0; b < 8; ++b)
+          {
+            uint32_t& w = rec_tmap[R * 32 + inc_pos[(k0 + s) * 8 + b] / 3];
+            w = (w & ~(15u << (4 * s))) | (uint32_t(b) << (4 * s));
+          }
+        }
+      }
+    });
+    std::vector<double> ex(d->n_ele * 24);
+    std::vector<int32_t> edof(d->n_ele * 8);
+    parallel_for(d->n_ele, [&](int64_t e) {
+      for (int b = 0; b < 8; ++b)
+      {
+        const int32_t nd = d->ele_nodes[e * 8 + b];
+        for (int k = 0; k < 3; ++k) ex[e * 24 + 3 * b + k] = d->node_x[3 * int64_t(nd) + k];
+        edof[e * 8 + b] = d->node_dof_col[nd];
+      }
+    });
+    chk(upload(&m.rec_ptr, rec_ptr.data(), nrn + 1, bytes));
+    chk(upload(&m.rec_row0, rec_row0.data(), n_rec, bytes));
+    chk(upload(&m.rec_meta, rec_meta.data(), n_rec, bytes));
+    chk(upload(&m.rec_ele, rec_ele.data(), n_rec * 8, bytes));
+    chk(upload(&m.rec_a, rec_a.data(), n_rec * 8, bytes));
+    chk(upload(&m.rec_tmap, rec_tmap.data(), n_rec * 32, bytes));
+    chk(upload(&m.ele_x, ex.data(), d->n_ele * 24, bytes));
+    chk(upload(&m.ele_dof, edof.data(), d->n_ele * 8, bytes));
+    // Gauss points of the hex8 stiffness rule: xi, eta, zeta, weight
+    std::vector<double> tab(32);
+    double xi[81], w[27];
+    fcg::gauss_rule(fcg::kHex8, xi, w);
+    for (int g = 0; g < 8; ++g)
+    {
+      for (int k = 0; k < 3; ++k) tab[4 * g + k] = xi[3 * g + k];
+      tab[4 * g + 3] = w[g];
+    }
+    chk(upload(&m.tables, tab.data(), int64_t(tab.size()), bytes));
   }
   else
   {
@@ -997,6 +1081,12 @@ int fcg_evaluate_device(fcg_ctx* ctx, int action, int mode, const double* d_u_co
     if (he == hipSuccess)
       he = fcg::launch_element_colored(m, d_u_col, want_k, mode == FCG_OVERWRITE, d_K_vals,
           d_fint_row, s);
+    if (T.enabled && he == hipSuccess) he = hipEventRecord(T.ev[1], s);
+  }
+  else if (m.path == FCG_PATH_GATHER)
+  {
+    if (he == hipSuccess)
+      he = fcg::launch_gather_h8(m, d_u_col, want_k, mode == FCG_OVERWRITE, d_K_vals, d_fint_row, s);
     if (T.enabled && he == hipSuccess) he = hipEventRecord(T.ev[1], s);
   }
   else

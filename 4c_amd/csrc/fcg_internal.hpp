@@ -47,6 +47,17 @@ struct DeviceMesh {
   uint8_t* ele_ft = nullptr;        // [n_ele] first-touch bits (see fcg_kernels.hip)
   int32_t* inc_row0 = nullptr;      // [n_inc] row LID of the incidence's node
 
+  // node-row gather plan (hex8, FCG_PATH_GATHER): a row node's incidences in records of <= 8
+  int64_t n_rec = 0;
+  int64_t* rec_ptr = nullptr;       // [n_rownodes+1] records of each row node
+  int32_t* rec_row0 = nullptr;      // [n_rec] first row LID of the record's node
+  int32_t* rec_meta = nullptr;      // [n_rec] slots | first record << 4 | last record << 5
+  int32_t* rec_ele = nullptr;       // [n_rec][8] element of each slot, -1 = empty
+  uint8_t* rec_a = nullptr;         // [n_rec][8] local node of the row node in the slot's element
+  uint32_t* rec_tmap = nullptr;     // [n_rec][32] per column triple: slot s's element node in nibble s (8 = none)
+  double* ele_x = nullptr;          // [n_ele][8][3] element node coordinates
+  int32_t* ele_dof = nullptr;       // [n_ele][8] column LID of each element node's first DOF
+
   // structured (row-block sweep) plan, hex8 only
   int path = FCG_PATH_GENERAL;
   int32_t tiles_x = 0, tiles_y = 0, tiles_z = 0, seg_planes = 0;
@@ -121,6 +132,10 @@ hipError_t launch_element_colored(const DeviceMesh& m, const double* d_u_col, bo
     bool overwrite, double* d_K, double* d_fint, hipStream_t stream);
 hipError_t launch_assemble(const DeviceMesh& m, bool want_k, bool overwrite, double* d_K,
     double* d_fint, hipStream_t stream);
+// Node-row gather (FCG_PATH_GATHER, hex8 StVK on any mesh): one wavefront per owned row node
+// (fcg_gather.hip).
+hipError_t launch_gather_h8(const DeviceMesh& m, const double* d_u_col, bool want_k, bool overwrite,
+    double* d_K, double* d_fint, hipStream_t stream);
 
 }  // namespace fcg
 

@@ -21,7 +21,7 @@ HEX8, HEX27 = 0, 1
 LINEAR, TOTLAG = 0, 1
 CALC_NLNSTIFF, CALC_INTERNALFORCE = 0, 1
 ACCUMULATE, OVERWRITE = 0, 1
-PATH_AUTO, PATH_GENERAL, PATH_STRUCTURED, PATH_COLORED = 0, 1, 2, 3
+PATH_AUTO, PATH_GENERAL, PATH_STRUCTURED, PATH_COLORED, PATH_GATHER = 0, 1, 2, 3, 4
 MAT_STVK, MAT_ELASTHYPER_COUPNEOHOOKE = 0, 1
 TSI_STRUCT_FORCE, TSI_STIFFTEMP, TSI_THERMO_FINTCOND, TSI_COUPLTANG = 1, 2, 4, 8
 TSI_ALL = 15
@@ -349,6 +349,35 @@ class Discretization:
         d.path = path
         d.material = material
         return d
+
+    @staticmethod
+    def renumbered(box, seed=0):
+        """A single-rank box mesh as an input-file mesh would arrive: random node and element
+        numbering (DOF LID = 3 * node), no lattice hint; same geometry, graph and element
+        orientation.  Vectorised, for benchmark-sized meshes."""
+        assert box.n_rows == box.n_cols and np.array_equal(box.node_dof_col, 3 * np.arange(box.n_node))
+        rng = np.random.default_rng(seed)
+        nn = box.n_node
+        perm = rng.permutation(nn)                 # new number of old node
+        inv = np.argsort(perm)                     # old node of new number
+        en = perm[box.ele_nodes][rng.permutation(box.n_ele)]
+        X = np.empty_like(box.node_x)
+        X[perm] = box.node_x
+        rp = box.rowptr
+        cnt = (rp[1::3][:nn] - rp[0::3][:nn]) // 3  # neighbour nodes of each old node
+        cnt_new = cnt[inv]
+        start = np.concatenate([[0], np.cumsum(cnt_new)])
+        owner = np.repeat(np.arange(nn), cnt_new)
+        k = np.arange(start[-1]) - start[owner]
+        nb = perm[box.col_lid[rp[3 * inv[owner]] + 3 * k] // 3]
+        nb = nb[np.lexsort((nb, owner))]
+        rowlen = np.repeat(3 * cnt_new, 3)
+        rowptr = np.concatenate([[0], np.cumsum(rowlen)]).astype(np.int64)
+        row = np.repeat(np.arange(3 * nn), rowlen)
+        off = np.arange(rowptr[-1]) - rowptr[row]
+        col = (3 * nb[start[row // 3] + off // 3] + off % 3).astype(np.int32)
+        dof = 3 * np.arange(nn, dtype=np.int32)
+        return Discretization(box.celltype, en, X, dof, dof, rowptr, col)
 
 
 def _neumann(entry, celltype, conn, node_x, node_dof_row, onoff, val, funct, fn, time, fext):

@@ -343,3 +343,83 @@ def test_negative_nodal_jacobian_all_paths(celltype, path):
     assert ei.value.code == 1 and ei.value.bad_ele_gid == min(rejected), (ei.value, rejected)
     mesh.node_x[:] = good_x
     _run_gpu(mesh, kinem, mesh.u_col(1e-3), path=path)
+
+
+# ------------------------------------------------------------------ hex8 node-row gather path
+def _scrambled_hex8(iv, seed, duplicate=0):
+    """A jittered box turned into an 'input-file' mesh: random node numbering, random element order,
+    every element's node list rotated about its local zeta axis (same orientation, different local
+    numbering), no lattice hint; `duplicate` elements repeated (their nodes then belong to more
+    than 8 elements, the gather's multi-chunk case)."""
+    box = fcg.BoxMesh(fcg.HEX8, iv, jitter=0.1, seed=seed)
+    rng = np.random.default_rng(seed)
+    perm = rng.permutation(box.n_node)
+    inv = np.empty_like(perm)
+    inv[perm] = np.arange(box.n_node)
+    X = box.node_x[perm]
+    en = inv[box.ele_nodes]
+    rot = rng.integers(0, 4, size=len(en))
+    out = []
+    for e, r in zip(en, rot):
+        bot, top = list(e[:4]), list(e[4:])
+        out.append(bot[r:] + bot[:r] + top[r:] + top[:r])
+    out = np.array(out)
+    if duplicate:
+        out = np.vstack([out, out[rng.choice(len(out), duplicate, replace=False)]])
+    out = out[rng.permutation(len(out))]
+    return fcg.Discretization.from_elements(fcg.HEX8, out, X)
+
+
+@pytest.mark.parametrize("kinem", [fcg.LINEAR, fcg.TOTLAG])
+@pytest.mark.parametrize("iv,dup", [((6, 5, 4), 0), ((3, 3, 2), 5), ((1, 1, 1), 0)])
+def test_gather_path_unstructured_matches_oracle(kinem, iv, dup):
+    import oracle_lib as orc
+    _dev()
+    dis = _scrambled_hex8(iv, 3 + dup, duplicate=dup)
+    u = np.random.default_rng(1).standard_normal(dis.n_cols) * (1e-3 if kinem == fcg.LINEAR else 5e-2)
+    # the oracle on the same discretization (one rank: every node owned)
+    mesh_like = type("M", (), {})()
+    mesh_like.row_gid = mesh_like.col_gid = np.arange(dis.n_cols, dtype=np.int32)
+    mesh_like.nnz, mesh_like.n_rows, mesh_like.rowptr, mesh_like.col_lid = dis.nnz, dis.n_rows, dis.rowptr, dis.col_lid
+    mesh_like.celltype, mesh_like.n_ele, mesh_like.ele_nodes = fcg.HEX8, dis.n_ele, dis.ele_nodes
+    mesh_like.n_node, mesh_like.node_x, mesh_like.node_dof_row = dis.n_node, dis.node_x, dis.node_dof_row
+    mesh_like.node_gid = np.arange(dis.n_node, dtype=np.int64)
+    err, _, Kr, fr = oracle_evaluate(mesh_like, kinem, E, NU, u)
+    assert err == 0
+    for path in (fcg.PATH_AUTO, fcg.PATH_GATHER, fcg.PATH_GENERAL):
+        Kg, fg, ev = _run_gpu(dis, kinem, u, path=path)
+        assert ev.info.path == (fcg.PATH_GENERAL if path == fcg.PATH_GENERAL else fcg.PATH_GATHER)
+        _check(Kg, fg, Kr, fr)
+    _, fi, _ = _run_gpu(dis, kinem, u, action=fcg.CALC_INTERNALFORCE, path=fcg.PATH_GATHER)
+    assert rel_err(fi, fr) <= 1e-10
+    assert orc is not None
+
+
+@pytest.mark.parametrize("kinem", [fcg.LINEAR, fcg.TOTLAG])
+def test_gather_path_box_ranks_accumulate_reproducible(kinem):
+    """Box ranks forced onto the gather path: owned rows equal the structured sweep's, ACCUMULATE
+    adds, and two evaluations agree bit for bit."""
+    for r in range(3):
+        m = fcg.BoxMesh(fcg.HEX8, (7, 5, 6), jitter=0.1, rank=r, nranks=3)
+        u = m.u_col(1e-3 if kinem == fcg.LINEAR else 5e-2)
+        Ks, fs, _ = _run_gpu(m, kinem, u, path=fcg.PATH_STRUCTURED)
+        K1, f1, ev = _run_gpu(m, kinem, u, path=fcg.PATH_GATHER)
+        assert ev.info.path == fcg.PATH_GATHER
+        _check(K1, f1, Ks, fs)
+        K2, f2, _ = _run_gpu(m, kinem, u, ev=ev)
+        assert np.array_equal(K1, K2) and np.array_equal(f1, f2)
+        rng = np.random.default_rng(r)
+        K0, f0 = rng.standard_normal(m.nnz), rng.standard_normal(m.n_rows)
+        Ka, fa, _ = _run_gpu(m, kinem, u, mode=fcg.ACCUMULATE, K0=K0.copy(), f0=f0.copy(), ev=ev)
+        np.testing.assert_allclose(Ka, K0 + K1, rtol=0, atol=1e-13 * np.abs(K1).max())
+        np.testing.assert_allclose(fa, f0 + f1, rtol=0, atol=1e-13 * np.abs(f1).max())
+
+
+def test_gather_path_negative_jacobian():
+    _dev()
+    dis = _scrambled_hex8((3, 2, 2), 9)
+    dis.ele_gid = np.arange(50, 50 + dis.n_ele, dtype=np.int32)
+    dis.node_x[:, 0] *= -1.0
+    with pytest.raises(fcg.FcgError) as ei:
+        _run_gpu(dis, fcg.LINEAR, np.zeros(dis.n_cols), path=fcg.PATH_GATHER)
+    assert ei.value.code == 1 and ei.value.bad_ele_gid == 50

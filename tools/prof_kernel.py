@@ -18,7 +18,8 @@ ap.add_argument("--reps", type=int, default=3)
 a = ap.parse_args()
 ct = fcg.HEX8 if a.celltype == "hex8" else fcg.HEX27
 kin = fcg.LINEAR if a.kinem == "linear" else fcg.TOTLAG
-path = {"auto": fcg.PATH_AUTO, "general": fcg.PATH_GENERAL, "structured": fcg.PATH_STRUCTURED}[a.path]
+path = {"auto": fcg.PATH_AUTO, "general": fcg.PATH_GENERAL, "structured": fcg.PATH_STRUCTURED,
+        "gather": fcg.PATH_GATHER}[a.path]
 m = fcg.BoxMesh(ct, (a.n, a.n, a.n), jitter=0.1 if ct == fcg.HEX8 else 0.02)
 ev = fcg.Evaluator(m, kinematics=kin, path=path)
 dev = torch.device("cuda:0")
