@@ -425,7 +425,7 @@ bool build_colored_plan(const fcg_desc* d, ColorHost& P, std::string& why)
 
 void free_mesh(fcg::DeviceMesh& m)
 {
-  void* ptrs[] = {m.rec_ptr, m.rec_row0, m.rec_meta, m.rec_ele, m.rec_a, m.rec_tmap, m.ele_x,
+  void* ptrs[] = {m.gather_dummy, m.multi_ptr, m.rec_row0, m.rec_meta, m.rec_base, m.rec_ele, m.rec_a, m.rec_tmap, m.ele_x,
       m.ele_dof, m.ele_nodes, m.ele_gid, m.node_x, m.node_dof_col, m.inc_of, m.inc_ptr,
       m.rownode_row0, m.inc_pos, m.rowptr, m.scratch, m.err, m.elem_at, m.lat_x, m.lat_dof,
       m.plane_rec,
@@ -806,24 +806,41 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
   {
     m.path = FCG_PATH_GATHER;
     // records of <= 8 incidences per row node (a node without elements keeps one empty record,
-    // which zeroes its rows under OVERWRITE)
-    std::vector<int64_t> rec_ptr(nrn + 1, 0);
+    // which zeroes its rows under OVERWRITE): first one record per node with <= 8 elements, in
+    // row order, then the records of the other nodes, node by node
+    std::vector<int64_t> rec_start(nrn), nrec(nrn), multi_ptr(1, 0);
+    int64_t n_single = 0;
     for (int64_t r = 0; r < nrn; ++r)
-      rec_ptr[r + 1] = rec_ptr[r] + std::max<int64_t>(1, (inc_ptr[r + 1] - inc_ptr[r] + 7) / 8);
-    const int64_t n_rec = rec_ptr[nrn];
+    {
+      nrec[r] = std::max<int64_t>(1, (inc_ptr[r + 1] - inc_ptr[r] + 7) / 8);
+      if (nrec[r] == 1) rec_start[r] = n_single++;
+    }
+    for (int64_t r = 0; r < nrn; ++r)
+      if (nrec[r] > 1)
+      {
+        rec_start[r] = n_single + multi_ptr.back();
+        multi_ptr.push_back(multi_ptr.back() + nrec[r]);
+      }
+    for (auto& v : multi_ptr) v += n_single;
+    const int64_t n_rec = multi_ptr.back();
     m.n_rec = n_rec;
+    m.n_rec_single = n_single;
+    m.n_multi = int64_t(multi_ptr.size()) - 1;
     std::vector<int32_t> rec_row0(n_rec), rec_meta(n_rec), rec_ele(n_rec * 8, -1);
+    std::vector<int64_t> rec_base(n_rec);
     std::vector<uint8_t> rec_a(n_rec * 8, 0);
     std::vector<uint32_t> rec_tmap(n_rec * 32, 0x88888888u);
     parallel_for(nrn, [&](int64_t r) {
-      const int64_t nr = rec_ptr[r + 1] - rec_ptr[r];
+      const int64_t nr = nrec[r];
       for (int64_t i = 0; i < nr; ++i)
       {
-        const int64_t R = rec_ptr[r] + i;
+        const int64_t R = rec_start[r] + i;
         const int64_t k0 = inc_ptr[r] + 8 * i;
         const int ns = int(std::min<int64_t>(8, std::max<int64_t>(0, inc_ptr[r + 1] - k0)));
         rec_row0[R] = row0[r];
-        rec_meta[R] = ns | (i == 0 ? 16 : 0) | (i == nr - 1 ? 32 : 0);
+        rec_meta[R] = ns | (i == 0 ? 16 : 0) | (i == nr - 1 ? 32 : 0) |
+                      int32_t(d->rowptr[row0[r] + 1] - d->rowptr[row0[r]]) << 8;
+        rec_base[R] = d->rowptr[row0[r]];
         // per column triple t of the rows: which element node of slot s lands there (nibble s;
         // 8 = none) -- stage 4 of the kernel sums a triple's blocks in slot (element) order
         for (int s = 0; s < ns; ++s)
@@ -848,14 +865,16 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
         edof[e * 8 + b] = d->node_dof_col[nd];
       }
     });
-    chk(upload(&m.rec_ptr, rec_ptr.data(), nrn + 1, bytes));
+    chk(upload(&m.multi_ptr, multi_ptr.data(), int64_t(multi_ptr.size()), bytes));
     chk(upload(&m.rec_row0, rec_row0.data(), n_rec, bytes));
     chk(upload(&m.rec_meta, rec_meta.data(), n_rec, bytes));
+    chk(upload(&m.rec_base, rec_base.data(), n_rec, bytes));
     chk(upload(&m.rec_ele, rec_ele.data(), n_rec * 8, bytes));
     chk(upload(&m.rec_a, rec_a.data(), n_rec * 8, bytes));
     chk(upload(&m.rec_tmap, rec_tmap.data(), n_rec * 32, bytes));
     chk(upload(&m.ele_x, ex.data(), d->n_ele * 24, bytes));
     chk(upload(&m.ele_dof, edof.data(), d->n_ele * 8, bytes));
+    chk(upload<double>(&m.gather_dummy, nullptr, 4, bytes));
     // Gauss points of the hex8 stiffness rule: xi, eta, zeta, weight
     std::vector<double> tab(32);
     double xi[81], w[27];

@@ -63,7 +63,7 @@ struct GatherShared {
   double C[kNs][8][24];              // trilinear coefficients [x | x_cur][slot][3 k + d]
   union {
     double NX[8][200];               // N_XYZ [slot][25 g + 3 node + d]
-    double blk[64][9];               // lane (slot, b): K_ab (column-major)
+    double blk[65][9];               // lane (slot, b): K_ab (column-major); row 64 = zeros
   } nb;
   double row[3 * kMaxRow];           // image of the node's rows (nodes with > 8 elements)
   double gp[8][4];                   // Gauss point coordinates | weight
@@ -71,21 +71,23 @@ struct GatherShared {
 };
 
 struct GatherArgs {
-  int64_t n_rownodes;
-  const int64_t* rec_ptr;    // [n_rownodes + 1] records of each row node
+  int64_t n_single;          // records [0, n_single): nodes with <= 8 elements, one record each
+  int64_t n_multi;           // nodes with more elements; their records follow
+  const int64_t* multi_ptr;  // [n_multi + 1] record range of each such node
   const int32_t* rec_row0;   // [n_rec] first row LID of the record's node
-  const int32_t* rec_meta;   // [n_rec] nslot | first << 4 | last << 5
+  const int32_t* rec_meta;   // [n_rec] nslot | first << 4 | last << 5 | row length << 8
+  const int64_t* rec_base;   // [n_rec] CSR offset of the node's first row
   const int32_t* rec_ele;    // [n_rec][8] element (-1 = empty slot)
   const uint8_t* rec_a;      // [n_rec][8] local node of the row node in the slot's element
   const uint32_t* rec_tmap;  // [n_rec][32] per column triple of the rows: slot s's node in nibble s
   const double* ele_x;       // [n_ele][8][3]
   const int32_t* ele_dof;    // [n_ele][8] column LID of each node's first DOF
-  const int64_t* rowptr;
   const double* u_col;
   const double* gp;          // Gauss points [8][4]: xi, eta, zeta, weight
   double* K;
   double* fint;
   int32_t* err;
+  double* dummy;             // [3] target of the stores of a row without columns
   StVK mat;
 };
 
@@ -95,15 +97,16 @@ __host__ __device__ constexpr double h8_sy(int n) { return (n & 3) >= 2 ? 1.0 : 
 __host__ __device__ constexpr double h8_sz(int n) { return n >= 4 ? 1.0 : -1.0; }
 
 // column-major Jacobian J[dir + 3 comp] = d x_comp / d xi_dir at (x, y, z) from the coefficients
+// (stored as c_k / 8)
 __device__ inline void h8_jac(const double* c, double x, double y, double z, double* J)
 {
   const double yz = y * z, xz = x * z, xy = x * y;
 #pragma unroll
   for (int d = 0; d < 3; ++d)
   {
-    J[0 + 3 * d] = 0.125 * (c[3 + d] + y * c[12 + d] + z * c[18 + d] + yz * c[21 + d]);
-    J[1 + 3 * d] = 0.125 * (c[6 + d] + x * c[12 + d] + z * c[15 + d] + xz * c[21 + d]);
-    J[2 + 3 * d] = 0.125 * (c[9 + d] + y * c[15 + d] + x * c[18 + d] + xy * c[21 + d]);
+    J[0 + 3 * d] = c[3 + d] + y * c[12 + d] + z * c[18 + d] + yz * c[21 + d];
+    J[1 + 3 * d] = c[6 + d] + x * c[12 + d] + z * c[15 + d] + xz * c[21 + d];
+    J[2 + 3 * d] = c[9 + d] + y * c[15 + d] + x * c[18 + d] + xy * c[21 + d];
   }
 }
 
@@ -114,57 +117,90 @@ __device__ inline double h8_det(const double* m)
 }
 
 struct RecRegs {
-  int32_t row0, meta, ele;  // ele, a: slot j's
-  int32_t a;
+  int32_t row0, meta;       // first row LID; nslot | first << 4 | last << 5 | row length << 8
+  int64_t base;             // CSR offset of the first row
+  int32_t ele, a;           // slot j's element (-1 = empty) and local node of the row node
   uint32_t tm;              // tmap word (lane & 31) of the record
 };
 
-template <int KIN, bool WANT_K, bool OVERWRITE>
+// sum over the 16 lanes of each DPP row (every lane of the row gets it): xor 1, xor 2, rotate 4, 8
+template <int CTRL>
+__device__ inline double dpp_mov(double v)
+{
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ inline double row_sum(double v)
+{
+  v += dpp_mov<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+  v += dpp_mov<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+  v += dpp_mov<0x124>(v);  // row_ror 4
+  v += dpp_mov<0x128>(v);  // row_ror 8
+  return v;
+}
+// wave sum in a fixed order (rows 0 + 16 + 32 + 48), uniform
+__device__ inline double wave_sum(double v)
+{
+  v = row_sum(v);
+  double r[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    r[k] = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), 16 * k),
+        __builtin_amdgcn_readlane(__double2loint(v), 16 * k));
+  return ((r[0] + r[1]) + r[2]) + r[3];
+}
+
+template <int KIN, bool WANT_K, bool OVERWRITE, bool MULTI>
 __global__ __launch_bounds__(64, KIN ? 1 : 2) void gather_h8_kernel(GatherArgs A)
 {
   __shared__ GatherShared<KIN> sh;
   const int lane = threadIdx.x;
   const int j = lane >> 3, q = lane & 7;  // slot, element node / Gauss point
   if (lane < 32) (&sh.gp[0][0])[lane] = A.gp[lane];
-  // XCD-contiguous node ranges: workgroup b runs on XCD b % 8 (round-robin dispatch); within the
-  // XCD's range every workgroup takes one contiguous block of row nodes
+  // XCD-contiguous ranges: workgroup b runs on XCD b % 8 (round-robin dispatch); within the XCD's
+  // range every workgroup takes one contiguous block -- of records (one per node) for nodes with
+  // <= 8 elements, of nodes for the others (MULTI)
+  const int64_t nwork = MULTI ? A.n_multi : A.n_single;
   const int64_t nwg = gridDim.x;
   const int xcd = int(blockIdx.x & 7u);
   const int64_t per_xcd = (nwg + 7 - xcd) / 8;
   const int64_t rank = blockIdx.x >> 3;
-  const int64_t chunk = (A.n_rownodes + 7) / 8;
-  const int64_t x0 = min(A.n_rownodes, int64_t(xcd) * chunk), x1 = min(A.n_rownodes, x0 + chunk);
+  const int64_t chunk = (nwork + 7) / 8;
+  const int64_t x0 = min(nwork, int64_t(xcd) * chunk), x1 = min(nwork, x0 + chunk);
   const int64_t sub = (x1 - x0 + per_xcd - 1) / per_xcd;
   const int64_t n0 = min(x1, x0 + rank * sub), n1 = min(x1, n0 + sub);
-  const int64_t R0 = A.rec_ptr[n0], R1 = A.rec_ptr[n1];
+  const int64_t R0 = MULTI ? A.multi_ptr[n0] : n0, R1 = MULTI ? A.multi_ptr[n1] : n1;
+  if (R0 >= R1) return;
 
+  // Loads are branch-free (indices clamped into range; an empty slot reads element 0, a record
+  // past the range re-reads the last one) and every record issues the same stores, so that the
+  // wait counts stay static: record i's words arrive three records ahead, its element data two,
+  // its displacements one, and no wait covers the stores of the record before.
   auto load_rec = [&](int64_t i) -> RecRegs {
-    RecRegs r{0, 0, -1, 0, 0u};
-    if (i < R1)
-    {
-      r.row0 = A.rec_row0[i];
-      r.meta = A.rec_meta[i];
-      r.ele = A.rec_ele[i * 8 + j];
-      r.a = A.rec_a[i * 8 + j];
-      r.tm = A.rec_tmap[i * 32 + (lane & 31)];
-    }
+    const int64_t k = min(i, R1 - 1);
+    RecRegs r;
+    r.row0 = A.rec_row0[k];
+    r.meta = A.rec_meta[k];
+    r.base = A.rec_base[k];
+    r.ele = A.rec_ele[k * 8 + j];
+    r.a = A.rec_a[k * 8 + j];
+    r.tm = A.rec_tmap[k * 32 + (lane & 31)];
     return r;
   };
   // element data of node q of slot j
   auto load_x = [&](const RecRegs& r, double* x, int32_t& dof) {
-    if (r.ele >= 0)
-    {
-      const double* p = A.ele_x + (int64_t(r.ele) * 8 + q) * 3;
-      x[0] = p[0];
-      x[1] = p[1];
-      x[2] = p[2];
-      dof = A.ele_dof[int64_t(r.ele) * 8 + q];
-    }
-    else
-    {
-      x[0] = x[1] = x[2] = 0.0;
-      dof = -1;
-    }
+    const int64_t el = max(r.ele, 0);
+    const double* p = A.ele_x + (el * 8 + q) * 3;
+    x[0] = p[0];
+    x[1] = p[1];
+    x[2] = p[2];
+    dof = A.ele_dof[el * 8 + q];
+  };
+  auto load_u = [&](int32_t dof, double* u) {
+    u[0] = A.u_col[dof];
+    u[1] = A.u_col[dof + 1];
+    u[2] = A.u_col[dof + 2];
   };
   // sign pattern of coefficient q over the nodes: bit n set = -x_n
   const bool ux = q == 1 || q == 4 || q == 6 || q == 7;
@@ -178,38 +214,36 @@ __global__ __launch_bounds__(64, KIN ? 1 : 2) void gather_h8_kernel(GatherArgs A
     negmask |= uint32_t(neg) << n;
   }
 
-  RecRegs cur = load_rec(R0), nxt = load_rec(R0 + 1);
-  double xc[3];
-  int32_t dofc;
+  RecRegs cur = load_rec(R0), nx1 = load_rec(R0 + 1), nx2 = load_rec(R0 + 2);
+  double xc[3], xn1[3], uc[3];
+  int32_t dofc, dof1;
   load_x(cur, xc, dofc);
+  load_x(nx1, xn1, dof1);
+  load_u(dofc, uc);
   double fA0 = 0.0, fA1 = 0.0, fA2 = 0.0;
+  int bad_code = 0, bad_ele = 0x7FFFFFFF;
+  // the prologue's loads have landed before the loop: the loop header then carries only the
+  // previous record's stores, and the waits inside stay at their static counts
+  __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   const double gx = sh.gp[q][0], gy = sh.gp[q][1], gz = sh.gp[q][2], gw = sh.gp[q][3];
   for (int64_t i = R0; i < R1; ++i)
   {
-    // in flight while this record computes: its displacements, the next record's element data,
-    // the record after that
-    double uc[3] = {0.0, 0.0, 0.0};
-    if (dofc >= 0)
-    {
-      uc[0] = A.u_col[dofc];
-      uc[1] = A.u_col[dofc + 1];
-      uc[2] = A.u_col[dofc + 2];
-    }
-    double xn[3];
-    int32_t dofn;
-    load_x(nxt, xn, dofn);
-    const RecRegs nn = load_rec(i + 2);
+    // in flight while this record computes: the next record's displacements, the element data of
+    // the one after, the words of the third
+    const RecRegs nx3 = load_rec(i + 3);
+    double xn2[3], u1[3];
+    int32_t dof2;
+    load_x(nx2, xn2, dof2);
+    load_u(dof1, u1);
 
     const bool first = (cur.meta >> 4) & 1, last = (cur.meta >> 5) & 1;
-    const bool single = first && last;
-    const int64_t base = A.rowptr[cur.row0];
-    const int len = int(A.rowptr[cur.row0 + 1] - base);
-    if (first)
+    const int64_t base = cur.base;
+    const int len = cur.meta >> 8;
+    if (MULTI && first)
     {
       fA0 = fA1 = fA2 = 0.0;
-      if (!single)
-        for (int v = lane; v < 3 * len; v += 64) sh.row[v] = 0.0;
+      for (int v = lane; v < 3 * len; v += 64) sh.row[v] = 0.0;
     }
     const int32_t e = cur.ele;
     const int a = cur.a;
@@ -239,9 +273,9 @@ __global__ __launch_bounds__(64, KIN ? 1 : 2) void gather_h8_kernel(GatherArgs A
           c1 += sg * sh.xa.X[s][j][3 * n + 1];
           c2 += sg * sh.xa.X[s][j][3 * n + 2];
         }
-        sh.C[s][j][3 * q + 0] = c0;
-        sh.C[s][j][3 * q + 1] = c1;
-        sh.C[s][j][3 * q + 2] = c2;
+        sh.C[s][j][3 * q + 0] = 0.125 * c0;
+        sh.C[s][j][3 * q + 1] = 0.125 * c1;
+        sh.C[s][j][3 * q + 2] = 0.125 * c2;
       }
     }
     __syncthreads();
@@ -262,16 +296,21 @@ __global__ __launch_bounds__(64, KIN ? 1 : 2) void gather_h8_kernel(GatherArgs A
       if (det == 0.0) bad = 2;
       const double fac = det * gw;
       // dN_n/dxi = sx (1 + sy eta)(1 + sz zeta) / 8, ...
+      // the 12 distinct products (1 +- eta)(1 +- zeta) / 8, ...; the node's sign is a negation
       const double xp = 1.0 + gx, xm = 1.0 - gx, yp = 1.0 + gy, ym = 1.0 - gy, zp = 1.0 + gz,
                    zm = 1.0 - gz;
+      const double hyp = 0.125 * yp, hym = 0.125 * ym, hxp = 0.125 * xp, hxm = 0.125 * xm;
+      const double pyz[2][2] = {{hym * zm, hym * zp}, {hyp * zm, hyp * zp}};
+      const double pxz[2][2] = {{hxm * zm, hxm * zp}, {hxp * zm, hxp * zp}};
+      const double pxy[2][2] = {{hxm * ym, hxm * yp}, {hxp * ym, hxp * yp}};
       double na[3] = {0.0, 0.0, 0.0};
 #pragma unroll
       for (int n = 0; n < 8; ++n)
       {
-        const double fx = h8_sx(n) > 0 ? xp : xm, fy = h8_sy(n) > 0 ? yp : ym, fz = h8_sz(n) > 0 ? zp : zm;
-        const double d0 = 0.125 * h8_sx(n) * (fy * fz);
-        const double d1 = 0.125 * h8_sy(n) * (fx * fz);
-        const double d2 = 0.125 * h8_sz(n) * (fx * fy);
+        const int ix = h8_sx(n) > 0, iy = h8_sy(n) > 0, iz = h8_sz(n) > 0;
+        const double d0 = ix ? pyz[iy][iz] : -pyz[iy][iz];
+        const double d1 = iy ? pxz[ix][iz] : -pxz[ix][iz];
+        const double d2 = iz ? pxy[ix][iy] : -pxy[ix][iy];
         const double n0 = J[0] * d0 + J[3] * d1 + J[6] * d2;
         const double n1 = J[1] * d0 + J[4] * d1 + J[7] * d2;
         const double n2 = J[2] * d0 + J[5] * d1 + J[8] * d2;
@@ -342,8 +381,8 @@ __global__ __launch_bounds__(64, KIN ? 1 : 2) void gather_h8_kernel(GatherArgs A
       }
       if (bad)
       {
-        atomicMax(&A.err[0], bad);
-        atomicMin(&A.err[1], e);
+        bad_code = max(bad_code, bad);
+        bad_ele = min(bad_ele, e);
       }
     }
     __syncthreads();
@@ -413,71 +452,68 @@ __global__ __launch_bounds__(64, KIN ? 1 : 2) void gather_h8_kernel(GatherArgs A
         Kb[2] += mu * H[5]; Kb[6] += mu * H[5];
       }
     }
-    // the record's part of f_A: a fixed butterfly over the wave
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1)
+    // the record's part of f_A: a fixed-order reduction over the wave
+    const double r0 = wave_sum(fp0), r1 = wave_sum(fp1), r2 = wave_sum(fp2);
+    if (MULTI)
     {
-      fp0 += __shfl_xor(fp0, o);
-      fp1 += __shfl_xor(fp1, o);
-      fp2 += __shfl_xor(fp2, o);
+      fA0 += r0;
+      fA1 += r1;
+      fA2 += r2;
     }
-    fA0 += fp0;
-    fA1 += fp1;
-    fA2 += fp2;
+    else
+    {
+      fA0 = r0;
+      fA1 = r1;
+      fA2 = r2;
+    }
     // 4. sum the blocks per row entry in slot order
+    // a node whose rows hold no column (len 0) stores into a dummy triple instead of branching
+    double* dst = len ? A.K + base : A.dummy;
     if (WANT_K)
     {
       __syncthreads();  // NX -> blk
 #pragma unroll
       for (int k = 0; k < 9; ++k) sh.nb.blk[lane][k] = Kb[k];
+      if (lane < 9) sh.nb.blk[64][lane] = 0.0;
       __syncthreads();
-      double* dst = A.K + base;
       // lane (triple t, half h): entries c = 2 e + h (column-major in the 3 x 3 block) of the
-      // triple's block, each summed over the slots in order
-      const int t = lane >> 1, h = lane & 1;
-      if (t < len / 3)
+      // triple's block, each summed over the slots in order.  Without MULTI and with OVERWRITE
+      // every lane stores five entries: lanes past the row's triples redo the last triple and the
+      // ninth entry stands in for the missing tenth (the same value to the same address).
+      const int ntrip = len / 3;
+      const int t = max(0, min(lane >> 1, ntrip - 1)), h = lane & 1;
+      const bool active = (lane >> 1) < ntrip;
       {
         const uint32_t tm = sh.tmap[t];
-        int off[8];
-        bool ok[8];
+        int off[8];  // block of slot sl aimed at triple t, or the zero row
 #pragma unroll
         for (int sl = 0; sl < 8; ++sl)
         {
           const uint32_t b = (tm >> (4 * sl)) & 15u;
-          ok[sl] = b < 8u;
-          off[sl] = 9 * (8 * sl + int(b & 7u));
+          off[sl] = 9 * (b < 8u ? 8 * sl + int(b) : 64);
         }
         const double* blk = &sh.nb.blk[0][0];
 #pragma unroll
-        for (int e = 0; e < 5; ++e)
+        for (int e5 = 0; e5 < 5; ++e5)
         {
-          const int c = h ? 2 * e + 1 : 2 * e;
-          if (c < 9)
-          {
-            double s = 0.0;
+          const int c = h ? min(2 * e5 + 1, 7) : 2 * e5;  // h = 1: entries 1, 3, 5, 7, 7
+          double x = blk[off[0] + c];
 #pragma unroll
-            for (int sl = 0; sl < 8; ++sl)
-            {
-              const double x = blk[off[sl] + c];
-              s += ok[sl] ? x : 0.0;
-            }
-            const int rr = h ? (2 * e + 1) % 3 : (2 * e) % 3;
-            const int cc = h ? (2 * e + 1) / 3 : (2 * e) / 3;
-            const int v = rr * len + 3 * t + cc;
-            if (single)
-            {
-              if (OVERWRITE)
-                __builtin_nontemporal_store(s, dst + v);
-              else
-                dst[v] += s;
-            }
-            else
-              sh.row[v] += s;
+          for (int sl = 1; sl < 8; ++sl) x += blk[off[sl] + c];
+          const int rr = c % 3, cc = c / 3;
+          const int v = rr * len + 3 * t + cc;
+          if (MULTI)
+          {
+            if (active && !(h && e5 == 4)) sh.row[v] += x;
           }
+          else if (OVERWRITE)
+            __builtin_nontemporal_store(x, dst + v);
+          else if (active && !(h && e5 == 4))
+            dst[v] += x;
         }
       }
-      // after the node's last record its image leaves contiguously
-      if (last && !single)
+      // a node with more records: its image leaves after the last one
+      if (MULTI && last)
       {
         __syncthreads();
         for (int v = lane; v < 3 * len; v += 64)
@@ -489,28 +525,38 @@ __global__ __launch_bounds__(64, KIN ? 1 : 2) void gather_h8_kernel(GatherArgs A
         }
       }
     }
-    if (last && lane == 0)
+    // f_A: lanes 0..2 (OVERWRITE without MULTI: every lane, lanes >= 2 all storing component 2)
     {
-      if (OVERWRITE)
+      const int comp = min(lane, 2);
+      const double fv = comp == 0 ? fA0 : (comp == 1 ? fA1 : fA2);
+      if (!MULTI && OVERWRITE)
+        A.fint[cur.row0 + comp] = fv;
+      else if ((!MULTI || last) && lane < 3)
       {
-        A.fint[cur.row0] = fA0;
-        A.fint[cur.row0 + 1] = fA1;
-        A.fint[cur.row0 + 2] = fA2;
-      }
-      else
-      {
-        A.fint[cur.row0] += fA0;
-        A.fint[cur.row0 + 1] += fA1;
-        A.fint[cur.row0 + 2] += fA2;
+        if (OVERWRITE)
+          A.fint[cur.row0 + comp] = fv;
+        else
+          A.fint[cur.row0 + comp] += fv;
       }
     }
     __syncthreads();
-    cur = nxt;
-    nxt = nn;
-    xc[0] = xn[0];
-    xc[1] = xn[1];
-    xc[2] = xn[2];
-    dofc = dofn;
+    cur = nx1;
+    nx1 = nx2;
+    nx2 = nx3;
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+    {
+      xc[k] = xn1[k];
+      xn1[k] = xn2[k];
+      uc[k] = u1[k];
+    }
+    dofc = dof1;
+    dof1 = dof2;
+  }
+  if (bad_code)
+  {
+    atomicMax(&A.err[0], bad_code);
+    atomicMin(&A.err[1], bad_ele);
   }
 }
 
@@ -519,46 +565,54 @@ __global__ __launch_bounds__(64, KIN ? 1 : 2) void gather_h8_kernel(GatherArgs A
 hipError_t launch_gather_h8(const DeviceMesh& m, const double* d_u_col, bool want_k, bool overwrite,
     double* d_K, double* d_fint, hipStream_t stream)
 {
-  if (m.n_rownodes == 0) return hipSuccess;
   GatherArgs a{};
-  a.n_rownodes = m.n_rownodes;
-  a.rec_ptr = m.rec_ptr;
+  a.n_single = m.n_rec_single;
+  a.n_multi = m.n_multi;
+  a.multi_ptr = m.multi_ptr;
   a.rec_row0 = m.rec_row0;
   a.rec_meta = m.rec_meta;
+  a.rec_base = m.rec_base;
   a.rec_ele = m.rec_ele;
   a.rec_a = m.rec_a;
   a.rec_tmap = m.rec_tmap;
   a.ele_x = m.ele_x;
   a.ele_dof = m.ele_dof;
-  a.rowptr = m.rowptr;
   a.u_col = d_u_col;
   a.gp = m.tables;
   a.K = d_K;
   a.fint = d_fint;
   a.err = m.err;
+  a.dummy = m.gather_dummy;
   a.mat = StVK{m.lambda, m.mu, m.cdiag};
-  // one-wave workgroups, a few per SIMD on every CU, a multiple of the 8 XCDs, each a contiguous
-  // block of row nodes
-  const int64_t want = int64_t(256) * (m.kinem ? 5 : 8);  // LDS-resident workgroups per CU
-  const int64_t wg = std::max<int64_t>(8, std::min<int64_t>(want, (m.n_rownodes + 7) / 8 * 8));
-  const dim3 grid{static_cast<unsigned>(wg), 1, 1};
+  // one-wave workgroups, as many as the LDS keeps resident on every CU, a multiple of the 8 XCDs,
+  // each a contiguous block of records / nodes
+  const int64_t want = int64_t(256) * (m.kinem ? 5 : 8);
   const dim3 block{64, 1, 1};
-#define FCG_GATHER(KIN)                                                                            \
-  if (want_k && overwrite)                                                                         \
-    hipLaunchKernelGGL((gather_h8_kernel<KIN, true, true>), grid, block, 0, stream, a);            \
-  else if (want_k)                                                                                 \
-    hipLaunchKernelGGL((gather_h8_kernel<KIN, true, false>), grid, block, 0, stream, a);           \
-  else if (overwrite)                                                                              \
-    hipLaunchKernelGGL((gather_h8_kernel<KIN, false, true>), grid, block, 0, stream, a);           \
-  else                                                                                             \
-    hipLaunchKernelGGL((gather_h8_kernel<KIN, false, false>), grid, block, 0, stream, a);
+  auto grid_of = [&](int64_t work) {
+    return dim3{static_cast<unsigned>(std::max<int64_t>(8, std::min<int64_t>(want, (work + 7) / 8 * 8))), 1, 1};
+  };
+#define FCG_GATHER(KIN, MULTI, WORK)                                                               \
+  if ((WORK) > 0)                                                                                  \
+  {                                                                                                \
+    const dim3 grid = grid_of(WORK);                                                               \
+    if (want_k && overwrite)                                                                       \
+      hipLaunchKernelGGL((gather_h8_kernel<KIN, true, true, MULTI>), grid, block, 0, stream, a);   \
+    else if (want_k)                                                                               \
+      hipLaunchKernelGGL((gather_h8_kernel<KIN, true, false, MULTI>), grid, block, 0, stream, a);  \
+    else if (overwrite)                                                                            \
+      hipLaunchKernelGGL((gather_h8_kernel<KIN, false, true, MULTI>), grid, block, 0, stream, a);  \
+    else                                                                                           \
+      hipLaunchKernelGGL((gather_h8_kernel<KIN, false, false, MULTI>), grid, block, 0, stream, a); \
+  }
   if (m.kinem == 0)
   {
-    FCG_GATHER(0)
+    FCG_GATHER(0, false, m.n_rec_single)
+    FCG_GATHER(0, true, m.n_multi)
   }
   else
   {
-    FCG_GATHER(1)
+    FCG_GATHER(1, false, m.n_rec_single)
+    FCG_GATHER(1, true, m.n_multi)
   }
 #undef FCG_GATHER
   return hipGetLastError();

@@ -48,15 +48,18 @@ struct DeviceMesh {
   int32_t* inc_row0 = nullptr;      // [n_inc] row LID of the incidence's node
 
   // node-row gather plan (hex8, FCG_PATH_GATHER): a row node's incidences in records of <= 8
-  int64_t n_rec = 0;
-  int64_t* rec_ptr = nullptr;       // [n_rownodes+1] records of each row node
+  // records: one per node with <= 8 elements [0, n_rec_single), then those of the other nodes
+  int64_t n_rec = 0, n_rec_single = 0, n_multi = 0;
+  int64_t* multi_ptr = nullptr;     // [n_multi+1] record range of each node with > 8 elements
   int32_t* rec_row0 = nullptr;      // [n_rec] first row LID of the record's node
-  int32_t* rec_meta = nullptr;      // [n_rec] slots | first record << 4 | last record << 5
+  int32_t* rec_meta = nullptr;      // [n_rec] slots | first record << 4 | last record << 5 | row length << 8
+  int64_t* rec_base = nullptr;      // [n_rec] CSR offset of the node's first row
   int32_t* rec_ele = nullptr;       // [n_rec][8] element of each slot, -1 = empty
   uint8_t* rec_a = nullptr;         // [n_rec][8] local node of the row node in the slot's element
   uint32_t* rec_tmap = nullptr;     // [n_rec][32] per column triple: slot s's element node in nibble s (8 = none)
   double* ele_x = nullptr;          // [n_ele][8][3] element node coordinates
   int32_t* ele_dof = nullptr;       // [n_ele][8] column LID of each element node's first DOF
+  double* gather_dummy = nullptr;   // [4] store target of a row without columns
 
   // structured (row-block sweep) plan, hex8 only
   int path = FCG_PATH_GENERAL;
