@@ -43,31 +43,34 @@ namespace {
 
 constexpr int kMaxRow = 81;  // hex8 node rows: 27 neighbour triples (fcg_create's limit)
 
-// LDS of one wave.  The regions are reused across the stages of a record (one wave per workgroup:
-// its LDS accesses are processed in program order, no barrier between a region's last read and
-// the next write):
-//   xa: X (and x_cur) in stage 1 -> per-Gauss-point data in stages 2-3
-//   nb: N_XYZ in stages 2-3 -> the 64 blocks in stage 4
-// Strides are chosen so that every access pattern of the stages is free of bank conflicts within
-// each 32-lane group (ds_read_b64 / ds_write_b64, bank = (address / 4) mod 64): per slot 24 or 200
-// doubles, per Gauss point 3 or 25, per node 3.
-template <int KIN>
+// LDS of one wave, one flat array with stage-dependent views (one wave per workgroup: its LDS
+// accesses are processed in program order, so a region is reused without a barrier between its
+// last read and the next write):
+//   linear:  [X | GP] (192) | C (192) | [NX (1600) | blk (585) + row (243) at 600]
+//   TotLag:  [X (384) + C (384) at 384 | GP (2112) | blk (585) + row (243) at 600]
+// (TotLag recomputes N_XYZ_b from J^-1 in stage 3 instead of keeping NX: 17 KB instead of 31 KB,
+// two waves per SIMD.)  A node with more records (MULTI) keeps its row image in its own array.
+// Strides make every access pattern of the stages free of bank conflicts within each 32-lane group
+// (ds_read_b64 / ds_write_b64, bank = (address / 4) mod 64): per slot 24 (X, C), 200 (NX), 24 or
+// 264 (GP); per Gauss point 25 (NX), 3 or 33 (GP); per node 3.
+template <int KIN, bool MULTI>
 struct GatherShared {
   static constexpr int kNs = KIN ? 2 : 1;
-  static constexpr int kGp = KIN ? 25 : 3;    // per (slot, GP): fac F a | fac S a | F | F F^T | fac a
-  static constexpr int kGpSlot = KIN ? 200 : 24;
-  union {
-    double X[kNs][8][24];            // [x | x_cur][slot][3 node + d]
-    double GP[8][kGpSlot];           // [slot][kGp g + k]
-  } xa;
-  double C[kNs][8][24];              // trilinear coefficients [x | x_cur][slot][3 k + d]
-  union {
-    double NX[8][200];               // N_XYZ [slot][25 g + 3 node + d]
-    double blk[65][9];               // lane (slot, b): K_ab (column-major); row 64 = zeros
-  } nb;
-  double row[3 * kMaxRow];           // image of the node's rows (nodes with > 8 elements)
-  double gp[8][4];                   // Gauss point coordinates | weight
-  uint32_t tmap[32];                 // triple t: element node b of slot s in nibble s, 8 = none
+  static constexpr int kGp = KIN ? 33 : 3;  // per (slot, GP): fac a [| fac F a | fac S a | F | F F^T | J^-1]
+  static constexpr int kGpSlot = KIN ? 264 : 24;
+  static constexpr int kX = 0, kC = KIN ? 384 : 192, kGpOff = 0;
+  static constexpr int kNX = KIN ? 0 : 384, kBlk = KIN ? 0 : 384, kRow = kBlk + 600;
+  static constexpr int kSize = KIN ? 8 * 264 : 384 + 1600;
+  double u[kSize];
+  double row_m[MULTI ? 3 * kMaxRow : 1];  // MULTI: the row image lives across records
+  double gp[8][4];                        // Gauss point coordinates | weight
+  uint32_t tmap[32];                      // triple t: element node b of slot s in nibble s, 8 = none
+  __device__ double* X(int s, int j) { return u + kX + 192 * s + 24 * j; }
+  __device__ double* C(int s, int j) { return u + kC + 192 * s + 24 * j; }
+  __device__ double* GP(int j, int g) { return u + kGpOff + kGpSlot * j + kGp * g; }
+  __device__ double* NX(int j, int g) { return u + kNX + 200 * j + 25 * g; }  // linear only
+  __device__ double* blk(int l) { return u + kBlk + 9 * l; }
+  __device__ double* row() { return MULTI ? row_m : u + kRow; }
 };
 
 struct GatherArgs {
@@ -152,9 +155,10 @@ __device__ inline double wave_sum(double v)
 }
 
 template <int KIN, bool WANT_K, bool OVERWRITE, bool MULTI>
-__global__ __launch_bounds__(64, KIN ? 1 : 2) void gather_h8_kernel(GatherArgs A)
+__global__ __launch_bounds__(64, 2) void gather_h8_kernel(GatherArgs A)
 {
-  __shared__ GatherShared<KIN> sh;
+  using Sh = GatherShared<KIN, MULTI>;
+  __shared__ Sh sh;
   const int lane = threadIdx.x;
   const int j = lane >> 3, q = lane & 7;  // slot, element node / Gauss point
   if (lane < 32) (&sh.gp[0][0])[lane] = A.gp[lane];
@@ -227,6 +231,9 @@ __global__ __launch_bounds__(64, KIN ? 1 : 2) void gather_h8_kernel(GatherArgs A
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   const double gx = sh.gp[q][0], gy = sh.gp[q][1], gz = sh.gp[q][2], gw = sh.gp[q][3];
+  // element node b = q: parametric signs (TotLag stage 3)
+  const double bsx = h8_sx(q & 3), bsy = (q & 3) >= 2 ? 1.0 : -1.0, bsz = q >= 4 ? 1.0 : -1.0;
+  const double bsx8 = 0.125 * bsx, bsy8 = 0.125 * bsy, bsz8 = 0.125 * bsz;
   for (int64_t i = R0; i < R1; ++i)
   {
     // in flight while this record computes: the next record's displacements, the element data of
@@ -243,18 +250,18 @@ __global__ __launch_bounds__(64, KIN ? 1 : 2) void gather_h8_kernel(GatherArgs A
     if (MULTI && first)
     {
       fA0 = fA1 = fA2 = 0.0;
-      for (int v = lane; v < 3 * len; v += 64) sh.row[v] = 0.0;
+      for (int v = lane; v < 3 * len; v += 64) sh.row()[v] = 0.0;
     }
     const int32_t e = cur.ele;
     const int a = cur.a;
-    sh.xa.X[0][j][3 * q + 0] = xc[0];
-    sh.xa.X[0][j][3 * q + 1] = xc[1];
-    sh.xa.X[0][j][3 * q + 2] = xc[2];
+    sh.X(0, j)[3 * q + 0] = xc[0];
+    sh.X(0, j)[3 * q + 1] = xc[1];
+    sh.X(0, j)[3 * q + 2] = xc[2];
     if (KIN == 1)
     {
-      sh.xa.X[KIN][j][3 * q + 0] = xc[0] + uc[0];
-      sh.xa.X[KIN][j][3 * q + 1] = xc[1] + uc[1];
-      sh.xa.X[KIN][j][3 * q + 2] = xc[2] + uc[2];
+      sh.X(1, j)[3 * q + 0] = xc[0] + uc[0];
+      sh.X(1, j)[3 * q + 1] = xc[1] + uc[1];
+      sh.X(1, j)[3 * q + 2] = xc[2] + uc[2];
     }
     if (lane < 32) sh.tmap[lane] = cur.tm;
     __syncthreads();
@@ -269,13 +276,13 @@ __global__ __launch_bounds__(64, KIN ? 1 : 2) void gather_h8_kernel(GatherArgs A
         for (int n = 0; n < 8; ++n)
         {
           const double sg = (negmask >> n) & 1u ? -1.0 : 1.0;
-          c0 += sg * sh.xa.X[s][j][3 * n + 0];
-          c1 += sg * sh.xa.X[s][j][3 * n + 1];
-          c2 += sg * sh.xa.X[s][j][3 * n + 2];
+          c0 += sg * sh.X(s, j)[3 * n + 0];
+          c1 += sg * sh.X(s, j)[3 * n + 1];
+          c2 += sg * sh.X(s, j)[3 * n + 2];
         }
-        sh.C[s][j][3 * q + 0] = 0.125 * c0;
-        sh.C[s][j][3 * q + 1] = 0.125 * c1;
-        sh.C[s][j][3 * q + 2] = 0.125 * c2;
+        sh.C(s, j)[3 * q + 0] = 0.125 * c0;
+        sh.C(s, j)[3 * q + 1] = 0.125 * c1;
+        sh.C(s, j)[3 * q + 2] = 0.125 * c2;
       }
     }
     __syncthreads();
@@ -286,12 +293,14 @@ __global__ __launch_bounds__(64, KIN ? 1 : 2) void gather_h8_kernel(GatherArgs A
       int bad = 0;
       double J[9];
       // nodal check at corner q (det J(corner) has the sign of the edge-vector determinant)
-      h8_jac(sh.C[0][j], ((q & 3) == 1 || (q & 3) == 2) ? 1.0 : -1.0, (q & 3) >= 2 ? 1.0 : -1.0,
+      h8_jac(sh.C(0, j), ((q & 3) == 1 || (q & 3) == 2) ? 1.0 : -1.0, (q & 3) >= 2 ? 1.0 : -1.0,
           q >= 4 ? 1.0 : -1.0, J);
       const double detn = h8_det(J);
       if (detn == 0.0) bad = 2;
       else if (!(detn > 0)) bad = 1;
-      h8_jac(sh.C[0][j], gx, gy, gz, J);
+      h8_jac(sh.C(0, j), gx, gy, gz, J);
+      double Jc[9];
+      if (KIN == 1) h8_jac(sh.C(1, j), gx, gy, gz, Jc);  // before GP (aliasing C) is written
       const double det = h8_invert3x3(J);
       if (det == 0.0) bad = 2;
       const double fac = det * gw;
@@ -303,26 +312,38 @@ __global__ __launch_bounds__(64, KIN ? 1 : 2) void gather_h8_kernel(GatherArgs A
       const double pyz[2][2] = {{hym * zm, hym * zp}, {hyp * zm, hyp * zp}};
       const double pxz[2][2] = {{hxm * zm, hxm * zp}, {hxp * zm, hxp * zp}};
       const double pxy[2][2] = {{hxm * ym, hxm * yp}, {hxp * ym, hxp * yp}};
-      double na[3] = {0.0, 0.0, 0.0};
-#pragma unroll
-      for (int n = 0; n < 8; ++n)
+      double na[3];
+      if (KIN == 0)
       {
-        const int ix = h8_sx(n) > 0, iy = h8_sy(n) > 0, iz = h8_sz(n) > 0;
+#pragma unroll
+        for (int n = 0; n < 8; ++n)
+        {
+          const int ix = h8_sx(n) > 0, iy = h8_sy(n) > 0, iz = h8_sz(n) > 0;
+          const double d0 = ix ? pyz[iy][iz] : -pyz[iy][iz];
+          const double d1 = iy ? pxz[ix][iz] : -pxz[ix][iz];
+          const double d2 = iz ? pxy[ix][iy] : -pxy[ix][iy];
+          double* nx = sh.NX(j, q) + 3 * n;
+          nx[0] = J[0] * d0 + J[3] * d1 + J[6] * d2;
+          nx[1] = J[1] * d0 + J[4] * d1 + J[7] * d2;
+          nx[2] = J[2] * d0 + J[5] * d1 + J[8] * d2;
+        }
+        // N_XYZ_a back from the lane's own stores (in order within the wave)
+        na[0] = sh.NX(j, q)[3 * a + 0];
+        na[1] = sh.NX(j, q)[3 * a + 1];
+        na[2] = sh.NX(j, q)[3 * a + 2];
+      }
+      else
+      {
+        // N_XYZ of node a only (stage 3 rebuilds the others from J^-1)
+        const int ix = ((a & 3) == 1 || (a & 3) == 2), iy = (a & 3) >= 2, iz = a >= 4;
         const double d0 = ix ? pyz[iy][iz] : -pyz[iy][iz];
         const double d1 = iy ? pxz[ix][iz] : -pxz[ix][iz];
         const double d2 = iz ? pxy[ix][iy] : -pxy[ix][iy];
-        const double n0 = J[0] * d0 + J[3] * d1 + J[6] * d2;
-        const double n1 = J[1] * d0 + J[4] * d1 + J[7] * d2;
-        const double n2 = J[2] * d0 + J[5] * d1 + J[8] * d2;
-        sh.nb.NX[j][25 * q + 3 * n + 0] = n0;
-        sh.nb.NX[j][25 * q + 3 * n + 1] = n1;
-        sh.nb.NX[j][25 * q + 3 * n + 2] = n2;
+        na[0] = J[0] * d0 + J[3] * d1 + J[6] * d2;
+        na[1] = J[1] * d0 + J[4] * d1 + J[7] * d2;
+        na[2] = J[2] * d0 + J[5] * d1 + J[8] * d2;
       }
-      // N_XYZ_a back from the lane's own stores (in order within the wave)
-      na[0] = sh.nb.NX[j][25 * q + 3 * a + 0];
-      na[1] = sh.nb.NX[j][25 * q + 3 * a + 1];
-      na[2] = sh.nb.NX[j][25 * q + 3 * a + 2];
-      double* P = &sh.xa.GP[j][GatherShared<KIN>::kGp * q];
+      double* P = sh.GP(j, q);
       if (KIN == 0)
       {
         P[0] = fac * na[0];
@@ -332,8 +353,6 @@ __global__ __launch_bounds__(64, KIN ? 1 : 2) void gather_h8_kernel(GatherArgs A
       else
       {
         // F = J_cur J^-1 (column-major F[i + 3 j] = d x_i / d X_j)
-        double Jc[9];
-        h8_jac(sh.C[KIN][j], gx, gy, gz, Jc);
         double F[9];
 #pragma unroll
         for (int ii = 0; ii < 3; ++ii)
@@ -360,7 +379,7 @@ __global__ __launch_bounds__(64, KIN ? 1 : 2) void gather_h8_kernel(GatherArgs A
         fp0 = fac * (F[0] * sa0 + F[3] * sa1 + F[6] * sa2);
         fp1 = fac * (F[1] * sa0 + F[4] * sa1 + F[7] * sa2);
         fp2 = fac * (F[2] * sa0 + F[5] * sa1 + F[8] * sa2);
-        // fac F a | fac S a | F | F F^T
+        // fac F a | fac S a | F | F F^T | fac a | J^-1
         P[0] = fac * (F[0] * na[0] + F[3] * na[1] + F[6] * na[2]);
         P[1] = fac * (F[1] * na[0] + F[4] * na[1] + F[7] * na[2]);
         P[2] = fac * (F[2] * na[0] + F[5] * na[1] + F[8] * na[2]);
@@ -378,6 +397,8 @@ __global__ __launch_bounds__(64, KIN ? 1 : 2) void gather_h8_kernel(GatherArgs A
         P[21] = fac * na[0];
         P[22] = fac * na[1];
         P[23] = fac * na[2];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) P[24 + k] = J[k];
       }
       if (bad)
       {
@@ -400,9 +421,25 @@ __global__ __launch_bounds__(64, KIN ? 1 : 2) void gather_h8_kernel(GatherArgs A
 #pragma unroll 4
       for (int g = 0; g < 8; ++g)
       {
-        const double* B = &sh.nb.NX[j][25 * g + 3 * q];
-        const double b0 = B[0], b1 = B[1], b2 = B[2];
-        const double* P = &sh.xa.GP[j][GatherShared<KIN>::kGp * g];
+        const double* P = sh.GP(j, g);
+        double b0, b1, b2;
+        if (KIN == 0)
+        {
+          const double* B = sh.NX(j, g) + 3 * q;
+          b0 = B[0];
+          b1 = B[1];
+          b2 = B[2];
+        }
+        else
+        {
+          // N_XYZ_b = J^-1 dN_b(xi_g), dN_b/dxi = sx (1 + sy eta)(1 + sz zeta) / 8, ...
+          const double fx = fma(bsx, sh.gp[g][0], 1.0), fy = fma(bsy, sh.gp[g][1], 1.0),
+                       fz = fma(bsz, sh.gp[g][2], 1.0);
+          const double d0 = (bsx8 * fy) * fz, d1 = (bsy8 * fx) * fz, d2 = (bsz8 * fx) * fy;
+          b0 = P[24] * d0 + P[27] * d1 + P[30] * d2;
+          b1 = P[25] * d0 + P[28] * d1 + P[31] * d2;
+          b2 = P[26] * d0 + P[29] * d1 + P[32] * d2;
+        }
         if (KIN == 0)
         {
           const double fa0 = P[0], fa1 = P[1], fa2 = P[2];
@@ -471,15 +508,15 @@ __global__ __launch_bounds__(64, KIN ? 1 : 2) void gather_h8_kernel(GatherArgs A
     double* dst = len ? A.K + base : A.dummy;
     if (WANT_K)
     {
-      __syncthreads();  // NX -> blk
+      __syncthreads();  // NX / GP -> blk
 #pragma unroll
-      for (int k = 0; k < 9; ++k) sh.nb.blk[lane][k] = Kb[k];
-      if (lane < 9) sh.nb.blk[64][lane] = 0.0;
+      for (int k = 0; k < 9; ++k) sh.blk(lane)[k] = Kb[k];
+      if (lane < 9) sh.blk(64)[lane] = 0.0;
       __syncthreads();
       // lane (triple t, half h): entries c = 2 e + h (column-major in the 3 x 3 block) of the
-      // triple's block, each summed over the slots in order.  Without MULTI and with OVERWRITE
-      // every lane stores five entries: lanes past the row's triples redo the last triple and the
-      // ninth entry stands in for the missing tenth (the same value to the same address).
+      // triple's block, each summed over the slots in order into the LDS image of the rows (lanes
+      // past the row's triples redo the last triple and the ninth entry stands in for the missing
+      // tenth: the same value to the same address, no branch).
       const int ntrip = len / 3;
       const int t = max(0, min(lane >> 1, ntrip - 1)), h = lane & 1;
       const bool active = (lane >> 1) < ntrip;
@@ -492,7 +529,7 @@ __global__ __launch_bounds__(64, KIN ? 1 : 2) void gather_h8_kernel(GatherArgs A
           const uint32_t b = (tm >> (4 * sl)) & 15u;
           off[sl] = 9 * (b < 8u ? 8 * sl + int(b) : 64);
         }
-        const double* blk = &sh.nb.blk[0][0];
+        const double* blk = sh.blk(0);
 #pragma unroll
         for (int e5 = 0; e5 < 5; ++e5)
         {
@@ -504,12 +541,25 @@ __global__ __launch_bounds__(64, KIN ? 1 : 2) void gather_h8_kernel(GatherArgs A
           const int v = rr * len + 3 * t + cc;
           if (MULTI)
           {
-            if (active && !(h && e5 == 4)) sh.row[v] += x;
+            if (active && !(h && e5 == 4)) sh.row()[v] += x;
           }
-          else if (OVERWRITE)
-            __builtin_nontemporal_store(x, dst + v);
-          else if (active && !(h && e5 == 4))
-            dst[v] += x;
+          else
+            sh.row()[v] = x;
+        }
+      }
+      // one record per node: the rows leave as contiguous runs of 64 (OVERWRITE: four stores per
+      // lane, lanes past the end repeating the last entry)
+      if (!MULTI)
+      {
+        const int n3 = 3 * len;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+        {
+          const int v = max(0, min(lane + 64 * k, n3 - 1));
+          if (OVERWRITE)
+            __builtin_nontemporal_store(sh.row()[v], dst + v);
+          else if (lane + 64 * k < n3)
+            dst[v] += sh.row()[v];
         }
       }
       // a node with more records: its image leaves after the last one
@@ -519,9 +569,9 @@ __global__ __launch_bounds__(64, KIN ? 1 : 2) void gather_h8_kernel(GatherArgs A
         for (int v = lane; v < 3 * len; v += 64)
         {
           if (OVERWRITE)
-            __builtin_nontemporal_store(sh.row[v], dst + v);
+            __builtin_nontemporal_store(sh.row()[v], dst + v);
           else
-            dst[v] += sh.row[v];
+            dst[v] += sh.row()[v];
         }
       }
     }
@@ -586,7 +636,7 @@ hipError_t launch_gather_h8(const DeviceMesh& m, const double* d_u_col, bool wan
   a.mat = StVK{m.lambda, m.mu, m.cdiag};
   // one-wave workgroups, as many as the LDS keeps resident on every CU, a multiple of the 8 XCDs,
   // each a contiguous block of records / nodes
-  const int64_t want = int64_t(256) * (m.kinem ? 5 : 8);
+  const int64_t want = int64_t(256) * 8;  // two waves per SIMD (VGPRs), LDS fits nine
   const dim3 block{64, 1, 1};
   auto grid_of = [&](int64_t work) {
     return dim3{static_cast<unsigned>(std::max<int64_t>(8, std::min<int64_t>(want, (work + 7) / 8 * 8))), 1, 1};
