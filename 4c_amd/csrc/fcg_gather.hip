@@ -47,20 +47,20 @@ constexpr int kMaxRow = 81;  // hex8 node rows: 27 neighbour triples (fcg_create
 // accesses are processed in program order, so a region is reused without a barrier between its
 // last read and the next write):
 //   linear:  [X | GP] (192) | C (192) | [NX (1600) | blk (585) + row (243) at 600]
-//   TotLag:  [X (384) + C (384) at 384 | GP (2112) | blk (585) + row (243) at 600]
-// (TotLag recomputes N_XYZ_b from J^-1 in stage 3 instead of keeping NX: 17 KB instead of 31 KB,
-// two waves per SIMD.)  A node with more records (MULTI) keeps its row image in its own array.
+//   TotLag:  [X (384) + C (384) at 384 | GP (1600) | blk (585) + row (243) at 600]
+// (TotLag forms its stage-3 terms from dN_b(xi_g) directly, with the Gauss point's J^-1 folded into
+// per-point 3 x 3 factors, instead of keeping NX: 13 KB instead of 31 KB.)  A node with more records (MULTI) keeps its row image in its own array.
 // Strides make every access pattern of the stages free of bank conflicts within each 32-lane group
 // (ds_read_b64 / ds_write_b64, bank = (address / 4) mod 64): per slot 24 (X, C), 200 (NX), 24 or
-// 264 (GP); per Gauss point 25 (NX), 3 or 33 (GP); per node 3.
+// 200 (GP); per Gauss point 25 (NX), 3 or 25 (GP); per node 3.
 template <int KIN, bool MULTI>
 struct GatherShared {
   static constexpr int kNs = KIN ? 2 : 1;
-  static constexpr int kGp = KIN ? 33 : 3;  // per (slot, GP): fac a [| fac F a | fac S a | F | F F^T | J^-1]
-  static constexpr int kGpSlot = KIN ? 264 : 24;
+  static constexpr int kGp = KIN ? 25 : 3;  // per (slot, GP): fac a | TotLag: fac F a, J^-T fac S a, F J^-T, F F^T, J^-T fac a
+  static constexpr int kGpSlot = KIN ? 200 : 24;
   static constexpr int kX = 0, kC = KIN ? 384 : 192, kGpOff = 0;
   static constexpr int kNX = KIN ? 0 : 384, kBlk = KIN ? 0 : 384, kRow = kBlk + 600;
-  static constexpr int kSize = KIN ? 8 * 264 : 384 + 1600;
+  static constexpr int kSize = KIN ? 8 * 200 : 384 + 1600;
   double u[kSize];
   double row_m[MULTI ? 3 * kMaxRow : 1];  // MULTI: the row image lives across records
   double gp[8][4];                        // Gauss point coordinates | weight
@@ -379,26 +379,28 @@ __global__ __launch_bounds__(64, 2) void gather_h8_kernel(GatherArgs A)
         fp0 = fac * (F[0] * sa0 + F[3] * sa1 + F[6] * sa2);
         fp1 = fac * (F[1] * sa0 + F[4] * sa1 + F[7] * sa2);
         fp2 = fac * (F[2] * sa0 + F[5] * sa1 + F[8] * sa2);
-        // fac F a | fac S a | F | F F^T | fac a | J^-1
-        P[0] = fac * (F[0] * na[0] + F[3] * na[1] + F[6] * na[2]);
-        P[1] = fac * (F[1] * na[0] + F[4] * na[1] + F[7] * na[2]);
-        P[2] = fac * (F[2] * na[0] + F[5] * na[1] + F[8] * na[2]);
-        P[3] = fac * sa0;
-        P[4] = fac * sa1;
-        P[5] = fac * sa2;
+        // stage 3 needs, for N_XYZ_b = J^-T dN_b (b_j = sum_dir J[j + 3 dir] d_dir):
+        //   fac F a | J^-T-folded fac S a | Q = F J^-T (Q[i + 3 dir]) | F F^T | J^-T-folded fac a
+        const double fs0 = fac * sa0, fs1 = fac * sa1, fs2 = fac * sa2;
+        const double fa0 = fac * na[0], fa1 = fac * na[1], fa2 = fac * na[2];
+        P[0] = F[0] * fa0 + F[3] * fa1 + F[6] * fa2;
+        P[1] = F[1] * fa0 + F[4] * fa1 + F[7] * fa2;
+        P[2] = F[2] * fa0 + F[5] * fa1 + F[8] * fa2;
 #pragma unroll
-        for (int k = 0; k < 9; ++k) P[6 + k] = F[k];
+        for (int dir = 0; dir < 3; ++dir)
+        {
+          const double j0 = J[0 + 3 * dir], j1 = J[1 + 3 * dir], j2 = J[2 + 3 * dir];
+          P[3 + dir] = fs0 * j0 + fs1 * j1 + fs2 * j2;
+          P[21 + dir] = fa0 * j0 + fa1 * j1 + fa2 * j2;
+#pragma unroll
+          for (int ii = 0; ii < 3; ++ii) P[6 + ii + 3 * dir] = F[ii] * j0 + F[ii + 3] * j1 + F[ii + 6] * j2;
+        }
         P[15] = F[0] * F[0] + F[3] * F[3] + F[6] * F[6];
         P[16] = F[1] * F[1] + F[4] * F[4] + F[7] * F[7];
         P[17] = F[2] * F[2] + F[5] * F[5] + F[8] * F[8];
         P[18] = F[0] * F[1] + F[3] * F[4] + F[6] * F[7];
         P[19] = F[1] * F[2] + F[4] * F[5] + F[7] * F[8];
         P[20] = F[2] * F[0] + F[5] * F[3] + F[8] * F[6];
-        P[21] = fac * na[0];
-        P[22] = fac * na[1];
-        P[23] = fac * na[2];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) P[24 + k] = J[k];
       }
       if (bad)
       {
@@ -422,26 +424,10 @@ __global__ __launch_bounds__(64, 2) void gather_h8_kernel(GatherArgs A)
       for (int g = 0; g < 8; ++g)
       {
         const double* P = sh.GP(j, g);
-        double b0, b1, b2;
         if (KIN == 0)
         {
           const double* B = sh.NX(j, g) + 3 * q;
-          b0 = B[0];
-          b1 = B[1];
-          b2 = B[2];
-        }
-        else
-        {
-          // N_XYZ_b = J^-1 dN_b(xi_g), dN_b/dxi = sx (1 + sy eta)(1 + sz zeta) / 8, ...
-          const double fx = fma(bsx, sh.gp[g][0], 1.0), fy = fma(bsy, sh.gp[g][1], 1.0),
-                       fz = fma(bsz, sh.gp[g][2], 1.0);
-          const double d0 = (bsx8 * fy) * fz, d1 = (bsy8 * fx) * fz, d2 = (bsz8 * fx) * fy;
-          b0 = P[24] * d0 + P[27] * d1 + P[30] * d2;
-          b1 = P[25] * d0 + P[28] * d1 + P[31] * d2;
-          b2 = P[26] * d0 + P[29] * d1 + P[32] * d2;
-        }
-        if (KIN == 0)
-        {
+          const double b0 = B[0], b1 = B[1], b2 = B[2];
           const double fa0 = P[0], fa1 = P[1], fa2 = P[2];
           G[0] += fa0 * b0; G[1] += fa0 * b1; G[2] += fa0 * b2;
           G[3] += fa1 * b0; G[4] += fa1 * b1; G[5] += fa1 * b2;
@@ -449,17 +435,22 @@ __global__ __launch_bounds__(64, 2) void gather_h8_kernel(GatherArgs A)
         }
         else
         {
+          // dN_b(xi_g): dN_b/dxi = sx (1 + sy eta)(1 + sz zeta) / 8, ...; N_XYZ_b = J^-T dN_b
+          // enters only through the folded factors: F N_XYZ_b = Q dN_b, a.b = (J^-1 fac a).dN_b
+          const double fx = fma(bsx, sh.gp[g][0], 1.0), fy = fma(bsy, sh.gp[g][1], 1.0),
+                       fz = fma(bsz, sh.gp[g][2], 1.0);
+          const double d0 = (bsx8 * fy) * fz, d1 = (bsy8 * fx) * fz, d2 = (bsz8 * fx) * fy;
           const double fpa0 = P[0], fpa1 = P[1], fpa2 = P[2];
-          const double pb0 = P[6] * b0 + P[9] * b1 + P[12] * b2;
-          const double pb1 = P[7] * b0 + P[10] * b1 + P[13] * b2;
-          const double pb2 = P[8] * b0 + P[11] * b1 + P[14] * b2;
+          const double pb0 = P[6] * d0 + P[9] * d1 + P[12] * d2;
+          const double pb1 = P[7] * d0 + P[10] * d1 + P[13] * d2;
+          const double pb2 = P[8] * d0 + P[11] * d1 + P[14] * d2;
           G[0] += fpa0 * pb0; G[1] += fpa0 * pb1; G[2] += fpa0 * pb2;
           G[3] += fpa1 * pb0; G[4] += fpa1 * pb1; G[5] += fpa1 * pb2;
           G[6] += fpa2 * pb0; G[7] += fpa2 * pb1; G[8] += fpa2 * pb2;
-          const double t = P[21] * b0 + P[22] * b1 + P[23] * b2;
+          const double t = P[21] * d0 + P[22] * d1 + P[23] * d2;
 #pragma unroll
           for (int k = 0; k < 6; ++k) H[k] += t * P[15 + k];
-          geo += P[3] * b0 + P[4] * b1 + P[5] * b2;
+          geo += P[3] * d0 + P[4] * d1 + P[5] * d2;
         }
       }
       // G[3 r + c] = sum_g fac (.)_r (.)_c -> K_ab[r + 3 c] = lambda G_rc + mu G_cr (+ I terms)
