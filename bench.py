@@ -467,6 +467,53 @@ def host_secondary(dev, n, steps):
         return {"workload": "host-buffer drop-in", "error": repr(e)}
 
 
+def gather_secondary(dev, n, steps):
+    """Config 2's element on an unstructured mesh: the n^3 hex8 box renumbered like an input-file
+    mesh (random node and element numbering, no lattice hint: fcg.Discretization.renumbered), so
+    that AUTO takes the node-row gather path (FCG_PATH_GATHER); linear and TotLag K + r, kernel
+    time by hipEvents, HBM fraction by SURVEY §8d's bytes per element."""
+    try:
+        box = fcg.BoxMesh(fcg.HEX8, (n, n, n), jitter=0.1, seed=20251015)
+        dis = fcg.Discretization.renumbered(box, seed=1)
+        del box
+        out = {"workload": f"hex8-{n}^3 renumbered (unstructured: random node/element order)",
+               "baseline_config": "BASELINE.json configs[1] element on a mesh without lattice",
+               "unit": "element-evaluations/s", "elements": dis.n_ele, "nnz": dis.nnz}
+        rng = np.random.default_rng(3)
+        for name, kinem, amp in (("linear", fcg.LINEAR, 1e-3), ("totlag", fcg.TOTLAG, 5e-2)):
+            ev = fcg.Evaluator(dis, kinematics=kinem, youngs=210.0, poisson=0.3, device=dev.index)
+            u = torch.from_numpy(rng.standard_normal(dis.n_cols) * amp).to(dev)
+            f = torch.zeros(dis.n_rows, dtype=torch.float64, device=dev)
+            K = torch.zeros(dis.nnz, dtype=torch.float64, device=dev)
+            for _ in range(3):
+                ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u, f, K)
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u, f, K)
+            torch.cuda.synchronize(dev)
+            wall = (time.perf_counter() - t0) / steps
+            ev.set_timing(True)
+            ts = []
+            for _ in range(steps):
+                ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u, f, K)
+                ts.append(sum(ev.timing()))
+            ms_kern = float(np.mean(ts))
+            gbs = ALG_BYTES_PER_ELE * dis.n_ele / (ms_kern * 1e-3) / 1e9
+            out[name] = {"value": dis.n_ele / wall, "ms_per_step": 1e3 * wall, "ms_kernel": ms_kern,
+                         "path": {fcg.PATH_GATHER: "gather", fcg.PATH_GENERAL: "general"}.get(
+                             int(ev.info.path), int(ev.info.path)),
+                         "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS,
+                                      "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS}}
+            ev.close()
+            del K, f, u
+            torch.cuda.empty_cache()
+        out["value"] = out["linear"]["value"]
+        return out
+    except Exception as e:  # report, never hide
+        return {"workload": "hex8 renumbered (gather path)", "error": repr(e)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -484,6 +531,8 @@ def main():
     ap.add_argument("--newton-n", type=int, default=100)
     ap.add_argument("--no-optionb", action="store_true", help="skip the option-B (shared-DOF) line")
     ap.add_argument("--no-host", action="store_true", help="skip the host-buffer drop-in line")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="skip the unstructured (renumbered) hex8 line")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -690,6 +739,9 @@ def main():
                                        else cpu_threads(args.cpu_threads)))
     if rank == 0 and world == 1 and not args.no_host:
         secondary.append(host_secondary(dev, args.n, 3))
+    if rank == 0 and world == 1 and not args.no_gather:
+        secondary.append(gather_secondary(dev, args.n, max(3, min(args.steps, 10))))
+        torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_hex27:
         try:
             secondary.append(hex27_secondary(dev, args.hex27_n, max(3, min(args.steps, 10)),

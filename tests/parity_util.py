@@ -109,3 +109,53 @@ def oracle_tsi_evaluate(mesh, g, E, nu, alpha, T0, conduct, timefac, timefac_d, 
         T_col.ctypes.data_as(orc._dp), ctypes.byref(css), ctypes.byref(cst), ctypes.byref(cts),
         ctypes.byref(ctt), fs.ctypes.data_as(orc._dp), ft.ctypes.data_as(orc._dp), ctypes.byref(bad))
     return (err,) + tuple(vals) + (fs, ft)
+
+
+def oracle_evaluate_single(dis, kinem, E, nu, u_col, want_k=True, nworkers=1):
+    """oracle_evaluate for a single-rank fcg.Discretization (DOF LID = GID, node GID = index)."""
+    m = type("SingleRank", (), {})()
+    m.row_gid = m.col_gid = np.arange(dis.n_cols, dtype=np.int32)
+    m.nnz, m.n_rows, m.rowptr, m.col_lid = dis.nnz, dis.n_rows, dis.rowptr, dis.col_lid
+    m.celltype, m.n_ele, m.ele_nodes = dis.celltype, dis.n_ele, dis.ele_nodes
+    m.n_node, m.node_x, m.node_dof_row = dis.n_node, dis.node_x, dis.node_dof_row
+    m.node_gid = np.arange(dis.n_node, dtype=np.int64)
+    return oracle_evaluate(m, kinem, E, nu, u_col, want_k=want_k, nworkers=nworkers)
+
+
+def tiled_input_mesh(fx, reps, jitter, seed):
+    """A reference input mesh (fixture `fx`, hex8) tiled reps[0] x reps[1] x reps[2] times along
+    its bounding box, coincident nodes merged, interior nodes jittered by `jitter` x the smallest
+    edge, then node and element numbering shuffled -- an unstructured mesh that keeps the input's
+    own element node orderings.  Returns an fcg.Discretization (no lattice hint)."""
+    ids = sorted(int(k) for k in fx["nodes"])
+    pos = {n: i for i, n in enumerate(ids)}
+    X0 = np.array([fx["nodes"][str(n)] for n in ids], dtype=np.float64)
+    E0 = np.array([[pos[n] for n in el["nodes"]] for el in fx["elements"] if el["shape"] == "HEX8"])
+    lo, hi = X0.min(axis=0), X0.max(axis=0)
+    L = hi - lo
+    Xs, Es = [], []
+    off = 0
+    for i in range(reps[0]):
+        for j in range(reps[1]):
+            for k in range(reps[2]):
+                Xs.append(X0 + L * np.array([i, j, k]))
+                Es.append(E0 + off)
+                off += len(X0)
+    X = np.vstack(Xs)
+    En = np.vstack(Es)
+    key = np.round((X - lo) / L.max() * 2**20).astype(np.int64)
+    _, first, inv = np.unique(key, axis=0, return_index=True, return_inverse=True)
+    inv = inv.ravel()
+    X = X[first]
+    En = inv[En]
+    rng = np.random.default_rng(seed)
+    h = np.min([np.linalg.norm(X[En[:, a]] - X[En[:, b]], axis=1).min()
+                for a, b in ((0, 1), (1, 2), (0, 4))])
+    span = L * np.array(reps)
+    interior = np.all((X > lo + 1e-9 * span) & (X < lo + span - 1e-9 * span), axis=1)
+    X[interior] += jitter * h * rng.uniform(-1, 1, size=(interior.sum(), 3))
+    perm = rng.permutation(len(X))
+    newX = np.empty_like(X)
+    newX[perm] = X
+    En = perm[En][rng.permutation(len(En))]
+    return fcg.Discretization.from_elements(fcg.HEX8, En, newX)
