@@ -403,7 +403,11 @@ def optionb_secondary(dev, rank, world, n, steps, staged):
             ev.evaluate_device(fcg.CALC_INTERNALFORCE, fcg.OVERWRITE, u_col, f, stream=stream)
             if staged:
                 sh.reduce_staged(f, stream)
-                nrm = halo.residual_norm(f[:n_own], None, stream)
+                loc = halo.residual_norm(f[:n_own], None, stream)
+                t = torch.tensor([loc * loc], dtype=torch.float64)
+                if world > 1:
+                    dist.all_reduce(t)
+                nrm = float(np.sqrt(t.item()))
             else:
                 sh.reduce(comm, f, stream)
                 nrm = halo.residual_norm(f[:n_own], comm, stream)
