@@ -776,13 +776,15 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
     chk(upload(&m.lat_x, sp.lat_x.data(), int64_t(sp.lat_x.size()), bytes));
     chk(upload(&m.lat_dof, sp.lat_dof.data(), int64_t(sp.lat_dof.size()), bytes));
     chk(upload(&m.plane_rec, sp.plane_rec.data(), int64_t(sp.plane_rec.size()), bytes));
-    std::vector<double> tab(8 * 8 * 3 * 2 + 8);
+    // dN at the GPs [192] | dN at the nodes [192] | weights [8] | GP coordinates [24]
+    std::vector<double> tab(8 * 8 * 3 * 2 + 8 + 24);
     double xi[81], w[27], xn[81];
     fcg::gauss_rule(fcg::kHex8, xi, w);
     fcg::node_param_coords(fcg::kHex8, xn);
     for (int g = 0; g < 8; ++g) fcg::shape_deriv(fcg::kHex8, &xi[3 * g], &tab[24 * g]);
     for (int g = 0; g < 8; ++g) fcg::shape_deriv(fcg::kHex8, &xn[3 * g], &tab[192 + 24 * g]);
     for (int g = 0; g < 8; ++g) tab[384 + g] = w[g];
+    for (int k = 0; k < 24; ++k) tab[392 + k] = xi[k];
     chk(upload(&m.tables, tab.data(), int64_t(tab.size()), bytes));
     // diagnostics (tools/stamps.py): FCG_STAMPS=1 turns on the per-phase s_memtime counters
     const char* st = std::getenv("FCG_STAMPS");

@@ -54,6 +54,31 @@ struct StVK {
   double lambda, mu, cdiag;
 };
 
+// hex8 shape derivatives at a point (xi, eta, zeta) without a table: dN_n/dxi = sx (1 + sy eta)
+// (1 + sz zeta) / 8 etc. (sx, sy, sz = the corner's parametric signs), from the 12 distinct
+// products; with n a compile-time constant the sign is a negation modifier.
+struct H8dN {
+  double pyz[2][2], pxz[2][2], pxy[2][2];  // [sign index][sign index], 1 = +
+};
+__device__ inline H8dN h8_dn_products(double x, double y, double z)
+{
+  const double xp = 1.0 + x, xm = 1.0 - x, yp = 1.0 + y, ym = 1.0 - y, zp = 1.0 + z, zm = 1.0 - z;
+  const double hyp = 0.125 * yp, hym = 0.125 * ym, hxp = 0.125 * xp, hxm = 0.125 * xm;
+  H8dN p;
+  p.pyz[0][0] = hym * zm; p.pyz[0][1] = hym * zp; p.pyz[1][0] = hyp * zm; p.pyz[1][1] = hyp * zp;
+  p.pxz[0][0] = hxm * zm; p.pxz[0][1] = hxm * zp; p.pxz[1][0] = hxp * zm; p.pxz[1][1] = hxp * zp;
+  p.pxy[0][0] = hxm * ym; p.pxy[0][1] = hxm * yp; p.pxy[1][0] = hxp * ym; p.pxy[1][1] = hxp * yp;
+  return p;
+}
+// node n in 4C order: x sign (n & 3) in {1, 2}, y sign (n & 3) >= 2, z sign n >= 4
+__device__ inline void h8_dn(const H8dN& p, int n, double& d0, double& d1, double& d2)
+{
+  const int ix = ((n & 3) == 1 || (n & 3) == 2), iy = (n & 3) >= 2, iz = n >= 4;
+  d0 = ix ? p.pyz[iy][iz] : -p.pyz[iy][iz];
+  d1 = iy ? p.pxz[ix][iz] : -p.pxz[ix][iz];
+  d2 = iz ? p.pxy[ix][iy] : -p.pxy[ix][iy];
+}
+
 // Stage A for Gauss point g = j.  Returns 0, 1 (nodal det J <= 0) or 2 (singular).
 template <int KIN>
 __device__ inline int h8_stage_a(int j, H8Slot<KIN>& s, const double (*dN)[8][3],

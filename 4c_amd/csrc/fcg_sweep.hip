@@ -100,10 +100,7 @@ struct SweepShared {
   alignas(16) double tg[TSI ? 8 : 1][TSI ? NSLOT : 1][4];
   double node[3][NNODE][node_comps<TSI>()];  // node columns of the 6 x 6 grid, ring by plane mod 3
   uint32_t prec[3][PLANE_REC_WORDS];  // plane records, ring by plane mod 3
-  // shape derivatives at Gauss point g, [g][3 n + d], rows padded to 25 doubles: the 8 Gauss
-  // points of a stage-A lane group then read 8 distinct bank pairs (a 24-double row put g and
-  // g + 4 on the same banks: every dN load 2-way conflicted)
-  double dN[8][25];
+  double gxi[8][4];  // Gauss point coordinates (stage A forms the shape derivatives from them)
   double Ng[TSI ? 8 : 1][8];  // TSI: shape values N_n at Gauss point g
   double w8[8];
   uint32_t neg[NSLOT];  // bit g set: fac < 0 at Gauss point g
@@ -144,6 +141,8 @@ __device__ inline void sweep_stage_a(SweepShared<KIN, TSI>& sh, const SweepArgs&
 #pragma unroll
   for (int n = 0; n < 8; ++n)
     nd[n] = sh.node[ring(L + node_oz(n))][(sy + node_oy(n)) * NXN + sx + node_ox(n)];
+  // shape derivatives at Gauss point g from its coordinates (no table loads)
+  const H8dN dn = h8_dn_products(sh.gxi[g][0], sh.gxi[g][1], sh.gxi[g][2]);
   double J[9];
 #pragma unroll
   for (int q = 0; q < 9; ++q) J[q] = 0.0;
@@ -151,7 +150,8 @@ __device__ inline void sweep_stage_a(SweepShared<KIN, TSI>& sh, const SweepArgs&
   for (int n = 0; n < 8; ++n)
   {
     const double x0 = nd[n][0], x1 = nd[n][1], x2 = nd[n][2];
-    const double d0 = sh.dN[g][3 * n], d1 = sh.dN[g][3 * n + 1], d2 = sh.dN[g][3 * n + 2];
+    double d0, d1, d2;
+    h8_dn(dn, n, d0, d1, d2);
     J[0] += d0 * x0; J[1] += d1 * x0; J[2] += d2 * x0;
     J[3] += d0 * x1; J[4] += d1 * x1; J[5] += d2 * x1;
     J[6] += d0 * x2; J[7] += d1 * x2; J[8] += d2 * x2;
@@ -196,7 +196,8 @@ __device__ inline void sweep_stage_a(SweepShared<KIN, TSI>& sh, const SweepArgs&
   const double ns = KIN == 0 ? 1.0 : sq;  // remaining scale of the stored N_XYZ
   // N_XYZ of node n (J now holds J^-1, column-major)
   auto nxyz = [&](int n, double& n0, double& n1, double& n2) {
-    const double d0 = sh.dN[g][3 * n], d1 = sh.dN[g][3 * n + 1], d2 = sh.dN[g][3 * n + 2];
+    double d0, d1, d2;
+    h8_dn(dn, n, d0, d1, d2);
     n0 = J[0] * d0 + J[3] * d1 + J[6] * d2;
     n1 = J[1] * d0 + J[4] * d1 + J[7] * d2;
     n2 = J[2] * d0 + J[5] * d1 + J[8] * d2;
@@ -446,10 +447,7 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
   const uint32_t* prec_tile = A.plane_rec + (int64_t(ty) * A.tiles_x + tx) * A.NK * PLANE_REC_WORDS;
   const int64_t LX = A.EX + 1, LY = A.EY + 1;
 
-  for (int v = tid; v < 192; v += 256)
-  {
-    sh.dN[v / 24][v % 24] = A.tables[v];
-  }
+  if (tid < 24) sh.gxi[tid / 3][tid % 3] = A.tables[392 + tid];
   if (tid < 8) sh.w8[tid] = A.tables[384 + tid];
   if (TSI && tid < 64) (&sh.Ng[0][0])[tid] = A.Ngp[tid];
 
