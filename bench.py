@@ -535,6 +535,8 @@ def main():
     ap.add_argument("--newton-n", type=int, default=100)
     ap.add_argument("--no-optionb", action="store_true", help="skip the option-B (shared-DOF) line")
     ap.add_argument("--no-host", action="store_true", help="skip the host-buffer drop-in line")
+    ap.add_argument("--peaks-after", action="store_true",
+                    help="measure the box's peaks after the timed steps instead of before the warm-up")
     ap.add_argument("--no-gather", action="store_true",
                     help="skip the unstructured (renumbered) hex8 line")
     args = ap.parse_args()
@@ -601,10 +603,12 @@ def main():
     # SURVEY §8d asks for the spec peaks re-measured on the box; measured here, on every rank's
     # GPU before its warm-up, so that the timed steps start on a GPU already at its working
     # clocks (the reported peaks are rank 0's)
-    try:
-        peaks = fcg.measure_peaks(dev.index)
-    except Exception as e:  # report, never hide
-        peaks = e
+    peaks = None
+    if not args.peaks_after:
+        try:
+            peaks = fcg.measure_peaks(dev.index)
+        except Exception as e:  # report, never hide
+            peaks = e
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -629,6 +633,11 @@ def main():
         t_as.append(b)
     torch.cuda.synchronize(dev)
     ev.set_timing(False)
+    if peaks is None:
+        try:
+            peaks = fcg.measure_peaks(dev.index)
+        except Exception as e:  # report, never hide
+            peaks = e
     elapsed = _ctl_max(t1 - t0, world)
     ms_step = 1e3 * elapsed / args.steps
     n_ele_global = mesh.n_ele_global
