@@ -1,0 +1,189 @@
+"""Multi-rank linear solve and static Newton over the C-ABI halo (SURVEY §8f row 2 across ranks).
+
+4C hands the distributed Epetra tangent to Belos CG with a point-block relaxation preconditioner
+(`4C_solver_nonlin_nox_linearsystem.cpp:275-353`; Ifpack point-block Jacobi, local to each rank)
+and NOX's full Newton measures the residual with Epetra `Norm2` (local sum + MPI_Allreduce).  Here
+every rank holds the owned rows of K in its column-map CSR (what `fcg_evaluate_device` assembles
+with the ghost-layer partition, option A):
+
+* the operator K p needs p in the column map: `fcg_halo_import` (RCCL grouped send/recv, or
+  host-staged through gloo) imports the ghost entries before `fcg_spmv`, as
+  `Epetra_CrsMatrix::Multiply` imports through the matrix's Importer;
+* the preconditioner is the inverse of the 3 x 3 nodal diagonal blocks of the owned rows
+  (`fcg_block_jacobi_setup` / `apply`), no communication;
+* dot products are local sums combined by one all-reduce of two numbers per iteration.
+
+`DistributedNewton` is `newton.StaticNewton` across ranks: set_state import of the displacement
+into the column map, evaluate, r = f_int - f_ext, Dirichlet rows, the global residual norm,
+`DistributedPCG` for the increment.  Transport: an RCCL `halo.Comm`, or None with `staged=True`
+(host-staged halo + gloo sums: several ranks on one device, where RCCL refuses)."""
+
+import ctypes
+import importlib
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+fcg = importlib.import_module("4c_amd").fcg
+halo = importlib.import_module("4c_amd.halo")
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class Transport:
+    """Halo import and all-reduce of a few float64 numbers, over RCCL or host-staged gloo."""
+
+    def __init__(self, imp, comm=None, staged=False, device=0):
+        self.imp, self.comm, self.staged = imp, comm, staged
+        self.dev = torch.device("cuda", device)
+        if not staged and comm is None:
+            raise ValueError("Transport needs an RCCL halo.Comm unless staged=True")
+
+    def import_(self, x_row, x_col, stream=None):
+        if self.staged:
+            self.imp.import_staged(x_row, x_col, stream)
+        else:
+            self.imp.import_(self.comm, x_row, x_col, stream)
+
+    def sum(self, vals):
+        """Sum of the ranks' `vals` (a float64 device tensor), returned as a host numpy array."""
+        if self.staged:
+            t = vals.cpu()
+            if dist.is_initialized() and dist.get_world_size() > 1:
+                dist.all_reduce(t)
+            return t.numpy()
+        self.comm.allreduce(vals)
+        return vals.cpu().numpy()
+
+
+class DistributedPCG:
+    """Preconditioned CG on the ranks' owned rows: solve(K, b, x, rtol, max_iter) ->
+    (iterations, relative residual), x = 0 start, |r| <= rtol |b| over all ranks (the
+    `StaticNewton` linear-solver interface)."""
+
+    def __init__(self, evaluator, transport):
+        info = evaluator.info
+        self.ev, self.tr = evaluator, transport
+        self.n, self.n_cols = int(info.n_rows), int(info.n_cols)
+        self.dev = torch.device("cuda", evaluator.device)
+        f64 = dict(dtype=torch.float64, device=self.dev)
+        self.r = torch.empty(self.n, **f64)
+        self.z = torch.empty(self.n, **f64)
+        self.p = torch.empty(self.n, **f64)
+        self.q = torch.empty(self.n, **f64)
+        self.p_col = torch.zeros(self.n_cols, **f64)
+        self.dinv = torch.empty(3 * self.n, **f64)  # 3 x 3 inverse per node (9 per 3 rows)
+        self.iterations, self.rel_residual = 0, None
+
+    def _precond(self, r, z):
+        s = torch.cuda.current_stream(self.dev).cuda_stream
+        rc = fcg.lib().fcg_block_jacobi_apply(self.ev._h, _ptr(self.dinv), _ptr(r), _ptr(z), 1.0, 0,
+                                              ctypes.c_void_p(s))
+        if rc != 0:
+            raise fcg.FcgError(rc, fcg.lib().fcg_last_error(self.ev._h).decode())
+
+    def _op(self, K, p, q):
+        self.tr.import_(p, self.p_col)
+        self.ev.spmv(K, self.p_col, q)
+
+    def solve(self, K, b, x, rtol=1e-10, max_iter=10000):
+        s = torch.cuda.current_stream(self.dev).cuda_stream
+        rc = fcg.lib().fcg_block_jacobi_setup(self.ev._h, _ptr(K), _ptr(self.dinv), ctypes.c_void_p(s))
+        if rc != 0:
+            raise fcg.FcgError(rc, fcg.lib().fcg_last_error(self.ev._h).decode())
+        x.zero_()
+        self.r.copy_(b)
+        self._precond(self.r, self.z)
+        self.p.copy_(self.z)
+        two = torch.empty(2, dtype=torch.float64, device=self.dev)
+        two[0] = torch.dot(self.r, self.z)
+        two[1] = torch.dot(b, b)
+        rz, bb = self.tr.sum(two)
+        bn = float(np.sqrt(bb))
+        if bn == 0.0:
+            self.iterations, self.rel_residual = 0, 0.0
+            return 0, 0.0
+        rn = bn
+        it = 0
+        while it < max_iter:
+            self._op(K, self.p, self.q)
+            pq = float(self.tr.sum(torch.dot(self.p, self.q).reshape(1))[0])
+            if not (pq > 0.0):
+                raise fcg.FcgError(fcg.FCG_ERR_SINGULAR, f"PCG breakdown: p.Kp = {pq} at iteration {it}")
+            alpha = rz / pq
+            x.add_(self.p, alpha=alpha)
+            self.r.add_(self.q, alpha=-alpha)
+            it += 1
+            self._precond(self.r, self.z)
+            two[0] = torch.dot(self.r, self.z)
+            two[1] = torch.dot(self.r, self.r)
+            rz_new, rr = self.tr.sum(two)
+            rn = float(np.sqrt(rr))
+            if not np.isfinite(rn):
+                raise fcg.FcgError(fcg.FCG_ERR_SINGULAR, "PCG: non-finite residual")
+            if rn <= rtol * bn:
+                break
+            self.p.mul_(rz_new / rz).add_(self.z)
+            rz = rz_new
+        self.iterations, self.rel_residual = it, rn / bn
+        return it, rn / bn
+
+
+class DistributedNewton:
+    """Static full Newton on the ranks of a ghost-layer partition: the rank's Evaluator (its
+    column elements, owned rows), the halo Transport, the owned rows' external force and
+    Dirichlet row LIDs.  solve() returns the converged owned-row displacement."""
+
+    def __init__(self, evaluator, transport, fext_row, dbc_rows, tol_res=1e-10, tol_inc=1e-10,
+                 max_iter=20, lin_rtol=1e-12, lin_max_iter=100000):
+        info = evaluator.info
+        self.ev, self.tr = evaluator, transport
+        self.dev = torch.device("cuda", evaluator.device)
+        self.n, self.n_cols, self.nnz = int(info.n_rows), int(info.n_cols), int(info.nnz)
+        f64 = dict(dtype=torch.float64, device=self.dev)
+        self.fext = torch.as_tensor(np.asarray(fext_row, dtype=np.float64)).to(self.dev)
+        self.dbc = torch.as_tensor(np.asarray(dbc_rows, dtype=np.int32)).to(self.dev)
+        self.K = torch.empty(self.nnz, **f64)
+        self.fint = torch.empty(self.n, **f64)
+        self.r = torch.empty(self.n, **f64)
+        self.du = torch.empty(self.n, **f64)
+        self.u_col = torch.zeros(self.n_cols, **f64)
+        self.freact = torch.zeros(self.n, **f64)
+        self.tol_res, self.tol_inc, self.max_iter = tol_res, tol_inc, max_iter
+        self.lin_rtol, self.lin_max_iter = lin_rtol, lin_max_iter
+        self.pcg = DistributedPCG(evaluator, transport)
+        self.history = []
+
+    def _norm(self, v):
+        return float(np.sqrt(self.tr.sum(torch.dot(v, v).reshape(1))[0]))
+
+    def solve(self, u0=None):
+        u = (torch.zeros(self.n, dtype=torch.float64, device=self.dev) if u0 is None
+             else torch.as_tensor(u0, dtype=torch.float64).to(self.dev).clone())
+        self.history = []
+        ndu = float("inf")
+        for it in range(self.max_iter + 1):
+            self.tr.import_(u, self.u_col)                      # set_state
+            self.ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, self.u_col, self.fint, self.K)
+            torch.sub(self.fint, self.fext, out=self.r)
+            self.ev.dirichlet_apply(self.dbc, self.K, self.r, self.freact)
+            nr = self._norm(self.r)
+            rec = {"iter": it, "norm_res": nr, "norm_inc": ndu if it else None}
+            if it > 0 and nr <= self.tol_res and ndu <= self.tol_inc:
+                self.history.append(rec)
+                return u
+            torch.neg(self.r, out=self.r)
+            lin_it, lin_res = self.pcg.solve(self.K, self.r, self.du, self.lin_rtol, self.lin_max_iter)
+            if not lin_res <= self.lin_rtol:
+                raise RuntimeError(f"linear solve of Newton step {it} stopped at relative residual "
+                                   f"{lin_res:.3e} ({lin_it} iterations)")
+            rec.update(lin_iter=lin_it, lin_relres=lin_res)
+            self.history.append(rec)
+            ndu = self._norm(self.du)
+            u += self.du
+            if nr == 0.0 and ndu == 0.0:
+                return u
+        raise RuntimeError(f"Newton did not converge in {self.max_iter} iterations: {self.history[-3:]}")

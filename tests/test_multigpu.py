@@ -244,3 +244,84 @@ def test_two_ranks_option_b_shared_allreduce(celltype, kinem, path):
             assert out["path"] == fcg.PATH_STRUCTURED  # strict ranks keep the fused sweep
         assert out["df"] <= 1e-10, (rank, out)
         assert out["dnorm"] <= 1e-10
+
+
+# ------------------------------------------------------ multi-rank Newton + PCG (host-staged)
+def _cantilever_loads(m, x_max):
+    """x = 0 clamped (all DOFs of the rank's owned nodes there), -1e-3 in z on every owned node at
+    x = x_max (point loads by GID: the same on any partition)."""
+    X = m.node_x
+    own = m.node_dof_row >= 0
+    fext = np.zeros(m.n_rows)
+    tip = np.nonzero(own & np.isclose(X[:, 0], x_max))[0]
+    for nd in tip:
+        fext[m.node_dof_row[nd] + 2] = -1e-3
+    cl = np.nonzero(own & np.isclose(X[:, 0], 0.0))[0]
+    dbc = np.sort((m.node_dof_row[cl][:, None] + np.arange(3)).ravel()).astype(np.int32)
+    return fext, dbc
+
+
+def _worker_solve(rank, world, port, q, kinem, path):
+    try:
+        for p in (ROOT, os.path.join(ROOT, "tests")):
+            if p not in sys.path:
+                sys.path.insert(0, p)
+        import torch.distributed as dist
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dsolve = importlib.import_module("4c_amd.dsolve")
+        iv = (8, 4, 4)
+        up = (8.0, 4.0, 4.0)
+        m = fcg.BoxMesh(fcg.HEX8, iv, upper=up, jitter=0.1, seed=5, rank=rank, nranks=world)
+        n_own = m.n_owned_rows
+        plan = halo.ImportPlan(rank, world, m.row_gid[:n_own], m.col_gid, halo.col_owner_of(m),
+                               halo.gloo_exchange())
+        h = halo.Halo(plan, 0)
+        ev = fcg.Evaluator(m, kinematics=kinem, youngs=E, poisson=NU, device=0, path=path)
+        fext, dbc = _cantilever_loads(m, up[0])
+        tr = dsolve.Transport(h, staged=True, device=0)
+        nt = dsolve.DistributedNewton(ev, tr, fext, dbc, tol_res=1e-10, tol_inc=1e-11, lin_rtol=1e-12)
+        u = nt.solve().cpu().numpy()
+        q.put((rank, True, {"u": dict(zip(m.row_gid[:n_own].tolist(), u.tolist())),
+                            "iters": [r.get("lin_iter") for r in nt.history]}))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, traceback.format_exc() + repr(e), {}))
+
+
+@pytest.mark.parametrize("kinem,path", [(fcg.LINEAR, fcg.PATH_AUTO), (fcg.TOTLAG, fcg.PATH_GENERAL)])
+def test_two_ranks_distributed_newton_pcg(kinem, path):
+    """dsolve.DistributedNewton on 2 ranks (halo import before every SpMV, global dots) converges
+    to the 1-rank StaticNewton solution of the same clamped, tip-loaded box (by DOF GID)."""
+    dev = _dev()
+    newton = importlib.import_module("4c_amd.newton")
+    iv, up = (8, 4, 4), (8.0, 4.0, 4.0)
+    m = fcg.BoxMesh(fcg.HEX8, iv, upper=up, jitter=0.1, seed=5)
+    fext, dbc = _cantilever_loads(m, up[0])
+    ev = fcg.Evaluator(m, kinematics=kinem, youngs=E, poisson=NU, device=0, path=path)
+    # tolerances above the f_int rounding floor (TotLag stalls near 1e-12 absolute here)
+    ref = newton.StaticNewton(ev, fext, dbc, tol_res=1e-10, tol_inc=1e-11, lin_rtol=1e-12).solve()
+    uref = dict(zip(m.row_gid.tolist(), ref.cpu().numpy().tolist()))
+    ev.close()
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    qq = ctx.Queue()
+    port = 29700 + os.getpid() % 1000
+    procs = [ctx.Process(target=_worker_solve, args=(r, 2, port, qq, kinem, path)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [qq.get(timeout=240) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+    got = {}
+    for rank, ok, out in res:
+        assert ok is True, (rank, ok)
+        got.update(out["u"])
+    assert set(got) == set(uref)
+    scale = max(abs(v) for v in uref.values())
+    assert scale > 0
+    worst = max(abs(got[g] - uref[g]) for g in uref)
+    assert worst <= 1e-8 * scale, (worst, scale)
+    assert dev is not None
