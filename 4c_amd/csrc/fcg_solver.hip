@@ -50,11 +50,12 @@ __device__ inline double block_sum(double v, double* sbuf)
 // (checked by fcg_create), so LPN lanes walk the node's neighbour triples -- one column index,
 // x[c..c+2] and the 3 x 3 block of the 3 rows per triple -- instead of one index per matrix entry.
 // Row-major sums in a fixed lane order: deterministic.  Optionally
-// partial[blockIdx] = sum over the block's rows of dotw[row] * y[row].
-template <int LPN>
+// partial[blockIdx] = sum over the block's rows of dotw[row] * y[row].  V = float: matrix values
+// stored in FP32 (the multigrid smoother's copy of K), vectors and sums in FP64.
+template <int LPN, typename V>
 __global__ __launch_bounds__(kBlock) void spmv_node_kernel(const int64_t* __restrict__ rowptr,
     const int32_t* __restrict__ row0_of, const int32_t* __restrict__ col,
-    const double* __restrict__ vals, const double* __restrict__ x, double* __restrict__ y,
+    const V* __restrict__ vals, const double* __restrict__ x, double* __restrict__ y,
     int64_t n_nodes, const double* __restrict__ dotw, double* partial)
 {
   __shared__ double sbuf[kBlock / 64];
@@ -72,16 +73,16 @@ __global__ __launch_bounds__(kBlock) void spmv_node_kernel(const int64_t* __rest
       row0 = row0_of[node];
       const int64_t s = rowptr[row0];
       const int64_t len = rowptr[row0 + 1] - s;
-      const double* v0 = vals + s;
-      const double* v1 = v0 + len;
-      const double* v2 = v1 + len;
+      const V* v0 = vals + s;
+      const V* v1 = v0 + len;
+      const V* v2 = v1 + len;
       for (int64_t k = 3 * lane; k < len; k += 3 * LPN)
       {
         const int32_t c = col[s + k];
         const double x0 = x[c], x1 = x[c + 1], x2 = x[c + 2];
-        a0 += v0[k] * x0 + v0[k + 1] * x1 + v0[k + 2] * x2;
-        a1 += v1[k] * x0 + v1[k + 1] * x1 + v1[k + 2] * x2;
-        a2 += v2[k] * x0 + v2[k + 1] * x1 + v2[k + 2] * x2;
+        a0 += double(v0[k]) * x0 + double(v0[k + 1]) * x1 + double(v0[k + 2]) * x2;
+        a1 += double(v1[k]) * x0 + double(v1[k + 1]) * x1 + double(v1[k + 2]) * x2;
+        a2 += double(v2[k]) * x0 + double(v2[k + 1]) * x1 + double(v2[k + 2]) * x2;
       }
     }
 #pragma unroll
@@ -385,17 +386,18 @@ __global__ __launch_bounds__(kBlock) void dot_kernel(const double* __restrict__ 
   if (threadIdx.x == 0) partial[blockIdx.x] = b;
 }
 
-hipError_t launch_spmv(const DeviceMesh& m, const double* K, const double* x, double* y,
+template <typename V>
+hipError_t launch_spmv(const DeviceMesh& m, const V* K, const double* x, double* y,
     const double* dotw, double* partial, hipStream_t s)
 {
   if (m.n_rows == 0) return hipSuccess;
   // node rows (every owned row belongs to a node triple, fcg_create checks the pattern)
   if (m.npe == 27)
-    hipLaunchKernelGGL((spmv_node_kernel<64>), dim3(spmv_grid(m, 64, partial != nullptr)),
+    hipLaunchKernelGGL((spmv_node_kernel<64, V>), dim3(spmv_grid(m, 64, partial != nullptr)),
         dim3(kBlock), 0, s, m.rowptr, m.rownode_row0, m.col_lid, K, x, y, m.n_rownodes, dotw,
         partial);
   else
-    hipLaunchKernelGGL((spmv_node_kernel<16>), dim3(spmv_grid(m, 16, partial != nullptr)),
+    hipLaunchKernelGGL((spmv_node_kernel<16, V>), dim3(spmv_grid(m, 16, partial != nullptr)),
         dim3(kBlock), 0, s, m.rowptr, m.rownode_row0, m.col_lid, K, x, y, m.n_rownodes, dotw,
         partial);
   return hipGetLastError();
@@ -416,6 +418,21 @@ int fcg_spmv(fcg_ctx* ctx, const double* d_K_vals, const double* d_x_col, double
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   hipError_t he = fcg::launch_spmv(ctx->mesh, d_K_vals, d_x_col, d_y_row, nullptr, nullptr, s);
   if (he == hipSuccess) he = hipStreamSynchronize(s);
+  if (he != hipSuccess)
+  {
+    ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
+    return FCG_ERR_DEVICE;
+  }
+  return FCG_OK;
+}
+
+int fcg_spmv_f32(fcg_ctx* ctx, const float* d_K32, const double* d_x_col, double* d_y_row,
+    void* stream)
+{
+  if (!ctx || (ctx->mesh.n_rows > 0 && (!d_K32 || !d_x_col || !d_y_row))) return FCG_ERR_ARG;
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  hipError_t he = fcg::launch_spmv(ctx->mesh, d_K32, d_x_col, d_y_row, nullptr, nullptr, s);
   if (he != hipSuccess)
   {
     ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);

@@ -20,7 +20,11 @@ the same polynomial before and after the coarse correction.  Coarsest level: blo
 loose tolerance -- a nonlinear preconditioner, so the outer iteration is flexible CG
 (Polak-Ribiere beta).  Every level's K, the work vectors and the transfer tables stay in HBM;
 torch supplies the buffers and the vector updates (axpy, dot), the library the operator, the
-smoother's block-diagonal solve and the transfers.
+smoother's block-diagonal solve and the transfers.  With mixed=True the fine level's Chebyshev
+smoother SpMVs (3 of the 5 per iteration) read an FP32 copy of K (fcg_spmv_f32); the outer
+flexible CG's SpMV and the residual restricted to the coarse level stay FP64.  Off by default:
+on the hex27 TotLag cantilever of tests/test_multigrid.py it raised the FCG iterations to a
+1e-12 tolerance from below 525 to 888.
 """
 
 import ctypes
@@ -139,6 +143,7 @@ class _Level:
             self.mask[torch.as_tensor(np.asarray(dbc_rows, dtype=np.int64), device=device)] = 0.0
         self.x, self.b, self.r, self.d, self.z = (torch.zeros(self.n, **f64) for _ in range(5))
         self.lmax = None
+        self.K32 = None  # FP32 copy of K for the smoother and the V-cycle residual (mixed=True)
 
     def stream(self):
         return torch.cuda.current_stream(self.dev)
@@ -157,6 +162,13 @@ class _Level:
             self.ev._raise(rc, -1)
 
     def spmv(self, x, y):
+        """The V-cycle's operator: K, or its FP32 copy when the level has one."""
+        if self.K32 is not None:
+            self.ev.spmv_f32(self.K32, x, y, stream=self.stream())
+        else:
+            self.ev.spmv(self.K, x, y, stream=self.stream())
+
+    def spmv_exact(self, x, y):
         self.ev.spmv(self.K, x, y, stream=self.stream())
 
     def estimate_lmax(self, iters=10, seed=20251015):
@@ -215,7 +227,8 @@ class Multigrid:
     dbc_nodes(mesh) -> bool mask of the clamped nodes of a mesh of the same box (all 3 DOFs)."""
 
     def __init__(self, fine_mesh, fine_ev, dbc_nodes, youngs, poisson, nu=2, min_intervals=4,
-                 max_levels=8, ratio=20.0, boost=1.1, coarse_rtol=1e-2, coarse_max_iter=2000):
+                 max_levels=8, ratio=20.0, boost=1.1, coarse_rtol=1e-2, coarse_max_iter=2000,
+                 mixed=False):
         box = getattr(fine_mesh, "box", None)
         if box is None or getattr(fine_mesh, "nranks", 1) != 1:
             raise ValueError("Multigrid needs a single-rank GridGenerator box (fcg.BoxMesh)")
@@ -232,6 +245,10 @@ class Multigrid:
                              f"with n/2 >= min_intervals ({min_intervals})")
         dev = torch.device("cuda", fine_ev.device)
         self.dev, self.nu, self.ratio, self.boost = dev, nu, ratio, boost
+        # mixed: the fine level's Chebyshev smoother uses an FP32 copy of K (half the bytes of
+        # 3 of the 5 SpMVs that dominate an iteration); the outer flexible CG and the restricted
+        # residual keep the FP64 operator, so the solve still converges to the FP64 tolerance
+        self.mixed = mixed
         self.coarse_rtol, self.coarse_max_iter = coarse_rtol, coarse_max_iter
         self.trace = bool(os.environ.get("FCG_MG_TRACE"))  # per-iteration residuals to stderr
         lower = [box.lower[d] for d in range(3)]
@@ -304,7 +321,7 @@ class Multigrid:
                              stream=torch.cuda.current_stream(self.dev))
             return
         self._cheb(lvl, b, x, x_zero=True)
-        lvl.spmv(x, lvl.r)
+        lvl.spmv_exact(x, lvl.r)  # the restricted residual stays FP64 (mixed: smoother only)
         torch.sub(b, lvl.r, out=lvl.r)
         c = self.levels[l + 1]
         self.R[l](lvl.r, c.b, accumulate=False)
@@ -336,6 +353,10 @@ class Multigrid:
         MultigridError."""
         f0 = self.levels[0]
         f0.K = K
+        if self.mixed:
+            if f0.K32 is None or f0.K32.numel() != K.numel():
+                f0.K32 = torch.empty(K.numel(), dtype=torch.float32, device=K.device)
+            f0.K32.copy_(K)
         f0.setup_diag()
         if f0.lmax is None:
             f0.estimate_lmax()
@@ -372,7 +393,7 @@ class Multigrid:
         it = 0
         while it < max_iter:
             it += 1
-            f0.spmv(p, q)
+            f0.spmv_exact(p, q)
             alpha = rz / float(torch.dot(p, q))
             x.add_(p, alpha=alpha)
             r_old = r.clone()  # z . r_old enters the Polak-Ribiere beta

@@ -195,6 +195,11 @@ int fcg_dirichlet_apply(fcg_ctx* ctx, int64_t n_dbc, const int32_t* d_rows, doub
     double* d_rhs_row, double* d_freact_row, void* stream);
 /* K x = b by CG preconditioned with the inverse 3x3 nodal diagonal blocks (block Jacobi) from x = 0 until |r| <= rtol |b| or max_iter iterations;
  * single-rank systems only (matrix column map = row map), else FCG_ERR_ARG.  Deterministic. */
+/* y_row = K x_col with the matrix values stored in FP32 (vectors and sums FP64): the multigrid
+ * smoother's reduced-precision copy of K (4c_amd/multigrid.py, mixed=True), half the bytes of
+ * fcg_spmv.  Asynchronous on `stream` (no drain). */
+int fcg_spmv_f32(fcg_ctx* ctx, const float* d_K32, const double* d_x_col, double* d_y_row,
+    void* stream);
 int fcg_pcg_solve(fcg_ctx* ctx, const double* d_K_vals, const double* d_b_row, double* d_x_row,
     double rtol, int max_iter, int* iterations, double* rel_residual, void* stream);
 /* Pieces of the geometric multigrid preconditioner (4c_amd/multigrid.py; the MueLu

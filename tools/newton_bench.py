@@ -35,6 +35,7 @@ ap.add_argument("--mg", action="store_true",
 ap.add_argument("--mg-nu", type=int, default=2, help="Chebyshev degree of the MG smoother")
 ap.add_argument("--mg-coarse-rtol", type=float, default=1e-2)
 ap.add_argument("--mg-ratio", type=float, default=20.0)
+ap.add_argument("--mg-mixed", action="store_true", help="FP32 copy of K in the fine smoother")
 a = ap.parse_args()
 ct = fcg.HEX8 if a.celltype == "hex8" else fcg.HEX27
 kin = fcg.LINEAR if a.kinem == "linear" else fcg.TOTLAG
@@ -106,7 +107,7 @@ if a.mg:
     t_mg = time.perf_counter()
     mg = importlib.import_module("4c_amd.multigrid").Multigrid(
         mesh, ev, lambda m: np.isclose(m.node_x[:, 0], 0.0), 210.0, 0.3, nu=a.mg_nu,
-        coarse_rtol=a.mg_coarse_rtol, ratio=a.mg_ratio)
+        coarse_rtol=a.mg_coarse_rtol, ratio=a.mg_ratio, mixed=a.mg_mixed)
     print(f"multigrid setup {time.perf_counter() - t_mg:.1f} s: {json.dumps(mg.describe())}",
           file=sys.stderr, flush=True)
     t_setup = time.perf_counter() - t0
