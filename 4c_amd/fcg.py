@@ -117,7 +117,11 @@ EXPORTS = ["fcg_create", "fcg_destroy", "fcg_last_error", "fcg_evaluate", "fcg_e
            "fcg_halo_destroy", "fcg_halo_import", "fcg_halo_pack", "fcg_halo_unpack",
            "fcg_shared_plan_build", "fcg_shared_create", "fcg_shared_destroy", "fcg_shared_reduce",
            "fcg_shared_pack", "fcg_shared_unpack", "fcg_norm2", "fcg_set_async", "fcg_check_error",
-           "fcg_evaluate_host"]
+           "fcg_evaluate_host",
+           "fcg_amg_aggregate", "fcg_amg_tentative", "fcg_bsr_symbolic", "fcg_bsr_transpose_pattern",
+           "fcg_bsr_spmv", "fcg_bsr_spgemm", "fcg_bsr_transpose_values", "fcg_bsr_from_node_csr",
+           "fcg_bsr_block_jacobi_setup", "fcg_bsr_block_jacobi_apply", "fcg_amg_smooth_prolongator",
+           "fcg_bsr_to_dense"]
 
 _lib = None
 FUNCT_FN = ctypes.CFUNCTYPE(ctypes.c_double, ctypes.c_int, _dp, ctypes.c_double, ctypes.c_void_p)
@@ -223,6 +227,23 @@ def lib():
                                           ctypes.c_double, vp, vp, vp, vp, vp, vp, _i32p]
     L.fcg_tsi_evaluate_fused.argtypes = [vp, vp, ctypes.c_int, vp, vp, vp, ctypes.c_double,
                                          ctypes.c_double, vp, vp, vp, vp, vp, vp, vp, _i32p]
+    i64, c_int, c_dbl = ctypes.c_int64, ctypes.c_int, ctypes.c_double
+    L.fcg_amg_aggregate.argtypes = [i64, vp, vp, vp, vp]
+    L.fcg_amg_aggregate.restype = i64
+    L.fcg_amg_tentative.argtypes = [i64, c_int, vp, vp, i64, vp, vp, vp]
+    L.fcg_bsr_symbolic.argtypes = [i64, vp, vp, vp, vp, i64, vp, vp]
+    L.fcg_bsr_symbolic.restype = i64
+    L.fcg_bsr_transpose_pattern.argtypes = [i64, i64, vp, vp, vp, vp, vp]
+    L.fcg_bsr_spmv.argtypes = [c_int, c_int, c_int, i64, vp, vp, vp, vp, vp, c_dbl, c_int, vp]
+    L.fcg_bsr_spgemm.argtypes = [c_int, c_int, c_int, c_int, i64, vp, vp, vp, vp, vp, vp, vp, vp,
+                                 vp, vp]
+    L.fcg_bsr_transpose_values.argtypes = [c_int, c_int, c_int, i64, vp, vp, vp, vp]
+    L.fcg_bsr_from_node_csr.argtypes = [c_int, i64, vp, vp, vp, vp, vp]
+    L.fcg_bsr_block_jacobi_setup.argtypes = [c_int, c_int, i64, vp, vp, vp, vp, vp, vp]
+    L.fcg_bsr_block_jacobi_apply.argtypes = [c_int, c_int, i64, vp, vp, vp, c_dbl, c_int, vp]
+    L.fcg_amg_smooth_prolongator.argtypes = [c_int, c_int, i64, vp, vp, vp, vp, vp, vp, c_dbl, vp,
+                                             vp]
+    L.fcg_bsr_to_dense.argtypes = [c_int, c_int, i64, vp, vp, vp, vp, vp]
     _lib = L
     return L
 
@@ -378,7 +399,9 @@ class Discretization:
         off = np.arange(rowptr[-1]) - rowptr[row]
         col = (3 * nb[start[row // 3] + off // 3] + off % 3).astype(np.int32)
         dof = 3 * np.arange(nn, dtype=np.int32)
-        return Discretization(box.celltype, en, X, dof, dof, rowptr, col)
+        dis = Discretization(box.celltype, en, X, dof, dof, rowptr, col)
+        dis.node_perm = perm  # new number of every box node (DOF 3 * perm[old] + d)
+        return dis
 
 
 def _neumann(entry, celltype, conn, node_x, node_dof_row, onoff, val, funct, fn, time, fext):

@@ -130,46 +130,9 @@ class _Transfer:
             raise fcg.FcgError(rc, "fcg_node_transfer failed")
 
 
-class _Level:
-    def __init__(self, mesh, ev, K, dbc_rows, device):
-        self.mesh, self.ev, self.K = mesh, ev, K
-        self.rows = np.asarray(dbc_rows, dtype=np.int32)
-        self.n = mesh.n_rows
-        self.dev = device
-        f64 = dict(dtype=torch.float64, device=device)
-        self.dinv = torch.empty(9 * (self.n // 3), **f64)
-        self.mask = torch.ones(self.n, **f64)
-        if len(dbc_rows):
-            self.mask[torch.as_tensor(np.asarray(dbc_rows, dtype=np.int64), device=device)] = 0.0
-        self.x, self.b, self.r, self.d, self.z = (torch.zeros(self.n, **f64) for _ in range(5))
-        self.lmax = None
-        self.K32 = None  # FP32 copy of K for the smoother and the V-cycle residual (mixed=True)
-
-    def stream(self):
-        return torch.cuda.current_stream(self.dev)
-
-    def setup_diag(self):
-        rc = fcg.lib().fcg_block_jacobi_setup(self.ev._h, _ptr(self.K), _ptr(self.dinv),
-                                              ctypes.c_void_p(self.stream().cuda_stream))
-        if rc != 0:
-            self.ev._raise(rc, -1)
-
-    def apply_dinv(self, r, z, scale=1.0, accumulate=False):
-        rc = fcg.lib().fcg_block_jacobi_apply(self.ev._h, _ptr(self.dinv), _ptr(r), _ptr(z),
-                                              ctypes.c_double(scale), 1 if accumulate else 0,
-                                              ctypes.c_void_p(self.stream().cuda_stream))
-        if rc != 0:
-            self.ev._raise(rc, -1)
-
-    def spmv(self, x, y):
-        """The V-cycle's operator: K, or its FP32 copy when the level has one."""
-        if self.K32 is not None:
-            self.ev.spmv_f32(self.K32, x, y, stream=self.stream())
-        else:
-            self.ev.spmv(self.K, x, y, stream=self.stream())
-
-    def spmv_exact(self, x, y):
-        self.ev.spmv(self.K, x, y, stream=self.stream())
+class _LevelOps:
+    """What the Chebyshev smoother and the Lanczos estimate need of a level: n, dev, mask, the
+    work vectors r and z, spmv(x, y) and apply_dinv(r, z, scale, accumulate)."""
 
     def estimate_lmax(self, iters=10, seed=20251015):
         """Largest eigenvalue of D^-1 K from the Lanczos tridiagonal of a short block-Jacobi PCG
@@ -211,6 +174,48 @@ class _Level:
         self.lmax = float(np.linalg.eigvalsh(T)[-1])
 
 
+class _Level(_LevelOps):
+    def __init__(self, mesh, ev, K, dbc_rows, device):
+        self.mesh, self.ev, self.K = mesh, ev, K
+        self.rows = np.asarray(dbc_rows, dtype=np.int32)
+        self.n = mesh.n_rows
+        self.dev = device
+        f64 = dict(dtype=torch.float64, device=device)
+        self.dinv = torch.empty(9 * (self.n // 3), **f64)
+        self.mask = torch.ones(self.n, **f64)
+        if len(dbc_rows):
+            self.mask[torch.as_tensor(np.asarray(dbc_rows, dtype=np.int64), device=device)] = 0.0
+        self.x, self.b, self.r, self.d, self.z = (torch.zeros(self.n, **f64) for _ in range(5))
+        self.lmax = None
+        self.K32 = None  # FP32 copy of K for the smoother and the V-cycle residual (mixed=True)
+
+    def stream(self):
+        return torch.cuda.current_stream(self.dev)
+
+    def setup_diag(self):
+        rc = fcg.lib().fcg_block_jacobi_setup(self.ev._h, _ptr(self.K), _ptr(self.dinv),
+                                              ctypes.c_void_p(self.stream().cuda_stream))
+        if rc != 0:
+            self.ev._raise(rc, -1)
+
+    def apply_dinv(self, r, z, scale=1.0, accumulate=False):
+        rc = fcg.lib().fcg_block_jacobi_apply(self.ev._h, _ptr(self.dinv), _ptr(r), _ptr(z),
+                                              ctypes.c_double(scale), 1 if accumulate else 0,
+                                              ctypes.c_void_p(self.stream().cuda_stream))
+        if rc != 0:
+            self.ev._raise(rc, -1)
+
+    def spmv(self, x, y):
+        """The V-cycle's operator: K, or its FP32 copy when the level has one."""
+        if self.K32 is not None:
+            self.ev.spmv_f32(self.K32, x, y, stream=self.stream())
+        else:
+            self.ev.spmv(self.K, x, y, stream=self.stream())
+
+    def spmv_exact(self, x, y):
+        self.ev.spmv(self.K, x, y, stream=self.stream())
+
+
 class _Indefinite(Exception):
     """The V-cycle returned a non-descent direction (r . z <= 0): smoother bound too low."""
 
@@ -220,7 +225,119 @@ class MultigridError(RuntimeError):
     fresh one (indefinite V-cycle, or no convergence to the requested tolerance)."""
 
 
-class Multigrid:
+class CycleFCG:
+    """Flexible CG preconditioned by one V-cycle (the outer solve of Multigrid and amg.AMG).
+    Subclasses hold `levels` (level 0: the system's _Level on the evaluator's K) and supply
+    _prepare(K) (per-tangent setup), _restrict(l, r, b_coarse), _prolong(l, x_coarse, x) (adds
+    into x) and _coarse_solve(level, b, x); nu, ratio, boost, trace and dev as in Multigrid."""
+
+    # -- smoother ---------------------------------------------------------------------------
+    def _cheb(self, lvl, b, x, x_zero):
+        lmax = self.boost * lvl.lmax
+        lmin = lmax / self.ratio
+        theta, delta = 0.5 * (lmax + lmin), 0.5 * (lmax - lmin)
+        sigma = theta / delta
+        rho = 1.0 / sigma
+        r, d = lvl.r, lvl.d
+        if x_zero:
+            lvl.apply_dinv(b, d, 1.0 / theta)
+            x.copy_(d)
+        else:
+            lvl.spmv(x, r)
+            torch.sub(b, r, out=r)
+            lvl.apply_dinv(r, d, 1.0 / theta)
+            x.add_(d)
+        for _ in range(self.nu - 1):
+            lvl.spmv(x, r)
+            torch.sub(b, r, out=r)
+            rho_n = 1.0 / (2.0 * sigma - rho)
+            d.mul_(rho_n * rho)
+            lvl.apply_dinv(r, d, 2.0 * rho_n / delta, accumulate=True)
+            x.add_(d)
+            rho = rho_n
+
+    def _vcycle(self, l, b, x):
+        lvl = self.levels[l]
+        if l == len(self.levels) - 1:
+            self._coarse_solve(lvl, b, x)
+            return
+        self._cheb(lvl, b, x, x_zero=True)
+        lvl.spmv_exact(x, lvl.r)  # the restricted residual stays FP64 (mixed: smoother only)
+        torch.sub(b, lvl.r, out=lvl.r)
+        c = self.levels[l + 1]
+        self._restrict(l, lvl.r, c.b)
+        self._vcycle(l + 1, c.b, c.x)
+        self._prolong(l, c.x, x)
+        self._cheb(lvl, b, x, x_zero=False)
+
+    # -- outer solve ------------------------------------------------------------------------
+    def solve(self, K, b, x, rtol, max_iter=1000):
+        """K x = b from x = 0 by flexible CG; returns (iterations, relative residual).
+
+        A solve that meets an indefinite preconditioned step, or ends above rtol (a stale, too
+        low lambda_max estimate lets the Chebyshev smoother amplify modes without r.z turning
+        negative), re-estimates the fine level's lambda_max and restarts once; a second failure
+        raises MultigridError."""
+        f0 = self.levels[0]
+        self._prepare(K)
+        why = None
+        for attempt in range(2):
+            if attempt:
+                f0.estimate_lmax()
+            try:
+                it, rel = self._fcg(f0, b, x, rtol, max_iter)
+            except (_Indefinite, FloatingPointError) as e:
+                why = repr(e) or "indefinite V-cycle"
+                continue
+            if rel <= rtol:
+                return it, rel
+            why = f"relative residual {rel:.3e} > {rtol:.3e} after {it} iterations"
+        raise MultigridError(f"multigrid FCG failed after a lambda_max re-estimate: {why}")
+
+    def _fcg(self, f0, b, x, rtol, max_iter):
+        if self.trace:
+            print(f"  levels: {self.describe()}", file=sys.stderr, flush=True)
+        bn = float(torch.linalg.vector_norm(b))
+        x.zero_()
+        if bn == 0.0:
+            return 0, 0.0
+        r = b.clone()
+        z = torch.zeros_like(b)
+        q = torch.empty_like(b)
+        self._vcycle(0, r, z)
+        p = z.clone()
+        rz = float(torch.dot(r, z))
+        if not rz > 0.0:
+            raise _Indefinite()
+        rn = bn
+        it = 0
+        while it < max_iter:
+            it += 1
+            f0.spmv_exact(p, q)
+            alpha = rz / float(torch.dot(p, q))
+            x.add_(p, alpha=alpha)
+            r_old = r.clone()  # z . r_old enters the Polak-Ribiere beta
+            r.add_(q, alpha=-alpha)
+            rn = float(torch.linalg.vector_norm(r))
+            if not np.isfinite(rn):
+                raise FloatingPointError("multigrid FCG diverged (non-finite residual)")
+            if rn <= rtol * bn:
+                break
+            z = torch.zeros_like(b)
+            self._vcycle(0, r, z)
+            rz_new = float(torch.dot(r, z))
+            if not rz_new > 0.0:
+                raise _Indefinite()
+            beta = (rz_new - float(torch.dot(z, r_old))) / rz
+            if self.trace:
+                print(f"  fcg {it}: |r|/|b| {rn / bn:.3e} rz {rz_new:.3e} beta {beta:.3e} "
+                      f"alpha {alpha:.3e}", file=sys.stderr, flush=True)
+            p.mul_(beta).add_(z)
+            rz = rz_new
+        return it, rn / bn
+
+
+class Multigrid(CycleFCG):
     """Flexible-CG solver preconditioned by a geometric multigrid V-cycle (see module doc).
 
     fine_mesh / fine_ev: the discretisation being solved (BoxMesh + Evaluator, single rank);
@@ -289,47 +406,30 @@ class Multigrid:
                  "intervals": [int(l.mesh.box.interval[d]) for d in range(3)], "dofs": l.n,
                  "lmax": l.lmax} for l in self.levels]
 
-    # -- smoother ---------------------------------------------------------------------------
-    def _cheb(self, lvl, b, x, x_zero):
-        lmax = self.boost * lvl.lmax
-        lmin = lmax / self.ratio
-        theta, delta = 0.5 * (lmax + lmin), 0.5 * (lmax - lmin)
-        sigma = theta / delta
-        rho = 1.0 / sigma
-        r, d = lvl.r, lvl.d
-        if x_zero:
-            lvl.apply_dinv(b, d, 1.0 / theta)
-            x.copy_(d)
-        else:
-            lvl.spmv(x, r)
-            torch.sub(b, r, out=r)
-            lvl.apply_dinv(r, d, 1.0 / theta)
-            x.add_(d)
-        for _ in range(self.nu - 1):
-            lvl.spmv(x, r)
-            torch.sub(b, r, out=r)
-            rho_n = 1.0 / (2.0 * sigma - rho)
-            d.mul_(rho_n * rho)
-            lvl.apply_dinv(r, d, 2.0 * rho_n / delta, accumulate=True)
-            x.add_(d)
-            rho = rho_n
+    def _prepare(self, K):
+        """lambda_max of D^-1 K barely moves between Newton iterations: it is estimated on the
+        first solve and kept (re-estimated by CycleFCG.solve's restart)."""
+        f0 = self.levels[0]
+        f0.K = K
+        if self.mixed:
+            if f0.K32 is None or f0.K32.numel() != K.numel():
+                f0.K32 = torch.empty(K.numel(), dtype=torch.float32, device=K.device)
+            f0.K32.copy_(K)
+        f0.setup_diag()
+        if f0.lmax is None:
+            f0.estimate_lmax()
 
-    def _vcycle(self, l, b, x):
-        lvl = self.levels[l]
-        if l == len(self.levels) - 1:
-            lvl.ev.pcg_solve(lvl.K, b, x, self.coarse_rtol, self.coarse_max_iter,
-                             stream=torch.cuda.current_stream(self.dev))
-            return
-        self._cheb(lvl, b, x, x_zero=True)
-        lvl.spmv_exact(x, lvl.r)  # the restricted residual stays FP64 (mixed: smoother only)
-        torch.sub(b, lvl.r, out=lvl.r)
-        c = self.levels[l + 1]
-        self.R[l](lvl.r, c.b, accumulate=False)
-        c.b.mul_(c.mask)
-        self._vcycle(l + 1, c.b, c.x)
-        self.P[l](c.x, x, accumulate=True)
-        x.mul_(lvl.mask)
-        self._cheb(lvl, b, x, x_zero=False)
+    def _restrict(self, l, r, cb):
+        self.R[l](r, cb, accumulate=False)
+        cb.mul_(self.levels[l + 1].mask)
+
+    def _prolong(self, l, cx, x):
+        self.P[l](cx, x, accumulate=True)
+        x.mul_(self.levels[l].mask)
+
+    def _coarse_solve(self, lvl, b, x):
+        lvl.ev.pcg_solve(lvl.K, b, x, self.coarse_rtol, self.coarse_max_iter,
+                         stream=torch.cuda.current_stream(self.dev))
 
     # -- outer solve ------------------------------------------------------------------------
     def check_dirichlet(self, dbc_rows):
@@ -342,76 +442,3 @@ class Multigrid:
             raise ValueError(f"multigrid Dirichlet rows ({len(mine)}) differ from the system's "
                              f"({len(theirs)}): pass a dbc_nodes mask with the same nodes and all "
                              f"three DOFs constrained")
-
-    def solve(self, K, b, x, rtol, max_iter=1000):
-        """K x = b from x = 0 by flexible CG; returns (iterations, relative residual).
-
-        lambda_max of D^-1 K barely moves between Newton iterations: it is estimated on the first
-        solve and kept.  A solve that meets an indefinite preconditioned step, or ends above rtol
-        (a stale, too low estimate lets the Chebyshev smoother amplify modes without r.z turning
-        negative), re-estimates lambda_max and restarts once; a second failure raises
-        MultigridError."""
-        f0 = self.levels[0]
-        f0.K = K
-        if self.mixed:
-            if f0.K32 is None or f0.K32.numel() != K.numel():
-                f0.K32 = torch.empty(K.numel(), dtype=torch.float32, device=K.device)
-            f0.K32.copy_(K)
-        f0.setup_diag()
-        if f0.lmax is None:
-            f0.estimate_lmax()
-        why = None
-        for attempt in range(2):
-            if attempt:
-                f0.estimate_lmax()
-            try:
-                it, rel = self._fcg(f0, b, x, rtol, max_iter)
-            except (_Indefinite, FloatingPointError) as e:
-                why = repr(e) or "indefinite V-cycle"
-                continue
-            if rel <= rtol:
-                return it, rel
-            why = f"relative residual {rel:.3e} > {rtol:.3e} after {it} iterations"
-        raise MultigridError(f"multigrid FCG failed after a lambda_max re-estimate: {why}")
-
-    def _fcg(self, f0, b, x, rtol, max_iter):
-        if self.trace:
-            print(f"  multigrid levels: {self.describe()}", file=sys.stderr, flush=True)
-        bn = float(torch.linalg.vector_norm(b))
-        x.zero_()
-        if bn == 0.0:
-            return 0, 0.0
-        r = b.clone()
-        z = torch.zeros_like(b)
-        q = torch.empty_like(b)
-        self._vcycle(0, r, z)
-        p = z.clone()
-        rz = float(torch.dot(r, z))
-        if not rz > 0.0:
-            raise _Indefinite()
-        rn = bn
-        it = 0
-        while it < max_iter:
-            it += 1
-            f0.spmv_exact(p, q)
-            alpha = rz / float(torch.dot(p, q))
-            x.add_(p, alpha=alpha)
-            r_old = r.clone()  # z . r_old enters the Polak-Ribiere beta
-            r.add_(q, alpha=-alpha)
-            rn = float(torch.linalg.vector_norm(r))
-            if not np.isfinite(rn):
-                raise FloatingPointError("multigrid FCG diverged (non-finite residual)")
-            if rn <= rtol * bn:
-                break
-            z = torch.zeros_like(b)
-            self._vcycle(0, r, z)
-            rz_new = float(torch.dot(r, z))
-            if not rz_new > 0.0:
-                raise _Indefinite()
-            beta = (rz_new - float(torch.dot(z, r_old))) / rz
-            if self.trace:
-                print(f"  fcg {it}: |r|/|b| {rn / bn:.3e} rz {rz_new:.3e} beta {beta:.3e} "
-                      f"alpha {alpha:.3e}", file=sys.stderr, flush=True)
-            p.mul_(beta).add_(z)
-            rz = rz_new
-        return it, rn / bn

@@ -217,6 +217,53 @@ int fcg_node_transfer(int device, int64_t n_out, const int64_t* d_ptr, const int
     const double* d_w, const int32_t* d_dst_row0, const double* d_x, double* d_y, int accumulate,
     void* stream);
 
+/* Smoothed-aggregation AMG for meshes without a box hierarchy (replaces the MueLu preconditioner
+ * 4C builds in 4C_linear_solver_preconditioner_muelu.cpp; algorithm in fcg_amg_setup.cpp).
+ * Host, graph only (block = node): fcg_amg_aggregate returns the number of aggregates (-1 on bad
+ * input) and agg[i] (-1 for skipped nodes); fcg_amg_tentative factors each aggregate's stacked
+ * near-null space ns[n][bs][6] into the tentative blocks p_vals[n][bs][6] and the coarse near-null
+ * space ns_coarse[n_agg][6][6]; fcg_bsr_symbolic gives the block pattern of C = A B (count pass
+ * with c_col = NULL, then fill pass; columns ascending); fcg_bsr_transpose_pattern the pattern of
+ * A^T with perm[t] = A's block index.
+ * Device (BSR: int64 block row pointers, int32 block columns, row-major blocks; asynchronous on
+ * `stream` except fcg_bsr_block_jacobi_setup, which drains it to read the flag):
+ * fcg_bsr_spmv y = alpha A x (+ y), blocks br x bc in {3,6}^2; fcg_bsr_spgemm C = A B on C's
+ * pattern for (br, bk, bc) in {(3,3,6), (6,3,6), (6,6,6), (3,3,3)}; fcg_bsr_transpose_values
+ * (3x6 and 6x6); fcg_bsr_from_node_csr copies a context's node-triple K (rows 3b..3b+2 = block
+ * row b) into 3 x 3 blocks; fcg_bsr_block_jacobi_setup inverts the diagonal blocks (b = 3, 6; a
+ * scalar row empty across its block row first gets a unit diagonal in d_vals) and returns
+ * FCG_ERR_SINGULAR for a missing or singular block; fcg_bsr_block_jacobi_apply z = scale D^-1 r
+ * (+ z); fcg_amg_smooth_prolongator P = T - omega D^-1 (A T) on P's pattern (br = 3, 6; 6
+ * columns); fcg_bsr_to_dense fills a zeroed row-major dense matrix. */
+int64_t fcg_amg_aggregate(int64_t n, const int64_t* ptr, const int32_t* adj, const uint8_t* skip,
+    int32_t* agg);
+int fcg_amg_tentative(int64_t n, int bs, const double* ns, const int32_t* agg, int64_t n_agg,
+    double* p_vals, double* ns_coarse, int64_t* n_deficient);
+int64_t fcg_bsr_symbolic(int64_t n_rows, const int64_t* a_ptr, const int32_t* a_col,
+    const int64_t* b_ptr, const int32_t* b_col, int64_t n_cols, int64_t* c_ptr, int32_t* c_col);
+int fcg_bsr_transpose_pattern(int64_t n_rows, int64_t n_cols, const int64_t* ptr,
+    const int32_t* col, int64_t* t_ptr, int32_t* t_col, int64_t* perm);
+int fcg_bsr_spmv(int device, int br, int bc, int64_t n_brows, const int64_t* d_ptr,
+    const int32_t* d_col, const double* d_vals, const double* d_x, double* d_y, double alpha,
+    int accumulate, void* stream);
+int fcg_bsr_spgemm(int device, int br, int bk, int bc, int64_t n_brows, const int64_t* d_a_ptr,
+    const int32_t* d_a_col, const double* d_a_vals, const int64_t* d_b_ptr, const int32_t* d_b_col,
+    const double* d_b_vals, const int64_t* d_c_ptr, const int32_t* d_c_col, double* d_c_vals,
+    void* stream);
+int fcg_bsr_transpose_values(int device, int br, int bc, int64_t nnzb, const int64_t* d_perm,
+    const double* d_vals, double* d_t_vals, void* stream);
+int fcg_bsr_from_node_csr(int device, int64_t n_brows, const int64_t* d_rowptr,
+    const int64_t* d_b_ptr, const double* d_K, double* d_b_vals, void* stream);
+int fcg_bsr_block_jacobi_setup(int device, int b, int64_t n_brows, const int64_t* d_ptr,
+    const int64_t* d_diag_idx, double* d_vals, double* d_dinv, int32_t* d_flag, void* stream);
+int fcg_bsr_block_jacobi_apply(int device, int b, int64_t n_brows, const double* d_dinv,
+    const double* d_r, double* d_z, double scale, int accumulate, void* stream);
+int fcg_amg_smooth_prolongator(int device, int br, int64_t n_brows, const int64_t* d_p_ptr,
+    const int32_t* d_p_col, const int32_t* d_agg, const double* d_tent, const double* d_dinv,
+    const double* d_at, double omega, double* d_p_vals, void* stream);
+int fcg_bsr_to_dense(int device, int b, int64_t n_brows, const int64_t* d_ptr, const int32_t* d_col,
+    const double* d_vals, double* d_dense, void* stream);
+
 /* Neumann loads (host arrays; added into fext_row, owned rows only).  funct[d] > 0 selects a
  * spatial function evaluated through `fn` at the reference position of each integration point
  * (Core::Utils::FunctionOfSpaceTime::evaluate); funct may be NULL.

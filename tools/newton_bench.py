@@ -36,6 +36,10 @@ ap.add_argument("--mg-nu", type=int, default=2, help="Chebyshev degree of the MG
 ap.add_argument("--mg-coarse-rtol", type=float, default=1e-2)
 ap.add_argument("--mg-ratio", type=float, default=20.0)
 ap.add_argument("--mg-mixed", action="store_true", help="FP32 copy of K in the fine smoother")
+ap.add_argument("--amg", action="store_true",
+                help="smoothed-aggregation AMG preconditioned flexible CG (4c_amd/amg.py)")
+ap.add_argument("--renumber", action="store_true",
+                help="solve on the box renumbered as an input-file mesh (no lattice, random order)")
 a = ap.parse_args()
 ct = fcg.HEX8 if a.celltype == "hex8" else fcg.HEX27
 kin = fcg.LINEAR if a.kinem == "linear" else fcg.TOTLAG
@@ -49,6 +53,14 @@ faces = mesh.ele_nodes[mesh.ele_ijk[:, 0] == a.n - 1][:, face]
 fext = np.zeros(mesh.n_rows)
 fcg.neumann_surface(ct, faces, X, mesh.node_dof_row, [1, 1, 1], [0.0, 0.0, a.load], fext)
 path = {"auto": fcg.PATH_AUTO, "general": fcg.PATH_GENERAL, "structured": fcg.PATH_STRUCTURED}[a.path]
+box = mesh
+if a.renumber:
+    mesh = fcg.Discretization.renumbered(box, seed=1)
+    newrow = (3 * mesh.node_perm[:, None] + np.arange(3)).ravel()  # box rows are 3 * node + d
+    f2 = np.zeros_like(fext)
+    f2[newrow] = fext
+    fext = f2
+    dbc = np.sort(newrow[dbc]).astype(np.int32)
 print(f"mesh {time.perf_counter() - t0:.1f} s: {mesh.n_ele} elements, {mesh.nnz} nonzeros", file=sys.stderr, flush=True)
 ev = fcg.Evaluator(mesh, kinematics=kin, youngs=210.0, poisson=0.3, path=path)
 t_setup = time.perf_counter() - t0
@@ -111,6 +123,13 @@ if a.mg:
     print(f"multigrid setup {time.perf_counter() - t_mg:.1f} s: {json.dumps(mg.describe())}",
           file=sys.stderr, flush=True)
     t_setup = time.perf_counter() - t0
+if a.amg:
+    t_mg = time.perf_counter()
+    mg = importlib.import_module("4c_amd.amg").AMG(mesh, ev, dbc, nu=a.mg_nu, ratio=a.mg_ratio)
+    t_amg_setup = time.perf_counter() - t_mg
+    print(f"AMG setup (host graph) {t_amg_setup:.1f} s: {json.dumps(mg.describe())}",
+          file=sys.stderr, flush=True)
+    t_setup = time.perf_counter() - t0
 print(f"setup {t_setup:.1f} s", file=sys.stderr, flush=True)
 nt = Timed(ev, fext, dbc, lin_max_iter=a.lin_max_iter, tol_res=a.tol * max(np.linalg.norm(fext), 1e-300), tol_inc=a.tol,
            lin_rtol=a.lin_rtol, max_iter=40,
@@ -135,7 +154,9 @@ del xv, yv, Kx, Ky
 out = {"config": f"{a.celltype}-{a.kinem}-{a.n}^3-cantilever", "forcing": a.forcing,
        "converged": True, "tangent_symmetry_rel": sym,
        "residual_rel_incl_dbc_rows": r_final,
-       "linear_solver": (f"multigrid-FCG (Chebyshev {a.mg_nu})" if a.mg else "block-Jacobi PCG"),
+       "linear_solver": (f"multigrid-FCG (Chebyshev {a.mg_nu})" if a.mg else
+                         f"SA-AMG-FCG (Chebyshev {a.mg_nu})" if a.amg else "block-Jacobi PCG"),
+       "mesh": "renumbered (input-file order, no lattice)" if a.renumber else "GridGenerator box",
        "mg_levels": mg.describe() if mg else None, "elements": mesh.n_ele,
        "dofs": mesh.n_rows, "nnz": mesh.nnz, "setup_s": t_setup, "newton_s": t_newton,
        "newton_iterations": len(h) - 1,
@@ -143,6 +164,7 @@ out = {"config": f"{a.celltype}-{a.kinem}-{a.n}^3-cantilever", "forcing": a.forc
        "assembly_elem_per_s": mesh.n_ele / (1e-3 * float(np.median([r["assembly_ms"] for r in h]))),
        "solve_ms_total": float(sum(r.get("solve_ms", 0.0) for r in h)),
        "pcg_iterations": [r.get("pcg_iter") for r in h[:-1]],
-       "tip_uz": float(u[mesh.node_dof_row[np.argmax(X[:, 0] + X[:, 1] + X[:, 2])] + 2]),
+       "tip_uz": float(u[mesh.node_dof_row[np.argmax(mesh.node_x.sum(axis=1))] + 2]),
+       "amg_graph_setup_s": t_amg_setup if a.amg else None,
        "history": h}
 print(json.dumps(out))
