@@ -25,6 +25,7 @@ fcg_amg_* kernels (fcg_amg.hip).  torch supplies the buffers, the vector updates
 dense Cholesky of the coarsest level."""
 
 import ctypes
+import time
 
 import numpy as np
 import torch
@@ -266,6 +267,7 @@ class AMG(CycleFCG):
         dev = torch.device("cuda", ev.device)
         self.dev, self.ev, self.nu, self.ratio, self.boost = dev, ev, nu, ratio, boost
         self.omega, self.trace = omega, False
+        self.setup_ms = []  # numeric setup time of every tangent (synchronised wall clock)
         self.rows = np.sort(np.asarray(dbc_rows, dtype=np.int32))
         # level 0 as a block graph: block row b = rows 3b..3b+2 (one pattern of DOF triples)
         rp = np.asarray(mesh.rowptr, dtype=np.int64)
@@ -327,6 +329,13 @@ class AMG(CycleFCG):
 
     # -- numeric setup for a tangent ----------------------------------------------------------
     def _prepare(self, K):
+        torch.cuda.synchronize(self.dev)
+        t0 = time.perf_counter()
+        self._setup(K)
+        torch.cuda.synchronize(self.dev)
+        self.setup_ms.append(1e3 * (time.perf_counter() - t0))
+
+    def _setup(self, K):
         L, dev = fcg.lib(), self.dev.index or 0
         f0 = self.levels[0]
         f0.K = K

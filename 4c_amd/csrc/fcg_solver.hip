@@ -416,8 +416,7 @@ int fcg_spmv(fcg_ctx* ctx, const double* d_K_vals, const double* d_x_col, double
   if (!ctx || (ctx->mesh.n_rows > 0 && (!d_K_vals || !d_x_col || !d_y_row))) return FCG_ERR_ARG;
   (void)hipSetDevice(ctx->device);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-  hipError_t he = fcg::launch_spmv(ctx->mesh, d_K_vals, d_x_col, d_y_row, nullptr, nullptr, s);
-  if (he == hipSuccess) he = hipStreamSynchronize(s);
+  const hipError_t he = fcg::launch_spmv(ctx->mesh, d_K_vals, d_x_col, d_y_row, nullptr, nullptr, s);
   if (he != hipSuccess)
   {
     ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);

@@ -295,6 +295,9 @@ class CycleFCG:
         raise MultigridError(f"multigrid FCG failed after a lambda_max re-estimate: {why}")
 
     def _fcg(self, f0, b, x, rtol, max_iter):
+        """Flexible CG with the scalars kept on the device: one host read per iteration (|r|,
+        r.z and z.r_old together, after the V-cycle of the new residual -- the last iteration's
+        V-cycle is spent for nothing, every other read would stall the queue)."""
         if self.trace:
             print(f"  levels: {self.describe()}", file=sys.stderr, flush=True)
         bn = float(torch.linalg.vector_norm(b))
@@ -302,11 +305,11 @@ class CycleFCG:
         if bn == 0.0:
             return 0, 0.0
         r = b.clone()
-        z = torch.zeros_like(b)
-        q = torch.empty_like(b)
+        z, q, r_old = (torch.empty_like(b) for _ in range(3))
         self._vcycle(0, r, z)
         p = z.clone()
-        rz = float(torch.dot(r, z))
+        rz_t = torch.dot(r, z)
+        rz = float(rz_t)
         if not rz > 0.0:
             raise _Indefinite()
         rn = bn
@@ -314,26 +317,28 @@ class CycleFCG:
         while it < max_iter:
             it += 1
             f0.spmv_exact(p, q)
-            alpha = rz / float(torch.dot(p, q))
-            x.add_(p, alpha=alpha)
-            r_old = r.clone()  # z . r_old enters the Polak-Ribiere beta
-            r.add_(q, alpha=-alpha)
-            rn = float(torch.linalg.vector_norm(r))
+            alpha = rz_t / torch.dot(p, q)
+            x.addcmul_(p, alpha)
+            r_old.copy_(r)  # z . r_old enters the Polak-Ribiere beta
+            r.addcmul_(q, alpha, value=-1.0)
+            rr = torch.dot(r, r)
+            self._vcycle(0, r, z)
+            st = torch.stack((rr, torch.dot(r, z), torch.dot(z, r_old)))
+            s3 = st.cpu().numpy()
+            rn = float(np.sqrt(s3[0]))
             if not np.isfinite(rn):
                 raise FloatingPointError("multigrid FCG diverged (non-finite residual)")
             if rn <= rtol * bn:
                 break
-            z = torch.zeros_like(b)
-            self._vcycle(0, r, z)
-            rz_new = float(torch.dot(r, z))
+            rz_new = float(s3[1])
             if not rz_new > 0.0:
                 raise _Indefinite()
-            beta = (rz_new - float(torch.dot(z, r_old))) / rz
+            beta = (rz_new - float(s3[2])) / rz
             if self.trace:
-                print(f"  fcg {it}: |r|/|b| {rn / bn:.3e} rz {rz_new:.3e} beta {beta:.3e} "
-                      f"alpha {alpha:.3e}", file=sys.stderr, flush=True)
+                print(f"  fcg {it}: |r|/|b| {rn / bn:.3e} rz {rz_new:.3e} beta {beta:.3e}",
+                      file=sys.stderr, flush=True)
             p.mul_(beta).add_(z)
-            rz = rz_new
+            rz, rz_t = rz_new, st[1]
         return it, rn / bn
 
 

@@ -184,7 +184,8 @@ int fcg_get_diagnostics(const fcg_ctx* ctx, uint64_t* out, int n);
  * (owned DOF rows unless stated); `stream` as for fcg_evaluate_device; the calls return after
  * the stream has drained.
  * ---------------------------------------------------------------------------------------- */
-/* y_row = K x_col (Epetra_CrsMatrix::Multiply on the owned rows). */
+/* y_row = K x_col (Epetra_CrsMatrix::Multiply on the owned rows).  Asynchronous: queued on
+ * `stream` (NULL: the context's stream), which orders it with the caller's later work. */
 int fcg_spmv(fcg_ctx* ctx, const double* d_K_vals, const double* d_x_col, double* d_y_row,
     void* stream);
 /* Dirichlet rows (row LIDs d_rows[n_dbc], device array): freact[row] = -rhs[row] (if freact is not
@@ -197,7 +198,7 @@ int fcg_dirichlet_apply(fcg_ctx* ctx, int64_t n_dbc, const int32_t* d_rows, doub
  * single-rank systems only (matrix column map = row map), else FCG_ERR_ARG.  Deterministic. */
 /* y_row = K x_col with the matrix values stored in FP32 (vectors and sums FP64): the multigrid
  * smoother's reduced-precision copy of K (4c_amd/multigrid.py, mixed=True), half the bytes of
- * fcg_spmv.  Asynchronous on `stream` (no drain). */
+ * fcg_spmv.  Asynchronous on `stream` like fcg_spmv. */
 int fcg_spmv_f32(fcg_ctx* ctx, const float* d_K32, const double* d_x_col, double* d_y_row,
     void* stream);
 int fcg_pcg_solve(fcg_ctx* ctx, const double* d_K_vals, const double* d_b_row, double* d_x_row,

@@ -159,7 +159,9 @@ def test_newton_multigrid_matches_pcg(ct, n, kin, load, length, jitter, tol):
     (u0, it0, n0, _), (u1, it1, n1, lv) = res["pcg"], res["mg"]
     assert len(lv) >= 2
     assert np.linalg.norm(u1 - u0) <= 100 * tol * np.linalg.norm(u0)
-    assert it1 * 3 < it0, (it0, it1)
+    # per linear solve: on the aspect-ratio-10 case the Newton's last steps solve round-off
+    # residuals, and how many of them it takes to meet tol_inc is not the preconditioner's doing
+    assert it1 / (n1 - 1) * 3 < it0 / (n0 - 1), (it0, n0, it1, n1)
 
 
 @pytest.mark.gpu
