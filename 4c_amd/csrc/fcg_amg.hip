@@ -5,9 +5,9 @@
 // pointers.  Per tangent the hierarchy is recomputed on the device from the fixed patterns:
 //   A_0 (BSR copy of the context's K)  -> P_0 = (I - omega D^-1 A_0) T_0   (T = tentative)
 //   A_1 = P_0^T (A_0 P_0), and so on;   the coarsest A_L becomes dense (fcg_bsr_to_dense).
-// Kernels: block SpMV (8 lanes per block row), block SpGEMM with a known output pattern (one
-// wavefront per output row, one lane per output block, the right operand's row binary-searched
-// per left block: fixed summation order, bitwise reproducible), block transpose, block-diagonal
+// Kernels: block SpMV (8 lanes per block row), block SpGEMM with a known output pattern (16 lanes
+// per output row, one lane per output block, the right operand's rows binary-searched: fixed
+// summation order, bitwise reproducible), block transpose, block-diagonal
 // inverse (Gauss-Jordan in registers; empty coarse rows -- the zero columns of rank-deficient
 // aggregates -- get a unit diagonal), and the prolongator smoothing.
 #include <hip/hip_runtime.h>
@@ -60,7 +60,10 @@ __global__ __launch_bounds__(kBlock) void bsr_spmv_kernel(int64_t n, const int64
       y[row * BR + r] = alpha * acc[r] + (accumulate ? y[row * BR + r] : 0.0);
 }
 
-// C = A B on C's given pattern: one wavefront per block row of C, one lane per block of the row
+// C = A B on C's given pattern: 16 lanes per block row of C (four rows per wavefront), one lane
+// per output block (strided), walking A's row in order and binary-searching B's row for the
+// block's column: a fixed summation order, bitwise reproducible.  (An LDS row image built
+// sequentially over A's blocks measured slower: it serialises the dependent loads of every block.)
 template <int BR, int BK, int BC>
 __global__ __launch_bounds__(kBlock) void bsr_spgemm_kernel(int64_t n,
     const int64_t* __restrict__ a_ptr, const int32_t* __restrict__ a_col,
@@ -68,12 +71,13 @@ __global__ __launch_bounds__(kBlock) void bsr_spgemm_kernel(int64_t n,
     const int32_t* __restrict__ b_col, const double* __restrict__ b_vals,
     const int64_t* __restrict__ c_ptr, const int32_t* __restrict__ c_col, double* c_vals)
 {
-  const int64_t row = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
+  constexpr int LPR = 16;
+  const int64_t row = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / LPR;
+  const int lane = threadIdx.x % LPR;
   if (row >= n) return;
   const int64_t a0 = a_ptr[row], a1 = a_ptr[row + 1];
   const int64_t c1 = c_ptr[row + 1];
-  for (int64_t ci = c_ptr[row] + lane; ci < c1; ci += 64)
+  for (int64_t ci = c_ptr[row] + lane; ci < c1; ci += LPR)
   {
     const int32_t tc = c_col[ci];
     double acc[BR * BC];
@@ -94,9 +98,6 @@ __global__ __launch_bounds__(kBlock) void bsr_spgemm_kernel(int64_t n,
       {
         const double* A = a_vals + ak * (BR * BK);
         const double* B = b_vals + lo * (BK * BC);
-        double bv[BK * BC];
-#pragma unroll
-        for (int q = 0; q < BK * BC; ++q) bv[q] = B[q];
 #pragma unroll
         for (int r = 0; r < BR; ++r)
 #pragma unroll
@@ -104,7 +105,7 @@ __global__ __launch_bounds__(kBlock) void bsr_spgemm_kernel(int64_t n,
           {
             const double av = A[r * BK + q];
 #pragma unroll
-            for (int c = 0; c < BC; ++c) acc[r * BC + c] += av * bv[q * BC + c];
+            for (int c = 0; c < BC; ++c) acc[r * BC + c] += av * B[q * BC + c];
           }
       }
     }
@@ -336,7 +337,7 @@ int fcg_bsr_spgemm(int device, int br, int bk, int bc, int64_t n_brows, const in
   if (n_brows == 0) return FCG_OK;
   if (hipSetDevice(device) != hipSuccess) return FCG_ERR_DEVICE;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const dim3 g(blocks_for(n_brows * 64, kBlock)), b(kBlock);
+  const dim3 g(blocks_for(n_brows * 16, kBlock)), b(kBlock);
 #define FCG_SPGEMM(R, K, C)                                                                        \
   hipLaunchKernelGGL((bsr_spgemm_kernel<R, K, C>), g, b, 0, s, n_brows, d_a_ptr, d_a_col, d_a_vals, \
       d_b_ptr, d_b_col, d_b_vals, d_c_ptr, d_c_col, d_c_vals)

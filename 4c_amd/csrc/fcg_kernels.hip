@@ -18,6 +18,8 @@
 // (4C_mat_stvenantkirchhoff.cpp:115-145); see DESIGN.md for the derivation.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <cstdio>
 
 #include "fcg_hex8_element.hpp"
@@ -322,6 +324,7 @@ struct ElementArgs {
   const int64_t* rowptr;
   double* K;
   double* fint;
+  int mfma;  // hex27 StVK: node-pair blocks on v_mfma_f64_16x16x4_f64 (else the VALU pair loop)
 };
 
 // Colour-ordered direct assembly: is element e (first-touch bits ft, see build_colored_plan in
@@ -339,6 +342,111 @@ __device__ inline bool first_touch27(const uint8_t* loc, uint32_t ft, int a, int
     if (x == y && x != 1u) first = first && ((ft >> (2 * d + (x == 2u ? 1 : 0))) & 1u);
   }
   return first;
+}
+
+// hex27 StVK node-pair blocks on the FP64 matrix cores (v_mfma_f64_16x16x4_f64).  With the rows
+// (a, i) of the element's 81 DOFs ordered i-major and each node range padded to 32,
+//   X_ij[a][b] = sum_g fac_g Q_g[a][i] Q_g[b][j]       (Q = N_XYZ linear, F N_XYZ TotLag)
+// is 9 tiles of 16 x 16 per (a-range, b-range) pair over K = 27 Gauss points (7 steps of 4), and
+// because the f64 MFMA's output layout depends only on the position in the tile, one lane holds
+// X_ij and X_ji of the same (a, b) for all i, j: K_ab[i][j] = lambda X_ij + mu X_ji + ... is formed
+// in registers.  TotLag adds mu H_ij + delta_ij geo = sum over (g, k) of N_a,k times
+// fac (mu (F F^T)_ij N_b,k + delta_ij (S N_b)_k) -- 6 more tiles over K = 81 (21 steps).  Waves
+// 0..2 take the (a, b) ranges (0,0), (0,1), (1,1) (a <= b is all the image needs); the blocks go to
+// the LDS image KS (which TotLag aliases with N_XYZ / P: written after a barrier).
+typedef double f64x4_t __attribute__((ext_vector_type(4)));
+template <int KIN, typename SH>
+__device__ inline void pair_phase_mfma27(SH& sh, double* KS, double lam, double mu, int tid)
+{
+  const int wave = tid >> 6, lane = tid & 63;
+  const int at = wave == 2 ? 1 : 0, bt = wave == 0 ? 0 : 1;
+  const int r16 = lane & 15, kq = lane >> 4;
+  const int a_l = 16 * at + r16, b_l = 16 * bt + r16;
+  const bool va = a_l < 27, vb = b_l < 27;
+  const int a_c = va ? a_l : 0, b_c = vb ? b_l : 0;  // clamped: no read past the node range
+  f64x4_t X[9], H[6];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) X[q] = f64x4_t{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int q = 0; q < 6; ++q) H[q] = f64x4_t{0.0, 0.0, 0.0, 0.0};
+  if (wave < 3)
+  {
+    const double* Q = KIN ? sh.P : sh.NX;  // [g][node][d]
+#pragma unroll
+    for (int st = 0; st < 7; ++st)
+    {
+      const int g = 4 * st + kq;
+      const bool vg = g < 27;
+      const int gc = vg ? g : 0;
+      const double fg = vg ? sh.fac[gc] : 0.0;
+      double av[3], bv[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+      {
+        av[i] = va ? fg * Q[3 * (27 * gc + a_c) + i] : 0.0;
+        bv[i] = (vg && vb) ? Q[3 * (27 * gc + b_c) + i] : 0.0;
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          X[3 * i + j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[j], X[3 * i + j], 0, 0, 0);
+    }
+    if constexpr (KIN == 1)
+    {
+      for (int st = 0; st < 21; ++st)
+      {
+        const int kk = 4 * st + kq;
+        const bool vk = kk < 81;
+        const int g = vk ? kk / 3 : 0, k = vk ? kk - 3 * (kk / 3) : 0;
+        const double fg = vk ? sh.fac[g] : 0.0;
+        const double an = va ? sh.NX[3 * (27 * g + a_c) + k] : 0.0;
+        const double* nb = sh.NX + 3 * (27 * g + b_c);
+        const double n0 = vb ? nb[0] : 0.0, n1 = vb ? nb[1] : 0.0, n2 = vb ? nb[2] : 0.0;
+        const double* S = sh.S + 6 * g;
+        const double* M = sh.M + 6 * g;
+        const double nk = k == 0 ? n0 : (k == 1 ? n1 : n2);
+        const double snk = k == 0 ? S[0] * n0 + S[3] * n1 + S[5] * n2
+                                  : (k == 1 ? S[3] * n0 + S[1] * n1 + S[4] * n2
+                                            : S[5] * n0 + S[4] * n1 + S[2] * n2);
+        const double fs = fg * snk, fm = fg * mu * nk;
+        H[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(an, fs + fm * M[0], H[0], 0, 0, 0);
+        H[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(an, fs + fm * M[1], H[1], 0, 0, 0);
+        H[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(an, fs + fm * M[2], H[2], 0, 0, 0);
+        H[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(an, fm * M[3], H[3], 0, 0, 0);
+        H[4] = __builtin_amdgcn_mfma_f64_16x16x4f64(an, fm * M[4], H[4], 0, 0, 0);
+        H[5] = __builtin_amdgcn_mfma_f64_16x16x4f64(an, fm * M[5], H[5], 0, 0, 0);
+      }
+    }
+  }
+  __syncthreads();  // TotLag: KS aliases N_XYZ / P
+  if (wave < 3)
+  {
+    const int b = 16 * bt + r16;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+    {
+      const int a = 16 * at + kq + 4 * r;
+      if (a < 27 && b < 27 && a <= b)
+      {
+        const int pidx = 27 * a - (a * (a - 1)) / 2 + b - a;
+        double* K = KS + 9 * pidx;
+        const double tr = mu * (X[0][r] + X[4][r] + X[8][r]);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j)
+          {
+            double v = lam * X[3 * i + j][r] + mu * X[3 * j + i][r];
+            if constexpr (KIN == 0)
+              v += i == j ? tr : 0.0;
+            else
+              v += i == j ? H[i][r] : H[(i + j == 1) ? 3 : ((i + j == 3) ? 4 : 5)][r];
+            K[i + 3 * j] = v;
+          }
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------- element
@@ -846,7 +954,7 @@ __global__ __launch_bounds__(BLOCK, (NPE == 27 && MAT == 0) ? 3 : 1) void elemen
         b = p - NPE * (p / NPE);
       }
     };
-    if constexpr (NPE == 27 && (KIN == 0 || ASM != 0))
+    if constexpr (NPE == 27 && (KIN == 0 || ASM != 0 || MAT == 0))
     {
       if (A.want_k)
       {
@@ -856,7 +964,13 @@ __global__ __launch_bounds__(BLOCK, (NPE == 27 && MAT == 0) ? 3 : 1) void elemen
       // runs of contiguous CSR columns (element nodes in lattice order) -- written by the first
       // element of the colour order that holds both nodes, added to by the others
       double* KS = sh.ks();
-      if constexpr (KIN == 0)
+      // matrix cores for the linear blocks and the colour-ordered TotLag path; the TotLag
+      // scratch path keeps the VALU loop (its 15 accumulator tiles would spill at three
+      // workgroups per CU, and at two the MFMA phase measured slower: DESIGN §7e)
+      constexpr bool kMfma = MAT == 0 && !(KIN == 1 && ASM == 0);
+      if (kMfma && A.mfma)
+        pair_phase_mfma27<KIN>(sh, KS, A.lambda, A.mu, tid);
+      else if constexpr (KIN == 0)
       {
         for (int p = tid; p < NPAIR; p += BLOCK)
         {
@@ -865,7 +979,7 @@ __global__ __launch_bounds__(BLOCK, (NPE == 27 && MAT == 0) ? 3 : 1) void elemen
           if (sh.inc[a] >= 0 || sh.inc[b] >= 0) pair_block(a, b, KS + 9 * p);
         }
       }
-      else
+      else if constexpr (ASM != 0)
       {
         double Kq[2][9];
 #pragma unroll
@@ -889,8 +1003,43 @@ __global__ __launch_bounds__(BLOCK, (NPE == 27 && MAT == 0) ? 3 : 1) void elemen
             for (int k = 0; k < 9; ++k) KS[9 * p + k] = Kq[q][k];
         }
       }
+      else
+      {
+        // TotLag general path without MFMA: each pair thread writes its block rows straight into
+        // the scratch records
+        for (int p = tid; p < NPAIR; p += BLOCK)
+        {
+          int a, b;
+          pair_of(p, a, b);
+          const int32_t ia = inc[a];
+          const int32_t ib = inc[b];
+          if (ia < 0 && ib < 0) continue;
+          double K[9];
+          pair_block(a, b, K);
+          if (ia >= 0)
+          {
+            double* rec = A.scratch + int64_t(ia) * REC + 3 * b;
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+              for (int j = 0; j < 3; ++j) rec[i * ROWLEN + j] = K[i + 3 * j];
+          }
+          if (a != b && ib >= 0)
+          {
+            double* rec = A.scratch + int64_t(ib) * REC + 3 * a;
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+              for (int j = 0; j < 3; ++j) rec[i * ROWLEN + j] = K[j + 3 * i];
+          }
+        }
+      }
+      const bool image = !(KIN == 1 && ASM == 0);
       __syncthreads();
-      if constexpr (ASM == 0)
+      if (!image)
+      {
+      }
+      else if constexpr (ASM == 0)
       {
         for (int v = tid; v < NPE * 243; v += BLOCK)
         {
@@ -1284,10 +1433,21 @@ static int grid_for(int64_t work, int cap)
   return int(work < cap ? (work > 0 ? work : 1) : cap);
 }
 
+// hex27 StVK pair phase on the matrix cores unless FCG_H27_MFMA=0 (A/B measurements)
+static int h27_mfma()
+{
+  static const int on = [] {
+    const char* e = std::getenv("FCG_H27_MFMA");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return on;
+}
+
 hipError_t launch_element(const DeviceMesh& m, const double* d_u_col, bool want_k, hipStream_t stream)
 {
   if (m.n_ele == 0) return hipSuccess;
   ElementArgs a{};
+  a.mfma = h27_mfma();
   a.n_ele = m.n_ele;
   a.ele_nodes = m.ele_nodes;
   a.node_x = m.node_x;
@@ -1338,6 +1498,7 @@ hipError_t launch_element_colored(const DeviceMesh& m, const double* d_u_col, bo
 {
   if (m.n_ele == 0 || m.npe != 27) return m.n_ele == 0 ? hipSuccess : hipErrorInvalidValue;
   ElementArgs a{};
+  a.mfma = h27_mfma();
   a.n_ele = m.n_ele;
   a.ele_nodes = m.ele_nodes;
   a.node_x = m.node_x;

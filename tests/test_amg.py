@@ -156,6 +156,22 @@ def test_bsr_kernels_match_numpy(br, bk, bc):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("br,bk,bc", [(3, 3, 6), (6, 6, 6)])
+def test_bsr_spgemm_long_rows(br, bk, bc):
+    """Output rows far longer than the lanes of a row (each lane loops over many blocks)."""
+    torch, dev = _dev()
+    rng = np.random.default_rng(7)
+    A = _rand_bsr(rng, 6, 5, br, bk, 0.6, dev)
+    B = _rand_bsr(rng, 5, 300, bk, bc, 0.9, dev)
+    p, c = amg.symbolic(A.ptr_h, A.col_h, B.ptr_h, B.col_h, 300)
+    assert np.diff(p).max() > 260
+    C = amg.Bsr(p, c, br, bc, 300, dev)
+    C.product(A, B)
+    ref = A.to_numpy() @ B.to_numpy()
+    assert np.abs(C.to_numpy() - ref).max() <= 1e-13 * np.abs(ref).max()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("b", [3, 6])
 def test_bsr_block_inverse_and_dense(b):
     torch, dev = _dev()
