@@ -376,3 +376,73 @@ class AMG(CycleFCG):
 
     def _coarse_solve(self, lvl, b, x):
         torch.mv(lvl.Ainv, b, out=x)
+
+
+class NativeAMG:
+    """The same smoothed-aggregation AMG solve as one native object behind the C ABI
+    (fcg_amg_create / fcg_amg_solve, fcg_amg_solver.hip) -- what a C++ host calls; the coarsest
+    level is solved by block-Jacobi CG to coarse_rtol instead of a dense factor.  Same interface
+    as AMG: solve(K, b, x, rtol, max_iter) -> (iterations, relative residual)."""
+
+    def __init__(self, mesh, ev, dbc_rows, **opts):
+        L = fcg.lib()
+        info = ev.info
+        n_rows = int(info.n_rows)
+        if int(info.n_cols) != n_rows or n_rows % 3:
+            raise ValueError("NativeAMG is single-rank: the column map must be the row map")
+        ndr = np.asarray(mesh.node_dof_row, dtype=np.int64)
+        order = np.argsort(ndr, kind="stable")
+        if not np.array_equal(ndr[order], 3 * np.arange(n_rows // 3)):
+            raise ValueError("NativeAMG needs node-major DOFs: row 3b + d = DOF d of the b-th node")
+        self.ev, self.dev = ev, torch.device("cuda", ev.device)
+        self.rows = np.sort(np.asarray(dbc_rows, dtype=np.int32))
+        self._rowptr = np.ascontiguousarray(mesh.rowptr, dtype=np.int64)
+        self._col = np.ascontiguousarray(mesh.col_lid, dtype=np.int32)
+        self._x = np.ascontiguousarray(np.asarray(mesh.node_x, dtype=np.float64)[order])
+        self.opt = fcg.FcgAmgOptions()
+        L.fcg_amg_default_options(ctypes.byref(self.opt))
+        for k, v in opts.items():
+            setattr(self.opt, k, v)
+        h = ctypes.c_void_p()
+        rc = L.fcg_amg_create(ev._h, _vp(self._rowptr), _vp(self._col), _vp(self._x), len(self.rows),
+                              _vp(self.rows), ctypes.byref(self.opt), ctypes.byref(h))
+        if rc != 0:
+            raise fcg.FcgError(rc, L.fcg_last_error(ev._h).decode())
+        self._h = h
+        self.setup_ms = []
+
+    def close(self):
+        if getattr(self, "_h", None):
+            fcg.lib().fcg_amg_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def check_dirichlet(self, dbc_rows):
+        theirs = np.sort(np.asarray(dbc_rows, dtype=np.int32))
+        if not np.array_equal(self.rows, theirs):
+            raise ValueError("NativeAMG Dirichlet rows differ from the system's")
+
+    def describe(self):
+        L = fcg.lib()
+        out = []
+        for l in range(L.fcg_amg_levels(self._h)):
+            d, b, lm = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_double()
+            L.fcg_amg_level_info(self._h, l, ctypes.byref(d), ctypes.byref(b), ctypes.byref(lm))
+            out.append({"level": l, "dofs": d.value, "blocks": b.value, "lmax": lm.value})
+        return out
+
+    def solve(self, K, b, x, rtol, max_iter=1000):
+        L = fcg.lib()
+        it, rel = ctypes.c_int(0), ctypes.c_double(0.0)
+        s = ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+        rc = L.fcg_amg_solve(self._h, _vp(K), _vp(b), _vp(x), float(rtol), int(max_iter),
+                             ctypes.byref(it), ctypes.byref(rel), s)
+        self.setup_ms.append(L.fcg_amg_setup_ms(self._h))
+        if rc != 0:
+            raise fcg.FcgError(rc, L.fcg_amg_last_error(self._h).decode())
+        return it.value, rel.value

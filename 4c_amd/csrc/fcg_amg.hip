@@ -16,7 +16,7 @@
 
 #include "fourc_gpu.h"
 
-namespace fcg_amg {
+namespace fcg_bsrk {
 
 constexpr int kBlock = 256;
 
@@ -298,7 +298,7 @@ __global__ __launch_bounds__(kBlock) void bsr_to_dense_kernel(int64_t n,
 
 inline int status(hipError_t e) { return e == hipSuccess ? FCG_OK : FCG_ERR_DEVICE; }
 
-}  // namespace fcg_amg
+}  // namespace fcg_bsrk
 
 extern "C" {
 
@@ -306,7 +306,7 @@ int fcg_bsr_spmv(int device, int br, int bc, int64_t n_brows, const int64_t* d_p
     const int32_t* d_col, const double* d_vals, const double* d_x, double* d_y, double alpha,
     int accumulate, void* stream)
 {
-  using namespace fcg_amg;
+  using namespace fcg_bsrk;
   if (n_brows < 0 || (n_brows > 0 && (!d_ptr || !d_col || !d_vals || !d_x || !d_y))) return FCG_ERR_ARG;
   if (n_brows == 0) return FCG_OK;
   if (hipSetDevice(device) != hipSuccess) return FCG_ERR_DEVICE;
@@ -330,7 +330,7 @@ int fcg_bsr_spgemm(int device, int br, int bk, int bc, int64_t n_brows, const in
     const double* d_b_vals, const int64_t* d_c_ptr, const int32_t* d_c_col, double* d_c_vals,
     void* stream)
 {
-  using namespace fcg_amg;
+  using namespace fcg_bsrk;
   if (n_brows < 0 || (n_brows > 0 && (!d_a_ptr || !d_a_col || !d_a_vals || !d_b_ptr || !d_b_col ||
                                       !d_b_vals || !d_c_ptr || !d_c_col || !d_c_vals)))
     return FCG_ERR_ARG;
@@ -353,7 +353,7 @@ int fcg_bsr_spgemm(int device, int br, int bk, int bc, int64_t n_brows, const in
 int fcg_bsr_transpose_values(int device, int br, int bc, int64_t nnzb, const int64_t* d_perm,
     const double* d_vals, double* d_t_vals, void* stream)
 {
-  using namespace fcg_amg;
+  using namespace fcg_bsrk;
   if (nnzb < 0 || (nnzb > 0 && (!d_perm || !d_vals || !d_t_vals))) return FCG_ERR_ARG;
   if (nnzb == 0) return FCG_OK;
   if (hipSetDevice(device) != hipSuccess) return FCG_ERR_DEVICE;
@@ -371,7 +371,7 @@ int fcg_bsr_transpose_values(int device, int br, int bc, int64_t nnzb, const int
 int fcg_bsr_from_node_csr(int device, int64_t n_brows, const int64_t* d_rowptr,
     const int64_t* d_b_ptr, const double* d_K, double* d_b_vals, void* stream)
 {
-  using namespace fcg_amg;
+  using namespace fcg_bsrk;
   if (n_brows < 0 || (n_brows > 0 && (!d_rowptr || !d_b_ptr || !d_K || !d_b_vals))) return FCG_ERR_ARG;
   if (n_brows == 0) return FCG_OK;
   if (hipSetDevice(device) != hipSuccess) return FCG_ERR_DEVICE;
@@ -384,7 +384,7 @@ int fcg_bsr_from_node_csr(int device, int64_t n_brows, const int64_t* d_rowptr,
 int fcg_bsr_block_jacobi_setup(int device, int b, int64_t n_brows, const int64_t* d_ptr,
     const int64_t* d_diag_idx, double* d_vals, double* d_dinv, int32_t* d_flag, void* stream)
 {
-  using namespace fcg_amg;
+  using namespace fcg_bsrk;
   if (n_brows < 0 || !d_flag || (n_brows > 0 && (!d_ptr || !d_diag_idx || !d_vals || !d_dinv)))
     return FCG_ERR_ARG;
   if (n_brows == 0) return FCG_OK;
@@ -410,7 +410,7 @@ int fcg_bsr_block_jacobi_setup(int device, int b, int64_t n_brows, const int64_t
 int fcg_bsr_block_jacobi_apply(int device, int b, int64_t n_brows, const double* d_dinv,
     const double* d_r, double* d_z, double scale, int accumulate, void* stream)
 {
-  using namespace fcg_amg;
+  using namespace fcg_bsrk;
   if (n_brows < 0 || (n_brows > 0 && (!d_dinv || !d_r || !d_z))) return FCG_ERR_ARG;
   if (n_brows == 0) return FCG_OK;
   if (hipSetDevice(device) != hipSuccess) return FCG_ERR_DEVICE;
@@ -429,7 +429,7 @@ int fcg_amg_smooth_prolongator(int device, int br, int64_t n_brows, const int64_
     const int32_t* d_p_col, const int32_t* d_agg, const double* d_tent, const double* d_dinv,
     const double* d_at, double omega, double* d_p_vals, void* stream)
 {
-  using namespace fcg_amg;
+  using namespace fcg_bsrk;
   if (n_brows < 0 || (n_brows > 0 && (!d_p_ptr || !d_p_col || !d_agg || !d_tent || !d_dinv ||
                                       !d_at || !d_p_vals)))
     return FCG_ERR_ARG;
@@ -449,7 +449,7 @@ int fcg_amg_smooth_prolongator(int device, int br, int64_t n_brows, const int64_
 int fcg_bsr_to_dense(int device, int b, int64_t n_brows, const int64_t* d_ptr, const int32_t* d_col,
     const double* d_vals, double* d_dense, void* stream)
 {
-  using namespace fcg_amg;
+  using namespace fcg_bsrk;
   if (n_brows < 0 || (n_brows > 0 && (!d_ptr || !d_col || !d_vals || !d_dense))) return FCG_ERR_ARG;
   if (n_brows == 0) return FCG_OK;
   if (hipSetDevice(device) != hipSuccess) return FCG_ERR_DEVICE;

@@ -1,0 +1,795 @@
+// fcg_amg_solver.hip -- the smoothed-aggregation AMG solve as a native C++ object behind the C ABI
+// (fcg_amg_create / fcg_amg_solve / fcg_amg_level_info / fcg_amg_destroy): what a C++ host such as
+// 4C calls in place of its Belos CG + MueLu preconditioner (4C_solver_nonlin_nox_linearsystem.cpp:
+// 275-353, 4C_linear_solver_preconditioner_muelu.cpp) on the tangent a context assembled.  The
+// hierarchy and cycle are those of 4c_amd/amg.py (which stays the Python-side mirror and test
+// reference): graph setup on the host once (fcg_amg_setup.cpp), numeric setup per tangent and the
+// flexible-CG / V-cycle / Chebyshev iteration on the device (fcg_amg.hip kernels, the context's
+// fcg_spmv / block-Jacobi on level 0).  Differences from amg.py: the coarsest level is solved by
+// block-Jacobi CG to a loose tolerance on the device (no dense factor: no solver library is linked)
+// and the scalars of every iteration stay on the device except one read per FCG iteration (and one
+// per 8 coarse CG iterations).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "fcg_internal.hpp"
+#include "fourc_gpu.h"
+
+namespace fcg_amgs {
+
+constexpr int kBlock = 256;
+constexpr int kMaxPartials = 1024;
+inline unsigned blocks_for(int64_t n) { return unsigned((n + kBlock - 1) / kBlock); }
+inline unsigned capped(int64_t n) { return unsigned(std::max<int64_t>(1, std::min<int64_t>(kMaxPartials, (n + kBlock - 1) / kBlock))); }
+
+__device__ inline double block_sum(double v, double* sbuf)
+{
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) sbuf[w] = v;
+  __syncthreads();
+  double t = 0.0;
+  if (threadIdx.x == 0)
+    for (int i = 0; i < int(blockDim.x >> 6); ++i) t += sbuf[i];
+  __syncthreads();
+  return t;
+}
+
+// partial[block] = sum over the block's grid-stride share of a . b (fixed assignment)
+__global__ __launch_bounds__(kBlock) void dot_kernel(const double* __restrict__ a,
+    const double* __restrict__ b, int64_t n, double* partial)
+{
+  __shared__ double sbuf[kBlock / 64];
+  double t = 0.0;
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock)
+    t += a[i] * b[i];
+  const double s = block_sum(t, sbuf);
+  if (threadIdx.x == 0) partial[blockIdx.x] = s;
+}
+
+// out = sum of n partials (one block, fixed order)
+__global__ __launch_bounds__(kBlock) void reduce_kernel(const double* __restrict__ partial, int n,
+    double* out)
+{
+  __shared__ double sbuf[kBlock / 64];
+  double t = 0.0;
+  for (int i = threadIdx.x; i < n; i += kBlock) t += partial[i];
+  const double s = block_sum(t, sbuf);
+  if (threadIdx.x == 0) *out = s;
+}
+
+// y = b - y
+__global__ __launch_bounds__(kBlock) void rsub_kernel(const double* __restrict__ b, double* y, int64_t n)
+{
+  const int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (i < n) y[i] = b[i] - y[i];
+}
+
+// y = a x + b y
+__global__ __launch_bounds__(kBlock) void axpby_kernel(double a, const double* __restrict__ x,
+    double b, double* y, int64_t n)
+{
+  const int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (i < n) y[i] = a * x[i] + b * y[i];
+}
+
+// FCG step: alpha = rz / (p.q); x += alpha p; r_old = r; r -= alpha q
+__global__ __launch_bounds__(kBlock) void fcg_step_kernel(double rz, const double* __restrict__ pq,
+    const double* __restrict__ p, const double* __restrict__ q, double* x, double* r, double* r_old,
+    int64_t n)
+{
+  const int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const double alpha = rz / *pq;
+  x[i] += alpha * p[i];
+  r_old[i] = r[i];
+  r[i] -= alpha * q[i];
+}
+
+// coarse CG, scalars on the device: sc[0] = r.z, sc[1] = p.q, sc[2] = r.z new, sc[3] = r.r
+__global__ __launch_bounds__(kBlock) void cg_step_kernel(const double* __restrict__ sc,
+    const double* __restrict__ p, const double* __restrict__ q, double* x, double* r, int64_t n)
+{
+  const int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const double alpha = sc[1] > 0.0 ? sc[0] / sc[1] : 0.0;
+  x[i] += alpha * p[i];
+  r[i] -= alpha * q[i];
+}
+__global__ __launch_bounds__(kBlock) void cg_dir_kernel(const double* __restrict__ sc,
+    const double* __restrict__ z, double* p, int64_t n)
+{
+  const int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const double beta = sc[0] != 0.0 ? sc[2] / sc[0] : 0.0;
+  p[i] = z[i] + beta * p[i];
+}
+__global__ void shift_kernel(double* sc) { sc[0] = sc[2]; }
+
+// deterministic pseudo-random vector in [-0.5, 0.5) times mask (Lanczos start)
+__global__ __launch_bounds__(kBlock) void random_kernel(double* v, const double* __restrict__ mask,
+    int64_t n, uint32_t seed)
+{
+  const int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= n) return;
+  uint64_t h = uint64_t(i) * 0x9E3779B97F4A7C15ull + seed;
+  h ^= h >> 33;
+  h *= 0xFF51AFD7ED558CCDull;
+  h ^= h >> 33;
+  h *= 0xC4CEB9FE1A85EC53ull;
+  h ^= h >> 33;
+  const double u = double(h >> 11) * (1.0 / 9007199254740992.0) - 0.5;
+  v[i] = mask ? u * mask[i] : u;
+}
+
+struct Bsr {
+  int64_t n = 0, nnzb = 0, n_cols = 0;
+  int br = 0, bc = 0;
+  std::vector<int64_t> ptr_h;
+  std::vector<int32_t> col_h;
+  int64_t* ptr = nullptr;
+  int32_t* col = nullptr;
+  double* vals = nullptr;
+};
+
+struct Step {  // level l -> l + 1
+  int bs = 3;
+  int64_t n_agg = 0;
+  Bsr T, P, AT, AP, Pt;
+  int32_t* agg = nullptr;
+  double* tent = nullptr;   // [n][bs][6], every row's T_i
+  int64_t* perm = nullptr;  // P^T block -> P block
+};
+
+struct Level {  // coarse level (6 x 6 blocks)
+  Bsr A;
+  int64_t* diag = nullptr;
+  double* dinv = nullptr;
+  double lmax = 0.0;
+  double *x = nullptr, *b = nullptr, *r = nullptr, *d = nullptr, *z = nullptr, *p = nullptr, *q = nullptr;
+};
+
+}  // namespace fcg_amgs
+
+struct fcg_amg {
+  fcg_ctx* ctx = nullptr;
+  int device = 0;
+  fcg_amg_options opt{};
+  int64_t n0 = 0, nb0 = 0;
+  fcg_amgs::Bsr A0;
+  int64_t* A0_diag = nullptr;
+  double* A0_dinv = nullptr;    // BSR block inverses of level 0 (prolongator smoothing)
+  double* ctx_dinv = nullptr;   // the context's block-Jacobi of level 0 (smoother)
+  double* mask0 = nullptr;      // 0 on the Dirichlet rows
+  double lmax0 = 0.0;
+  double *r0 = nullptr, *d0 = nullptr, *z0 = nullptr, *q0 = nullptr, *p0 = nullptr, *ro0 = nullptr,
+         *fr = nullptr, *fz = nullptr, *fx = nullptr;
+  std::vector<fcg_amgs::Step> steps;
+  std::vector<fcg_amgs::Level> levels;  // levels[l] = hierarchy level l + 1
+  double* partial = nullptr;  // dot partials
+  double* sc = nullptr;       // device scalars
+  int32_t* flag = nullptr;
+  std::string last_error;
+  std::vector<void*> allocs;
+  double setup_ms = 0.0;
+};
+
+namespace fcg_amgs {
+
+struct Fail {
+  int code;
+  std::string msg;
+};
+
+inline void ck(hipError_t e, const char* what)
+{
+  if (e != hipSuccess) throw Fail{FCG_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e)};
+}
+inline void ck(int rc, const char* what)
+{
+  if (rc != FCG_OK) throw Fail{rc, what};
+}
+
+template <typename T>
+T* dalloc(fcg_amg* h, int64_t n)
+{
+  void* p = nullptr;
+  ck(hipMalloc(&p, sizeof(T) * size_t(std::max<int64_t>(n, 1))), "hipMalloc");
+  h->allocs.push_back(p);
+  return static_cast<T*>(p);
+}
+template <typename T>
+T* upload(fcg_amg* h, const std::vector<T>& v)
+{
+  T* d = dalloc<T>(h, int64_t(v.size()));
+  if (!v.empty()) ck(hipMemcpy(d, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice), "hipMemcpy");
+  return d;
+}
+
+void make_bsr(fcg_amg* h, Bsr& M, std::vector<int64_t> ptr, std::vector<int32_t> col, int br, int bc,
+    int64_t n_cols)
+{
+  M.n = int64_t(ptr.size()) - 1;
+  M.nnzb = ptr.back();
+  M.br = br;
+  M.bc = bc;
+  M.n_cols = n_cols;
+  M.ptr_h = std::move(ptr);
+  M.col_h = std::move(col);
+  M.ptr = upload(h, M.ptr_h);
+  M.col = upload(h, M.col_h);
+  M.vals = dalloc<double>(h, M.nnzb * br * bc);
+  ck(hipMemset(M.vals, 0, sizeof(double) * size_t(std::max<int64_t>(M.nnzb * br * bc, 1))), "hipMemset");
+}
+
+void symbolic(const Bsr& A, const std::vector<int64_t>& bp, const std::vector<int32_t>& bc_,
+    int64_t n_cols, std::vector<int64_t>& cp, std::vector<int32_t>& cc)
+{
+  cp.assign(size_t(A.n) + 1, 0);
+  const int64_t nnz = fcg_bsr_symbolic(A.n, A.ptr_h.data(), A.col_h.data(), bp.data(), bc_.data(),
+      n_cols, cp.data(), nullptr);
+  if (nnz < 0) throw Fail{FCG_ERR_ARG, "AMG: symbolic product failed"};
+  cc.assign(size_t(std::max<int64_t>(nnz, 1)), 0);
+  if (fcg_bsr_symbolic(A.n, A.ptr_h.data(), A.col_h.data(), bp.data(), bc_.data(), n_cols, cp.data(),
+          cc.data()) != nnz)
+    throw Fail{FCG_ERR_ARG, "AMG: symbolic fill pass"};
+  cc.resize(size_t(nnz));
+}
+
+std::vector<int64_t> diag_index(const Bsr& A)
+{
+  std::vector<int64_t> d(size_t(A.n), -1);
+  for (int64_t i = 0; i < A.n; ++i)
+    for (int64_t k = A.ptr_h[size_t(i)]; k < A.ptr_h[size_t(i) + 1]; ++k)
+      if (A.col_h[size_t(k)] == i) d[size_t(i)] = k;
+  for (int64_t v : d)
+    if (v < 0) throw Fail{FCG_ERR_ARG, "AMG: block row without a diagonal block"};
+  return d;
+}
+
+// ---- device helpers --------------------------------------------------------------------------
+double dot_host(fcg_amg* h, const double* a, const double* b, int64_t n, hipStream_t s)
+{
+  const unsigned g = capped(n);
+  hipLaunchKernelGGL(dot_kernel, dim3(g), dim3(kBlock), 0, s, a, b, n, h->partial);
+  hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(kBlock), 0, s, h->partial, int(g), h->sc + 6);
+  double v = 0.0;
+  ck(hipMemcpyAsync(&v, h->sc + 6, sizeof(double), hipMemcpyDeviceToHost, s), "hipMemcpyAsync");
+  ck(hipStreamSynchronize(s), "hipStreamSynchronize");
+  return v;
+}
+void dot_dev(fcg_amg* h, const double* a, const double* b, int64_t n, double* out, hipStream_t s)
+{
+  const unsigned g = capped(n);
+  hipLaunchKernelGGL(dot_kernel, dim3(g), dim3(kBlock), 0, s, a, b, n, h->partial);
+  hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(kBlock), 0, s, h->partial, int(g), out);
+}
+
+// a level's operator and smoother pieces: l = 0 the context, l >= 1 levels[l - 1]
+struct Ops {
+  fcg_amg* h;
+  int l;
+  const double* K;  // level 0 values
+  hipStream_t s;
+  int64_t n() const { return l == 0 ? h->n0 : h->levels[size_t(l - 1)].A.n * 6; }
+  void spmv(const double* x, double* y) const
+  {
+    if (l == 0)
+      ck(fcg_spmv(h->ctx, K, x, y, s), "fcg_spmv");
+    else
+    {
+      const Bsr& A = h->levels[size_t(l - 1)].A;
+      ck(fcg_bsr_spmv(h->device, 6, 6, A.n, A.ptr, A.col, A.vals, x, y, 1.0, 0, s), "fcg_bsr_spmv");
+    }
+  }
+  void dinv(const double* r, double* z, double scale, bool acc) const
+  {
+    if (l == 0)
+      ck(fcg_block_jacobi_apply(h->ctx, h->ctx_dinv, r, z, scale, acc ? 1 : 0, s), "fcg_block_jacobi_apply");
+    else
+    {
+      const Level& L = h->levels[size_t(l - 1)];
+      ck(fcg_bsr_block_jacobi_apply(h->device, 6, L.A.n, L.dinv, r, z, scale, acc ? 1 : 0, s),
+          "fcg_bsr_block_jacobi_apply");
+    }
+  }
+  double& lmax() const { return l == 0 ? h->lmax0 : h->levels[size_t(l - 1)].lmax; }
+  double* r() const { return l == 0 ? h->r0 : h->levels[size_t(l - 1)].r; }
+  double* d() const { return l == 0 ? h->d0 : h->levels[size_t(l - 1)].d; }
+  double* z() const { return l == 0 ? h->z0 : h->levels[size_t(l - 1)].z; }
+  double* p() const { return l == 0 ? h->p0 : h->levels[size_t(l - 1)].p; }
+  double* q() const { return l == 0 ? h->q0 : h->levels[size_t(l - 1)].q; }
+};
+
+// largest eigenvalue of D^-1 A from a 10-step Lanczos (block-Jacobi CG on a random vector)
+void estimate_lmax(const Ops& o)
+{
+  fcg_amg* h = o.h;
+  const int64_t n = o.n();
+  double *b = o.d(), *r = o.r(), *z = o.z(), *p = o.p(), *q = o.q();
+  hipLaunchKernelGGL(random_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, o.s, b, o.l == 0 ? h->mask0 : nullptr, n, 20251015u);
+  ck(hipMemcpyAsync(r, b, sizeof(double) * size_t(n), hipMemcpyDeviceToDevice, o.s), "copy");
+  o.dinv(r, z, 1.0, false);
+  ck(hipMemcpyAsync(p, z, sizeof(double) * size_t(n), hipMemcpyDeviceToDevice, o.s), "copy");
+  double rz = dot_host(h, r, z, n, o.s);
+  std::vector<double> al, be;
+  for (int it = 0; it < 10; ++it)
+  {
+    o.spmv(p, q);
+    const double pq = dot_host(h, p, q, n, o.s);
+    if (!(pq > 0.0))
+    {
+      if (al.empty()) throw Fail{FCG_ERR_SINGULAR, "AMG Lanczos estimate: p.Ap <= 0"};
+      break;
+    }
+    const double alpha = rz / pq;
+    hipLaunchKernelGGL(axpby_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, o.s, -alpha, q, 1.0, r, n);
+    o.dinv(r, z, 1.0, false);
+    const double rzn = dot_host(h, r, z, n, o.s);
+    al.push_back(alpha);
+    if (!(rzn > 0.0)) break;
+    be.push_back(rzn / rz);
+    hipLaunchKernelGGL(axpby_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, o.s, 1.0, z, rzn / rz, p, n);
+    rz = rzn;
+  }
+  // largest eigenvalue of the Lanczos tridiagonal (bisection on the Sturm sequence)
+  const int k = int(al.size());
+  std::vector<double> a(static_cast<size_t>(k)), e(static_cast<size_t>(k), 0.0);
+  for (int i = 0; i < k; ++i)
+  {
+    a[size_t(i)] = 1.0 / al[size_t(i)] + (i > 0 ? be[size_t(i - 1)] / al[size_t(i - 1)] : 0.0);
+    if (i + 1 < k) e[size_t(i)] = std::sqrt(be[size_t(i)]) / al[size_t(i)];
+  }
+  double hi = 0.0;
+  for (int i = 0; i < k; ++i)
+    hi = std::max(hi, a[size_t(i)] + (i > 0 ? std::fabs(e[size_t(i - 1)]) : 0.0) + (i + 1 < k ? std::fabs(e[size_t(i)]) : 0.0));
+  double lo = 0.0;
+  auto count_below = [&](double x) {  // eigenvalues < x
+    int c = 0;
+    double dd = 1.0;
+    for (int i = 0; i < k; ++i)
+    {
+      dd = a[size_t(i)] - x - (i > 0 ? e[size_t(i - 1)] * e[size_t(i - 1)] / dd : 0.0);
+      if (dd == 0.0) dd = -1e-300;
+      if (dd < 0.0) ++c;
+    }
+    return c;
+  };
+  for (int it = 0; it < 200 && hi - lo > 1e-14 * hi; ++it)
+  {
+    const double mid = 0.5 * (lo + hi);
+    if (count_below(mid) >= k) hi = mid;
+    else lo = mid;
+  }
+  o.lmax() = hi;
+}
+
+void cheb(const fcg_amg* hc, const Ops& o, const double* b, double* x, bool x_zero)
+{
+  const fcg_amg_options& op = hc->opt;
+  const int64_t n = o.n();
+  const double lmax = op.boost * o.lmax();
+  const double lmin = lmax / op.ratio;
+  const double theta = 0.5 * (lmax + lmin), delta = 0.5 * (lmax - lmin);
+  const double sigma = theta / delta;
+  double rho = 1.0 / sigma;
+  double *r = o.r(), *d = o.d();
+  const dim3 g(blocks_for(n)), bl(kBlock);
+  if (x_zero)
+  {
+    o.dinv(b, d, 1.0 / theta, false);
+    ck(hipMemcpyAsync(x, d, sizeof(double) * size_t(n), hipMemcpyDeviceToDevice, o.s), "copy");
+  }
+  else
+  {
+    o.spmv(x, r);
+    hipLaunchKernelGGL(rsub_kernel, g, bl, 0, o.s, b, r, n);
+    o.dinv(r, d, 1.0 / theta, false);
+    hipLaunchKernelGGL(axpby_kernel, g, bl, 0, o.s, 1.0, d, 1.0, x, n);
+  }
+  for (int k = 1; k < op.nu; ++k)
+  {
+    o.spmv(x, r);
+    hipLaunchKernelGGL(rsub_kernel, g, bl, 0, o.s, b, r, n);
+    const double rho_n = 1.0 / (2.0 * sigma - rho);
+    hipLaunchKernelGGL(axpby_kernel, g, bl, 0, o.s, 0.0, d, rho_n * rho, d, n);
+    o.dinv(r, d, 2.0 * rho_n / delta, true);
+    hipLaunchKernelGGL(axpby_kernel, g, bl, 0, o.s, 1.0, d, 1.0, x, n);
+    rho = rho_n;
+  }
+}
+
+// coarsest level: block-Jacobi CG from x = 0 to |r| <= coarse_rtol |b| (checked every 8 steps;
+// scalars on the device in between)
+void coarse_solve(fcg_amg* h, const Ops& o, const double* b, double* x)
+{
+  const int64_t n = o.n();
+  double *r = o.r(), *z = o.z(), *p = o.p(), *q = o.q();
+  // its own scalars (the outer FCG keeps r.r in sc[3] across the V-cycle): 0 r.z, 1 p.q,
+  // 2 r.z new, 3 r.r, 4 b.b
+  double* sc = h->sc + 8;
+  const dim3 g(blocks_for(n)), bl(kBlock);
+  ck(hipMemsetAsync(x, 0, sizeof(double) * size_t(n), o.s), "memset");
+  ck(hipMemcpyAsync(r, b, sizeof(double) * size_t(n), hipMemcpyDeviceToDevice, o.s), "copy");
+  o.dinv(r, z, 1.0, false);
+  ck(hipMemcpyAsync(p, z, sizeof(double) * size_t(n), hipMemcpyDeviceToDevice, o.s), "copy");
+  dot_dev(h, r, z, n, sc + 0, o.s);
+  dot_dev(h, b, b, n, sc + 4, o.s);
+  const double tol2 = h->opt.coarse_rtol * h->opt.coarse_rtol;
+  for (int it = 0; it < h->opt.coarse_max_iter;)
+  {
+    for (int k = 0; k < 8 && it < h->opt.coarse_max_iter; ++k, ++it)
+    {
+      o.spmv(p, q);
+      dot_dev(h, p, q, n, sc + 1, o.s);
+      hipLaunchKernelGGL(cg_step_kernel, g, bl, 0, o.s, sc, p, q, x, r, n);
+      o.dinv(r, z, 1.0, false);
+      dot_dev(h, r, z, n, sc + 2, o.s);
+      hipLaunchKernelGGL(cg_dir_kernel, g, bl, 0, o.s, sc, z, p, n);
+      hipLaunchKernelGGL(shift_kernel, dim3(1), dim3(1), 0, o.s, sc);
+    }
+    dot_dev(h, r, r, n, sc + 3, o.s);
+    double hs[5];
+    ck(hipMemcpyAsync(hs, sc, sizeof(hs), hipMemcpyDeviceToHost, o.s), "hipMemcpyAsync");
+    ck(hipStreamSynchronize(o.s), "hipStreamSynchronize");
+    if (!std::isfinite(hs[3])) throw Fail{FCG_ERR_SINGULAR, "AMG coarsest CG: non-finite residual"};
+    if (hs[3] <= tol2 * hs[4]) break;
+  }
+}
+
+void vcycle(fcg_amg* h, int l, const double* K, const double* b, double* x, hipStream_t s)
+{
+  const Ops o{h, l, K, s};
+  if (l == int(h->levels.size()))
+  {
+    coarse_solve(h, o, b, x);
+    return;
+  }
+  cheb(h, o, b, x, true);
+  double* r = o.r();
+  o.spmv(x, r);
+  const int64_t n = o.n();
+  hipLaunchKernelGGL(rsub_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, s, b, r, n);
+  const Step& st = h->steps[size_t(l)];
+  Level& c = h->levels[size_t(l)];
+  ck(fcg_bsr_spmv(h->device, 6, st.bs, st.Pt.n, st.Pt.ptr, st.Pt.col, st.Pt.vals, r, c.b, 1.0, 0, s),
+      "restriction");
+  vcycle(h, l + 1, K, c.b, c.x, s);
+  ck(fcg_bsr_spmv(h->device, st.bs, 6, st.P.n, st.P.ptr, st.P.col, st.P.vals, c.x, x, 1.0, 1, s),
+      "prolongation");
+  cheb(h, o, b, x, false);
+}
+
+// numeric setup for the tangent K (level-0 values in the context's CSR order)
+void setup(fcg_amg* h, const double* K, hipStream_t s)
+{
+  ck(fcg_block_jacobi_setup(h->ctx, K, h->ctx_dinv, s), "singular nodal block of K (block Jacobi)");
+  estimate_lmax(Ops{h, 0, K, s});
+  ck(fcg_bsr_from_node_csr(h->device, h->nb0, h->ctx->mesh.rowptr, h->A0.ptr, K, h->A0.vals, s),
+      "fcg_bsr_from_node_csr");
+  ck(fcg_bsr_block_jacobi_setup(h->device, 3, h->nb0, h->A0.ptr, h->A0_diag, h->A0.vals, h->A0_dinv,
+         h->flag, s),
+      "singular nodal block of K");
+  const Bsr* A = &h->A0;
+  const double* dinv = h->A0_dinv;
+  for (size_t l = 0; l < h->steps.size(); ++l)
+  {
+    Step& st = h->steps[l];
+    const double lm = l == 0 ? h->lmax0 : h->levels[l - 1].lmax;
+    auto product = [&](Bsr& C, const Bsr& X, const Bsr& Y) {
+      ck(fcg_bsr_spgemm(h->device, X.br, X.bc, Y.bc, X.n, X.ptr, X.col, X.vals, Y.ptr, Y.col, Y.vals,
+             C.ptr, C.col, C.vals, s),
+          "fcg_bsr_spgemm");
+    };
+    product(st.AT, *A, st.T);
+    ck(fcg_amg_smooth_prolongator(h->device, st.bs, A->n, st.P.ptr, st.P.col, st.agg, st.tent, dinv,
+           st.AT.vals, h->opt.omega / lm, st.P.vals, s),
+        "fcg_amg_smooth_prolongator");
+    product(st.AP, *A, st.P);
+    ck(fcg_bsr_transpose_values(h->device, st.bs, 6, st.P.nnzb, st.perm, st.P.vals, st.Pt.vals, s),
+        "fcg_bsr_transpose_values");
+    Level& c = h->levels[l];
+    product(c.A, st.Pt, st.AP);
+    ck(fcg_bsr_block_jacobi_setup(h->device, 6, c.A.n, c.A.ptr, c.diag, c.A.vals, c.dinv, h->flag, s),
+        "AMG coarse level: singular diagonal block");
+    if (l + 1 < h->steps.size()) estimate_lmax(Ops{h, int(l) + 1, K, s});
+    A = &c.A;
+    dinv = c.dinv;
+  }
+}
+
+// flexible CG (Polak-Ribiere) preconditioned by one V-cycle; one host read per iteration
+void run_fcg(fcg_amg* h, const double* K, const double* b, double* x, double rtol, int max_iter,
+    int* iterations, double* rel, hipStream_t s)
+{
+  const int64_t n = h->n0;
+  const dim3 g(blocks_for(n)), bl(kBlock);
+  // FCG vectors (the V-cycle's level-0 work vectors r0 / d0 are separate)
+  double *r = h->fr, *z = h->fz, *pp = h->fx, *q = h->q0, *ro = h->ro0;
+  ck(hipMemsetAsync(x, 0, sizeof(double) * size_t(n), s), "memset");
+  const double bn = std::sqrt(dot_host(h, b, b, n, s));
+  *iterations = 0;
+  *rel = 0.0;
+  if (bn == 0.0) return;
+  ck(hipMemcpyAsync(r, b, sizeof(double) * size_t(n), hipMemcpyDeviceToDevice, s), "copy");
+  vcycle(h, 0, K, r, z, s);
+  ck(hipMemcpyAsync(pp, z, sizeof(double) * size_t(n), hipMemcpyDeviceToDevice, s), "copy");
+  double rz = dot_host(h, r, z, n, s);
+  if (!(rz > 0.0)) throw Fail{FCG_ERR_SINGULAR, "AMG: indefinite V-cycle (r.z <= 0)"};
+  double rn = bn;
+  int it = 0;
+  double* sc = h->sc;
+  while (it < max_iter)
+  {
+    ++it;
+    ck(fcg_spmv(h->ctx, K, pp, q, s), "fcg_spmv");
+    dot_dev(h, pp, q, n, sc + 1, s);
+    hipLaunchKernelGGL(fcg_step_kernel, g, bl, 0, s, rz, sc + 1, pp, q, x, r, ro, n);
+    dot_dev(h, r, r, n, sc + 3, s);
+    vcycle(h, 0, K, r, z, s);
+    dot_dev(h, r, z, n, sc + 2, s);
+    dot_dev(h, z, ro, n, sc + 5, s);
+    double hs[6];
+    ck(hipMemcpyAsync(hs, sc, sizeof(hs), hipMemcpyDeviceToHost, s), "hipMemcpyAsync");
+    ck(hipStreamSynchronize(s), "hipStreamSynchronize");
+    rn = std::sqrt(hs[3]);
+    if (!std::isfinite(rn)) throw Fail{FCG_ERR_SINGULAR, "AMG FCG: non-finite residual"};
+    if (rn <= rtol * bn) break;
+    if (!(hs[2] > 0.0)) throw Fail{FCG_ERR_SINGULAR, "AMG: indefinite V-cycle (r.z <= 0)"};
+    const double beta = (hs[2] - hs[5]) / rz;
+    hipLaunchKernelGGL(axpby_kernel, g, bl, 0, s, 1.0, z, beta, pp, n);
+    rz = hs[2];
+  }
+  *iterations = it;
+  *rel = rn / bn;
+}
+
+}  // namespace fcg_amgs
+
+extern "C" {
+
+void fcg_amg_default_options(fcg_amg_options* opt)
+{
+  if (!opt) return;
+  opt->nu = 2;
+  opt->max_levels = 10;
+  opt->coarse_max = 3000;
+  opt->coarse_max_iter = 500;
+  opt->coarse_rtol = 1e-2;
+  opt->omega = 4.0 / 3.0;
+  opt->ratio = 20.0;
+  opt->boost = 1.1;
+}
+
+int fcg_amg_create(fcg_ctx* ctx, const int64_t* rowptr, const int32_t* col_lid,
+    const double* node_x, int64_t n_dbc, const int32_t* dbc_rows, const fcg_amg_options* opt,
+    fcg_amg** out)
+{
+  using namespace fcg_amgs;
+  if (!ctx || !rowptr || !col_lid || !node_x || !out || n_dbc < 0 || (n_dbc > 0 && !dbc_rows))
+    return FCG_ERR_ARG;
+  *out = nullptr;
+  const fcg::DeviceMesh& m = ctx->mesh;
+  if (!m.square_local || m.n_rows % 3 != 0 || m.n_rows == 0)
+  {
+    ctx->last_error = "fcg_amg_create: single-rank system with 3 DOFs per node rows 3b..3b+2";
+    return FCG_ERR_ARG;
+  }
+  fcg_amg* h = new fcg_amg();
+  h->ctx = ctx;
+  h->device = ctx->device;
+  if (opt) h->opt = *opt;
+  else fcg_amg_default_options(&h->opt);
+  try
+  {
+    ck(hipSetDevice(h->device), "hipSetDevice");
+    const int64_t n = m.n_rows, nb = n / 3;
+    h->n0 = n;
+    h->nb0 = nb;
+    // level 0 block graph: block row b = rows 3b..3b+2 (one pattern of DOF triples)
+    std::vector<int64_t> bptr(size_t(nb) + 1, 0);
+    for (int64_t b = 0; b < nb; ++b)
+    {
+      const int64_t len = rowptr[3 * b + 1] - rowptr[3 * b];
+      if (len % 3 != 0 || rowptr[3 * b + 2] - rowptr[3 * b + 1] != len || rowptr[3 * b + 3] - rowptr[3 * b + 2] != len)
+        throw Fail{FCG_ERR_ARG, "fcg_amg_create: rows 3b..3b+2 must share one pattern of DOF triples"};
+      bptr[size_t(b) + 1] = bptr[size_t(b)] + len / 3;
+    }
+    std::vector<int32_t> bcol(size_t(bptr.back()));
+    for (int64_t b = 0; b < nb; ++b)
+      for (int64_t k = 0; k < bptr[size_t(b) + 1] - bptr[size_t(b)]; ++k)
+      {
+        const int32_t c = col_lid[rowptr[3 * b] + 3 * k];
+        if (c < 0 || c % 3 != 0 || c >= n) throw Fail{FCG_ERR_ARG, "fcg_amg_create: column triples must start at 3 c"};
+        bcol[size_t(bptr[size_t(b)] + k)] = c / 3;
+      }
+    make_bsr(h, h->A0, bptr, bcol, 3, 3, nb);
+    h->A0_diag = upload(h, diag_index(h->A0));
+    h->A0_dinv = dalloc<double>(h, 9 * nb);
+    h->ctx_dinv = dalloc<double>(h, 9 * nb);
+    std::vector<uint8_t> dbc(size_t(n), 0);
+    for (int64_t k = 0; k < n_dbc; ++k)
+    {
+      if (dbc_rows[k] < 0 || dbc_rows[k] >= n) throw Fail{FCG_ERR_ARG, "fcg_amg_create: Dirichlet row out of range"};
+      dbc[size_t(dbc_rows[k])] = 1;
+    }
+    std::vector<double> mask(static_cast<size_t>(n));
+    for (int64_t i = 0; i < n; ++i) mask[size_t(i)] = dbc[size_t(i)] ? 0.0 : 1.0;
+    h->mask0 = upload(h, mask);
+    // near-null space: rigid-body modes about the centroid, Dirichlet rows zeroed
+    double cen[3] = {0, 0, 0};
+    for (int64_t b = 0; b < nb; ++b)
+      for (int d = 0; d < 3; ++d) cen[d] += node_x[3 * b + d] / double(nb);
+    std::vector<double> ns(size_t(nb) * 18, 0.0);
+    std::vector<uint8_t> skip(size_t(nb), 0);
+    for (int64_t b = 0; b < nb; ++b)
+    {
+      const double x = node_x[3 * b] - cen[0], y = node_x[3 * b + 1] - cen[1], z = node_x[3 * b + 2] - cen[2];
+      double* B = ns.data() + 18 * b;  // [3][6]
+      B[0 * 6 + 0] = B[1 * 6 + 1] = B[2 * 6 + 2] = 1.0;
+      B[0 * 6 + 3] = -y; B[1 * 6 + 3] = x;
+      B[1 * 6 + 4] = -z; B[2 * 6 + 4] = y;
+      B[0 * 6 + 5] = z;  B[2 * 6 + 5] = -x;
+      int nd = 0;
+      for (int d = 0; d < 3; ++d)
+        if (dbc[size_t(3 * b + d)])
+        {
+          ++nd;
+          for (int j = 0; j < 6; ++j) B[d * 6 + j] = 0.0;
+        }
+      skip[size_t(b)] = nd == 3;
+    }
+    const Bsr* A = &h->A0;
+    int bs = 3;
+    bool first = true;
+    while ((A->n * bs > h->opt.coarse_max || h->steps.empty()) && int(h->steps.size()) + 1 < h->opt.max_levels)
+    {
+      std::vector<int32_t> agg(size_t(A->n));
+      const int64_t n_agg = fcg_amg_aggregate(A->n, A->ptr_h.data(), A->col_h.data(), first ? skip.data() : nullptr, agg.data());
+      if (n_agg <= 0 || n_agg >= A->n) break;
+      std::vector<double> tent(size_t(A->n) * bs * 6), nsc(size_t(n_agg) * 36);
+      int64_t nd = 0;
+      ck(fcg_amg_tentative(A->n, bs, ns.data(), agg.data(), n_agg, tent.data(), nsc.data(), &nd), "fcg_amg_tentative");
+      h->steps.emplace_back();
+      Step& st = h->steps.back();
+      st.bs = bs;
+      st.n_agg = n_agg;
+      std::vector<int64_t> tptr(size_t(A->n) + 1, 0);
+      std::vector<int32_t> tcol;
+      std::vector<double> tvals;
+      for (int64_t i = 0; i < A->n; ++i)
+      {
+        tptr[size_t(i) + 1] = tptr[size_t(i)] + (agg[size_t(i)] >= 0 ? 1 : 0);
+        if (agg[size_t(i)] >= 0)
+        {
+          tcol.push_back(agg[size_t(i)]);
+          tvals.insert(tvals.end(), tent.begin() + i * bs * 6, tent.begin() + (i + 1) * bs * 6);
+        }
+      }
+      make_bsr(h, st.T, tptr, tcol, bs, 6, n_agg);
+      if (!tvals.empty())
+        ck(hipMemcpy(st.T.vals, tvals.data(), sizeof(double) * tvals.size(), hipMemcpyHostToDevice), "hipMemcpy");
+      st.agg = upload(h, agg);
+      st.tent = upload(h, tent);
+      std::vector<int64_t> pp, app, tp, cp;
+      std::vector<int32_t> pc, apc, tc, cc;
+      symbolic(*A, st.T.ptr_h, st.T.col_h, n_agg, pp, pc);
+      make_bsr(h, st.P, pp, pc, bs, 6, n_agg);
+      make_bsr(h, st.AT, pp, pc, bs, 6, n_agg);
+      symbolic(*A, pp, pc, n_agg, app, apc);
+      make_bsr(h, st.AP, app, apc, bs, 6, n_agg);
+      tp.assign(size_t(n_agg) + 1, 0);
+      tc.assign(size_t(std::max<int64_t>(pp.back(), 1)), 0);
+      std::vector<int64_t> perm(size_t(std::max<int64_t>(pp.back(), 1)));
+      ck(fcg_bsr_transpose_pattern(A->n, n_agg, pp.data(), pc.data(), tp.data(), tc.data(), perm.data()), "fcg_bsr_transpose_pattern");
+      tc.resize(size_t(pp.back()));
+      perm.resize(size_t(pp.back()));
+      make_bsr(h, st.Pt, tp, tc, 6, bs, A->n);
+      st.perm = upload(h, perm);
+      symbolic(st.Pt, app, apc, n_agg, cp, cc);
+      h->levels.emplace_back();
+      Level& c = h->levels.back();
+      make_bsr(h, c.A, cp, cc, 6, 6, n_agg);
+      c.diag = upload(h, diag_index(c.A));
+      c.dinv = dalloc<double>(h, 36 * n_agg);
+      for (double** v : {&c.x, &c.b, &c.r, &c.d, &c.z, &c.p, &c.q}) *v = dalloc<double>(h, 6 * n_agg);
+      ns.swap(nsc);
+      A = &c.A;
+      bs = 6;
+      first = false;
+    }
+    if (h->levels.empty()) throw Fail{FCG_ERR_ARG, "fcg_amg_create: no coarse level (aggregation did not coarsen)"};
+    for (double** v : {&h->r0, &h->d0, &h->z0, &h->q0, &h->p0, &h->ro0, &h->fr, &h->fz, &h->fx})
+      *v = dalloc<double>(h, n);
+    h->partial = dalloc<double>(h, kMaxPartials);
+    h->sc = dalloc<double>(h, 16);  // [0, 6) outer FCG, 6 host dots, [8, 13) coarsest CG
+    h->flag = dalloc<int32_t>(h, 1);
+  }
+  catch (const Fail& f)
+  {
+    ctx->last_error = f.msg;
+    fcg_amg_destroy(h);
+    return f.code;
+  }
+  *out = h;
+  return FCG_OK;
+}
+
+int fcg_amg_solve(fcg_amg* h, const double* d_K_vals, const double* d_b_row, double* d_x_row,
+    double rtol, int max_iter, int* iterations, double* rel_residual, void* stream)
+{
+  using namespace fcg_amgs;
+  if (!h || !d_K_vals || !d_b_row || !d_x_row || !(rtol >= 0.0) || max_iter < 0) return FCG_ERR_ARG;
+  int it = 0;
+  double rel = 0.0;
+  try
+  {
+    ck(hipSetDevice(h->device), "hipSetDevice");
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->ctx->stream;
+    hipEvent_t e0, e1;
+    ck(hipEventCreate(&e0), "hipEventCreate");
+    ck(hipEventCreate(&e1), "hipEventCreate");
+    ck(hipEventRecord(e0, s), "hipEventRecord");
+    setup(h, d_K_vals, s);
+    ck(hipEventRecord(e1, s), "hipEventRecord");
+    ck(hipEventSynchronize(e1), "hipEventSynchronize");
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    h->setup_ms = ms;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    run_fcg(h, d_K_vals, d_b_row, d_x_row, rtol, max_iter, &it, &rel, s);
+  }
+  catch (const Fail& f)
+  {
+    h->last_error = f.msg;
+    h->ctx->last_error = f.msg;
+    if (iterations) *iterations = it;
+    if (rel_residual) *rel_residual = rel;
+    return f.code;
+  }
+  if (iterations) *iterations = it;
+  if (rel_residual) *rel_residual = rel;
+  return FCG_OK;
+}
+
+int fcg_amg_level_info(const fcg_amg* h, int level, int64_t* dofs, int64_t* blocks, double* lmax)
+{
+  if (!h || level < 0 || level > int(h->levels.size())) return FCG_ERR_ARG;
+  if (level == 0)
+  {
+    if (dofs) *dofs = h->n0;
+    if (blocks) *blocks = h->A0.nnzb;
+    if (lmax) *lmax = h->lmax0;
+    return FCG_OK;
+  }
+  const fcg_amgs::Level& c = h->levels[size_t(level - 1)];
+  if (dofs) *dofs = c.A.n * 6;
+  if (blocks) *blocks = c.A.nnzb;
+  if (lmax) *lmax = c.lmax;
+  return FCG_OK;
+}
+
+int fcg_amg_levels(const fcg_amg* h) { return h ? int(h->levels.size()) + 1 : 0; }
+
+double fcg_amg_setup_ms(const fcg_amg* h) { return h ? h->setup_ms : -1.0; }
+
+const char* fcg_amg_last_error(const fcg_amg* h) { return h ? h->last_error.c_str() : ""; }
+
+int fcg_amg_destroy(fcg_amg* h)
+{
+  if (!h) return FCG_OK;
+  (void)hipSetDevice(h->device);
+  for (void* p : h->allocs) (void)hipFree(p);
+  delete h;
+  return FCG_OK;
+}
+
+}  // extern "C"

@@ -101,6 +101,14 @@ class FcgTsiDesc(ctypes.Structure):
 
 
 # every symbol declared in include/fourc_gpu.h
+class FcgAmgOptions(ctypes.Structure):
+    """fcg_amg_options (include/fourc_gpu.h)."""
+    _fields_ = [("nu", ctypes.c_int32), ("max_levels", ctypes.c_int32),
+                ("coarse_max", ctypes.c_int64), ("coarse_max_iter", ctypes.c_int32),
+                ("coarse_rtol", ctypes.c_double), ("omega", ctypes.c_double),
+                ("ratio", ctypes.c_double), ("boost", ctypes.c_double)]
+
+
 EXPORTS = ["fcg_create", "fcg_destroy", "fcg_last_error", "fcg_evaluate", "fcg_evaluate_device",
            "fcg_device_alloc", "fcg_device_free", "fcg_memcpy_h2d", "fcg_memcpy_d2h",
            "fcg_memset_device", "fcg_set_timing", "fcg_get_timing", "fcg_get_info",
@@ -121,7 +129,9 @@ EXPORTS = ["fcg_create", "fcg_destroy", "fcg_last_error", "fcg_evaluate", "fcg_e
            "fcg_amg_aggregate", "fcg_amg_tentative", "fcg_bsr_symbolic", "fcg_bsr_transpose_pattern",
            "fcg_bsr_spmv", "fcg_bsr_spgemm", "fcg_bsr_transpose_values", "fcg_bsr_from_node_csr",
            "fcg_bsr_block_jacobi_setup", "fcg_bsr_block_jacobi_apply", "fcg_amg_smooth_prolongator",
-           "fcg_bsr_to_dense"]
+           "fcg_bsr_to_dense", "fcg_amg_default_options", "fcg_amg_create", "fcg_amg_solve",
+           "fcg_amg_levels", "fcg_amg_level_info", "fcg_amg_setup_ms", "fcg_amg_last_error",
+           "fcg_amg_destroy"]
 
 _lib = None
 FUNCT_FN = ctypes.CFUNCTYPE(ctypes.c_double, ctypes.c_int, _dp, ctypes.c_double, ctypes.c_void_p)
@@ -244,6 +254,18 @@ def lib():
     L.fcg_amg_smooth_prolongator.argtypes = [c_int, c_int, i64, vp, vp, vp, vp, vp, vp, c_dbl, vp,
                                              vp]
     L.fcg_bsr_to_dense.argtypes = [c_int, c_int, i64, vp, vp, vp, vp, vp]
+    L.fcg_amg_default_options.argtypes = [ctypes.POINTER(FcgAmgOptions)]
+    L.fcg_amg_default_options.restype = None
+    L.fcg_amg_create.argtypes = [vp, vp, vp, vp, i64, vp, ctypes.POINTER(FcgAmgOptions),
+                                 ctypes.POINTER(vp)]
+    L.fcg_amg_solve.argtypes = [vp, vp, vp, vp, c_dbl, c_int, ctypes.POINTER(c_int), _dp, vp]
+    L.fcg_amg_levels.argtypes = [vp]
+    L.fcg_amg_level_info.argtypes = [vp, c_int, _i64p, _i64p, _dp]
+    L.fcg_amg_setup_ms.argtypes = [vp]
+    L.fcg_amg_setup_ms.restype = c_dbl
+    L.fcg_amg_last_error.argtypes = [vp]
+    L.fcg_amg_last_error.restype = ctypes.c_char_p
+    L.fcg_amg_destroy.argtypes = [vp]
     _lib = L
     return L
 

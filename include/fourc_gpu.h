@@ -265,6 +265,38 @@ int fcg_amg_smooth_prolongator(int device, int br, int64_t n_brows, const int64_
 int fcg_bsr_to_dense(int device, int b, int64_t n_brows, const int64_t* d_ptr, const int32_t* d_col,
     const double* d_vals, double* d_dense, void* stream);
 
+/* The smoothed-aggregation AMG solve as one native object (fcg_amg_solver.hip): what a C++ host
+ * calls instead of its Belos CG + MueLu preconditioner on a tangent the context assembled.
+ * fcg_amg_create: the context's own CSR graph (host rowptr / col_lid as in fcg_desc; rows 3b..3b+2
+ * = the DOFs of block row b, single rank), node_x[b][3] the reference coordinates of block row b's
+ * node, the Dirichlet rows (unit rows of K); builds the hierarchy's patterns on the host.
+ * fcg_amg_solve: numeric setup for d_K_vals (the tangent after fcg_dirichlet_apply) and flexible
+ * CG with one V-cycle per iteration from x = 0 to |r| <= rtol |b|; returns FCG_ERR_SINGULAR when
+ * the V-cycle turns indefinite or the iteration diverges.  fcg_amg_level_info: DOFs, blocks and
+ * the lambda_max estimate of level 0 .. fcg_amg_levels() - 1; fcg_amg_setup_ms: the last numeric
+ * setup (hipEvent time). */
+typedef struct fcg_amg fcg_amg;
+typedef struct fcg_amg_options {
+  int32_t nu;               /* Chebyshev degree of the smoother (2) */
+  int32_t max_levels;       /* (10) */
+  int64_t coarse_max;       /* coarsen until a level has at most this many DOFs (3000) */
+  int32_t coarse_max_iter;  /* block-Jacobi CG iterations on the coarsest level, at most (500) */
+  double coarse_rtol;       /* ... until |r| <= coarse_rtol |b| (1e-2) */
+  double omega;             /* prolongator damping times 1 / lambda_max(D^-1 A) (4/3) */
+  double ratio, boost;      /* Chebyshev eigenvalue ratio (20) and lambda_max boost (1.1) */
+} fcg_amg_options;
+void fcg_amg_default_options(fcg_amg_options* opt);
+int fcg_amg_create(fcg_ctx* ctx, const int64_t* rowptr, const int32_t* col_lid,
+    const double* node_x, int64_t n_dbc, const int32_t* dbc_rows, const fcg_amg_options* opt,
+    fcg_amg** out);
+int fcg_amg_solve(fcg_amg* amg, const double* d_K_vals, const double* d_b_row, double* d_x_row,
+    double rtol, int max_iter, int* iterations, double* rel_residual, void* stream);
+int fcg_amg_levels(const fcg_amg* amg);
+int fcg_amg_level_info(const fcg_amg* amg, int level, int64_t* dofs, int64_t* blocks, double* lmax);
+double fcg_amg_setup_ms(const fcg_amg* amg);
+const char* fcg_amg_last_error(const fcg_amg* amg);
+int fcg_amg_destroy(fcg_amg* amg);
+
 /* Neumann loads (host arrays; added into fext_row, owned rows only).  funct[d] > 0 selects a
  * spatial function evaluated through `fn` at the reference position of each integration point
  * (Core::Utils::FunctionOfSpaceTime::evaluate); funct may be NULL.

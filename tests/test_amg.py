@@ -221,18 +221,21 @@ def _loads(dis, load, axis_load=2):
     return dbc, fext
 
 
-def _newton_pair(dis, kin, load, tol=1e-10, **amg_kw):
+def _newton_pair(dis, kin, load, tol=1e-10, cls=None, **amg_kw):
     torch, dev = _dev()
     dbc, fext = _loads(dis, load)
+    cls = cls or amg.AMG
     out = {}
     for name in ("pcg", "amg"):
         ev = fcg.Evaluator(dis, kinematics=kin, youngs=E, poisson=NU)
-        solver = amg.AMG(dis, ev, dbc, **amg_kw) if name == "amg" else None
+        solver = cls(dis, ev, dbc, **amg_kw) if name == "amg" else None
         nt = newton.StaticNewton(ev, fext, dbc, tol_res=tol * np.linalg.norm(fext), tol_inc=1e-9,
                                  lin_rtol=1e-12, linear_solver=solver)
         u = nt.solve()
         out[name] = (u.cpu().numpy(), sum(h.get("lin_iter", 0) for h in nt.history),
                      solver.describe() if solver else None)
+        if solver is not None and hasattr(solver, "close"):
+            solver.close()
         ev.close()
     return out
 
@@ -278,6 +281,72 @@ def test_hierarchy_matches_its_definition():
         Acref[empty, empty] = 1.0
         assert np.abs(Ac - Acref).max() <= 1e-11 * np.abs(Acref).max()
         A = Ac
+    ev.close()
+
+
+def _case(case):
+    if case == "renumbered-linear":
+        return fcg.Discretization.renumbered(fcg.BoxMesh(fcg.HEX8, (16, 6, 6), upper=(4.0, 1.0, 1.0), jitter=0.1), seed=1), fcg.LINEAR, -1e-2
+    if case == "renumbered-totlag":
+        return fcg.Discretization.renumbered(fcg.BoxMesh(fcg.HEX8, (12, 4, 4), upper=(3.0, 1.0, 1.0)), seed=2), fcg.TOTLAG, -0.5
+    if case == "tiled-beam":
+        return tiled_input_mesh(load_fixture(FX), (3, 6, 2), jitter=0.15, seed=11), fcg.LINEAR, -1e-3
+    return fcg.Discretization.renumbered(fcg.BoxMesh(fcg.HEX27, (6, 3, 3), upper=(3.0, 1.0, 1.0)), seed=3), fcg.TOTLAG, -0.5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["renumbered-linear", "renumbered-totlag", "tiled-beam", "hex27"])
+def test_newton_native_amg_matches_pcg(case):
+    """The C-ABI AMG object (fcg_amg_create / fcg_amg_solve) in the Newton loop."""
+    dis, kin, load = _case(case)
+    out = _newton_pair(dis, kin, load, cls=amg.NativeAMG)
+    (u0, it0, _), (u1, it1, lv) = out["pcg"], out["amg"]
+    assert len(lv) >= 2 and all(l["lmax"] > 0 for l in lv[:-1])
+    assert np.linalg.norm(u1 - u0) <= 1e-8 * np.linalg.norm(u0)
+    assert it1 * 3 < it0, (it0, it1, lv)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cls", ["AMG", "NativeAMG"])
+def test_amg_reported_residual_is_the_true_one(cls):
+    """The returned relative residual is |b - K x| / |b| of the returned x (not a stale scalar)."""
+    torch, dev = _dev()
+    dis, kin, load = _case("renumbered-linear")
+    dbc, fext = _loads(dis, load)
+    ev = fcg.Evaluator(dis, kinematics=fcg.LINEAR, youngs=E, poisson=NU)
+    f64 = dict(dtype=torch.float64, device=dev)
+    K = torch.zeros(dis.nnz, **f64)
+    ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, torch.zeros(dis.n_cols, **f64),
+                       torch.zeros(dis.n_rows, **f64), K)
+    b = torch.from_numpy(fext).to(dev)
+    ev.dirichlet_apply(torch.from_numpy(dbc).to(dev), K, b)
+    solver = getattr(amg, cls)(dis, ev, dbc)
+    for rtol in (1e-4, 1e-9):
+        x = torch.empty_like(b)
+        it, rel = solver.solve(K, b, x, rtol, 500)
+        Kx = torch.empty_like(b)
+        ev.spmv(K, x, Kx)
+        true = float(torch.linalg.vector_norm(b - Kx) / torch.linalg.vector_norm(b))
+        assert rel <= rtol and true <= 2 * rtol and abs(true - rel) <= 0.5 * rtol, (cls, rtol, it, rel, true)
+    if hasattr(solver, "close"):
+        solver.close()
+    ev.close()
+
+
+@pytest.mark.gpu
+def test_native_amg_rejects_bad_input():
+    torch, dev = _dev()
+    dis, kin, load = _case("renumbered-totlag")
+    dbc, fext = _loads(dis, load)
+    ev = fcg.Evaluator(dis, kinematics=kin, youngs=E, poisson=NU)
+    with pytest.raises(fcg.FcgError):
+        amg.NativeAMG(dis, ev, np.array([dis.n_rows + 5], dtype=np.int32))
+    solver = amg.NativeAMG(dis, ev, dbc)
+    K = torch.zeros(dis.nnz, dtype=torch.float64, device=dev)  # all-zero tangent: singular blocks
+    b = torch.ones(dis.n_rows, dtype=torch.float64, device=dev)
+    with pytest.raises(fcg.FcgError):
+        solver.solve(K, b, torch.empty_like(b), 1e-8)
+    solver.close()
     ev.close()
 
 

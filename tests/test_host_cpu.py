@@ -21,7 +21,7 @@ def test_library_exports_every_header_symbol():
     L = fcg.lib()
     with open(os.path.join(ROOT, "include", "fourc_gpu.h")) as f:
         hdr = f.read()
-    declared = set(re.findall(r"^(?:int|int64_t|void|const char\*)\s+\*?(fcg_[a-z0-9_]+)\s*\(", hdr, re.M))
+    declared = set(re.findall(r"^(?:int|int64_t|double|void|const char\*)\s+\*?(fcg_[a-z0-9_]+)\s*\(", hdr, re.M))
     assert declared == set(fcg.EXPORTS), declared ^ set(fcg.EXPORTS)
     for name in declared:
         assert hasattr(L, name), name

@@ -38,6 +38,8 @@ ap.add_argument("--mg-ratio", type=float, default=20.0)
 ap.add_argument("--mg-mixed", action="store_true", help="FP32 copy of K in the fine smoother")
 ap.add_argument("--amg", action="store_true",
                 help="smoothed-aggregation AMG preconditioned flexible CG (4c_amd/amg.py)")
+ap.add_argument("--amg-native", action="store_true",
+                help="the same AMG as the native C-ABI object (fcg_amg_create / fcg_amg_solve)")
 ap.add_argument("--renumber", action="store_true",
                 help="solve on the box renumbered as an input-file mesh (no lattice, random order)")
 a = ap.parse_args()
@@ -123,9 +125,11 @@ if a.mg:
     print(f"multigrid setup {time.perf_counter() - t_mg:.1f} s: {json.dumps(mg.describe())}",
           file=sys.stderr, flush=True)
     t_setup = time.perf_counter() - t0
-if a.amg:
+if a.amg or a.amg_native:
     t_mg = time.perf_counter()
-    mg = importlib.import_module("4c_amd.amg").AMG(mesh, ev, dbc, nu=a.mg_nu, ratio=a.mg_ratio)
+    amg_mod = importlib.import_module("4c_amd.amg")
+    mg = (amg_mod.NativeAMG(mesh, ev, dbc, nu=a.mg_nu, ratio=a.mg_ratio) if a.amg_native
+          else amg_mod.AMG(mesh, ev, dbc, nu=a.mg_nu, ratio=a.mg_ratio))
     t_amg_setup = time.perf_counter() - t_mg
     print(f"AMG setup (host graph) {t_amg_setup:.1f} s: {json.dumps(mg.describe())}",
           file=sys.stderr, flush=True)
@@ -155,7 +159,9 @@ out = {"config": f"{a.celltype}-{a.kinem}-{a.n}^3-cantilever", "forcing": a.forc
        "converged": True, "tangent_symmetry_rel": sym,
        "residual_rel_incl_dbc_rows": r_final,
        "linear_solver": (f"multigrid-FCG (Chebyshev {a.mg_nu})" if a.mg else
-                         f"SA-AMG-FCG (Chebyshev {a.mg_nu})" if a.amg else "block-Jacobi PCG"),
+                         f"SA-AMG-FCG (Chebyshev {a.mg_nu})" if a.amg else
+                         f"SA-AMG-FCG native C ABI (Chebyshev {a.mg_nu})" if a.amg_native else
+                         "block-Jacobi PCG"),
        "mesh": "renumbered (input-file order, no lattice)" if a.renumber else "GridGenerator box",
        "mg_levels": mg.describe() if mg else None, "elements": mesh.n_ele,
        "dofs": mesh.n_rows, "nnz": mesh.nnz, "setup_s": t_setup, "newton_s": t_newton,
@@ -165,7 +171,7 @@ out = {"config": f"{a.celltype}-{a.kinem}-{a.n}^3-cantilever", "forcing": a.forc
        "solve_ms_total": float(sum(r.get("solve_ms", 0.0) for r in h)),
        "pcg_iterations": [r.get("pcg_iter") for r in h[:-1]],
        "tip_uz": float(u[mesh.node_dof_row[np.argmax(mesh.node_x.sum(axis=1))] + 2]),
-       "amg_graph_setup_s": t_amg_setup if a.amg else None,
-       "amg_numeric_setup_ms": mg.setup_ms if a.amg else None,
+       "amg_graph_setup_s": t_amg_setup if (a.amg or a.amg_native) else None,
+       "amg_numeric_setup_ms": mg.setup_ms if (a.amg or a.amg_native) else None,
        "history": h}
 print(json.dumps(out))
