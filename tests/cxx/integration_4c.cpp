@@ -267,6 +267,64 @@ int main(int argc, char** argv)
         nranks, (long long)d.n_ele, nrows, ek, ef);
     failures += !(ek <= 1e-12 && ef <= 1e-10);
 
+    // single rank: the tangent's linear solve through the native AMG object instead of Belos +
+    // MueLu ("The linear solve on the device"), clamped x = 0 face
+    if (nranks == 1)
+    {
+      const int64_t nnz = rowptr[nrows];
+      std::vector<int32_t> dbc;
+      std::vector<double> xb(size_t(nrows), 0.0), b(size_t(nrows), 0.0);
+      for (int n = 0; n < colnode.NumMyElements(); ++n)
+      {
+        const int r0 = node_dof_row[n];
+        if (r0 < 0) continue;
+        for (int k = 0; k < 3; ++k) xb[size_t(r0 + k)] = x[3 * n + k];
+        if (x[3 * n] == 0.0)
+          for (int k = 0; k < 3; ++k) dbc.push_back(r0 + k);
+        b[size_t(r0 + 2)] = -1e-3 * (1.0 + x[3 * n]);  // a distributed downward load
+      }
+      std::vector<double> xnode(xb.size());  // coordinates of block row b's node: rows 3b..3b+2
+      for (int i = 0; i < nrows; ++i) xnode[size_t(i)] = xb[size_t(i)];
+      void *dK = nullptr, *db = nullptr, *dx = nullptr, *drows = nullptr;
+      fcg_device_alloc(0, nnz * 8, &dK);
+      fcg_device_alloc(0, int64_t(nrows) * 8, &db);
+      fcg_device_alloc(0, int64_t(nrows) * 8, &dx);
+      fcg_device_alloc(0, int64_t(dbc.size()) * 4, &drows);
+      fcg_memcpy_h2d(dK, vals, nnz * 8);
+      fcg_memcpy_h2d(db, b.data(), int64_t(nrows) * 8);
+      fcg_memcpy_h2d(drows, dbc.data(), int64_t(dbc.size()) * 4);
+      rc = fcg_dirichlet_apply(ctx, int64_t(dbc.size()), static_cast<int32_t*>(drows),
+          static_cast<double*>(dK), static_cast<double*>(db), nullptr, nullptr);
+      if (rc != FCG_OK) FOUR_C_THROW("{}", fcg_last_error(ctx));
+      fcg_amg* amg = nullptr;
+      rc = fcg_amg_create(ctx, rowptr.data(), cols, xnode.data(), int64_t(dbc.size()), dbc.data(),
+          nullptr, &amg);
+      if (rc != FCG_OK) FOUR_C_THROW("{}", fcg_last_error(ctx));
+      int iters = 0;
+      double relres = 0.0;
+      rc = fcg_amg_solve(amg, static_cast<double*>(dK), static_cast<double*>(db),
+          static_cast<double*>(dx), 1e-8, 500, &iters, &relres, nullptr);
+      if (rc != FCG_OK) FOUR_C_THROW("{}", fcg_amg_last_error(amg));
+      std::vector<double> Kd(static_cast<size_t>(nnz)), bd(static_cast<size_t>(nrows)), xs(static_cast<size_t>(nrows));
+      fcg_memcpy_d2h(Kd.data(), dK, nnz * 8);
+      fcg_memcpy_d2h(bd.data(), db, int64_t(nrows) * 8);
+      fcg_memcpy_d2h(xs.data(), dx, int64_t(nrows) * 8);
+      double rr = 0.0, bb = 0.0;
+      for (int i = 0; i < nrows; ++i)
+      {
+        double t = bd[size_t(i)];
+        for (int64_t j = rowptr[i]; j < rowptr[i + 1]; ++j) t -= Kd[size_t(j)] * xs[size_t(cols[j])];
+        rr += t * t;
+        bb += bd[size_t(i)] * bd[size_t(i)];
+      }
+      const double truerel = std::sqrt(rr / bb);
+      std::printf("  fcg_amg: %d levels, %d FCG iterations, reported |r|/|b| %.2e, recomputed %.2e\n",
+          fcg_amg_levels(amg), iters, relres, truerel);
+      failures += !(relres <= 1e-8 && truerel <= 2e-8 && fcg_amg_levels(amg) >= 2);
+      fcg_amg_destroy(amg);
+      for (void* pbuf : {dK, db, dx, drows}) fcg_device_free(pbuf);
+    }
+
     // the C++ facade: Discretization::evaluate(params, stiff, null, fint, null, null) (+=) and
     // its zero()-fused variant on garbage-filled storage
     fcg_destroy(ctx);
