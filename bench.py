@@ -179,6 +179,36 @@ def newton_secondary(n, timeout_s=900):
     }
 
 
+def amg_newton_secondary(n, timeout_s=600):
+    """The 1M-hex8 box renumbered as an input-file mesh (no lattice: the gather path), x- clamped,
+    tip load, StVK TotLag full Newton with the native smoothed-aggregation AMG object
+    (fcg_amg_create / fcg_amg_solve) -- the solve 4C's MueLu does on meshes without a box --
+    run by tools/newton_bench.py in a child process."""
+    cmd = [sys.executable, os.path.join(ROOT, "tools", "newton_bench.py"), "--celltype", "hex8",
+           "--kinem", "totlag", "--n", str(n), "--length", "1", "--load=-1e-2", "--renumber",
+           "--amg-native"]
+    t = time.perf_counter()
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s)
+    wall = time.perf_counter() - t
+    name = f"hex8-totlag-{n}^3-renumbered-full-newton-amg"
+    if p.returncode != 0:
+        return {"workload": name, "error": p.stderr[-2000:]}
+    d = json.loads(p.stdout.strip().splitlines()[-1])
+    if not d.get("converged"):
+        return {"workload": name, "error": "Newton did not converge"}
+    return {
+        "workload": name,
+        "baseline_config": "BASELINE.json configs[1] mesh without lattice, full Newton (SURVEY §8f row 2)",
+        "value": d["newton_s"], "unit": "s (Newton loop, setup excluded)", "higher_is_better": False,
+        "newton_iterations": d["newton_iterations"], "linear_iterations": d["pcg_iterations"],
+        "linear_solver": d["linear_solver"], "amg_levels": d["mg_levels"],
+        "amg_numeric_setup_ms": d["amg_numeric_setup_ms"], "amg_graph_setup_s": d["amg_graph_setup_s"],
+        "assembly_ms_mean": d["assembly_ms_mean"], "solve_ms_total": d["solve_ms_total"],
+        "norm_res": [h["norm_res"] for h in d["history"]], "wall_s": wall,
+        "elements": d["elements"], "dofs": d["dofs"], "nnz": d["nnz"],
+    }
+
+
 # SURVEY.md §8d algorithmic figures for hex27 TotLag K + r (per element)
 ALG_BYTES_PER_ELE_H27 = 37695.0
 ALG_FLOP_PER_ELE_H27_TOTLAG = 2.59e6
@@ -532,6 +562,8 @@ def main():
     ap.add_argument("--no-tsi", action="store_true", help="skip the TSI (config 5) line")
     ap.add_argument("--hex27-n", type=int, default=40)
     ap.add_argument("--no-newton", action="store_true", help="skip the config-3 Newton line")
+    ap.add_argument("--no-amg", action="store_true",
+                    help="skip the unstructured-mesh Newton line (native AMG)")
     ap.add_argument("--newton-n", type=int, default=100)
     ap.add_argument("--no-optionb", action="store_true", help="skip the option-B (shared-DOF) line")
     ap.add_argument("--no-host", action="store_true", help="skip the host-buffer drop-in line")
@@ -782,6 +814,12 @@ def main():
             secondary.append(newton_secondary(args.newton_n))
         except Exception as e:  # report, never hide
             secondary.append({"workload": "hex27-totlag-newton", "error": repr(e)})
+    if rank == 0 and world == 1 and not args.no_amg:
+        torch.cuda.empty_cache()
+        try:
+            secondary.append(amg_newton_secondary(args.n))
+        except Exception as e:  # report, never hide
+            secondary.append({"workload": "hex8-renumbered-newton-amg", "error": repr(e)})
     if secondary:
         out["secondary"] = secondary
     if rank == 0:

@@ -15,7 +15,7 @@ rc=$?
 echo "bench rc=$rc"; cat gpurun_out/bench_$TAG.json; tail -3 gpurun_out/bench_$TAG.err
 if [ $rc -ne 0 ]; then exit $rc; fi
 export TMPDIR=/tmp
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --no-newton > "$GRAFT_REPO_ROOT/gpurun_out/bench_prof_$TAG.json" 2> "$GRAFT_REPO_ROOT/gpurun_out/bench_prof_$TAG.err"
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --no-newton --no-amg > "$GRAFT_REPO_ROOT/gpurun_out/bench_prof_$TAG.json" 2> "$GRAFT_REPO_ROOT/gpurun_out/bench_prof_$TAG.err"
 rc=$?
 echo "rocprof rc=$rc"
 if [ $rc -ne 0 ]; then exit $rc; fi
