@@ -108,7 +108,8 @@ struct SweepShared {
   // lane k + 8, read by the U-side lane k of the next layer in the same instruction that precedes
   // the next write (LDS operations of a wavefront complete in order): one buffer suffices.
   // [column][in-plane neighbour (dy+1)*3 + dx+1][3x3 | TSI: k_ST 3 | k_TS 3 | k_TT 1]
-  double hold[TX * TY][9][TSI ? 16 : 9];
+  // (TSI rows padded to 18 doubles: with 16 every (column, t) record started on the same bank)
+  double hold[TX * TY][9][TSI ? 18 : 9];
 };
 
 __device__ inline int ring(int p) { return (p % 3 + 3) % 3; }
