@@ -34,7 +34,8 @@ ap.add_argument("--mg", action="store_true",
                 help="geometric multigrid preconditioned flexible CG (4c_amd/multigrid.py)")
 ap.add_argument("--mg-nu", type=int, default=2, help="Chebyshev degree of the MG smoother")
 ap.add_argument("--mg-coarse-rtol", type=float, default=1e-2)
-ap.add_argument("--mg-ratio", type=float, default=20.0)
+ap.add_argument("--mg-ratio", type=float, default=None,
+                help="Chebyshev eigenvalue ratio (default: the solver's own)")
 ap.add_argument("--mg-mixed", action="store_true", help="FP32 copy of K in the fine smoother")
 ap.add_argument("--amg", action="store_true",
                 help="smoothed-aggregation AMG preconditioned flexible CG (4c_amd/amg.py)")
@@ -121,15 +122,17 @@ if a.mg:
     t_mg = time.perf_counter()
     mg = importlib.import_module("4c_amd.multigrid").Multigrid(
         mesh, ev, lambda m: np.isclose(m.node_x[:, 0], 0.0), 210.0, 0.3, nu=a.mg_nu,
-        coarse_rtol=a.mg_coarse_rtol, ratio=a.mg_ratio, mixed=a.mg_mixed)
+        coarse_rtol=a.mg_coarse_rtol, mixed=a.mg_mixed,
+        **({"ratio": a.mg_ratio} if a.mg_ratio else {}))
     print(f"multigrid setup {time.perf_counter() - t_mg:.1f} s: {json.dumps(mg.describe())}",
           file=sys.stderr, flush=True)
     t_setup = time.perf_counter() - t0
 if a.amg or a.amg_native:
     t_mg = time.perf_counter()
     amg_mod = importlib.import_module("4c_amd.amg")
-    mg = (amg_mod.NativeAMG(mesh, ev, dbc, nu=a.mg_nu, ratio=a.mg_ratio) if a.amg_native
-          else amg_mod.AMG(mesh, ev, dbc, nu=a.mg_nu, ratio=a.mg_ratio))
+    kw = {"ratio": a.mg_ratio} if a.mg_ratio else {}
+    mg = (amg_mod.NativeAMG(mesh, ev, dbc, nu=a.mg_nu, **kw) if a.amg_native
+          else amg_mod.AMG(mesh, ev, dbc, nu=a.mg_nu, **kw))
     t_amg_setup = time.perf_counter() - t_mg
     print(f"AMG setup (host graph) {t_amg_setup:.1f} s: {json.dumps(mg.describe())}",
           file=sys.stderr, flush=True)
