@@ -436,13 +436,24 @@ class NativeAMG:
             out.append({"level": l, "dofs": d.value, "blocks": b.value, "lmax": lm.value})
         return out
 
-    def solve(self, K, b, x, rtol, max_iter=1000):
+    def setup(self, K):
+        """Numeric setup for the tangent K (fcg_amg_setup)."""
         L = fcg.lib()
+        s = ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+        rc = L.fcg_amg_setup(self._h, _vp(K), s)
+        if rc != 0:
+            raise fcg.FcgError(rc, L.fcg_amg_last_error(self._h).decode())
+        self.setup_ms.append(L.fcg_amg_setup_ms(self._h))
+
+    def solve(self, K, b, x, rtol, max_iter=1000, setup=True):
+        """K x = b from x = 0; setup=False iterates on the last setup (a constant operator)."""
+        L = fcg.lib()
+        if setup:
+            self.setup(K)
         it, rel = ctypes.c_int(0), ctypes.c_double(0.0)
         s = ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
-        rc = L.fcg_amg_solve(self._h, _vp(K), _vp(b), _vp(x), float(rtol), int(max_iter),
-                             ctypes.byref(it), ctypes.byref(rel), s)
-        self.setup_ms.append(L.fcg_amg_setup_ms(self._h))
+        rc = L.fcg_amg_iterate(self._h, _vp(K), _vp(b), _vp(x), float(rtol), int(max_iter),
+                               ctypes.byref(it), ctypes.byref(rel), s)
         if rc != 0:
             raise fcg.FcgError(rc, L.fcg_amg_last_error(self._h).decode())
         return it.value, rel.value

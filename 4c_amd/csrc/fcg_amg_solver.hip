@@ -179,6 +179,7 @@ struct fcg_amg {
   std::string last_error;
   std::vector<void*> allocs;
   double setup_ms = 0.0;
+  bool ready = false;  // a numeric setup has been made (fcg_amg_setup)
 };
 
 namespace fcg_amgs {
@@ -722,13 +723,10 @@ int fcg_amg_create(fcg_ctx* ctx, const int64_t* rowptr, const int32_t* col_lid,
   return FCG_OK;
 }
 
-int fcg_amg_solve(fcg_amg* h, const double* d_K_vals, const double* d_b_row, double* d_x_row,
-    double rtol, int max_iter, int* iterations, double* rel_residual, void* stream)
+int fcg_amg_setup(fcg_amg* h, const double* d_K_vals, void* stream)
 {
   using namespace fcg_amgs;
-  if (!h || !d_K_vals || !d_b_row || !d_x_row || !(rtol >= 0.0) || max_iter < 0) return FCG_ERR_ARG;
-  int it = 0;
-  double rel = 0.0;
+  if (!h || !d_K_vals) return FCG_ERR_ARG;
   try
   {
     ck(hipSetDevice(h->device), "hipSetDevice");
@@ -745,6 +743,34 @@ int fcg_amg_solve(fcg_amg* h, const double* d_K_vals, const double* d_b_row, dou
     h->setup_ms = ms;
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
+    h->ready = true;
+  }
+  catch (const Fail& f)
+  {
+    h->ready = false;
+    h->last_error = f.msg;
+    h->ctx->last_error = f.msg;
+    return f.code;
+  }
+  return FCG_OK;
+}
+
+int fcg_amg_iterate(fcg_amg* h, const double* d_K_vals, const double* d_b_row, double* d_x_row,
+    double rtol, int max_iter, int* iterations, double* rel_residual, void* stream)
+{
+  using namespace fcg_amgs;
+  if (!h || !d_K_vals || !d_b_row || !d_x_row || !(rtol >= 0.0) || max_iter < 0) return FCG_ERR_ARG;
+  if (!h->ready)
+  {
+    h->last_error = "fcg_amg_iterate: no numeric setup (call fcg_amg_setup first)";
+    return FCG_ERR_ARG;
+  }
+  int it = 0;
+  double rel = 0.0;
+  try
+  {
+    ck(hipSetDevice(h->device), "hipSetDevice");
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->ctx->stream;
     run_fcg(h, d_K_vals, d_b_row, d_x_row, rtol, max_iter, &it, &rel, s);
   }
   catch (const Fail& f)
@@ -758,6 +784,17 @@ int fcg_amg_solve(fcg_amg* h, const double* d_K_vals, const double* d_b_row, dou
   if (iterations) *iterations = it;
   if (rel_residual) *rel_residual = rel;
   return FCG_OK;
+}
+
+int fcg_amg_solve(fcg_amg* h, const double* d_K_vals, const double* d_b_row, double* d_x_row,
+    double rtol, int max_iter, int* iterations, double* rel_residual, void* stream)
+{
+  if (iterations) *iterations = 0;
+  if (rel_residual) *rel_residual = 0.0;
+  if (!h || !d_K_vals || !d_b_row || !d_x_row || !(rtol >= 0.0) || max_iter < 0) return FCG_ERR_ARG;
+  const int rc = fcg_amg_setup(h, d_K_vals, stream);
+  if (rc != FCG_OK) return rc;
+  return fcg_amg_iterate(h, d_K_vals, d_b_row, d_x_row, rtol, max_iter, iterations, rel_residual, stream);
 }
 
 int fcg_amg_level_info(const fcg_amg* h, int level, int64_t* dofs, int64_t* blocks, double* lmax)

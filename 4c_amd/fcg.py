@@ -131,7 +131,7 @@ EXPORTS = ["fcg_create", "fcg_destroy", "fcg_last_error", "fcg_evaluate", "fcg_e
            "fcg_bsr_block_jacobi_setup", "fcg_bsr_block_jacobi_apply", "fcg_amg_smooth_prolongator",
            "fcg_bsr_to_dense", "fcg_amg_default_options", "fcg_amg_create", "fcg_amg_solve",
            "fcg_amg_levels", "fcg_amg_level_info", "fcg_amg_setup_ms", "fcg_amg_last_error",
-           "fcg_amg_destroy"]
+           "fcg_amg_destroy", "fcg_amg_setup", "fcg_amg_iterate"]
 
 _lib = None
 FUNCT_FN = ctypes.CFUNCTYPE(ctypes.c_double, ctypes.c_int, _dp, ctypes.c_double, ctypes.c_void_p)
@@ -259,6 +259,8 @@ def lib():
     L.fcg_amg_create.argtypes = [vp, vp, vp, vp, i64, vp, ctypes.POINTER(FcgAmgOptions),
                                  ctypes.POINTER(vp)]
     L.fcg_amg_solve.argtypes = [vp, vp, vp, vp, c_dbl, c_int, ctypes.POINTER(c_int), _dp, vp]
+    L.fcg_amg_setup.argtypes = [vp, vp, vp]
+    L.fcg_amg_iterate.argtypes = [vp, vp, vp, vp, c_dbl, c_int, ctypes.POINTER(c_int), _dp, vp]
     L.fcg_amg_levels.argtypes = [vp]
     L.fcg_amg_level_info.argtypes = [vp, c_int, _i64p, _i64p, _dp]
     L.fcg_amg_setup_ms.argtypes = [vp]

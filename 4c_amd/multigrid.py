@@ -351,7 +351,9 @@ class Multigrid(CycleFCG):
 
     def __init__(self, fine_mesh, fine_ev, dbc_nodes, youngs, poisson, nu=2, min_intervals=4,
                  max_levels=8, ratio=10.0, boost=1.1, coarse_rtol=1e-2, coarse_max_iter=2000,
-                 mixed=False):
+                 mixed=False, coarse_solver="pcg"):
+        if coarse_solver not in ("pcg", "amg"):
+            raise ValueError(f"coarse_solver must be 'pcg' or 'amg', not {coarse_solver!r}")
         box = getattr(fine_mesh, "box", None)
         if box is None or getattr(fine_mesh, "nranks", 1) != 1:
             raise ValueError("Multigrid needs a single-rank GridGenerator box (fcg.BoxMesh)")
@@ -406,6 +408,14 @@ class Multigrid(CycleFCG):
             prev = m
         for lvl in self.levels[1:-1]:
             lvl.estimate_lmax()
+        # coarsest level: block-Jacobi PCG (fcg_pcg_solve), or the native smoothed-aggregation AMG
+        # set up once on it (its rediscretised linear operator does not change between tangents)
+        self.coarse_amg = None
+        if coarse_solver == "amg":
+            from .amg import NativeAMG
+            last = self.levels[-1]
+            self.coarse_amg = NativeAMG(last.mesh, last.ev, last.rows)
+            self.coarse_amg.setup(last.K)
 
     def describe(self):
         return [{"celltype": "hex27" if l.mesh.celltype == fcg.HEX27 else "hex8",
@@ -434,6 +444,9 @@ class Multigrid(CycleFCG):
         x.mul_(self.levels[l].mask)
 
     def _coarse_solve(self, lvl, b, x):
+        if self.coarse_amg is not None:
+            self.coarse_amg.solve(lvl.K, b, x, self.coarse_rtol, self.coarse_max_iter, setup=False)
+            return
         lvl.ev.pcg_solve(lvl.K, b, x, self.coarse_rtol, self.coarse_max_iter,
                          stream=torch.cuda.current_stream(self.dev))
 

@@ -291,6 +291,12 @@ int fcg_amg_create(fcg_ctx* ctx, const int64_t* rowptr, const int32_t* col_lid,
     fcg_amg** out);
 int fcg_amg_solve(fcg_amg* amg, const double* d_K_vals, const double* d_b_row, double* d_x_row,
     double rtol, int max_iter, int* iterations, double* rel_residual, void* stream);
+/* fcg_amg_solve = fcg_amg_setup (numeric setup for d_K_vals) + fcg_amg_iterate (the flexible CG
+ * on the last setup): a constant operator -- e.g. a linear coarse level of a geometric hierarchy
+ * -- is set up once and iterated many times. */
+int fcg_amg_setup(fcg_amg* amg, const double* d_K_vals, void* stream);
+int fcg_amg_iterate(fcg_amg* amg, const double* d_K_vals, const double* d_b_row, double* d_x_row,
+    double rtol, int max_iter, int* iterations, double* rel_residual, void* stream);
 int fcg_amg_levels(const fcg_amg* amg);
 int fcg_amg_level_info(const fcg_amg* amg, int level, int64_t* dofs, int64_t* blocks, double* lmax);
 double fcg_amg_setup_ms(const fcg_amg* amg);

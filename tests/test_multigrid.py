@@ -165,6 +165,28 @@ def test_newton_multigrid_matches_pcg(ct, n, kin, load, length, jitter, tol):
 
 
 @pytest.mark.gpu
+def test_multigrid_with_native_amg_coarsest_level():
+    """coarse_solver="amg": the coarsest hex8 level solved by the native AMG set up once."""
+    torch, dev = _dev()
+    mesh, clamp, dbc, fext = _cantilever(fcg.HEX27, 8, fcg.TOTLAG, -2.0)
+    res = {}
+    for cs in ("pcg", "amg"):
+        ev = fcg.Evaluator(mesh, kinematics=fcg.TOTLAG, youngs=E, poisson=NU)
+        mg = mgm.Multigrid(mesh, ev, clamp, E, NU, min_intervals=2, coarse_solver=cs)
+        nt = newton.StaticNewton(ev, fext, dbc, tol_res=1e-10 * np.linalg.norm(fext), tol_inc=1e-9,
+                                 lin_rtol=1e-10, linear_solver=mg)
+        res[cs] = (nt.solve().cpu().numpy(), [h.get("lin_iter") for h in nt.history])
+        if mg.coarse_amg is not None:
+            mg.coarse_amg.close()
+        ev.close()
+    (u0, it0), (u1, it1) = res["pcg"], res["amg"]
+    assert np.linalg.norm(u1 - u0) <= 1e-8 * np.linalg.norm(u0)
+    assert sum(i or 0 for i in it1) <= 1.5 * sum(i or 0 for i in it0), (it0, it1)
+    with pytest.raises(ValueError):
+        mgm.Multigrid(mesh, None, clamp, E, NU, coarse_solver="lu")
+
+
+@pytest.mark.gpu
 def test_stale_lmax_restarts_and_dirichlet_mismatch_raises():
     """a too-low kept lambda_max estimate is re-estimated and the solve restarted (the
     restart path), and a multigrid mask that disagrees with the Newton's Dirichlet rows is refused."""
