@@ -1,7 +1,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 2
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests_r02_v4.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests_${TAG:-r02_v5}.log 2>&1
 rc=$?
-echo "pytest rc=$rc"; tail -5 gpurun_out/gpu_tests_r02_v4.log
+echo "pytest rc=$rc"; tail -5 gpurun_out/gpu_tests_${TAG:-r02_v5}.log
 exit $rc
