@@ -14,6 +14,7 @@ u = 1e-3 (sin2piX cospiY, sinpiY cos2piZ, sin2piZ cospiX), StVK E=210 nu=0.3.
 """
 
 import argparse
+import glob
 import json
 import os
 import platform
@@ -695,7 +696,8 @@ def main():
     achieved = ALG_BYTES_PER_ELE * n_row_ele / (ms_kern * 1e-3) / 1e9
     flops = ALG_FLOP_PER_ELE * n_row_ele / (ms_kern * 1e-3) / 1e12
     traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_r01.json")
+    # the newest committed PMC pass of this kernel (tools/pmc.sh + tools/pmc_traffic.py)
+    pmc_path = max(glob.glob(os.path.join(ROOT, "profiles", "pmc_r*.json")) or [""])
     if os.path.exists(pmc_path):
         try:
             pmc = json.load(open(pmc_path))
@@ -750,6 +752,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
+            "traffic_source": os.path.basename(pmc_path) if traffic is not None else None,
             "alg_bytes_per_element": ALG_BYTES_PER_ELE,
             "elements_per_launch": n_row_ele,
             "ms_element_kernel": ms_el,
