@@ -334,11 +334,13 @@ __global__ __launch_bounds__(64, 2) void gather_h8_kernel(GatherArgs A)
       }
       else
       {
-        // N_XYZ of node a only (stage 3 rebuilds the others from J^-1)
-        const int ix = ((a & 3) == 1 || (a & 3) == 2), iy = (a & 3) >= 2, iz = a >= 4;
-        const double d0 = ix ? pyz[iy][iz] : -pyz[iy][iz];
-        const double d1 = iy ? pxz[ix][iz] : -pxz[ix][iz];
-        const double d2 = iz ? pxy[ix][iy] : -pxy[ix][iy];
+        // N_XYZ of node a only (stage 3 rebuilds the others from J^-1); a is a runtime index, so
+        // the factors are selected, not looked up (an indexed private array lives in scratch)
+        const bool ix = ((a & 3) == 1 || (a & 3) == 2), iy = (a & 3) >= 2, iz = a >= 4;
+        const double ex = ix ? xp : xm, ey = iy ? yp : ym, ez = iz ? zp : zm;
+        const double d0 = (ix ? 0.125 : -0.125) * ey * ez;
+        const double d1 = (iy ? 0.125 : -0.125) * ex * ez;
+        const double d2 = (iz ? 0.125 : -0.125) * ex * ey;
         na[0] = J[0] * d0 + J[3] * d1 + J[6] * d2;
         na[1] = J[1] * d0 + J[4] * d1 + J[7] * d2;
         na[2] = J[2] * d0 + J[5] * d1 + J[8] * d2;
