@@ -38,6 +38,55 @@ __global__ __launch_bounds__(256) void triad_kernel(const double* __restrict__ b
   }
 }
 
+// copy: U 16-byte pieces per lane in flight, all loads before the stores; NT selects
+// non-temporal stores
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void copy_kernel(const double2* __restrict__ b,
+    double2* __restrict__ a, int64_t n2)
+{
+  const int64_t step = blockDim.x;
+  const int64_t stride = int64_t(gridDim.x) * step * U;
+  for (int64_t i = int64_t(blockIdx.x) * step * U + threadIdx.x; i < n2; i += stride)
+  {
+    double2 bb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) bb[u] = b[i + u * step];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+    {
+      if (NT)
+      {
+        __builtin_nontemporal_store(bb[u].x, &a[i + u * step].x);
+        __builtin_nontemporal_store(bb[u].y, &a[i + u * step].y);
+      }
+      else
+        a[i + u * step] = bb[u];
+    }
+  }
+}
+
+// write-only fill, U 16-byte stores per lane and iteration
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void fill_kernel(double2* __restrict__ a, double v, int64_t n2)
+{
+  const int64_t step = blockDim.x;
+  const int64_t stride = int64_t(gridDim.x) * step * U;
+  for (int64_t i = int64_t(blockIdx.x) * step * U + threadIdx.x; i < n2; i += stride)
+  {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+    {
+      if (NT)
+      {
+        __builtin_nontemporal_store(v, &a[i + u * step].x);
+        __builtin_nontemporal_store(v, &a[i + u * step].y);
+      }
+      else
+        a[i + u * step] = double2{v, v};
+    }
+  }
+}
+
 // NCH independent FMA chains per lane; the result is stored so nothing is dead code
 constexpr int NCH = 16;
 __global__ __launch_bounds__(256) void fma_kernel(double* out, int iters, double x)
@@ -146,6 +195,42 @@ extern "C" int fcg_measure_peaks(int device, double* hbm_triad_gbs, double* fp64
     if (hipStreamSynchronize(s) != hipSuccess || hipGetLastError() != hipSuccess) rc = FCG_ERR_DEVICE;
   }
   for (double* p : {a, b, c, out})
+    if (p) (void)hipFree(p);
+  (void)hipStreamDestroy(s);
+  return rc;
+}
+
+extern "C" int fcg_measure_hbm(int device, double* copy_gbs, double* write_gbs)
+{
+  if (hipSetDevice(device) != hipSuccess) return FCG_ERR_DEVICE;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return FCG_ERR_DEVICE;
+  const int cus = std::max(1, prop.multiProcessorCount);
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return FCG_ERR_DEVICE;
+  int rc = FCG_OK;
+  // 2 x 2 GiB: far beyond the 256 MB Infinity Cache
+  const int64_t n2 = int64_t(1) << 27;  // double2 elements = 2 GiB
+  double2 *a = nullptr, *b = nullptr;
+  if (hipMalloc(&a, n2 * 16) != hipSuccess || hipMalloc(&b, n2 * 16) != hipSuccess) rc = FCG_ERR_DEVICE;
+  if (rc == FCG_OK)
+  {
+    (void)hipMemsetAsync(b, 0, n2 * 16, s);
+    float mc = 1e30f, mw = 1e30f;
+    for (int g : {4, 8, 16, 32})
+    {
+      const dim3 grid(cus * g), blk(256);
+      mc = std::min(mc, time_ms(s, 10, [&] { hipLaunchKernelGGL((copy_kernel<4, false>), grid, blk, 0, s, b, a, n2); }));
+      mc = std::min(mc, time_ms(s, 10, [&] { hipLaunchKernelGGL((copy_kernel<4, true>), grid, blk, 0, s, b, a, n2); }));
+      mc = std::min(mc, time_ms(s, 10, [&] { hipLaunchKernelGGL((copy_kernel<2, false>), grid, blk, 0, s, b, a, n2); }));
+      mw = std::min(mw, time_ms(s, 10, [&] { hipLaunchKernelGGL((fill_kernel<4, false>), grid, blk, 0, s, a, 1.0, n2); }));
+      mw = std::min(mw, time_ms(s, 10, [&] { hipLaunchKernelGGL((fill_kernel<4, true>), grid, blk, 0, s, a, 1.0, n2); }));
+    }
+    if (copy_gbs) *copy_gbs = 2.0 * 16.0 * double(n2) / (mc * 1e-3) / 1e9;
+    if (write_gbs) *write_gbs = 16.0 * double(n2) / (mw * 1e-3) / 1e9;
+    if (hipStreamSynchronize(s) != hipSuccess || hipGetLastError() != hipSuccess) rc = FCG_ERR_DEVICE;
+  }
+  for (double2* p : {a, b})
     if (p) (void)hipFree(p);
   (void)hipStreamDestroy(s);
   return rc;

@@ -112,7 +112,7 @@ class FcgAmgOptions(ctypes.Structure):
 EXPORTS = ["fcg_create", "fcg_destroy", "fcg_last_error", "fcg_evaluate", "fcg_evaluate_device",
            "fcg_device_alloc", "fcg_device_free", "fcg_memcpy_h2d", "fcg_memcpy_d2h",
            "fcg_memset_device", "fcg_set_timing", "fcg_get_timing", "fcg_get_info",
-           "fcg_get_diagnostics", "fcg_measure_peaks", "fcg_spmv", "fcg_dirichlet_apply",
+           "fcg_get_diagnostics", "fcg_measure_peaks", "fcg_measure_hbm", "fcg_spmv", "fcg_dirichlet_apply",
            "fcg_pcg_solve", "fcg_spmv_f32", "fcg_block_jacobi_setup", "fcg_block_jacobi_apply", "fcg_node_transfer",
            "fcg_neumann_surface", "fcg_neumann_volume",
            "fcg_graph_build_device",
@@ -176,6 +176,7 @@ def lib():
     L.fcg_get_diagnostics.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
     L.fcg_spmv.argtypes = [vp, vp, vp, vp, vp]
     L.fcg_measure_peaks.argtypes = [ctypes.c_int, _dp, _dp, _dp]
+    L.fcg_measure_hbm.argtypes = [ctypes.c_int, _dp, _dp]
     L.fcg_dirichlet_apply.argtypes = [vp, ctypes.c_int64, vp, vp, vp, vp, vp]
     L.fcg_pcg_solve.argtypes = [vp, vp, vp, vp, ctypes.c_double, ctypes.c_int,
                                 ctypes.POINTER(ctypes.c_int), _dp, vp]
@@ -839,3 +840,12 @@ def measure_peaks(device=0):
     if rc != 0:
         raise FcgError(rc, "fcg_measure_peaks failed")
     return a.value, b.value, c.value
+
+
+def measure_hbm(device=0):
+    """fcg_measure_hbm: (16-byte copy GB/s, write-only fill GB/s) on `device`."""
+    a, b = ctypes.c_double(), ctypes.c_double()
+    rc = lib().fcg_measure_hbm(int(device), ctypes.byref(a), ctypes.byref(b))
+    if rc != 0:
+        raise FcgError(rc, "fcg_measure_hbm failed")
+    return a.value, b.value

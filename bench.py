@@ -642,7 +642,7 @@ def main():
     peaks = None
     if not args.peaks_after:
         try:
-            peaks = fcg.measure_peaks(dev.index)
+            peaks = fcg.measure_peaks(dev.index) + fcg.measure_hbm(dev.index)
         except Exception as e:  # report, never hide
             peaks = e
     # the kernel's own duration (hipEvents on its launch stream) from a separate pass of K steps,
@@ -681,7 +681,7 @@ def main():
     t_el, t_as = kernel_timing_pass()
     if peaks is None:
         try:
-            peaks = fcg.measure_peaks(dev.index)
+            peaks = fcg.measure_peaks(dev.index) + fcg.measure_hbm(dev.index)
         except Exception as e:  # report, never hide
             peaks = e
     elapsed = _ctl_max(t1 - t0, world)
@@ -776,11 +776,14 @@ def main():
         try:
             if isinstance(peaks, Exception):
                 raise peaks
-            triad, valu, mfma = peaks
+            triad, valu, mfma, copy, write = peaks
             fp64_meas = max(valu, mfma)
+            hbm_best = max(triad, copy, write)
             out["roofline"]["measured_peaks"] = {
-                "hbm_triad_gbs": triad, "fp64_valu_tflops": valu, "fp64_mfma_tflops": mfma,
+                "hbm_triad_gbs": triad, "hbm_copy_gbs": copy, "hbm_write_only_gbs": write,
+                "fp64_valu_tflops": valu, "fp64_mfma_tflops": mfma,
                 "hbm_frac_vs_triad": achieved / triad if triad > 0 else None,
+                "hbm_frac_vs_best_measured": achieved / hbm_best if hbm_best > 0 else None,
                 "fp64_frac_vs_measured": flops / fp64_meas if fp64_meas > 0 else None}
         except Exception as e:  # report, never hide
             out["roofline"]["measured_peaks"] = {"error": repr(e)}

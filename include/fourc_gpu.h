@@ -171,6 +171,12 @@ int fcg_get_info(const fcg_ctx* ctx, fcg_info* info);
 int fcg_measure_peaks(int device, double* hbm_triad_gbs, double* fp64_valu_tflops,
     double* fp64_mfma_tflops);
 
+/* The HBM patterns beside the triad (GB/s, best over in-flight depths, grid sizes and store
+ * policies): a 16-byte-per-lane copy of 2 GiB (read + write, the pattern of the guide's measured
+ * 6.29 TB/s) and a write-only fill of 2 GiB (the pattern of the assembly's K stores).  Outputs may
+ * be NULL. */
+int fcg_measure_hbm(int device, double* copy_gbs, double* write_gbs);
+
 /* Diagnostics only: with FCG_STAMPS=1 in the environment at fcg_create, the fused kernel sums
  * per-phase cycle counts (s_memtime, thread 0 of every workgroup) into 8 counters: commit,
  * Gauss-point stage, node-row stage, accumulation, flush, workgroups (index 5).  Returns the number of
