@@ -8,8 +8,10 @@ mkdir -p gpurun_out
 for rep in 1 2; do
   for v in "$@"; do
     if [ "$v" = default ]; then unset FCG_LIB; else export FCG_LIB=$v; fi
-    r=$(timeout -k 10 120 python tools/eval_timing.py --n 100 --reps 60 | tail -1) || exit 1
-    echo "$v linear $(echo "$r" | python3 -c 'import json,sys; d=json.load(sys.stdin); print(round(d["ms_evaluate"],4))')"
+    if [ -z "$NOLIN" ]; then
+      r=$(timeout -k 10 120 python tools/eval_timing.py --n 100 --reps 60 | tail -1) || exit 1
+      echo "$v linear $(echo "$r" | python3 -c 'import json,sys; d=json.load(sys.stdin); print(round(d["ms_evaluate"],4))')"
+    fi
     if [ -n "$TSI" ]; then
       r=$(timeout -k 10 180 python tools/tsi_bench.py --reps 20 | tail -1) || exit 1
       echo "$v tsi_fused $(echo "$r" | python3 -c 'import json,sys; d=json.load(sys.stdin); print(round(d["ms_fused"],4))')"
