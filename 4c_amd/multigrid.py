@@ -232,6 +232,11 @@ class CycleFCG:
     _prepare(K) (per-tangent setup), _restrict(l, r, b_coarse), _prolong(l, x_coarse, x) (adds
     into x) and _coarse_solve(level, b, x); nu, ratio, boost, trace and dev as in Multigrid."""
 
+    # post-smoothing on the finest level (False: the V-cycle pre-smooths only there -- a
+    # nonsymmetric preconditioner, which the flexible CG's Polak-Ribiere beta admits; it saves
+    # the fine level's two post-smoothing SpMVs of the five an iteration costs)
+    fine_post = True
+
     # -- smoother ---------------------------------------------------------------------------
     def _cheb(self, lvl, b, x, x_zero):
         lmax = self.boost * lvl.lmax
@@ -269,7 +274,8 @@ class CycleFCG:
         self._restrict(l, lvl.r, c.b)
         self._vcycle(l + 1, c.b, c.x)
         self._prolong(l, c.x, x)
-        self._cheb(lvl, b, x, x_zero=False)
+        if l > 0 or self.fine_post:
+            self._cheb(lvl, b, x, x_zero=False)
 
     # -- outer solve ------------------------------------------------------------------------
     def solve(self, K, b, x, rtol, max_iter=1000):
@@ -351,7 +357,8 @@ class Multigrid(CycleFCG):
 
     def __init__(self, fine_mesh, fine_ev, dbc_nodes, youngs, poisson, nu=2, min_intervals=4,
                  max_levels=8, ratio=10.0, boost=1.1, coarse_rtol=1e-2, coarse_max_iter=2000,
-                 mixed=False, coarse_solver="pcg"):
+                 mixed=False, coarse_solver="pcg", fine_post=True):
+        self.fine_post = bool(fine_post)
         if coarse_solver not in ("pcg", "amg"):
             raise ValueError(f"coarse_solver must be 'pcg' or 'amg', not {coarse_solver!r}")
         box = getattr(fine_mesh, "box", None)

@@ -37,6 +37,8 @@ ap.add_argument("--mg-coarse-rtol", type=float, default=1e-2)
 ap.add_argument("--mg-ratio", type=float, default=None,
                 help="Chebyshev eigenvalue ratio (default: the solver's own)")
 ap.add_argument("--mg-mixed", action="store_true", help="FP32 copy of K in the fine smoother")
+ap.add_argument("--mg-no-fine-post", action="store_true",
+                help="no post-smoothing on the finest level (pre-smoothing V-cycle there)")
 ap.add_argument("--mg-coarse", default="pcg", choices=["pcg", "amg"],
                 help="coarsest-level solver of the geometric multigrid")
 ap.add_argument("--amg", action="store_true",
@@ -125,6 +127,7 @@ if a.mg:
     mg = importlib.import_module("4c_amd.multigrid").Multigrid(
         mesh, ev, lambda m: np.isclose(m.node_x[:, 0], 0.0), 210.0, 0.3, nu=a.mg_nu,
         coarse_rtol=a.mg_coarse_rtol, mixed=a.mg_mixed, coarse_solver=a.mg_coarse,
+        fine_post=not a.mg_no_fine_post,
         **({"ratio": a.mg_ratio} if a.mg_ratio else {}))
     print(f"multigrid setup {time.perf_counter() - t_mg:.1f} s: {json.dumps(mg.describe())}",
           file=sys.stderr, flush=True)
