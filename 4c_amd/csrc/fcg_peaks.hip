@@ -150,7 +150,11 @@ float time_ms(hipStream_t s, int reps, F launch)
 extern "C" int fcg_measure_peaks(int device, double* hbm_triad_gbs, double* fp64_valu_tflops,
     double* fp64_mfma_tflops)
 {
-  if (hipSetDevice(device) != hipSuccess) return FCG_ERR_DEVICE;
+  if (hipSetDevice(device) != hipSuccess)
+  {
+    (void)hipGetLastError();  // do not leave the error for the caller's next HIP call
+    return FCG_ERR_DEVICE;
+  }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) return FCG_ERR_DEVICE;
   const int cus = std::max(1, prop.multiProcessorCount);
@@ -202,7 +206,11 @@ extern "C" int fcg_measure_peaks(int device, double* hbm_triad_gbs, double* fp64
 
 extern "C" int fcg_measure_hbm(int device, double* copy_gbs, double* write_gbs)
 {
-  if (hipSetDevice(device) != hipSuccess) return FCG_ERR_DEVICE;
+  if (hipSetDevice(device) != hipSuccess)
+  {
+    (void)hipGetLastError();  // do not leave the error for the caller's next HIP call
+    return FCG_ERR_DEVICE;
+  }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) return FCG_ERR_DEVICE;
   const int cus = std::max(1, prop.multiProcessorCount);

@@ -592,6 +592,16 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
       // the part held by lane k + 8 (same role, D side) since the previous layer.  TSI: Tv holds
       // the block's k_ST / k_TS / k_TT entries (tsi_block), treated the same way.
       auto emit = [&](int act, int t, double* Kb, double* Tv) {
+        // the block's record fields first, all four reads before any branch: one LDS round trip,
+        // which the residual and hold work below overlaps (read one by one behind the early
+        // returns, each waited for in turn)
+        const bool to_l1 = act == kActWriteL1;
+        const uint32_t* rec = to_l1 ? recL1 : recL;
+        const int32_t row0 = WANT_K ? int32_t(rec[PR_ROW0 + c]) : -1;
+        const uint16_t pos = WANT_K ? reinterpret_cast<const uint16_t*>(rec + PR_NPOS)[27 * c + t] : 0;
+        const uint32_t base_lo = WANT_K ? rec[PR_BASE + 2 * c] : 0u;
+        const uint32_t base_hi = WANT_K ? rec[PR_BASE + 2 * c + 1] : 0u;
+        const int32_t len32 = WANT_K ? int32_t(rec[PR_LEN + c]) : 0;
         if (KIN == 0)
         {
           const int dx = t % 3 - 1, dy = (t / 3) % 3 - 1, dz = t / 9 - 1;
@@ -639,15 +649,9 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
           }
         }
         if (act == kActHold || !WANT_K) return;
-        const bool to_l1 = act == kActWriteL1;
-        if (!(to_l1 ? wl1 : wl)) return;
-        const uint32_t* rec = to_l1 ? recL1 : recL;
-        const int32_t row0 = int32_t(rec[PR_ROW0 + c]);
-        if (row0 < 0) return;
-        const uint16_t pos = reinterpret_cast<const uint16_t*>(rec + PR_NPOS)[27 * c + t];
-        if (pos == 0xFFFF) return;
-        const int64_t base = int64_t(rec[PR_BASE + 2 * c]) | (int64_t(rec[PR_BASE + 2 * c + 1]) << 32);
-        const int64_t len = int32_t(rec[PR_LEN + c]);
+        if (!(to_l1 ? wl1 : wl) || row0 < 0 || pos == 0xFFFF) return;
+        const int64_t base = int64_t(base_lo) | (int64_t(base_hi) << 32);
+        const int64_t len = len32;
         double* dst = A.K + base + pos;
 #pragma unroll
         for (int r = 0; r < 3; ++r)
@@ -722,7 +726,7 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
         for (int i = 0; i < 9; ++i)
         {
           const double o = dpp_f64<kDppXor1>(Kb[i]);
-          if (pair == kPairRecv) Kb[i] += o;
+          Kb[i] = pair == kPairRecv ? Kb[i] + o : Kb[i];  // a select, not a branch per entry
         }
         if (TSI)
         {
@@ -731,7 +735,7 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
           for (int i = 0; i < 7; ++i)
           {
             const double o = dpp_f64<kDppXor1>(Tv[i]);
-            if (pair == kPairRecv) Tv[i] += o;
+            Tv[i] = pair == kPairRecv ? Tv[i] + o : Tv[i];
           }
         }
         if (pair != kPairGive) emit(int((vis1 >> 21) & 7), int((vis1 >> 11) & 31), Kb, Tv);

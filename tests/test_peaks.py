@@ -23,7 +23,3 @@ def test_measured_peaks_are_plausible():
     for tfs in (valu, mfma):
         assert 1.0 < tfs < FP64_SPEC_TFS * 1.05, (valu, mfma)
 
-
-def test_measure_hbm_rejects_a_missing_device():
-    with pytest.raises(fcg.FcgError):
-        fcg.measure_hbm(1 << 20)

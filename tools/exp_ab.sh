@@ -5,7 +5,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 2
 mkdir -p gpurun_out
-for rep in 1 2; do
+for rep in $(seq ${ROUNDS:-2}); do
   for v in "$@"; do
     if [ "$v" = default ]; then unset FCG_LIB; else export FCG_LIB=$v; fi
     if [ -z "$NOLIN" ]; then
