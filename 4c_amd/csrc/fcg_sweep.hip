@@ -695,14 +695,23 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
       double acc1[NACC], acc2[NACC];
 #pragma unroll
       for (int i = 0; i < NACC; ++i) acc1[i] = acc2[i] = 0.0;
-      // the two element visits of this lane; acc2 is finished after a visit when flush2 is set
+      // the two element visits of this lane; acc2 is finished after a visit when flush2 is set.
+      // Without TSI both visits' negative-fac masks are read up front (one LDS round trip instead
+      // of one ahead of each visit's branch; the TSI instantiation has no registers to spare).
+      auto slot_of = [&](uint32_t w) { return (cx + int(w & 1)) + EXN * (cy + int((w >> 1) & 1)); };
+      uint32_t nm_pre[2] = {0u, 0u};
+      if constexpr (!TSI)
+      {
+        nm_pre[0] = sh.neg[slot_of(vis0)];
+        nm_pre[1] = sh.neg[slot_of(vis1)];
+      }
 #pragma unroll 1
       for (int v = 0; v < 2; ++v)
       {
         const uint32_t w = v == 0 ? vis0 : vis1;
-        const int q = w & 3, a = (w >> 2) & 7, b1 = (w >> 5) & 7, b2 = (w >> 8) & 7;
-        const int slot = (cx + (q & 1)) + EXN * (cy + (q >> 1));
-        const uint32_t nm = sh.neg[slot];
+        const int a = (w >> 2) & 7, b1 = (w >> 5) & 7, b2 = (w >> 8) & 7;
+        const int slot = slot_of(w);
+        const uint32_t nm = TSI ? sh.neg[slot] : (v == 0 ? nm_pre[0] : nm_pre[1]);
         if (nm == 0u)
           sweep_visit<KIN, false, TSI>(sh, slot, a, b1, b2, nm, acc1, acc2);
         else
@@ -779,6 +788,7 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
           f[2] += cc * (P[2] * t0 + P[5] * t1 + P[8] * t2);
         }
       }
+      const int32_t frow0 = int32_t(recL[PR_ROW0 + c]);  // read ahead of the butterfly
       double fp[NF];
 #pragma unroll
       for (int d = 0; d < NF; ++d)
@@ -795,7 +805,7 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
       }
       else if (k == 0 && wl)
       {
-        const int32_t row0 = int32_t(recL[PR_ROW0 + c]);
+        const int32_t row0 = frow0;
         if (row0 >= 0)
         {
 #pragma unroll

@@ -8,7 +8,7 @@ import time
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-fcg = importlib.import_module("4c_amd").fcg
+fcg = importlib.import_module("4c_amd").fcg  # FCG_LIB selects an A/B build
 halo = importlib.import_module("4c_amd.halo")
 m = fcg.BoxMesh(fcg.HEX8, (100, 100, 100), jitter=0.1, seed=20251015)
 ev = fcg.Evaluator(m, kinematics=fcg.LINEAR, youngs=210.0, poisson=0.3)
