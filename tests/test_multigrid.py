@@ -165,6 +165,23 @@ def test_newton_multigrid_matches_pcg(ct, n, kin, load, length, jitter, tol):
 
 
 @pytest.mark.gpu
+def test_multigrid_pre_smoothing_only_on_the_finest_level():
+    """fine_post=False: a nonsymmetric V-cycle (no fine post-smoothing), which the flexible CG
+    admits -- same Newton solution, every linear solve converged."""
+    torch, dev = _dev()
+    mesh, clamp, dbc, fext = _cantilever(fcg.HEX8, 8, fcg.TOTLAG, -2.0)
+    res = {}
+    for post in (True, False):
+        ev = fcg.Evaluator(mesh, kinematics=fcg.TOTLAG, youngs=E, poisson=NU)
+        mg = mgm.Multigrid(mesh, ev, clamp, E, NU, min_intervals=2, fine_post=post)
+        nt = newton.StaticNewton(ev, fext, dbc, tol_res=1e-10 * np.linalg.norm(fext), tol_inc=1e-9,
+                                 lin_rtol=1e-10, linear_solver=mg)
+        res[post] = nt.solve().cpu().numpy()
+        ev.close()
+    assert np.linalg.norm(res[False] - res[True]) <= 1e-8 * np.linalg.norm(res[True])
+
+
+@pytest.mark.gpu
 def test_multigrid_with_native_amg_coarsest_level():
     """coarse_solver="amg": the coarsest hex8 level solved by the native AMG set up once."""
     torch, dev = _dev()
