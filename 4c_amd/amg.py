@@ -253,6 +253,10 @@ class AMG(CycleFCG):
     mesh / ev: the single-rank discretization being solved (fcg.Discretization or BoxMesh and its
     Evaluator); dbc_rows: the Newton's Dirichlet rows (unit rows of K)."""
 
+    # _setup estimates lambda_max afresh for every tangent (same seed) and the prolongators
+    # depend on it: a retry would repeat the failed solve exactly, so fail at once
+    retry_lmax = False
+
     def __init__(self, mesh, ev, dbc_rows, nu=2, max_levels=10, coarse_max=3000, omega=4.0 / 3.0,
                  ratio=20.0, boost=1.1):
         info = ev.info

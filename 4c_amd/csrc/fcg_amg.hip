@@ -15,6 +15,7 @@
 #include <cstdint>
 
 #include "fourc_gpu.h"
+#include "fcg_status.hpp"
 
 namespace fcg_bsrk {
 
@@ -296,7 +297,7 @@ __global__ __launch_bounds__(kBlock) void bsr_to_dense_kernel(int64_t n,
   }
 }
 
-inline int status(hipError_t e) { return e == hipSuccess ? FCG_OK : FCG_ERR_DEVICE; }
+inline int status(hipError_t e) { return e == hipSuccess ? FCG_OK : fcg_device_error(); }
 
 }  // namespace fcg_bsrk
 
@@ -309,7 +310,7 @@ int fcg_bsr_spmv(int device, int br, int bc, int64_t n_brows, const int64_t* d_p
   using namespace fcg_bsrk;
   if (n_brows < 0 || (n_brows > 0 && (!d_ptr || !d_col || !d_vals || !d_x || !d_y))) return FCG_ERR_ARG;
   if (n_brows == 0) return FCG_OK;
-  if (hipSetDevice(device) != hipSuccess) return FCG_ERR_DEVICE;
+  if (!fcg_use_device(device)) return fcg_device_error();
   hipStream_t s = static_cast<hipStream_t>(stream);
   const dim3 g(blocks_for(n_brows * 8, kBlock)), b(kBlock);
   if (br == 3 && bc == 3)
@@ -335,7 +336,7 @@ int fcg_bsr_spgemm(int device, int br, int bk, int bc, int64_t n_brows, const in
                                       !d_b_vals || !d_c_ptr || !d_c_col || !d_c_vals)))
     return FCG_ERR_ARG;
   if (n_brows == 0) return FCG_OK;
-  if (hipSetDevice(device) != hipSuccess) return FCG_ERR_DEVICE;
+  if (!fcg_use_device(device)) return fcg_device_error();
   hipStream_t s = static_cast<hipStream_t>(stream);
   const dim3 g(blocks_for(n_brows * 16, kBlock)), b(kBlock);
 #define FCG_SPGEMM(R, K, C)                                                                        \
@@ -356,7 +357,7 @@ int fcg_bsr_transpose_values(int device, int br, int bc, int64_t nnzb, const int
   using namespace fcg_bsrk;
   if (nnzb < 0 || (nnzb > 0 && (!d_perm || !d_vals || !d_t_vals))) return FCG_ERR_ARG;
   if (nnzb == 0) return FCG_OK;
-  if (hipSetDevice(device) != hipSuccess) return FCG_ERR_DEVICE;
+  if (!fcg_use_device(device)) return fcg_device_error();
   hipStream_t s = static_cast<hipStream_t>(stream);
   const dim3 g(blocks_for(nnzb, kBlock)), b(kBlock);
   if (br == 3 && bc == 6)
@@ -374,7 +375,7 @@ int fcg_bsr_from_node_csr(int device, int64_t n_brows, const int64_t* d_rowptr,
   using namespace fcg_bsrk;
   if (n_brows < 0 || (n_brows > 0 && (!d_rowptr || !d_b_ptr || !d_K || !d_b_vals))) return FCG_ERR_ARG;
   if (n_brows == 0) return FCG_OK;
-  if (hipSetDevice(device) != hipSuccess) return FCG_ERR_DEVICE;
+  if (!fcg_use_device(device)) return fcg_device_error();
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(node_csr_to_bsr_kernel, dim3(blocks_for(n_brows * 16, kBlock)), dim3(kBlock), 0,
       s, n_brows, d_rowptr, d_b_ptr, d_K, d_b_vals);
@@ -388,10 +389,10 @@ int fcg_bsr_block_jacobi_setup(int device, int b, int64_t n_brows, const int64_t
   if (n_brows < 0 || !d_flag || (n_brows > 0 && (!d_ptr || !d_diag_idx || !d_vals || !d_dinv)))
     return FCG_ERR_ARG;
   if (n_brows == 0) return FCG_OK;
-  if (hipSetDevice(device) != hipSuccess) return FCG_ERR_DEVICE;
+  if (!fcg_use_device(device)) return fcg_device_error();
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipError_t he = hipMemsetAsync(d_flag, 0, sizeof(int32_t), s);
-  if (he != hipSuccess) return FCG_ERR_DEVICE;
+  if (he != hipSuccess) return fcg_device_error();
   const dim3 g(blocks_for(n_brows, kBlock)), bl(kBlock);
   if (b == 3)
     hipLaunchKernelGGL((bsr_block_inverse_kernel<3>), g, bl, 0, s, n_brows, d_ptr, d_diag_idx, d_vals, d_dinv, d_flag);
@@ -403,7 +404,7 @@ int fcg_bsr_block_jacobi_setup(int device, int b, int64_t n_brows, const int64_t
   int32_t bad = 0;
   if (he == hipSuccess) he = hipMemcpyAsync(&bad, d_flag, sizeof(bad), hipMemcpyDeviceToHost, s);
   if (he == hipSuccess) he = hipStreamSynchronize(s);
-  if (he != hipSuccess) return FCG_ERR_DEVICE;
+  if (he != hipSuccess) return fcg_device_error();
   return bad ? FCG_ERR_SINGULAR : FCG_OK;
 }
 
@@ -413,7 +414,7 @@ int fcg_bsr_block_jacobi_apply(int device, int b, int64_t n_brows, const double*
   using namespace fcg_bsrk;
   if (n_brows < 0 || (n_brows > 0 && (!d_dinv || !d_r || !d_z))) return FCG_ERR_ARG;
   if (n_brows == 0) return FCG_OK;
-  if (hipSetDevice(device) != hipSuccess) return FCG_ERR_DEVICE;
+  if (!fcg_use_device(device)) return fcg_device_error();
   hipStream_t s = static_cast<hipStream_t>(stream);
   const dim3 g(blocks_for(n_brows, kBlock)), bl(kBlock);
   if (b == 3)
@@ -434,7 +435,7 @@ int fcg_amg_smooth_prolongator(int device, int br, int64_t n_brows, const int64_
                                       !d_at || !d_p_vals)))
     return FCG_ERR_ARG;
   if (n_brows == 0) return FCG_OK;
-  if (hipSetDevice(device) != hipSuccess) return FCG_ERR_DEVICE;
+  if (!fcg_use_device(device)) return fcg_device_error();
   hipStream_t s = static_cast<hipStream_t>(stream);
   const dim3 g(blocks_for(n_brows, kBlock)), bl(kBlock);
   if (br == 3)
@@ -452,7 +453,7 @@ int fcg_bsr_to_dense(int device, int b, int64_t n_brows, const int64_t* d_ptr, c
   using namespace fcg_bsrk;
   if (n_brows < 0 || (n_brows > 0 && (!d_ptr || !d_col || !d_vals || !d_dense))) return FCG_ERR_ARG;
   if (n_brows == 0) return FCG_OK;
-  if (hipSetDevice(device) != hipSuccess) return FCG_ERR_DEVICE;
+  if (!fcg_use_device(device)) return fcg_device_error();
   hipStream_t s = static_cast<hipStream_t>(stream);
   const dim3 g(blocks_for(n_brows, kBlock)), bl(kBlock);
   if (b == 3)

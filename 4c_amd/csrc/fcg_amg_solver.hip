@@ -191,7 +191,11 @@ struct Fail {
 
 inline void ck(hipError_t e, const char* what)
 {
-  if (e != hipSuccess) throw Fail{FCG_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e)};
+  if (e != hipSuccess)
+  {
+    (void)hipGetLastError();  // leave no sticky status for the caller (fcg_status.hpp)
+    throw Fail{FCG_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e)};
+  }
 }
 inline void ck(int rc, const char* what)
 {

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "fourc_gpu.h"
+#include "fcg_status.hpp"
 
 struct fcg_comm {
   ncclComm_t nccl = nullptr;
@@ -157,7 +158,7 @@ __global__ __launch_bounds__(kBlock) void sum_partials_kernel(double* __restrict
   if (threadIdx.x == 0) *out = t;
 }
 
-int nccl_status(ncclResult_t r) { return r == ncclSuccess ? FCG_OK : FCG_ERR_DEVICE; }
+int nccl_status(ncclResult_t r) { return r == ncclSuccess ? FCG_OK : fcg_device_error(); }
 
 }  // namespace
 
@@ -167,7 +168,7 @@ int fcg_comm_unique_id(void* id)
 {
   if (!id) return FCG_ERR_ARG;
   ncclUniqueId u;
-  if (ncclGetUniqueId(&u) != ncclSuccess) return FCG_ERR_DEVICE;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return fcg_device_error();
   std::memcpy(id, &u, sizeof(u));
   return FCG_OK;
 }
@@ -176,7 +177,7 @@ int fcg_comm_create(const void* id, int nranks, int rank, int device, fcg_comm**
 {
   if (!id || !out || nranks < 1 || rank < 0 || rank >= nranks) return FCG_ERR_ARG;
   *out = nullptr;
-  if (hipSetDevice(device) != hipSuccess) return FCG_ERR_DEVICE;
+  if (!fcg_use_device(device)) return fcg_device_error();
   auto* c = new fcg_comm();
   c->nranks = nranks;
   c->rank = rank;
@@ -190,7 +191,7 @@ int fcg_comm_create(const void* id, int nranks, int rank, int device, fcg_comm**
   {
     c->nccl = nullptr;
     fcg_comm_destroy(c);
-    return FCG_ERR_DEVICE;
+    return fcg_device_error();
   }
   *out = c;
   return FCG_OK;
@@ -205,6 +206,15 @@ int fcg_comm_destroy(fcg_comm* c)
   if (c->d_scalar) (void)hipFree(c->d_scalar);
   if (c->h_scalar) (void)hipHostFree(c->h_scalar);
   delete c;
+  return FCG_OK;
+}
+
+int fcg_comm_size(const fcg_comm* c, int* nranks)
+{
+  if (!c || !nranks) return FCG_ERR_ARG;
+  int n = 0;
+  if (ncclCommCount(c->nccl, &n) != ncclSuccess) return fcg_device_error();
+  *nranks = n;
   return FCG_OK;
 }
 
@@ -236,7 +246,7 @@ int fcg_comm_alltoallv(const void* send_buf, const int64_t* send_counts, void* r
   if (he == hipSuccess) he = hipMalloc(&d_recv, std::max<int64_t>(1, nr * item_bytes));
   if (he == hipSuccess && ns)
     he = hipMemcpyAsync(d_send, send_buf, ns * item_bytes, hipMemcpyHostToDevice, c->stream);
-  int rc = he == hipSuccess ? FCG_OK : FCG_ERR_DEVICE;
+  int rc = he == hipSuccess ? FCG_OK : fcg_device_error();
   if (rc == FCG_OK)
   {
     int64_t so = 0, ro = 0;
@@ -253,14 +263,14 @@ int fcg_comm_alltoallv(const void* send_buf, const int64_t* send_counts, void* r
       ro += recv_counts[p];
     }
     const ncclResult_t r2 = ncclGroupEnd();
-    rc = (r == ncclSuccess && r2 == ncclSuccess) ? FCG_OK : FCG_ERR_DEVICE;
+    rc = (r == ncclSuccess && r2 == ncclSuccess) ? FCG_OK : fcg_device_error();
   }
   if (rc == FCG_OK && nr)
     rc = hipMemcpyAsync(recv_buf, d_recv, nr * item_bytes, hipMemcpyDeviceToHost, c->stream) ==
                  hipSuccess
              ? FCG_OK
-             : FCG_ERR_DEVICE;
-  if (hipStreamSynchronize(c->stream) != hipSuccess) rc = FCG_ERR_DEVICE;
+             : fcg_device_error();
+  if (hipStreamSynchronize(c->stream) != hipSuccess) rc = fcg_device_error();
   if (d_send) (void)hipFree(d_send);
   if (d_recv) (void)hipFree(d_recv);
   return rc;
@@ -312,10 +322,10 @@ int fcg_halo_create(const fcg_import_plan* p, int device, fcg_halo** out)
     else
       h->scatter_needed = true;
   }
-  if (hipSetDevice(device) != hipSuccess)
+  if (!fcg_use_device(device))
   {
     delete h;
-    return FCG_ERR_DEVICE;
+    return fcg_device_error();
   }
   hipError_t he = to_device(&h->permute_from, p->permute_from, p->n_permute);
   if (he == hipSuccess) he = to_device(&h->permute_to, p->permute_to, p->n_permute);
@@ -326,7 +336,7 @@ int fcg_halo_create(const fcg_import_plan* p, int device, fcg_halo** out)
   if (he != hipSuccess)
   {
     fcg_halo_destroy(h);
-    return FCG_ERR_DEVICE;
+    return fcg_device_error();
   }
   *out = h;
   return FCG_OK;
@@ -355,7 +365,7 @@ int fcg_halo_pack(fcg_halo* h, const double* d_u_row, double* d_u_col, double* d
   hipStream_t s = static_cast<hipStream_t>(stream);
   halo_local_kernel<<<grid_for(total), kBlock, 0, s>>>(d_u_row, d_u_col, h->n_same,
       h->permute_from, h->permute_to, h->n_permute, h->send_row, d_send, h->n_send);
-  return hipGetLastError() == hipSuccess ? FCG_OK : FCG_ERR_DEVICE;
+  return hipGetLastError() == hipSuccess ? FCG_OK : fcg_device_error();
 }
 
 int fcg_halo_unpack(fcg_halo* h, const double* d_recv, double* d_u_col, void* stream)
@@ -365,7 +375,7 @@ int fcg_halo_unpack(fcg_halo* h, const double* d_recv, double* d_u_col, void* st
   (void)hipSetDevice(h->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
   scatter_kernel<<<grid_for(h->n_recv), kBlock, 0, s>>>(d_recv, h->recv_col, d_u_col, h->n_recv);
-  return hipGetLastError() == hipSuccess ? FCG_OK : FCG_ERR_DEVICE;
+  return hipGetLastError() == hipSuccess ? FCG_OK : fcg_device_error();
 }
 
 int fcg_halo_import(fcg_halo* h, fcg_comm* c, const double* d_u_row, double* d_u_col, void* stream)
@@ -388,7 +398,7 @@ int fcg_halo_import(fcg_halo* h, fcg_comm* c, const double* d_u_row, double* d_u
     }
   }
   const ncclResult_t r2 = ncclGroupEnd();
-  if (r != ncclSuccess || r2 != ncclSuccess) return FCG_ERR_DEVICE;
+  if (r != ncclSuccess || r2 != ncclSuccess) return fcg_device_error();
   if (!h->scatter_needed) return FCG_OK;
   // peers with scattered ghost columns landed in h->recv: scatter those blocks
   for (int q = 0; q < h->nranks; ++q)
@@ -397,7 +407,7 @@ int fcg_halo_import(fcg_halo* h, fcg_comm* c, const double* d_u_row, double* d_u
     if (n == 0 || h->recv_first[q] >= 0) continue;
     scatter_kernel<<<grid_for(n), kBlock, 0, s>>>(h->recv + a, h->recv_col + a, d_u_col, n);
   }
-  return hipGetLastError() == hipSuccess ? FCG_OK : FCG_ERR_DEVICE;
+  return hipGetLastError() == hipSuccess ? FCG_OK : fcg_device_error();
 }
 
 int fcg_shared_create(const fcg_shared_plan* p, int device, fcg_shared** out)
@@ -408,7 +418,7 @@ int fcg_shared_create(const fcg_shared_plan* p, int device, fcg_shared** out)
   *out = nullptr;
   for (int64_t i = 0; i < p->n_local; ++i)
     if (p->row[i] < 0 || p->pos[i] < 0 || p->pos[i] >= p->n_global) return FCG_ERR_ARG;
-  if (hipSetDevice(device) != hipSuccess) return FCG_ERR_DEVICE;
+  if (!fcg_use_device(device)) return fcg_device_error();
   auto* s = new fcg_shared();
   s->device = device;
   s->n_global = p->n_global;
@@ -420,7 +430,7 @@ int fcg_shared_create(const fcg_shared_plan* p, int device, fcg_shared** out)
   if (he != hipSuccess)
   {
     fcg_shared_destroy(s);
-    return FCG_ERR_DEVICE;
+    return fcg_device_error();
   }
   *out = s;
   return FCG_OK;
@@ -443,10 +453,10 @@ int fcg_shared_pack(fcg_shared* s, const double* d_f, double* d_buf, void* strea
   if (s->n_global == 0) return FCG_OK;
   (void)hipSetDevice(s->device);
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (hipMemsetAsync(d_buf, 0, sizeof(double) * s->n_global, st) != hipSuccess) return FCG_ERR_DEVICE;
+  if (hipMemsetAsync(d_buf, 0, sizeof(double) * s->n_global, st) != hipSuccess) return fcg_device_error();
   if (s->n_local)
     shared_pack_kernel<<<grid_for(s->n_local), kBlock, 0, st>>>(d_f, s->row, s->pos, d_buf, s->n_local);
-  return hipGetLastError() == hipSuccess ? FCG_OK : FCG_ERR_DEVICE;
+  return hipGetLastError() == hipSuccess ? FCG_OK : fcg_device_error();
 }
 
 int fcg_shared_unpack(fcg_shared* s, const double* d_buf, double* d_f, void* stream)
@@ -456,7 +466,7 @@ int fcg_shared_unpack(fcg_shared* s, const double* d_buf, double* d_f, void* str
   (void)hipSetDevice(s->device);
   hipStream_t st = static_cast<hipStream_t>(stream);
   shared_unpack_kernel<<<grid_for(s->n_owned), kBlock, 0, st>>>(d_buf, s->row, s->pos, d_f, s->n_owned);
-  return hipGetLastError() == hipSuccess ? FCG_OK : FCG_ERR_DEVICE;
+  return hipGetLastError() == hipSuccess ? FCG_OK : fcg_device_error();
 }
 
 int fcg_shared_reduce(fcg_shared* s, fcg_comm* c, double* d_f, void* stream)
@@ -487,25 +497,25 @@ int fcg_norm2(fcg_comm* c, const double* d_x, int64_t n, void* stream, double* o
   else
   {
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return FCG_ERR_DEVICE;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return fcg_device_error();
     if (!local_dev[dev] && (hipMalloc(&local_dev[dev], sizeof(double) * (kNormBlocks + 1)) != hipSuccess ||
                                hipHostMalloc(&local_host[dev], sizeof(double)) != hipSuccess))
-      return FCG_ERR_DEVICE;
+      return fcg_device_error();
     d_part = local_dev[dev];
     h_res = local_host[dev];
   }
   const int nb = int(std::min<int64_t>(kNormBlocks, std::max<int64_t>(1, (n + kBlock - 1) / kBlock)));
   sumsq_kernel<<<nb, kBlock, 0, s>>>(d_x, n, d_part);
   sum_partials_kernel<<<1, kBlock, 0, s>>>(d_part, nb, d_part + kNormBlocks);
-  if (hipGetLastError() != hipSuccess) return FCG_ERR_DEVICE;
+  if (hipGetLastError() != hipSuccess) return fcg_device_error();
   if (c && c->nranks > 1 &&
       ncclAllReduce(d_part + kNormBlocks, d_part + kNormBlocks, 1, ncclFloat64, ncclSum, c->nccl, s) !=
           ncclSuccess)
-    return FCG_ERR_DEVICE;
+    return fcg_device_error();
   if (hipMemcpyAsync(h_res, d_part + kNormBlocks, sizeof(double), hipMemcpyDeviceToHost, s) !=
           hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
-    return FCG_ERR_DEVICE;
+    return fcg_device_error();
   *out = std::sqrt(*h_res);
   return FCG_OK;
 }

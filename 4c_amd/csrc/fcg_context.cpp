@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "fcg_internal.hpp"
+#include "fcg_status.hpp"
 #include "fcg_shape.hpp"
 
 namespace {
@@ -694,7 +695,7 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
   {
     set_create_error(std::string("HIP: ") + hipGetErrorString(he));
     delete ctx;
-    return FCG_ERR_DEVICE;
+    return fcg_device_error();
   }
   fcg::upload_constant_tables(d->celltype);
   fcg::DeviceMesh& m = ctx->mesh;
@@ -911,7 +912,7 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
   {
     set_create_error(std::string("HIP allocation/copy failed: ") + hipGetErrorString(he));
     fcg_destroy(ctx);
-    return FCG_ERR_DEVICE;
+    return fcg_device_error();
   }
   *out = ctx;
   return FCG_OK;
@@ -1137,7 +1138,7 @@ int fcg_evaluate_device(fcg_ctx* ctx, int action, int mode, const double* d_u_co
     m.err_clean = false;
     ctx->pending = false;
     ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
-    return FCG_ERR_DEVICE;
+    return fcg_device_error();
   }
   ctx->pending = false;
   read_timing(T);
@@ -1167,7 +1168,7 @@ int fcg_check_error(fcg_ctx* ctx, int32_t* bad_ele_gid)
   {
     ctx->mesh.err_clean = false;
     ctx->last_error = "HIP: stream failed";
-    return FCG_ERR_DEVICE;
+    return fcg_device_error();
   }
   return report_error(ctx, bad_ele_gid);
 }
@@ -1207,7 +1208,7 @@ int fcg_evaluate_host(fcg_ctx* ctx, int action, int mode, const double* u_col, d
   if (he != hipSuccess)
   {
     ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
-    return FCG_ERR_DEVICE;
+    return fcg_device_error();
   }
   const bool was_async = ctx->async;
   ctx->async = false;
@@ -1221,7 +1222,7 @@ int fcg_evaluate_host(fcg_ctx* ctx, int action, int mode, const double* u_col, d
   if (he != hipSuccess)
   {
     ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
-    return FCG_ERR_DEVICE;
+    return fcg_device_error();
   }
   return FCG_OK;
 }
@@ -1254,7 +1255,7 @@ int fcg_get_diagnostics(const fcg_ctx* ctx, uint64_t* out, int n)
   const fcg::DeviceMesh& m = ctx->mesh;
   unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (m.stamps && hipMemcpy(v, m.stamps, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess)
-    return FCG_ERR_DEVICE;
+    return fcg_device_error();
   for (int i = 0; i < n && i < 8; ++i) out[i] = v[i];
   return m.stamps ? 8 : 0;
 }
@@ -1278,21 +1279,21 @@ int fcg_get_info(const fcg_ctx* ctx, fcg_info* info)
 int fcg_device_alloc(int device, int64_t bytes, void** d_ptr)
 {
   if (!d_ptr || bytes < 0) return FCG_ERR_ARG;
-  if (hipSetDevice(device) != hipSuccess) return FCG_ERR_DEVICE;
-  return hipMalloc(d_ptr, bytes > 0 ? bytes : 1) == hipSuccess ? FCG_OK : FCG_ERR_DEVICE;
+  if (!fcg_use_device(device)) return fcg_device_error();
+  return hipMalloc(d_ptr, bytes > 0 ? bytes : 1) == hipSuccess ? FCG_OK : fcg_device_error();
 }
-int fcg_device_free(void* p) { return hipFree(p) == hipSuccess ? FCG_OK : FCG_ERR_DEVICE; }
+int fcg_device_free(void* p) { return hipFree(p) == hipSuccess ? FCG_OK : fcg_device_error(); }
 int fcg_memcpy_h2d(void* dst, const void* src, int64_t n)
 {
-  return hipMemcpy(dst, src, n, hipMemcpyHostToDevice) == hipSuccess ? FCG_OK : FCG_ERR_DEVICE;
+  return hipMemcpy(dst, src, n, hipMemcpyHostToDevice) == hipSuccess ? FCG_OK : fcg_device_error();
 }
 int fcg_memcpy_d2h(void* dst, const void* src, int64_t n)
 {
-  return hipMemcpy(dst, src, n, hipMemcpyDeviceToHost) == hipSuccess ? FCG_OK : FCG_ERR_DEVICE;
+  return hipMemcpy(dst, src, n, hipMemcpyDeviceToHost) == hipSuccess ? FCG_OK : fcg_device_error();
 }
 int fcg_memset_device(void* dst, int v, int64_t n)
 {
-  return hipMemset(dst, v, n) == hipSuccess ? FCG_OK : FCG_ERR_DEVICE;
+  return hipMemset(dst, v, n) == hipSuccess ? FCG_OK : fcg_device_error();
 }
 
 }  // extern "C"

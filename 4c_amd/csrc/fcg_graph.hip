@@ -21,6 +21,7 @@
 #include <climits>
 
 #include "fourc_gpu.h"
+#include "fcg_status.hpp"
 
 namespace fcg {
 namespace {
@@ -248,7 +249,7 @@ extern "C" int fcg_graph_build_device(int device, int celltype, int64_t n_ele,
            static_cast<void*>(rowlen), static_cast<void*>(inc_ele), static_cast<void*>(err)})
     if (p) (void)hipFreeAsync(p, s);
   (void)hipStreamSynchronize(s);
-  if (he != hipSuccess) return FCG_ERR_DEVICE;
+  if (he != hipSuccess) return fcg_device_error();
   if (errv != 0) return FCG_ERR_ARG;
   *nnz = total;
   return FCG_OK;

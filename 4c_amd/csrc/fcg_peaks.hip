@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "fourc_gpu.h"
+#include "fcg_status.hpp"
 
 namespace {
 
@@ -150,16 +151,16 @@ float time_ms(hipStream_t s, int reps, F launch)
 extern "C" int fcg_measure_peaks(int device, double* hbm_triad_gbs, double* fp64_valu_tflops,
     double* fp64_mfma_tflops)
 {
-  if (hipSetDevice(device) != hipSuccess)
+  if (!fcg_use_device(device))
   {
     (void)hipGetLastError();  // do not leave the error for the caller's next HIP call
-    return FCG_ERR_DEVICE;
+    return fcg_device_error();
   }
   hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return FCG_ERR_DEVICE;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return fcg_device_error();
   const int cus = std::max(1, prop.multiProcessorCount);
   hipStream_t s = nullptr;
-  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return FCG_ERR_DEVICE;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return fcg_device_error();
   int rc = FCG_OK;
   // triad over 3 x 1 GiB (far beyond the 256 MB Infinity Cache)
   const int64_t n = int64_t(1) << 27;
@@ -167,7 +168,7 @@ extern "C" int fcg_measure_peaks(int device, double* hbm_triad_gbs, double* fp64
   const int grid_v = cus * 8, iters = 4096;
   if (hipMalloc(&a, n * 8) != hipSuccess || hipMalloc(&b, n * 8) != hipSuccess ||
       hipMalloc(&c, n * 8) != hipSuccess || hipMalloc(&out, int64_t(grid_v) * 256 * 8) != hipSuccess)
-    rc = FCG_ERR_DEVICE;
+    rc = fcg_device_error();
   if (rc == FCG_OK)
   {
     (void)hipMemsetAsync(b, 0, n * 8, s);
@@ -196,7 +197,7 @@ extern "C" int fcg_measure_peaks(int device, double* hbm_triad_gbs, double* fp64
     if (fp64_mfma_tflops)
       *fp64_mfma_tflops =
           2.0 * 1024.0 * NACC * double(iters / NACC) * grid_v * 4 / (mm * 1e-3) / 1e12;
-    if (hipStreamSynchronize(s) != hipSuccess || hipGetLastError() != hipSuccess) rc = FCG_ERR_DEVICE;
+    if (hipStreamSynchronize(s) != hipSuccess || hipGetLastError() != hipSuccess) rc = fcg_device_error();
   }
   for (double* p : {a, b, c, out})
     if (p) (void)hipFree(p);
@@ -206,21 +207,21 @@ extern "C" int fcg_measure_peaks(int device, double* hbm_triad_gbs, double* fp64
 
 extern "C" int fcg_measure_hbm(int device, double* copy_gbs, double* write_gbs)
 {
-  if (hipSetDevice(device) != hipSuccess)
+  if (!fcg_use_device(device))
   {
     (void)hipGetLastError();  // do not leave the error for the caller's next HIP call
-    return FCG_ERR_DEVICE;
+    return fcg_device_error();
   }
   hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return FCG_ERR_DEVICE;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return fcg_device_error();
   const int cus = std::max(1, prop.multiProcessorCount);
   hipStream_t s = nullptr;
-  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return FCG_ERR_DEVICE;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return fcg_device_error();
   int rc = FCG_OK;
   // 2 x 2 GiB: far beyond the 256 MB Infinity Cache
   const int64_t n2 = int64_t(1) << 27;  // double2 elements = 2 GiB
   double2 *a = nullptr, *b = nullptr;
-  if (hipMalloc(&a, n2 * 16) != hipSuccess || hipMalloc(&b, n2 * 16) != hipSuccess) rc = FCG_ERR_DEVICE;
+  if (hipMalloc(&a, n2 * 16) != hipSuccess || hipMalloc(&b, n2 * 16) != hipSuccess) rc = fcg_device_error();
   if (rc == FCG_OK)
   {
     (void)hipMemsetAsync(b, 0, n2 * 16, s);
@@ -236,7 +237,7 @@ extern "C" int fcg_measure_hbm(int device, double* copy_gbs, double* write_gbs)
     }
     if (copy_gbs) *copy_gbs = 2.0 * 16.0 * double(n2) / (mc * 1e-3) / 1e9;
     if (write_gbs) *write_gbs = 16.0 * double(n2) / (mw * 1e-3) / 1e9;
-    if (hipStreamSynchronize(s) != hipSuccess || hipGetLastError() != hipSuccess) rc = FCG_ERR_DEVICE;
+    if (hipStreamSynchronize(s) != hipSuccess || hipGetLastError() != hipSuccess) rc = fcg_device_error();
   }
   for (double2* p : {a, b})
     if (p) (void)hipFree(p);

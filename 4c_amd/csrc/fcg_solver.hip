@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "fcg_internal.hpp"
+#include "fcg_status.hpp"
 
 namespace fcg {
 
@@ -420,7 +421,7 @@ int fcg_spmv(fcg_ctx* ctx, const double* d_K_vals, const double* d_x_col, double
   if (he != hipSuccess)
   {
     ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
-    return FCG_ERR_DEVICE;
+    return fcg_device_error();
   }
   return FCG_OK;
 }
@@ -435,7 +436,7 @@ int fcg_spmv_f32(fcg_ctx* ctx, const float* d_K32, const double* d_x_col, double
   if (he != hipSuccess)
   {
     ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
-    return FCG_ERR_DEVICE;
+    return fcg_device_error();
   }
   return FCG_OK;
 }
@@ -464,7 +465,7 @@ int fcg_dirichlet_apply(fcg_ctx* ctx, int64_t n_dbc, const int32_t* d_rows, doub
   if (he != hipSuccess)
   {
     ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
-    return FCG_ERR_DEVICE;
+    return fcg_device_error();
   }
   if (bad)
   {
@@ -510,7 +511,7 @@ int fcg_pcg_solve(fcg_ctx* ctx, const double* d_K_vals, const double* d_b_row, d
     if (he != hipSuccess)
     {
       ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
-      return FCG_ERR_DEVICE;
+      return fcg_device_error();
     }
     m.pcg_n = n;
   }
@@ -544,7 +545,7 @@ int fcg_pcg_solve(fcg_ctx* ctx, const double* d_K_vals, const double* d_b_row, d
   if (he != hipSuccess)
   {
     ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
-    return FCG_ERR_DEVICE;
+    return fcg_device_error();
   }
   if (bad)
   {
@@ -586,7 +587,7 @@ int fcg_pcg_solve(fcg_ctx* ctx, const double* d_K_vals, const double* d_b_row, d
     if (he != hipSuccess)
     {
       ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
-      return FCG_ERR_DEVICE;
+      return fcg_device_error();
     }
     it += burst;
     rr = hsc[fcg::SC_RR];
@@ -632,7 +633,7 @@ int fcg_block_jacobi_setup(fcg_ctx* ctx, const double* d_K_vals, double* d_dinv,
   if (he != hipSuccess)
   {
     ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
-    return FCG_ERR_DEVICE;
+    return fcg_device_error();
   }
   if (bad)
   {
@@ -657,7 +658,7 @@ int fcg_block_jacobi_apply(fcg_ctx* ctx, const double* d_dinv, const double* d_r
   if (he != hipSuccess)
   {
     ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
-    return FCG_ERR_DEVICE;
+    return fcg_device_error();
   }
   return FCG_OK;
 }
@@ -669,11 +670,11 @@ int fcg_node_transfer(int device, int64_t n_out, const int64_t* d_ptr, const int
   if (n_out < 0 || (n_out > 0 && (!d_ptr || !d_src_row0 || !d_w || !d_dst_row0 || !d_x || !d_y)))
     return FCG_ERR_ARG;
   if (n_out == 0) return FCG_OK;
-  if (hipSetDevice(device) != hipSuccess) return FCG_ERR_DEVICE;
+  if (!fcg_use_device(device)) return fcg_device_error();
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(fcg::node_transfer_kernel, dim3(fcg::blocks_for(n_out, fcg::kBlock)), dim3(fcg::kBlock), 0, s,
       d_ptr, d_src_row0, d_w, d_dst_row0, d_x, d_y, n_out, accumulate);
-  return hipGetLastError() == hipSuccess ? FCG_OK : FCG_ERR_DEVICE;
+  return hipGetLastError() == hipSuccess ? FCG_OK : fcg_device_error();
 }
 
 }  // extern "C"

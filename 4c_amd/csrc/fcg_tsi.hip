@@ -40,6 +40,7 @@
 
 #include "fcg_hex8_element.hpp"
 #include "fcg_internal.hpp"
+#include "fcg_status.hpp"
 #include "fcg_shape.hpp"
 
 namespace fcg {
@@ -676,7 +677,7 @@ int fcg_tsi_create(const fcg_tsi_desc* D, fcg_tsi_ctx** out)
   {
     set_tsi_create_error(std::string("HIP: ") + hipGetErrorString(he));
     delete ctx;
-    return FCG_ERR_DEVICE;
+    return fcg_device_error();
   }
   fcg::TsiDevice& d = ctx->d;
   d.npe = npe;
@@ -738,7 +739,7 @@ int fcg_tsi_create(const fcg_tsi_desc* D, fcg_tsi_ctx** out)
   {
     set_tsi_create_error(std::string("HIP allocation/copy failed: ") + hipGetErrorString(he));
     fcg_tsi_destroy(ctx);
-    return FCG_ERR_DEVICE;
+    return fcg_device_error();
   }
   *out = ctx;
   return FCG_OK;
@@ -825,7 +826,7 @@ int fcg_tsi_evaluate_device(fcg_tsi_ctx* ctx, int parts, int mode, const double*
   if (he != hipSuccess)
   {
     ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
-    return FCG_ERR_DEVICE;
+    return fcg_device_error();
   }
   if (errv[0] != 0)
   {
@@ -906,7 +907,7 @@ int fcg_tsi_evaluate_fused(fcg_ctx* sctx, fcg_tsi_ctx* ctx, int mode, const doub
     if (he != hipSuccess)
     {
       ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
-      return FCG_ERR_DEVICE;
+      return fcg_device_error();
     }
     if (flag)
     {
@@ -940,7 +941,7 @@ int fcg_tsi_evaluate_fused(fcg_ctx* sctx, fcg_tsi_ctx* ctx, int mode, const doub
   if (he != hipSuccess)
   {
     ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
-    return FCG_ERR_DEVICE;
+    return fcg_device_error();
   }
   if (errv[0] != 0)
   {

@@ -27,6 +27,7 @@ import torch.distributed as dist
 
 fcg = importlib.import_module("4c_amd").fcg
 halo = importlib.import_module("4c_amd.halo")
+newton = importlib.import_module("4c_amd.newton")
 
 
 def _ptr(t):
@@ -138,7 +139,7 @@ class DistributedNewton:
     Dirichlet row LIDs.  solve() returns the converged owned-row displacement."""
 
     def __init__(self, evaluator, transport, fext_row, dbc_rows, tol_res=1e-10, tol_inc=1e-10,
-                 max_iter=20, lin_rtol=1e-12, lin_max_iter=100000):
+                 max_iter=20, lin_rtol=1e-12, lin_max_iter=100000, rescue_bad_newton_solve=True):
         info = evaluator.info
         self.ev, self.tr = evaluator, transport
         self.dev = torch.device("cuda", evaluator.device)
@@ -154,6 +155,7 @@ class DistributedNewton:
         self.freact = torch.zeros(self.n, **f64)
         self.tol_res, self.tol_inc, self.max_iter = tol_res, tol_inc, max_iter
         self.lin_rtol, self.lin_max_iter = lin_rtol, lin_max_iter
+        self.rescue = rescue_bad_newton_solve  # NOX "Rescue Bad Newton Solve" (newton.StaticNewton)
         self.pcg = DistributedPCG(evaluator, transport)
         self.history = []
 
@@ -176,10 +178,9 @@ class DistributedNewton:
                 self.history.append(rec)
                 return u
             torch.neg(self.r, out=self.r)
-            lin_it, lin_res = self.pcg.solve(self.K, self.r, self.du, self.lin_rtol, self.lin_max_iter)
-            if not lin_res <= self.lin_rtol:
-                raise RuntimeError(f"linear solve of Newton step {it} stopped at relative residual "
-                                   f"{lin_res:.3e} ({lin_it} iterations)")
+            lin_it, lin_res = newton.accept_linear_solve(
+                lambda: self.pcg.solve(self.K, self.r, self.du, self.lin_rtol, self.lin_max_iter),
+                self.lin_rtol, it, self.rescue, rec)
             rec.update(lin_iter=lin_it, lin_relres=lin_res)
             self.history.append(rec)
             ndu = self._norm(self.du)

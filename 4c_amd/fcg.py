@@ -27,6 +27,7 @@ TSI_STRUCT_FORCE, TSI_STIFFTEMP, TSI_THERMO_FINTCOND, TSI_COUPLTANG = 1, 2, 4, 8
 TSI_ALL = 15
 ABI_VERSION = 1
 
+FCG_OK, FCG_ERR_NODAL_DETJ, FCG_ERR_SINGULAR, FCG_ERR_ARG, FCG_ERR_DEVICE = 0, 1, 2, 3, 4
 STATUS = {0: "FCG_OK", 1: "FCG_ERR_NODAL_DETJ", 2: "FCG_ERR_SINGULAR", 3: "FCG_ERR_ARG",
           4: "FCG_ERR_DEVICE"}
 
@@ -120,7 +121,7 @@ EXPORTS = ["fcg_create", "fcg_destroy", "fcg_last_error", "fcg_evaluate", "fcg_e
            "fcg_tsi_evaluate_fused",
            "fcg_box_mesh_create", "fcg_box_mesh_destroy", "fcg_box_mesh_desc", "fcg_box_mesh_maps",
            "fcg_box_mesh_counts", "fcg_box_mesh_create_ex", "fcg_box_mesh_owned_rows",
-           "fcg_comm_unique_id", "fcg_comm_create", "fcg_comm_destroy", "fcg_comm_allreduce",
+           "fcg_comm_unique_id", "fcg_comm_create", "fcg_comm_destroy", "fcg_comm_size", "fcg_comm_allreduce",
            "fcg_comm_alltoallv", "fcg_import_plan_build", "fcg_plan_free", "fcg_halo_create",
            "fcg_halo_destroy", "fcg_halo_import", "fcg_halo_pack", "fcg_halo_unpack",
            "fcg_shared_plan_build", "fcg_shared_create", "fcg_shared_destroy", "fcg_shared_reduce",
@@ -203,6 +204,7 @@ def lib():
     L.fcg_comm_unique_id.argtypes = [vp]
     L.fcg_comm_create.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
     L.fcg_comm_destroy.argtypes = [vp]
+    L.fcg_comm_size.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
     L.fcg_comm_allreduce.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_int, vp]
     L.fcg_comm_alltoallv.argtypes = [vp, _i64p, vp, _i64p, ctypes.c_int64, vp]
     L.fcg_import_plan_build.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64, _i32p,

@@ -65,6 +65,14 @@ class Comm:
         self._h, self.rank, self.world, self.device = h, rank, world, device
         self.exchange = Exchange(ctypes.cast(L.fcg_comm_alltoallv, ctypes.c_void_p).value, h)
 
+    def size(self):
+        """ncclCommCount of the communicator (fcg_comm_size)."""
+        n = ctypes.c_int()
+        rc = fcg.lib().fcg_comm_size(self._h, ctypes.byref(n))
+        if rc != 0:
+            raise fcg.FcgError(rc, "fcg_comm_size failed")
+        return n.value
+
     def allreduce(self, t, op=fcg.FCG_OP_SUM, stream=None):
         """In-place all-reduce of a float64 device tensor."""
         rc = fcg.lib().fcg_comm_allreduce(self._h, _ptr(t), t.numel(), op,
@@ -232,8 +240,15 @@ class Halo:
         rb = torch.empty(self.n_recv, dtype=torch.float64)
         dist.all_to_all_single(rb, send[:self.n_send].cpu(), output_split_sizes=self.recv_counts,
                                input_split_sizes=self.send_counts)
-        recv = rb.to(u_row.device)
-        self.unpack(recv, u_col, stream)
+        # the device copy of the received values is made on `stream`, the stream unpack is queued
+        # on, and both buffers are marked in use by it, so that the caching allocator cannot hand
+        # them to other work before unpack has run
+        st = stream or torch.cuda.current_stream(u_row.device)
+        with torch.cuda.stream(st):
+            recv = rb.to(u_row.device, non_blocking=False)
+        recv.record_stream(st)
+        send.record_stream(st)
+        self.unpack(recv, u_col, st)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -337,12 +352,14 @@ class Shared:
         """Host-staged transport (gloo all-reduce of the interface buffer)."""
         import torch
         import torch.distributed as dist
-        buf = torch.empty(max(1, self.n_global), dtype=torch.float64, device=f.device)
-        self.pack(f, buf, stream)
-        h = buf[:self.n_global].cpu()
-        dist.all_reduce(h)
-        buf[:self.n_global].copy_(h)
-        self.unpack(buf, f, stream)
+        st = stream or torch.cuda.current_stream(f.device)
+        with torch.cuda.stream(st):
+            buf = torch.empty(max(1, self.n_global), dtype=torch.float64, device=f.device)
+            self.pack(f, buf, st)
+            h = buf[:self.n_global].cpu()
+            dist.all_reduce(h)
+            buf[:self.n_global].copy_(h)
+            self.unpack(buf, f, st)
 
     def close(self):
         if getattr(self, "_h", None):

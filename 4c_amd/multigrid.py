@@ -222,12 +222,20 @@ class _Indefinite(Exception):
 
 
 class MultigridError(RuntimeError):
-    """The preconditioned solve failed twice: with the kept lambda_max estimate and again with a
-    fresh one (indefinite V-cycle, or no convergence to the requested tolerance)."""
+    """The preconditioned solve failed: with the kept lambda_max estimate and (Multigrid) again
+    with a fresh one -- an indefinite V-cycle, or no convergence to the requested tolerance.  In
+    the second case `iterations` and `relres` are set and x holds the last iterate, which a Newton
+    loop with 'Rescue Bad Newton Solve' may still use as its direction."""
+
+    def __init__(self, msg, iterations=None, relres=None):
+        super().__init__(msg)
+        self.iterations, self.relres = iterations, relres
 
 
 class CycleFCG:
     """Flexible CG preconditioned by one V-cycle (the outer solve of Multigrid and amg.AMG).
+    `retry_lmax`: on failure, re-estimate the fine level's lambda_max and solve once more (useful
+    only where the estimate can be stale, i.e. Multigrid, which keeps it across tangents).
     Subclasses hold `levels` (level 0: the system's _Level on the evaluator's K) and supply
     _prepare(K) (per-tangent setup), _restrict(l, r, b_coarse), _prolong(l, x_coarse, x) (adds
     into x) and _coarse_solve(level, b, x); nu, ratio, boost, trace and dev as in Multigrid."""
@@ -236,6 +244,7 @@ class CycleFCG:
     # nonsymmetric preconditioner, which the flexible CG's Polak-Ribiere beta admits; it saves
     # the fine level's two post-smoothing SpMVs of the five an iteration costs)
     fine_post = True
+    retry_lmax = True
 
     # -- smoother ---------------------------------------------------------------------------
     def _cheb(self, lvl, b, x, x_zero):
@@ -287,19 +296,20 @@ class CycleFCG:
         raises MultigridError."""
         f0 = self.levels[0]
         self._prepare(K)
-        why = None
-        for attempt in range(2):
+        why, last = None, (None, None)
+        for attempt in range(2 if self.retry_lmax else 1):
             if attempt:
                 f0.estimate_lmax()
             try:
                 it, rel = self._fcg(f0, b, x, rtol, max_iter)
             except (_Indefinite, FloatingPointError) as e:
-                why = repr(e) or "indefinite V-cycle"
+                why, last = repr(e) or "indefinite V-cycle", (None, None)
                 continue
             if rel <= rtol:
                 return it, rel
-            why = f"relative residual {rel:.3e} > {rtol:.3e} after {it} iterations"
-        raise MultigridError(f"multigrid FCG failed after a lambda_max re-estimate: {why}")
+            why, last = f"relative residual {rel:.3e} > {rtol:.3e} after {it} iterations", (it, rel)
+        what = "after a lambda_max re-estimate" if self.retry_lmax else "(no retry)"
+        raise MultigridError(f"multigrid FCG failed {what}: {why}", *last)
 
     def _fcg(self, f0, b, x, rtol, max_iter):
         """Flexible CG with the scalars kept on the device: one host read per iteration (|r|,

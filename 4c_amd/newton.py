@@ -16,6 +16,7 @@ in HBM; torch only supplies the device buffers and the vector updates.
 """
 
 import math
+import warnings
 
 import numpy as np
 import torch
@@ -72,12 +73,39 @@ class ForcingTerm:
         return self.eta
 
 
+def accept_linear_solve(solve, tol, it, rescue, rec):
+    """Run a Newton step's linear solve and decide whether its direction is used, as NOX's
+    Newton direction does with "Rescue Bad Newton Solve" (4C_inpar_solver_nonlin.cpp:65-69):
+    a finite solution above the tolerance is kept when `rescue` (marked in `rec`, warned);
+    otherwise, or for a non-finite residual or an indefinite preconditioner, raise."""
+    from .multigrid import MultigridError
+    try:
+        lin_it, lin_res = solve()
+    except MultigridError as e:
+        if not rescue or e.relres is None:
+            raise
+        lin_it, lin_res = e.iterations, e.relres
+    if lin_res <= tol:
+        return lin_it, lin_res
+    msg = (f"linear solve of Newton step {it} stopped at relative residual {lin_res:.3e} above "
+           f"its tolerance {tol:.3e} ({lin_it} iterations)")
+    if not rescue or not math.isfinite(lin_res):
+        raise RuntimeError(msg)
+    warnings.warn(msg + "; direction kept (Rescue Bad Newton Solve)", RuntimeWarning, stacklevel=3)
+    rec["lin_rescued"] = True
+    return lin_it, lin_res
+
+
 class StaticNewton:
     def __init__(self, evaluator, fext_row, dbc_rows, tol_res=1e-10, tol_inc=1e-10, max_iter=20,
-                 lin_rtol=1e-13, lin_max_iter=100000, forcing=None, linear_solver=None):
+                 lin_rtol=1e-13, lin_max_iter=100000, forcing=None, linear_solver=None,
+                 rescue_bad_newton_solve=True):
         """forcing: ForcingTerm (None: Constant at lin_rtol).  linear_solver: an object with
         solve(K, b, x, rtol, max_iter) -> (iterations, relative residual), e.g.
-        multigrid.Multigrid (None: the library's block-Jacobi PCG)."""
+        multigrid.Multigrid (None: the library's block-Jacobi PCG).
+        rescue_bad_newton_solve: NOX's "Rescue Bad Newton Solve" (4C default true,
+        4C_inpar_solver_nonlin.cpp:65-69): a linear solve that stops above its tolerance still
+        gives the step (recorded in history, with a warning); false: raise."""
         info = evaluator.info
         self.ev = evaluator
         self.dev = torch.device("cuda", evaluator.device)
@@ -95,6 +123,7 @@ class StaticNewton:
         self.freact = torch.zeros(self.n, **f64)
         self.tol_res, self.tol_inc, self.max_iter = tol_res, tol_inc, max_iter
         self.lin_rtol, self.lin_max_iter = lin_rtol, lin_max_iter
+        self.rescue = rescue_bad_newton_solve
         self.forcing = forcing if forcing is not None else ForcingTerm("Constant", constant=lin_rtol)
         self.linear_solver = linear_solver
         if linear_solver is not None and hasattr(linear_solver, "check_dirichlet"):
@@ -125,11 +154,8 @@ class StaticNewton:
                 return u
             torch.neg(self.r, out=self.r)
             eta = self.forcing.compute(it, nr, nr_old, lin_abs)
-            lin_it, lin_res = self.linear_solve(self.r, self.du, eta)
-            if not lin_res <= eta:
-                raise RuntimeError(f"linear solve of Newton step {it} stopped at relative residual "
-                                   f"{lin_res:.3e} above the forcing tolerance {eta:.3e} "
-                                   f"({lin_it} iterations)")
+            lin_it, lin_res = accept_linear_solve(lambda: self.linear_solve(self.r, self.du, eta),
+                                                  eta, it, self.rescue, rec)
             nr_old, lin_abs = nr, lin_res * nr  # ‖F_k + J_k d_k‖ (full step, no line search)
             rec.update(lin_iter=lin_it, lin_relres=lin_res, eta=eta)
             self.history.append(rec)

@@ -1,8 +1,12 @@
 """Benchmark: element evaluations/s and global-assembly wall time of 4C's SOLID hex8 linear
 elasticity path (BASELINE.json config 2: 1M hex8 per GPU, K and r assembled) on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W]      (N > 1: starts its N ranks itself)
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
+
+Without WORLD_SIZE in the environment, `--gpus N` (N > 1) starts N rank processes of this script
+(tools/rank_launcher.py: RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*, before torch is imported, no
+exec) and exits with the first failing rank's code; under a launcher WORLD_SIZE must equal N.
 
 One step = Discretization::set_state (row -> column import of the displacement; RCCL all-to-all
 of the ghost DOFs when N > 1) + Discretization::evaluate(struct_calc_nlnstiff) with zero() fused
@@ -18,15 +22,23 @@ import glob
 import json
 import os
 import platform
+import re
 import subprocess
 import sys
 import time
 
-import numpy as np
-import torch
-import torch.distributed as dist
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import rank_launcher  # noqa: E402  (standard library only)
+
+if __name__ == "__main__":
+    # one process per GPU: start the ranks here, before anything can initialise HIP
+    rank_launcher.run_or_spawn(sys.argv, os.path.abspath(__file__))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
 sys.path.insert(0, ROOT)
 
 import importlib  # noqa: E402
@@ -94,10 +106,21 @@ def cpu_baseline(n, kinem, threads):
     t = time.perf_counter()
     parity_util.oracle_evaluate(small, kinem, 210.0, 0.3, us, nworkers=1)
     t1 = time.perf_counter() - t
+    # thread scaling of the same slab, measured up to the granted share (the GridGenerator split
+    # into t ranks, each assembling its own rows): backs the all-core extrapolation below
+    scaling = {}
+    tc = 2
+    while tc < threads:
+        t = time.perf_counter()
+        parity_util.oracle_evaluate(small, kinem, 210.0, 0.3, us, nworkers=tc)
+        scaling[str(tc)] = small.n_ele / (time.perf_counter() - t)
+        tc *= 2
     t = time.perf_counter()
     err, _, _, _ = parity_util.oracle_evaluate(mesh, kinem, 210.0, 0.3, u, nworkers=threads)
     tn = time.perf_counter() - t
     assert err == 0
+    scaling["1"] = small.n_ele / t1
+    scaling[str(threads)] = mesh.n_ele / tn
     try:
         model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
     except Exception:
@@ -113,11 +136,82 @@ def cpu_baseline(n, kinem, threads):
                   f"{small.n_ele} elements",
         "wall_s": tn, "single_core_value": small.n_ele / t1, "cpu_model": model,
         "topology": topo,
-        # not measured: the single-core rate times every physical core of the host (what a full
-        # MPI run of the reference could reach at perfect scaling)
-        "all_physical_cores_extrapolated": small.n_ele / t1 * phys,
+        "thread_scaling_measured": scaling,
+        "parallel_efficiency_measured": (mesh.n_ele / tn) / (threads * small.n_ele / t1),
+        # not measured: the GPU box grants this process `threads` CPUs (OMP_NUM_THREADS; the
+        # other cores belong to other GPUs' jobs), so the all-core figure is the single-core rate
+        # times every physical core at the parallel efficiency measured at `threads`
+        "all_physical_cores_extrapolated": small.n_ele / t1 * phys
+                                           * min(1.0, (mesh.n_ele / tn) / (threads * small.n_ele / t1)),
+        "all_cores_note": "not run: the box's CPU share for one GPU is the granted thread count; "
+                          "extrapolated from the measured single-core rate and scaling",
         "compiler": "gcc -O3 -march=native -fopenmp",
     }
+
+
+def _pmc_key(path):
+    """(round, version) of profiles/pmc_rNN[_vM].json; older files sort first."""
+    m = re.search(r"pmc_r(\d+)(?:_v(\d+))?\.json$", os.path.basename(path))
+    return (int(m.group(1)), int(m.group(2) or 0)) if m else (-1, -1)
+
+
+def committed_pmc(explicit=None):
+    """The committed PMC traffic file: `explicit`, else the newest by (round, version)."""
+    if explicit:
+        return explicit
+    files = glob.glob(os.path.join(ROOT, "profiles", "pmc_r*.json"))
+    return max(files, key=_pmc_key) if files else None
+
+
+def _under_profiler():
+    pre = os.environ.get("LD_PRELOAD", "") + os.environ.get("HSA_TOOLS_LIB", "")
+    return "rocprof" in pre or any(k.startswith("ROCPROF") for k in os.environ)
+
+
+def measure_traffic(n, kernel="sweep_h8", timeout_s=150):
+    """HBM bytes per evaluate of the bench kernel, measured in this run: two rocprofv3 counter
+    passes (FETCH_SIZE, then WRITE_SIZE -- they do not fit one pass), each a child process
+    (tools/prof_kernel.py: the same n^3 mesh, seed and kernel, 3 evaluates) under its own time
+    limit.  Corrections of MI355X_MICROARCH.md "HBM": counters in KiB, gfx950 FETCH_SIZE counts
+    half the bytes of wide reads (x2), WRITE_SIZE exact.  Returns a dict (or one with "error")."""
+    import csv
+    import shutil
+    import tempfile
+    rp = shutil.which("rocprofv3")
+    if rp is None:
+        return {"error": "rocprofv3 not found"}
+    if _under_profiler():
+        return {"error": "bench.py is itself running under a profiler: no nested counter passes"}
+    work = tempfile.mkdtemp(prefix="fcg_pmc_")
+    per = {}
+    try:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(work, ctr)
+            cmd = [rp, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "run", "--",
+                   sys.executable, os.path.join(ROOT, "tools", "prof_kernel.py"), "--n", str(n),
+                   "--seed", "20251015", "--reps", "3"]
+            env = dict(os.environ, TMPDIR=work)
+            p = subprocess.run(cmd, cwd=work, env=env, capture_output=True, text=True,
+                               timeout=timeout_s)
+            if p.returncode != 0:
+                return {"error": f"{ctr} pass exited {p.returncode}: {p.stderr[-400:]}"}
+            vals = {}
+            for fn in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+                for r in csv.DictReader(open(fn)):
+                    if kernel in r["Kernel_Name"] and r["Counter_Name"] == ctr:
+                        vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+            if not vals:
+                return {"error": f"{ctr}: no {kernel} dispatch in the counter output"}
+            per[ctr] = sum(vals.values()) / len(vals)
+        fetch = 2.0 * 1024.0 * per["FETCH_SIZE"]
+        write = 1024.0 * per["WRITE_SIZE"]
+        return {"fetch_bytes_x2": fetch, "write_bytes": write, "hbm_bytes_per_evaluate": fetch + write,
+                "source": "measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate "
+                          "child passes of tools/prof_kernel.py (3 evaluates, mean per dispatch)"}
+    except subprocess.TimeoutExpired:
+        return {"error": f"counter pass exceeded {timeout_s} s"}
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
 
 
 def cpu_threads(requested):
@@ -428,21 +522,27 @@ def optionb_secondary(dev, rank, world, n, steps, staged):
         f = torch.zeros(m.n_rows, dtype=torch.float64, device=dev)
         stream = torch.cuda.current_stream(dev)
 
-        def step():
+        def step(marks=None):
             if staged:
                 h.import_staged(u_row, u_col, stream)
             else:
                 h.import_(comm, u_row, u_col, stream)
             ev.evaluate_device(fcg.CALC_INTERNALFORCE, fcg.OVERWRITE, u_col, f, stream=stream)
+            if marks is not None:
+                marks[0].record(stream)
             if staged:
                 sh.reduce_staged(f, stream)
+            else:
+                sh.reduce(comm, f, stream)
+            if marks is not None:
+                marks[1].record(stream)
+            if staged:
                 loc = halo.residual_norm(f[:n_own], None, stream)
                 t = torch.tensor([loc * loc], dtype=torch.float64)
                 if world > 1:
                     dist.all_reduce(t)
                 nrm = float(np.sqrt(t.item()))
             else:
-                sh.reduce(comm, f, stream)
                 nrm = halo.residual_norm(f[:n_own], comm, stream)
             ev.check_error()
             return nrm
@@ -457,13 +557,21 @@ def optionb_secondary(dev, rank, world, n, steps, staged):
             nrm = step()
         torch.cuda.synchronize(dev)
         wall = _ctl_max((time.perf_counter() - t0) / steps, world)
+        red = []
+        for _ in range(3):
+            mk = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            step(mk)
+            red.append(mk[0].elapsed_time(mk[1]))
+        ms_reduce = _ctl_max(float(np.mean(red)), world)
         out = {"workload": f"hex8-linear-{n}^3-per-gpu strict partition, internal force + shared-DOF "
                            f"all-reduce (option B)",
                "baseline_config": "BASELINE.json configs[3] (RCCL shared-DOF all-reduce)",
                "value": m.n_ele_global / wall, "unit": "element-evaluations/s (residual only)",
                "ms_per_step": 1e3 * wall, "elements_global": m.n_ele_global,
                "elements_evaluated_rank0": m.n_ele, "interface_dofs_global": sp.n_global,
-               "allreduce_bytes": 8 * sp.n_global, "residual_norm": nrm,
+               "allreduce_bytes": 8 * sp.n_global, "ms_shared_reduce_max": ms_reduce,
+               "rccl_comm_size": comm.size() if comm is not None else None,
+               "residual_norm": nrm,
                "transport": "host-staged gloo" if staged else "RCCL (fcg_halo_import + fcg_shared_reduce)"}
         for o in (sh, h, ev):
             o.close()
@@ -575,6 +683,10 @@ def main():
                          "timed steps always runs)")
     ap.add_argument("--peaks-after", action="store_true",
                     help="measure the box's peaks after the timed steps instead of before the warm-up")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="no in-run rocprofv3 counter passes for roofline.traffic")
+    ap.add_argument("--pmc-json", default=None,
+                    help="committed PMC file to fall back on (default: newest profiles/pmc_rNN_vM.json)")
     ap.add_argument("--no-gather", action="store_true",
                     help="skip the unstructured (renumbered) hex8 line")
     args = ap.parse_args()
@@ -621,13 +733,21 @@ def main():
     # evaluate returns once queued; 4C's throws are collected after the norm (one drain per step)
     ev.set_async(True)
 
-    def step():
+    def step(marks=None):
+        if marks is not None:
+            marks[0].record(stream)
         if imp is not None:
             if staged:
                 imp.import_staged(u_row, u_col, stream)
             else:
                 imp.import_(comm, u_row, u_col, stream)
+        if marks is not None:
+            marks[1].record(stream)
         ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u_col, f, K, stream=stream)
+        if marks is not None:
+            marks[2].record(stream)
+            marks[2].synchronize()
+            marks.append(time.perf_counter())
         if staged and world > 1:
             loc = halo.residual_norm(f, None, stream)
             t = torch.tensor([loc * loc], dtype=torch.float64)
@@ -635,8 +755,24 @@ def main():
             nrm = float(np.sqrt(t.item()))
         else:
             nrm = halo.residual_norm(f, comm, stream)
+        if marks is not None:
+            marks.append(time.perf_counter())
         ev.check_error()
         return nrm
+
+    def phase_pass(n):
+        """Where a step's time goes on this rank (a separate pass, outside the timed window):
+        set_state import (halo) and evaluate by hipEvents on the launch stream, the residual norm
+        (sum of squares + RCCL all-reduce + read-back, blocking) by the host clock."""
+        halo_ms, eval_ms, norm_ms = [], [], []
+        for _ in range(n):
+            mk = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            step(mk)
+            halo_ms.append(mk[0].elapsed_time(mk[1]))
+            eval_ms.append(mk[1].elapsed_time(mk[2]))
+            norm_ms.append(1e3 * (mk[4] - mk[3]))
+        return {"ms_halo_import": float(np.mean(halo_ms)), "ms_evaluate": float(np.mean(eval_ms)),
+                "ms_norm_allreduce": float(np.mean(norm_ms))}
 
     # SURVEY §8d asks for the spec peaks re-measured on the box; measured here, on every rank's
     # GPU before its warm-up, so that the timed steps start on a GPU already at its working
@@ -681,6 +817,20 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     t_el, t_as = kernel_timing_pass()
+    phases = phase_pass(max(3, min(args.steps, 10)))
+    rank_info = dict(rank=rank, device=local, elements_owned=int(mesh.n_ele_row),
+                     elements_ghost=int(mesh.n_ele - mesh.n_ele_row),
+                     elements_evaluated=int(mesh.n_ele), dofs_owned=int(mesh.n_rows),
+                     nnz=int(mesh.nnz),
+                     halo_send_doubles=imp.n_send if imp is not None else 0,
+                     halo_recv_doubles=imp.n_recv if imp is not None else 0,
+                     halo_bytes=8 * ((imp.n_send + imp.n_recv) if imp is not None else 0),
+                     ms_kernel=float(np.mean(t_el) + np.mean(t_as)), **phases)
+    ranks = [None] * world
+    if world > 1:
+        dist.all_gather_object(ranks, rank_info)
+    else:
+        ranks = [rank_info]
     if peaks is None:
         try:
             peaks = fcg.measure_peaks(dev.index) + fcg.measure_hbm(dev.index)
@@ -697,16 +847,25 @@ def main():
     n_row_ele = mesh.n_ele_row
     achieved = ALG_BYTES_PER_ELE * n_row_ele / (ms_kern * 1e-3) / 1e9
     flops = ALG_FLOP_PER_ELE * n_row_ele / (ms_kern * 1e-3) / 1e12
-    traffic = None
-    # the newest committed PMC pass of this kernel (tools/pmc.sh + tools/pmc_traffic.py)
-    pmc_path = max(glob.glob(os.path.join(ROOT, "profiles", "pmc_r*.json")) or [""])
-    if os.path.exists(pmc_path):
-        try:
-            pmc = json.load(open(pmc_path))
-            if pmc.get("workload") == f"hex8-linear-{args.n}^3-per-gpu":
-                traffic = pmc.get("hbm_bytes_per_evaluate")
-        except Exception:
-            traffic = None
+    traffic, traffic_source, traffic_detail = None, None, None
+    if rank == 0 and world == 1 and not args.no_pmc and ev.info.path == fcg.PATH_STRUCTURED:
+        traffic_detail = measure_traffic(args.n)
+        if "error" not in traffic_detail:
+            traffic = traffic_detail["hbm_bytes_per_evaluate"]
+            traffic_source = "this run (rocprofv3 --pmc, child passes)"
+    if traffic is None:
+        # fall back to a committed PMC pass of this kernel (tools/pmc.sh + tools/pmc_traffic.py),
+        # named in the output: it is not a measurement of this run
+        pmc_path = committed_pmc(args.pmc_json)
+        if pmc_path and os.path.exists(pmc_path):
+            try:
+                pmc = json.load(open(pmc_path))
+                if pmc.get("workload") == f"hex8-linear-{args.n}^3-per-gpu":
+                    traffic = pmc.get("hbm_bytes_per_evaluate")
+                    traffic_source = (f"committed file profiles/{os.path.basename(pmc_path)} "
+                                      f"(not measured in this run)")
+            except Exception:
+                traffic = None
 
     out = {
         "metric": "element-evaluations/sec (hex8 linear elasticity, K+r global assembly)",
@@ -754,7 +913,10 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
-            "traffic_source": os.path.basename(pmc_path) if traffic is not None else None,
+            "traffic_source": traffic_source,
+            "traffic_detail": traffic_detail,
+            "traffic_ratio_to_algorithmic": (traffic / (ALG_BYTES_PER_ELE * n_row_ele)
+                                             if traffic else None),
             "alg_bytes_per_element": ALG_BYTES_PER_ELE,
             "elements_per_launch": n_row_ele,
             "ms_element_kernel": ms_el,
@@ -763,6 +925,19 @@ def main():
             "fp64_valu": {"achieved_tflops_by_survey_count": flops, "peak_tflops": FP64_PEAK_TFS,
                           "frac": flops / FP64_PEAK_TFS, "alg_flop_per_element": ALG_FLOP_PER_ELE,
                           "note": "SURVEY §8d flop count; the isotropic contraction executes fewer"},
+        },
+        # one line per rank: its GridGenerator share, halo volume and where its step time went
+        "ranks": ranks,
+        "collectives": {
+            "transport": ("RCCL (fcg_comm: grouped ncclSend/ncclRecv + ncclAllReduce)" if comm is not None
+                          else "host-staged gloo" if world > 1 else "none (single GPU)"),
+            "rccl_comm_size": comm.size() if comm is not None else None,
+            "halo_bytes_per_step_total": int(sum(r["halo_bytes"] for r in ranks)) // 2,
+            "norm_allreduce_bytes": 8 if world > 1 else 0,
+            "ms_halo_import_max": max(r["ms_halo_import"] for r in ranks),
+            "ms_norm_allreduce_max": max(r["ms_norm_allreduce"] for r in ranks),
+            "note": "K and r need no exchange (ghost layer, owned rows; SURVEY §8e option A); "
+                    "option B's interface all-reduce is the `optionb` secondary line",
         },
         "assembly_wall_ms": ms_step,
         "untimed_steps_before_timed": args.warmup + (args.steps if cold else 0),

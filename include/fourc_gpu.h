@@ -488,6 +488,8 @@ int fcg_comm_unique_id(void* id);
 /* Collective over nranks: one RCCL communicator per rank, on HIP device `device`. */
 int fcg_comm_create(const void* id, int nranks, int rank, int device, fcg_comm** out);
 int fcg_comm_destroy(fcg_comm* comm);
+/* The communicator's size as RCCL reports it (ncclCommCount); Epetra_Comm::NumProc in 4C. */
+int fcg_comm_size(const fcg_comm* comm, int* nranks);
 /* In-place all-reduce of n doubles in device memory (ncclAllReduce). */
 int fcg_comm_allreduce(fcg_comm* comm, double* d_buf, int64_t n, int op, void* stream);
 

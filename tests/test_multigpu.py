@@ -261,7 +261,7 @@ def _cantilever_loads(m, x_max):
     return fext, dbc
 
 
-def _worker_solve(rank, world, port, q, kinem, path):
+def _worker_solve(rank, world, port, q, kinem, path, transport="staged"):
     try:
         for p in (ROOT, os.path.join(ROOT, "tests")):
             if p not in sys.path:
@@ -275,12 +275,25 @@ def _worker_solve(rank, world, port, q, kinem, path):
         up = (8.0, 4.0, 4.0)
         m = fcg.BoxMesh(fcg.HEX8, iv, upper=up, jitter=0.1, seed=5, rank=rank, nranks=world)
         n_own = m.n_owned_rows
-        plan = halo.ImportPlan(rank, world, m.row_gid[:n_own], m.col_gid, halo.col_owner_of(m),
-                               halo.gloo_exchange())
-        h = halo.Halo(plan, 0)
-        ev = fcg.Evaluator(m, kinematics=kinem, youngs=E, poisson=NU, device=0, path=path)
+        comm = None
+        if transport == "rccl":  # one GPU per rank: halo + dots over the library's RCCL comm
+            dev = rank
+            torch.cuda.set_device(dev)
+
+            def bcast(b):
+                box = [b]
+                dist.broadcast_object_list(box, src=0)
+                return box[0]
+            comm = halo.Comm(rank, world, dev, bcast)
+            xchg = comm.exchange
+        else:
+            dev, xchg = 0, halo.gloo_exchange()
+        plan = halo.ImportPlan(rank, world, m.row_gid[:n_own], m.col_gid, halo.col_owner_of(m), xchg)
+        h = halo.Halo(plan, dev)
+        ev = fcg.Evaluator(m, kinematics=kinem, youngs=E, poisson=NU, device=dev, path=path)
         fext, dbc = _cantilever_loads(m, up[0])
-        tr = dsolve.Transport(h, staged=True, device=0)
+        tr = (dsolve.Transport(h, comm=comm, device=dev) if comm is not None
+              else dsolve.Transport(h, staged=True, device=dev))
         nt = dsolve.DistributedNewton(ev, tr, fext, dbc, tol_res=1e-10, tol_inc=1e-11, lin_rtol=1e-12)
         u = nt.solve().cpu().numpy()
         q.put((rank, True, {"u": dict(zip(m.row_gid[:n_own].tolist(), u.tolist())),
@@ -291,11 +304,16 @@ def _worker_solve(rank, world, port, q, kinem, path):
         q.put((rank, traceback.format_exc() + repr(e), {}))
 
 
+@pytest.mark.parametrize("transport", ["staged", "rccl"])
 @pytest.mark.parametrize("kinem,path", [(fcg.LINEAR, fcg.PATH_AUTO), (fcg.TOTLAG, fcg.PATH_GENERAL)])
-def test_two_ranks_distributed_newton_pcg(kinem, path):
+def test_two_ranks_distributed_newton_pcg(kinem, path, transport):
     """dsolve.DistributedNewton on 2 ranks (halo import before every SpMV, global dots) converges
-    to the 1-rank StaticNewton solution of the same clamped, tip-loaded box (by DOF GID)."""
+    to the 1-rank StaticNewton solution of the same clamped, tip-loaded box (by DOF GID).
+    transport "staged": both ranks on GPU 0, host-staged gloo; "rccl": one GPU per rank with the
+    RCCL halo and all-reduce inside the solver loop (needs two GPUs; RCCL refuses two ranks on one)."""
     dev = _dev()
+    if transport == "rccl" and torch.cuda.device_count() < 2:
+        pytest.skip("RCCL transport needs two GPUs (RCCL refuses two ranks on one device)")
     newton = importlib.import_module("4c_amd.newton")
     iv, up = (8, 4, 4), (8.0, 4.0, 4.0)
     m = fcg.BoxMesh(fcg.HEX8, iv, upper=up, jitter=0.1, seed=5)
@@ -309,7 +327,8 @@ def test_two_ranks_distributed_newton_pcg(kinem, path):
     ctx = mp.get_context("spawn")
     qq = ctx.Queue()
     port = 29700 + os.getpid() % 1000
-    procs = [ctx.Process(target=_worker_solve, args=(r, 2, port, qq, kinem, path)) for r in range(2)]
+    procs = [ctx.Process(target=_worker_solve, args=(r, 2, port, qq, kinem, path, transport))
+             for r in range(2)]
     for p in procs:
         p.start()
     res = [qq.get(timeout=240) for _ in range(2)]

@@ -66,3 +66,37 @@ def test_forcing_term_sequence():
     assert math.isclose(t1.compute(1, 0.5, 2.0, 0.498), 1e-3, rel_tol=1e-12)
     with pytest.raises(ValueError):
         newton.ForcingTerm("Type 3")
+
+
+def test_accept_linear_solve_rescue_rules():
+    """newton.accept_linear_solve: NOX's Rescue Bad Newton Solve decision, host logic only."""
+    import importlib
+    import math
+    import warnings
+    newton = importlib.import_module("4c_amd.newton")
+    mg = importlib.import_module("4c_amd.multigrid")
+    rec = {}
+    assert newton.accept_linear_solve(lambda: (5, 1e-12), 1e-10, 0, True, rec) == (5, 1e-12)
+    assert "lin_rescued" not in rec
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        assert newton.accept_linear_solve(lambda: (25, 1e-3), 1e-10, 1, True, rec) == (25, 1e-3)
+    assert rec["lin_rescued"] and "Rescue Bad Newton Solve" in str(w[0].message)
+    with pytest.raises(RuntimeError):
+        newton.accept_linear_solve(lambda: (25, 1e-3), 1e-10, 1, False, {})
+    with pytest.raises(RuntimeError):
+        newton.accept_linear_solve(lambda: (25, math.nan), 1e-10, 1, True, {})
+
+    def mg_fail(relres):
+        def f():
+            raise mg.MultigridError("stopped", 30 if relres else None, relres)
+        return f
+    rec = {}
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        assert newton.accept_linear_solve(mg_fail(2e-9), 1e-10, 2, True, rec) == (30, 2e-9)
+    assert rec["lin_rescued"]
+    with pytest.raises(mg.MultigridError):
+        newton.accept_linear_solve(mg_fail(None), 1e-10, 2, True, {})  # indefinite: no direction
+    with pytest.raises(mg.MultigridError):
+        newton.accept_linear_solve(mg_fail(2e-9), 1e-10, 2, False, {})

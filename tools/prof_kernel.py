@@ -16,13 +16,14 @@ ap.add_argument("--celltype", default="hex8")
 ap.add_argument("--kinem", default="linear")
 ap.add_argument("--path", default="auto")
 ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--seed", type=int, default=20251015, help="jitter seed (bench.py's mesh)")
 ap.add_argument("--renumber", action="store_true", help="random node/element numbering (input-file mesh)")
 a = ap.parse_args()
 ct = fcg.HEX8 if a.celltype == "hex8" else fcg.HEX27
 kin = fcg.LINEAR if a.kinem == "linear" else fcg.TOTLAG
 path = {"auto": fcg.PATH_AUTO, "general": fcg.PATH_GENERAL, "structured": fcg.PATH_STRUCTURED,
         "gather": fcg.PATH_GATHER}[a.path]
-m = fcg.BoxMesh(ct, (a.n, a.n, a.n), jitter=0.1 if ct == fcg.HEX8 else 0.02)
+m = fcg.BoxMesh(ct, (a.n, a.n, a.n), jitter=0.1 if ct == fcg.HEX8 else 0.02, seed=a.seed)
 if a.renumber:
     box = m
     m = fcg.Discretization.renumbered(box, seed=1)
