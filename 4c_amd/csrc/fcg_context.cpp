@@ -89,6 +89,34 @@ struct StructHost {
 const int kOff8[8][3] = {{0, 0, 0}, {1, 0, 0}, {1, 1, 0}, {0, 1, 0}, {0, 0, 1}, {1, 0, 1}, {1, 1, 1},
     {0, 1, 1}};  // hex8 4C node order (4C_io_gridgenerator.cpp:371-379)
 
+// Morton (Z-order) key of a point of the box [lo, hi]: 21 bits per axis, interleaved.  Sorting by
+// it puts points that are close in space close in the order (gather plan).
+uint64_t morton_key(const double* x, const double* lo, const double* hi)
+{
+  uint64_t key = 0;
+  uint32_t q[3];
+  for (int k = 0; k < 3; ++k)
+  {
+    const double ext = hi[k] - lo[k];
+    const double t = ext > 0 ? (x[k] - lo[k]) / ext : 0.0;
+    q[k] = uint32_t(std::min(2097151.0, std::max(0.0, t * 2097151.0)));
+  }
+  for (int b = 20; b >= 0; --b)
+    for (int k = 0; k < 3; ++k) key = (key << 1) | ((q[k] >> b) & 1u);
+  return key;
+}
+
+// Permutation sorting items by their Morton keys (ties by index: deterministic)
+std::vector<int64_t> morton_order(const std::vector<uint64_t>& key)
+{
+  std::vector<int64_t> ord(key.size());
+  for (size_t i = 0; i < ord.size(); ++i) ord[i] = int64_t(i);
+  std::sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) {
+    return key[a] != key[b] ? key[a] < key[b] : a < b;
+  });
+  return ord;
+}
+
 bool build_structured_plan(const fcg_desc* d, const std::vector<int32_t>& rownodes,
     const std::vector<int32_t>& row0, const int32_t* kcol, int cus, StructHost& P, std::string& why)
 {
@@ -426,7 +454,7 @@ bool build_colored_plan(const fcg_desc* d, ColorHost& P, std::string& why)
 
 void free_mesh(fcg::DeviceMesh& m)
 {
-  void* ptrs[] = {m.gather_dummy, m.multi_ptr, m.rec_row0, m.rec_meta, m.rec_base, m.rec_ele, m.rec_a, m.rec_tmap, m.ele_x,
+  void* ptrs[] = {m.gather_dummy, m.multi_ptr, m.rec_row0, m.rec_meta, m.rec_base, m.rec_ele, m.rec_a, m.rec_tmap, m.ele_orig, m.ele_x,
       m.ele_dof, m.ele_nodes, m.ele_gid, m.node_x, m.node_dof_col, m.inc_of, m.inc_ptr,
       m.rownode_row0, m.inc_pos, m.rowptr, m.scratch, m.err, m.elem_at, m.lat_x, m.lat_dof,
       m.plane_rec,
@@ -811,19 +839,48 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
     // records of <= 8 incidences per row node (a node without elements keeps one empty record,
     // which zeroes its rows under OVERWRITE): first one record per node with <= 8 elements, in
     // row order, then the records of the other nodes, node by node
+    //
+    // Locality (input-file meshes carry arbitrary node and element numbers): the records follow
+    // the Morton order of their row nodes' coordinates and the element data the Morton order of
+    // the element centroids, so that the wavefronts working at the same time, and the records of
+    // one XCD's contiguous range, share elements and displacements in L2 instead of re-reading
+    // them from HBM (6.7 GB fetched per 1M-hex8 evaluate in random order).
+    double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+    for (int64_t n = 0; n < d->n_node; ++n)
+      for (int k = 0; k < 3; ++k)
+      {
+        lo[k] = std::min(lo[k], d->node_x[3 * n + k]);
+        hi[k] = std::max(hi[k], d->node_x[3 * n + k]);
+      }
+    std::vector<uint64_t> nkey(nrn), ekey(d->n_ele);
+    parallel_for(nrn, [&](int64_t r) { nkey[r] = morton_key(d->node_x + 3 * int64_t(rownodes[r]), lo, hi); });
+    parallel_for(d->n_ele, [&](int64_t e) {
+      double c[3] = {0.0, 0.0, 0.0};
+      for (int b = 0; b < 8; ++b)
+        for (int k = 0; k < 3; ++k) c[k] += 0.125 * d->node_x[3 * int64_t(d->ele_nodes[e * 8 + b]) + k];
+      ekey[e] = morton_key(c, lo, hi);
+    });
+    const std::vector<int64_t> rorder = morton_order(nkey);
+    const std::vector<int64_t> eorder = morton_order(ekey);  // storage slot -> element
+    std::vector<int32_t> eslot(d->n_ele);                     // element -> storage slot
+    for (int64_t i = 0; i < d->n_ele; ++i) eslot[eorder[i]] = int32_t(i);
     std::vector<int64_t> rec_start(nrn), nrec(nrn), multi_ptr(1, 0);
     int64_t n_single = 0;
-    for (int64_t r = 0; r < nrn; ++r)
+    for (int64_t i = 0; i < nrn; ++i)
     {
+      const int64_t r = rorder[i];
       nrec[r] = std::max<int64_t>(1, (inc_ptr[r + 1] - inc_ptr[r] + 7) / 8);
       if (nrec[r] == 1) rec_start[r] = n_single++;
     }
-    for (int64_t r = 0; r < nrn; ++r)
+    for (int64_t i = 0; i < nrn; ++i)
+    {
+      const int64_t r = rorder[i];
       if (nrec[r] > 1)
       {
         rec_start[r] = n_single + multi_ptr.back();
         multi_ptr.push_back(multi_ptr.back() + nrec[r]);
       }
+    }
     for (auto& v : multi_ptr) v += n_single;
     const int64_t n_rec = multi_ptr.back();
     m.n_rec = n_rec;
@@ -848,7 +905,7 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
         // 8 = none) -- stage 4 of the kernel sums a triple's blocks in slot (element) order
         for (int s = 0; s < ns; ++s)
         {
-          rec_ele[R * 8 + s] = inc_ele[k0 + s];
+          rec_ele[R * 8 + s] = eslot[inc_ele[k0 + s]];
           rec_a[R * 8 + s] = inc_a[k0 + s];
           for (int b = 0; b < 8; ++b)
           {
@@ -859,15 +916,18 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
       }
     });
     std::vector<double> ex(d->n_ele * 24);
-    std::vector<int32_t> edof(d->n_ele * 8);
-    parallel_for(d->n_ele, [&](int64_t e) {
+    std::vector<int32_t> edof(d->n_ele * 8), eorig(d->n_ele);
+    parallel_for(d->n_ele, [&](int64_t i) {
+      const int64_t e = eorder[i];
+      eorig[i] = int32_t(e);
       for (int b = 0; b < 8; ++b)
       {
         const int32_t nd = d->ele_nodes[e * 8 + b];
-        for (int k = 0; k < 3; ++k) ex[e * 24 + 3 * b + k] = d->node_x[3 * int64_t(nd) + k];
-        edof[e * 8 + b] = d->node_dof_col[nd];
+        for (int k = 0; k < 3; ++k) ex[i * 24 + 3 * b + k] = d->node_x[3 * int64_t(nd) + k];
+        edof[i * 8 + b] = d->node_dof_col[nd];
       }
     });
+    chk(upload(&m.ele_orig, eorig.data(), d->n_ele, bytes));
     chk(upload(&m.multi_ptr, multi_ptr.data(), int64_t(multi_ptr.size()), bytes));
     chk(upload(&m.rec_row0, rec_row0.data(), n_rec, bytes));
     chk(upload(&m.rec_meta, rec_meta.data(), n_rec, bytes));

@@ -83,6 +83,7 @@ struct GatherArgs {
   const int32_t* rec_ele;    // [n_rec][8] element (-1 = empty slot)
   const uint8_t* rec_a;      // [n_rec][8] local node of the row node in the slot's element
   const uint32_t* rec_tmap;  // [n_rec][32] per column triple of the rows: slot s's node in nibble s
+  const int32_t* ele_orig;   // [n_ele] column element index of each storage slot (error report)
   const double* ele_x;       // [n_ele][8][3]
   const int32_t* ele_dof;    // [n_ele][8] column LID of each node's first DOF
   const double* u_col;
@@ -407,7 +408,7 @@ __global__ __launch_bounds__(64, 2) void gather_h8_kernel(GatherArgs A)
       if (bad)
       {
         bad_code = max(bad_code, bad);
-        bad_ele = min(bad_ele, e);
+        bad_ele = min(bad_ele, A.ele_orig[e]);  // the column element index (4C's loop order)
       }
     }
     __syncthreads();
@@ -618,6 +619,7 @@ hipError_t launch_gather_h8(const DeviceMesh& m, const double* d_u_col, bool wan
   a.rec_ele = m.rec_ele;
   a.rec_a = m.rec_a;
   a.rec_tmap = m.rec_tmap;
+  a.ele_orig = m.ele_orig;
   a.ele_x = m.ele_x;
   a.ele_dof = m.ele_dof;
   a.u_col = d_u_col;

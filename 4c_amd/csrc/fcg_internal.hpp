@@ -57,7 +57,8 @@ struct DeviceMesh {
   int32_t* rec_ele = nullptr;       // [n_rec][8] element of each slot, -1 = empty
   uint8_t* rec_a = nullptr;         // [n_rec][8] local node of the row node in the slot's element
   uint32_t* rec_tmap = nullptr;     // [n_rec][32] per column triple: slot s's element node in nibble s (8 = none)
-  double* ele_x = nullptr;          // [n_ele][8][3] element node coordinates
+  int32_t* ele_orig = nullptr;      // [n_ele] column element index of each storage slot (Morton order)
+  double* ele_x = nullptr;          // [n_ele][8][3] element node coordinates (storage slot order)
   int32_t* ele_dof = nullptr;       // [n_ele][8] column LID of each element node's first DOF
   double* gather_dummy = nullptr;   // [4] store target of a row without columns
 

@@ -54,10 +54,16 @@ def test_totlag_full_size_against_oracle(celltype, n, amp):
     assert np.abs(Kg - Kr).max() <= 1e-12 * np.abs(Kr).max()
 
 
-def test_config3_newton_equilibrium_and_symmetry():
+# the bench's config-3 line (tools/newton_bench.py --celltype hex27 --kinem totlag --n 100 --mg,
+# profiles/r01_config3_hex27_1M_totlag_newton_mg.json): tip displacement u_z at (1, 1, 1)
+CONFIG3_TIP_UZ = -0.03406788471634048
+
+
+@pytest.mark.parametrize("n", [int(os.environ.get("FCG_FULLSIZE_N", "40")), 100])
+def test_config3_newton_equilibrium_and_symmetry(n):
+    """n = 100 is BASELINE config 3 itself (1M hex27, 4.63e9 nonzeros)."""
     import oracle_lib as orc
     dev = _dev()
-    n = int(os.environ.get("FCG_FULLSIZE_N", "40"))
     mg_mod = importlib.import_module("4c_amd.multigrid")
     mesh = fcg.BoxMesh(fcg.HEX27, (n, n, n), upper=(1.0, 1.0, 1.0))
     X = mesh.node_x
@@ -74,6 +80,10 @@ def test_config3_newton_equilibrium_and_symmetry():
     u = nt.solve()
     assert nt.history[-1]["norm_res"] <= 1e-10 * np.linalg.norm(fext), nt.history
     uh = u.cpu().numpy()
+    if n == 100:  # pins the bench's 1M Newton result
+        tip = uh[mesh.node_dof_row[np.argmax(X.sum(axis=1))] + 2]
+        assert abs(tip - CONFIG3_TIP_UZ) <= 1e-9 * abs(CONFIG3_TIP_UZ), tip
+        assert len(nt.history) - 1 <= 6, nt.history
     # symmetry of the tangent at the solution (before Dirichlet rows): x.(K y) == y.(K x)
     K = torch.empty(mesh.nnz, dtype=torch.float64, device=dev)
     f = torch.empty(mesh.n_rows, dtype=torch.float64, device=dev)
