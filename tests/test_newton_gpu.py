@@ -128,23 +128,24 @@ def test_totlag_newton_structured():
 
 def test_rescue_bad_newton_solve_continues_with_truncated_solves():
     """NOX "Rescue Bad Newton Solve" (4C default true, 4C_inpar_solver_nonlin.cpp:65-69): PCG
-    capped at 25 iterations never reaches its tolerance, Newton keeps the inexact directions
-    (each step marked) and still converges to the exact-solve displacement; with the rescue off
-    the first truncated solve raises."""
+    capped at 60 % of the iterations the exact solves take never reaches its tolerance, Newton
+    keeps the inexact directions (each step marked) and still converges to the exact-solve
+    displacement; with the rescue off the first truncated solve raises."""
     _dev()
     mesh, dbc, fext = _cantilever(iv=(6, 3, 3), upper=(6.0, 1.0, 1.0))
     fext *= 2e3
     ev = fcg.Evaluator(mesh, kinematics=fcg.TOTLAG, youngs=E, poisson=NU)
-    u_ref = newton.StaticNewton(ev, fext, dbc, tol_res=1e-10, tol_inc=1e-10,
-                                lin_rtol=1e-14).solve().cpu().numpy()
+    exact = newton.StaticNewton(ev, fext, dbc, tol_res=1e-10, tol_inc=1e-10, lin_rtol=1e-14)
+    u_ref = exact.solve().cpu().numpy()
+    cap = max(10, int(0.6 * max(h["lin_iter"] for h in exact.history if "lin_iter" in h)))
     nt = newton.StaticNewton(ev, fext, dbc, tol_res=1e-8, tol_inc=1e-8, max_iter=200,
-                             lin_rtol=1e-14, lin_max_iter=25)
+                             lin_rtol=1e-14, lin_max_iter=cap)
     with pytest.warns(RuntimeWarning, match="Rescue Bad Newton Solve"):
         u = nt.solve().cpu().numpy()
     assert sum(1 for h in nt.history if h.get("lin_rescued")) >= 2, nt.history
-    assert all(h["lin_iter"] <= 25 for h in nt.history if "lin_iter" in h)
+    assert all(h["lin_iter"] <= cap for h in nt.history if "lin_iter" in h)
     assert rel_err(u, u_ref) <= 1e-6, rel_err(u, u_ref)
-    strict = newton.StaticNewton(ev, fext, dbc, lin_rtol=1e-14, lin_max_iter=25,
+    strict = newton.StaticNewton(ev, fext, dbc, lin_rtol=1e-14, lin_max_iter=cap,
                                  rescue_bad_newton_solve=False)
     with pytest.raises(RuntimeError, match="above its tolerance"):
         strict.solve()
