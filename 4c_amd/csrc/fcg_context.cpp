@@ -454,7 +454,7 @@ bool build_colored_plan(const fcg_desc* d, ColorHost& P, std::string& why)
 
 void free_mesh(fcg::DeviceMesh& m)
 {
-  void* ptrs[] = {m.gather_dummy, m.multi_ptr, m.rec_row0, m.rec_meta, m.rec_base, m.rec_ele, m.rec_a, m.rec_tmap, m.ele_orig, m.ele_x,
+  void* ptrs[] = {m.gather_dummy, m.multi_ptr, m.rec_row0, m.rec_meta, m.rec_base, m.rec_ele, m.rec_a, m.rec_tmap, m.ele_orig, m.inc_ele, m.inc_a, m.asm_order, m.ele_x,
       m.ele_dof, m.ele_nodes, m.ele_gid, m.node_x, m.node_dof_col, m.inc_of, m.inc_ptr,
       m.rownode_row0, m.inc_pos, m.rowptr, m.scratch, m.err, m.elem_at, m.lat_x, m.lat_dof,
       m.plane_rec,
@@ -955,7 +955,32 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
     chk(upload(&m.inc_of, inc_of.data(), d->n_ele * npe, bytes));
     chk(upload(&m.inc_ptr, inc_ptr.data(), nrn + 1, bytes));
     chk(upload(&m.inc_pos, inc_pos.data(), n_inc * npe, bytes));
-    chk(upload<double>(&m.scratch, nullptr, n_inc * fcg::record_doubles(npe), bytes));
+    // hex27 StVK: the matrix-core element kernel with symmetric per-element records
+    // (fcg_hex27.hip; FCG_H27_LEGACY=1 keeps the incidence-record kernels for A/B runs)
+    const char* legacy = std::getenv("FCG_H27_LEGACY");
+    m.h27s = npe == 27 && d->material == FCG_MAT_STVK && !(legacy && legacy[0] == '1');
+    if (m.h27s)
+    {
+      fcg::upload_h27_tables();
+      chk(upload(&m.inc_ele, inc_ele.data(), n_inc, bytes));
+      chk(upload(&m.inc_a, inc_a.data(), n_inc, bytes));
+      // assembly order: Morton order of the row nodes' coordinates
+      double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+      for (int64_t n = 0; n < d->n_node; ++n)
+        for (int k = 0; k < 3; ++k)
+        {
+          lo[k] = std::min(lo[k], d->node_x[3 * n + k]);
+          hi[k] = std::max(hi[k], d->node_x[3 * n + k]);
+        }
+      std::vector<uint64_t> key(nrn);
+      parallel_for(nrn, [&](int64_t r) { key[r] = morton_key(d->node_x + 3 * int64_t(rownodes[r]), lo, hi); });
+      const std::vector<int64_t> ord = morton_order(key);
+      std::vector<int32_t> ord32(ord.begin(), ord.end());
+      chk(upload(&m.asm_order, ord32.data(), nrn, bytes));
+      chk(upload<double>(&m.scratch, nullptr, d->n_ele * fcg::kH27RecDoubles, bytes));
+    }
+    else
+      chk(upload<double>(&m.scratch, nullptr, n_inc * fcg::record_doubles(npe), bytes));
   }
   if (!structured)
   {
@@ -1173,10 +1198,13 @@ int fcg_evaluate_device(fcg_ctx* ctx, int action, int mode, const double* d_u_co
   }
   else
   {
-    if (he == hipSuccess) he = fcg::launch_element(m, d_u_col, want_k, s);
+    if (he == hipSuccess)
+      he = m.h27s ? fcg::launch_h27_element(m, d_u_col, want_k, s)
+                  : fcg::launch_element(m, d_u_col, want_k, s);
     if (T.enabled && he == hipSuccess) he = hipEventRecord(T.ev[1], s);
     if (he == hipSuccess)
-      he = fcg::launch_assemble(m, want_k, mode == FCG_OVERWRITE, d_K_vals, d_fint_row, s);
+      he = m.h27s ? fcg::launch_h27_assemble(m, want_k, mode == FCG_OVERWRITE, d_K_vals, d_fint_row, s)
+                  : fcg::launch_assemble(m, want_k, mode == FCG_OVERWRITE, d_K_vals, d_fint_row, s);
   }
   if (T.enabled && he == hipSuccess)
   {

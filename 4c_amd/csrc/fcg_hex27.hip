@@ -1,0 +1,711 @@
+// fcg_hex27.hip -- hex27 StVenantKirchhoff element evaluation + assembly for any mesh (the general
+// path of BASELINE config 3's element), redesigned around the FP64 matrix cores and a symmetric
+// per-element record.
+//
+//  h27_element_kernel<KIN>  one 256-lane workgroup per element (two per CU), SolidEleCalc's
+//      Gauss-point loop (4C_solid_3D_ele_calc.cpp:110-240, calc_lib.hpp:380-993) in reference
+//      coordinates:
+//        1. lanes (g, coordinate, X|u): J and du/dxi at the 27 Gauss points (dN . X); 27 more
+//           lanes: the nodal det J > 0 check (calc_lib.hpp:475-496);
+//        2. lanes g: J^-1, fac = det J w (calc_lib.hpp:435-448, 974-993), F = I + du/dX
+//           (calc_lib.hpp:579-605), E, StVK S (4C_mat_stvenantkirchhoff.cpp:169-177), and the
+//           per-point 3 x 3 factors that let every later stage work on the constant dN_a(xi_g):
+//             q_a = T d_a  with T = F J^-1 (linear: J^-1)            (B-operator columns F N_XYZ)
+//             fac N_XYZ_a . N_XYZ_b = d_a^T W d_b,  W = fac J^-T J^-1
+//             fac N_XYZ_a . S N_XYZ_b = d_a^T V d_b, V = fac J^-T S J^-1
+//             f_a = sum_g R_g d_a,  R = fac F S J^-1 (linear: fac S J^-1)     (calc_lib.hpp:851-860)
+//        3. the isotropic StVK blocks of every node pair a <= b (B_a^T C B_b + K_geo,
+//           calc_lib.hpp:872-927):
+//             K_ab = lambda G + mu G^T + mu H + geo I          (linear: mu tr(G) I, no H / geo)
+//             G_ij = sum_g fac q_a,i q_b,j     -> v_mfma_f64_16x16x4_f64 (waves 0-2)
+//             H = sum_g (d_a^T W d_b) F F^T, geo = sum_g d_a^T V d_b  -> VALU, 2 pairs a lane
+//           The matrix cores take the 9-FMA part of the 21 FMAs per pair and point; the VALU
+//           lanes the other 12.
+//      Output: one record per element, the 378 blocks a <= b (3 x 3 column-major, pair order
+//      a-major) and f_e (27 x 3) -- 27.9 KB instead of the 53 KB of per-incidence block rows,
+//      since K_ba = K_ab^T is not stored twice.
+//  h27_assemble_kernel  SparseMatrix::assemble + LinAlg::assemble (4C_linalg_sparsematrix.cpp:
+//      444-576, 4C_linalg_utils_sparse_algebra_assemble.cpp:72-92) for owned rows: one wavefront
+//      per owned row node sums the block rows of its incident elements (K_ab or K_ba^T from the
+//      records) in element order in an LDS row image and writes its 3 CSR rows once.  Row nodes
+//      are visited in the Morton order of their coordinates, so the records that concurrently
+//      running wavefronts read stay within a compact piece of the mesh (L2 / Infinity Cache).
+// Fixed summation orders everywhere: bitwise reproducible, no atomics on K or f.
+#include <hip/hip_runtime.h>
+
+#include "fcg_internal.hpp"
+#include "fcg_shape.hpp"
+
+namespace fcg {
+
+namespace {
+
+constexpr int kNpe = 27;
+constexpr int kNpair = 378;
+constexpr int kBlk = 256;
+constexpr int kNchunk = 196;  // VALU pair chunks (a, b0, nb <= 2)
+
+__constant__ double c_dN[27 * 27 * 3];  // dN_c,d at Gauss point g: [g][c][d]
+__constant__ double c_w[27];
+__constant__ double c_L1[9], c_dL1[9], c_dLn[9];  // 1D Lagrange factors (fcg_kernels.hip)
+__constant__ uint8_t c_loc[27], c_latnode[27];
+__constant__ uint32_t c_chunk[kNchunk];  // a | b0 << 8 | nb << 16
+
+__device__ inline int pidx(int a, int b)  // a <= b
+{
+  return 27 * a - (a * (a - 1)) / 2 + b - a;
+}
+
+// invert3x3 of the reference (4C_linalg_fixedsizematrix.hpp:1382-1409), column-major m[r + 3c]
+__device__ inline double inv3(double* m)
+{
+  const double t00 = m[4] * m[8] - m[5] * m[7];
+  const double t10 = m[2] * m[7] - m[1] * m[8];
+  const double t20 = m[1] * m[5] - m[2] * m[4];
+  const double det = m[0] * t00 + m[3] * t10 + m[6] * t20;
+  if (det == 0.0) return 0.0;
+  const double id = 1.0 / det;
+  const double t01 = m[3], t11 = m[4], t12 = m[7];
+  const double r3 = id * (m[5] * m[6] - t01 * m[8]);
+  const double r4 = id * (m[0] * m[8] - m[2] * m[6]);
+  const double r7 = id * (m[1] * m[6] - m[0] * t12);
+  const double r5 = id * (m[2] * t01 - m[0] * m[5]);
+  const double r6 = id * (t01 * t12 - t11 * m[6]);
+  const double r8 = id * (m[0] * t11 - m[1] * t01);
+  m[3] = r3;
+  m[4] = r4;
+  m[7] = r7;
+  m[5] = r5;
+  m[6] = r6;
+  m[8] = r8;
+  m[0] = id * t00;
+  m[1] = id * t10;
+  m[2] = id * t20;
+  return det;
+}
+
+struct H27Shared {
+  double dN[27 * 27 * 3];  // [g][c][d], loaded once per workgroup
+  double X[81], U[81];
+  double J[27 * 9];        // per g: J (col-major r + 3c = d xi_r / ...), then J^-1
+  double Gu[27 * 9];       // per g: du_i / dxi_k at k + 3 i
+  double fac[27];
+  double T[27 * 9];        // per g: T(i, k) at 3 i + k
+  double W[27 * 6], V[27 * 6], M[27 * 6];  // symmetric: xx yy zz xy yz zx
+  double R[27 * 9];        // per g: R(i, k) at 3 i + k
+  // stage views: w, v per (g, a) [27][27][6] (TotLag) | q per (g, a) [27][27][3] |
+  // mu H + geo I per pair [378][7] (TotLag)
+  double work[27 * 27 * 6];
+  double L1[9], dL1[9], dLn[9];
+  int bad;
+  uint8_t loc[27], latnode[27];
+};
+
+struct H27Args {
+  int64_t n_ele;
+  const int32_t* ele_nodes;
+  const double* node_x;
+  const int32_t* node_dof_col;
+  const double* u_col;
+  double* rec;
+  int32_t* err;
+  double lambda, mu, cdiag;
+  int want_k;
+};
+
+typedef double f64x4_t __attribute__((ext_vector_type(4)));
+
+__device__ inline void symv(const double* S, const double* x, double* y)  // y = S x, S sym6
+{
+  y[0] = S[0] * x[0] + S[3] * x[1] + S[5] * x[2];
+  y[1] = S[3] * x[0] + S[1] * x[1] + S[4] * x[2];
+  y[2] = S[5] * x[0] + S[4] * x[1] + S[2] * x[2];
+}
+
+template <int KIN>
+__global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
+{
+  __shared__ H27Shared sh;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  for (int v = tid; v < 27 * 27 * 3; v += kBlk) sh.dN[v] = c_dN[v];
+  if (tid < 9)
+  {
+    sh.L1[tid] = c_L1[tid];
+    sh.dL1[tid] = c_dL1[tid];
+    sh.dLn[tid] = c_dLn[tid];
+  }
+  if (tid < 27)
+  {
+    sh.loc[tid] = c_loc[tid];
+    sh.latnode[tid] = c_latnode[tid];
+  }
+  // VALU pair chunk of this lane (TotLag)
+  const uint32_t chunk = tid < kNchunk ? c_chunk[tid] : 0u;
+  const int ca = chunk & 0xff, cb0 = (chunk >> 8) & 0xff, cnb = tid < kNchunk ? int(chunk >> 16) : 0;
+  const double lam = A.lambda, mu = A.mu;
+
+  for (int64_t e = blockIdx.x; e < A.n_ele; e += gridDim.x)
+  {
+    const int32_t* en = A.ele_nodes + e * kNpe;
+    double* rec = A.rec + e * int64_t(kNpair * 9 + 81);
+    // 0. gather X and u (evaluate_element_nodes, calc_lib.hpp:180-203)
+    if (tid < 81)
+    {
+      const int a = tid / 3, d = tid - 3 * (tid / 3);
+      const int node = en[a];
+      sh.X[tid] = A.node_x[3 * int64_t(node) + d];
+      sh.U[tid] = A.u_col[A.node_dof_col[node] + d];
+    }
+    if (tid == 0) sh.bad = 0;
+    __syncthreads();
+
+    // 1. J and du/dxi at the Gauss points; nodal det J check (calc_lib.hpp:475-496) via the 1D
+    //    factors: at a node they are Kronecker deltas, so J sums the 3 nodes on each line
+    if (tid < 162)
+    {
+      const int g = tid / 6, rem = tid - 6 * (tid / 6);
+      const int k = rem % 3, s = rem / 3;
+      const double* src = s ? sh.U : sh.X;
+      const double* d = sh.dN + 81 * g;
+      double j0 = 0.0, j1 = 0.0, j2 = 0.0;
+#pragma unroll 9
+      for (int c = 0; c < kNpe; ++c)
+      {
+        const double x = src[3 * c + k];
+        j0 += d[3 * c + 0] * x;
+        j1 += d[3 * c + 1] * x;
+        j2 += d[3 * c + 2] * x;
+      }
+      double* dst = (s ? sh.Gu : sh.J) + 9 * g + 3 * k;
+      dst[0] = j0;
+      dst[1] = j1;
+      dst[2] = j2;
+    }
+    else if (tid < 162 + kNpe)
+    {
+      const int g = tid - 162;
+      const uint32_t l = sh.loc[g];
+      const int p = l & 3, q = (l >> 2) & 3, r = l >> 4;
+      double J[9];
+#pragma unroll
+      for (int kk = 0; kk < 9; ++kk) J[kk] = 0.0;
+#pragma unroll
+      for (int m = 0; m < 3; ++m)
+      {
+        const double* x0 = sh.X + 3 * sh.latnode[m + 3 * q + 9 * r];
+        const double* x1 = sh.X + 3 * sh.latnode[p + 3 * m + 9 * r];
+        const double* x2 = sh.X + 3 * sh.latnode[p + 3 * q + 9 * m];
+        const double d0 = sh.dLn[3 * p + m], d1 = sh.dLn[3 * q + m], d2 = sh.dLn[3 * r + m];
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+        {
+          J[3 * c + 0] += d0 * x0[c];
+          J[3 * c + 1] += d1 * x1[c];
+          J[3 * c + 2] += d2 * x2[c];
+        }
+      }
+      const double det = inv3(J);
+      if (det == 0.0) atomicMax(&sh.bad, 2);
+      else if (!(det > 0)) atomicMax(&sh.bad, 1);
+    }
+    __syncthreads();
+
+    // 2. per Gauss point: J^-1, fac, strains, StVK stress and the folded 3 x 3 factors
+    if (tid < kNpe)
+    {
+      const int g = tid;
+      double iJ[9];
+#pragma unroll
+      for (int kk = 0; kk < 9; ++kk) iJ[kk] = sh.J[9 * g + kk];
+      const double det = inv3(iJ);
+      if (det == 0.0) atomicMax(&sh.bad, 2);
+      const double fac = det * c_w[g];
+      sh.fac[g] = fac;
+      // grad u: Hu(i, j) = du_i / dX_j = sum_k J^-1(j, k) du_i / dxi_k
+      double Hu[3][3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          Hu[i][j] = iJ[j] * sh.Gu[9 * g + 3 * i] + iJ[j + 3] * sh.Gu[9 * g + 3 * i + 1] +
+                     iJ[j + 6] * sh.Gu[9 * g + 3 * i + 2];
+      double E[6], F[3][3];
+      if (KIN == 0)
+      {
+        // evaluate_linear_gl_strain (calc_lib.hpp:682-695): engineering shear
+        E[0] = Hu[0][0];
+        E[1] = Hu[1][1];
+        E[2] = Hu[2][2];
+        E[3] = Hu[0][1] + Hu[1][0];
+        E[4] = Hu[1][2] + Hu[2][1];
+        E[5] = Hu[0][2] + Hu[2][0];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) F[i][j] = i == j ? 1.0 : 0.0;
+      }
+      else
+      {
+        // F = I + u N_XYZ^T (hex27, calc_lib.hpp:579-605); F^-1 must exist (calc_lib.hpp:562)
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) F[i][j] = Hu[i][j] + (i == j ? 1.0 : 0.0);
+        double Fi[9];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) Fi[i + 3 * j] = F[i][j];
+        if (inv3(Fi) == 0.0) atomicMax(&sh.bad, 2);
+        // C = F^T F, E = (C - I) / 2 in strain-like Voigt form (calc_lib.hpp:639-676)
+        double C[3][3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) C[i][j] = F[0][i] * F[0][j] + F[1][i] * F[1][j] + F[2][i] * F[2][j];
+        E[0] = 0.5 * (C[0][0] - 1.0);
+        E[1] = 0.5 * (C[1][1] - 1.0);
+        E[2] = 0.5 * (C[2][2] - 1.0);
+        E[3] = C[0][1];
+        E[4] = C[1][2];
+        E[5] = C[0][2];
+      }
+      // S = C E (fill_cmat, 4C_mat_stvenantkirchhoff.cpp:115-145)
+      double S[3][3];
+      S[0][0] = A.cdiag * E[0] + A.lambda * (E[1] + E[2]);
+      S[1][1] = A.cdiag * E[1] + A.lambda * (E[0] + E[2]);
+      S[2][2] = A.cdiag * E[2] + A.lambda * (E[0] + E[1]);
+      S[0][1] = S[1][0] = A.mu * E[3];
+      S[1][2] = S[2][1] = A.mu * E[4];
+      S[0][2] = S[2][0] = A.mu * E[5];
+      // T = F J^-1, R = fac F S J^-1
+      double FS[3][3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) FS[i][j] = F[i][0] * S[0][j] + F[i][1] * S[1][j] + F[i][2] * S[2][j];
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+        {
+          sh.T[9 * g + 3 * i + k] = F[i][0] * iJ[3 * k] + F[i][1] * iJ[3 * k + 1] + F[i][2] * iJ[3 * k + 2];
+          sh.R[9 * g + 3 * i + k] =
+              fac * (FS[i][0] * iJ[3 * k] + FS[i][1] * iJ[3 * k + 1] + FS[i][2] * iJ[3 * k + 2]);
+        }
+      if (KIN == 1)
+      {
+        // W = fac J^-T J^-1, V = fac J^-T S J^-1, M = F F^T  (xx yy zz xy yz zx)
+        double SJ[3][3];  // S J^-1
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int l = 0; l < 3; ++l) SJ[i][l] = S[i][0] * iJ[3 * l] + S[i][1] * iJ[3 * l + 1] + S[i][2] * iJ[3 * l + 2];
+        const int kk[6] = {0, 1, 2, 0, 1, 0}, ll[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+        for (int s = 0; s < 6; ++s)
+        {
+          const int k = kk[s], l = ll[s];
+          // J^-1(j, k) = iJ[j + 3 k]
+          sh.W[6 * g + s] = fac * (iJ[3 * k] * iJ[3 * l] + iJ[3 * k + 1] * iJ[3 * l + 1] + iJ[3 * k + 2] * iJ[3 * l + 2]);
+          sh.V[6 * g + s] = fac * (iJ[3 * k] * SJ[0][l] + iJ[3 * k + 1] * SJ[1][l] + iJ[3 * k + 2] * SJ[2][l]);
+          sh.M[6 * g + s] = F[k][0] * F[l][0] + F[k][1] * F[l][1] + F[k][2] * F[l][2];
+        }
+      }
+    }
+    __syncthreads();
+    if (sh.bad)
+    {
+      if (tid == 0)
+      {
+        atomicMax(&A.err[0], sh.bad);
+        atomicMin(&A.err[1], int32_t(e));
+      }
+      __syncthreads();
+      continue;
+    }
+
+    // 3a / 4. TotLag: w = W d_a, v = V d_a per (g, a); then the VALU pair sums
+    //   mu H + geo I:  H = sum_g (w_a . d_b) M_g,  geo = sum_g v_a . d_b
+    double Hacc[2][7];
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int k = 0; k < 7; ++k) Hacc[p][k] = 0.0;
+    if (KIN == 1 && A.want_k)
+    {
+      for (int it = tid; it < 729; it += kBlk)
+      {
+        const int g = it / 27;
+        const double* d = sh.dN + 3 * it;
+        double* o = sh.work + 6 * it;
+        symv(sh.W + 6 * g, d, o);
+        symv(sh.V + 6 * g, d, o + 3);
+      }
+      __syncthreads();
+      if (tid < kNchunk)
+      {
+        for (int g = 0; g < kNpe; ++g)
+        {
+          const double* wv = sh.work + 6 * (27 * g + ca);
+          const double w0 = wv[0], w1 = wv[1], w2 = wv[2], v0 = wv[3], v1 = wv[4], v2 = wv[5];
+          const double* Mg = sh.M + 6 * g;
+          double m[6];
+#pragma unroll
+          for (int k = 0; k < 6; ++k) m[k] = Mg[k];
+#pragma unroll
+          for (int p = 0; p < 2; ++p)
+          {
+            if (p < cnb)
+            {
+              const double* d = sh.dN + 3 * (27 * g + cb0 + p);
+              const double d0 = d[0], d1 = d[1], d2 = d[2];
+              const double c = w0 * d0 + w1 * d1 + w2 * d2;
+              Hacc[p][6] += v0 * d0 + v1 * d1 + v2 * d2;
+#pragma unroll
+              for (int k = 0; k < 6; ++k) Hacc[p][k] += c * m[k];
+            }
+          }
+        }
+      }
+      __syncthreads();  // every read of w, v done: the region becomes q
+    }
+
+    // 3b. q_a = T d_a per (g, a); f_a = sum_g R_g d_a (add_internal_force_vector)
+    if (A.want_k)
+      for (int it = tid; it < 729; it += kBlk)
+      {
+        const int g = it / 27;
+        const double* d = sh.dN + 3 * it;
+        const double* T = sh.T + 9 * g;
+        double* o = sh.work + 3 * it;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) o[i] = T[3 * i] * d[0] + T[3 * i + 1] * d[1] + T[3 * i + 2] * d[2];
+      }
+    if (tid >= 175 && tid < 256)
+    {
+      const int t = tid - 175;
+      const int a = t / 3, i = t - 3 * (t / 3);
+      double f = 0.0;
+      for (int g = 0; g < kNpe; ++g)
+      {
+        const double* R = sh.R + 9 * g + 3 * i;
+        const double* d = sh.dN + 3 * (27 * g + a);
+        f += R[0] * d[0] + R[1] * d[1] + R[2] * d[2];
+      }
+      rec[kNpair * 9 + t] = f;
+    }
+    if (!A.want_k)
+    {
+      __syncthreads();
+      continue;
+    }
+    __syncthreads();
+
+    // 5. G on the matrix cores: waves 0..2 take the node ranges (0,0), (0,1), (1,1) of 16
+    const int at = wave == 2 ? 1 : 0, bt = wave == 0 ? 0 : 1;
+    const int r16 = lane & 15, kq = lane >> 4;
+    const int a_l = 16 * at + r16, b_l = 16 * bt + r16;
+    const bool va = a_l < 27, vb = b_l < 27;
+    const int a_c = va ? a_l : 0, b_c = vb ? b_l : 0;
+    f64x4_t X[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) X[k] = f64x4_t{0.0, 0.0, 0.0, 0.0};
+    if (wave < 3)
+    {
+#pragma unroll
+      for (int st = 0; st < 7; ++st)
+      {
+        const int g = 4 * st + kq;
+        const bool vg = g < 27;
+        const int gc = vg ? g : 0;
+        const double fg = vg ? sh.fac[gc] : 0.0;
+        const double* qa = sh.work + 3 * (27 * gc + a_c);
+        const double* qb = sh.work + 3 * (27 * gc + b_c);
+        double av[3], bv[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+        {
+          av[i] = va ? fg * qa[i] : 0.0;
+          bv[i] = (vg && vb) ? qb[i] : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j)
+            X[3 * i + j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[j], X[3 * i + j], 0, 0, 0);
+      }
+    }
+    if (KIN == 1)
+    {
+      __syncthreads();  // q dead: the region becomes the mu H + geo I image
+      if (tid < kNchunk)
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          if (p < cnb)
+          {
+            double* o = sh.work + 7 * pidx(ca, cb0 + p);
+            const double geo = Hacc[p][6];
+            o[0] = mu * Hacc[p][0] + geo;
+            o[1] = mu * Hacc[p][1] + geo;
+            o[2] = mu * Hacc[p][2] + geo;
+            o[3] = mu * Hacc[p][3];
+            o[4] = mu * Hacc[p][4];
+            o[5] = mu * Hacc[p][5];
+          }
+      __syncthreads();
+    }
+    if (wave < 3)
+    {
+      const int b = 16 * bt + r16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+      {
+        const int a = 16 * at + kq + 4 * r;
+        if (a < 27 && b < 27 && a <= b)
+        {
+          const int p = pidx(a, b);
+          double* K = rec + 9 * p;
+          double add[9];
+          if (KIN == 0)
+          {
+            const double tr = mu * (X[0][r] + X[4][r] + X[8][r]);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) add[k] = (k == 0 || k == 4 || k == 8) ? tr : 0.0;
+          }
+          else
+          {
+            const double* h = sh.work + 7 * p;
+            add[0] = h[0];
+            add[4] = h[1];
+            add[8] = h[2];
+            add[1] = add[3] = h[3];
+            add[5] = add[7] = h[4];
+            add[2] = add[6] = h[5];
+          }
+#pragma unroll
+          for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+              K[i + 3 * j] = lam * X[3 * i + j][r] + mu * X[3 * j + i][r] + add[i + 3 * j];
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+struct H27AsmArgs {
+  int64_t n_rownodes;
+  const int32_t* order;  // row nodes in Morton order
+  const int64_t* inc_ptr;
+  const int32_t* inc_ele;
+  const uint8_t* inc_a;
+  const uint16_t* inc_pos;
+  const int32_t* rownode_row0;
+  const int64_t* rowptr;
+  const double* rec;
+  double* K;
+  double* fint;
+};
+
+template <bool WANT_K, bool OVERWRITE>
+__global__ __launch_bounds__(64) void h27_assemble_kernel(H27AsmArgs A)
+{
+  constexpr int REC = kNpair * 9 + 81;
+  constexpr int NS = 4;  // entries per lane and incidence: 243 = 3 rows x 27 nodes x 3
+  __shared__ double acc[WANT_K ? 3 * 375 : 1];
+  const int lane = threadIdx.x;
+  // this lane's entries v = lane + 64 s of a node's block row: row i, element node b, column j
+  int ei[NS], eb[NS], ej[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+  {
+    const int v = lane + 64 * s;
+    ei[s] = v / 81;
+    const int rem = v - 81 * ei[s];
+    eb[s] = rem / 3;
+    ej[s] = rem - 3 * eb[s];
+  }
+  for (int64_t it = blockIdx.x; it < A.n_rownodes; it += gridDim.x)
+  {
+    const int64_t r = A.order ? A.order[it] : it;
+    const int32_t row0 = A.rownode_row0[r];
+    const int64_t base = A.rowptr[row0];
+    const int rowlen = int(A.rowptr[row0 + 1] - base);
+    if (WANT_K)
+      for (int v = lane; v < 3 * rowlen; v += 64) acc[v] = 0.0;
+    double f = 0.0;
+    const int64_t k0 = A.inc_ptr[r], k1 = A.inc_ptr[r + 1];
+    double cur[NS], nxt[NS];
+    int dst[NS], ndst[NS];
+    double fc = 0.0, fn = 0.0;
+    auto load = [&](int64_t k, double* val, int* off, double& fv) {
+      const int64_t e = A.inc_ele[k];
+      const int a = A.inc_a[k];
+      const double* src = A.rec + e * int64_t(REC);
+      fv = lane < 3 ? src[kNpair * 9 + 3 * a + lane] : 0.0;
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+      {
+        val[s] = 0.0;
+        off[s] = -1;
+        if (!WANT_K || lane + 64 * s >= 243) continue;
+        const int b = eb[s];
+        const bool up = a <= b;
+        const int p = up ? pidx(a, b) : pidx(b, a);
+        val[s] = src[9 * p + (up ? ei[s] + 3 * ej[s] : ej[s] + 3 * ei[s])];
+        off[s] = ei[s] * rowlen + A.inc_pos[k * kNpe + b] + ej[s];
+      }
+    };
+    if (k0 < k1) load(k0, cur, dst, fc);
+    for (int64_t k = k0; k < k1; ++k)
+    {
+      if (k + 1 < k1)
+        load(k + 1, nxt, ndst, fn);
+      else
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+        {
+          nxt[s] = 0.0;
+          ndst[s] = -1;
+        }
+      if (WANT_K)
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+          if (dst[s] >= 0) acc[dst[s]] += cur[s];
+      f += fc;
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+      {
+        cur[s] = nxt[s];
+        dst[s] = ndst[s];
+      }
+      fc = fn;
+    }
+    __syncthreads();
+    if (WANT_K)
+    {
+      double* out = A.K + base;  // the node's 3 rows are contiguous (checked at setup)
+      for (int v = lane; v < 3 * rowlen; v += 64)
+      {
+        if (OVERWRITE)
+          out[v] = acc[v];
+        else
+          out[v] += acc[v];
+      }
+    }
+    if (lane < 3)
+    {
+      if (OVERWRITE)
+        A.fint[row0 + lane] = f;
+      else
+        A.fint[row0 + lane] += f;
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+void upload_h27_tables()
+{
+  static bool done = false;
+  if (done) return;
+  double xi[81], w[27];
+  gauss_rule(kHex27, xi, w);
+  double dN[27 * 27 * 3];
+  for (int g = 0; g < 27; ++g) shape_deriv(kHex27, &xi[3 * g], &dN[81 * g]);
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(c_dN), dN, sizeof(dN));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(c_w), w, sizeof(w));
+  // 1D quadratic Lagrange factors as fcg_kernels.hip: L_i'(x_p) at the nodes x = -1, 0, 1
+  double dLn[9], L1[9], dL1[9];
+  const double xs[3] = {xi[3 * 0], xi[3 * 8], xi[3 * 1]};
+  for (int p = 0; p < 3; ++p)
+  {
+    const double r = xs[p], t = double(p - 1);
+    L1[3 * p + 0] = 0.5 * r * (r - 1.0);
+    L1[3 * p + 1] = 1.0 - r * r;
+    L1[3 * p + 2] = 0.5 * r * (r + 1.0);
+    dL1[3 * p + 0] = r - 0.5;
+    dL1[3 * p + 1] = -2.0 * r;
+    dL1[3 * p + 2] = r + 0.5;
+    dLn[3 * p + 0] = t - 0.5;
+    dLn[3 * p + 1] = -2.0 * t;
+    dLn[3 * p + 2] = t + 0.5;
+  }
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(c_L1), L1, sizeof(L1));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(c_dL1), dL1, sizeof(dL1));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(c_dLn), dLn, sizeof(dLn));
+  uint8_t loc[27], latnode[27];
+  for (int a = 0; a < 27; ++a)
+  {
+    loc[a] = uint8_t(kHex27NodePos[a][0] | (kHex27NodePos[a][1] << 2) | (kHex27NodePos[a][2] << 4));
+    latnode[kHex27NodePos[a][0] + 3 * kHex27NodePos[a][1] + 9 * kHex27NodePos[a][2]] = uint8_t(a);
+  }
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(c_loc), loc, sizeof(loc));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(c_latnode), latnode, sizeof(latnode));
+  uint32_t chunk[kNchunk];
+  int n = 0;
+  for (int a = 0; a < 27; ++a)
+    for (int b = a; b < 27; b += 2) chunk[n++] = uint32_t(a | (b << 8) | ((b + 1 < 27 ? 2 : 1) << 16));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(c_chunk), chunk, sizeof(chunk));
+  done = true;
+}
+
+hipError_t launch_h27_element(const DeviceMesh& m, const double* d_u_col, bool want_k,
+    hipStream_t stream)
+{
+  if (m.n_ele == 0) return hipSuccess;
+  H27Args a{};
+  a.n_ele = m.n_ele;
+  a.ele_nodes = m.ele_nodes;
+  a.node_x = m.node_x;
+  a.node_dof_col = m.node_dof_col;
+  a.u_col = d_u_col;
+  a.rec = m.scratch;
+  a.err = m.err;
+  a.lambda = m.lambda;
+  a.mu = m.mu;
+  a.cdiag = m.cdiag;
+  a.want_k = want_k ? 1 : 0;
+  const int64_t cap = 256 * 8;
+  const dim3 grid(unsigned(m.n_ele < cap ? m.n_ele : cap)), block(kBlk);
+  if (m.kinem == 0)
+    hipLaunchKernelGGL((h27_element_kernel<0>), grid, block, 0, stream, a);
+  else
+    hipLaunchKernelGGL((h27_element_kernel<1>), grid, block, 0, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_h27_assemble(const DeviceMesh& m, bool want_k, bool overwrite, double* d_K,
+    double* d_fint, hipStream_t stream)
+{
+  if (m.n_rownodes == 0) return hipSuccess;
+  H27AsmArgs a{};
+  a.n_rownodes = m.n_rownodes;
+  a.order = m.asm_order;
+  a.inc_ptr = m.inc_ptr;
+  a.inc_ele = m.inc_ele;
+  a.inc_a = m.inc_a;
+  a.inc_pos = m.inc_pos;
+  a.rownode_row0 = m.rownode_row0;
+  a.rowptr = m.rowptr;
+  a.rec = m.scratch;
+  a.K = d_K;
+  a.fint = d_fint;
+  const int64_t cap = 256 * 32;
+  const dim3 grid(unsigned(m.n_rownodes < cap ? m.n_rownodes : cap)), block(64);
+  if (want_k && overwrite)
+    hipLaunchKernelGGL((h27_assemble_kernel<true, true>), grid, block, 0, stream, a);
+  else if (want_k)
+    hipLaunchKernelGGL((h27_assemble_kernel<true, false>), grid, block, 0, stream, a);
+  else if (overwrite)
+    hipLaunchKernelGGL((h27_assemble_kernel<false, true>), grid, block, 0, stream, a);
+  else
+    hipLaunchKernelGGL((h27_assemble_kernel<false, false>), grid, block, 0, stream, a);
+  return hipGetLastError();
+}
+
+}  // namespace fcg

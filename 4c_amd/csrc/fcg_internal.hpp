@@ -57,6 +57,11 @@ struct DeviceMesh {
   int32_t* rec_ele = nullptr;       // [n_rec][8] element of each slot, -1 = empty
   uint8_t* rec_a = nullptr;         // [n_rec][8] local node of the row node in the slot's element
   uint32_t* rec_tmap = nullptr;     // [n_rec][32] per column triple: slot s's element node in nibble s (8 = none)
+  // hex27 StVK general path (fcg_hex27.hip): per-element symmetric records in `scratch`
+  bool h27s = false;
+  int32_t* inc_ele = nullptr;       // [n_inc] element of each incidence
+  uint8_t* inc_a = nullptr;         // [n_inc] local node of the row node in that element
+  int32_t* asm_order = nullptr;     // [n_rownodes] row nodes in Morton order of their coordinates
   int32_t* ele_orig = nullptr;      // [n_ele] column element index of each storage slot (Morton order)
   double* ele_x = nullptr;          // [n_ele][8][3] element node coordinates (storage slot order)
   int32_t* ele_dof = nullptr;       // [n_ele][8] column LID of each element node's first DOF
@@ -135,6 +140,14 @@ hipError_t launch_element(const DeviceMesh& m, const double* d_u_col, bool want_
 hipError_t launch_element_colored(const DeviceMesh& m, const double* d_u_col, bool want_k,
     bool overwrite, double* d_K, double* d_fint, hipStream_t stream);
 hipError_t launch_assemble(const DeviceMesh& m, bool want_k, bool overwrite, double* d_K,
+    double* d_fint, hipStream_t stream);
+// hex27 StVK on any mesh (fcg_hex27.hip): element kernel writing one symmetric record per
+// element (blocks a <= b + f_e), then one wavefront per owned row node in Morton order.
+void upload_h27_tables();
+constexpr int64_t kH27RecDoubles = 378 * 9 + 81;
+hipError_t launch_h27_element(const DeviceMesh& m, const double* d_u_col, bool want_k,
+    hipStream_t stream);
+hipError_t launch_h27_assemble(const DeviceMesh& m, bool want_k, bool overwrite, double* d_K,
     double* d_fint, hipStream_t stream);
 // Node-row gather (FCG_PATH_GATHER, hex8 StVK on any mesh): one wavefront per owned row node
 // (fcg_gather.hip).
