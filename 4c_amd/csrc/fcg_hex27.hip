@@ -44,6 +44,7 @@ constexpr int kNpe = 27;
 constexpr int kNpair = 378;
 constexpr int kBlk = 256;
 constexpr int kNchunk = 196;  // VALU pair chunks (a, b0, nb <= 2)
+constexpr int64_t kRec = kH27RecDoubles;  // 378 blocks x 9 | f 27 x 3 | pad
 
 __constant__ double c_dN[27 * 27 * 3];  // dN_c,d at Gauss point g: [g][c][d]
 __constant__ double c_w[27];
@@ -84,21 +85,36 @@ __device__ inline double inv3(double* m)
   return det;
 }
 
+// LDS of one element's workgroup.  `big` holds stage-dependent views (offsets below):
+//   J | Gu | T | W | V | M | R (Gauss-point data, dead after the matrix-core phase) followed by
+//   the pair-stage work area: w, v per (g, a) [27][27][6] (TotLag) | q per (g, a) [27][27][3];
+//   after the matrix-core phase the mu H + geo I image [378][7] lies at H_IMG (TotLag) and the
+//   element's K image [378][9] at 0: disjoint, so a lane reads its H entries and writes its K
+//   blocks without a barrier in between.
+constexpr int OFF_J = 0, OFF_GU = 243, OFF_T = 486, OFF_W = 729, OFF_V = 891, OFF_M = 1053,
+              OFF_R = 1215, OFF_WORK = 1458, OFF_KIMG = 0, OFF_HIMG = kNpair * 9;
+constexpr int BIG = OFF_HIMG + kNpair * 7;  // >= OFF_WORK + 27 * 27 * 6
+static_assert(BIG >= OFF_WORK + 27 * 27 * 6, "work area");
 struct H27Shared {
   double dN[27 * 27 * 3];  // [g][c][d], loaded once per workgroup
-  double X[81], U[81];
-  double J[27 * 9];        // per g: J (col-major r + 3c = d xi_r / ...), then J^-1
-  double Gu[27 * 9];       // per g: du_i / dxi_k at k + 3 i
+  double X[2][81], U[2][81];  // double-buffered: the next element's arrive during this one
   double fac[27];
-  double T[27 * 9];        // per g: T(i, k) at 3 i + k
-  double W[27 * 6], V[27 * 6], M[27 * 6];  // symmetric: xx yy zz xy yz zx
-  double R[27 * 9];        // per g: R(i, k) at 3 i + k
-  // stage views: w, v per (g, a) [27][27][6] (TotLag) | q per (g, a) [27][27][3] |
-  // mu H + geo I per pair [378][7] (TotLag)
-  double work[27 * 27 * 6];
+  alignas(16) double big[BIG];
   double L1[9], dL1[9], dLn[9];
   int bad;
   uint8_t loc[27], latnode[27];
+  // views: J per g col-major (r + 3c), then J^-1 | du_i/dxi_k at k + 3i | T(i, k) at 3i + k |
+  // W, V, M symmetric (xx yy zz xy yz zx) | R(i, k) at 3i + k
+  __device__ double* J() { return big + OFF_J; }
+  __device__ double* Gu() { return big + OFF_GU; }
+  __device__ double* T() { return big + OFF_T; }
+  __device__ double* W() { return big + OFF_W; }
+  __device__ double* V() { return big + OFF_V; }
+  __device__ double* M() { return big + OFF_M; }
+  __device__ double* R() { return big + OFF_R; }
+  __device__ double* work() { return big + OFF_WORK; }
+  __device__ double* kimg() { return big + OFF_KIMG; }
+  __device__ double* himg() { return big + OFF_HIMG; }
 };
 
 struct H27Args {
@@ -145,20 +161,35 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
   const int ca = chunk & 0xff, cb0 = (chunk >> 8) & 0xff, cnb = tid < kNchunk ? int(chunk >> 16) : 0;
   const double lam = A.lambda, mu = A.mu;
 
-  for (int64_t e = blockIdx.x; e < A.n_ele; e += gridDim.x)
-  {
-    const int32_t* en = A.ele_nodes + e * kNpe;
-    double* rec = A.rec + e * int64_t(kNpair * 9 + 81);
-    // 0. gather X and u (evaluate_element_nodes, calc_lib.hpp:180-203)
-    if (tid < 81)
+  // 0. X and u of the element (evaluate_element_nodes, calc_lib.hpp:180-203) are loaded one
+  //    element ahead: the dependent chain node id -> coordinates / DOF -> u is issued at the top
+  //    of an element and lands in the other LDS buffer before that element's first global store
+  //    (gfx9 counts stores in vmcnt: a wait for loads issued after stores would wait for those)
+  double xpre = 0.0, upre = 0.0;
+  auto prefetch = [&](int64_t e) {
+    if (tid < 81 && e < A.n_ele)
     {
       const int a = tid / 3, d = tid - 3 * (tid / 3);
-      const int node = en[a];
-      sh.X[tid] = A.node_x[3 * int64_t(node) + d];
-      sh.U[tid] = A.u_col[A.node_dof_col[node] + d];
+      const int node = A.ele_nodes[e * kNpe + a];
+      xpre = A.node_x[3 * int64_t(node) + d];
+      upre = A.u_col[A.node_dof_col[node] + d];
     }
+  };
+  prefetch(blockIdx.x);
+  if (tid < 81)
+  {
+    sh.X[0][tid] = xpre;
+    sh.U[0][tid] = upre;
+  }
+  int buf = 0;
+  for (int64_t e = blockIdx.x; e < A.n_ele; e += gridDim.x, buf ^= 1)
+  {
+    double* rec = A.rec + e * kRec;
     if (tid == 0) sh.bad = 0;
     __syncthreads();
+    prefetch(e + gridDim.x);
+    const double* Xe = sh.X[buf];
+    const double* Ue = sh.U[buf];
 
     // 1. J and du/dxi at the Gauss points; nodal det J check (calc_lib.hpp:475-496) via the 1D
     //    factors: at a node they are Kronecker deltas, so J sums the 3 nodes on each line
@@ -166,7 +197,7 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
     {
       const int g = tid / 6, rem = tid - 6 * (tid / 6);
       const int k = rem % 3, s = rem / 3;
-      const double* src = s ? sh.U : sh.X;
+      const double* src = s ? Ue : Xe;
       const double* d = sh.dN + 81 * g;
       double j0 = 0.0, j1 = 0.0, j2 = 0.0;
 #pragma unroll 9
@@ -177,7 +208,7 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
         j1 += d[3 * c + 1] * x;
         j2 += d[3 * c + 2] * x;
       }
-      double* dst = (s ? sh.Gu : sh.J) + 9 * g + 3 * k;
+      double* dst = (s ? sh.Gu() : sh.J()) + 9 * g + 3 * k;
       dst[0] = j0;
       dst[1] = j1;
       dst[2] = j2;
@@ -193,9 +224,9 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
 #pragma unroll
       for (int m = 0; m < 3; ++m)
       {
-        const double* x0 = sh.X + 3 * sh.latnode[m + 3 * q + 9 * r];
-        const double* x1 = sh.X + 3 * sh.latnode[p + 3 * m + 9 * r];
-        const double* x2 = sh.X + 3 * sh.latnode[p + 3 * q + 9 * m];
+        const double* x0 = Xe + 3 * sh.latnode[m + 3 * q + 9 * r];
+        const double* x1 = Xe + 3 * sh.latnode[p + 3 * m + 9 * r];
+        const double* x2 = Xe + 3 * sh.latnode[p + 3 * q + 9 * m];
         const double d0 = sh.dLn[3 * p + m], d1 = sh.dLn[3 * q + m], d2 = sh.dLn[3 * r + m];
 #pragma unroll
         for (int c = 0; c < 3; ++c)
@@ -217,7 +248,7 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
       const int g = tid;
       double iJ[9];
 #pragma unroll
-      for (int kk = 0; kk < 9; ++kk) iJ[kk] = sh.J[9 * g + kk];
+      for (int kk = 0; kk < 9; ++kk) iJ[kk] = sh.J()[9 * g + kk];
       const double det = inv3(iJ);
       if (det == 0.0) atomicMax(&sh.bad, 2);
       const double fac = det * c_w[g];
@@ -228,8 +259,8 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
       for (int i = 0; i < 3; ++i)
 #pragma unroll
         for (int j = 0; j < 3; ++j)
-          Hu[i][j] = iJ[j] * sh.Gu[9 * g + 3 * i] + iJ[j + 3] * sh.Gu[9 * g + 3 * i + 1] +
-                     iJ[j + 6] * sh.Gu[9 * g + 3 * i + 2];
+          Hu[i][j] = iJ[j] * sh.Gu()[9 * g + 3 * i] + iJ[j + 3] * sh.Gu()[9 * g + 3 * i + 1] +
+                     iJ[j + 6] * sh.Gu()[9 * g + 3 * i + 2];
       double E[6], F[3][3];
       if (KIN == 0)
       {
@@ -290,8 +321,8 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
 #pragma unroll
         for (int k = 0; k < 3; ++k)
         {
-          sh.T[9 * g + 3 * i + k] = F[i][0] * iJ[3 * k] + F[i][1] * iJ[3 * k + 1] + F[i][2] * iJ[3 * k + 2];
-          sh.R[9 * g + 3 * i + k] =
+          sh.T()[9 * g + 3 * i + k] = F[i][0] * iJ[3 * k] + F[i][1] * iJ[3 * k + 1] + F[i][2] * iJ[3 * k + 2];
+          sh.R()[9 * g + 3 * i + k] =
               fac * (FS[i][0] * iJ[3 * k] + FS[i][1] * iJ[3 * k + 1] + FS[i][2] * iJ[3 * k + 2]);
         }
       if (KIN == 1)
@@ -308,13 +339,18 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
         {
           const int k = kk[s], l = ll[s];
           // J^-1(j, k) = iJ[j + 3 k]
-          sh.W[6 * g + s] = fac * (iJ[3 * k] * iJ[3 * l] + iJ[3 * k + 1] * iJ[3 * l + 1] + iJ[3 * k + 2] * iJ[3 * l + 2]);
-          sh.V[6 * g + s] = fac * (iJ[3 * k] * SJ[0][l] + iJ[3 * k + 1] * SJ[1][l] + iJ[3 * k + 2] * SJ[2][l]);
-          sh.M[6 * g + s] = F[k][0] * F[l][0] + F[k][1] * F[l][1] + F[k][2] * F[l][2];
+          sh.W()[6 * g + s] = fac * (iJ[3 * k] * iJ[3 * l] + iJ[3 * k + 1] * iJ[3 * l + 1] + iJ[3 * k + 2] * iJ[3 * l + 2]);
+          sh.V()[6 * g + s] = fac * (iJ[3 * k] * SJ[0][l] + iJ[3 * k + 1] * SJ[1][l] + iJ[3 * k + 2] * SJ[2][l]);
+          sh.M()[6 * g + s] = F[k][0] * F[l][0] + F[k][1] * F[l][1] + F[k][2] * F[l][2];
         }
       }
     }
     __syncthreads();
+    if (tid < 81)  // the next element's X and u, before this one's first global store
+    {
+      sh.X[buf ^ 1][tid] = xpre;
+      sh.U[buf ^ 1][tid] = upre;
+    }
     if (sh.bad)
     {
       if (tid == 0)
@@ -339,18 +375,18 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
       {
         const int g = it / 27;
         const double* d = sh.dN + 3 * it;
-        double* o = sh.work + 6 * it;
-        symv(sh.W + 6 * g, d, o);
-        symv(sh.V + 6 * g, d, o + 3);
+        double* o = sh.work() + 6 * it;
+        symv(sh.W() + 6 * g, d, o);
+        symv(sh.V() + 6 * g, d, o + 3);
       }
       __syncthreads();
       if (tid < kNchunk)
       {
         for (int g = 0; g < kNpe; ++g)
         {
-          const double* wv = sh.work + 6 * (27 * g + ca);
+          const double* wv = sh.work() + 6 * (27 * g + ca);
           const double w0 = wv[0], w1 = wv[1], w2 = wv[2], v0 = wv[3], v1 = wv[4], v2 = wv[5];
-          const double* Mg = sh.M + 6 * g;
+          const double* Mg = sh.M() + 6 * g;
           double m[6];
 #pragma unroll
           for (int k = 0; k < 6; ++k) m[k] = Mg[k];
@@ -378,8 +414,8 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
       {
         const int g = it / 27;
         const double* d = sh.dN + 3 * it;
-        const double* T = sh.T + 9 * g;
-        double* o = sh.work + 3 * it;
+        const double* T = sh.T() + 9 * g;
+        double* o = sh.work() + 3 * it;
 #pragma unroll
         for (int i = 0; i < 3; ++i) o[i] = T[3 * i] * d[0] + T[3 * i + 1] * d[1] + T[3 * i + 2] * d[2];
       }
@@ -390,7 +426,7 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
       double f = 0.0;
       for (int g = 0; g < kNpe; ++g)
       {
-        const double* R = sh.R + 9 * g + 3 * i;
+        const double* R = sh.R() + 9 * g + 3 * i;
         const double* d = sh.dN + 3 * (27 * g + a);
         f += R[0] * d[0] + R[1] * d[1] + R[2] * d[2];
       }
@@ -421,8 +457,8 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
         const bool vg = g < 27;
         const int gc = vg ? g : 0;
         const double fg = vg ? sh.fac[gc] : 0.0;
-        const double* qa = sh.work + 3 * (27 * gc + a_c);
-        const double* qb = sh.work + 3 * (27 * gc + b_c);
+        const double* qa = sh.work() + 3 * (27 * gc + a_c);
+        const double* qb = sh.work() + 3 * (27 * gc + b_c);
         double av[3], bv[3];
 #pragma unroll
         for (int i = 0; i < 3; ++i)
@@ -437,15 +473,15 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
             X[3 * i + j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[j], X[3 * i + j], 0, 0, 0);
       }
     }
+    __syncthreads();  // q dead: the region becomes the mu H + geo I image (TotLag) / K image
     if (KIN == 1)
     {
-      __syncthreads();  // q dead: the region becomes the mu H + geo I image
       if (tid < kNchunk)
 #pragma unroll
         for (int p = 0; p < 2; ++p)
           if (p < cnb)
           {
-            double* o = sh.work + 7 * pidx(ca, cb0 + p);
+            double* o = sh.himg() + 7 * pidx(ca, cb0 + p);
             const double geo = Hacc[p][6];
             o[0] = mu * Hacc[p][0] + geo;
             o[1] = mu * Hacc[p][1] + geo;
@@ -456,6 +492,9 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
           }
       __syncthreads();
     }
+    // K_ab = lambda G + mu G^T + (mu tr G I | mu H + geo I) into the LDS image of the record,
+    // which then leaves as contiguous 16-byte pieces: one store instruction covers 1 KB of the
+    // record instead of 64 scattered 8-byte entries
     if (wave < 3)
     {
       const int b = 16 * bt + r16;
@@ -465,8 +504,6 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
         const int a = 16 * at + kq + 4 * r;
         if (a < 27 && b < 27 && a <= b)
         {
-          const int p = pidx(a, b);
-          double* K = rec + 9 * p;
           double add[9];
           if (KIN == 0)
           {
@@ -476,7 +513,7 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
           }
           else
           {
-            const double* h = sh.work + 7 * p;
+            const double* h = sh.himg() + 7 * pidx(a, b);
             add[0] = h[0];
             add[4] = h[1];
             add[8] = h[2];
@@ -484,6 +521,7 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
             add[5] = add[7] = h[4];
             add[2] = add[6] = h[5];
           }
+          double* K = sh.kimg() + 9 * pidx(a, b);
 #pragma unroll
           for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -491,6 +529,12 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
               K[i + 3 * j] = lam * X[3 * i + j][r] + mu * X[3 * j + i][r] + add[i + 3 * j];
         }
       }
+    }
+    __syncthreads();
+    {
+      const double2* src = reinterpret_cast<const double2*>(sh.kimg());
+      double2* dst = reinterpret_cast<double2*>(rec);  // records are 16-byte aligned (kRec even)
+      for (int v = tid; v < kNpair * 9 / 2; v += kBlk) dst[v] = src[v];
     }
     __syncthreads();
   }
@@ -513,21 +557,53 @@ struct H27AsmArgs {
 template <bool WANT_K, bool OVERWRITE>
 __global__ __launch_bounds__(64) void h27_assemble_kernel(H27AsmArgs A)
 {
-  constexpr int REC = kNpair * 9 + 81;
-  constexpr int NS = 4;  // entries per lane and incidence: 243 = 3 rows x 27 nodes x 3
+  constexpr int NS = 4;  // 243 entries of a node's block row (3 rows x 27 nodes x 3) over 64 lanes
+  constexpr int NB = 3;  // incidences in flight
   __shared__ double acc[WANT_K ? 3 * 375 : 1];
   const int lane = threadIdx.x;
-  // this lane's entries v = lane + 64 s of a node's block row: row i, element node b, column j
-  int ei[NS], eb[NS], ej[NS];
+  // Entry t of incidence (e, a), lanes reading consecutive record addresses:
+  //   t <  9 (27 - a): the contiguous blocks (a, b >= a) from pidx(a, a) on, K_ab col-major;
+  //   t >= 9 (27 - a): block (b, a) of b = (t - 9 (27 - a)) / 9 < a, read transposed (K_ab = K_ba^T).
+  struct Inc {
+    double val[NS];
+    int off[NS];
+    double f;
+  };
+  auto load = [&](int64_t k, int rowlen, Inc& c) {
+    const int64_t e = A.inc_ele[k];
+    const int a = A.inc_a[k];
+    const double* src = A.rec + e * kRec;
+    const uint16_t* pos = A.inc_pos + k * kNpe;
+    const int n1 = 9 * (27 - a), p0 = 9 * pidx(a, a);
+    c.f = lane < 3 ? src[kNpair * 9 + 3 * a + lane] : 0.0;
 #pragma unroll
-  for (int s = 0; s < NS; ++s)
-  {
-    const int v = lane + 64 * s;
-    ei[s] = v / 81;
-    const int rem = v - 81 * ei[s];
-    eb[s] = rem / 3;
-    ej[s] = rem - 3 * eb[s];
-  }
+    for (int s = 0; s < NS; ++s)
+    {
+      const int t = lane + 64 * s;
+      c.val[s] = 0.0;
+      c.off[s] = -1;
+      if (!WANT_K || t >= 243) continue;
+      int addr, b, i, j;
+      if (t < n1)
+      {
+        const int q = t / 9, kk = t - 9 * q;
+        b = a + q;
+        i = kk % 3;
+        j = kk / 3;
+        addr = p0 + t;
+      }
+      else
+      {
+        const int tt = t - n1, q = tt / 9, kk = tt - 9 * q;
+        b = q;
+        i = kk / 3;
+        j = kk % 3;
+        addr = 9 * pidx(b, a) + kk;
+      }
+      c.val[s] = src[addr];
+      c.off[s] = i * rowlen + pos[b] + j;
+    }
+  };
   for (int64_t it = blockIdx.x; it < A.n_rownodes; it += gridDim.x)
   {
     const int64_t r = A.order ? A.order[it] : it;
@@ -538,51 +614,24 @@ __global__ __launch_bounds__(64) void h27_assemble_kernel(H27AsmArgs A)
       for (int v = lane; v < 3 * rowlen; v += 64) acc[v] = 0.0;
     double f = 0.0;
     const int64_t k0 = A.inc_ptr[r], k1 = A.inc_ptr[r + 1];
-    double cur[NS], nxt[NS];
-    int dst[NS], ndst[NS];
-    double fc = 0.0, fn = 0.0;
-    auto load = [&](int64_t k, double* val, int* off, double& fv) {
-      const int64_t e = A.inc_ele[k];
-      const int a = A.inc_a[k];
-      const double* src = A.rec + e * int64_t(REC);
-      fv = lane < 3 ? src[kNpair * 9 + 3 * a + lane] : 0.0;
+    Inc ring[NB];
 #pragma unroll
-      for (int s = 0; s < NS; ++s)
-      {
-        val[s] = 0.0;
-        off[s] = -1;
-        if (!WANT_K || lane + 64 * s >= 243) continue;
-        const int b = eb[s];
-        const bool up = a <= b;
-        const int p = up ? pidx(a, b) : pidx(b, a);
-        val[s] = src[9 * p + (up ? ei[s] + 3 * ej[s] : ej[s] + 3 * ei[s])];
-        off[s] = ei[s] * rowlen + A.inc_pos[k * kNpe + b] + ej[s];
-      }
-    };
-    if (k0 < k1) load(k0, cur, dst, fc);
-    for (int64_t k = k0; k < k1; ++k)
+    for (int q = 0; q < NB; ++q)
+      if (k0 + q < k1) load(k0 + q, rowlen, ring[q]);
+    for (int64_t k = k0; k < k1; k += NB)
     {
-      if (k + 1 < k1)
-        load(k + 1, nxt, ndst, fn);
-      else
 #pragma unroll
-        for (int s = 0; s < NS; ++s)
-        {
-          nxt[s] = 0.0;
-          ndst[s] = -1;
-        }
-      if (WANT_K)
-#pragma unroll
-        for (int s = 0; s < NS; ++s)
-          if (dst[s] >= 0) acc[dst[s]] += cur[s];
-      f += fc;
-#pragma unroll
-      for (int s = 0; s < NS; ++s)
+      for (int q = 0; q < NB; ++q)
       {
-        cur[s] = nxt[s];
-        dst[s] = ndst[s];
+        if (k + q >= k1) break;
+        Inc& c = ring[q];
+        if (WANT_K)
+#pragma unroll
+          for (int s = 0; s < NS; ++s)
+            if (c.off[s] >= 0) acc[c.off[s]] += c.val[s];
+        f += c.f;
+        if (k + q + NB < k1) load(k + q + NB, rowlen, c);
       }
-      fc = fn;
     }
     __syncthreads();
     if (WANT_K)

@@ -144,7 +144,7 @@ hipError_t launch_assemble(const DeviceMesh& m, bool want_k, bool overwrite, dou
 // hex27 StVK on any mesh (fcg_hex27.hip): element kernel writing one symmetric record per
 // element (blocks a <= b + f_e), then one wavefront per owned row node in Morton order.
 void upload_h27_tables();
-constexpr int64_t kH27RecDoubles = 378 * 9 + 81;
+constexpr int64_t kH27RecDoubles = 378 * 9 + 81 + 1;  // even: 16-byte aligned records
 hipError_t launch_h27_element(const DeviceMesh& m, const double* d_u_col, bool want_k,
     hipStream_t stream);
 hipError_t launch_h27_assemble(const DeviceMesh& m, bool want_k, bool overwrite, double* d_K,
