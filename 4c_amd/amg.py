@@ -389,14 +389,18 @@ class NativeAMG:
     as AMG: solve(K, b, x, rtol, max_iter) -> (iterations, relative residual)."""
 
     def __init__(self, mesh, ev, dbc_rows, **opts):
+        """On a rank of a multi-rank partition (column map = owned DOFs first, then ghosts) the
+        AMG is built on the rank's owned block: the local preconditioner of dsolve.NativeDFCG."""
         L = fcg.lib()
         info = ev.info
         n_rows = int(info.n_rows)
-        if int(info.n_cols) != n_rows or n_rows % 3:
-            raise ValueError("NativeAMG is single-rank: the column map must be the row map")
-        ndr = np.asarray(mesh.node_dof_row, dtype=np.int64)
-        order = np.argsort(ndr, kind="stable")
-        if not np.array_equal(ndr[order], 3 * np.arange(n_rows // 3)):
+        if n_rows % 3:
+            raise ValueError("NativeAMG needs 3 DOFs per owned node")
+        ndr_all = np.asarray(mesh.node_dof_row, dtype=np.int64)
+        own = np.nonzero(ndr_all >= 0)[0]
+        ndr = ndr_all[own]
+        order = own[np.argsort(ndr, kind="stable")]
+        if not np.array_equal(ndr_all[order], 3 * np.arange(n_rows // 3)):
             raise ValueError("NativeAMG needs node-major DOFs: row 3b + d = DOF d of the b-th node")
         self.ev, self.dev = ev, torch.device("cuda", ev.device)
         self.rows = np.sort(np.asarray(dbc_rows, dtype=np.int32))

@@ -180,6 +180,9 @@ struct fcg_amg {
   std::vector<void*> allocs;
   double setup_ms = 0.0;
   bool ready = false;  // a numeric setup has been made (fcg_amg_setup)
+  // rank-local preconditioner of a multi-rank context: level 0 is the owned block (ghost column
+  // triples dropped) and is applied through its BSR copy instead of the context's fcg_spmv
+  bool local = false;
 };
 
 namespace fcg_amgs {
@@ -277,6 +280,16 @@ void dot_dev(fcg_amg* h, const double* a, const double* b, int64_t n, double* ou
   hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(kBlock), 0, s, h->partial, int(g), out);
 }
 
+// level 0: the context's SpMV (single rank), or the owned block's BSR copy (local)
+void apply_A0(fcg_amg* h, const double* K, const double* x, double* y, hipStream_t s)
+{
+  if (h->local)
+    ck(fcg_bsr_spmv(h->device, 3, 3, h->A0.n, h->A0.ptr, h->A0.col, h->A0.vals, x, y, 1.0, 0, s),
+        "fcg_bsr_spmv (level 0)");
+  else
+    ck(fcg_spmv(h->ctx, K, x, y, s), "fcg_spmv");
+}
+
 // a level's operator and smoother pieces: l = 0 the context, l >= 1 levels[l - 1]
 struct Ops {
   fcg_amg* h;
@@ -287,7 +300,7 @@ struct Ops {
   void spmv(const double* x, double* y) const
   {
     if (l == 0)
-      ck(fcg_spmv(h->ctx, K, x, y, s), "fcg_spmv");
+      apply_A0(h, K, x, y, s);
     else
     {
       const Bsr& A = h->levels[size_t(l - 1)].A;
@@ -476,9 +489,10 @@ void vcycle(fcg_amg* h, int l, const double* K, const double* b, double* x, hipS
 void setup(fcg_amg* h, const double* K, hipStream_t s)
 {
   ck(fcg_block_jacobi_setup(h->ctx, K, h->ctx_dinv, s), "singular nodal block of K (block Jacobi)");
-  estimate_lmax(Ops{h, 0, K, s});
+  // the BSR copy first: the local level 0 applies it in the lambda_max estimate
   ck(fcg_bsr_from_node_csr(h->device, h->nb0, h->ctx->mesh.rowptr, h->A0.ptr, K, h->A0.vals, s),
       "fcg_bsr_from_node_csr");
+  estimate_lmax(Ops{h, 0, K, s});
   ck(fcg_bsr_block_jacobi_setup(h->device, 3, h->nb0, h->A0.ptr, h->A0_diag, h->A0.vals, h->A0_dinv,
          h->flag, s),
       "singular nodal block of K");
@@ -534,7 +548,7 @@ void run_fcg(fcg_amg* h, const double* K, const double* b, double* x, double rto
   while (it < max_iter)
   {
     ++it;
-    ck(fcg_spmv(h->ctx, K, pp, q, s), "fcg_spmv");
+    apply_A0(h, K, pp, q, s);
     dot_dev(h, pp, q, n, sc + 1, s);
     hipLaunchKernelGGL(fcg_step_kernel, g, bl, 0, s, rz, sc + 1, pp, q, x, r, ro, n);
     dot_dev(h, r, r, n, sc + 3, s);
@@ -582,14 +596,15 @@ int fcg_amg_create(fcg_ctx* ctx, const int64_t* rowptr, const int32_t* col_lid,
     return FCG_ERR_ARG;
   *out = nullptr;
   const fcg::DeviceMesh& m = ctx->mesh;
-  if (!m.square_local || m.n_rows % 3 != 0 || m.n_rows == 0)
+  if (!m.owned_cols_first || m.n_rows % 3 != 0 || m.n_rows == 0)
   {
-    ctx->last_error = "fcg_amg_create: single-rank system with 3 DOFs per node rows 3b..3b+2";
+    ctx->last_error = "fcg_amg_create: 3 DOFs per owned node (rows 3b..3b+2), owned columns first";
     return FCG_ERR_ARG;
   }
   fcg_amg* h = new fcg_amg();
   h->ctx = ctx;
   h->device = ctx->device;
+  h->local = !m.square_local;
   if (opt) h->opt = *opt;
   else fcg_amg_default_options(&h->opt);
   try
@@ -599,13 +614,20 @@ int fcg_amg_create(fcg_ctx* ctx, const int64_t* rowptr, const int32_t* col_lid,
     h->n0 = n;
     h->nb0 = nb;
     // level 0 block graph: block row b = rows 3b..3b+2 (one pattern of DOF triples)
+    // (local: the owned block only -- owned column LIDs are < n and, the columns being sorted,
+    // come before every ghost column)
     std::vector<int64_t> bptr(size_t(nb) + 1, 0);
     for (int64_t b = 0; b < nb; ++b)
     {
       const int64_t len = rowptr[3 * b + 1] - rowptr[3 * b];
       if (len % 3 != 0 || rowptr[3 * b + 2] - rowptr[3 * b + 1] != len || rowptr[3 * b + 3] - rowptr[3 * b + 2] != len)
         throw Fail{FCG_ERR_ARG, "fcg_amg_create: rows 3b..3b+2 must share one pattern of DOF triples"};
-      bptr[size_t(b) + 1] = bptr[size_t(b)] + len / 3;
+      int64_t own = 0;
+      while (own < len / 3 && col_lid[rowptr[3 * b] + 3 * own] < n) ++own;
+      for (int64_t k = own; k < len / 3; ++k)
+        if (col_lid[rowptr[3 * b] + 3 * k] < n)
+          throw Fail{FCG_ERR_ARG, "fcg_amg_create: row columns must be sorted (owned before ghosts)"};
+      bptr[size_t(b) + 1] = bptr[size_t(b)] + own;
     }
     std::vector<int32_t> bcol(size_t(bptr.back()));
     for (int64_t b = 0; b < nb; ++b)
@@ -823,6 +845,31 @@ int fcg_amg_levels(const fcg_amg* h) { return h ? int(h->levels.size()) + 1 : 0;
 double fcg_amg_setup_ms(const fcg_amg* h) { return h ? h->setup_ms : -1.0; }
 
 const char* fcg_amg_last_error(const fcg_amg* h) { return h ? h->last_error.c_str() : ""; }
+
+int fcg_amg_apply(fcg_amg* h, const double* d_K_vals, const double* d_r_row, double* d_z_row,
+    void* stream)
+{
+  using namespace fcg_amgs;
+  if (!h || !d_K_vals || !d_r_row || !d_z_row) return FCG_ERR_ARG;
+  if (!h->ready)
+  {
+    h->last_error = "fcg_amg_apply: no numeric setup (call fcg_amg_setup first)";
+    return FCG_ERR_ARG;
+  }
+  try
+  {
+    ck(hipSetDevice(h->device), "hipSetDevice");
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->ctx->stream;
+    vcycle(h, 0, d_K_vals, d_r_row, d_z_row, s);
+  }
+  catch (const Fail& f)
+  {
+    h->last_error = f.msg;
+    h->ctx->last_error = f.msg;
+    return f.code;
+  }
+  return FCG_OK;
+}
 
 int fcg_amg_destroy(fcg_amg* h)
 {

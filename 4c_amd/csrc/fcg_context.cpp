@@ -769,11 +769,11 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
   // preconditioner need them) and whether the matrix column map is the row map (single rank)
   {
     std::vector<int64_t> diag(d->n_rows, -1);
-    bool square = d->n_rows == d->n_cols;
+    bool rowcol = 3 * int64_t(rownodes.size()) == d->n_rows;  // owned column triple == row triple
     for (size_t r = 0; r < rownodes.size(); ++r)
     {
       const int32_t nd = rownodes[r];
-      if (kcol[nd] != row0[r]) square = false;
+      if (kcol[nd] != row0[r]) rowcol = false;
       for (int dd = 0; dd < 3; ++dd)
       {
         const int64_t row = row0[r] + dd;
@@ -783,7 +783,8 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
         if (it != e && *it == kcol[nd] + dd) diag[row] = d->rowptr[row] + (it - b);
       }
     }
-    m.square_local = square;
+    m.square_local = rowcol && d->n_rows == d->n_cols;
+    m.owned_cols_first = rowcol;
     chk(upload(&m.col_lid, d->col_lid, m.nnz, bytes));
     chk(upload(&m.diag_pos, diag.data(), d->n_rows, bytes));
   }

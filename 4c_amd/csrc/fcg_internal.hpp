@@ -83,6 +83,7 @@ struct DeviceMesh {
   int32_t* col_lid = nullptr;       // [nnz] CSR column LIDs (matrix column map)
   int64_t* diag_pos = nullptr;      // [n_rows] position of the diagonal entry in K values, -1 = none
   bool square_local = false;        // matrix column map == row map (single rank)
+  bool owned_cols_first = false;    // column LID of every owned DOF == its row LID (ghosts after)
   double* pcg_work = nullptr;       // PCG vectors and partial sums (allocated on first solve)
   int64_t pcg_n = 0;
 };

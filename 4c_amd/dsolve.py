@@ -133,13 +133,84 @@ class DistributedPCG:
         return it, rn / bn
 
 
+class NativeDFCG:
+    """fcg_dfcg_solve: the same distributed solve as one native call (fcg_dsolve.hip) -- flexible
+    CG with one import per SpMV and all-reduced inner products, preconditioned by the rank's
+    NativeAMG on its owned block (amg) or the nodal block Jacobi (amg=None).  `transport`:
+    a Transport over RCCL (halo.Comm) or host-staged (gloo callbacks into the library).  Same
+    solve(K, b, x, rtol, max_iter) interface as DistributedPCG."""
+
+    def __init__(self, evaluator, transport, amg=None):
+        self.ev, self.tr, self.amg = evaluator, transport, amg
+        self.dev = torch.device("cuda", evaluator.device)
+        self._keep = []
+        L = fcg.lib()
+        t = fcg.FcgTransport()
+        if not transport.staged:
+            self._pair = fcg.FcgRcclPair(transport.comm._h.value, transport.imp._h.value)
+            rc = L.fcg_transport_rccl(ctypes.byref(self._pair), ctypes.byref(t))
+            if rc != 0:
+                raise fcg.FcgError(rc, "fcg_transport_rccl failed")
+        else:
+            imp = transport.imp
+            send = torch.empty(max(1, imp.n_send), dtype=torch.float64, device=self.dev)
+            recv = torch.empty(max(1, imp.n_recv), dtype=torch.float64, device=self.dev)
+
+            def import_cb(_user, x_row, x_col, stream):
+                try:
+                    Lb = fcg.lib()
+                    rc = Lb.fcg_halo_pack(imp._h, x_row, x_col, _ptr(send), stream)
+                    if rc != 0:
+                        return rc
+                    torch.cuda.synchronize(self.dev)
+                    rb = torch.empty(imp.n_recv, dtype=torch.float64)
+                    dist.all_to_all_single(rb, send[:imp.n_send].cpu(), output_split_sizes=imp.recv_counts,
+                                           input_split_sizes=imp.send_counts)
+                    recv[:imp.n_recv].copy_(rb)
+                    torch.cuda.synchronize(self.dev)
+                    return Lb.fcg_halo_unpack(imp._h, _ptr(recv), x_col, stream)
+                except Exception:  # noqa: BLE001 - surfaced as an error code
+                    return fcg.FCG_ERR_DEVICE
+
+            def allreduce_cb(_user, d_vals, n, _stream):
+                try:
+                    Lb = fcg.lib()
+                    h = np.zeros(n)
+                    if Lb.fcg_memcpy_d2h(h.ctypes.data_as(ctypes.c_void_p), d_vals, 8 * n) != 0:
+                        return fcg.FCG_ERR_DEVICE
+                    ht = torch.from_numpy(h)
+                    if dist.is_initialized() and dist.get_world_size() > 1:
+                        dist.all_reduce(ht)
+                    return Lb.fcg_memcpy_h2d(d_vals, ht.numpy().ctypes.data_as(ctypes.c_void_p), 8 * n)
+                except Exception:  # noqa: BLE001
+                    return fcg.FCG_ERR_DEVICE
+
+            t.import_fn = fcg.IMPORT_FN(import_cb)
+            t.allreduce_fn = fcg.ALLREDUCE_FN(allreduce_cb)
+            self._keep += [t.import_fn, t.allreduce_fn, send, recv]
+        self._t = t
+        self.iterations, self.rel_residual = 0, None
+
+    def solve(self, K, b, x, rtol=1e-10, max_iter=10000):
+        it, rel = ctypes.c_int(0), ctypes.c_double(0.0)
+        s = ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+        rc = fcg.lib().fcg_dfcg_solve(self.ev._h, self.amg._h if self.amg is not None else None,
+                                      ctypes.byref(self._t), _ptr(K), _ptr(b), _ptr(x), float(rtol),
+                                      int(max_iter), s, ctypes.byref(it), ctypes.byref(rel))
+        if rc != 0:
+            raise fcg.FcgError(rc, fcg.lib().fcg_last_error(self.ev._h).decode())
+        self.iterations, self.rel_residual = it.value, rel.value
+        return it.value, rel.value
+
+
 class DistributedNewton:
     """Static full Newton on the ranks of a ghost-layer partition: the rank's Evaluator (its
     column elements, owned rows), the halo Transport, the owned rows' external force and
     Dirichlet row LIDs.  solve() returns the converged owned-row displacement."""
 
     def __init__(self, evaluator, transport, fext_row, dbc_rows, tol_res=1e-10, tol_inc=1e-10,
-                 max_iter=20, lin_rtol=1e-12, lin_max_iter=100000, rescue_bad_newton_solve=True):
+                 max_iter=20, lin_rtol=1e-12, lin_max_iter=100000, rescue_bad_newton_solve=True,
+                 linear_solver=None):
         info = evaluator.info
         self.ev, self.tr = evaluator, transport
         self.dev = torch.device("cuda", evaluator.device)
@@ -156,7 +227,9 @@ class DistributedNewton:
         self.tol_res, self.tol_inc, self.max_iter = tol_res, tol_inc, max_iter
         self.lin_rtol, self.lin_max_iter = lin_rtol, lin_max_iter
         self.rescue = rescue_bad_newton_solve  # NOX "Rescue Bad Newton Solve" (newton.StaticNewton)
-        self.pcg = DistributedPCG(evaluator, transport)
+        # linear_solver: e.g. NativeDFCG (the native solve with a rank-local AMG); default the
+        # block-Jacobi DistributedPCG
+        self.pcg = linear_solver if linear_solver is not None else DistributedPCG(evaluator, transport)
         self.history = []
 
     def _norm(self, v):

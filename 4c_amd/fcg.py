@@ -82,6 +82,20 @@ ALLTOALLV_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, _i64p, ctypes.c_v
                                 ctypes.c_int64, ctypes.c_void_p)
 FCG_OP_SUM, FCG_OP_MAX = 0, 1
 BOX_GHOSTED, BOX_STRICT = 0, 1
+# fcg_transport (distributed solve): import (user, d_x_row, d_x_col, stream), all-reduce (user,
+# d_vals, n, stream), both -> int
+IMPORT_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                             ctypes.c_void_p)
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                ctypes.c_void_p)
+
+
+class FcgTransport(ctypes.Structure):
+    _fields_ = [("import_fn", IMPORT_FN), ("allreduce_fn", ALLREDUCE_FN), ("user", ctypes.c_void_p)]
+
+
+class FcgRcclPair(ctypes.Structure):
+    _fields_ = [("comm", ctypes.c_void_p), ("halo", ctypes.c_void_p)]
 
 
 class FcgTsiDesc(ctypes.Structure):
@@ -132,7 +146,8 @@ EXPORTS = ["fcg_create", "fcg_destroy", "fcg_last_error", "fcg_evaluate", "fcg_e
            "fcg_bsr_block_jacobi_setup", "fcg_bsr_block_jacobi_apply", "fcg_amg_smooth_prolongator",
            "fcg_bsr_to_dense", "fcg_amg_default_options", "fcg_amg_create", "fcg_amg_solve",
            "fcg_amg_levels", "fcg_amg_level_info", "fcg_amg_setup_ms", "fcg_amg_last_error",
-           "fcg_amg_destroy", "fcg_amg_setup", "fcg_amg_iterate"]
+           "fcg_amg_destroy", "fcg_amg_setup", "fcg_amg_iterate", "fcg_amg_apply",
+           "fcg_transport_rccl", "fcg_dfcg_solve"]
 
 _lib = None
 FUNCT_FN = ctypes.CFUNCTYPE(ctypes.c_double, ctypes.c_int, _dp, ctypes.c_double, ctypes.c_void_p)
@@ -271,6 +286,10 @@ def lib():
     L.fcg_amg_last_error.argtypes = [vp]
     L.fcg_amg_last_error.restype = ctypes.c_char_p
     L.fcg_amg_destroy.argtypes = [vp]
+    L.fcg_amg_apply.argtypes = [vp, vp, vp, vp, vp]
+    L.fcg_transport_rccl.argtypes = [ctypes.POINTER(FcgRcclPair), ctypes.POINTER(FcgTransport)]
+    L.fcg_dfcg_solve.argtypes = [vp, vp, ctypes.POINTER(FcgTransport), vp, vp, vp, c_dbl, c_int, vp,
+                                 ctypes.POINTER(c_int), _dp]
     _lib = L
     return L
 

@@ -571,6 +571,40 @@ int fcg_shared_unpack(fcg_shared* s, const double* d_buf, double* d_f, void* str
 int fcg_norm2(fcg_comm* comm, const double* d_x, int64_t n, void* stream, double* out);
 
 /* ------------------------------------------------------------------------------------------
+ * Linear solve across ranks (what 4C hands to Belos with a MueLu / Ifpack preconditioner on
+ * every rank, 4C_solver_nonlin_nox_linearsystem.cpp:275-353,
+ * 4C_linear_solver_preconditioner_muelu.cpp): flexible CG on the ghost-layer partition.  Per
+ * iteration: one import of the search direction into the column map (Epetra_CrsMatrix::Multiply's
+ * Importer), one fcg_spmv of the rank's owned rows, one preconditioner application local to the
+ * rank -- the rank's fcg_amg on its owned block (subdomain AMG, additive Schwarz without overlap)
+ * or, with amg = NULL, the nodal 3 x 3 block Jacobi -- and two all-reduces of a few scalars.
+ * Data movement goes through an fcg_transport: fcg_transport_rccl (fcg_halo_import + ncclAllReduce
+ * of a device buffer), or caller callbacks (MPI, or a host-staged rehearsal).  K holds the
+ * Dirichlet unit rows (fcg_dirichlet_apply); the context's column map must start with its owned
+ * DOFs in row order (Epetra's local-first column maps).  Blocking; x starts at 0.
+ * ---------------------------------------------------------------------------------------- */
+typedef int (*fcg_import_fn)(void* user, const double* d_x_row, double* d_x_col, void* stream);
+typedef int (*fcg_allreduce_fn)(void* user, double* d_vals, int64_t n, void* stream);  /* in place, sum */
+typedef struct fcg_transport {
+  fcg_import_fn import_fn;
+  fcg_allreduce_fn allreduce_fn;
+  void* user;
+} fcg_transport;
+/* The RCCL transport of (comm, halo): fills *out; `pair` (caller-owned, alive while used) holds
+ * the two handles the callbacks receive as `user`. */
+typedef struct fcg_rccl_pair {
+  fcg_comm* comm;
+  fcg_halo* halo;
+} fcg_rccl_pair;
+int fcg_transport_rccl(fcg_rccl_pair* pair, fcg_transport* out);
+/* AMG as the rank's local preconditioner: one V-cycle z = M^-1 r on the owned block after
+ * fcg_amg_setup (fcg_amg_create accepts a multi-rank context: ghost columns are dropped). */
+int fcg_amg_apply(fcg_amg* amg, const double* d_K_vals, const double* d_r_row, double* d_z_row, void* stream);
+int fcg_dfcg_solve(fcg_ctx* ctx, fcg_amg* amg, const fcg_transport* tr, const double* d_K_vals,
+    const double* d_b_row, double* d_x_row, double rtol, int max_iter, void* stream,
+    int* iterations, double* rel_residual);
+
+/* ------------------------------------------------------------------------------------------
  * Deferred error check.  With fcg_set_async(ctx, 1), fcg_evaluate_device returns once the work is
  * queued on the stream (no drain, no host round trip per call); 4C's throws (FCG_ERR_NODAL_DETJ,
  * FCG_ERR_SINGULAR) are then reported by fcg_check_error, which waits for the queued evaluates

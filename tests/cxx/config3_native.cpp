@@ -1,0 +1,380 @@
+// config3_native.cpp -- BASELINE config 3's problem solved by a C++ host through the C ABI alone
+// (TEST INFRASTRUCTURE): the StVK TotLag hex27 cube [0,1]^3, x = 0 clamped, traction -1 in z on
+// x = 1 (tools/newton_bench.py's problem), GridGenerator box split over R ranks.  The ranks run as
+// R threads on one GPU with an in-process stand-in for MPI (shared-memory all-to-all-v and sums,
+// the role Epetra_MpiComm plays in 4C).  Per rank, the Newton loop of Solid statics:
+//   set_state          import of the owned displacement into the column map (fcg_halo_pack /
+//                      fcg_halo_unpack around the host exchange; RCCL's fcg_halo_import on GPUs)
+//   evaluate           fcg_evaluate_device(NLNSTIFF, OVERWRITE)
+//   residual, norms    r = f_int - f_ext, global |r| and |du| (all-reduce)
+//   Dirichlet          fcg_dirichlet_apply
+//   linear solve       fcg_dfcg_solve with the rank's fcg_amg on its owned block
+// R = 1 and R = 2 must reach the same displacement (by DOF GID), and the loop must converge
+// quadratically as the reference's full Newton does.
+//
+// usage: config3_native N R     (N elements per direction, R ranks; prints PASS / FAIL)
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "fourc_gpu.h"
+
+namespace {
+
+constexpr double kE = 210.0, kNu = 0.3;
+
+// ------------------------------------------------------------ the in-process "MPI" of R threads
+struct ThreadComm {
+  int n;
+  std::mutex m;
+  std::condition_variable cv;
+  int arrived = 0;
+  long gen = 0;
+  bool failed = false;  // a rank gave up: the others leave their barriers instead of hanging
+  std::vector<std::vector<char>> buf;
+  std::vector<std::vector<int64_t>> cnt;
+  explicit ThreadComm(int n_) : n(n_), buf(size_t(n_)), cnt(size_t(n_)) {}
+  void barrier()
+  {
+    std::unique_lock<std::mutex> lk(m);
+    const long g = gen;
+    if (++arrived == n)
+    {
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+    }
+    else
+      cv.wait(lk, [&] { return gen != g || failed; });
+  }
+  void fail()
+  {
+    std::lock_guard<std::mutex> lk(m);
+    failed = true;
+    cv.notify_all();
+  }
+  bool ok()
+  {
+    std::lock_guard<std::mutex> lk(m);
+    return !failed;
+  }
+  // MPI_Alltoallv: rank r sends scounts[p] items to p (packed in rank order)
+  void alltoallv(int r, const void* send, const int64_t* sc, void* recv, const int64_t* rc, int64_t item)
+  {
+    int64_t ns = 0;
+    for (int p = 0; p < n; ++p) ns += sc[p];
+    buf[size_t(r)].assign(static_cast<const char*>(send), static_cast<const char*>(send) + ns * item);
+    cnt[size_t(r)].assign(sc, sc + n);
+    barrier();
+    if (!ok()) return;
+    int64_t ro = 0;
+    for (int p = 0; p < n; ++p)
+    {
+      int64_t off = 0;
+      for (int q = 0; q < r; ++q) off += cnt[size_t(p)][size_t(q)];
+      if (cnt[size_t(p)][size_t(r)] != rc[p]) std::abort();  // inconsistent plan: a test bug
+      std::memcpy(static_cast<char*>(recv) + ro * item, buf[size_t(p)].data() + off * item, size_t(rc[p] * item));
+      ro += rc[p];
+    }
+    barrier();
+  }
+  // MPI_Allreduce(SUM), rank order (deterministic)
+  void sum(int r, double* v, int64_t k)
+  {
+    buf[size_t(r)].assign(reinterpret_cast<char*>(v), reinterpret_cast<char*>(v) + k * 8);
+    barrier();
+    if (!ok()) return;
+    for (int64_t i = 0; i < k; ++i)
+    {
+      double t = 0.0;
+      for (int p = 0; p < n; ++p) t += reinterpret_cast<const double*>(buf[size_t(p)].data())[i];
+      v[i] = t;
+    }
+    barrier();
+  }
+};
+
+struct RankComm {
+  ThreadComm* tc;
+  int rank;
+};
+
+int xchg(const void* send, const int64_t* sc, void* recv, const int64_t* rc, int64_t item, void* user)
+{
+  auto* c = static_cast<RankComm*>(user);
+  c->tc->alltoallv(c->rank, send, sc, recv, rc, item);
+  return c->tc->ok() ? 0 : FCG_ERR_DEVICE;
+}
+
+// the halo over the host exchange + the sums, as an fcg_transport
+struct HostTransport {
+  RankComm rc;
+  fcg_halo* halo;
+  const fcg_import_plan* plan;
+  double* d_send;
+  double* d_recv;
+  std::vector<double> hs, hr;
+};
+
+int tr_import(void* user, const double* x_row, double* x_col, void* stream)
+{
+  auto* t = static_cast<HostTransport*>(user);
+  int rc = fcg_halo_pack(t->halo, x_row, x_col, t->d_send, stream);
+  if (rc != FCG_OK) return rc;
+  if ((rc = fcg_memcpy_d2h(t->hs.data(), t->d_send, int64_t(t->hs.size()) * 8)) != FCG_OK) return rc;
+  t->rc.tc->alltoallv(t->rc.rank, t->hs.data(), t->plan->send_counts, t->hr.data(), t->plan->recv_counts, 8);
+  if (!t->rc.tc->ok()) return FCG_ERR_DEVICE;
+  if ((rc = fcg_memcpy_h2d(t->d_recv, t->hr.data(), int64_t(t->hr.size()) * 8)) != FCG_OK) return rc;
+  return fcg_halo_unpack(t->halo, t->d_recv, x_col, stream);
+}
+
+int tr_sum(void* user, double* d_vals, int64_t n, void*)
+{
+  auto* t = static_cast<HostTransport*>(user);
+  std::vector<double> h(static_cast<size_t>(n));
+  int rc = fcg_memcpy_d2h(h.data(), d_vals, n * 8);
+  if (rc != FCG_OK) return rc;
+  t->rc.tc->sum(t->rc.rank, h.data(), n);
+  if (!t->rc.tc->ok()) return FCG_ERR_DEVICE;
+  return fcg_memcpy_h2d(d_vals, h.data(), n * 8);
+}
+
+struct RankResult {
+  std::map<int32_t, double> u;  // DOF GID -> displacement
+  std::vector<double> norm_res;
+  std::vector<int> lin_iters;
+  bool ok = false;
+  std::string err;
+};
+
+std::mutex g_create;  // contexts are created one at a time (library setup is per process)
+
+void run_rank(int n, int nranks, int rank, ThreadComm* tc, RankResult* out)
+{
+  auto fail = [&](const std::string& what) {
+    out->err = what;
+    out->ok = false;
+    tc->fail();
+  };
+  fcg_box box{};
+  box.celltype = FCG_HEX27;
+  for (int k = 0; k < 3; ++k)
+  {
+    box.interval[k] = n;
+    box.lower[k] = 0.0;
+    box.upper[k] = 1.0;
+  }
+  fcg_box_mesh* bm = nullptr;
+  fcg_desc d{};
+  fcg_ctx* ctx = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_create);
+    if (fcg_box_mesh_create_ex(&box, rank, nranks, FCG_BOX_GHOSTED, &bm) != FCG_OK) return fail("box mesh");
+    fcg_box_mesh_desc(bm, FCG_TOTLAG, kE, kNu, 0, &d);
+    if (fcg_create(&d, &ctx) != FCG_OK) return fail(std::string("fcg_create: ") + fcg_last_error(nullptr));
+  }
+  const int32_t *row_gid, *col_gid, *node_owner;
+  const int64_t* node_gid;
+  fcg_box_mesh_maps(bm, &row_gid, &col_gid, &node_gid, &node_owner);
+  const int64_t nr = d.n_rows, nc = d.n_cols;
+  // column owners, the import plan (collective) and its device copy
+  std::vector<int32_t> col_owner(static_cast<size_t>(nc));
+  for (int64_t v = 0; v < d.n_node; ++v)
+    for (int k = 0; k < 3; ++k) col_owner[size_t(d.node_dof_col[v] + k)] = node_owner[v];
+  RankComm rcm{tc, rank};
+  fcg_import_plan plan{};
+  void* plan_store = nullptr;
+  if (fcg_import_plan_build(rank, nranks, nr, row_gid, nc, col_gid, col_owner.data(), xchg, &rcm, &plan,
+          &plan_store) != FCG_OK)
+    return fail("fcg_import_plan_build");
+  fcg_halo* halo = nullptr;
+  if (fcg_halo_create(&plan, 0, &halo) != FCG_OK) return fail("fcg_halo_create");
+  int64_t ns = 0, nrv = 0;
+  for (int p = 0; p < nranks; ++p)
+  {
+    ns += plan.send_counts[p];
+    nrv += plan.recv_counts[p];
+  }
+  HostTransport ht{rcm, halo, &plan, nullptr, nullptr, std::vector<double>(size_t(std::max<int64_t>(1, ns))),
+      std::vector<double>(size_t(std::max<int64_t>(1, nrv)))};
+  void *d_send, *d_recv;
+  fcg_device_alloc(0, 8 * std::max<int64_t>(1, ns), &d_send);
+  fcg_device_alloc(0, 8 * std::max<int64_t>(1, nrv), &d_recv);
+  ht.d_send = static_cast<double*>(d_send);
+  ht.d_recv = static_cast<double*>(d_recv);
+  fcg_transport tr{tr_import, tr_sum, &ht};
+
+  // external load: traction (0, 0, -1) on the x = 1 face (quad9 faces of the last element layer)
+  std::vector<int32_t> faces;
+  for (int64_t e = 0; e < d.n_ele; ++e)
+    if (d.ele_ijk[3 * e] == n - 1)
+      for (int a : {1, 2, 6, 5, 9, 14, 17, 13, 22}) faces.push_back(d.ele_nodes[e * 27 + a]);
+  std::vector<double> fext(static_cast<size_t>(nr), 0.0);
+  const int32_t onoff[3] = {1, 1, 1};
+  const double val[3] = {0.0, 0.0, -1.0};
+  fcg_neumann_surface(FCG_HEX27, int64_t(faces.size() / 9), faces.data(), d.node_x, d.node_dof_row, onoff,
+      val, nullptr, nullptr, nullptr, 0.0, fext.data());
+  // Dirichlet rows: owned nodes on x = 0; node coordinates of the owned rows (AMG modes)
+  std::vector<int32_t> dbc;
+  std::vector<double> xrow(static_cast<size_t>(nr), 0.0);
+  for (int64_t v = 0; v < d.n_node; ++v)
+  {
+    const int32_t r0 = d.node_dof_row[v];
+    if (r0 < 0) continue;
+    for (int k = 0; k < 3; ++k) xrow[size_t(r0 + k)] = d.node_x[3 * v + k];
+    if (d.node_x[3 * v] == 0.0)
+      for (int k = 0; k < 3; ++k) dbc.push_back(r0 + k);
+  }
+  std::sort(dbc.begin(), dbc.end());
+  fcg_amg* amg = nullptr;
+  if (fcg_amg_create(ctx, d.rowptr, d.col_lid, xrow.data(), int64_t(dbc.size()), dbc.data(), nullptr, &amg) != FCG_OK)
+    return fail(std::string("fcg_amg_create: ") + fcg_last_error(ctx));
+  const int64_t nnz = d.rowptr[nr];
+  void *dK, *du_row, *du_col, *df, *drhs, *ddu, *ddbc;
+  fcg_device_alloc(0, nnz * 8, &dK);
+  fcg_device_alloc(0, nr * 8, &du_row);
+  fcg_device_alloc(0, nc * 8, &du_col);
+  fcg_device_alloc(0, nr * 8, &df);
+  fcg_device_alloc(0, nr * 8, &drhs);
+  fcg_device_alloc(0, nr * 8, &ddu);
+  fcg_device_alloc(0, std::max<int64_t>(1, int64_t(dbc.size())) * 4, &ddbc);
+  fcg_memcpy_h2d(ddbc, dbc.data(), int64_t(dbc.size()) * 4);
+  std::vector<double> u(static_cast<size_t>(nr), 0.0), f(static_cast<size_t>(nr)), du(static_cast<size_t>(nr));
+  double fn2 = 0.0;
+  for (double v : fext) fn2 += v * v;
+  tc->sum(rank, &fn2, 1);
+  const double tol = 1e-10 * std::sqrt(fn2);
+  double ndu = 1e300;
+  bool conv = false;
+  for (int it = 0; it <= 20; ++it)
+  {
+    fcg_memcpy_h2d(du_row, u.data(), nr * 8);
+    if (tr_import(&ht, static_cast<double*>(du_row), static_cast<double*>(du_col), nullptr) != FCG_OK)
+      return fail("set_state import");
+    int32_t bad = -1;
+    if (fcg_evaluate_device(ctx, FCG_CALC_NLNSTIFF, FCG_OVERWRITE, static_cast<double*>(du_col),
+            static_cast<double*>(df), static_cast<double*>(dK), nullptr, &bad) != FCG_OK)
+      return fail(std::string("evaluate: ") + fcg_last_error(ctx));
+    fcg_memcpy_d2h(f.data(), df, nr * 8);
+    std::vector<double> rhs(static_cast<size_t>(nr));
+    double rr = 0.0;
+    for (int64_t i = 0; i < nr; ++i) rhs[size_t(i)] = -(f[size_t(i)] - fext[size_t(i)]);
+    for (int32_t r : dbc) rhs[size_t(r)] = 0.0;
+    for (double v : rhs) rr += v * v;
+    tc->sum(rank, &rr, 1);
+    if (!tc->ok()) return fail("another rank failed");
+    const double nres = std::sqrt(rr);
+    out->norm_res.push_back(nres);
+    if (it > 0 && nres <= tol && ndu <= 1e-10)
+    {
+      conv = true;
+      break;
+    }
+    fcg_memcpy_h2d(drhs, rhs.data(), nr * 8);
+    if (fcg_dirichlet_apply(ctx, int64_t(dbc.size()), static_cast<int32_t*>(ddbc), static_cast<double*>(dK),
+            static_cast<double*>(drhs), nullptr, nullptr) != FCG_OK)
+      return fail("dirichlet");
+    int li = 0;
+    double rel = 0.0;
+    if (fcg_dfcg_solve(ctx, amg, &tr, static_cast<double*>(dK), static_cast<double*>(drhs),
+            static_cast<double*>(ddu), 1e-10, 500, nullptr, &li, &rel) != FCG_OK)
+      return fail(std::string("fcg_dfcg_solve: ") + fcg_last_error(ctx));
+    out->lin_iters.push_back(li);
+    fcg_memcpy_d2h(du.data(), ddu, nr * 8);
+    double dd = 0.0;
+    for (int64_t i = 0; i < nr; ++i)
+    {
+      u[size_t(i)] += du[size_t(i)];
+      dd += du[size_t(i)] * du[size_t(i)];
+    }
+    tc->sum(rank, &dd, 1);
+    ndu = std::sqrt(dd);
+  }
+  for (int64_t i = 0; i < nr; ++i) out->u[row_gid[i]] = u[size_t(i)];
+  out->ok = conv;
+  if (!conv) out->err = "Newton did not converge";
+  for (void* p : {dK, du_row, du_col, df, drhs, ddu, ddbc, d_send, d_recv}) fcg_device_free(p);
+  fcg_amg_destroy(amg);
+  fcg_halo_destroy(halo);
+  fcg_plan_free(plan_store);
+  fcg_destroy(ctx);
+  fcg_box_mesh_destroy(bm);
+}
+
+bool solve(int n, int nranks, std::map<int32_t, double>& u, std::vector<double>& res, std::vector<int>& lin)
+{
+  ThreadComm tc(nranks);
+  std::vector<RankResult> rr(static_cast<size_t>(nranks));
+  std::vector<std::thread> th;
+  for (int r = 0; r < nranks; ++r) th.emplace_back(run_rank, n, nranks, r, &tc, &rr[size_t(r)]);
+  for (auto& t : th) t.join();
+  bool ok = true;
+  for (int r = 0; r < nranks; ++r)
+  {
+    if (!rr[size_t(r)].ok)
+    {
+      std::printf("rank %d/%d: %s\n", r, nranks, rr[size_t(r)].err.c_str());
+      ok = false;
+    }
+    u.insert(rr[size_t(r)].u.begin(), rr[size_t(r)].u.end());
+  }
+  res = rr[0].norm_res;
+  lin = rr[0].lin_iters;
+  return ok;
+}
+
+}  // namespace
+
+int main(int argc, char** argv)
+{
+  const int n = argc > 1 ? std::atoi(argv[1]) : 8;
+  const int nranks = argc > 2 ? std::atoi(argv[2]) : 2;
+  int failures = 0;
+  std::map<int32_t, double> u1, uR;
+  std::vector<double> res1, resR;
+  std::vector<int> lin1, linR;
+  failures += !solve(n, 1, u1, res1, lin1);
+  auto report = [&](int R, const std::vector<double>& res, const std::vector<int>& lin, const std::map<int32_t, double>& u) {
+    std::printf("hex27 TotLag %d^3 on %d rank(s): Newton |r|", n, R);
+    for (double v : res) std::printf(" %.3e", v);
+    std::printf("; FCG iterations");
+    for (int v : lin) std::printf(" %d", v);
+    double tip = 0.0;
+    if (!u.empty()) tip = u.rbegin()->second;  // the last DOF GID: u_z of the node at (1, 1, 1)
+    std::printf("; tip u_z %.15g\n", tip);
+  };
+  report(1, res1, lin1, u1);
+  // quadratic convergence: the last two residual reductions
+  if (res1.size() < 3 || !(res1.back() < 1e-6 * res1[res1.size() - 3])) ++failures;
+  if (nranks > 1)
+  {
+    failures += !solve(n, nranks, uR, resR, linR);
+    report(nranks, resR, linR, uR);
+    double worst = 0.0, scale = 0.0;
+    bool same = uR.size() == u1.size();
+    for (const auto& kv : u1)
+    {
+      scale = std::max(scale, std::fabs(kv.second));
+      auto it = uR.find(kv.first);
+      if (it == uR.end())
+      {
+        same = false;
+        break;
+      }
+      worst = std::max(worst, std::fabs(it->second - kv.second));
+    }
+    std::printf("max |u_%d - u_1| = %.3e (max |u| %.3e)\n", nranks, worst, scale);
+    failures += !(same && worst <= 1e-8 * scale);
+  }
+  std::printf(failures ? "FAIL (%d)\n" : "PASS\n", failures);
+  return failures ? 1 : 0;
+}

@@ -35,3 +35,20 @@ def test_integration_on_device(args):
     p = subprocess.run([_binary()] + args, capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "PASS" in p.stdout, p.stdout
+
+
+NATIVE = os.path.join(CXX, "_build", "config3_native")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,ranks", [(8, 2), (40, 2)])
+def test_config3_native_cxx_host(n, ranks):
+    """BASELINE config 3's problem (hex27 StVK TotLag cube, x- clamped, traction -1 on x+) solved by
+    a C++ host through the C ABI alone (tests/cxx/config3_native.cpp): Newton with fcg_dfcg_solve
+    and each rank's fcg_amg; ranks as threads with a host exchange on one GPU.  1 rank and `ranks`
+    ranks converge quadratically to the same displacement by DOF GID (n = 40: config 3 at 40^3)."""
+    if not os.path.exists(NATIVE):
+        subprocess.run(["make", "-s", "-C", CXX], check=True)
+    p = subprocess.run([NATIVE, str(n), str(ranks)], capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "PASS" in p.stdout, p.stdout

@@ -261,7 +261,8 @@ def _cantilever_loads(m, x_max):
     return fext, dbc
 
 
-def _worker_solve(rank, world, port, q, kinem, path, transport="staged"):
+def _worker_solve(rank, world, port, q, kinem, path, transport="staged", solver="pcg",
+                  celltype=None):
     try:
         for p in (ROOT, os.path.join(ROOT, "tests")):
             if p not in sys.path:
@@ -271,9 +272,10 @@ def _worker_solve(rank, world, port, q, kinem, path, transport="staged"):
         os.environ["MASTER_PORT"] = str(port)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         dsolve = importlib.import_module("4c_amd.dsolve")
-        iv = (8, 4, 4)
-        up = (8.0, 4.0, 4.0)
-        m = fcg.BoxMesh(fcg.HEX8, iv, upper=up, jitter=0.1, seed=5, rank=rank, nranks=world)
+        ct = fcg.HEX8 if celltype is None else celltype
+        iv, up = _solve_box(ct)
+        m = fcg.BoxMesh(ct, iv, upper=up, jitter=0.1 if ct == fcg.HEX8 else 0.02, seed=5, rank=rank,
+                        nranks=world)
         n_own = m.n_owned_rows
         comm = None
         if transport == "rccl":  # one GPU per rank: halo + dots over the library's RCCL comm
@@ -294,14 +296,75 @@ def _worker_solve(rank, world, port, q, kinem, path, transport="staged"):
         fext, dbc = _cantilever_loads(m, up[0])
         tr = (dsolve.Transport(h, comm=comm, device=dev) if comm is not None
               else dsolve.Transport(h, staged=True, device=dev))
-        nt = dsolve.DistributedNewton(ev, tr, fext, dbc, tol_res=1e-10, tol_inc=1e-11, lin_rtol=1e-12)
+        lin = None
+        if solver != "pcg":
+            amg_mod = importlib.import_module("4c_amd.amg")
+            amg = amg_mod.NativeAMG(m, ev, dbc) if solver == "native" else None
+            lin = dsolve.NativeDFCG(ev, tr, amg)
+        nt = dsolve.DistributedNewton(ev, tr, fext, dbc, tol_res=1e-10, tol_inc=1e-11, lin_rtol=1e-12,
+                                      linear_solver=lin)
         u = nt.solve().cpu().numpy()
         q.put((rank, True, {"u": dict(zip(m.row_gid[:n_own].tolist(), u.tolist())),
                             "iters": [r.get("lin_iter") for r in nt.history]}))
+        if lin is not None and lin.amg is not None:
+            lin.amg.close()
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover - reported to the parent
         import traceback
         q.put((rank, traceback.format_exc() + repr(e), {}))
+
+
+def _solve_box(celltype):
+    return ((8, 4, 4), (8.0, 4.0, 4.0)) if celltype == fcg.HEX8 else ((6, 2, 2), (6.0, 2.0, 2.0))
+
+
+def _run_two_rank_solve(kinem, path, transport, solver="pcg", celltype=fcg.HEX8):
+    """The 2-rank DistributedNewton of the clamped, tip-loaded box against the 1-rank StaticNewton
+    (by DOF GID); returns the ranks' linear iteration counts."""
+    dev = _dev()
+    newton = importlib.import_module("4c_amd.newton")
+    iv, up = _solve_box(celltype)
+    m = fcg.BoxMesh(celltype, iv, upper=up, jitter=0.1 if celltype == fcg.HEX8 else 0.02, seed=5)
+    fext, dbc = _cantilever_loads(m, up[0])
+    ev = fcg.Evaluator(m, kinematics=kinem, youngs=E, poisson=NU, device=0, path=path)
+    ref = newton.StaticNewton(ev, fext, dbc, tol_res=1e-10, tol_inc=1e-11, lin_rtol=1e-12).solve()
+    uref = dict(zip(m.row_gid.tolist(), ref.cpu().numpy().tolist()))
+    ev.close()
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    qq = ctx.Queue()
+    port = 29700 + os.getpid() % 1000
+    procs = [ctx.Process(target=_worker_solve, args=(r, 2, port, qq, kinem, path, transport, solver,
+                                                     celltype)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [qq.get(timeout=240) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+    got, iters = {}, []
+    for rank, ok, out in res:
+        assert ok is True, (rank, ok)
+        got.update(out["u"])
+        iters.append(out["iters"])
+    assert set(got) == set(uref)
+    scale = max(abs(v) for v in uref.values())
+    assert scale > 0
+    worst = max(abs(got[g] - uref[g]) for g in uref)
+    assert worst <= 1e-8 * scale, (worst, scale)
+    assert dev is not None
+    return iters
+
+
+@pytest.mark.parametrize("solver", ["native", "native-bj"])
+@pytest.mark.parametrize("celltype,kinem", [(fcg.HEX8, fcg.LINEAR), (fcg.HEX27, fcg.TOTLAG)])
+def test_two_ranks_native_dfcg(celltype, kinem, solver):
+    """fcg_dfcg_solve (the native distributed flexible CG: one import per SpMV, all-reduced inner
+    products) with each rank's fcg_amg on its owned block ("native") or the nodal block Jacobi,
+    inside the 2-rank Newton, host-staged transport callbacks on one GPU: the 1-rank solution."""
+    iters = _run_two_rank_solve(kinem, fcg.PATH_AUTO, "staged", solver, celltype)
+    if solver == "native":
+        bj = _run_two_rank_solve(kinem, fcg.PATH_AUTO, "staged", "native-bj", celltype)
+        assert sum(i or 0 for i in iters[0]) < sum(i or 0 for i in bj[0]), (iters, bj)
 
 
 @pytest.mark.parametrize("transport", ["staged", "rccl"])
