@@ -107,6 +107,7 @@ struct SweepTsi {
   double* Ktt = nullptr;
   double* fT = nullptr;
   double m = 0, T0 = 0, conduct = 0, kts = 0;  // kts = -timefac timefac_d
+  bool split = true;  // structural sweep + thermal-only pass (FCG_TSI_SPLIT=0: one fused pass)
 };
 hipError_t launch_sweep_h8_tsi(const DeviceMesh& m, const double* d_u_col, bool overwrite,
     double* d_K, double* d_fint, const SweepTsi& t, hipStream_t stream);

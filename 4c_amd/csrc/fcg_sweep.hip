@@ -91,7 +91,7 @@ struct SweepArgs {
 template <bool TSI>
 constexpr int node_comps() { return TSI ? 10 : 6; }
 
-template <int KIN, bool TSI>
+template <int KIN, bool TSI, bool TH = false>
 struct SweepShared {
   alignas(16) double nx[3 * 4 * NSLOT * 8 * 2];  // sqrt|fac| N_XYZ, see nx2i()
   // TotLag: F (column-major) | S (Voigt) | c = fac / sqrt|fac|  (linear kinematics: unused)
@@ -108,8 +108,9 @@ struct SweepShared {
   // lane k + 8, read by the U-side lane k of the next layer in the same instruction that precedes
   // the next write (LDS operations of a wavefront complete in order): one buffer suffices.
   // [column][in-plane neighbour (dy+1)*3 + dx+1][3x3 | TSI: k_ST 3 | k_TS 3 | k_TT 1]
-  // (TSI rows padded to 18 doubles: with 16 every (column, t) record started on the same bank)
-  double hold[TX * TY][9][TSI ? 18 : 9];
+  // (TSI rows padded to 18 doubles: with 16 every (column, t) record started on the same bank;
+  // thermal-only pass TH: k_ST 3 | k_TS 3 | k_TT 1, padded to 9)
+  double hold[TX * TY][9][TSI ? (TH ? 9 : 18) : 9];
 };
 
 __device__ inline int ring(int p) { return (p % 3 + 3) % 3; }
@@ -132,8 +133,8 @@ __device__ inline int node_at(int ox, int oy, int oz) { return 4 * oz + (oy ? (o
 
 // Stage A for element slot s, Gauss point g of layer L (element e, -1 = none).  Written for a
 // small register footprint: node data stays in LDS and N_XYZ is recomputed where needed.
-template <int KIN, bool TSI>
-__device__ inline void sweep_stage_a(SweepShared<KIN, TSI>& sh, const SweepArgs& A, int s, int g,
+template <int KIN, bool TSI, class SH>
+__device__ inline void sweep_stage_a(SH& sh, const SweepArgs& A, int s, int g,
     int sx, int sy, int L, int e)
 {
   constexpr int NC = node_comps<TSI>();
@@ -286,12 +287,32 @@ __device__ inline void sweep_stage_a(SweepShared<KIN, TSI>& sh, const SweepArgs&
 // Gauss points of element slot `slot`.  Acc layout: G[9] (row-major, G[3r+q] = sum a'_r b'_q)
 // then, for TotLag, H[6] and geo; for TSI (linear) sum c N_b a[3], sum c N_a T_g b[3] and
 // sum m fac tr(e') N_a N_b (the factors m, -timefac timefac_d and k enter in tsi_block).
-template <int KIN, bool NEG, bool TSI>
-__device__ inline void sweep_visit(const SweepShared<KIN, TSI>& sh, int slot, int a, int b1, int b2,
+// TH (the thermal-only pass beside the linear structural sweep): no G, the thermal sums at
+// acc[0..5], fac a.b at acc[6] (k_TT's conduction part) and sum m fac tr(e') N_a N_b at acc[7].
+template <int KIN, bool NEG, bool TSI, bool TH = false, class SH>
+__device__ inline void sweep_visit(const SH& sh, int slot, int a, int b1, int b2,
     uint32_t nm, double* acc1, double* acc2)
 {
   auto gp_body = [&](int g, double a0, double a1, double a2, double p0, double p1, double p2,
                      double q0, double q1, double q2) {
+    if (TH)
+    {
+      const double* t = sh.tg[g][slot];
+      const double cf = t[0], Tg = t[1], qq = t[2];
+      const double Na = sh.Ng[g][a], N1 = sh.Ng[g][b1], N2 = sh.Ng[g][b2];
+      const double c1 = cf * N1, c2 = cf * N2, ct = cf * Na * Tg, qa = qq * Na;
+      acc1[0] += c1 * a0; acc1[1] += c1 * a1; acc1[2] += c1 * a2;
+      acc2[0] += c2 * a0; acc2[1] += c2 * a1; acc2[2] += c2 * a2;
+      acc1[3] += ct * p0; acc1[4] += ct * p1; acc1[5] += ct * p2;
+      acc2[3] += ct * q0; acc2[4] += ct * q1; acc2[5] += ct * q2;
+      acc1[7] += qa * N1;
+      acc2[7] += qa * N2;
+      // fac a.b: sqrt|fac| a . sqrt|fac| b with the sign of fac
+      const double sg = (NEG && ((nm >> g) & 1u)) ? -1.0 : 1.0;
+      acc1[6] += sg * (a0 * p0 + a1 * p1 + a2 * p2);
+      acc2[6] += sg * (a0 * q0 + a1 * q1 + a2 * q2);
+      return;
+    }
     if (TSI)
     {
       // unflipped sqrt|fac| N_XYZ times c = fac / sqrt|fac| gives fac N_XYZ
@@ -376,16 +397,18 @@ __device__ inline void sweep_visit(const SweepShared<KIN, TSI>& sh, int slot, in
 }
 
 // TSI blocks of an accumulated (linear) part: k_ST(A,B) [3] | k_TS(A,B) [3] | k_TT(A,B)
+template <bool TH = false>
 __device__ inline void tsi_block(const SweepArgs& A, const double* acc, double* Tv)
 {
   const double m = A.tsi_m, mk = A.tsi_m * A.tsi_kts;
-  Tv[0] = m * acc[9];
-  Tv[1] = m * acc[10];
-  Tv[2] = m * acc[11];
-  Tv[3] = mk * acc[12];
-  Tv[4] = mk * acc[13];
-  Tv[5] = mk * acc[14];
-  Tv[6] = A.tsi_k * (acc[0] + acc[4] + acc[8]) - acc[15];
+  constexpr int o = TH ? 0 : 9;
+  Tv[0] = m * acc[o + 0];
+  Tv[1] = m * acc[o + 1];
+  Tv[2] = m * acc[o + 2];
+  Tv[3] = mk * acc[o + 3];
+  Tv[4] = mk * acc[o + 4];
+  Tv[5] = mk * acc[o + 5];
+  Tv[6] = TH ? A.tsi_k * acc[6] - acc[7] : A.tsi_k * (acc[0] + acc[4] + acc[8]) - acc[15];
 }
 
 // K_AB of an accumulated part (isotropic StVK)
@@ -426,12 +449,16 @@ __device__ inline void block_k(const StVK& m, const double* acc, double* Kb)
     st_last = now;                                                                                 \
   }
 
-template <int KIN, bool WANT_K, bool OVERWRITE, bool TSI>
+// MODE 0: structure (K, f_int); 1: fused TSI (K_SS, k_ST, k_TS, k_TT, f_S, f_T in one pass);
+// 2: the thermal-only pass that follows a MODE-0 linear sweep (k_ST, k_TS, k_TT, f_T, and
+// k_ST (T - T_0) added into f_S) -- 8 accumulators per block instead of 16, no K stores.
+template <int KIN, bool WANT_K, bool OVERWRITE, int MODE>
 __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
 {
+  constexpr bool TSI = MODE != 0, TH = MODE == 2;
   static_assert(!TSI || (KIN == 0 && WANT_K), "TSI is geometrically linear, full tangent");
-  __shared__ SweepShared<KIN, TSI> sh;
-  constexpr int NACC = (KIN || TSI) ? 16 : 9;
+  __shared__ SweepShared<KIN, TSI, TH> sh;
+  constexpr int NACC = TH ? 8 : ((KIN || TSI) ? 16 : 9);
   constexpr int NC = node_comps<TSI>();
   constexpr int NLD = (NNODE * NC + 255) / 256;  // node-load items per lane
   constexpr int NF = TSI ? 4 : 3;                // residual rows per node: f_S (3) | f_T
@@ -607,8 +634,9 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
           const int dx = t % 3 - 1, dy = (t / 3) % 3 - 1, dz = t / 9 - 1;
           const double* ub = &sh.node[ring(L + (k >> 3) + dz)][(cy + 1 + dy) * NXN + cx + 1 + dx][3];
           const double u0 = ub[0], u1 = ub[1], u2 = ub[2];
+          if (!TH)
 #pragma unroll
-          for (int r = 0; r < 3; ++r) fpart[r] += Kb[3 * r] * u0 + Kb[3 * r + 1] * u1 + Kb[3 * r + 2] * u2;
+            for (int r = 0; r < 3; ++r) fpart[r] += Kb[3 * r] * u0 + Kb[3 * r + 1] * u1 + Kb[3 * r + 2] * u2;
           if (TSI)
           {
             // f_S += k_ST (T - T_0) (partition of unity), f_T = k_TT T (exact for linear TSI)
@@ -623,7 +651,8 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
         // (D side) stores this layer's part and the U side adds the part held since last layer
         if (act == kActHold || act == kActWriteLHold)
         {
-          constexpr int NH = TSI ? 16 : 9;
+          constexpr int NK = TH ? 0 : 9;  // structural entries held (none in the thermal pass)
+          constexpr int NH = NK + (TSI ? 7 : 0);
           double* h = sh.hold[c][t - 9];
           double held[NH];
 #pragma unroll
@@ -634,18 +663,18 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
           if (act == kActHold)
           {
 #pragma unroll
-            for (int i = 0; i < 9; ++i) h[i] = Kb[i];
+            for (int i = 0; i < NK; ++i) h[i] = Kb[i];
             if (TSI)
 #pragma unroll
-              for (int i = 0; i < 7; ++i) h[9 + i] = Tv[i];
+              for (int i = 0; i < 7; ++i) h[NK + i] = Tv[i];
           }
           else
           {
 #pragma unroll
-            for (int i = 0; i < 9; ++i) Kb[i] = held[i] + Kb[i];
+            for (int i = 0; i < NK; ++i) Kb[i] = held[i] + Kb[i];
             if (TSI)
 #pragma unroll
-              for (int i = 0; i < 7; ++i) Tv[i] = held[9 + i] + Tv[i];
+              for (int i = 0; i < 7; ++i) Tv[i] = held[NK + i] + Tv[i];
           }
         }
         if (act == kActHold || !WANT_K) return;
@@ -653,16 +682,17 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
         const int64_t base = int64_t(base_lo) | (int64_t(base_hi) << 32);
         const int64_t len = len32;
         double* dst = A.K + base + pos;
+        if (!TH)
 #pragma unroll
-        for (int r = 0; r < 3; ++r)
+          for (int r = 0; r < 3; ++r)
 #pragma unroll
-          for (int qq = 0; qq < 3; ++qq)
-          {
-            if (OVERWRITE)
-              dst[r * len + qq] = Kb[3 * r + qq];
-            else
-              dst[r * len + qq] += Kb[3 * r + qq];
-          }
+            for (int qq = 0; qq < 3; ++qq)
+            {
+              if (OVERWRITE)
+                dst[r * len + qq] = Kb[3 * r + qq];
+              else
+                dst[r * len + qq] += Kb[3 * r + qq];
+            }
         if (TSI)
         {
           // node-consistent block graphs (checked by fcg_tsi_evaluate_fused): the k_ST rows of the
@@ -713,14 +743,14 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
         const int slot = slot_of(w);
         const uint32_t nm = TSI ? sh.neg[slot] : (v == 0 ? nm_pre[0] : nm_pre[1]);
         if (nm == 0u)
-          sweep_visit<KIN, false, TSI>(sh, slot, a, b1, b2, nm, acc1, acc2);
+          sweep_visit<KIN, false, TSI, TH>(sh, slot, a, b1, b2, nm, acc1, acc2);
         else
-          sweep_visit<KIN, true, TSI>(sh, slot, a, b1, b2, nm, acc1, acc2);
+          sweep_visit<KIN, true, TSI, TH>(sh, slot, a, b1, b2, nm, acc1, acc2);
         if ((w >> 24) & 1u)
         {
           double Kb[9], Tv[7];
-          block_k<KIN>(A.mat, acc2, Kb);
-          if (TSI) tsi_block(A, acc2, Tv);
+          if (!TH) block_k<KIN>(A.mat, acc2, Kb);
+          if (TSI) tsi_block<TH>(A, acc2, Tv);
 #pragma unroll
           for (int i = 0; i < NACC; ++i) acc2[i] = 0.0;
           emit(int((w >> 21) & 7), int((w >> 16) & 31), Kb, Tv);
@@ -730,16 +760,19 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
       {
         const int pair = int((vis1 >> 26) & 3);
         double Kb[9], Tv[7];
-        block_k<KIN>(A.mat, acc1, Kb);
-#pragma unroll
-        for (int i = 0; i < 9; ++i)
+        if (!TH)
         {
-          const double o = dpp_f64<kDppXor1>(Kb[i]);
-          Kb[i] = pair == kPairRecv ? Kb[i] + o : Kb[i];  // a select, not a branch per entry
+          block_k<KIN>(A.mat, acc1, Kb);
+#pragma unroll
+          for (int i = 0; i < 9; ++i)
+          {
+            const double o = dpp_f64<kDppXor1>(Kb[i]);
+            Kb[i] = pair == kPairRecv ? Kb[i] + o : Kb[i];  // a select, not a branch per entry
+          }
         }
         if (TSI)
         {
-          tsi_block(A, acc1, Tv);
+          tsi_block<TH>(A, acc1, Tv);
 #pragma unroll
           for (int i = 0; i < 7; ++i)
           {
@@ -811,7 +844,7 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
 #pragma unroll
           for (int d = 0; d < 3; ++d)
           {
-            if (OVERWRITE)
+            if (OVERWRITE && !TH)  // the thermal pass adds k_ST (T - T_0) to the structural f_S
               A.fint[row0 + d] = fp[d] + f[d];
             else
               A.fint[row0 + d] += fp[d] + f[d];
@@ -874,13 +907,13 @@ hipError_t launch_sweep_h8(const DeviceMesh& m, const double* d_u_col, bool want
   const dim3 block{256, 1, 1};
 #define FCG_SWEEP(KIN)                                                                             \
   if (want_k && overwrite)                                                                         \
-    hipLaunchKernelGGL((sweep_h8_kernel<KIN, true, true, false>), grid, block, 0, stream, a);      \
+    hipLaunchKernelGGL((sweep_h8_kernel<KIN, true, true, 0>), grid, block, 0, stream, a);      \
   else if (want_k)                                                                                 \
-    hipLaunchKernelGGL((sweep_h8_kernel<KIN, true, false, false>), grid, block, 0, stream, a);     \
+    hipLaunchKernelGGL((sweep_h8_kernel<KIN, true, false, 0>), grid, block, 0, stream, a);     \
   else if (overwrite)                                                                              \
-    hipLaunchKernelGGL((sweep_h8_kernel<KIN, false, true, false>), grid, block, 0, stream, a);     \
+    hipLaunchKernelGGL((sweep_h8_kernel<KIN, false, true, 0>), grid, block, 0, stream, a);     \
   else                                                                                             \
-    hipLaunchKernelGGL((sweep_h8_kernel<KIN, false, false, false>), grid, block, 0, stream, a);
+    hipLaunchKernelGGL((sweep_h8_kernel<KIN, false, false, 0>), grid, block, 0, stream, a);
   if (m.kinem == 0)
   {
     FCG_SWEEP(0)
@@ -912,10 +945,25 @@ hipError_t launch_sweep_h8_tsi(const DeviceMesh& m, const double* d_u_col, bool 
   a.tsi_kts = t.kts;
   const dim3 grid{static_cast<unsigned>(ntiles), 1, 1};
   const dim3 block{256, 1, 1};
+  if (!t.split)
+  {
+    if (overwrite)
+      hipLaunchKernelGGL((sweep_h8_kernel<0, true, true, 1>), grid, block, 0, stream, a);
+    else
+      hipLaunchKernelGGL((sweep_h8_kernel<0, true, false, 1>), grid, block, 0, stream, a);
+    return hipGetLastError();
+  }
+  // split: the linear structural sweep (K_SS, f_S = K_SS u), then the thermal-only pass
   if (overwrite)
-    hipLaunchKernelGGL((sweep_h8_kernel<0, true, true, true>), grid, block, 0, stream, a);
+  {
+    hipLaunchKernelGGL((sweep_h8_kernel<0, true, true, 0>), grid, block, 0, stream, a);
+    hipLaunchKernelGGL((sweep_h8_kernel<0, true, true, 2>), grid, block, 0, stream, a);
+  }
   else
-    hipLaunchKernelGGL((sweep_h8_kernel<0, true, false, true>), grid, block, 0, stream, a);
+  {
+    hipLaunchKernelGGL((sweep_h8_kernel<0, true, false, 0>), grid, block, 0, stream, a);
+    hipLaunchKernelGGL((sweep_h8_kernel<0, true, false, 2>), grid, block, 0, stream, a);
+  }
   return hipGetLastError();
 }
 

@@ -30,6 +30,8 @@
 // no atomics, bitwise reproducible -- the contract of the structural path.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <cmath>
 #include <climits>
@@ -933,6 +935,12 @@ int fcg_tsi_evaluate_fused(fcg_ctx* sctx, fcg_tsi_ctx* ctx, int mode, const doub
     t.T0 = d.T0;
     t.conduct = d.conduct;
     t.kts = -timefac * timefac_d;  // linear_coupled_tang (4C_thermo_ele_impl.cpp:1189)
+    // the structural sweep + a thermal-only pass (default), or the one fused pass
+    static const bool split = [] {
+      const char* e = std::getenv("FCG_TSI_SPLIT");
+      return !(e && e[0] == '0');
+    }();
+    t.split = split;
     he = fcg::launch_sweep_h8_tsi(m, d_u_col, mode == FCG_OVERWRITE, d_Kss, d_fs_row, t, s);
   }
   int32_t errv[2] = {0, INT32_MAX};
