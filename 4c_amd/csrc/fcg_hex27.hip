@@ -127,6 +127,7 @@ struct H27Args {
   int32_t* err;
   double lambda, mu, cdiag;
   int want_k;
+  unsigned long long* stamps;  // FCG_STAMPS=1: per-phase s_memtime sums of thread 0, else NULL
 };
 
 typedef double f64x4_t __attribute__((ext_vector_type(4)));
@@ -182,8 +183,22 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
     sh.U[0][tid] = upre;
   }
   int buf = 0;
+  // diagnostic phase timers (FCG_STAMPS=1, tools/h27_stamps.py): thread 0's s_memtime deltas per
+  // phase, barrier waits included: 0 gather + J, 1 Gauss-point algebra, 2 VALU pair sums,
+  // 3 q + f_e, 4 matrix-core G + H image, 5 K image + record stores
+  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long st_last = A.stamps ? __builtin_amdgcn_s_memtime() : 0ull;
+  int64_t st_n = 0;
+#define H27_STAMP(i)                                                                               \
+  if (A.stamps && tid == 0)                                                                        \
+  {                                                                                                \
+    const unsigned long long now = __builtin_amdgcn_s_memtime();                                  \
+    st_acc[i] += now - st_last;                                                                    \
+    st_last = now;                                                                                 \
+  }
   for (int64_t e = blockIdx.x; e < A.n_ele; e += gridDim.x, buf ^= 1)
   {
+    ++st_n;
     double* rec = A.rec + e * kRec;
     if (tid == 0) sh.bad = 0;
     __syncthreads();
@@ -241,6 +256,7 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
       else if (!(det > 0)) atomicMax(&sh.bad, 1);
     }
     __syncthreads();
+    H27_STAMP(0);
 
     // 2. per Gauss point: J^-1, fac, strains, StVK stress and the folded 3 x 3 factors
     if (tid < kNpe)
@@ -346,6 +362,7 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
       }
     }
     __syncthreads();
+    H27_STAMP(1);
     if (tid < 81)  // the next element's X and u, before this one's first global store
     {
       sh.X[buf ^ 1][tid] = xpre;
@@ -407,6 +424,7 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
       }
       __syncthreads();  // every read of w, v done: the region becomes q
     }
+    H27_STAMP(2);
 
     // 3b. q_a = T d_a per (g, a); f_a = sum_g R_g d_a (add_internal_force_vector)
     if (A.want_k)
@@ -438,6 +456,7 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
       continue;
     }
     __syncthreads();
+    H27_STAMP(3);
 
     // 5. G on the matrix cores: waves 0..2 take the node ranges (0,0), (0,1), (1,1) of 16
     const int at = wave == 2 ? 1 : 0, bt = wave == 0 ? 0 : 1;
@@ -492,6 +511,7 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
           }
       __syncthreads();
     }
+    H27_STAMP(4);
     // K_ab = lambda G + mu G^T + (mu tr G I | mu H + geo I) into the LDS image of the record,
     // which then leaves as contiguous 16-byte pieces: one store instruction covers 1 KB of the
     // record instead of 64 scattered 8-byte entries
@@ -537,7 +557,15 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
       for (int v = tid; v < kNpair * 9 / 2; v += kBlk) dst[v] = src[v];
     }
     __syncthreads();
+    H27_STAMP(5);
   }
+  if (A.stamps && tid == 0)
+  {
+    for (int i = 0; i < 6; ++i) atomicAdd(&A.stamps[i], st_acc[i]);
+    atomicAdd(&A.stamps[6], 1ull);
+    atomicAdd(&A.stamps[7], (unsigned long long)st_n);
+  }
+#undef H27_STAMP
 }
 
 struct H27AsmArgs {
@@ -719,6 +747,7 @@ hipError_t launch_h27_element(const DeviceMesh& m, const double* d_u_col, bool w
   a.mu = m.mu;
   a.cdiag = m.cdiag;
   a.want_k = want_k ? 1 : 0;
+  a.stamps = m.stamps;
   const int64_t cap = 256 * 8;
   const dim3 grid(unsigned(m.n_ele < cap ? m.n_ele : cap)), block(kBlk);
   if (m.kinem == 0)

@@ -305,6 +305,13 @@ def amg_newton_secondary(n, timeout_s=600):
 # SURVEY.md §8d algorithmic figures for hex27 TotLag K + r (per element)
 ALG_BYTES_PER_ELE_H27 = 37695.0
 ALG_FLOP_PER_ELE_H27_TOTLAG = 2.59e6
+# flops the hex27 kernel (fcg_hex27.hip, reference-coordinate contracted form) executes per
+# TotLag element, useful work only (no MFMA padding): J and du/dxi 162 x 27 x 3 FMA; w, v per
+# (g, a) 729 x 18; H + geo of the 378 pairs a <= b 378 x 27 x 12; q and f_e 2 x 729 x 9; G on the
+# matrix cores 378 x 27 x 9 -- 253.8k FMA = 507.6k flop -- plus ~20k flop of Gauss-point algebra
+# and block assembly
+EXEC_FLOP_PER_ELE_H27_TOTLAG = 2.0 * (162 * 27 * 3 + 729 * 18 + 378 * 27 * 12 + 2 * 729 * 9
+                                      + 378 * 27 * 9) + 2.0e4
 
 
 def _oracle_native():
@@ -345,16 +352,22 @@ def hex27_secondary(dev, n, steps, threads, with_cpu):
     torch.cuda.synchronize(dev)
     wall = (time.perf_counter() - t0) / steps
     ms_kern = float(np.mean([a + b for a, b in ts]))
-    flops = ALG_FLOP_PER_ELE_H27_TOTLAG * mesh.n_ele / (ms_kern * 1e-3) / 1e12
+    flops = EXEC_FLOP_PER_ELE_H27_TOTLAG * mesh.n_ele / (ms_kern * 1e-3) / 1e12
+    flops_survey = ALG_FLOP_PER_ELE_H27_TOTLAG * mesh.n_ele / (ms_kern * 1e-3) / 1e12
     gbs = ALG_BYTES_PER_ELE_H27 * mesh.n_ele / (ms_kern * 1e-3) / 1e9
     out = {
         "workload": f"hex27-totlag-{n}^3", "baseline_config": "BASELINE.json configs[2] element",
         "value": mesh.n_ele / wall, "unit": "element-evaluations/s", "ms_per_step": 1e3 * wall,
-        "elements": mesh.n_ele, "nnz": mesh.nnz, "path": "general (element_kernel + assemble_kernel)",
-        # FP64-bound by SURVEY §8d's count (2.59 Mflop vs 37.7 kB per element); the TotLag pair
-        # phase runs on the FP64 VALU (the MFMA form spills there), FP64 peak the same
-        "roofline": {"bound": "fp64-valu", "achieved": flops, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
-                     "frac": flops / FP64_PEAK_TFS, "alg_flop_per_element": ALG_FLOP_PER_ELE_H27_TOTLAG,
+        "elements": mesh.n_ele, "nnz": mesh.nnz,
+        "path": ("general: h27_element_kernel (G on v_mfma_f64_16x16x4_f64, H/geo on the VALU) + "
+                 "h27_assemble_kernel (symmetric records)"),
+        # bound by the flops the kernel executes (507.6k FMA-flop + ~20k per element, the
+        # reference-coordinate contracted form; EXEC_FLOP_PER_ELE_H27_TOTLAG) against the 37.7 kB
+        # of HBM: 6.7 ns vs 4.7 ns per element at the spec peaks -> FP64 (matrix = vector peak)
+        "roofline": {"bound": "fp64", "achieved": flops, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                     "frac": flops / FP64_PEAK_TFS, "exec_flop_per_element": EXEC_FLOP_PER_ELE_H27_TOTLAG,
+                     "survey_flop_per_element": ALG_FLOP_PER_ELE_H27_TOTLAG,
+                     "survey_count_tflops": flops_survey,
                      "hbm_achieved_gbs": gbs, "hbm_frac": gbs / HBM_PEAK_GBS,
                      "alg_bytes_per_element": ALG_BYTES_PER_ELE_H27,
                      "ms_element_kernel": float(np.mean([a for a, _ in ts])),
