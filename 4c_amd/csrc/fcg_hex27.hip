@@ -33,6 +33,9 @@
 // Fixed summation orders everywhere: bitwise reproducible, no atomics on K or f.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "fcg_internal.hpp"
 #include "fcg_shape.hpp"
 
@@ -399,6 +402,9 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
       __syncthreads();
       if (tid < kNchunk)
       {
+        // unrolled by 3: three Gauss points' LDS loads in flight at once (the loop is LDS-latency
+        // bound otherwise: FCG_STAMPS measured 20k cycles per element for this phase)
+#pragma unroll 3
         for (int g = 0; g < kNpe; ++g)
         {
           const double* wv = sh.work() + 6 * (27 * g + ca);
@@ -442,6 +448,7 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
       const int t = tid - 175;
       const int a = t / 3, i = t - 3 * (t / 3);
       double f = 0.0;
+#pragma unroll 9
       for (int g = 0; g < kNpe; ++g)
       {
         const double* R = sh.R() + 9 * g + 3 * i;
@@ -632,7 +639,14 @@ __global__ __launch_bounds__(64) void h27_assemble_kernel(H27AsmArgs A)
       c.off[s] = i * rowlen + pos[b] + j;
     }
   };
-  for (int64_t it = blockIdx.x; it < A.n_rownodes; it += gridDim.x)
+  // XCD-contiguous work: workgroup b runs on XCD b % 8 (round-robin dispatch); XCD x walks its
+  // own eighth of the Morton order, its workgroups interleaved, so that the row nodes in flight on
+  // one XCD are a compact piece of the mesh and the records they share stay in that XCD's L2
+  const int xcd = int(blockIdx.x & 7u);
+  const int64_t per_xcd = (int64_t(gridDim.x) + 7 - xcd) / 8;
+  const int64_t chunk = (A.n_rownodes + 7) / 8;
+  const int64_t x0 = min(A.n_rownodes, int64_t(xcd) * chunk), x1 = min(A.n_rownodes, x0 + chunk);
+  for (int64_t it = x0 + (blockIdx.x >> 3); it < x1; it += per_xcd)
   {
     const int64_t r = A.order ? A.order[it] : it;
     const int32_t row0 = A.rownode_row0[r];
@@ -773,8 +787,14 @@ hipError_t launch_h27_assemble(const DeviceMesh& m, bool want_k, bool overwrite,
   a.rec = m.scratch;
   a.K = d_K;
   a.fint = d_fint;
-  const int64_t cap = 256 * 32;
-  const dim3 grid(unsigned(m.n_rownodes < cap ? m.n_rownodes : cap)), block(64);
+  // a multiple of the 8 XCDs; 512 wavefronts in flight per XCD keep its records' working set
+  // near its 4 MB L2 (FCG_H27_ASM_GRID overrides, for A/B runs)
+  static const int64_t cap = [] {
+    const char* e = std::getenv("FCG_H27_ASM_GRID");
+    return e ? std::max<int64_t>(8, std::atoll(e) / 8 * 8) : int64_t(4096);
+  }();
+  const int64_t want = std::min<int64_t>(cap, (m.n_rownodes + 7) / 8 * 8);
+  const dim3 grid(unsigned(std::max<int64_t>(8, want))), block(64);
   if (want_k && overwrite)
     hipLaunchKernelGGL((h27_assemble_kernel<true, true>), grid, block, 0, stream, a);
   else if (want_k)
