@@ -395,11 +395,12 @@ def test_tsi_fused_rejects_unqualified_contexts():
 
 
 @pytest.mark.gpu
-def test_tsi_fused_full_size_properties():
-    """Config 5 at 100^3 hex8 (1M elements): fused and two-kernel paths agree; f_T = K_TT T and
-    f_S = K_SS u + K_ST (T - T_0) hold through the library's SpMV."""
+@pytest.mark.parametrize("n", [100, 126])
+def test_tsi_fused_full_size_properties(n):
+    """Config 5's box at 100^3 and at its stated 126^3 (2M hex8): fused and two-kernel paths
+    agree; f_T = K_TT T and f_S = K_SS u + K_ST (T - T_0) hold through the library's SpMV."""
     torch, dev = _dev()
-    mesh = fcg.BoxMesh(fcg.HEX8, (100, 100, 100))
+    mesh = fcg.BoxMesh(fcg.HEX8, (n, n, n))
     u, v, Tn = _fields(mesh)
     ev = fcg.Evaluator(mesh, kinematics=fcg.LINEAR, youngs=E, poisson=NU, path=fcg.PATH_STRUCTURED)
     tev = fcg.TsiEvaluator(mesh, E, NU, ALPHA, T0, COND)
@@ -419,6 +420,63 @@ def test_tsi_fused_full_size_properties():
     assert _rel(Ktt @ Tn, r["fT"]) <= 1e-12
     assert _rel(Kss @ u + Kst @ (Tn - T0), r["fs"]) <= 1e-12
 
+
+
+def _fields_xyz(mesh):
+    """States as functions of the node position only, so that every rank split sees the same."""
+    X = mesh.node_x
+    u = mesh.u_col(1e-3)
+    vn = 1e-2 * np.stack([np.cos(3 * X[:, 0] + X[:, 1]), np.sin(2 * X[:, 1] - X[:, 2]),
+                          np.cos(X[:, 0] * X[:, 2])], axis=1)
+    v = np.zeros(mesh.n_cols)
+    for d in range(3):
+        v[mesh.node_dof_col + d] = vn[:, d]
+    Tn = T0 + 50.0 * np.sin(2 * np.pi * X[:, 0]) * np.cos(np.pi * X[:, 1]) + 10.0 * X[:, 2]
+    return u, v, Tn
+
+
+@pytest.mark.gpu
+def test_tsi_config5_eight_rank_split_full_size():
+    """Config 5 as it is partitioned on 8 GPUs (126^3 hex8, GridGenerator split into 8 ranks with
+    ghost layers), every rank evaluated in turn on one GPU: each rank's rows satisfy
+    f_T = K_TT T and f_S = K_SS u + K_ST (T - T_0) on its column map, and its owned residual rows
+    equal the 1-rank evaluation's by DOF / node GID."""
+    torch, dev = _dev()
+    sp = pytest.importorskip("scipy.sparse")
+    n = 126
+
+    def run(rank, nranks):
+        mesh = fcg.BoxMesh(fcg.HEX8, (n, n, n), rank=rank, nranks=nranks)
+        u, v, Tn = _fields_xyz(mesh)
+        ev = fcg.Evaluator(mesh, kinematics=fcg.LINEAR, youngs=E, poisson=NU, path=fcg.PATH_STRUCTURED)
+        tev = fcg.TsiEvaluator(mesh, E, NU, ALPHA, T0, COND)
+        g = tev.graph
+        r = _gpu_fused(mesh, tev, ev, u, v, Tn)
+        ev.close()
+        tev.close()
+        Ktt = sp.csr_matrix((r["Ktt"], g.col_tt, g.rowptr_tt), shape=(g.n_rows_t, g.n_cols_t))
+        Kss = sp.csr_matrix((r["Kss"], mesh.col_lid, mesh.rowptr), shape=(mesh.n_rows, mesh.n_cols))
+        Kst = sp.csr_matrix((r["Kst"], g.col_st, g.rowptr_st), shape=(mesh.n_rows, g.n_cols_t))
+        assert _rel(Ktt @ Tn, r["fT"]) <= 1e-12, rank
+        assert _rel(Kss @ u + Kst @ (Tn - T0), r["fs"]) <= 1e-12, rank
+        # owned residual rows by GID (thermo row t = the node of structural rows 3t..3t+2)
+        return mesh.row_gid.astype(np.int64), r["fs"], mesh.row_gid[0::3].astype(np.int64), r["fT"], \
+            mesh.n_ele_global
+
+    gs, fs1, gt, fT1, n_glob = run(0, 1)
+    size = int(gs.max()) + 1
+    S1, S8 = np.full(size, np.nan), np.full(size, np.nan)
+    T1, T8 = np.full(size, np.nan), np.full(size, np.nan)
+    S1[gs], T1[gt] = fs1, fT1
+    for rank in range(8):
+        a, fa, b, fb, ng = run(rank, 8)
+        assert ng == n_glob == 2_000_376
+        assert np.all(np.isnan(S8[a]))  # every row owned by exactly one rank
+        S8[a], T8[b] = fa, fb
+    assert np.array_equal(np.isnan(S1), np.isnan(S8)) and np.array_equal(np.isnan(T1), np.isnan(T8))
+    ok_s, ok_t = ~np.isnan(S1), ~np.isnan(T1)
+    assert np.linalg.norm(S8[ok_s] - S1[ok_s]) <= 1e-12 * np.linalg.norm(S1[ok_s])
+    assert np.linalg.norm(T8[ok_t] - T1[ok_t]) <= 1e-12 * np.linalg.norm(T1[ok_t])
 
 
 @pytest.mark.parametrize("nranks,nworkers", [(1, 1), (1, 4), (2, 3)])
