@@ -272,7 +272,10 @@ bool build_structured_plan(const fcg_desc* d, const std::vector<int32_t>& rownod
   P.tiles_x = (P.n[0] + 3) / 4;
   P.tiles_y = (P.n[1] + 3) / 4;
   const int64_t txy = int64_t(P.tiles_x) * P.tiles_y;
-  const int64_t slots = int64_t(std::max(1, cus)) * (d->kinematics == FCG_TOTLAG ? 1 : 2);
+  // FCG_SWEEP_WGS_PER_CU: occupancy probes (tools/exp_lib.sh builds with another launch bound)
+  const char* wenv = std::getenv("FCG_SWEEP_WGS_PER_CU");
+  const int wpc = wenv ? std::max(1, std::atoi(wenv)) : 2;
+  const int64_t slots = int64_t(std::max(1, cus)) * (d->kinematics == FCG_TOTLAG ? 1 : wpc);
   int64_t nseg = 1;
   double best = 0.0;
   for (int64_t k = 1; k <= std::min<int64_t>(P.n[2], 64); ++k)
@@ -465,6 +468,72 @@ void free_mesh(fcg::DeviceMesh& m)
   m = fcg::DeviceMesh{};
 }
 
+// The CSR graph of the owned rows from the column elements, built by fcg_graph_build_device (the
+// sorted-row graph Epetra_CrsMatrix::FillComplete gives 4C after the first assembly through the
+// unfilled path, 4C_linalg_sparsematrix.cpp:578-611, 843-865), columns in the matrix column map
+// (kcol), brought back to the host for the plan builders below.
+int graph_on_device(const fcg_desc* d, const int32_t* kcol, std::vector<int64_t>& rowptr,
+    std::vector<int32_t>& col, std::string& why)
+{
+  const int npe = d->celltype == FCG_HEX27 ? 27 : 8;
+  if (d->n_rows % 3 != 0)
+  {
+    why = "n_rows must be 3 x owned nodes";
+    return FCG_ERR_ARG;
+  }
+  for (int64_t n = 0; n < d->n_node; ++n)
+    if (kcol[n] < 0 || (d->node_dof_row[n] >= 0 && d->node_dof_row[n] % 3 != 0))
+    {
+      why = "node DOF LIDs must be non-negative and owned rows start at multiples of 3";
+      return FCG_ERR_ARG;
+    }
+  if (!fcg_use_device(d->device))
+  {
+    why = "hipSetDevice failed";
+    return fcg_device_error();
+  }
+  int32_t *en = nullptr, *dc = nullptr, *dr = nullptr, *cl = nullptr;
+  int64_t* rp = nullptr;
+  int64_t bytes = 0, nnz = 0;
+  hipError_t he = hipSuccess;
+  auto chk = [&](hipError_t x) {
+    if (he == hipSuccess) he = x;
+  };
+  chk(upload(&en, d->ele_nodes, d->n_ele * npe, bytes));
+  chk(upload(&dc, kcol, d->n_node, bytes));
+  chk(upload(&dr, d->node_dof_row, d->n_node, bytes));
+  chk(upload<int64_t>(&rp, nullptr, d->n_rows + 1, bytes));
+  int rc = FCG_OK;
+  if (he == hipSuccess)
+    rc = fcg_graph_build_device(d->device, d->celltype, d->n_ele, en, d->n_node, dc, dr, d->n_rows, rp,
+        nullptr, 0, &nnz, nullptr);
+  if (he == hipSuccess && rc == FCG_OK)
+  {
+    chk(upload<int32_t>(&cl, nullptr, std::max<int64_t>(nnz, 1), bytes));
+    if (he == hipSuccess)
+      rc = fcg_graph_build_device(d->device, d->celltype, d->n_ele, en, d->n_node, dc, dr, d->n_rows,
+          rp, cl, nnz, &nnz, nullptr);
+  }
+  if (he == hipSuccess && rc == FCG_OK)
+  {
+    rowptr.resize(d->n_rows + 1);
+    col.resize(nnz);
+    chk(hipMemcpy(rowptr.data(), rp, sizeof(int64_t) * rowptr.size(), hipMemcpyDeviceToHost));
+    if (nnz > 0) chk(hipMemcpy(col.data(), cl, sizeof(int32_t) * size_t(nnz), hipMemcpyDeviceToHost));
+  }
+  for (void* p : {static_cast<void*>(en), static_cast<void*>(dc), static_cast<void*>(dr),
+           static_cast<void*>(rp), static_cast<void*>(cl)})
+    if (p) (void)hipFree(p);
+  if (he != hipSuccess)
+  {
+    why = hipGetErrorString(he);
+    return fcg_device_error();
+  }
+  if (rc != FCG_OK) why = rc == FCG_ERR_ARG ? "row LIDs inconsistent or more than 16 elements at a node"
+                                            : "device error";
+  return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -512,9 +581,12 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
     set_create_error("the structured sweep implements StVenantKirchhoff only");
     return FCG_ERR_ARG;
   }
+  // rowptr = col_lid = NULL: the graph is built here, on the device (FillComplete of the first
+  // assembly, see graph_on_device); one of the two alone is an error
+  const bool build_graph = d->n_rows > 0 && !d->rowptr && !d->col_lid;
   if (d->n_ele < 0 || d->n_node < 0 || d->n_rows < 0 || d->n_cols < 0 ||
       (d->n_ele > 0 && (!d->ele_nodes || !d->node_x || !d->node_dof_col || !d->node_dof_row)) ||
-      (d->n_rows > 0 && (!d->rowptr || !d->col_lid)) || d->n_ele >= (int64_t(1) << 31))
+      (d->n_rows > 0 && !build_graph && (!d->rowptr || !d->col_lid)) || d->n_ele >= (int64_t(1) << 31))
   {
     set_create_error("invalid descriptor arrays/sizes");
     return FCG_ERR_ARG;
@@ -542,6 +614,23 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
       set_create_error("node_dof_row out of range");
       return FCG_ERR_ARG;
     }
+  }
+  fcg_desc dg;
+  std::vector<int64_t> g_rowptr;
+  std::vector<int32_t> g_col;
+  if (build_graph)
+  {
+    std::string why;
+    const int rc = graph_on_device(d, kcol, g_rowptr, g_col, why);
+    if (rc != FCG_OK)
+    {
+      set_create_error("graph on the device: " + why);
+      return rc;
+    }
+    dg = *d;
+    dg.rowptr = g_rowptr.data();
+    dg.col_lid = g_col.data();
+    d = &dg;
   }
 
   // --- owned row nodes, ascending by row LID
@@ -1359,10 +1448,30 @@ int fcg_get_info(const fcg_ctx* ctx, fcg_info* info)
   info->n_cols = m.n_cols;
   info->nnz = m.nnz;
   info->n_incidences = m.n_inc;
-  info->scratch_bytes = m.scratch ? m.n_inc * fcg::record_doubles(m.npe) * int64_t(sizeof(double)) : 0;
+  info->scratch_bytes = !m.scratch ? 0
+                        : m.h27s   ? m.n_ele * fcg::kH27RecDoubles * int64_t(sizeof(double))
+                                   : m.n_inc * fcg::record_doubles(m.npe) * int64_t(sizeof(double));
   info->device_bytes = ctx->device_bytes;
   info->path = m.path;
   return FCG_OK;
+}
+
+int fcg_get_graph(const fcg_ctx* ctx, int64_t* rowptr, int32_t* col_lid, int64_t col_capacity,
+    int64_t* nnz)
+{
+  if (!ctx || !nnz) return FCG_ERR_ARG;
+  const fcg::DeviceMesh& m = ctx->mesh;
+  *nnz = m.nnz;
+  if (col_lid && col_capacity < m.nnz) return FCG_ERR_ARG;
+  if (!fcg_use_device(ctx->device)) return fcg_device_error();
+  hipError_t he = hipSuccess;
+  if (rowptr && m.n_rows > 0)
+    he = hipMemcpy(rowptr, m.rowptr, sizeof(int64_t) * size_t(m.n_rows + 1), hipMemcpyDeviceToHost);
+  else if (rowptr)
+    rowptr[0] = 0;
+  if (he == hipSuccess && col_lid && m.nnz > 0)
+    he = hipMemcpy(col_lid, m.col_lid, sizeof(int32_t) * size_t(m.nnz), hipMemcpyDeviceToHost);
+  return he == hipSuccess ? FCG_OK : fcg_device_error();
 }
 
 int fcg_device_alloc(int device, int64_t bytes, void** d_ptr)

@@ -110,7 +110,11 @@ struct SweepShared {
   // [column][in-plane neighbour (dy+1)*3 + dx+1][3x3 | TSI: k_ST 3 | k_TS 3 | k_TT 1]
   // (TSI rows padded to 18 doubles: with 16 every (column, t) record started on the same bank;
   // thermal-only pass TH: k_ST 3 | k_TS 3 | k_TT 1, padded to 9)
+#ifdef FCG_PROBE_WG3
+  double hold[1][9][TSI ? (TH ? 9 : 18) : 9];  // timing probe only: one column's buffer for all
+#else
   double hold[TX * TY][9][TSI ? (TH ? 9 : 18) : 9];
+#endif
 };
 
 __device__ inline int ring(int p) { return (p % 3 + 3) % 3; }
@@ -453,7 +457,10 @@ __device__ inline void block_k(const StVK& m, const double* acc, double* Kb)
 // 2: the thermal-only pass that follows a MODE-0 linear sweep (k_ST, k_TS, k_TT, f_T, and
 // k_ST (T - T_0) added into f_S) -- 8 accumulators per block instead of 16, no K stores.
 template <int KIN, bool WANT_K, bool OVERWRITE, int MODE>
-__global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
+#ifndef FCG_SWEEP_WGS
+#define FCG_SWEEP_WGS 2
+#endif
+__global__ __launch_bounds__(256, KIN ? 1 : FCG_SWEEP_WGS) void sweep_h8_kernel(SweepArgs A)
 {
   constexpr bool TSI = MODE != 0, TH = MODE == 2;
   static_assert(!TSI || (KIN == 0 && WANT_K), "TSI is geometrically linear, full tangent");
@@ -653,7 +660,11 @@ __global__ __launch_bounds__(256, KIN ? 1 : 2) void sweep_h8_kernel(SweepArgs A)
         {
           constexpr int NK = TH ? 0 : 9;  // structural entries held (none in the thermal pass)
           constexpr int NH = NK + (TSI ? 7 : 0);
+#ifdef FCG_PROBE_WG3
+          double* h = sh.hold[0][t - 9];
+#else
           double* h = sh.hold[c][t - 9];
+#endif
           double held[NH];
 #pragma unroll
           for (int i = 0; i < NH; ++i) held[i] = h[i];

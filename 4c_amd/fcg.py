@@ -130,7 +130,7 @@ EXPORTS = ["fcg_create", "fcg_destroy", "fcg_last_error", "fcg_evaluate", "fcg_e
            "fcg_get_diagnostics", "fcg_measure_peaks", "fcg_measure_hbm", "fcg_spmv", "fcg_dirichlet_apply",
            "fcg_pcg_solve", "fcg_spmv_f32", "fcg_block_jacobi_setup", "fcg_block_jacobi_apply", "fcg_node_transfer",
            "fcg_neumann_surface", "fcg_neumann_volume",
-           "fcg_graph_build_device",
+           "fcg_graph_build_device", "fcg_get_graph",
            "fcg_tsi_create", "fcg_tsi_destroy", "fcg_tsi_last_error", "fcg_tsi_evaluate_device",
            "fcg_tsi_evaluate_fused",
            "fcg_box_mesh_create", "fcg_box_mesh_destroy", "fcg_box_mesh_desc", "fcg_box_mesh_maps",
@@ -247,6 +247,7 @@ def lib():
     L.fcg_graph_build_device.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64, vp,
                                          ctypes.c_int64, vp, vp, ctypes.c_int64, vp, vp,
                                          ctypes.c_int64, _i64p, vp]
+    L.fcg_get_graph.argtypes = [vp, _i64p, _i32p, ctypes.c_int64, _i64p]
     L.fcg_tsi_create.argtypes = [ctypes.POINTER(FcgTsiDesc), ctypes.POINTER(vp)]
     L.fcg_tsi_destroy.argtypes = [vp]
     L.fcg_tsi_last_error.argtypes = [vp]
@@ -620,6 +621,22 @@ class Evaluator:
         info = FcgInfo()
         L.fcg_get_info(h, ctypes.byref(info))
         self.info = info
+
+    def graph(self):
+        """fcg_get_graph: (rowptr int64, col_lid int32) host copies of the context's CSR graph --
+        the device-built one when the descriptor came without rowptr / col_lid."""
+        L = lib()
+        nnz = ctypes.c_int64(0)
+        rc = L.fcg_get_graph(self._h, None, None, 0, ctypes.byref(nnz))
+        if rc != 0:
+            self._raise(rc, -1)
+        rowptr = np.empty(self.info.n_rows + 1, dtype=np.int64)
+        col = np.empty(max(nnz.value, 1), dtype=np.int32)
+        rc = L.fcg_get_graph(self._h, _np_ptr(rowptr, _i64p), _np_ptr(col, _i32p), nnz.value,
+                             ctypes.byref(nnz))
+        if rc != 0:
+            self._raise(rc, -1)
+        return rowptr, col[:nnz.value]
 
     def close(self):
         if getattr(self, "_h", None):

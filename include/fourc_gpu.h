@@ -79,7 +79,12 @@ typedef struct fcg_desc {
   const int32_t* node_dof_kcol;/* [n_node] LID of the node's first DOF in the MATRIX column map
                                   (Epetra_CrsMatrix::ColMap after FillComplete); NULL = same as
                                   node_dof_col */
-  const int64_t* rowptr;       /* [n_rows + 1] */
+  const int64_t* rowptr;       /* [n_rows + 1]; rowptr = col_lid = NULL: fcg_create builds the graph
+                                  on the device (fcg_graph_build_device: rows = owned DOFs, columns
+                                  = DOFs of the nodes sharing an element, sorted) and
+                                  fcg_get_graph returns it -- 4C's first assembly through the
+                                  unfilled path + FillComplete, 4C_linalg_sparsematrix.cpp:578-611,
+                                  843-865.  Needs n_rows = 3 x owned nodes. */
   const int32_t* col_lid;      /* [rowptr[n_rows]] */
   /* Optional structured-lattice hint (GridGenerator meshes): [n_ele][3] element lattice
    * position (ex, ey, ez) = (gid % nx, gid / nx % ny, gid / (nx ny)), 4C_io_gridgenerator.cpp:336-338.
@@ -164,6 +169,13 @@ typedef struct fcg_info {
   int32_t reserved;
 } fcg_info;
 int fcg_get_info(const fcg_ctx* ctx, fcg_info* info);
+
+/* The context's CSR graph (host copies): rowptr [n_rows + 1] when non-NULL, col_lid [nnz] when
+ * non-NULL and col_capacity >= nnz; *nnz always.  For a context created with rowptr = col_lid =
+ * NULL this is the graph fcg_create built on the device -- what a 4C host then hands to its
+ * Epetra_CrsGraph / SparseMatrix (the FillComplete'd graph of the first assembly). */
+int fcg_get_graph(const fcg_ctx* ctx, int64_t* rowptr, int32_t* col_lid, int64_t col_capacity,
+    int64_t* nnz);
 
 /* On-box peaks for the roofline (SURVEY §8d asks to re-measure the spec figures): STREAM triad
  * bandwidth over 3 x 1 GiB HBM arrays (GB/s), FP64 VALU FMA and FP64 MFMA (v_mfma_f64_16x16x4_f64)

@@ -71,3 +71,51 @@ def test_device_graph_full_size():
     print(f"device graph 100^3 hex8: {t1 - t0:.3f} s for {len(cl)} nonzeros (incl. copies)")
     assert np.array_equal(rp, m.rowptr)
     assert np.array_equal(cl, m.col_lid)
+
+
+def _u_col(mesh):
+    """A displacement column vector of the mesh: the synthetic field at the column nodes."""
+    u = np.zeros(mesh.n_cols)
+    X = mesh.node_x
+    for d in range(3):
+        u[mesh.node_dof_col + d] = 0.01 * np.sin(2.0 * X[:, d] + d)
+    return u
+
+
+@pytest.mark.parametrize("celltype,iv,rank,nranks,kin,path", [
+    (fcg.HEX8, (6, 5, 4), 0, 1, fcg.LINEAR, fcg.PATH_AUTO),
+    (fcg.HEX8, (6, 4, 4), 1, 2, fcg.TOTLAG, fcg.PATH_AUTO),
+    (fcg.HEX8, (5, 4, 3), 0, 1, fcg.TOTLAG, fcg.PATH_GATHER),
+    (fcg.HEX27, (3, 2, 2), 0, 1, fcg.TOTLAG, fcg.PATH_AUTO),
+    (fcg.HEX27, (4, 2, 2), 1, 2, fcg.LINEAR, fcg.PATH_AUTO)])
+def test_create_builds_the_graph_on_the_device(celltype, iv, rank, nranks, kin, path):
+    """fcg_create with rowptr = col_lid = NULL builds the FillComplete graph on the device and
+    hands it back (fcg_get_graph); the assembly into it is bitwise the one into the host graph."""
+    _dev()
+    m = fcg.BoxMesh(celltype, iv, rank=rank, nranks=nranks)
+    d_host = m.desc(kin, 210.0, 0.3, path=path)
+    d_dev = m.desc(kin, 210.0, 0.3, path=path)
+    d_dev.rowptr = None
+    d_dev.col_lid = None
+    ev_h, ev_d = fcg.Evaluator(d_host), fcg.Evaluator(d_dev)
+    assert ev_d.info.path == ev_h.info.path and ev_d.info.nnz == m.nnz
+    rp, cl = ev_d.graph()
+    assert np.array_equal(rp, m.rowptr) and np.array_equal(cl, m.col_lid)
+    u = _u_col(m)
+    out = []
+    for ev in (ev_h, ev_d):
+        f, K = np.zeros(m.n_rows), np.zeros(m.nnz)
+        ev.evaluate(fcg.CALC_NLNSTIFF, u, f, K)
+        out.append((f, K))
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+    assert np.abs(out[0][1]).max() > 0.0
+
+
+def test_create_rejects_half_a_graph():
+    _dev()
+    m = fcg.BoxMesh(fcg.HEX8, (2, 2, 2))
+    d = m.desc(fcg.LINEAR, 210.0, 0.3)
+    d.col_lid = None
+    with pytest.raises(fcg.FcgError) as ei:
+        fcg.Evaluator(d)
+    assert ei.value.code == 3
