@@ -1067,7 +1067,12 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
       const std::vector<int64_t> ord = morton_order(key);
       std::vector<int32_t> ord32(ord.begin(), ord.end());
       chk(upload(&m.asm_order, ord32.data(), nrn, bytes));
-      chk(upload<double>(&m.scratch, nullptr, d->n_ele * fcg::kH27RecDoubles, bytes));
+      // output: the owned incidences' block rows (assemble27_kernel reads each once, contiguous);
+      // FCG_H27_SYMREC=1: one symmetric record per element (blocks a <= b) and h27_assemble_kernel
+      const char* sym = std::getenv("FCG_H27_SYMREC");
+      m.h27_increc = !(sym && sym[0] == '1');
+      chk(upload<double>(&m.scratch, nullptr,
+          m.h27_increc ? n_inc * fcg::record_doubles(npe) : d->n_ele * fcg::kH27RecDoubles, bytes));
     }
     else
       chk(upload<double>(&m.scratch, nullptr, n_inc * fcg::record_doubles(npe), bytes));
@@ -1293,8 +1298,9 @@ int fcg_evaluate_device(fcg_ctx* ctx, int action, int mode, const double* d_u_co
                   : fcg::launch_element(m, d_u_col, want_k, s);
     if (T.enabled && he == hipSuccess) he = hipEventRecord(T.ev[1], s);
     if (he == hipSuccess)
-      he = m.h27s ? fcg::launch_h27_assemble(m, want_k, mode == FCG_OVERWRITE, d_K_vals, d_fint_row, s)
-                  : fcg::launch_assemble(m, want_k, mode == FCG_OVERWRITE, d_K_vals, d_fint_row, s);
+      he = m.h27s && !m.h27_increc
+               ? fcg::launch_h27_assemble(m, want_k, mode == FCG_OVERWRITE, d_K_vals, d_fint_row, s)
+               : fcg::launch_assemble(m, want_k, mode == FCG_OVERWRITE, d_K_vals, d_fint_row, s);
   }
   if (T.enabled && he == hipSuccess)
   {
@@ -1449,7 +1455,7 @@ int fcg_get_info(const fcg_ctx* ctx, fcg_info* info)
   info->nnz = m.nnz;
   info->n_incidences = m.n_inc;
   info->scratch_bytes = !m.scratch ? 0
-                        : m.h27s   ? m.n_ele * fcg::kH27RecDoubles * int64_t(sizeof(double))
+                        : m.h27s && !m.h27_increc ? m.n_ele * fcg::kH27RecDoubles * int64_t(sizeof(double))
                                    : m.n_inc * fcg::record_doubles(m.npe) * int64_t(sizeof(double));
   info->device_bytes = ctx->device_bytes;
   info->path = m.path;

@@ -15,15 +15,18 @@
 //             fac N_XYZ_a . S N_XYZ_b = d_a^T V d_b, V = fac J^-T S J^-1
 //             f_a = sum_g R_g d_a,  R = fac F S J^-1 (linear: fac S J^-1)     (calc_lib.hpp:851-860)
 //        3. the isotropic StVK blocks of every node pair a <= b (B_a^T C B_b + K_geo,
-//           calc_lib.hpp:872-927):
+//           calc_lib.hpp:872-927), all on v_mfma_f64_16x16x4_f64 tiles of 16 x 16 node pairs:
 //             K_ab = lambda G + mu G^T + mu H + geo I          (linear: mu tr(G) I, no H / geo)
-//             G_ij = sum_g fac q_a,i q_b,j     -> v_mfma_f64_16x16x4_f64 (waves 0-2)
-//             H = sum_g (d_a^T W d_b) F F^T, geo = sum_g d_a^T V d_b  -> VALU, 2 pairs a lane
-//           The matrix cores take the 9-FMA part of the 21 FMAs per pair and point; the VALU
-//           lanes the other 12.
-//      Output: one record per element, the 378 blocks a <= b (3 x 3 column-major, pair order
-//      a-major) and f_e (27 x 3) -- 27.9 KB instead of the 53 KB of per-incidence block rows,
-//      since K_ba = K_ab^T is not stored twice.
+//             G_ij = sum_g fac q_a,i q_b,j                     (waves 0-2, K = 27 Gauss points)
+//             H = sum_g c_ab(g) F F^T, c_ab = d_a^T W d_b     (waves 0-2: one MFMA per point
+//                                                                for c, then 24 lane FMAs)
+//             geo = sum_(g,k) (V d_a)_k d_b,k                  (wave 3, K = 81)
+//           and f_a (wave 3, while waves 0-2 run G); every operand is formed on the fly from
+//           the constant dN_a(xi_g) and the per-point factors (no per-(g, a) work arrays);
+//        4. K_ab into an LDS image of the element's 378 blocks a <= b.
+//      Output: the owned incidences' block rows (3 x 81 + f, the general path's record, read
+//      contiguously by assemble27_kernel) -- or, FCG_H27_SYMREC=1, one record per element with the
+//      378 blocks a <= b and f_e (27.9 KB instead of 27 x 1.9 KB) for h27_assemble_kernel.
 //  h27_assemble_kernel  SparseMatrix::assemble + LinAlg::assemble (4C_linalg_sparsematrix.cpp:
 //      444-576, 4C_linalg_utils_sparse_algebra_assemble.cpp:72-92) for owned rows: one wavefront
 //      per owned row node sums the block rows of its incident elements (K_ab or K_ba^T from the
@@ -46,14 +49,13 @@ namespace {
 constexpr int kNpe = 27;
 constexpr int kNpair = 378;
 constexpr int kBlk = 256;
-constexpr int kNchunk = 196;  // VALU pair chunks (a, b0, nb <= 2)
 constexpr int64_t kRec = kH27RecDoubles;  // 378 blocks x 9 | f 27 x 3 | pad
+constexpr int64_t kIncRec = 9 * kNpe + 3;  // increc: one owned incidence's 3 x 81 block row | f
 
 __constant__ double c_dN[27 * 27 * 3];  // dN_c,d at Gauss point g: [g][c][d]
 __constant__ double c_w[27];
 __constant__ double c_L1[9], c_dL1[9], c_dLn[9];  // 1D Lagrange factors (fcg_kernels.hip)
 __constant__ uint8_t c_loc[27], c_latnode[27];
-__constant__ uint32_t c_chunk[kNchunk];  // a | b0 << 8 | nb << 16
 
 __device__ inline int pidx(int a, int b)  // a <= b
 {
@@ -89,18 +91,16 @@ __device__ inline double inv3(double* m)
 }
 
 // LDS of one element's workgroup.  `big` holds stage-dependent views (offsets below):
-//   J | Gu | T | W | V | M | R (Gauss-point data, dead after the matrix-core phase) followed by
-//   the pair-stage work area: w, v per (g, a) [27][27][6] (TotLag) | q per (g, a) [27][27][3];
-//   after the matrix-core phase the mu H + geo I image [378][7] lies at H_IMG (TotLag) and the
-//   element's K image [378][9] at 0: disjoint, so a lane reads its H entries and writes its K
-//   blocks without a barrier in between.
+//   J | Gu | T | W | V | M | R (Gauss-point data, dead after the matrix-core phases), overlaid by
+//   the element's K image [378][9] once they are done; the geo image [378] (TotLag) after it.
 constexpr int OFF_J = 0, OFF_GU = 243, OFF_T = 486, OFF_W = 729, OFF_V = 891, OFF_M = 1053,
-              OFF_R = 1215, OFF_WORK = 1458, OFF_KIMG = 0, OFF_HIMG = kNpair * 9;
-constexpr int BIG = OFF_HIMG + kNpair * 7;  // >= OFF_WORK + 27 * 27 * 6
-static_assert(BIG >= OFF_WORK + 27 * 27 * 6, "work area");
+              OFF_R = 1215, OFF_KIMG = 0, OFF_GEO = kNpair * 9;
+constexpr int BIG = OFF_GEO + kNpair;
+static_assert(OFF_R + 243 <= OFF_GEO, "Gauss-point factors inside the K image region");
 struct H27Shared {
   double dN[27 * 27 * 3];  // [g][c][d], loaded once per workgroup
   double X[2][81], U[2][81];  // double-buffered: the next element's arrive during this one
+  int32_t inc[2][27];         // increc: incidence of (e, a), double-buffered like X, U
   double fac[27];
   alignas(16) double big[BIG];
   double L1[9], dL1[9], dLn[9];
@@ -115,9 +115,8 @@ struct H27Shared {
   __device__ double* V() { return big + OFF_V; }
   __device__ double* M() { return big + OFF_M; }
   __device__ double* R() { return big + OFF_R; }
-  __device__ double* work() { return big + OFF_WORK; }
   __device__ double* kimg() { return big + OFF_KIMG; }
-  __device__ double* himg() { return big + OFF_HIMG; }
+  __device__ double* geo() { return big + OFF_GEO; }
 };
 
 struct H27Args {
@@ -127,6 +126,8 @@ struct H27Args {
   const int32_t* node_dof_col;
   const double* u_col;
   double* rec;
+  const int32_t* inc_of;  // increc: [n_ele][27] incidence of (e, a), -1 = a not owned
+  int increc;             // 1: per-incidence block rows [n_inc][246] (assembled by assemble27_kernel)
   int32_t* err;
   double lambda, mu, cdiag;
   int want_k;
@@ -135,15 +136,11 @@ struct H27Args {
 
 typedef double f64x4_t __attribute__((ext_vector_type(4)));
 
-__device__ inline void symv(const double* S, const double* x, double* y)  // y = S x, S sym6
-{
-  y[0] = S[0] * x[0] + S[3] * x[1] + S[5] * x[2];
-  y[1] = S[3] * x[0] + S[1] * x[1] + S[4] * x[2];
-  y[2] = S[5] * x[0] + S[4] * x[1] + S[2] * x[2];
-}
-
 template <int KIN>
-__global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
+#ifndef FCG_H27_LIN_WGS
+#define FCG_H27_LIN_WGS 2
+#endif
+__global__ __launch_bounds__(kBlk, KIN ? 2 : FCG_H27_LIN_WGS) void h27_element_kernel(H27Args A)
 {
   __shared__ H27Shared sh;
   const int tid = threadIdx.x;
@@ -160,9 +157,6 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
     sh.loc[tid] = c_loc[tid];
     sh.latnode[tid] = c_latnode[tid];
   }
-  // VALU pair chunk of this lane (TotLag)
-  const uint32_t chunk = tid < kNchunk ? c_chunk[tid] : 0u;
-  const int ca = chunk & 0xff, cb0 = (chunk >> 8) & 0xff, cnb = tid < kNchunk ? int(chunk >> 16) : 0;
   const double lam = A.lambda, mu = A.mu;
 
   // 0. X and u of the element (evaluate_element_nodes, calc_lib.hpp:180-203) are loaded one
@@ -170,6 +164,7 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
   //    of an element and lands in the other LDS buffer before that element's first global store
   //    (gfx9 counts stores in vmcnt: a wait for loads issued after stores would wait for those)
   double xpre = 0.0, upre = 0.0;
+  int32_t ipre = -1;
   auto prefetch = [&](int64_t e) {
     if (tid < 81 && e < A.n_ele)
     {
@@ -178,6 +173,8 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
       xpre = A.node_x[3 * int64_t(node) + d];
       upre = A.u_col[A.node_dof_col[node] + d];
     }
+    else if (A.increc && tid >= 96 && tid < 96 + kNpe && e < A.n_ele)
+      ipre = A.inc_of[e * kNpe + tid - 96];
   };
   prefetch(blockIdx.x);
   if (tid < 81)
@@ -185,6 +182,8 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
     sh.X[0][tid] = xpre;
     sh.U[0][tid] = upre;
   }
+  else if (tid >= 96 && tid < 96 + kNpe)
+    sh.inc[0][tid - 96] = ipre;
   int buf = 0;
   // diagnostic phase timers (FCG_STAMPS=1, tools/h27_stamps.py): thread 0's s_memtime deltas per
   // phase, barrier waits included: 0 gather + J, 1 Gauss-point algebra, 2 VALU pair sums,
@@ -202,7 +201,7 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
   for (int64_t e = blockIdx.x; e < A.n_ele; e += gridDim.x, buf ^= 1)
   {
     ++st_n;
-    double* rec = A.rec + e * kRec;
+    double* rec = A.rec + (A.increc ? 0 : e * kRec);
     if (tid == 0) sh.bad = 0;
     __syncthreads();
     prefetch(e + gridDim.x);
@@ -371,6 +370,8 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
       sh.X[buf ^ 1][tid] = xpre;
       sh.U[buf ^ 1][tid] = upre;
     }
+    else if (tid >= 96 && tid < 96 + kNpe)
+      sh.inc[buf ^ 1][tid - 96] = ipre;
     if (sh.bad)
     {
       if (tid == 0)
@@ -382,146 +383,164 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
       continue;
     }
 
-    // 3a / 4. TotLag: w = W d_a, v = V d_a per (g, a); then the VALU pair sums
-    //   mu H + geo I:  H = sum_g (w_a . d_b) M_g,  geo = sum_g v_a . d_b
-    double Hacc[2][7];
-#pragma unroll
-    for (int p = 0; p < 2; ++p)
-#pragma unroll
-      for (int k = 0; k < 7; ++k) Hacc[p][k] = 0.0;
-    if (KIN == 1 && A.want_k)
-    {
-      for (int it = tid; it < 729; it += kBlk)
-      {
-        const int g = it / 27;
-        const double* d = sh.dN + 3 * it;
-        double* o = sh.work() + 6 * it;
-        symv(sh.W() + 6 * g, d, o);
-        symv(sh.V() + 6 * g, d, o + 3);
-      }
-      __syncthreads();
-      if (tid < kNchunk)
-      {
-        // unrolled by 3: three Gauss points' LDS loads in flight at once (the loop is LDS-latency
-        // bound otherwise: FCG_STAMPS measured 20k cycles per element for this phase)
-#pragma unroll 3
-        for (int g = 0; g < kNpe; ++g)
-        {
-          const double* wv = sh.work() + 6 * (27 * g + ca);
-          const double w0 = wv[0], w1 = wv[1], w2 = wv[2], v0 = wv[3], v1 = wv[4], v2 = wv[5];
-          const double* Mg = sh.M() + 6 * g;
-          double m[6];
-#pragma unroll
-          for (int k = 0; k < 6; ++k) m[k] = Mg[k];
-#pragma unroll
-          for (int p = 0; p < 2; ++p)
-          {
-            if (p < cnb)
-            {
-              const double* d = sh.dN + 3 * (27 * g + cb0 + p);
-              const double d0 = d[0], d1 = d[1], d2 = d[2];
-              const double c = w0 * d0 + w1 * d1 + w2 * d2;
-              Hacc[p][6] += v0 * d0 + v1 * d1 + v2 * d2;
-#pragma unroll
-              for (int k = 0; k < 6; ++k) Hacc[p][k] += c * m[k];
-            }
-          }
-        }
-      }
-      __syncthreads();  // every read of w, v done: the region becomes q
-    }
-    H27_STAMP(2);
-
-    // 3b. q_a = T d_a per (g, a); f_a = sum_g R_g d_a (add_internal_force_vector)
-    if (A.want_k)
-      for (int it = tid; it < 729; it += kBlk)
-      {
-        const int g = it / 27;
-        const double* d = sh.dN + 3 * it;
-        const double* T = sh.T() + 9 * g;
-        double* o = sh.work() + 3 * it;
-#pragma unroll
-        for (int i = 0; i < 3; ++i) o[i] = T[3 * i] * d[0] + T[3 * i + 1] * d[1] + T[3 * i + 2] * d[2];
-      }
-    if (tid >= 175 && tid < 256)
-    {
-      const int t = tid - 175;
-      const int a = t / 3, i = t - 3 * (t / 3);
-      double f = 0.0;
-#pragma unroll 9
-      for (int g = 0; g < kNpe; ++g)
-      {
-        const double* R = sh.R() + 9 * g + 3 * i;
-        const double* d = sh.dN + 3 * (27 * g + a);
-        f += R[0] * d[0] + R[1] * d[1] + R[2] * d[2];
-      }
-      rec[kNpair * 9 + t] = f;
-    }
-    if (!A.want_k)
-    {
-      __syncthreads();
-      continue;
-    }
-    __syncthreads();
-    H27_STAMP(3);
-
-    // 5. G on the matrix cores: waves 0..2 take the node ranges (0,0), (0,1), (1,1) of 16
+    // matrix-core tiles of this wave: waves 0..2 take the node ranges (0,0), (0,1), (1,1) of 16;
+    // lane (r16, kq) feeds A[r16][kq] and B[kq][r16] and holds D[kq + 4 r][r16], r = 0..3.
+    // Operands come from the constant dN_a(xi_g) and the per-point 3 x 3 factors at clamped
+    // indices, always loaded and masked by multiplication (a load under a lane condition turns
+    // into a branch with its own wait: one LDS round trip per operand).
     const int at = wave == 2 ? 1 : 0, bt = wave == 0 ? 0 : 1;
     const int r16 = lane & 15, kq = lane >> 4;
     const int a_l = 16 * at + r16, b_l = 16 * bt + r16;
     const bool va = a_l < 27, vb = b_l < 27;
     const int a_c = va ? a_l : 0, b_c = vb ? b_l : 0;
-    f64x4_t X[9];
+    const f64x4_t zero4 = {0.0, 0.0, 0.0, 0.0};
+    f64x4_t Hm[6];  // TotLag: H per component (xx yy zz xy yz zx), mu applied when K is formed
 #pragma unroll
-    for (int k = 0; k < 9; ++k) X[k] = f64x4_t{0.0, 0.0, 0.0, 0.0};
-    if (wave < 3)
+    for (int k = 0; k < 6; ++k) Hm[k] = zero4;
+
+    // 3. TotLag: mu H + geo I.  Waves 0..2: per Gauss point the tile c_ab = d_a^T W d_b by one
+    //    MFMA over k (K = 3, padded to 4; A = W d_a formed on the fly), then H += c_ab M_g on the
+    //    lanes.  Wave 3: geo_ab = sum over (g, k) of (V d_a)_k d_b,k, one K = 81 product per tile,
+    //    parked as an image [378] that is read when K_ab is formed.
+    if (KIN == 1 && A.want_k)
     {
-#pragma unroll
-      for (int st = 0; st < 7; ++st)
+      if (wave < 3)
       {
-        const int g = 4 * st + kq;
-        const bool vg = g < 27;
-        const int gc = vg ? g : 0;
-        const double fg = vg ? sh.fac[gc] : 0.0;
-        const double* qa = sh.work() + 3 * (27 * gc + a_c);
-        const double* qb = sh.work() + 3 * (27 * gc + b_c);
-        double av[3], bv[3];
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
+        const bool vk = kq < 3;
+        const int kc = vk ? kq : 0;
+        const double ma = (va && vk) ? 1.0 : 0.0, mb = (vb && vk) ? 1.0 : 0.0;
+        const int wr0 = kc == 0 ? 0 : (kc == 1 ? 3 : 5), wr1 = kc == 0 ? 3 : (kc == 1 ? 1 : 4),
+                  wr2 = kc == 0 ? 5 : (kc == 1 ? 4 : 2);  // row kc of the symmetric W
+#pragma unroll 3
+        for (int g = 0; g < kNpe; ++g)
         {
-          av[i] = va ? fg * qa[i] : 0.0;
-          bv[i] = (vg && vb) ? qb[i] : 0.0;
+          const double* da = sh.dN + 3 * (27 * g + a_c);
+          const double* Wg = sh.W() + 6 * g;
+          const double av = (Wg[wr0] * da[0] + Wg[wr1] * da[1] + Wg[wr2] * da[2]) * ma;
+          const double bv = sh.dN[3 * (27 * g + b_c) + kc] * mb;
+          const f64x4_t c = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, zero4, 0, 0, 0);
+          const double* Mg = sh.M() + 6 * g;
+#pragma unroll
+          for (int s = 0; s < 6; ++s)
+          {
+            const double m = Mg[s];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Hm[s][r] += c[r] * m;
+          }
+        }
+      }
+      else
+      {
+        f64x4_t Geo[3] = {zero4, zero4, zero4};
+        const int r1 = r16 < 11 ? 16 + r16 : 0;  // a, b in [16, 27)
+#pragma unroll 3
+        for (int st = 0; st < 21; ++st)
+        {
+          const int fk = 4 * st + kq;
+          const bool vf = fk < 81;
+          const int g = vf ? fk / 3 : 0, k = vf ? fk - 3 * (fk / 3) : 0;
+          const double m0 = vf ? 1.0 : 0.0, m1 = (vf && r16 < 11) ? 1.0 : 0.0;
+          const int vr0 = k == 0 ? 0 : (k == 1 ? 3 : 5), vr1 = k == 0 ? 3 : (k == 1 ? 1 : 4),
+                    vr2 = k == 0 ? 5 : (k == 1 ? 4 : 2);  // row k of the symmetric V
+          const double* Vg = sh.V() + 6 * g;
+          const double q0 = Vg[vr0], q1 = Vg[vr1], q2 = Vg[vr2];
+          const double* d0p = sh.dN + 3 * (27 * g + r16);
+          const double* d1p = sh.dN + 3 * (27 * g + r1);
+          const double v0 = (q0 * d0p[0] + q1 * d0p[1] + q2 * d0p[2]) * m0;
+          const double v1 = (q0 * d1p[0] + q1 * d1p[1] + q2 * d1p[2]) * m1;
+          const double d0 = d0p[k] * m0, d1 = d1p[k] * m1;
+          Geo[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(v0, d0, Geo[0], 0, 0, 0);
+          Geo[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(v0, d1, Geo[1], 0, 0, 0);
+          Geo[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(v1, d1, Geo[2], 0, 0, 0);
         }
 #pragma unroll
-        for (int i = 0; i < 3; ++i)
+        for (int t = 0; t < 3; ++t)
+        {
+          const int ta = t == 2 ? 1 : 0, tb = t == 0 ? 0 : 1;
+          const int b = 16 * tb + r16;
 #pragma unroll
-          for (int j = 0; j < 3; ++j)
-            X[3 * i + j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[j], X[3 * i + j], 0, 0, 0);
+          for (int r = 0; r < 4; ++r)
+          {
+            const int a = 16 * ta + kq + 4 * r;
+            if (a < 27 && b < 27 && a <= b) sh.geo()[pidx(a, b)] = Geo[t][r];
+          }
+        }
       }
     }
-    __syncthreads();  // q dead: the region becomes the mu H + geo I image (TotLag) / K image
-    if (KIN == 1)
-    {
-      if (tid < kNchunk)
+    H27_STAMP(2);
+
+    // 4. G_ij = sum_g fac q_a,i q_b,j on the matrix cores (waves 0..2, 7 steps of 4 Gauss points;
+    //    q_a = T_g d_a formed on the fly) and, on wave 3 meanwhile, f_a = sum_g R_g d_a
+    //    (add_internal_force_vector, calc_lib.hpp:851-860)
+    f64x4_t X[9];
 #pragma unroll
-        for (int p = 0; p < 2; ++p)
-          if (p < cnb)
+    for (int k = 0; k < 9; ++k) X[k] = zero4;
+    if (wave < 3)
+    {
+      if (A.want_k)
+      {
+#pragma unroll
+        for (int st = 0; st < 7; ++st)
+        {
+          const int g = 4 * st + kq;
+          const bool vg = g < 27;
+          const int gc = vg ? g : 0;
+          const double fg = sh.fac[gc] * ((vg && va) ? 1.0 : 0.0);
+          const double mb = (vg && vb) ? 1.0 : 0.0;
+          const double* T = sh.T() + 9 * gc;
+          const double* da = sh.dN + 3 * (27 * gc + a_c);
+          const double* db = sh.dN + 3 * (27 * gc + b_c);
+          const double a0 = da[0], a1 = da[1], a2 = da[2], b0 = db[0], b1 = db[1], b2 = db[2];
+          double av[3], bv[3];
+#pragma unroll
+          for (int i = 0; i < 3; ++i)
           {
-            double* o = sh.himg() + 7 * pidx(ca, cb0 + p);
-            const double geo = Hacc[p][6];
-            o[0] = mu * Hacc[p][0] + geo;
-            o[1] = mu * Hacc[p][1] + geo;
-            o[2] = mu * Hacc[p][2] + geo;
-            o[3] = mu * Hacc[p][3];
-            o[4] = mu * Hacc[p][4];
-            o[5] = mu * Hacc[p][5];
+            const double t0 = T[3 * i], t1 = T[3 * i + 1], t2 = T[3 * i + 2];
+            av[i] = fg * (t0 * a0 + t1 * a1 + t2 * a2);
+            bv[i] = mb * (t0 * b0 + t1 * b1 + t2 * b2);
           }
-      __syncthreads();
+#pragma unroll
+          for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+              X[3 * i + j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[j], X[3 * i + j], 0, 0, 0);
+        }
+      }
     }
-    H27_STAMP(4);
-    // K_ab = lambda G + mu G^T + (mu tr G I | mu H + geo I) into the LDS image of the record,
-    // which then leaves as contiguous 16-byte pieces: one store instruction covers 1 KB of the
-    // record instead of 64 scattered 8-byte entries
+    else if (lane < kNpe)
+    {
+      const int a = lane;
+      double f0 = 0.0, f1 = 0.0, f2 = 0.0;
+#pragma unroll 3
+      for (int g = 0; g < kNpe; ++g)
+      {
+        const double* R = sh.R() + 9 * g;
+        const double* d = sh.dN + 3 * (27 * g + a);
+        const double d0 = d[0], d1 = d[1], d2 = d[2];
+        f0 += R[0] * d0 + R[1] * d1 + R[2] * d2;
+        f1 += R[3] * d0 + R[4] * d1 + R[5] * d2;
+        f2 += R[6] * d0 + R[7] * d1 + R[8] * d2;
+      }
+      if (!A.increc)
+      {
+        rec[kNpair * 9 + 3 * a + 0] = f0;
+        rec[kNpair * 9 + 3 * a + 1] = f1;
+        rec[kNpair * 9 + 3 * a + 2] = f2;
+      }
+      else if (sh.inc[buf][a] >= 0)
+      {
+        double* o = A.rec + int64_t(sh.inc[buf][a]) * kIncRec + 243;
+        o[0] = f0;
+        o[1] = f1;
+        o[2] = f2;
+      }
+    }
+    __syncthreads();  // the Gauss-point factors are dead: the region becomes the K image
+    H27_STAMP(3);
+    if (!A.want_k) continue;
+
+    // 5. K_ab = lambda G + mu G^T + (mu tr G I | mu H + geo I) into the LDS image, which leaves
+    //    as contiguous pieces: one store instruction covers 1 KB instead of 64 scattered entries
     if (wave < 3)
     {
       const int b = 16 * bt + r16;
@@ -540,13 +559,13 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
           }
           else
           {
-            const double* h = sh.himg() + 7 * pidx(a, b);
-            add[0] = h[0];
-            add[4] = h[1];
-            add[8] = h[2];
-            add[1] = add[3] = h[3];
-            add[5] = add[7] = h[4];
-            add[2] = add[6] = h[5];
+            const double geo = sh.geo()[pidx(a, b)];
+            add[0] = mu * Hm[0][r] + geo;
+            add[4] = mu * Hm[1][r] + geo;
+            add[8] = mu * Hm[2][r] + geo;
+            add[1] = add[3] = mu * Hm[3][r];
+            add[5] = add[7] = mu * Hm[4][r];
+            add[2] = add[6] = mu * Hm[5][r];
           }
           double* K = sh.kimg() + 9 * pidx(a, b);
 #pragma unroll
@@ -558,6 +577,31 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
       }
     }
     __syncthreads();
+    H27_STAMP(4);
+    // 6. the record(s)
+    if (A.increc)
+    {
+      // the owned incidences' block rows K_ab, b = 0..26 (K_ba^T for b < a), row-major 3 x 81:
+      // the record of the general path's assemble27_kernel.  One (a, b) block per lane: its 9
+      // entries from the image, then 3 pieces of 3 into the rows (lanes b, b + 1 contiguous)
+      for (int p = tid; p < kNpe * kNpe; p += kBlk)
+      {
+        const int a = p / kNpe, b = p - kNpe * a;
+        const int32_t k = sh.inc[buf][a];
+        if (k < 0) continue;
+        const bool up = a <= b;
+        const double* src = sh.kimg() + 9 * (up ? pidx(a, b) : pidx(b, a));
+        double v[9];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) v[q] = src[q];  // col-major K_(min,max)
+        double* dst = A.rec + int64_t(k) * kIncRec + 3 * b;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) dst[81 * i + j] = up ? v[i + 3 * j] : v[j + 3 * i];
+      }
+    }
+    else
     {
       const double2* src = reinterpret_cast<const double2*>(sh.kimg());
       double2* dst = reinterpret_cast<double2*>(rec);  // records are 16-byte aligned (kRec even)
@@ -737,11 +781,6 @@ void upload_h27_tables()
   }
   (void)hipMemcpyToSymbol(HIP_SYMBOL(c_loc), loc, sizeof(loc));
   (void)hipMemcpyToSymbol(HIP_SYMBOL(c_latnode), latnode, sizeof(latnode));
-  uint32_t chunk[kNchunk];
-  int n = 0;
-  for (int a = 0; a < 27; ++a)
-    for (int b = a; b < 27; b += 2) chunk[n++] = uint32_t(a | (b << 8) | ((b + 1 < 27 ? 2 : 1) << 16));
-  (void)hipMemcpyToSymbol(HIP_SYMBOL(c_chunk), chunk, sizeof(chunk));
   done = true;
 }
 
@@ -756,6 +795,8 @@ hipError_t launch_h27_element(const DeviceMesh& m, const double* d_u_col, bool w
   a.node_dof_col = m.node_dof_col;
   a.u_col = d_u_col;
   a.rec = m.scratch;
+  a.inc_of = m.inc_of;
+  a.increc = m.h27_increc ? 1 : 0;
   a.err = m.err;
   a.lambda = m.lambda;
   a.mu = m.mu;

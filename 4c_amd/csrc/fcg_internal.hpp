@@ -59,6 +59,7 @@ struct DeviceMesh {
   uint32_t* rec_tmap = nullptr;     // [n_rec][32] per column triple: slot s's element node in nibble s (8 = none)
   // hex27 StVK general path (fcg_hex27.hip): per-element symmetric records in `scratch`
   bool h27s = false;
+  bool h27_increc = false;  // hex27 element kernel writes incidence block rows (assemble27_kernel)
   int32_t* inc_ele = nullptr;       // [n_inc] element of each incidence
   uint8_t* inc_a = nullptr;         // [n_inc] local node of the row node in that element
   int32_t* asm_order = nullptr;     // [n_rownodes] row nodes in Morton order of their coordinates

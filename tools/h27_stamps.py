@@ -10,7 +10,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 fcg = importlib.import_module("4c_amd").fcg
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 40
 dev = torch.device("cuda:0")
-names = ["gather+J", "gp-algebra", "valu-pairs", "q+f", "mfma+H", "store"]
+names = ["gather+J", "gp-algebra", "H+geo(wave0)", "G+f+barrier", "K-image", "store"]
 for kin in (fcg.LINEAR, fcg.TOTLAG):
     m = fcg.BoxMesh(fcg.HEX27, (n, n, n), jitter=0.02)
     u = torch.from_numpy(m.u_col(1e-3 if kin == fcg.LINEAR else 5e-2)).to(dev)
