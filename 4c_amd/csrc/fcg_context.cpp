@@ -344,6 +344,15 @@ struct ColorHost {
   std::vector<int32_t> col_ele;
   std::vector<uint8_t> ft;
   int64_t color_ptr[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  // pencil order (hex27 StVK, fcg_hex27.hip): colour (ey & 1) + 2 (ez & 1); inside a colour the
+  // maximal runs of lattice-consecutive elements along x ("pencils"), each walked in x order by
+  // one workgroup.  pen_ele: elements by colour, pencil, ex; pen_ptr: pencil ranges in pen_ele;
+  // pen_color: pencil range of colour c.  nb[e]: bit (dx+1) + 3 (dy+1) + 9 (dz+1) = lattice
+  // neighbour e + (dx, dy, dz) exists; bits 27, 28 = ey & 1, ez & 1.
+  std::vector<int32_t> pen_ele;
+  std::vector<int64_t> pen_ptr;
+  int64_t pen_color[5] = {0, 0, 0, 0, 0};
+  std::vector<uint32_t> nb;
 };
 
 bool build_colored_plan(const fcg_desc* d, ColorHost& P, std::string& why)
@@ -452,6 +461,47 @@ bool build_colored_plan(const fcg_desc* d, ColorHost& P, std::string& why)
   P.col_ele.resize(d->n_ele);
   std::vector<int64_t> fill(P.color_ptr, P.color_ptr + 8);
   for (int64_t e = 0; e < d->n_ele; ++e) P.col_ele[fill[color[e]]++] = int32_t(e);
+
+  // pencil order: walk the lattice box colour by colour, (ez, ey) rows, x runs
+  P.nb.assign(d->n_ele, 0u);
+  P.pen_ele.clear();
+  P.pen_ele.reserve(d->n_ele);
+  P.pen_ptr.assign(1, 0);
+  auto at = [&](int64_t x, int64_t y, int64_t z) -> int32_t {
+    if (x < 0 || y < 0 || z < 0 || x >= EX || y >= EY || z >= EZ) return -1;
+    return elem_at[(z * EY + y) * EX + x];
+  };
+  for (int c = 0; c < 4; ++c)
+  {
+    P.pen_color[c] = int64_t(P.pen_ptr.size()) - 1;
+    // parity of the absolute lattice index (the same colours on every rank of a box split)
+    for (int64_t z = 0; z < EZ; ++z)
+    {
+      if (((z + mn[2]) & 1) != (c >> 1)) continue;
+      for (int64_t y = 0; y < EY; ++y)
+      {
+        if (((y + mn[1]) & 1) != (c & 1)) continue;
+        for (int64_t x = 0; x < EX; ++x)
+        {
+          const int32_t e = at(x, y, z);
+          if (e < 0) continue;
+          if (at(x - 1, y, z) < 0 && !P.pen_ele.empty() && int64_t(P.pen_ele.size()) != P.pen_ptr.back())
+            P.pen_ptr.push_back(int64_t(P.pen_ele.size()));  // a new run starts
+          P.pen_ele.push_back(e);
+          uint32_t bits = 0;
+          for (int dz = -1; dz <= 1; ++dz)
+            for (int dy = -1; dy <= 1; ++dy)
+              for (int dx = -1; dx <= 1; ++dx)
+                if (at(x + dx, y + dy, z + dz) >= 0) bits |= 1u << ((dx + 1) + 3 * (dy + 1) + 9 * (dz + 1));
+          bits |= uint32_t((y + mn[1]) & 1) << 27;
+          bits |= uint32_t((z + mn[2]) & 1) << 28;
+          P.nb[e] = bits;
+        }
+      }
+    }
+    if (int64_t(P.pen_ele.size()) != P.pen_ptr.back()) P.pen_ptr.push_back(int64_t(P.pen_ele.size()));
+  }
+  P.pen_color[4] = int64_t(P.pen_ptr.size()) - 1;
   return true;
 }
 
@@ -461,7 +511,8 @@ void free_mesh(fcg::DeviceMesh& m)
       m.ele_dof, m.ele_nodes, m.ele_gid, m.node_x, m.node_dof_col, m.inc_of, m.inc_ptr,
       m.rownode_row0, m.inc_pos, m.rowptr, m.scratch, m.err, m.elem_at, m.lat_x, m.lat_dof,
       m.plane_rec,
-      m.tables, m.stamps, m.col_lid, m.diag_pos, m.pcg_work, m.col_ele, m.ele_ft, m.inc_row0};
+      m.tables, m.stamps, m.col_lid, m.diag_pos, m.pcg_work, m.col_ele, m.ele_ft, m.inc_row0,
+      m.pen_ptr, m.ele_nb};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (m.err_host) (void)hipHostFree(m.err_host);
@@ -919,9 +970,24 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
     chk(upload(&m.inc_of, inc_of.data(), d->n_ele * npe, bytes));
     chk(upload(&m.inc_pos, inc_pos.data(), n_inc * npe, bytes));
     chk(upload(&m.inc_row0, inc_row0.data(), n_inc, bytes));
-    chk(upload(&m.col_ele, cp.col_ele.data(), d->n_ele, bytes));
-    chk(upload(&m.ele_ft, cp.ft.data(), d->n_ele, bytes));
-    for (int c = 0; c < 9; ++c) m.color_ptr[c] = cp.color_ptr[c];
+    // hex27 StVK: the matrix-core element kernel in pencil order (4 launches, fcg_hex27.hip);
+    // FCG_H27_LEGACY=1 or another material: the eight-colour element_kernel launches
+    const char* legacy = std::getenv("FCG_H27_LEGACY");
+    m.h27_pencil = d->material == FCG_MAT_STVK && !(legacy && legacy[0] == '1');
+    if (m.h27_pencil)
+    {
+      fcg::upload_h27_tables();
+      chk(upload(&m.col_ele, cp.pen_ele.data(), d->n_ele, bytes));
+      chk(upload(&m.pen_ptr, cp.pen_ptr.data(), int64_t(cp.pen_ptr.size()), bytes));
+      chk(upload(&m.ele_nb, cp.nb.data(), d->n_ele, bytes));
+      for (int c = 0; c < 5; ++c) m.pen_color[c] = cp.pen_color[c];
+    }
+    else
+    {
+      chk(upload(&m.col_ele, cp.col_ele.data(), d->n_ele, bytes));
+      chk(upload(&m.ele_ft, cp.ft.data(), d->n_ele, bytes));
+      for (int c = 0; c < 9; ++c) m.color_ptr[c] = cp.color_ptr[c];
+    }
   }
   else if (gather)
   {
@@ -1281,8 +1347,10 @@ int fcg_evaluate_device(fcg_ctx* ctx, int action, int mode, const double* d_u_co
   else if (m.path == FCG_PATH_COLORED)
   {
     if (he == hipSuccess)
-      he = fcg::launch_element_colored(m, d_u_col, want_k, mode == FCG_OVERWRITE, d_K_vals,
-          d_fint_row, s);
+      he = m.h27_pencil ? fcg::launch_h27_pencil(m, d_u_col, want_k, mode == FCG_OVERWRITE, d_K_vals,
+                              d_fint_row, s)
+                        : fcg::launch_element_colored(m, d_u_col, want_k, mode == FCG_OVERWRITE,
+                              d_K_vals, d_fint_row, s);
     if (T.enabled && he == hipSuccess) he = hipEventRecord(T.ev[1], s);
   }
   else if (m.path == FCG_PATH_GATHER)

@@ -18,9 +18,10 @@
 //           calc_lib.hpp:872-927), all on v_mfma_f64_16x16x4_f64 tiles of 16 x 16 node pairs:
 //             K_ab = lambda G + mu G^T + mu H + geo I          (linear: mu tr(G) I, no H / geo)
 //             G_ij = sum_g fac q_a,i q_b,j                     (waves 0-2, K = 27 Gauss points)
-//             H = sum_g c_ab(g) F F^T, c_ab = d_a^T W d_b     (waves 0-2: one MFMA per point
-//                                                                for c, then 24 lane FMAs)
-//             geo = sum_(g,k) (V d_a)_k d_b,k                  (wave 3, K = 81)
+//             H = sum_g c_ab(g) F F^T, c_ab = d_a^T W d_b     (one MFMA per point for c,
+//                                                                then 24 lane FMAs)
+//             geo = sum_g d_a^T V d_b                          (one accumulating MFMA per point,
+//                                                                same B operand as c)
 //           and f_a (wave 3, while waves 0-2 run G); every operand is formed on the fly from
 //           the constant dN_a(xi_g) and the per-point factors (no per-(g, a) work arrays);
 //        4. K_ab into an LDS image of the element's 378 blocks a <= b.
@@ -90,33 +91,41 @@ __device__ inline double inv3(double* m)
   return det;
 }
 
-// LDS of one element's workgroup.  `big` holds stage-dependent views (offsets below):
-//   J | Gu | T | W | V | M | R (Gauss-point data, dead after the matrix-core phases), overlaid by
-//   the element's K image [378][9] once they are done; the geo image [378] (TotLag) after it.
-constexpr int OFF_J = 0, OFF_GU = 243, OFF_T = 486, OFF_W = 729, OFF_V = 891, OFF_M = 1053,
-              OFF_R = 1215, OFF_KIMG = 0, OFF_GEO = kNpair * 9;
-constexpr int BIG = OFF_GEO + kNpair;
-static_assert(OFF_R + 243 <= OFF_GEO, "Gauss-point factors inside the K image region");
+// LDS of one element's workgroup.  `big` holds stage-dependent views (offsets below): J | Gu
+// (stages 1-2) overlaid by the element's K image [378][9] (TotLag: mu H + geo I from the end of
+// stage 3 on); the per-point factors T | W | V | M | R live beside it in `gpf` (read until the
+// end of stage 4, while the K image is being written).
+constexpr int OFF_J = 0, OFF_GU = 243, OFF_KIMG = 0;
+constexpr int OFF_T = 0, OFF_W = 243, OFF_V = 405, OFF_M = 567, OFF_R = 729, GPF = 972;
+constexpr int BIG = kNpair * 9;
+static_assert(OFF_GU + 243 <= BIG, "Jacobians inside the K image region");
 struct H27Shared {
   double dN[27 * 27 * 3];  // [g][c][d], loaded once per workgroup
   double X[2][81], U[2][81];  // double-buffered: the next element's arrive during this one
-  int32_t inc[2][27];         // increc: incidence of (e, a), double-buffered like X, U
+  int32_t inc[2][27];         // increc / pencil: incidence of (e, a), double-buffered like X, U
   double fac[27];
   alignas(16) double big[BIG];
+  double gpf[GPF];
   double L1[9], dL1[9], dLn[9];
+  // pencil output: CSR offset of row (a, 0), row length, column position of node b in a's rows,
+  // the first-holder bit per pair class, and the pair class of (a, b)
+  int64_t rbase[27];
+  int32_t rlen[27], frow[27];  // frow: row LID of (a, 0) | first holder of (a, a) << 31
+  uint16_t ipos[27 * 27];
+  uint32_t fmask;
+  uint8_t pcls[27 * 27];
   int bad;
   uint8_t loc[27], latnode[27];
   // views: J per g col-major (r + 3c), then J^-1 | du_i/dxi_k at k + 3i | T(i, k) at 3i + k |
   // W, V, M symmetric (xx yy zz xy yz zx) | R(i, k) at 3i + k
   __device__ double* J() { return big + OFF_J; }
   __device__ double* Gu() { return big + OFF_GU; }
-  __device__ double* T() { return big + OFF_T; }
-  __device__ double* W() { return big + OFF_W; }
-  __device__ double* V() { return big + OFF_V; }
-  __device__ double* M() { return big + OFF_M; }
-  __device__ double* R() { return big + OFF_R; }
+  __device__ double* T() { return gpf + OFF_T; }
+  __device__ double* W() { return gpf + OFF_W; }
+  __device__ double* V() { return gpf + OFF_V; }
+  __device__ double* M() { return gpf + OFF_M; }
+  __device__ double* R() { return gpf + OFF_R; }
   __device__ double* kimg() { return big + OFF_KIMG; }
-  __device__ double* geo() { return big + OFF_GEO; }
 };
 
 struct H27Args {
@@ -132,20 +141,76 @@ struct H27Args {
   double lambda, mu, cdiag;
   int want_k;
   unsigned long long* stamps;  // FCG_STAMPS=1: per-phase s_memtime sums of thread 0, else NULL
+  // pencil output (ASM != 0): pencils [pen_begin, pen_end) of one colour, elements col_ele in x
+  // order per pencil; the blocks go straight into the owned CSR rows
+  const int32_t* col_ele;
+  const int64_t* pen_ptr;
+  int64_t pen_begin, pen_end;
+  const uint32_t* ele_nb;
+  const uint16_t* inc_pos;
+  const int32_t* inc_row0;
+  const int64_t* rowptr;
+  double* K;
+  double* fint;
 };
 
 typedef double f64x4_t __attribute__((ext_vector_type(4)));
 
-template <int KIN>
+// Pair class of element nodes (a, b): per axis 0 = both on the lower face, 2 = both on the upper
+// face, 1 = otherwise; class = t_x + 3 t_y + 9 t_z.  The elements holding both nodes are e
+// shifted by the offsets {-1, 0}, {0}, {0, +1} of the three axes.
+__device__ inline int pair_class(uint32_t la, uint32_t lb)
+{
+  int c = 0, m = 1;
+#pragma unroll
+  for (int d = 0; d < 3; ++d, m *= 3)
+  {
+    const uint32_t x = (la >> (2 * d)) & 3u, y = (lb >> (2 * d)) & 3u;
+    c += m * ((x == y && x != 1u) ? int(x) : 1);
+  }
+  return c;
+}
+
+// Pencil order: colour (ey & 1) + 2 (ez & 1), then x along the pencil.  The first of the present
+// holders of a pair class in that order writes (OVERWRITE), the others add.  nb: ele_nb[e].
+__device__ inline bool first_holder(int cls, uint32_t nb)
+{
+  const int t[3] = {cls % 3, (cls / 3) % 3, cls / 9};
+  const int py = int((nb >> 27) & 1u), pz = int((nb >> 28) & 1u);
+  const int ekey = 4 * (py + 2 * pz) + 1;
+  bool first = true;
+  for (int dz = (t[2] == 0 ? -1 : 0); dz <= (t[2] == 2 ? 1 : 0); ++dz)
+    for (int dy = (t[1] == 0 ? -1 : 0); dy <= (t[1] == 2 ? 1 : 0); ++dy)
+      for (int dx = (t[0] == 0 ? -1 : 0); dx <= (t[0] == 2 ? 1 : 0); ++dx)
+      {
+        if (!((nb >> ((dx + 1) + 3 * (dy + 1) + 9 * (dz + 1))) & 1u)) continue;
+        const int key = 4 * (((py + dy) & 1) + 2 * ((pz + dz) & 1)) + dx + 1;
+        if (key < ekey) first = false;
+      }
+  return first;
+}
+
 #ifndef FCG_H27_LIN_WGS
 #define FCG_H27_LIN_WGS 2
 #endif
+#ifndef FCG_H27P_NV
+#define FCG_H27P_NV 9  // pencil output: entries in flight per lane
+#endif
+// ASM: 0 = records for the row assembly; 1 = pencil order, add into K; 2 = pencil order, the first
+// holder writes (OVERWRITE)
+template <int KIN, int ASM>
 __global__ __launch_bounds__(kBlk, KIN ? 2 : FCG_H27_LIN_WGS) void h27_element_kernel(H27Args A)
 {
   __shared__ H27Shared sh;
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
   for (int v = tid; v < 27 * 27 * 3; v += kBlk) sh.dN[v] = c_dN[v];
+  if (ASM)
+    for (int v = tid; v < 27 * 27; v += kBlk)
+    {
+      const int a = v / 27;
+      sh.pcls[v] = uint8_t(pair_class(c_loc[a], c_loc[v - 27 * a]));
+    }
   if (tid < 9)
   {
     sh.L1[tid] = c_L1[tid];
@@ -166,17 +231,37 @@ __global__ __launch_bounds__(kBlk, KIN ? 2 : FCG_H27_LIN_WGS) void h27_element_k
   double xpre = 0.0, upre = 0.0;
   int32_t ipre = -1;
   auto prefetch = [&](int64_t e) {
-    if (tid < 81 && e < A.n_ele)
+    if (tid < 81 && e >= 0)
     {
       const int a = tid / 3, d = tid - 3 * (tid / 3);
       const int node = A.ele_nodes[e * kNpe + a];
       xpre = A.node_x[3 * int64_t(node) + d];
       upre = A.u_col[A.node_dof_col[node] + d];
     }
-    else if (A.increc && tid >= 96 && tid < 96 + kNpe && e < A.n_ele)
+    else if ((ASM || A.increc) && tid >= 96 && tid < 96 + kNpe && e >= 0)
       ipre = A.inc_of[e * kNpe + tid - 96];
   };
-  prefetch(blockIdx.x);
+  // the elements of this workgroup: e = blockIdx.x + k gridDim.x, or (pencil order) the pencils
+  // pen_begin + blockIdx.x + k gridDim.x, each walked in x order
+  int64_t pen = A.pen_begin + blockIdx.x, pos = -1, pend = -1;
+  auto first_element = [&]() -> int64_t {
+    if (!ASM) return blockIdx.x < A.n_ele ? int64_t(blockIdx.x) : -1;
+    if (pen >= A.pen_end) return -1;
+    pos = A.pen_ptr[pen];
+    pend = A.pen_ptr[pen + 1];
+    return A.col_ele[pos];
+  };
+  auto next_element = [&](int64_t e) -> int64_t {
+    if (!ASM) return e + gridDim.x < A.n_ele ? e + gridDim.x : -1;
+    if (++pos < pend) return A.col_ele[pos];
+    pen += gridDim.x;
+    if (pen >= A.pen_end) return -1;
+    pos = A.pen_ptr[pen];
+    pend = A.pen_ptr[pen + 1];
+    return A.col_ele[pos];
+  };
+  const int64_t e_first = first_element();
+  prefetch(e_first);
   if (tid < 81)
   {
     sh.X[0][tid] = xpre;
@@ -198,15 +283,64 @@ __global__ __launch_bounds__(kBlk, KIN ? 2 : FCG_H27_LIN_WGS) void h27_element_k
     st_acc[i] += now - st_last;                                                                    \
     st_last = now;                                                                                 \
   }
-  for (int64_t e = blockIdx.x; e < A.n_ele; e += gridDim.x, buf ^= 1)
+  int64_t e_next = -1;
+  for (int64_t e = e_first; e >= 0; e = e_next, buf ^= 1)
   {
     ++st_n;
-    double* rec = A.rec + (A.increc ? 0 : e * kRec);
+    double* rec = A.rec + (A.increc || ASM ? 0 : e * kRec);
     if (tid == 0) sh.bad = 0;
     __syncthreads();
-    prefetch(e + gridDim.x);
+    e_next = next_element(e);
+    prefetch(e_next);
     const double* Xe = sh.X[buf];
     const double* Ue = sh.U[buf];
+    // pencil output: this element's row bookkeeping, loaded by wave 3 (idle in stages 1-2) and
+    // parked in LDS at once: one global round trip, shorter than stage 1; wave 0 forms the
+    // first-holder mask of the pair classes
+    if (ASM && wave == 3)
+    {
+      uint32_t ipos_r[12];
+#pragma unroll
+      for (int q = 0; q < 12; ++q)
+      {
+        const int v = lane + 64 * q;
+        ipos_r[q] = 0u;
+        if (v < kNpe * kNpe)
+        {
+          const int a = v / kNpe;
+          const int32_t k = sh.inc[buf][a];
+          if (k >= 0) ipos_r[q] = A.inc_pos[int64_t(k) * kNpe + (v - kNpe * a)];
+        }
+      }
+      if (lane < kNpe)
+      {
+        const int32_t k = sh.inc[buf][lane];
+        int64_t rb = 0;
+        int32_t rl = 0, fr = -1;
+        if (k >= 0)
+        {
+          fr = A.inc_row0[k];
+          rb = A.rowptr[fr];
+          rl = int32_t(A.rowptr[fr + 1] - rb);
+          if (ASM == 2 && first_holder(pair_class(sh.loc[lane], sh.loc[lane]), A.ele_nb[e]))
+            fr = int32_t(uint32_t(fr) | 0x80000000u);
+        }
+        sh.rbase[lane] = rb;
+        sh.rlen[lane] = rl;
+        sh.frow[lane] = fr;
+      }
+#pragma unroll
+      for (int q = 0; q < 12; ++q)
+      {
+        const int v = lane + 64 * q;
+        if (v < kNpe * kNpe) sh.ipos[v] = uint16_t(ipos_r[q]);
+      }
+    }
+    if (ASM == 2 && wave == 0)
+    {
+      const uint64_t m = __ballot(tid < 27 && first_holder(tid, A.ele_nb[e]));
+      if (tid == 0) sh.fmask = uint32_t(m);
+    }
 
     // 1. J and du/dxi at the Gauss points; nodal det J check (calc_lib.hpp:475-496) via the 1D
     //    factors: at a node they are Kronecker deltas, so J sums the 3 nodes on each line
@@ -394,76 +528,58 @@ __global__ __launch_bounds__(kBlk, KIN ? 2 : FCG_H27_LIN_WGS) void h27_element_k
     const bool va = a_l < 27, vb = b_l < 27;
     const int a_c = va ? a_l : 0, b_c = vb ? b_l : 0;
     const f64x4_t zero4 = {0.0, 0.0, 0.0, 0.0};
-    f64x4_t Hm[6];  // TotLag: H per component (xx yy zz xy yz zx), mu applied when K is formed
-#pragma unroll
-    for (int k = 0; k < 6; ++k) Hm[k] = zero4;
 
-    // 3. TotLag: mu H + geo I.  Waves 0..2: per Gauss point the tile c_ab = d_a^T W d_b by one
-    //    MFMA over k (K = 3, padded to 4; A = W d_a formed on the fly), then H += c_ab M_g on the
-    //    lanes.  Wave 3: geo_ab = sum over (g, k) of (V d_a)_k d_b,k, one K = 81 product per tile,
-    //    parked as an image [378] that is read when K_ab is formed.
-    if (KIN == 1 && A.want_k)
+    // 3. TotLag: mu H + geo I, waves 0..2 on their tiles.  Per Gauss point one MFMA over k (K = 3,
+    //    padded to 4) gives c_ab = d_a^T W d_b, and H += c_ab M_g on the lanes; a second MFMA with
+    //    the same B operand accumulates geo_ab += d_a^T V d_b in its C input.  Both go into the
+    //    K image at once (J, Gu under it are dead), so that stage 4 holds only G.
+    if (KIN == 1 && A.want_k && wave < 3)
     {
-      if (wave < 3)
-      {
-        const bool vk = kq < 3;
-        const int kc = vk ? kq : 0;
-        const double ma = (va && vk) ? 1.0 : 0.0, mb = (vb && vk) ? 1.0 : 0.0;
-        const int wr0 = kc == 0 ? 0 : (kc == 1 ? 3 : 5), wr1 = kc == 0 ? 3 : (kc == 1 ? 1 : 4),
-                  wr2 = kc == 0 ? 5 : (kc == 1 ? 4 : 2);  // row kc of the symmetric W
+      f64x4_t Hm[6];  // H per component (xx yy zz xy yz zx)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) Hm[k] = zero4;
+      f64x4_t Geo = zero4;
+      const bool vk = kq < 3;
+      const int kc = vk ? kq : 0;
+      const double ma = (va && vk) ? 1.0 : 0.0, mb = (vb && vk) ? 1.0 : 0.0;
+      const int wr0 = kc == 0 ? 0 : (kc == 1 ? 3 : 5), wr1 = kc == 0 ? 3 : (kc == 1 ? 1 : 4),
+                wr2 = kc == 0 ? 5 : (kc == 1 ? 4 : 2);  // row kc of the symmetric W, V
 #pragma unroll 3
-        for (int g = 0; g < kNpe; ++g)
+      for (int g = 0; g < kNpe; ++g)
+      {
+        const double* da = sh.dN + 3 * (27 * g + a_c);
+        const double* Wg = sh.W() + 6 * g;
+        const double* Vg = sh.V() + 6 * g;
+        const double d0 = da[0], d1 = da[1], d2 = da[2];
+        const double av = (Wg[wr0] * d0 + Wg[wr1] * d1 + Wg[wr2] * d2) * ma;
+        const double avv = (Vg[wr0] * d0 + Vg[wr1] * d1 + Vg[wr2] * d2) * ma;
+        const double bv = sh.dN[3 * (27 * g + b_c) + kc] * mb;
+        const f64x4_t c = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, zero4, 0, 0, 0);
+        Geo = __builtin_amdgcn_mfma_f64_16x16x4f64(avv, bv, Geo, 0, 0, 0);
+        const double* Mg = sh.M() + 6 * g;
+#pragma unroll
+        for (int s = 0; s < 6; ++s)
         {
-          const double* da = sh.dN + 3 * (27 * g + a_c);
-          const double* Wg = sh.W() + 6 * g;
-          const double av = (Wg[wr0] * da[0] + Wg[wr1] * da[1] + Wg[wr2] * da[2]) * ma;
-          const double bv = sh.dN[3 * (27 * g + b_c) + kc] * mb;
-          const f64x4_t c = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, zero4, 0, 0, 0);
-          const double* Mg = sh.M() + 6 * g;
+          const double m = Mg[s];
 #pragma unroll
-          for (int s = 0; s < 6; ++s)
-          {
-            const double m = Mg[s];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) Hm[s][r] += c[r] * m;
-          }
+          for (int r = 0; r < 4; ++r) Hm[s][r] += c[r] * m;
         }
       }
-      else
+      const int b = 16 * bt + r16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
       {
-        f64x4_t Geo[3] = {zero4, zero4, zero4};
-        const int r1 = r16 < 11 ? 16 + r16 : 0;  // a, b in [16, 27)
-#pragma unroll 3
-        for (int st = 0; st < 21; ++st)
+        const int a = 16 * at + kq + 4 * r;
+        if (a < 27 && b < 27 && a <= b)
         {
-          const int fk = 4 * st + kq;
-          const bool vf = fk < 81;
-          const int g = vf ? fk / 3 : 0, k = vf ? fk - 3 * (fk / 3) : 0;
-          const double m0 = vf ? 1.0 : 0.0, m1 = (vf && r16 < 11) ? 1.0 : 0.0;
-          const int vr0 = k == 0 ? 0 : (k == 1 ? 3 : 5), vr1 = k == 0 ? 3 : (k == 1 ? 1 : 4),
-                    vr2 = k == 0 ? 5 : (k == 1 ? 4 : 2);  // row k of the symmetric V
-          const double* Vg = sh.V() + 6 * g;
-          const double q0 = Vg[vr0], q1 = Vg[vr1], q2 = Vg[vr2];
-          const double* d0p = sh.dN + 3 * (27 * g + r16);
-          const double* d1p = sh.dN + 3 * (27 * g + r1);
-          const double v0 = (q0 * d0p[0] + q1 * d0p[1] + q2 * d0p[2]) * m0;
-          const double v1 = (q0 * d1p[0] + q1 * d1p[1] + q2 * d1p[2]) * m1;
-          const double d0 = d0p[k] * m0, d1 = d1p[k] * m1;
-          Geo[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(v0, d0, Geo[0], 0, 0, 0);
-          Geo[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(v0, d1, Geo[1], 0, 0, 0);
-          Geo[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(v1, d1, Geo[2], 0, 0, 0);
-        }
-#pragma unroll
-        for (int t = 0; t < 3; ++t)
-        {
-          const int ta = t == 2 ? 1 : 0, tb = t == 0 ? 0 : 1;
-          const int b = 16 * tb + r16;
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-          {
-            const int a = 16 * ta + kq + 4 * r;
-            if (a < 27 && b < 27 && a <= b) sh.geo()[pidx(a, b)] = Geo[t][r];
-          }
+          double* K = sh.kimg() + 9 * pidx(a, b);
+          const double geo = Geo[r];
+          K[0] = mu * Hm[0][r] + geo;
+          K[4] = mu * Hm[1][r] + geo;
+          K[8] = mu * Hm[2][r] + geo;
+          K[1] = K[3] = mu * Hm[3][r];
+          K[5] = K[7] = mu * Hm[4][r];
+          K[2] = K[6] = mu * Hm[5][r];
         }
       }
     }
@@ -521,7 +637,27 @@ __global__ __launch_bounds__(kBlk, KIN ? 2 : FCG_H27_LIN_WGS) void h27_element_k
         f1 += R[3] * d0 + R[4] * d1 + R[5] * d2;
         f2 += R[6] * d0 + R[7] * d1 + R[8] * d2;
       }
-      if (!A.increc)
+      if (ASM)
+      {
+        const int32_t fr = sh.frow[a];
+        if (fr != -1)
+        {
+          double* o = A.fint + (fr & 0x7FFFFFFF);
+          if (ASM == 2 && fr < 0)
+          {
+            o[0] = f0;
+            o[1] = f1;
+            o[2] = f2;
+          }
+          else
+          {
+            o[0] += f0;
+            o[1] += f1;
+            o[2] += f2;
+          }
+        }
+      }
+      else if (!A.increc)
       {
         rec[kNpair * 9 + 3 * a + 0] = f0;
         rec[kNpair * 9 + 3 * a + 1] = f1;
@@ -535,8 +671,7 @@ __global__ __launch_bounds__(kBlk, KIN ? 2 : FCG_H27_LIN_WGS) void h27_element_k
         o[2] = f2;
       }
     }
-    __syncthreads();  // the Gauss-point factors are dead: the region becomes the K image
-    H27_STAMP(3);
+    H27_STAMP(3);  // no barrier: stage 5 reads and writes only this lane's own image entries
     if (!A.want_k) continue;
 
     // 5. K_ab = lambda G + mu G^T + (mu tr G I | mu H + geo I) into the LDS image, which leaves
@@ -557,17 +692,12 @@ __global__ __launch_bounds__(kBlk, KIN ? 2 : FCG_H27_LIN_WGS) void h27_element_k
 #pragma unroll
             for (int k = 0; k < 9; ++k) add[k] = (k == 0 || k == 4 || k == 8) ? tr : 0.0;
           }
-          else
-          {
-            const double geo = sh.geo()[pidx(a, b)];
-            add[0] = mu * Hm[0][r] + geo;
-            add[4] = mu * Hm[1][r] + geo;
-            add[8] = mu * Hm[2][r] + geo;
-            add[1] = add[3] = mu * Hm[3][r];
-            add[5] = add[7] = mu * Hm[4][r];
-            add[2] = add[6] = mu * Hm[5][r];
-          }
           double* K = sh.kimg() + 9 * pidx(a, b);
+          if (KIN == 1)
+          {
+#pragma unroll
+            for (int k = 0; k < 9; ++k) add[k] = K[k];  // mu H + geo I from stage 3
+          }
 #pragma unroll
           for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -579,7 +709,41 @@ __global__ __launch_bounds__(kBlk, KIN ? 2 : FCG_H27_LIN_WGS) void h27_element_k
     __syncthreads();
     H27_STAMP(4);
     // 6. the record(s)
-    if (A.increc)
+    if (ASM)
+    {
+      // straight into the owned rows: entry v = (a, i, c) of a's 3 rows over the 81 columns in
+      // lattice order (c / 3 = lattice node, so lanes v, v + 1 hit contiguous CSR columns in runs
+      // of 3 nodes); every load of a batch is issued before its stores.  The pencil's previous
+      // element wrote its shared rows before this element's barriers, from this workgroup.
+      constexpr int NV = FCG_H27P_NV;
+      const uint32_t fmask = sh.fmask;
+      for (int v0 = 0; v0 < kNpe * 243; v0 += NV * kBlk)
+      {
+        int64_t addr[NV];
+        double val[NV];
+#pragma unroll
+        for (int k = 0; k < NV; ++k)
+        {
+          const int v = v0 + tid + kBlk * k;
+          addr[k] = -1;
+          val[k] = 0.0;
+          if (v >= kNpe * 243) continue;
+          const int a = v / 243;
+          if (sh.inc[buf][a] < 0) continue;
+          const int r = v - 243 * a;
+          const int i = r / 81, c = r - 81 * (r / 81);
+          const int b = sh.latnode[c / 3], j = c - 3 * (c / 3);
+          addr[k] = sh.rbase[a] + int64_t(i * sh.rlen[a] + sh.ipos[kNpe * a + b] + j);
+          const bool up = a <= b;
+          val[k] = sh.kimg()[9 * (up ? pidx(a, b) : pidx(b, a)) + (up ? i + 3 * j : j + 3 * i)];
+          if (ASM == 1 || !((fmask >> sh.pcls[kNpe * a + b]) & 1u)) val[k] += A.K[addr[k]];
+        }
+#pragma unroll
+        for (int k = 0; k < NV; ++k)
+          if (addr[k] >= 0) A.K[addr[k]] = val[k];
+      }
+    }
+    else if (A.increc)
     {
       // the owned incidences' block rows K_ab, b = 0..26 (K_ba^T for b < a), row-major 3 x 81:
       // the record of the general path's assemble27_kernel.  One (a, b) block per lane: its 9
@@ -806,10 +970,67 @@ hipError_t launch_h27_element(const DeviceMesh& m, const double* d_u_col, bool w
   const int64_t cap = 256 * 8;
   const dim3 grid(unsigned(m.n_ele < cap ? m.n_ele : cap)), block(kBlk);
   if (m.kinem == 0)
-    hipLaunchKernelGGL((h27_element_kernel<0>), grid, block, 0, stream, a);
+    hipLaunchKernelGGL((h27_element_kernel<0, 0>), grid, block, 0, stream, a);
   else
-    hipLaunchKernelGGL((h27_element_kernel<1>), grid, block, 0, stream, a);
+    hipLaunchKernelGGL((h27_element_kernel<1, 0>), grid, block, 0, stream, a);
   return hipGetLastError();
+}
+
+hipError_t launch_h27_pencil(const DeviceMesh& m, const double* d_u_col, bool want_k,
+    bool overwrite, double* d_K, double* d_fint, hipStream_t stream)
+{
+  if (m.n_ele == 0) return hipSuccess;
+  H27Args a{};
+  a.n_ele = m.n_ele;
+  a.ele_nodes = m.ele_nodes;
+  a.node_x = m.node_x;
+  a.node_dof_col = m.node_dof_col;
+  a.u_col = d_u_col;
+  a.rec = nullptr;
+  a.inc_of = m.inc_of;
+  a.increc = 0;
+  a.err = m.err;
+  a.lambda = m.lambda;
+  a.mu = m.mu;
+  a.cdiag = m.cdiag;
+  a.want_k = want_k ? 1 : 0;
+  a.stamps = m.stamps;
+  a.col_ele = m.col_ele;
+  a.pen_ptr = m.pen_ptr;
+  a.ele_nb = m.ele_nb;
+  a.inc_pos = m.inc_pos;
+  a.inc_row0 = m.inc_row0;
+  a.rowptr = m.rowptr;
+  a.K = d_K;
+  a.fint = d_fint;
+  // one workgroup per pencil (two resident per CU); the pencils of a colour have equal lengths
+  // on a box, so the hardware's dispatch balances them
+  const int64_t cap = int64_t(1) << 30;
+  for (int c = 0; c < 4; ++c)
+  {
+    a.pen_begin = m.pen_color[c];
+    a.pen_end = m.pen_color[c + 1];
+    const int64_t n = a.pen_end - a.pen_begin;
+    if (n == 0) continue;
+    const dim3 grid(unsigned(n < cap ? n : cap)), block(kBlk);
+#define FCG_H27P(KIN)                                                                              \
+  if (overwrite)                                                                                   \
+    hipLaunchKernelGGL((h27_element_kernel<KIN, 2>), grid, block, 0, stream, a);                   \
+  else                                                                                             \
+    hipLaunchKernelGGL((h27_element_kernel<KIN, 1>), grid, block, 0, stream, a);
+    if (m.kinem == 0)
+    {
+      FCG_H27P(0)
+    }
+    else
+    {
+      FCG_H27P(1)
+    }
+#undef FCG_H27P
+    const hipError_t he = hipGetLastError();
+    if (he != hipSuccess) return he;
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_h27_assemble(const DeviceMesh& m, bool want_k, bool overwrite, double* d_K,

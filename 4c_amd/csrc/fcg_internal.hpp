@@ -46,6 +46,11 @@ struct DeviceMesh {
   int64_t color_ptr[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // col_ele range of colour c
   uint8_t* ele_ft = nullptr;        // [n_ele] first-touch bits (see fcg_kernels.hip)
   int32_t* inc_row0 = nullptr;      // [n_inc] row LID of the incidence's node
+  // hex27 StVK on a verified lattice: the matrix-core element kernel in pencil order (fcg_hex27.hip)
+  bool h27_pencil = false;
+  int64_t* pen_ptr = nullptr;       // [n_pencils+1] pencil ranges in col_ele (pencil order)
+  int64_t pen_color[5] = {0, 0, 0, 0, 0};  // pencil range of colour c
+  uint32_t* ele_nb = nullptr;       // [n_ele] lattice neighbours present | ey & 1 << 27 | ez & 1 << 28
 
   // node-row gather plan (hex8, FCG_PATH_GATHER): a row node's incidences in records of <= 8
   // records: one per node with <= 8 elements [0, n_rec_single), then those of the other nodes
@@ -152,6 +157,10 @@ hipError_t launch_h27_element(const DeviceMesh& m, const double* d_u_col, bool w
     hipStream_t stream);
 hipError_t launch_h27_assemble(const DeviceMesh& m, bool want_k, bool overwrite, double* d_K,
     double* d_fint, hipStream_t stream);
+// hex27 StVK on a verified lattice: the same element kernel adding its blocks straight into the
+// CSR rows, four colour launches of pencils (runs of elements along x, one workgroup each)
+hipError_t launch_h27_pencil(const DeviceMesh& m, const double* d_u_col, bool want_k,
+    bool overwrite, double* d_K, double* d_fint, hipStream_t stream);
 // Node-row gather (FCG_PATH_GATHER, hex8 StVK on any mesh): one wavefront per owned row node
 // (fcg_gather.hip).
 hipError_t launch_gather_h8(const DeviceMesh& m, const double* d_u_col, bool want_k, bool overwrite,

@@ -25,7 +25,7 @@ a = ap.parse_args()
 ct = fcg.HEX8 if a.celltype == "hex8" else fcg.HEX27
 kin = fcg.LINEAR if a.kinem == "linear" else fcg.TOTLAG
 path = {"auto": fcg.PATH_AUTO, "general": fcg.PATH_GENERAL, "structured": fcg.PATH_STRUCTURED,
-        "gather": fcg.PATH_GATHER}[a.path]
+        "gather": fcg.PATH_GATHER, "colored": fcg.PATH_COLORED}[a.path]
 t0 = time.perf_counter()
 m = fcg.BoxMesh(ct, (a.n, a.n, a.n), jitter=0.1 if ct == fcg.HEX8 else 0.02)
 u_np = m.u_col(1e-3 if kin == fcg.LINEAR else 5e-2)

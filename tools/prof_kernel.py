@@ -22,7 +22,7 @@ a = ap.parse_args()
 ct = fcg.HEX8 if a.celltype == "hex8" else fcg.HEX27
 kin = fcg.LINEAR if a.kinem == "linear" else fcg.TOTLAG
 path = {"auto": fcg.PATH_AUTO, "general": fcg.PATH_GENERAL, "structured": fcg.PATH_STRUCTURED,
-        "gather": fcg.PATH_GATHER}[a.path]
+        "gather": fcg.PATH_GATHER, "colored": fcg.PATH_COLORED}[a.path]
 m = fcg.BoxMesh(ct, (a.n, a.n, a.n), jitter=0.1 if ct == fcg.HEX8 else 0.02, seed=a.seed)
 if a.renumber:
     box = m
