@@ -960,8 +960,8 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
     const char* st = std::getenv("FCG_STAMPS");
     if (st && st[0] == '1')
     {
-      const unsigned long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      chk(upload(&m.stamps, zero, 8, bytes));
+      const unsigned long long zero[16] = {};
+      chk(upload(&m.stamps, zero, 16, bytes));
     }
   }
   else if (colored)
@@ -1149,8 +1149,8 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
     const char* st = std::getenv("FCG_STAMPS");
     if (st && st[0] == '1')
     {
-      const unsigned long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      chk(upload(&m.stamps, zero, 8, bytes));
+      const unsigned long long zero[16] = {};
+      chk(upload(&m.stamps, zero, 16, bytes));
     }
   }
   for (auto& ev : ctx->timing.ev) chk(hipEventCreate(&ev));
@@ -1505,11 +1505,11 @@ int fcg_get_diagnostics(const fcg_ctx* ctx, uint64_t* out, int n)
 {
   if (!ctx || !out || n < 0) return FCG_ERR_ARG;
   const fcg::DeviceMesh& m = ctx->mesh;
-  unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long v[16] = {};
   if (m.stamps && hipMemcpy(v, m.stamps, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess)
     return fcg_device_error();
-  for (int i = 0; i < n && i < 8; ++i) out[i] = v[i];
-  return m.stamps ? 8 : 0;
+  for (int i = 0; i < n && i < 16; ++i) out[i] = v[i];
+  return m.stamps ? 16 : 0;
 }
 
 int fcg_get_info(const fcg_ctx* ctx, fcg_info* info)

@@ -2,32 +2,38 @@
 // path of BASELINE config 3's element), redesigned around the FP64 matrix cores and a symmetric
 // per-element record.
 //
-//  h27_element_kernel<KIN>  one 256-lane workgroup per element (two per CU), SolidEleCalc's
-//      Gauss-point loop (4C_solid_3D_ele_calc.cpp:110-240, calc_lib.hpp:380-993) in reference
-//      coordinates:
-//        1. lanes (g, coordinate, X|u): J and du/dxi at the 27 Gauss points (dN . X); 27 more
-//           lanes: the nodal det J > 0 check (calc_lib.hpp:475-496);
+//  h27_element_kernel<KIN, ASM>  256 lanes per workgroup (two per CU) with two elements in
+//      flight: wave 3 produces element s while waves 0-2 consume element s - 1 (LDS double
+//      buffers, one barrier between the phases, one after).  SolidEleCalc's Gauss-point loop
+//      (4C_solid_3D_ele_calc.cpp:110-240, calc_lib.hpp:380-993) in reference coordinates:
+//        producer (wave 3):
+//        1. J and du/dxi at the 27 Gauss points (dN . X, dN . u), the nodal det J > 0 check
+//           (calc_lib.hpp:475-496);
 //        2. lanes g: J^-1, fac = det J w (calc_lib.hpp:435-448, 974-993), F = I + du/dX
 //           (calc_lib.hpp:579-605), E, StVK S (4C_mat_stvenantkirchhoff.cpp:169-177), and the
 //           per-point 3 x 3 factors that let every later stage work on the constant dN_a(xi_g):
 //             q_a = T d_a  with T = F J^-1 (linear: J^-1)            (B-operator columns F N_XYZ)
 //             fac N_XYZ_a . N_XYZ_b = d_a^T W d_b,  W = fac J^-T J^-1
 //             fac N_XYZ_a . S N_XYZ_b = d_a^T V d_b, V = fac J^-T S J^-1
-//             f_a = sum_g R_g d_a,  R = fac F S J^-1 (linear: fac S J^-1)     (calc_lib.hpp:851-860)
+//        and f_a = sum_g R_g d_a, R = fac F S J^-1 (linear: fac S J^-1) (calc_lib.hpp:851-860),
+//           written at once;
+//        consumers (waves 0-2, one 16 x 16 tile of node pairs each):
 //        3. the isotropic StVK blocks of every node pair a <= b (B_a^T C B_b + K_geo,
-//           calc_lib.hpp:872-927), all on v_mfma_f64_16x16x4_f64 tiles of 16 x 16 node pairs:
+//           calc_lib.hpp:872-927), all on v_mfma_f64_16x16x4_f64:
 //             K_ab = lambda G + mu G^T + mu H + geo I          (linear: mu tr(G) I, no H / geo)
-//             G_ij = sum_g fac q_a,i q_b,j                     (waves 0-2, K = 27 Gauss points)
+//             G_ij = sum_g fac q_a,i q_b,j                     (K = 27 Gauss points)
 //             H = sum_g c_ab(g) F F^T, c_ab = d_a^T W d_b     (one MFMA per point for c,
 //                                                                then 24 lane FMAs)
 //             geo = sum_g d_a^T V d_b                          (one accumulating MFMA per point,
 //                                                                same B operand as c)
-//           and f_a (wave 3, while waves 0-2 run G); every operand is formed on the fly from
-//           the constant dN_a(xi_g) and the per-point factors (no per-(g, a) work arrays);
-//        4. K_ab into an LDS image of the element's 378 blocks a <= b.
-//      Output: the owned incidences' block rows (3 x 81 + f, the general path's record, read
-//      contiguously by assemble27_kernel) -- or, FCG_H27_SYMREC=1, one record per element with the
-//      378 blocks a <= b and f_e (27.9 KB instead of 27 x 1.9 KB) for h27_assemble_kernel.
+//           every operand formed on the fly from the constant dN_a(xi_g) and the per-point
+//           factors (no per-(g, a) work arrays);
+//        4. K_ab into an LDS image of the element's 378 blocks a <= b, which all four waves write
+//           out after the phase barrier.
+//      Output (ASM 0): the owned incidences' block rows (3 x 81 + f, the general path's record,
+//      read contiguously by assemble27_kernel) -- or, FCG_H27_SYMREC=1, one record per element with
+//      the 378 blocks a <= b and f_e for h27_assemble_kernel.  ASM 1/2 (FCG_PATH_COLORED on a
+//      verified lattice): pencil order, the blocks added straight into the owned CSR rows.
 //  h27_assemble_kernel  SparseMatrix::assemble + LinAlg::assemble (4C_linalg_sparsematrix.cpp:
 //      444-576, 4C_linalg_utils_sparse_algebra_assemble.cpp:72-92) for owned rows: one wavefront
 //      per owned row node sums the block rows of its incident elements (K_ab or K_ba^T from the
@@ -91,41 +97,35 @@ __device__ inline double inv3(double* m)
   return det;
 }
 
-// LDS of one element's workgroup.  `big` holds stage-dependent views (offsets below): J | Gu
-// (stages 1-2) overlaid by the element's K image [378][9] (TotLag: mu H + geo I from the end of
-// stage 3 on); the per-point factors T | W | V | M | R live beside it in `gpf` (read until the
-// end of stage 4, while the K image is being written).
-constexpr int OFF_J = 0, OFF_GU = 243, OFF_KIMG = 0;
+// LDS of one workgroup.  The element pipeline (h27_element_kernel) keeps two elements in flight:
+// wave 3 produces element s (its Jacobians in J | Gu, its per-point factors into gpf[s & 1]) while
+// waves 0-2 consume element s - 1 from gpf[(s - 1) & 1] into the K image.  Per-point factors:
+// T | W | V | M | R (offsets below) and fac.
 constexpr int OFF_T = 0, OFF_W = 243, OFF_V = 405, OFF_M = 567, OFF_R = 729, GPF = 972;
-constexpr int BIG = kNpair * 9;
-static_assert(OFF_GU + 243 <= BIG, "Jacobians inside the K image region");
 struct H27Shared {
-  double dN[27 * 27 * 3];  // [g][c][d], loaded once per workgroup
-  double X[2][81], U[2][81];  // double-buffered: the next element's arrive during this one
-  int32_t inc[2][27];         // increc / pencil: incidence of (e, a), double-buffered like X, U
-  double fac[27];
-  alignas(16) double big[BIG];
-  double gpf[GPF];
+  double dN[27 * 27 * 3];       // [g][c][d], loaded once per workgroup
+  double X[81], U[81];          // the produced element's coordinates and displacements
+  double J[243], Gu[243];       // producer scratch: J, du/dxi per Gauss point
+  double gpf[2][GPF];           // per-point factors of the produced / consumed element
+  double fac[2][27];
+  alignas(16) double kimg[kNpair * 9];  // consumed element's blocks a <= b (col-major 3 x 3)
   double L1[9], dL1[9], dLn[9];
-  // pencil output: CSR offset of row (a, 0), row length, column position of node b in a's rows,
-  // the first-holder bit per pair class, and the pair class of (a, b)
-  int64_t rbase[27];
-  int32_t rlen[27], frow[27];  // frow: row LID of (a, 0) | first holder of (a, a) << 31
-  uint16_t ipos[27 * 27];
-  uint32_t fmask;
-  uint8_t pcls[27 * 27];
-  int bad;
+  int32_t inc[3][27];           // incidence of (e, a), -1 = not owned, by sequence index mod 3
+  // pencil output of the consumed element (by sequence parity): CSR offset of row (a, 0), row
+  // length, column position of node b in a's rows, first-holder bits of the pair classes
+  int64_t rbase[2][27];
+  int32_t rlen[2][27];
+  uint16_t ipos[2][27 * 27];
+  uint32_t fmask[2];
+  uint8_t pcls[27 * 27];        // pair class of (a, b)
+  int bad[2];
   uint8_t loc[27], latnode[27];
-  // views: J per g col-major (r + 3c), then J^-1 | du_i/dxi_k at k + 3i | T(i, k) at 3i + k |
-  // W, V, M symmetric (xx yy zz xy yz zx) | R(i, k) at 3i + k
-  __device__ double* J() { return big + OFF_J; }
-  __device__ double* Gu() { return big + OFF_GU; }
-  __device__ double* T() { return gpf + OFF_T; }
-  __device__ double* W() { return gpf + OFF_W; }
-  __device__ double* V() { return gpf + OFF_V; }
-  __device__ double* M() { return gpf + OFF_M; }
-  __device__ double* R() { return gpf + OFF_R; }
-  __device__ double* kimg() { return big + OFF_KIMG; }
+  // views of gpf[b]: T(i, k) at 3i + k, W, V, M symmetric (xx yy zz xy yz zx), R(i, k) at 3i + k
+  __device__ double* T(int b) { return gpf[b] + OFF_T; }
+  __device__ double* W(int b) { return gpf[b] + OFF_W; }
+  __device__ double* V(int b) { return gpf[b] + OFF_V; }
+  __device__ double* M(int b) { return gpf[b] + OFF_M; }
+  __device__ double* R(int b) { return gpf[b] + OFF_R; }
 };
 
 struct H27Args {
@@ -199,7 +199,7 @@ __device__ inline bool first_holder(int cls, uint32_t nb)
 // ASM: 0 = records for the row assembly; 1 = pencil order, add into K; 2 = pencil order, the first
 // holder writes (OVERWRITE)
 template <int KIN, int ASM>
-__global__ __launch_bounds__(kBlk, KIN ? 2 : FCG_H27_LIN_WGS) void h27_element_kernel(H27Args A)
+__global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
 {
   __shared__ H27Shared sh;
   const int tid = threadIdx.x;
@@ -224,25 +224,9 @@ __global__ __launch_bounds__(kBlk, KIN ? 2 : FCG_H27_LIN_WGS) void h27_element_k
   }
   const double lam = A.lambda, mu = A.mu;
 
-  // 0. X and u of the element (evaluate_element_nodes, calc_lib.hpp:180-203) are loaded one
-  //    element ahead: the dependent chain node id -> coordinates / DOF -> u is issued at the top
-  //    of an element and lands in the other LDS buffer before that element's first global store
-  //    (gfx9 counts stores in vmcnt: a wait for loads issued after stores would wait for those)
-  double xpre = 0.0, upre = 0.0;
-  int32_t ipre = -1;
-  auto prefetch = [&](int64_t e) {
-    if (tid < 81 && e >= 0)
-    {
-      const int a = tid / 3, d = tid - 3 * (tid / 3);
-      const int node = A.ele_nodes[e * kNpe + a];
-      xpre = A.node_x[3 * int64_t(node) + d];
-      upre = A.u_col[A.node_dof_col[node] + d];
-    }
-    else if ((ASM || A.increc) && tid >= 96 && tid < 96 + kNpe && e >= 0)
-      ipre = A.inc_of[e * kNpe + tid - 96];
-  };
-  // the elements of this workgroup: e = blockIdx.x + k gridDim.x, or (pencil order) the pencils
-  // pen_begin + blockIdx.x + k gridDim.x, each walked in x order
+  // the elements of this workgroup, in sequence: e = blockIdx.x + k gridDim.x, or (pencil order)
+  // the pencils pen_begin + blockIdx.x + k gridDim.x, each walked in x order.  Every thread walks
+  // the same sequence.
   int64_t pen = A.pen_begin + blockIdx.x, pos = -1, pend = -1;
   auto first_element = [&]() -> int64_t {
     if (!ASM) return blockIdx.x < A.n_ele ? int64_t(blockIdx.x) : -1;
@@ -252,6 +236,7 @@ __global__ __launch_bounds__(kBlk, KIN ? 2 : FCG_H27_LIN_WGS) void h27_element_k
     return A.col_ele[pos];
   };
   auto next_element = [&](int64_t e) -> int64_t {
+    if (e < 0) return -1;
     if (!ASM) return e + gridDim.x < A.n_ele ? e + gridDim.x : -1;
     if (++pos < pend) return A.col_ele[pos];
     pen += gridDim.x;
@@ -260,431 +245,457 @@ __global__ __launch_bounds__(kBlk, KIN ? 2 : FCG_H27_LIN_WGS) void h27_element_k
     pend = A.pen_ptr[pen + 1];
     return A.col_ele[pos];
   };
-  const int64_t e_first = first_element();
-  prefetch(e_first);
-  if (tid < 81)
-  {
-    sh.X[0][tid] = xpre;
-    sh.U[0][tid] = upre;
-  }
-  else if (tid >= 96 && tid < 96 + kNpe)
-    sh.inc[0][tid - 96] = ipre;
-  int buf = 0;
-  // diagnostic phase timers (FCG_STAMPS=1, tools/h27_stamps.py): thread 0's s_memtime deltas per
-  // phase, barrier waits included: 0 gather + J, 1 Gauss-point algebra, 2 VALU pair sums,
-  // 3 q + f_e, 4 matrix-core G + H image, 5 K image + record stores
+
+  // X, u and the incidences of an element (evaluate_element_nodes, calc_lib.hpp:180-203), by the
+  // producer wave: item t = lane + 64 q of 81 X | 81 u | 27 incidences
+  double xu_r[3];
+  int32_t inc_r[3];
+  auto load_xu = [&](int64_t e) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+    {
+      const int t = lane + 64 * q;
+      xu_r[q] = 0.0;
+      inc_r[q] = -1;
+      if (e < 0) continue;
+      if (t < 162)
+      {
+        const int tt = t < 81 ? t : t - 81, a = tt / 3, d = tt - 3 * (tt / 3);
+        const int node = A.ele_nodes[e * kNpe + a];
+        xu_r[q] = t < 81 ? A.node_x[3 * int64_t(node) + d] : A.u_col[A.node_dof_col[node] + d];
+      }
+      else if (t < 162 + kNpe && (ASM || A.increc))
+        inc_r[q] = A.inc_of[e * kNpe + t - 162];
+    }
+  };
+  auto store_xu = [&](int ib) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+    {
+      const int t = lane + 64 * q;
+      if (t < 81)
+        sh.X[t] = xu_r[q];
+      else if (t < 162)
+        sh.U[t - 81] = xu_r[q];
+      else if (t < 162 + kNpe)
+        sh.inc[ib][t - 162] = inc_r[q];
+    }
+  };
+  // LDS written by some lanes of the producer wave and read by others: a wavefront's LDS
+  // operations complete in order, so a wait for its own accesses plus a compiler barrier suffice
+  auto wave_lds_sync = [&]() { __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+
+  // diagnostic phase timers (FCG_STAMPS=1, tools/h27_stamps.py): s_memtime deltas per element,
+  // thread 0 (consumer): 0 wait at the top barrier, 1 H + geo, 2 G, 3 K image, 4 barrier + stores;
+  // thread 192 (producer): 5 gather + J + Gauss-point algebra + f
   unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0};
   unsigned long long st_last = A.stamps ? __builtin_amdgcn_s_memtime() : 0ull;
   int64_t st_n = 0;
 #define H27_STAMP(i)                                                                               \
-  if (A.stamps && tid == 0)                                                                        \
+  if (A.stamps && (tid == 0 || tid == 192))                                                        \
   {                                                                                                \
     const unsigned long long now = __builtin_amdgcn_s_memtime();                                  \
     st_acc[i] += now - st_last;                                                                    \
     st_last = now;                                                                                 \
   }
-  int64_t e_next = -1;
-  for (int64_t e = e_first; e >= 0; e = e_next, buf ^= 1)
-  {
-    ++st_n;
-    double* rec = A.rec + (A.increc || ASM ? 0 : e * kRec);
-    if (tid == 0) sh.bad = 0;
-    __syncthreads();
-    e_next = next_element(e);
-    prefetch(e_next);
-    const double* Xe = sh.X[buf];
-    const double* Ue = sh.U[buf];
-    // pencil output: this element's row bookkeeping, loaded by wave 3 (idle in stages 1-2) and
-    // parked in LDS at once: one global round trip, shorter than stage 1; wave 0 forms the
-    // first-holder mask of the pair classes
-    if (ASM && wave == 3)
-    {
-      uint32_t ipos_r[12];
-#pragma unroll
-      for (int q = 0; q < 12; ++q)
-      {
-        const int v = lane + 64 * q;
-        ipos_r[q] = 0u;
-        if (v < kNpe * kNpe)
-        {
-          const int a = v / kNpe;
-          const int32_t k = sh.inc[buf][a];
-          if (k >= 0) ipos_r[q] = A.inc_pos[int64_t(k) * kNpe + (v - kNpe * a)];
-        }
-      }
-      if (lane < kNpe)
-      {
-        const int32_t k = sh.inc[buf][lane];
-        int64_t rb = 0;
-        int32_t rl = 0, fr = -1;
-        if (k >= 0)
-        {
-          fr = A.inc_row0[k];
-          rb = A.rowptr[fr];
-          rl = int32_t(A.rowptr[fr + 1] - rb);
-          if (ASM == 2 && first_holder(pair_class(sh.loc[lane], sh.loc[lane]), A.ele_nb[e]))
-            fr = int32_t(uint32_t(fr) | 0x80000000u);
-        }
-        sh.rbase[lane] = rb;
-        sh.rlen[lane] = rl;
-        sh.frow[lane] = fr;
-      }
-#pragma unroll
-      for (int q = 0; q < 12; ++q)
-      {
-        const int v = lane + 64 * q;
-        if (v < kNpe * kNpe) sh.ipos[v] = uint16_t(ipos_r[q]);
-      }
-    }
-    if (ASM == 2 && wave == 0)
-    {
-      const uint64_t m = __ballot(tid < 27 && first_holder(tid, A.ele_nb[e]));
-      if (tid == 0) sh.fmask = uint32_t(m);
-    }
 
-    // 1. J and du/dxi at the Gauss points; nodal det J check (calc_lib.hpp:475-496) via the 1D
-    //    factors: at a node they are Kronecker deltas, so J sums the 3 nodes on each line
-    if (tid < 162)
-    {
-      const int g = tid / 6, rem = tid - 6 * (tid / 6);
-      const int k = rem % 3, s = rem / 3;
-      const double* src = s ? Ue : Xe;
-      const double* d = sh.dN + 81 * g;
-      double j0 = 0.0, j1 = 0.0, j2 = 0.0;
-#pragma unroll 9
-      for (int c = 0; c < kNpe; ++c)
-      {
-        const double x = src[3 * c + k];
-        j0 += d[3 * c + 0] * x;
-        j1 += d[3 * c + 1] * x;
-        j2 += d[3 * c + 2] * x;
-      }
-      double* dst = (s ? sh.Gu() : sh.J()) + 9 * g + 3 * k;
-      dst[0] = j0;
-      dst[1] = j1;
-      dst[2] = j2;
-    }
-    else if (tid < 162 + kNpe)
-    {
-      const int g = tid - 162;
-      const uint32_t l = sh.loc[g];
-      const int p = l & 3, q = (l >> 2) & 3, r = l >> 4;
-      double J[9];
-#pragma unroll
-      for (int kk = 0; kk < 9; ++kk) J[kk] = 0.0;
-#pragma unroll
-      for (int m = 0; m < 3; ++m)
-      {
-        const double* x0 = Xe + 3 * sh.latnode[m + 3 * q + 9 * r];
-        const double* x1 = Xe + 3 * sh.latnode[p + 3 * m + 9 * r];
-        const double* x2 = Xe + 3 * sh.latnode[p + 3 * q + 9 * m];
-        const double d0 = sh.dLn[3 * p + m], d1 = sh.dLn[3 * q + m], d2 = sh.dLn[3 * r + m];
-#pragma unroll
-        for (int c = 0; c < 3; ++c)
-        {
-          J[3 * c + 0] += d0 * x0[c];
-          J[3 * c + 1] += d1 * x1[c];
-          J[3 * c + 2] += d2 * x2[c];
-        }
-      }
-      const double det = inv3(J);
-      if (det == 0.0) atomicMax(&sh.bad, 2);
-      else if (!(det > 0)) atomicMax(&sh.bad, 1);
-    }
+  // prologue: the first element's X, u, incidences
+  int64_t ep = first_element();  // element produced in this iteration (sequence index s)
+  if (wave == 3)
+  {
+    load_xu(ep);
+    store_xu(0);
+  }
+  int64_t ec = -1;                    // element consumed in this iteration (sequence index s - 1)
+  int64_t epp = next_element(ep);     // element produced in the next iteration
+  for (int s = 0; ec >= 0 || ep >= 0; ++s)
+  {
+    const int pb = s & 1, cb = pb ^ 1;              // factor buffers of ep, ec
+    const int pi = s % 3, ci = (s + 2) % 3, ni = (s + 1) % 3;  // incidence buffers of ep, ec, epp
     __syncthreads();
     H27_STAMP(0);
+    const bool cons = ec >= 0 && sh.bad[cb] == 0;
 
-    // 2. per Gauss point: J^-1, fac, strains, StVK stress and the folded 3 x 3 factors
-    if (tid < kNpe)
+    if (wave == 3)
     {
-      const int g = tid;
-      double iJ[9];
-#pragma unroll
-      for (int kk = 0; kk < 9; ++kk) iJ[kk] = sh.J()[9 * g + kk];
-      const double det = inv3(iJ);
-      if (det == 0.0) atomicMax(&sh.bad, 2);
-      const double fac = det * c_w[g];
-      sh.fac[g] = fac;
-      // grad u: Hu(i, j) = du_i / dX_j = sum_k J^-1(j, k) du_i / dxi_k
-      double Hu[3][3];
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j)
-          Hu[i][j] = iJ[j] * sh.Gu()[9 * g + 3 * i] + iJ[j + 3] * sh.Gu()[9 * g + 3 * i + 1] +
-                     iJ[j + 6] * sh.Gu()[9 * g + 3 * i + 2];
-      double E[6], F[3][3];
-      if (KIN == 0)
+      // ---------------- producer: element ep
+      if (ep >= 0)
       {
-        // evaluate_linear_gl_strain (calc_lib.hpp:682-695): engineering shear
-        E[0] = Hu[0][0];
-        E[1] = Hu[1][1];
-        E[2] = Hu[2][2];
-        E[3] = Hu[0][1] + Hu[1][0];
-        E[4] = Hu[1][2] + Hu[2][1];
-        E[5] = Hu[0][2] + Hu[2][0];
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-          for (int j = 0; j < 3; ++j) F[i][j] = i == j ? 1.0 : 0.0;
-      }
-      else
-      {
-        // F = I + u N_XYZ^T (hex27, calc_lib.hpp:579-605); F^-1 must exist (calc_lib.hpp:562)
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-          for (int j = 0; j < 3; ++j) F[i][j] = Hu[i][j] + (i == j ? 1.0 : 0.0);
-        double Fi[9];
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-          for (int j = 0; j < 3; ++j) Fi[i + 3 * j] = F[i][j];
-        if (inv3(Fi) == 0.0) atomicMax(&sh.bad, 2);
-        // C = F^T F, E = (C - I) / 2 in strain-like Voigt form (calc_lib.hpp:639-676)
-        double C[3][3];
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-          for (int j = 0; j < 3; ++j) C[i][j] = F[0][i] * F[0][j] + F[1][i] * F[1][j] + F[2][i] * F[2][j];
-        E[0] = 0.5 * (C[0][0] - 1.0);
-        E[1] = 0.5 * (C[1][1] - 1.0);
-        E[2] = 0.5 * (C[2][2] - 1.0);
-        E[3] = C[0][1];
-        E[4] = C[1][2];
-        E[5] = C[0][2];
-      }
-      // S = C E (fill_cmat, 4C_mat_stvenantkirchhoff.cpp:115-145)
-      double S[3][3];
-      S[0][0] = A.cdiag * E[0] + A.lambda * (E[1] + E[2]);
-      S[1][1] = A.cdiag * E[1] + A.lambda * (E[0] + E[2]);
-      S[2][2] = A.cdiag * E[2] + A.lambda * (E[0] + E[1]);
-      S[0][1] = S[1][0] = A.mu * E[3];
-      S[1][2] = S[2][1] = A.mu * E[4];
-      S[0][2] = S[2][0] = A.mu * E[5];
-      // T = F J^-1, R = fac F S J^-1
-      double FS[3][3];
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) FS[i][j] = F[i][0] * S[0][j] + F[i][1] * S[1][j] + F[i][2] * S[2][j];
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int k = 0; k < 3; ++k)
+        ++st_n;
+        load_xu(epp);  // lands while ep's stages run; stored after stage 1 has read X, u
+        if (lane == 0) sh.bad[pb] = 0;
+        // pencil output bookkeeping of ep (read by all waves when ep is consumed)
+        const uint32_t nb = ASM ? A.ele_nb[ep] : 0u;
+        if (ASM)
         {
-          sh.T()[9 * g + 3 * i + k] = F[i][0] * iJ[3 * k] + F[i][1] * iJ[3 * k + 1] + F[i][2] * iJ[3 * k + 2];
-          sh.R()[9 * g + 3 * i + k] =
-              fac * (FS[i][0] * iJ[3 * k] + FS[i][1] * iJ[3 * k + 1] + FS[i][2] * iJ[3 * k + 2]);
-        }
-      if (KIN == 1)
-      {
-        // W = fac J^-T J^-1, V = fac J^-T S J^-1, M = F F^T  (xx yy zz xy yz zx)
-        double SJ[3][3];  // S J^-1
+          uint32_t ipos_r[12];
 #pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-          for (int l = 0; l < 3; ++l) SJ[i][l] = S[i][0] * iJ[3 * l] + S[i][1] * iJ[3 * l + 1] + S[i][2] * iJ[3 * l + 2];
-        const int kk[6] = {0, 1, 2, 0, 1, 0}, ll[6] = {0, 1, 2, 1, 2, 2};
-#pragma unroll
-        for (int s = 0; s < 6; ++s)
-        {
-          const int k = kk[s], l = ll[s];
-          // J^-1(j, k) = iJ[j + 3 k]
-          sh.W()[6 * g + s] = fac * (iJ[3 * k] * iJ[3 * l] + iJ[3 * k + 1] * iJ[3 * l + 1] + iJ[3 * k + 2] * iJ[3 * l + 2]);
-          sh.V()[6 * g + s] = fac * (iJ[3 * k] * SJ[0][l] + iJ[3 * k + 1] * SJ[1][l] + iJ[3 * k + 2] * SJ[2][l]);
-          sh.M()[6 * g + s] = F[k][0] * F[l][0] + F[k][1] * F[l][1] + F[k][2] * F[l][2];
-        }
-      }
-    }
-    __syncthreads();
-    H27_STAMP(1);
-    if (tid < 81)  // the next element's X and u, before this one's first global store
-    {
-      sh.X[buf ^ 1][tid] = xpre;
-      sh.U[buf ^ 1][tid] = upre;
-    }
-    else if (tid >= 96 && tid < 96 + kNpe)
-      sh.inc[buf ^ 1][tid - 96] = ipre;
-    if (sh.bad)
-    {
-      if (tid == 0)
-      {
-        atomicMax(&A.err[0], sh.bad);
-        atomicMin(&A.err[1], int32_t(e));
-      }
-      __syncthreads();
-      continue;
-    }
-
-    // matrix-core tiles of this wave: waves 0..2 take the node ranges (0,0), (0,1), (1,1) of 16;
-    // lane (r16, kq) feeds A[r16][kq] and B[kq][r16] and holds D[kq + 4 r][r16], r = 0..3.
-    // Operands come from the constant dN_a(xi_g) and the per-point 3 x 3 factors at clamped
-    // indices, always loaded and masked by multiplication (a load under a lane condition turns
-    // into a branch with its own wait: one LDS round trip per operand).
-    const int at = wave == 2 ? 1 : 0, bt = wave == 0 ? 0 : 1;
-    const int r16 = lane & 15, kq = lane >> 4;
-    const int a_l = 16 * at + r16, b_l = 16 * bt + r16;
-    const bool va = a_l < 27, vb = b_l < 27;
-    const int a_c = va ? a_l : 0, b_c = vb ? b_l : 0;
-    const f64x4_t zero4 = {0.0, 0.0, 0.0, 0.0};
-
-    // 3. TotLag: mu H + geo I, waves 0..2 on their tiles.  Per Gauss point one MFMA over k (K = 3,
-    //    padded to 4) gives c_ab = d_a^T W d_b, and H += c_ab M_g on the lanes; a second MFMA with
-    //    the same B operand accumulates geo_ab += d_a^T V d_b in its C input.  Both go into the
-    //    K image at once (J, Gu under it are dead), so that stage 4 holds only G.
-    if (KIN == 1 && A.want_k && wave < 3)
-    {
-      f64x4_t Hm[6];  // H per component (xx yy zz xy yz zx)
-#pragma unroll
-      for (int k = 0; k < 6; ++k) Hm[k] = zero4;
-      f64x4_t Geo = zero4;
-      const bool vk = kq < 3;
-      const int kc = vk ? kq : 0;
-      const double ma = (va && vk) ? 1.0 : 0.0, mb = (vb && vk) ? 1.0 : 0.0;
-      const int wr0 = kc == 0 ? 0 : (kc == 1 ? 3 : 5), wr1 = kc == 0 ? 3 : (kc == 1 ? 1 : 4),
-                wr2 = kc == 0 ? 5 : (kc == 1 ? 4 : 2);  // row kc of the symmetric W, V
-#pragma unroll 3
-      for (int g = 0; g < kNpe; ++g)
-      {
-        const double* da = sh.dN + 3 * (27 * g + a_c);
-        const double* Wg = sh.W() + 6 * g;
-        const double* Vg = sh.V() + 6 * g;
-        const double d0 = da[0], d1 = da[1], d2 = da[2];
-        const double av = (Wg[wr0] * d0 + Wg[wr1] * d1 + Wg[wr2] * d2) * ma;
-        const double avv = (Vg[wr0] * d0 + Vg[wr1] * d1 + Vg[wr2] * d2) * ma;
-        const double bv = sh.dN[3 * (27 * g + b_c) + kc] * mb;
-        const f64x4_t c = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, zero4, 0, 0, 0);
-        Geo = __builtin_amdgcn_mfma_f64_16x16x4f64(avv, bv, Geo, 0, 0, 0);
-        const double* Mg = sh.M() + 6 * g;
-#pragma unroll
-        for (int s = 0; s < 6; ++s)
-        {
-          const double m = Mg[s];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) Hm[s][r] += c[r] * m;
-        }
-      }
-      const int b = 16 * bt + r16;
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-      {
-        const int a = 16 * at + kq + 4 * r;
-        if (a < 27 && b < 27 && a <= b)
-        {
-          double* K = sh.kimg() + 9 * pidx(a, b);
-          const double geo = Geo[r];
-          K[0] = mu * Hm[0][r] + geo;
-          K[4] = mu * Hm[1][r] + geo;
-          K[8] = mu * Hm[2][r] + geo;
-          K[1] = K[3] = mu * Hm[3][r];
-          K[5] = K[7] = mu * Hm[4][r];
-          K[2] = K[6] = mu * Hm[5][r];
-        }
-      }
-    }
-    H27_STAMP(2);
-
-    // 4. G_ij = sum_g fac q_a,i q_b,j on the matrix cores (waves 0..2, 7 steps of 4 Gauss points;
-    //    q_a = T_g d_a formed on the fly) and, on wave 3 meanwhile, f_a = sum_g R_g d_a
-    //    (add_internal_force_vector, calc_lib.hpp:851-860)
-    f64x4_t X[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) X[k] = zero4;
-    if (wave < 3)
-    {
-      if (A.want_k)
-      {
-#pragma unroll
-        for (int st = 0; st < 7; ++st)
-        {
-          const int g = 4 * st + kq;
-          const bool vg = g < 27;
-          const int gc = vg ? g : 0;
-          const double fg = sh.fac[gc] * ((vg && va) ? 1.0 : 0.0);
-          const double mb = (vg && vb) ? 1.0 : 0.0;
-          const double* T = sh.T() + 9 * gc;
-          const double* da = sh.dN + 3 * (27 * gc + a_c);
-          const double* db = sh.dN + 3 * (27 * gc + b_c);
-          const double a0 = da[0], a1 = da[1], a2 = da[2], b0 = db[0], b1 = db[1], b2 = db[2];
-          double av[3], bv[3];
-#pragma unroll
-          for (int i = 0; i < 3; ++i)
+          for (int q = 0; q < 12; ++q)
           {
-            const double t0 = T[3 * i], t1 = T[3 * i + 1], t2 = T[3 * i + 2];
-            av[i] = fg * (t0 * a0 + t1 * a1 + t2 * a2);
-            bv[i] = mb * (t0 * b0 + t1 * b1 + t2 * b2);
+            const int v = lane + 64 * q;
+            ipos_r[q] = 0u;
+            if (v < kNpe * kNpe)
+            {
+              const int a = v / kNpe;
+              const int32_t k = sh.inc[pi][a];
+              if (k >= 0) ipos_r[q] = A.inc_pos[int64_t(k) * kNpe + (v - kNpe * a)];
+            }
           }
+          if (lane < kNpe)
+          {
+            const int32_t k = sh.inc[pi][lane];
+            int64_t rb = 0;
+            int32_t rl = 0;
+            if (k >= 0)
+            {
+              const int32_t r0 = A.inc_row0[k];
+              rb = A.rowptr[r0];
+              rl = int32_t(A.rowptr[r0 + 1] - rb);
+            }
+            sh.rbase[pb][lane] = rb;
+            sh.rlen[pb][lane] = rl;
+          }
+          if (ASM == 2)
+          {
+            const uint64_t m = __ballot(lane < 27 && first_holder(lane, nb));
+            if (lane == 0) sh.fmask[pb] = uint32_t(m);
+          }
+#pragma unroll
+          for (int q = 0; q < 12; ++q)
+          {
+            const int v = lane + 64 * q;
+            if (v < kNpe * kNpe) sh.ipos[pb][v] = uint16_t(ipos_r[q]);
+          }
+        }
+
+        // 1. J and du/dxi at the Gauss points (task t < 162: g, k, X|u) and the nodal det J check
+        //    (calc_lib.hpp:475-496, t = 162 + node) via the 1D factors: at a node they are
+        //    Kronecker deltas, so J sums the 3 nodes on each parametric line
+#pragma unroll 1
+        for (int q = 0; q < 3; ++q)
+        {
+          const int t = lane + 64 * q;
+          if (t < 162)
+          {
+            const int g = t / 6, rem = t - 6 * (t / 6);
+            const int k = rem % 3, sx = rem / 3;
+            const double* src = sx ? sh.U : sh.X;
+            const double* d = sh.dN + 81 * g;
+            double j0 = 0.0, j1 = 0.0, j2 = 0.0;
+#pragma unroll 9
+            for (int c = 0; c < kNpe; ++c)
+            {
+              const double x = src[3 * c + k];
+              j0 += d[3 * c + 0] * x;
+              j1 += d[3 * c + 1] * x;
+              j2 += d[3 * c + 2] * x;
+            }
+            double* dst = (sx ? sh.Gu : sh.J) + 9 * g + 3 * k;
+            dst[0] = j0;
+            dst[1] = j1;
+            dst[2] = j2;
+          }
+          else if (t < 162 + kNpe)
+          {
+            const int g = t - 162;
+            const uint32_t l = sh.loc[g];
+            const int p = l & 3, qq = (l >> 2) & 3, r = l >> 4;
+            double J[9];
+#pragma unroll
+            for (int kk = 0; kk < 9; ++kk) J[kk] = 0.0;
+#pragma unroll
+            for (int m = 0; m < 3; ++m)
+            {
+              const double* x0 = sh.X + 3 * sh.latnode[m + 3 * qq + 9 * r];
+              const double* x1 = sh.X + 3 * sh.latnode[p + 3 * m + 9 * r];
+              const double* x2 = sh.X + 3 * sh.latnode[p + 3 * qq + 9 * m];
+              const double d0 = sh.dLn[3 * p + m], d1 = sh.dLn[3 * qq + m], d2 = sh.dLn[3 * r + m];
+#pragma unroll
+              for (int c = 0; c < 3; ++c)
+              {
+                J[3 * c + 0] += d0 * x0[c];
+                J[3 * c + 1] += d1 * x1[c];
+                J[3 * c + 2] += d2 * x2[c];
+              }
+            }
+            const double det = inv3(J);
+            if (det == 0.0) atomicMax(&sh.bad[pb], 2);
+            else if (!(det > 0)) atomicMax(&sh.bad[pb], 1);
+          }
+        }
+        wave_lds_sync();
+
+        // 2. per Gauss point: J^-1, fac, strains, StVK stress and the folded 3 x 3 factors
+        if (lane < kNpe)
+        {
+          const int g = lane;
+          double iJ[9];
+#pragma unroll
+          for (int kk = 0; kk < 9; ++kk) iJ[kk] = sh.J[9 * g + kk];
+          const double det = inv3(iJ);
+          if (det == 0.0) atomicMax(&sh.bad[pb], 2);
+          const double fac = det * c_w[g];
+          sh.fac[pb][g] = fac;
+          // grad u: Hu(i, j) = du_i / dX_j = sum_k J^-1(j, k) du_i / dxi_k
+          double Hu[3][3];
 #pragma unroll
           for (int i = 0; i < 3; ++i)
 #pragma unroll
             for (int j = 0; j < 3; ++j)
-              X[3 * i + j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[j], X[3 * i + j], 0, 0, 0);
-        }
-      }
-    }
-    else if (lane < kNpe)
-    {
-      const int a = lane;
-      double f0 = 0.0, f1 = 0.0, f2 = 0.0;
-#pragma unroll 3
-      for (int g = 0; g < kNpe; ++g)
-      {
-        const double* R = sh.R() + 9 * g;
-        const double* d = sh.dN + 3 * (27 * g + a);
-        const double d0 = d[0], d1 = d[1], d2 = d[2];
-        f0 += R[0] * d0 + R[1] * d1 + R[2] * d2;
-        f1 += R[3] * d0 + R[4] * d1 + R[5] * d2;
-        f2 += R[6] * d0 + R[7] * d1 + R[8] * d2;
-      }
-      if (ASM)
-      {
-        const int32_t fr = sh.frow[a];
-        if (fr != -1)
-        {
-          double* o = A.fint + (fr & 0x7FFFFFFF);
-          if (ASM == 2 && fr < 0)
+              Hu[i][j] = iJ[j] * sh.Gu[9 * g + 3 * i] + iJ[j + 3] * sh.Gu[9 * g + 3 * i + 1] +
+                         iJ[j + 6] * sh.Gu[9 * g + 3 * i + 2];
+          double E[6], F[3][3];
+          if (KIN == 0)
           {
+            // evaluate_linear_gl_strain (calc_lib.hpp:682-695): engineering shear
+            E[0] = Hu[0][0];
+            E[1] = Hu[1][1];
+            E[2] = Hu[2][2];
+            E[3] = Hu[0][1] + Hu[1][0];
+            E[4] = Hu[1][2] + Hu[2][1];
+            E[5] = Hu[0][2] + Hu[2][0];
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+              for (int j = 0; j < 3; ++j) F[i][j] = i == j ? 1.0 : 0.0;
+          }
+          else
+          {
+            // F = I + u N_XYZ^T (hex27, calc_lib.hpp:579-605); F^-1 must exist (calc_lib.hpp:562)
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+              for (int j = 0; j < 3; ++j) F[i][j] = Hu[i][j] + (i == j ? 1.0 : 0.0);
+            double Fi[9];
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+              for (int j = 0; j < 3; ++j) Fi[i + 3 * j] = F[i][j];
+            if (inv3(Fi) == 0.0) atomicMax(&sh.bad[pb], 2);
+            // C = F^T F, E = (C - I) / 2 in strain-like Voigt form (calc_lib.hpp:639-676)
+            double C[3][3];
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+              for (int j = 0; j < 3; ++j) C[i][j] = F[0][i] * F[0][j] + F[1][i] * F[1][j] + F[2][i] * F[2][j];
+            E[0] = 0.5 * (C[0][0] - 1.0);
+            E[1] = 0.5 * (C[1][1] - 1.0);
+            E[2] = 0.5 * (C[2][2] - 1.0);
+            E[3] = C[0][1];
+            E[4] = C[1][2];
+            E[5] = C[0][2];
+          }
+          // S = C E (fill_cmat, 4C_mat_stvenantkirchhoff.cpp:115-145)
+          double S[3][3];
+          S[0][0] = A.cdiag * E[0] + A.lambda * (E[1] + E[2]);
+          S[1][1] = A.cdiag * E[1] + A.lambda * (E[0] + E[2]);
+          S[2][2] = A.cdiag * E[2] + A.lambda * (E[0] + E[1]);
+          S[0][1] = S[1][0] = A.mu * E[3];
+          S[1][2] = S[2][1] = A.mu * E[4];
+          S[0][2] = S[2][0] = A.mu * E[5];
+          // T = F J^-1, R = fac F S J^-1
+          double FS[3][3];
+#pragma unroll
+          for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) FS[i][j] = F[i][0] * S[0][j] + F[i][1] * S[1][j] + F[i][2] * S[2][j];
+#pragma unroll
+          for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+            {
+              sh.T(pb)[9 * g + 3 * i + k] = F[i][0] * iJ[3 * k] + F[i][1] * iJ[3 * k + 1] + F[i][2] * iJ[3 * k + 2];
+              sh.R(pb)[9 * g + 3 * i + k] =
+                  fac * (FS[i][0] * iJ[3 * k] + FS[i][1] * iJ[3 * k + 1] + FS[i][2] * iJ[3 * k + 2]);
+            }
+          if (KIN == 1)
+          {
+            // W = fac J^-T J^-1, V = fac J^-T S J^-1, M = F F^T  (xx yy zz xy yz zx)
+            double SJ[3][3];  // S J^-1
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+              for (int l = 0; l < 3; ++l) SJ[i][l] = S[i][0] * iJ[3 * l] + S[i][1] * iJ[3 * l + 1] + S[i][2] * iJ[3 * l + 2];
+            const int kk[6] = {0, 1, 2, 0, 1, 0}, ll[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+            for (int x = 0; x < 6; ++x)
+            {
+              const int k = kk[x], l = ll[x];
+              // J^-1(j, k) = iJ[j + 3 k]
+              sh.W(pb)[6 * g + x] = fac * (iJ[3 * k] * iJ[3 * l] + iJ[3 * k + 1] * iJ[3 * l + 1] + iJ[3 * k + 2] * iJ[3 * l + 2]);
+              sh.V(pb)[6 * g + x] = fac * (iJ[3 * k] * SJ[0][l] + iJ[3 * k + 1] * SJ[1][l] + iJ[3 * k + 2] * SJ[2][l]);
+              sh.M(pb)[6 * g + x] = F[k][0] * F[l][0] + F[k][1] * F[l][1] + F[k][2] * F[l][2];
+            }
+          }
+        }
+        wave_lds_sync();
+        store_xu(ni);  // stage 1 has read X, u: the next element's take their place
+
+        // f_a = sum_g R_g d_a (add_internal_force_vector, calc_lib.hpp:851-860) of ep, written
+        // now (a skipped element leaves its rows to the error report)
+        if (lane < kNpe && sh.bad[pb] == 0)
+        {
+          const int a = lane;
+          double f0 = 0.0, f1 = 0.0, f2 = 0.0;
+#pragma unroll 3
+          for (int g = 0; g < kNpe; ++g)
+          {
+            const double* R = sh.R(pb) + 9 * g;
+            const double* d = sh.dN + 3 * (27 * g + a);
+            const double d0 = d[0], d1 = d[1], d2 = d[2];
+            f0 += R[0] * d0 + R[1] * d1 + R[2] * d2;
+            f1 += R[3] * d0 + R[4] * d1 + R[5] * d2;
+            f2 += R[6] * d0 + R[7] * d1 + R[8] * d2;
+          }
+          const int32_t k = sh.inc[pi][a];
+          if (ASM)
+          {
+            if (k >= 0)
+            {
+              double* o = A.fint + A.inc_row0[k];
+              if (ASM == 2 && first_holder(pair_class(sh.loc[a], sh.loc[a]), nb))
+              {
+                o[0] = f0;
+                o[1] = f1;
+                o[2] = f2;
+              }
+              else
+              {
+                o[0] += f0;
+                o[1] += f1;
+                o[2] += f2;
+              }
+            }
+          }
+          else if (!A.increc)
+          {
+            double* o = A.rec + ep * kRec + kNpair * 9 + 3 * a;
             o[0] = f0;
             o[1] = f1;
             o[2] = f2;
           }
-          else
+          else if (k >= 0)
           {
-            o[0] += f0;
-            o[1] += f1;
-            o[2] += f2;
+            double* o = A.rec + int64_t(k) * kIncRec + 243;
+            o[0] = f0;
+            o[1] = f1;
+            o[2] = f2;
           }
         }
       }
-      else if (!A.increc)
-      {
-        rec[kNpair * 9 + 3 * a + 0] = f0;
-        rec[kNpair * 9 + 3 * a + 1] = f1;
-        rec[kNpair * 9 + 3 * a + 2] = f2;
-      }
-      else if (sh.inc[buf][a] >= 0)
-      {
-        double* o = A.rec + int64_t(sh.inc[buf][a]) * kIncRec + 243;
-        o[0] = f0;
-        o[1] = f1;
-        o[2] = f2;
-      }
+      H27_STAMP(5);
     }
-    H27_STAMP(3);  // no barrier: stage 5 reads and writes only this lane's own image entries
-    if (!A.want_k) continue;
-
-    // 5. K_ab = lambda G + mu G^T + (mu tr G I | mu H + geo I) into the LDS image, which leaves
-    //    as contiguous pieces: one store instruction covers 1 KB instead of 64 scattered entries
-    if (wave < 3)
+    else if (cons && A.want_k)
     {
+      // ---------------- consumers (waves 0-2): element ec's node-pair blocks on the matrix cores.
+      // Wave w takes the node ranges (0,0), (0,1), (1,1) of 16; lane (r16, kq) feeds A[r16][kq]
+      // and B[kq][r16] and holds D[kq + 4 r][r16], r = 0..3.  Operands come from the constant
+      // dN_a(xi_g) and the per-point 3 x 3 factors at clamped indices, always loaded and masked by
+      // multiplication (a load under a lane condition turns into a branch with its own wait).
+      const int at = wave == 2 ? 1 : 0, bt = wave == 0 ? 0 : 1;
+      const int r16 = lane & 15, kq = lane >> 4;
+      const int a_l = 16 * at + r16, b_l = 16 * bt + r16;
+      const bool va = a_l < 27, vb = b_l < 27;
+      const int a_c = va ? a_l : 0, b_c = vb ? b_l : 0;
+      const f64x4_t zero4 = {0.0, 0.0, 0.0, 0.0};
       const int b = 16 * bt + r16;
+
+      // 3. TotLag: mu H + geo I.  Per Gauss point one MFMA over k (K = 3, padded to 4) gives
+      //    c_ab = d_a^T W d_b, and H += c_ab M_g on the lanes; a second MFMA with the same B operand
+      //    accumulates geo_ab += d_a^T V d_b in its C input.  Both go into the K image at once, so
+      //    that stage 4 holds only G.
+      if (KIN == 1)
+      {
+        f64x4_t Hm[6];  // H per component (xx yy zz xy yz zx)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) Hm[k] = zero4;
+        f64x4_t Geo = zero4;
+        const bool vk = kq < 3;
+        const int kc = vk ? kq : 0;
+        const double ma = (va && vk) ? 1.0 : 0.0, mb = (vb && vk) ? 1.0 : 0.0;
+        const int wr0 = kc == 0 ? 0 : (kc == 1 ? 3 : 5), wr1 = kc == 0 ? 3 : (kc == 1 ? 1 : 4),
+                  wr2 = kc == 0 ? 5 : (kc == 1 ? 4 : 2);  // row kc of the symmetric W, V
+#pragma unroll 3
+        for (int g = 0; g < kNpe; ++g)
+        {
+          const double* da = sh.dN + 3 * (27 * g + a_c);
+          const double* Wg = sh.W(cb) + 6 * g;
+          const double* Vg = sh.V(cb) + 6 * g;
+          const double d0 = da[0], d1 = da[1], d2 = da[2];
+          const double av = (Wg[wr0] * d0 + Wg[wr1] * d1 + Wg[wr2] * d2) * ma;
+          const double avv = (Vg[wr0] * d0 + Vg[wr1] * d1 + Vg[wr2] * d2) * ma;
+          const double bv = sh.dN[3 * (27 * g + b_c) + kc] * mb;
+          const f64x4_t c = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, zero4, 0, 0, 0);
+          Geo = __builtin_amdgcn_mfma_f64_16x16x4f64(avv, bv, Geo, 0, 0, 0);
+          const double* Mg = sh.M(cb) + 6 * g;
+#pragma unroll
+          for (int x = 0; x < 6; ++x)
+          {
+            const double m = Mg[x];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Hm[x][r] += c[r] * m;
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+          const int a = 16 * at + kq + 4 * r;
+          if (a < 27 && b < 27 && a <= b)
+          {
+            double* K = sh.kimg + 9 * pidx(a, b);
+            const double geo = Geo[r];
+            K[0] = mu * Hm[0][r] + geo;
+            K[4] = mu * Hm[1][r] + geo;
+            K[8] = mu * Hm[2][r] + geo;
+            K[1] = K[3] = mu * Hm[3][r];
+            K[5] = K[7] = mu * Hm[4][r];
+            K[2] = K[6] = mu * Hm[5][r];
+          }
+        }
+      }
+      H27_STAMP(1);
+
+      // 4. G_ij = sum_g fac q_a,i q_b,j (7 steps of 4 Gauss points; q_a = T_g d_a on the fly)
+      f64x4_t X[9];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) X[k] = zero4;
+#pragma unroll
+      for (int st = 0; st < 7; ++st)
+      {
+        const int g = 4 * st + kq;
+        const bool vg = g < 27;
+        const int gc = vg ? g : 0;
+        const double fg = sh.fac[cb][gc] * ((vg && va) ? 1.0 : 0.0);
+        const double mb = (vg && vb) ? 1.0 : 0.0;
+        const double* T = sh.T(cb) + 9 * gc;
+        const double* da = sh.dN + 3 * (27 * gc + a_c);
+        const double* db = sh.dN + 3 * (27 * gc + b_c);
+        const double a0 = da[0], a1 = da[1], a2 = da[2], b0 = db[0], b1 = db[1], b2 = db[2];
+        double av[3], bv[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+        {
+          const double t0 = T[3 * i], t1 = T[3 * i + 1], t2 = T[3 * i + 2];
+          av[i] = fg * (t0 * a0 + t1 * a1 + t2 * a2);
+          bv[i] = mb * (t0 * b0 + t1 * b1 + t2 * b2);
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j)
+            X[3 * i + j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[j], X[3 * i + j], 0, 0, 0);
+      }
+      H27_STAMP(2);
+
+      // 5. K_ab = lambda G + mu G^T + (mu tr G I | mu H + geo I) into the LDS image, which leaves
+      //    as contiguous pieces: one store instruction covers 1 KB instead of 64 scattered entries
 #pragma unroll
       for (int r = 0; r < 4; ++r)
       {
         const int a = 16 * at + kq + 4 * r;
         if (a < 27 && b < 27 && a <= b)
         {
+          double* K = sh.kimg + 9 * pidx(a, b);
           double add[9];
           if (KIN == 0)
           {
@@ -692,8 +703,7 @@ __global__ __launch_bounds__(kBlk, KIN ? 2 : FCG_H27_LIN_WGS) void h27_element_k
 #pragma unroll
             for (int k = 0; k < 9; ++k) add[k] = (k == 0 || k == 4 || k == 8) ? tr : 0.0;
           }
-          double* K = sh.kimg() + 9 * pidx(a, b);
-          if (KIN == 1)
+          else
           {
 #pragma unroll
             for (int k = 0; k < 9; ++k) add[k] = K[k];  // mu H + geo I from stage 3
@@ -705,80 +715,99 @@ __global__ __launch_bounds__(kBlk, KIN ? 2 : FCG_H27_LIN_WGS) void h27_element_k
               K[i + 3 * j] = lam * X[3 * i + j][r] + mu * X[3 * j + i][r] + add[i + 3 * j];
         }
       }
+      H27_STAMP(3);
     }
     __syncthreads();
-    H27_STAMP(4);
-    // 6. the record(s)
-    if (ASM)
+
+    // 6. element ec's record(s) or rows, by all waves
+    if (ec >= 0 && sh.bad[cb] != 0)
     {
-      // straight into the owned rows: entry v = (a, i, c) of a's 3 rows over the 81 columns in
-      // lattice order (c / 3 = lattice node, so lanes v, v + 1 hit contiguous CSR columns in runs
-      // of 3 nodes); every load of a batch is issued before its stores.  The pencil's previous
-      // element wrote its shared rows before this element's barriers, from this workgroup.
-      constexpr int NV = FCG_H27P_NV;
-      const uint32_t fmask = sh.fmask;
-      for (int v0 = 0; v0 < kNpe * 243; v0 += NV * kBlk)
+      if (tid == 0)
       {
-        int64_t addr[NV];
-        double val[NV];
-#pragma unroll
-        for (int k = 0; k < NV; ++k)
+        atomicMax(&A.err[0], sh.bad[cb]);
+        atomicMin(&A.err[1], int32_t(ec));
+      }
+    }
+    else if (cons && A.want_k)
+    {
+      if (ASM)
+      {
+        // straight into the owned rows: entry v = (a, i, c) of a's 3 rows over the 81 columns in
+        // lattice order (c / 3 = lattice node, so lanes v, v + 1 hit contiguous CSR columns in runs
+        // of 3 nodes); every load of a batch is issued before its stores.  The pencil's previous
+        // element wrote its shared rows in the previous iteration, from this workgroup.
+        constexpr int NV = FCG_H27P_NV;
+        const uint32_t fmask = sh.fmask[cb];
+        for (int v0 = 0; v0 < kNpe * 243; v0 += NV * kBlk)
         {
-          const int v = v0 + tid + kBlk * k;
-          addr[k] = -1;
-          val[k] = 0.0;
-          if (v >= kNpe * 243) continue;
-          const int a = v / 243;
-          if (sh.inc[buf][a] < 0) continue;
-          const int r = v - 243 * a;
-          const int i = r / 81, c = r - 81 * (r / 81);
-          const int b = sh.latnode[c / 3], j = c - 3 * (c / 3);
-          addr[k] = sh.rbase[a] + int64_t(i * sh.rlen[a] + sh.ipos[kNpe * a + b] + j);
-          const bool up = a <= b;
-          val[k] = sh.kimg()[9 * (up ? pidx(a, b) : pidx(b, a)) + (up ? i + 3 * j : j + 3 * i)];
-          if (ASM == 1 || !((fmask >> sh.pcls[kNpe * a + b]) & 1u)) val[k] += A.K[addr[k]];
+          int64_t addr[NV];
+          double val[NV];
+#pragma unroll
+          for (int k = 0; k < NV; ++k)
+          {
+            const int v = v0 + tid + kBlk * k;
+            addr[k] = -1;
+            val[k] = 0.0;
+            if (v >= kNpe * 243) continue;
+            const int a = v / 243;
+            if (sh.inc[ci][a] < 0) continue;
+            const int r = v - 243 * a;
+            const int i = r / 81, c = r - 81 * (r / 81);
+            const int b = sh.latnode[c / 3], j = c - 3 * (c / 3);
+            addr[k] = sh.rbase[cb][a] + int64_t(i * sh.rlen[cb][a] + sh.ipos[cb][kNpe * a + b] + j);
+            const bool up = a <= b;
+            val[k] = sh.kimg[9 * (up ? pidx(a, b) : pidx(b, a)) + (up ? i + 3 * j : j + 3 * i)];
+            if (ASM == 1 || !((fmask >> sh.pcls[kNpe * a + b]) & 1u)) val[k] += A.K[addr[k]];
+          }
+#pragma unroll
+          for (int k = 0; k < NV; ++k)
+            if (addr[k] >= 0) A.K[addr[k]] = val[k];
         }
-#pragma unroll
-        for (int k = 0; k < NV; ++k)
-          if (addr[k] >= 0) A.K[addr[k]] = val[k];
       }
-    }
-    else if (A.increc)
-    {
-      // the owned incidences' block rows K_ab, b = 0..26 (K_ba^T for b < a), row-major 3 x 81:
-      // the record of the general path's assemble27_kernel.  One (a, b) block per lane: its 9
-      // entries from the image, then 3 pieces of 3 into the rows (lanes b, b + 1 contiguous)
-      for (int p = tid; p < kNpe * kNpe; p += kBlk)
+      else if (A.increc)
       {
-        const int a = p / kNpe, b = p - kNpe * a;
-        const int32_t k = sh.inc[buf][a];
-        if (k < 0) continue;
-        const bool up = a <= b;
-        const double* src = sh.kimg() + 9 * (up ? pidx(a, b) : pidx(b, a));
-        double v[9];
+        // the owned incidences' block rows K_ab, b = 0..26 (K_ba^T for b < a), row-major 3 x 81:
+        // the record of the general path's assemble27_kernel.  One (a, b) block per lane: its 9
+        // entries from the image, then 3 pieces of 3 into the rows (lanes b, b + 1 contiguous)
+        for (int p = tid; p < kNpe * kNpe; p += kBlk)
+        {
+          const int a = p / kNpe, b = p - kNpe * a;
+          const int32_t k = sh.inc[ci][a];
+          if (k < 0) continue;
+          const bool up = a <= b;
+          const double* src = sh.kimg + 9 * (up ? pidx(a, b) : pidx(b, a));
+          double v[9];
 #pragma unroll
-        for (int q = 0; q < 9; ++q) v[q] = src[q];  // col-major K_(min,max)
-        double* dst = A.rec + int64_t(k) * kIncRec + 3 * b;
+          for (int q = 0; q < 9; ++q) v[q] = src[q];  // col-major K_(min,max)
+          double* dst = A.rec + int64_t(k) * kIncRec + 3 * b;
 #pragma unroll
-        for (int i = 0; i < 3; ++i)
+          for (int i = 0; i < 3; ++i)
 #pragma unroll
-          for (int j = 0; j < 3; ++j) dst[81 * i + j] = up ? v[i + 3 * j] : v[j + 3 * i];
+            for (int j = 0; j < 3; ++j) dst[81 * i + j] = up ? v[i + 3 * j] : v[j + 3 * i];
+        }
+      }
+      else
+      {
+        const double2* src = reinterpret_cast<const double2*>(sh.kimg);
+        double2* dst = reinterpret_cast<double2*>(A.rec + ec * kRec);  // 16-byte aligned (kRec even)
+        for (int v = tid; v < kNpair * 9 / 2; v += kBlk) dst[v] = src[v];
       }
     }
+    H27_STAMP(4);
+    ec = ep;
+    ep = epp;
+    epp = next_element(epp);
+  }
+  if (A.stamps && (tid == 0 || tid == 192))
+  {
+    if (tid == 0)
+      for (int i = 0; i < 5; ++i) atomicAdd(&A.stamps[i], st_acc[i]);
     else
     {
-      const double2* src = reinterpret_cast<const double2*>(sh.kimg());
-      double2* dst = reinterpret_cast<double2*>(rec);  // records are 16-byte aligned (kRec even)
-      for (int v = tid; v < kNpair * 9 / 2; v += kBlk) dst[v] = src[v];
+      atomicAdd(&A.stamps[5], st_acc[5]);
+      atomicAdd(&A.stamps[7], (unsigned long long)st_n);
     }
-    __syncthreads();
-    H27_STAMP(5);
-  }
-  if (A.stamps && tid == 0)
-  {
-    for (int i = 0; i < 6; ++i) atomicAdd(&A.stamps[i], st_acc[i]);
-    atomicAdd(&A.stamps[6], 1ull);
-    atomicAdd(&A.stamps[7], (unsigned long long)st_n);
+    if (tid == 0) atomicAdd(&A.stamps[6], 1ull);
   }
 #undef H27_STAMP
 }

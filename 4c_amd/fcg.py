@@ -732,8 +732,8 @@ class Evaluator:
 
     def diagnostics(self):
         """Per-phase cycle counters of the fused kernel (FCG_STAMPS=1 at creation), or None."""
-        buf = (ctypes.c_uint64 * 8)()
-        n = lib().fcg_get_diagnostics(self._h, buf, 8)
+        buf = (ctypes.c_uint64 * 16)()
+        n = lib().fcg_get_diagnostics(self._h, buf, 16)
         return list(buf) if n > 0 else None
 
     def timing(self):

@@ -359,8 +359,10 @@ def hex27_secondary(dev, n, steps, threads, with_cpu):
         "workload": f"hex27-totlag-{n}^3", "baseline_config": "BASELINE.json configs[2] element",
         "value": mesh.n_ele / wall, "unit": "element-evaluations/s", "ms_per_step": 1e3 * wall,
         "elements": mesh.n_ele, "nnz": mesh.nnz,
-        "path": ("general: h27_element_kernel (G on v_mfma_f64_16x16x4_f64, H/geo on the VALU) + "
-                 "h27_assemble_kernel (symmetric records)"),
+        "path": ("general: h27_element_kernel (two elements in flight per workgroup: wave 3 forms "
+                 "the next element's Jacobians (MFMA) and Gauss-point factors while waves 0-2 put "
+                 "this one's G, c_ab, geo on v_mfma_f64_16x16x4_f64) writing the owned incidences' "
+                 "block rows + assemble27_kernel (one contiguous row write per node)"),
         # bound by the flops the kernel executes (507.6k FMA-flop + ~20k per element, the
         # reference-coordinate contracted form; EXEC_FLOP_PER_ELE_H27_TOTLAG) against the 37.7 kB
         # of HBM: 6.7 ns vs 4.7 ns per element at the spec peaks -> FP64 (matrix = vector peak)

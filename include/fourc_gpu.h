@@ -190,9 +190,9 @@ int fcg_measure_peaks(int device, double* hbm_triad_gbs, double* fp64_valu_tflop
 int fcg_measure_hbm(int device, double* copy_gbs, double* write_gbs);
 
 /* Diagnostics only: with FCG_STAMPS=1 in the environment at fcg_create, the fused kernel sums
- * per-phase cycle counts (s_memtime, thread 0 of every workgroup) into 8 counters: commit,
- * Gauss-point stage, node-row stage, accumulation, flush, workgroups (index 5).  Returns the number of
- * counters (0 when off). */
+ * per-phase cycle counts (s_memtime, thread 0 of every workgroup) into 16 counters: commit,
+ * Gauss-point stage, node-row stage, accumulation, flush, workgroups (index 5); the hex27 element
+ * kernel's layout is in fcg_hex27.hip.  Returns the number of counters (0 when off). */
 int fcg_get_diagnostics(const fcg_ctx* ctx, uint64_t* out, int n);
 
 /* ------------------------------------------------------------------------------------------
