@@ -193,6 +193,9 @@ __device__ inline bool first_holder(int cls, uint32_t nb)
 #ifndef FCG_H27_LIN_WGS
 #define FCG_H27_LIN_WGS 2
 #endif
+#ifndef FCG_H27_HUNROLL
+#define FCG_H27_HUNROLL 3  // unroll of the consumers' H + geo loop over the Gauss points
+#endif
 #ifndef FCG_H27P_NV
 #define FCG_H27P_NV 9  // pencil output: entries in flight per lane
 #endif
@@ -284,6 +287,60 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
   // LDS written by some lanes of the producer wave and read by others: a wavefront's LDS
   // operations complete in order, so a wait for its own accesses plus a compiler barrier suffice
   auto wave_lds_sync = [&]() { __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+
+  // f_a = sum_g R_g d_a (add_internal_force_vector, calc_lib.hpp:851-860) of element e from the
+  // factor buffer fb, written at once (a skipped element leaves its rows to the error report)
+  auto emit_f = [&](int64_t e, int fb, int ib, uint32_t nbv) {
+    if (lane < kNpe && sh.bad[fb] == 0)
+    {
+      const int a = lane;
+      double f0 = 0.0, f1 = 0.0, f2 = 0.0;
+#pragma unroll 3
+      for (int g = 0; g < kNpe; ++g)
+      {
+        const double* R = sh.R(fb) + 9 * g;
+        const double* d = sh.dN + 3 * (27 * g + a);
+        const double d0 = d[0], d1 = d[1], d2 = d[2];
+        f0 += R[0] * d0 + R[1] * d1 + R[2] * d2;
+        f1 += R[3] * d0 + R[4] * d1 + R[5] * d2;
+        f2 += R[6] * d0 + R[7] * d1 + R[8] * d2;
+      }
+      const int32_t k = sh.inc[ib][a];
+      if (ASM)
+      {
+        if (k >= 0)
+        {
+          double* o = A.fint + A.inc_row0[k];
+          if (ASM == 2 && first_holder(pair_class(sh.loc[a], sh.loc[a]), nbv))
+          {
+            o[0] = f0;
+            o[1] = f1;
+            o[2] = f2;
+          }
+          else
+          {
+            o[0] += f0;
+            o[1] += f1;
+            o[2] += f2;
+          }
+        }
+      }
+      else if (!A.increc)
+      {
+        double* o = A.rec + e * kRec + kNpair * 9 + 3 * a;
+        o[0] = f0;
+        o[1] = f1;
+        o[2] = f2;
+      }
+      else if (k >= 0)
+      {
+        double* o = A.rec + int64_t(k) * kIncRec + 243;
+        o[0] = f0;
+        o[1] = f1;
+        o[2] = f2;
+      }
+    }
+  };
 
   // diagnostic phase timers (FCG_STAMPS=1, tools/h27_stamps.py): s_memtime deltas per element,
   // thread 0 (consumer): 0 wait at the top barrier, 1 H + geo, 2 G, 3 K image, 4 barrier + stores;
@@ -531,57 +588,7 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
         wave_lds_sync();
         store_xu(ni);  // stage 1 has read X, u: the next element's take their place
 
-        // f_a = sum_g R_g d_a (add_internal_force_vector, calc_lib.hpp:851-860) of ep, written
-        // now (a skipped element leaves its rows to the error report)
-        if (lane < kNpe && sh.bad[pb] == 0)
-        {
-          const int a = lane;
-          double f0 = 0.0, f1 = 0.0, f2 = 0.0;
-#pragma unroll 3
-          for (int g = 0; g < kNpe; ++g)
-          {
-            const double* R = sh.R(pb) + 9 * g;
-            const double* d = sh.dN + 3 * (27 * g + a);
-            const double d0 = d[0], d1 = d[1], d2 = d[2];
-            f0 += R[0] * d0 + R[1] * d1 + R[2] * d2;
-            f1 += R[3] * d0 + R[4] * d1 + R[5] * d2;
-            f2 += R[6] * d0 + R[7] * d1 + R[8] * d2;
-          }
-          const int32_t k = sh.inc[pi][a];
-          if (ASM)
-          {
-            if (k >= 0)
-            {
-              double* o = A.fint + A.inc_row0[k];
-              if (ASM == 2 && first_holder(pair_class(sh.loc[a], sh.loc[a]), nb))
-              {
-                o[0] = f0;
-                o[1] = f1;
-                o[2] = f2;
-              }
-              else
-              {
-                o[0] += f0;
-                o[1] += f1;
-                o[2] += f2;
-              }
-            }
-          }
-          else if (!A.increc)
-          {
-            double* o = A.rec + ep * kRec + kNpair * 9 + 3 * a;
-            o[0] = f0;
-            o[1] = f1;
-            o[2] = f2;
-          }
-          else if (k >= 0)
-          {
-            double* o = A.rec + int64_t(k) * kIncRec + 243;
-            o[0] = f0;
-            o[1] = f1;
-            o[2] = f2;
-          }
-        }
+        emit_f(ep, pb, pi, nb);
       }
       H27_STAMP(5);
     }
@@ -615,7 +622,7 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
         const double ma = (va && vk) ? 1.0 : 0.0, mb = (vb && vk) ? 1.0 : 0.0;
         const int wr0 = kc == 0 ? 0 : (kc == 1 ? 3 : 5), wr1 = kc == 0 ? 3 : (kc == 1 ? 1 : 4),
                   wr2 = kc == 0 ? 5 : (kc == 1 ? 4 : 2);  // row kc of the symmetric W, V
-#pragma unroll 3
+#pragma unroll FCG_H27_HUNROLL
         for (int g = 0; g < kNpe; ++g)
         {
           const double* da = sh.dN + 3 * (27 * g + a_c);
