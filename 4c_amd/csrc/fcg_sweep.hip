@@ -704,6 +704,18 @@ __global__ __launch_bounds__(256, KIN ? 1 : FCG_SWEEP_WGS) void sweep_h8_kernel(
               else
                 dst[r * len + qq] += Kb[3 * r + qq];
             }
+#if defined(FCG_PROBE_TH_NOSTORE) || defined(FCG_PROBE_TH_1STORE)
+        if (TH)
+        {
+          // timing probes only (wrong results): no thermal stores / one 8-byte store per block
+#ifdef FCG_PROBE_TH_1STORE
+          A.Ktt[base / 9 + pos / 3] = Tv[0] + Tv[1] + Tv[2] + Tv[3] + Tv[4] + Tv[5] + Tv[6];
+#else
+          if (Tv[0] == 12345.678) A.Ktt[0] = Tv[1];
+#endif
+          return;
+        }
+#endif
         if (TSI)
         {
           // node-consistent block graphs (checked by fcg_tsi_evaluate_fused): the k_ST rows of the
