@@ -117,6 +117,124 @@ std::vector<int64_t> morton_order(const std::vector<uint64_t>& key)
   return ord;
 }
 
+// Lattice positions (ex, ey, ez) of a hex8 mesh whose elements stack like a GridGenerator box,
+// found from the connectivity alone (an input-file mesh without the fcg_desc.ele_ijk hint):
+// neighbours share whole faces in 4C node order (+x: nodes 1 2 6 5 of an element are 0 3 7 4 of
+// the neighbour; +y: 3 2 6 7 -> 0 1 5 4; +z: 4 5 6 7 -> 0 1 2 3), faces matched by sorting, the
+// positions spread from element 0 over the face graph.  false (and why) when the elements are
+// not such a lattice -- any other orientation, a disconnected element set, two elements at one
+// position; build_structured_plan verifies the node positions against it as for a given hint.
+bool detect_lattice_hex8(const fcg_desc* d, std::vector<int32_t>& ijk, std::string& why)
+{
+  const int64_t n = d->n_ele;
+  if (d->celltype != FCG_HEX8 || n == 0 || n >= (int64_t(1) << 31))
+  {
+    why = "not a hex8 mesh";
+    return false;
+  }
+  static const int kHi[3][4] = {{1, 2, 6, 5}, {3, 2, 6, 7}, {4, 5, 6, 7}};
+  static const int kLo[3][4] = {{0, 3, 7, 4}, {0, 1, 5, 4}, {0, 1, 2, 3}};
+  struct Face {
+    int32_t v[4];
+    int32_t e;
+    bool operator<(const Face& o) const
+    {
+      for (int k = 0; k < 4; ++k)
+        if (v[k] != o.v[k]) return v[k] < o.v[k];
+      return e < o.e;
+    }
+  };
+  // nb[6 e + 2 dir + 0/1]: the neighbour below / above along dir, -1 = none
+  std::vector<int32_t> nb(6 * n, -1);
+  std::vector<Face> hi(n), lo(n);
+  for (int dir = 0; dir < 3; ++dir)
+  {
+    parallel_for(n, [&](int64_t e) {
+      const int32_t* en = d->ele_nodes + 8 * e;
+      for (int k = 0; k < 4; ++k)
+      {
+        hi[e].v[k] = en[kHi[dir][k]];
+        lo[e].v[k] = en[kLo[dir][k]];
+      }
+      hi[e].e = lo[e].e = int32_t(e);
+    });
+    std::sort(hi.begin(), hi.end());
+    std::sort(lo.begin(), lo.end());
+    auto same = [](const Face& a, const Face& b) { return std::memcmp(a.v, b.v, sizeof(a.v)) == 0; };
+    for (size_t i = 1; i < hi.size(); ++i)
+      if (same(hi[i], hi[i - 1]) || same(lo[i], lo[i - 1]))
+      {
+        why = "two elements share an oriented face";
+        return false;
+      }
+    for (size_t i = 0, j = 0; i < hi.size() && j < lo.size();)
+    {
+      if (same(hi[i], lo[j]))
+      {
+        nb[6 * int64_t(hi[i].e) + 2 * dir + 1] = lo[j].e;
+        nb[6 * int64_t(lo[j].e) + 2 * dir + 0] = hi[i].e;
+        ++i;
+        ++j;
+      }
+      else if (std::lexicographical_compare(hi[i].v, hi[i].v + 4, lo[j].v, lo[j].v + 4))
+        ++i;
+      else
+        ++j;
+    }
+  }
+  const int64_t unset = INT64_MIN;
+  std::vector<int64_t> pos(3 * n, unset);
+  std::vector<int32_t> stack{0};
+  pos[0] = pos[1] = pos[2] = 0;
+  int64_t seen = 1;
+  while (!stack.empty())
+  {
+    const int32_t e = stack.back();
+    stack.pop_back();
+    for (int dir = 0; dir < 3; ++dir)
+      for (int side = 0; side < 2; ++side)
+      {
+        const int32_t f = nb[6 * int64_t(e) + 2 * dir + side];
+        if (f < 0) continue;
+        int64_t want[3] = {pos[3 * e], pos[3 * e + 1], pos[3 * e + 2]};
+        want[dir] += side ? 1 : -1;
+        if (pos[3 * int64_t(f)] == unset)
+        {
+          for (int k = 0; k < 3; ++k) pos[3 * int64_t(f) + k] = want[k];
+          stack.push_back(f);
+          ++seen;
+        }
+        else if (pos[3 * int64_t(f)] != want[0] || pos[3 * int64_t(f) + 1] != want[1] ||
+                 pos[3 * int64_t(f) + 2] != want[2])
+        {
+          why = "face neighbours give inconsistent lattice positions";
+          return false;
+        }
+      }
+  }
+  if (seen != n)
+  {
+    why = "the elements are not one face-connected block";
+    return false;
+  }
+  int64_t mn[3] = {INT64_MAX, INT64_MAX, INT64_MAX};
+  for (int64_t e = 0; e < n; ++e)
+    for (int k = 0; k < 3; ++k) mn[k] = std::min(mn[k], pos[3 * e + k]);
+  ijk.resize(3 * n);
+  for (int64_t e = 0; e < n; ++e)
+    for (int k = 0; k < 3; ++k)
+    {
+      const int64_t v = pos[3 * e + k] - mn[k];
+      if (v >= INT32_MAX)
+      {
+        why = "lattice too large";
+        return false;
+      }
+      ijk[3 * e + k] = int32_t(v);
+    }
+  return true;  // uniqueness of positions and nodes: build_structured_plan's checks
+}
+
 bool build_structured_plan(const fcg_desc* d, const std::vector<int32_t>& rownodes,
     const std::vector<int32_t>& row0, const int32_t* kcol, int cus, StructHost& P, std::string& why)
 {
@@ -742,7 +860,24 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
       cus = prop.multiProcessorCount;
     else
       (void)hipGetLastError();
-    structured = build_structured_plan(d, rownodes, row0, kcol, cus, sp, why);
+    // an input-file hex8 mesh without the hint: look for the lattice in the connectivity
+    // (FCG_DETECT_LATTICE=0 turns this off)
+    static const bool detect = [] {
+      const char* e = std::getenv("FCG_DETECT_LATTICE");
+      return !(e && e[0] == '0');
+    }();
+    std::vector<int32_t> found_ijk;
+    fcg_desc dl;
+    if (!d->ele_ijk && d->celltype == FCG_HEX8 && detect && detect_lattice_hex8(d, found_ijk, why))
+    {
+      dl = *d;
+      dl.ele_ijk = found_ijk.data();
+      structured = build_structured_plan(&dl, rownodes, row0, kcol, cus, sp, why);
+    }
+    else if (d->ele_ijk)
+      structured = build_structured_plan(d, rownodes, row0, kcol, cus, sp, why);
+    else if (why.empty())
+      why = "no lattice hint";
     if (!structured && d->path == FCG_PATH_STRUCTURED && d->celltype == FCG_HEX8)
     {
       set_create_error("structured path requested but the lattice hint does not verify: " + why);

@@ -273,7 +273,7 @@ def newton_secondary(n, timeout_s=900):
 
 
 def amg_newton_secondary(n, timeout_s=600):
-    """The 1M-hex8 box renumbered as an input-file mesh (no lattice: the gather path), x- clamped,
+    """The 1M-hex8 box renumbered as an input-file mesh (no lattice hint), x- clamped,
     tip load, StVK TotLag full Newton with the native smoothed-aggregation AMG object
     (fcg_amg_create / fcg_amg_solve) -- the solve 4C's MueLu does on meshes without a box --
     run by tools/newton_bench.py in a child process."""
@@ -627,9 +627,11 @@ def host_secondary(dev, n, steps):
 
 def gather_secondary(dev, n, steps):
     """Config 2's element on an unstructured mesh: the n^3 hex8 box renumbered like an input-file
-    mesh (random node and element numbering, no lattice hint: fcg.Discretization.renumbered), so
-    that AUTO takes the node-row gather path (FCG_PATH_GATHER); linear and TotLag K + r, kernel
-    time by hipEvents, HBM fraction by SURVEY §8d's bytes per element."""
+    mesh (random node and element numbering, no lattice hint: fcg.Discretization.renumbered) on
+    the node-row gather path (FCG_PATH_GATHER, what any mesh without a lattice takes); linear and
+    TotLag K + r, kernel time by hipEvents, HBM fraction by SURVEY §8d's bytes per element.  The
+    "auto" entry: the same mesh under FCG_PATH_AUTO, where fcg_create finds the lattice in the
+    connectivity and takes the row-block sweep."""
     try:
         box = fcg.BoxMesh(fcg.HEX8, (n, n, n), jitter=0.1, seed=20251015)
         dis = fcg.Discretization.renumbered(box, seed=1)
@@ -638,8 +640,11 @@ def gather_secondary(dev, n, steps):
                "baseline_config": "BASELINE.json configs[1] element on a mesh without lattice",
                "unit": "element-evaluations/s", "elements": dis.n_ele, "nnz": dis.nnz}
         rng = np.random.default_rng(3)
-        for name, kinem, amp in (("linear", fcg.LINEAR, 1e-3), ("totlag", fcg.TOTLAG, 5e-2)):
-            ev = fcg.Evaluator(dis, kinematics=kinem, youngs=210.0, poisson=0.3, device=dev.index)
+        for name, kinem, amp, path in (("linear", fcg.LINEAR, 1e-3, fcg.PATH_GATHER),
+                                       ("totlag", fcg.TOTLAG, 5e-2, fcg.PATH_GATHER),
+                                       ("auto_linear", fcg.LINEAR, 1e-3, fcg.PATH_AUTO)):
+            ev = fcg.Evaluator(dis, kinematics=kinem, youngs=210.0, poisson=0.3, device=dev.index,
+                               path=path)
             u = torch.from_numpy(rng.standard_normal(dis.n_cols) * amp).to(dev)
             f = torch.zeros(dis.n_rows, dtype=torch.float64, device=dev)
             K = torch.zeros(dis.nnz, dtype=torch.float64, device=dev)
@@ -659,7 +664,8 @@ def gather_secondary(dev, n, steps):
             ms_kern = float(np.mean(ts))
             gbs = ALG_BYTES_PER_ELE * dis.n_ele / (ms_kern * 1e-3) / 1e9
             out[name] = {"value": dis.n_ele / wall, "ms_per_step": 1e3 * wall, "ms_kernel": ms_kern,
-                         "path": {fcg.PATH_GATHER: "gather", fcg.PATH_GENERAL: "general"}.get(
+                         "path": {fcg.PATH_GATHER: "gather", fcg.PATH_GENERAL: "general",
+                                  fcg.PATH_STRUCTURED: "structured (lattice found in the connectivity)"}.get(
                              int(ev.info.path), int(ev.info.path)),
                          "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS,
                                       "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS}}

@@ -103,14 +103,18 @@ typedef struct fcg_desc {
 enum fcg_material { FCG_MAT_STVK = 0, FCG_MAT_ELASTHYPER_COUPNEOHOOKE = 1 };
 
 /* Evaluation paths.  AUTO picks the hex8 row-block sweep (FCG_PATH_STRUCTURED) when the lattice
- * hint verifies; other hex8 StVK meshes take FCG_PATH_GATHER (one wavefront per owned row node
+ * hint verifies -- or, without a hint, when fcg_create finds the lattice in the connectivity
+ * (elements stacked like a GridGenerator box, faces shared in 4C node order; FCG_DETECT_LATTICE=0
+ * in the environment turns the search off); other hex8 StVK meshes take FCG_PATH_GATHER (one wavefront per owned row node
  * recomputes the node's elements and writes its 3 CSR rows once: no scratch, no atomics, any
  * conforming mesh with <= 27 neighbour nodes per node); everything else GENERAL (element kernel +
  * incidence scratch + row assembly).  STRUCTURED requests the lattice path and fails fcg_create with
  * FCG_ERR_ARG when the hint does not verify: for hex8 the fused row-block sweep, for hex27 the
- * colour-ordered direct assembly (reported as FCG_PATH_COLORED: eight launches, one per
- * element-parity colour; each element adds its blocks straight into the CSR rows, the first
- * colour to reach a matrix entry writes it -- no scratch records, no atomics, fixed order).
+ * colour-ordered direct assembly (reported as FCG_PATH_COLORED: for StVK four launches of
+ * pencils -- runs of elements along x walked by one workgroup each -- in (y, z)-parity colours,
+ * otherwise eight launches, one per element-parity colour; each element adds its blocks straight
+ * into the CSR rows, the first holder of a matrix entry in that order writes it -- no scratch
+ * records, no atomics, fixed order).
  * COLORED requests the latter explicitly (hex27 only). */
 enum fcg_path { FCG_PATH_AUTO = 0, FCG_PATH_GENERAL = 1, FCG_PATH_STRUCTURED = 2, FCG_PATH_COLORED = 3,
   FCG_PATH_GATHER = 4 };
