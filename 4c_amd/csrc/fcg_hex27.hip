@@ -119,6 +119,7 @@ struct H27Shared {
   uint32_t fmask[2];
   uint8_t pcls[27 * 27];        // pair class of (a, b)
   int bad[2];
+  int32_t nodal[27];            // nodal det J check of the produced element: 0 | 1 (<= 0) | 2 (= 0)
   uint8_t loc[27], latnode[27];
   // views of gpf[b]: T(i, k) at 3i + k, W, V, M symmetric (xx yy zz xy yz zx), R(i, k) at 3i + k
   __device__ double* T(int b) { return gpf[b] + OFF_T; }
@@ -288,6 +289,58 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
   // operations complete in order, so a wait for its own accesses plus a compiler barrier suffice
   auto wave_lds_sync = [&]() { __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
 
+  // 1. J and du/dxi at the Gauss points (task t < 162: g, k, X|u) and the nodal det J check
+  //    (calc_lib.hpp:475-496, t = 162 + node; code into sh.nodal) via the 1D factors: at a node
+  //    they are Kronecker deltas, so J sums the 3 nodes on each parametric line
+  auto s1_task = [&](int t) {
+    if (t < 162)
+    {
+      const int g = t / 6, rem = t - 6 * (t / 6);
+      const int k = rem % 3, sx = rem / 3;
+      const double* src = sx ? sh.U : sh.X;
+      const double* d = sh.dN + 81 * g;
+      double j0 = 0.0, j1 = 0.0, j2 = 0.0;
+#pragma unroll 9
+      for (int c = 0; c < kNpe; ++c)
+      {
+        const double x = src[3 * c + k];
+        j0 += d[3 * c + 0] * x;
+        j1 += d[3 * c + 1] * x;
+        j2 += d[3 * c + 2] * x;
+      }
+      double* dst = (sx ? sh.Gu : sh.J) + 9 * g + 3 * k;
+      dst[0] = j0;
+      dst[1] = j1;
+      dst[2] = j2;
+    }
+    else if (t < 162 + kNpe)
+    {
+      const int g = t - 162;
+      const uint32_t l = sh.loc[g];
+      const int p = l & 3, qq = (l >> 2) & 3, r = l >> 4;
+      double J[9];
+#pragma unroll
+      for (int kk = 0; kk < 9; ++kk) J[kk] = 0.0;
+#pragma unroll
+      for (int m = 0; m < 3; ++m)
+      {
+        const double* x0 = sh.X + 3 * sh.latnode[m + 3 * qq + 9 * r];
+        const double* x1 = sh.X + 3 * sh.latnode[p + 3 * m + 9 * r];
+        const double* x2 = sh.X + 3 * sh.latnode[p + 3 * qq + 9 * m];
+        const double d0 = sh.dLn[3 * p + m], d1 = sh.dLn[3 * qq + m], d2 = sh.dLn[3 * r + m];
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+        {
+          J[3 * c + 0] += d0 * x0[c];
+          J[3 * c + 1] += d1 * x1[c];
+          J[3 * c + 2] += d2 * x2[c];
+        }
+      }
+      const double det = inv3(J);
+      sh.nodal[g] = det == 0.0 ? 2 : (!(det > 0) ? 1 : 0);
+    }
+  };
+
   // f_a = sum_g R_g d_a (add_internal_force_vector, calc_lib.hpp:851-860) of element e from the
   // factor buffer fb, written at once (a skipped element leaves its rows to the error report)
   auto emit_f = [&](int64_t e, int fb, int ib, uint32_t nbv) {
@@ -372,6 +425,14 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
     __syncthreads();
     H27_STAMP(0);
     const bool cons = ec >= 0 && sh.bad[cb] == 0;
+    if (KIN == 0 && ep >= 0)
+    {
+      // linear kinematics: the producer would be the longer side, so stage 1 of ep runs on all
+      // four waves first (wave 3 issues the next element's loads meanwhile)
+      if (wave == 3) load_xu(epp);
+      s1_task(tid);
+      __syncthreads();
+    }
 
     if (wave == 3)
     {
@@ -379,7 +440,7 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
       if (ep >= 0)
       {
         ++st_n;
-        load_xu(epp);  // lands while ep's stages run; stored after stage 1 has read X, u
+        if (KIN == 1) load_xu(epp);  // lands while ep's stages run; stored after stage 1 has read X, u
         if (lane == 0) sh.bad[pb] = 0;
         // pencil output bookkeeping of ep (read by all waves when ep is consumed)
         const uint32_t nb = ASM ? A.ele_nb[ep] : 0u;
@@ -425,61 +486,14 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
           }
         }
 
-        // 1. J and du/dxi at the Gauss points (task t < 162: g, k, X|u) and the nodal det J check
-        //    (calc_lib.hpp:475-496, t = 162 + node) via the 1D factors: at a node they are
-        //    Kronecker deltas, so J sums the 3 nodes on each parametric line
-#pragma unroll 1
-        for (int q = 0; q < 3; ++q)
+        // 1. (TotLag: here, by this wave; linear: by all four waves before the phase barrier)
+        if (KIN == 1)
         {
-          const int t = lane + 64 * q;
-          if (t < 162)
-          {
-            const int g = t / 6, rem = t - 6 * (t / 6);
-            const int k = rem % 3, sx = rem / 3;
-            const double* src = sx ? sh.U : sh.X;
-            const double* d = sh.dN + 81 * g;
-            double j0 = 0.0, j1 = 0.0, j2 = 0.0;
-#pragma unroll 9
-            for (int c = 0; c < kNpe; ++c)
-            {
-              const double x = src[3 * c + k];
-              j0 += d[3 * c + 0] * x;
-              j1 += d[3 * c + 1] * x;
-              j2 += d[3 * c + 2] * x;
-            }
-            double* dst = (sx ? sh.Gu : sh.J) + 9 * g + 3 * k;
-            dst[0] = j0;
-            dst[1] = j1;
-            dst[2] = j2;
-          }
-          else if (t < 162 + kNpe)
-          {
-            const int g = t - 162;
-            const uint32_t l = sh.loc[g];
-            const int p = l & 3, qq = (l >> 2) & 3, r = l >> 4;
-            double J[9];
-#pragma unroll
-            for (int kk = 0; kk < 9; ++kk) J[kk] = 0.0;
-#pragma unroll
-            for (int m = 0; m < 3; ++m)
-            {
-              const double* x0 = sh.X + 3 * sh.latnode[m + 3 * qq + 9 * r];
-              const double* x1 = sh.X + 3 * sh.latnode[p + 3 * m + 9 * r];
-              const double* x2 = sh.X + 3 * sh.latnode[p + 3 * qq + 9 * m];
-              const double d0 = sh.dLn[3 * p + m], d1 = sh.dLn[3 * qq + m], d2 = sh.dLn[3 * r + m];
-#pragma unroll
-              for (int c = 0; c < 3; ++c)
-              {
-                J[3 * c + 0] += d0 * x0[c];
-                J[3 * c + 1] += d1 * x1[c];
-                J[3 * c + 2] += d2 * x2[c];
-              }
-            }
-            const double det = inv3(J);
-            if (det == 0.0) atomicMax(&sh.bad[pb], 2);
-            else if (!(det > 0)) atomicMax(&sh.bad[pb], 1);
-          }
+#pragma unroll 1
+          for (int q = 0; q < 3; ++q) s1_task(lane + 64 * q);
+          wave_lds_sync();
         }
+        if (lane < kNpe && sh.nodal[lane] != 0) atomicMax(&sh.bad[pb], sh.nodal[lane]);
         wave_lds_sync();
 
         // 2. per Gauss point: J^-1, fac, strains, StVK stress and the folded 3 x 3 factors
