@@ -61,7 +61,7 @@ constexpr int64_t kIncRec = 9 * kNpe + 3;  // increc: one owned incidence's 3 x 
 
 __constant__ double c_dN[27 * 27 * 3];  // dN_c,d at Gauss point g: [g][c][d]
 __constant__ double c_w[27];
-__constant__ double c_L1[9], c_dL1[9], c_dLn[9];  // 1D Lagrange factors (fcg_kernels.hip)
+__constant__ double c_dLn[9];  // 1D Lagrange derivatives at the nodes (fcg_kernels.hip)
 __constant__ uint8_t c_loc[27], c_latnode[27];
 
 __device__ inline int pidx(int a, int b)  // a <= b
@@ -109,7 +109,7 @@ struct H27Shared {
   double gpf[2][GPF];           // per-point factors of the produced / consumed element
   double fac[2][27];
   alignas(16) double kimg[kNpair * 9];  // consumed element's blocks a <= b (col-major 3 x 3)
-  double L1[9], dL1[9], dLn[9];
+  double dLn[9];                // 1D Lagrange derivatives at the nodes (nodal det J check)
   int32_t inc[3][27];           // incidence of (e, a), -1 = not owned, by sequence index mod 3
   // pencil output of the consumed element (by sequence parity): CSR offset of row (a, 0), row
   // length, column position of node b in a's rows, first-holder bits of the pair classes
@@ -191,9 +191,6 @@ __device__ inline bool first_holder(int cls, uint32_t nb)
   return first;
 }
 
-#ifndef FCG_H27_LIN_WGS
-#define FCG_H27_LIN_WGS 2
-#endif
 #ifndef FCG_H27_HUNROLL
 #define FCG_H27_HUNROLL 3  // unroll of the consumers' H + geo loop over the Gauss points
 #endif
@@ -217,8 +214,6 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
     }
   if (tid < 9)
   {
-    sh.L1[tid] = c_L1[tid];
-    sh.dL1[tid] = c_dL1[tid];
     sh.dLn[tid] = c_dLn[tid];
   }
   if (tid < 27)
@@ -968,24 +963,15 @@ void upload_h27_tables()
   for (int g = 0; g < 27; ++g) shape_deriv(kHex27, &xi[3 * g], &dN[81 * g]);
   (void)hipMemcpyToSymbol(HIP_SYMBOL(c_dN), dN, sizeof(dN));
   (void)hipMemcpyToSymbol(HIP_SYMBOL(c_w), w, sizeof(w));
-  // 1D quadratic Lagrange factors as fcg_kernels.hip: L_i'(x_p) at the nodes x = -1, 0, 1
-  double dLn[9], L1[9], dL1[9];
-  const double xs[3] = {xi[3 * 0], xi[3 * 8], xi[3 * 1]};
+  // 1D quadratic Lagrange derivatives L_i'(x_p) at the nodes x = -1, 0, 1 (as fcg_kernels.hip)
+  double dLn[9];
   for (int p = 0; p < 3; ++p)
   {
-    const double r = xs[p], t = double(p - 1);
-    L1[3 * p + 0] = 0.5 * r * (r - 1.0);
-    L1[3 * p + 1] = 1.0 - r * r;
-    L1[3 * p + 2] = 0.5 * r * (r + 1.0);
-    dL1[3 * p + 0] = r - 0.5;
-    dL1[3 * p + 1] = -2.0 * r;
-    dL1[3 * p + 2] = r + 0.5;
+    const double t = double(p - 1);
     dLn[3 * p + 0] = t - 0.5;
     dLn[3 * p + 1] = -2.0 * t;
     dLn[3 * p + 2] = t + 0.5;
   }
-  (void)hipMemcpyToSymbol(HIP_SYMBOL(c_L1), L1, sizeof(L1));
-  (void)hipMemcpyToSymbol(HIP_SYMBOL(c_dL1), dL1, sizeof(dL1));
   (void)hipMemcpyToSymbol(HIP_SYMBOL(c_dLn), dLn, sizeof(dLn));
   uint8_t loc[27], latnode[27];
   for (int a = 0; a < 27; ++a)
