@@ -357,6 +357,16 @@ bool build_structured_plan(const fcg_desc* d, const std::vector<int32_t>& rownod
       if (x < 0 || x >= NXn || y < 0 || y >= NYn || z < 0 || z >= NZn) continue;
       const int32_t m = node_at[(z * NYn + y) * NXn + x];
       if (m < 0) continue;
+      // coupled only through an element holding both nodes (meshes with holes: a lattice
+      // neighbour across a missing element is no column of the row, and its position stays absent)
+      bool coupled = false;
+      for (int64_t ez = std::max(k, z) - 1; ez <= std::min(k, z) && !coupled; ++ez)
+        for (int64_t ey = std::max(jj, y) - 1; ey <= std::min(jj, y) && !coupled; ++ey)
+          for (int64_t ex = std::max(i, x) - 1; ex <= std::min(i, x) && !coupled; ++ex)
+            if (ex >= 0 && ey >= 0 && ez >= 0 && ex < EX && ey < EY && ez < EZ &&
+                P.elem_at[(ez * EY + ey) * EX + ex] >= 0)
+              coupled = true;
+      if (!coupled) continue;
       const int32_t c = kcol[m];
       const int32_t* it = std::lower_bound(cols, cols + len, c);
       const int64_t pos = it - cols;

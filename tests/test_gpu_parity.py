@@ -403,6 +403,38 @@ def test_renumbered_box_takes_the_sweep_by_lattice_detection(kinem):
     assert ev.info.path == fcg.PATH_GATHER
 
 
+def test_lattice_detection_with_holes_matches_oracle():
+    """Lattice detection on an input-file mesh with elements missing (a hole through the box and an
+    L-shaped notch): the found lattice has empty positions, which the row-block sweep treats like
+    a rank's missing neighbours -- same K, f as the oracle."""
+    _dev()
+    box = fcg.BoxMesh(fcg.HEX8, (6, 5, 4), jitter=0.1, seed=21)
+    keep = np.ones(box.n_ele, dtype=bool)
+    ijk = box.ele_ijk
+    keep &= ~((ijk[:, 0] == 2) & (ijk[:, 1] == 2))                    # a hole along z
+    keep &= ~((ijk[:, 0] >= 4) & (ijk[:, 1] >= 3) & (ijk[:, 2] >= 2))  # a notch at a corner
+    en = box.ele_nodes[keep]
+    used = np.unique(en)
+    renum = np.full(box.n_node, -1, dtype=np.int64)
+    renum[used] = np.random.default_rng(4).permutation(len(used))
+    X = np.empty((len(used), 3))
+    X[renum[used]] = box.node_x[used]
+    en = renum[en][np.random.default_rng(5).permutation(len(en))]
+    dis = fcg.Discretization.from_elements(fcg.HEX8, en, X)
+    u = np.random.default_rng(6).standard_normal(dis.n_cols) * 1e-3
+    mesh_like = type("M", (), {})()
+    mesh_like.row_gid = mesh_like.col_gid = np.arange(dis.n_cols, dtype=np.int32)
+    mesh_like.nnz, mesh_like.n_rows, mesh_like.rowptr, mesh_like.col_lid = dis.nnz, dis.n_rows, dis.rowptr, dis.col_lid
+    mesh_like.celltype, mesh_like.n_ele, mesh_like.ele_nodes = fcg.HEX8, dis.n_ele, dis.ele_nodes
+    mesh_like.n_node, mesh_like.node_x, mesh_like.node_dof_row = dis.n_node, dis.node_x, dis.node_dof_row
+    mesh_like.node_gid = np.arange(dis.n_node, dtype=np.int64)
+    err, _, Kr, fr = oracle_evaluate(mesh_like, fcg.LINEAR, E, NU, u)
+    assert err == 0
+    Ks, fs, ev = _run_gpu(dis, fcg.LINEAR, u, path=fcg.PATH_AUTO)
+    assert ev.info.path == fcg.PATH_STRUCTURED
+    _check(Ks, fs, Kr, fr)
+
+
 @pytest.mark.parametrize("kinem", [fcg.LINEAR, fcg.TOTLAG])
 @pytest.mark.parametrize("iv,dup", [((6, 5, 4), 0), ((3, 3, 2), 5), ((1, 1, 1), 0)])
 def test_gather_path_unstructured_matches_oracle(kinem, iv, dup):
