@@ -118,120 +118,232 @@ std::vector<int64_t> morton_order(const std::vector<uint64_t>& key)
 }
 
 // Lattice positions (ex, ey, ez) of a hex8 mesh whose elements stack like a GridGenerator box,
-// found from the connectivity alone (an input-file mesh without the fcg_desc.ele_ijk hint):
-// neighbours share whole faces in 4C node order (+x: nodes 1 2 6 5 of an element are 0 3 7 4 of
-// the neighbour; +y: 3 2 6 7 -> 0 1 5 4; +z: 4 5 6 7 -> 0 1 2 3), faces matched by sorting, the
-// positions spread from element 0 over the face graph.  false (and why) when the elements are
-// not such a lattice -- any other orientation, a disconnected element set, two elements at one
-// position; build_structured_plan verifies the node positions against it as for a given hint.
-bool detect_lattice_hex8(const fcg_desc* d, std::vector<int32_t>& ijk, std::string& why)
+// found from the connectivity alone (an input-file mesh without the fcg_desc.ele_ijk hint), with
+// every element's own local numbering allowed to be any proper rotation of 4C's (mesh generators
+// rotate element frames): element 0's local frame fixes the lattice axes; across every shared face
+// (matched by sorting the sorted node quadruples) the neighbour's other four nodes sit one step
+// along the face normal from their edge partners on the face; then every element must occupy one
+// unit cell, with a right-handed local frame.  Returns the cells and the connectivity in 4C's
+// local order for those cells (canon, what the row-block sweep reads); false (and why) otherwise
+// -- build_structured_plan verifies the result like a given hint.
+bool detect_lattice_hex8(const fcg_desc* d, std::vector<int32_t>& ijk, std::vector<int32_t>& canon,
+    std::string& why)
 {
   const int64_t n = d->n_ele;
-  if (d->celltype != FCG_HEX8 || n == 0 || n >= (int64_t(1) << 31))
+  if (d->celltype != FCG_HEX8 || n == 0 || n >= (int64_t(1) << 31) / 6)
   {
     why = "not a hex8 mesh";
     return false;
   }
-  static const int kHi[3][4] = {{1, 2, 6, 5}, {3, 2, 6, 7}, {4, 5, 6, 7}};
-  static const int kLo[3][4] = {{0, 3, 7, 4}, {0, 1, 5, 4}, {0, 1, 2, 3}};
+  // local faces (4C hex8 order) and, per local node, its three edge partners
+  static const int kFace[6][4] = {{0, 1, 2, 3}, {4, 5, 6, 7}, {0, 1, 5, 4}, {3, 2, 6, 7},
+      {0, 3, 7, 4}, {1, 2, 6, 5}};
+  int partner[8][3];
+  for (int u = 0; u < 8; ++u)
+  {
+    int c = 0;
+    for (int v = 0; v < 8; ++v)
+    {
+      int diff = 0;
+      for (int k = 0; k < 3; ++k) diff += kOff8[u][k] != kOff8[v][k];
+      if (diff == 1) partner[u][c++] = v;
+    }
+  }
   struct Face {
     int32_t v[4];
-    int32_t e;
+    int32_t ef;  // element * 6 + local face
     bool operator<(const Face& o) const
     {
       for (int k = 0; k < 4; ++k)
         if (v[k] != o.v[k]) return v[k] < o.v[k];
-      return e < o.e;
+      return ef < o.ef;
     }
   };
-  // nb[6 e + 2 dir + 0/1]: the neighbour below / above along dir, -1 = none
-  std::vector<int32_t> nb(6 * n, -1);
-  std::vector<Face> hi(n), lo(n);
-  for (int dir = 0; dir < 3; ++dir)
-  {
-    parallel_for(n, [&](int64_t e) {
-      const int32_t* en = d->ele_nodes + 8 * e;
-      for (int k = 0; k < 4; ++k)
+  std::vector<Face> faces(6 * n);
+  parallel_for(n, [&](int64_t e) {
+    const int32_t* en = d->ele_nodes + 8 * e;
+    for (int f = 0; f < 6; ++f)
+    {
+      Face& F = faces[6 * e + f];
+      for (int k = 0; k < 4; ++k) F.v[k] = en[kFace[f][k]];
+      std::sort(F.v, F.v + 4);
+      F.ef = int32_t(6 * e + f);
+    }
+  });
+  std::sort(faces.begin(), faces.end());
+  std::vector<int32_t> nbr(6 * n, -1);  // element across local face f of e
+  for (size_t i = 0; i + 1 < faces.size(); ++i)
+    if (std::memcmp(faces[i].v, faces[i + 1].v, sizeof(faces[i].v)) == 0)
+    {
+      if (i + 2 < faces.size() && std::memcmp(faces[i].v, faces[i + 2].v, sizeof(faces[i].v)) == 0)
       {
-        hi[e].v[k] = en[kHi[dir][k]];
-        lo[e].v[k] = en[kLo[dir][k]];
-      }
-      hi[e].e = lo[e].e = int32_t(e);
-    });
-    std::sort(hi.begin(), hi.end());
-    std::sort(lo.begin(), lo.end());
-    auto same = [](const Face& a, const Face& b) { return std::memcmp(a.v, b.v, sizeof(a.v)) == 0; };
-    for (size_t i = 1; i < hi.size(); ++i)
-      if (same(hi[i], hi[i - 1]) || same(lo[i], lo[i - 1]))
-      {
-        why = "two elements share an oriented face";
+        why = "a face is shared by more than two elements";
         return false;
       }
-    for (size_t i = 0, j = 0; i < hi.size() && j < lo.size();)
+      nbr[faces[i].ef] = faces[i + 1].ef / 6;
+      nbr[faces[i + 1].ef] = faces[i].ef / 6;
+      ++i;
+    }
+  std::vector<Face>().swap(faces);
+
+  // node positions spread from element 0 (its local frame = the lattice axes)
+  const int64_t unset = INT64_MIN;
+  std::vector<int64_t> pos(3 * int64_t(d->n_node), unset);
+  auto set_pos = [&](int32_t node, const int64_t* p) -> bool {
+    int64_t* q = &pos[3 * int64_t(node)];
+    if (q[0] == unset)
     {
-      if (same(hi[i], lo[j]))
+      q[0] = p[0];
+      q[1] = p[1];
+      q[2] = p[2];
+      return true;
+    }
+    return q[0] == p[0] && q[1] == p[1] && q[2] == p[2];
+  };
+  std::vector<uint8_t> done(n, 0);
+  {
+    const int32_t* en = d->ele_nodes;
+    for (int a = 0; a < 8; ++a)
+    {
+      const int64_t p[3] = {kOff8[a][0], kOff8[a][1], kOff8[a][2]};
+      if (!set_pos(en[a], p))
       {
-        nb[6 * int64_t(hi[i].e) + 2 * dir + 1] = lo[j].e;
-        nb[6 * int64_t(lo[j].e) + 2 * dir + 0] = hi[i].e;
-        ++i;
-        ++j;
+        why = "an element repeats a node";
+        return false;
       }
-      else if (std::lexicographical_compare(hi[i].v, hi[i].v + 4, lo[j].v, lo[j].v + 4))
-        ++i;
-      else
-        ++j;
     }
   }
-  const int64_t unset = INT64_MIN;
-  std::vector<int64_t> pos(3 * n, unset);
   std::vector<int32_t> stack{0};
-  pos[0] = pos[1] = pos[2] = 0;
+  done[0] = 1;
   int64_t seen = 1;
   while (!stack.empty())
   {
     const int32_t e = stack.back();
     stack.pop_back();
-    for (int dir = 0; dir < 3; ++dir)
-      for (int side = 0; side < 2; ++side)
+    const int32_t* en = d->ele_nodes + 8 * int64_t(e);
+    for (int f = 0; f < 6; ++f)
+    {
+      const int32_t g = nbr[6 * int64_t(e) + f];
+      if (g < 0) continue;
+      // the face normal (out of e, into g): the coordinate the face's nodes share, away from
+      // e's other nodes
+      const int32_t* fn = en;
+      int axis = -1;
+      int64_t sgn = 0;
+      const int64_t* p0 = &pos[3 * int64_t(fn[kFace[f][0]])];
+      for (int k = 0; k < 3 && axis < 0; ++k)
       {
-        const int32_t f = nb[6 * int64_t(e) + 2 * dir + side];
-        if (f < 0) continue;
-        int64_t want[3] = {pos[3 * e], pos[3 * e + 1], pos[3 * e + 2]};
-        want[dir] += side ? 1 : -1;
-        if (pos[3 * int64_t(f)] == unset)
+        bool same = true;
+        for (int q = 1; q < 4; ++q) same = same && pos[3 * int64_t(fn[kFace[f][q]]) + k] == p0[k];
+        if (same) axis = k;
+      }
+      if (axis < 0)
+      {
+        why = "an element is not a lattice cell";
+        return false;
+      }
+      for (int a = 0; a < 8; ++a)
+      {
+        const int64_t c = pos[3 * int64_t(en[a]) + axis];
+        if (c != p0[axis]) sgn = p0[axis] > c ? 1 : -1;
+      }
+      // g's nodes off the face: one step along the normal from their edge partner on the face
+      const int32_t* gn = d->ele_nodes + 8 * int64_t(g);
+      const int32_t sh[4] = {en[kFace[f][0]], en[kFace[f][1]], en[kFace[f][2]], en[kFace[f][3]]};
+      auto on_face = [&](int32_t node) { return node == sh[0] || node == sh[1] || node == sh[2] || node == sh[3]; };
+      int placed = 0;
+      for (int u = 0; u < 8; ++u)
+      {
+        if (!on_face(gn[u])) continue;
+        for (int j = 0; j < 3; ++j)
         {
-          for (int k = 0; k < 3; ++k) pos[3 * int64_t(f) + k] = want[k];
-          stack.push_back(f);
-          ++seen;
-        }
-        else if (pos[3 * int64_t(f)] != want[0] || pos[3 * int64_t(f) + 1] != want[1] ||
-                 pos[3 * int64_t(f) + 2] != want[2])
-        {
-          why = "face neighbours give inconsistent lattice positions";
-          return false;
+          const int32_t m = gn[partner[u][j]];
+          if (on_face(m)) continue;
+          int64_t p[3] = {pos[3 * int64_t(gn[u])], pos[3 * int64_t(gn[u]) + 1], pos[3 * int64_t(gn[u]) + 2]};
+          p[axis] += sgn;
+          if (!set_pos(m, p))
+          {
+            why = "face neighbours give inconsistent lattice positions";
+            return false;
+          }
+          ++placed;
         }
       }
+      if (placed != 4)
+      {
+        why = "an element is not a lattice cell";
+        return false;
+      }
+      if (!done[g])
+      {
+        done[g] = 1;
+        stack.push_back(g);
+        ++seen;
+      }
+    }
   }
   if (seen != n)
   {
     why = "the elements are not one face-connected block";
     return false;
   }
+  // every element one unit cell with a right-handed local frame; cells and 4C-order connectivity
   int64_t mn[3] = {INT64_MAX, INT64_MAX, INT64_MAX};
-  for (int64_t e = 0; e < n; ++e)
-    for (int k = 0; k < 3; ++k) mn[k] = std::min(mn[k], pos[3 * e + k]);
-  ijk.resize(3 * n);
-  for (int64_t e = 0; e < n; ++e)
+  for (int64_t nd = 0; nd < d->n_node; ++nd)
+    if (pos[3 * nd] != unset)
+      for (int k = 0; k < 3; ++k) mn[k] = std::min(mn[k], pos[3 * nd + k]);
+  ijk.assign(3 * n, 0);
+  canon.assign(8 * n, -1);
+  std::atomic<int> bad{0};
+  parallel_for(n, [&](int64_t e) {
+    const int32_t* en = d->ele_nodes + 8 * e;
+    int64_t c[3] = {INT64_MAX, INT64_MAX, INT64_MAX};
+    for (int a = 0; a < 8; ++a)
+      for (int k = 0; k < 3; ++k) c[k] = std::min(c[k], pos[3 * int64_t(en[a]) + k]);
+    int32_t* out = &canon[8 * e];
+    for (int a = 0; a < 8; ++a)
+    {
+      int off[3], slot = -1;
+      for (int k = 0; k < 3; ++k) off[k] = int(pos[3 * int64_t(en[a]) + k] - c[k]);
+      for (int b = 0; b < 8; ++b)
+        if (off[0] == kOff8[b][0] && off[1] == kOff8[b][1] && off[2] == kOff8[b][2]) slot = b;
+      if (slot < 0 || out[slot] != -1)
+      {
+        bad = 1;
+        return;
+      }
+      out[slot] = en[a];
+    }
+    // handedness of the local frame: local x, y, z axes (nodes 1, 3, 4 from node 0)
+    int64_t ax[3][3];
+    const int idx[3] = {1, 3, 4};
+    for (int q = 0; q < 3; ++q)
+      for (int k = 0; k < 3; ++k) ax[q][k] = pos[3 * int64_t(en[idx[q]]) + k] - pos[3 * int64_t(en[0]) + k];
+    const int64_t det = ax[0][0] * (ax[1][1] * ax[2][2] - ax[1][2] * ax[2][1]) -
+                        ax[0][1] * (ax[1][0] * ax[2][2] - ax[1][2] * ax[2][0]) +
+                        ax[0][2] * (ax[1][0] * ax[2][1] - ax[1][1] * ax[2][0]);
+    if (det != 1)
+    {
+      bad = 2;
+      return;
+    }
     for (int k = 0; k < 3; ++k)
     {
-      const int64_t v = pos[3 * e + k] - mn[k];
+      const int64_t v = c[k] - mn[k];
       if (v >= INT32_MAX)
       {
-        why = "lattice too large";
-        return false;
+        bad = 1;
+        return;
       }
       ijk[3 * e + k] = int32_t(v);
     }
+  });
+  if (bad != 0)
+  {
+    why = bad == 2 ? "an element's local frame is mirrored against the lattice"
+                   : "an element is not a lattice cell";
+    return false;
+  }
   return true;  // uniqueness of positions and nodes: build_structured_plan's checks
 }
 
@@ -876,12 +988,16 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
       const char* e = std::getenv("FCG_DETECT_LATTICE");
       return !(e && e[0] == '0');
     }();
-    std::vector<int32_t> found_ijk;
+    std::vector<int32_t> found_ijk, found_nodes;
     fcg_desc dl;
-    if (!d->ele_ijk && d->celltype == FCG_HEX8 && detect && detect_lattice_hex8(d, found_ijk, why))
+    if (!d->ele_ijk && d->celltype == FCG_HEX8 && detect &&
+        detect_lattice_hex8(d, found_ijk, found_nodes, why))
     {
+      // the sweep reads the cells and the nodes in 4C's local order for them (element frames of
+      // an input file may be any rotation of it; K and f do not depend on the local numbering)
       dl = *d;
       dl.ele_ijk = found_ijk.data();
+      dl.ele_nodes = found_nodes.data();
       structured = build_structured_plan(&dl, rownodes, row0, kcol, cus, sp, why);
     }
     else if (d->ele_ijk)

@@ -1246,7 +1246,10 @@ struct AssembleArgs {
 template <bool WANT_K, bool OVERWRITE>
 __global__ __launch_bounds__(64) void assemble27_kernel(AssembleArgs A)
 {
-  constexpr int NPE = 27, REC = 9 * NPE + 3, NB = 2;
+#ifndef FCG_A27_NB
+#define FCG_A27_NB 2
+#endif
+  constexpr int NPE = 27, REC = 9 * NPE + 3, NB = FCG_A27_NB;
   constexpr int NV2 = 2;  // double2 pieces per lane and record: 122 pieces of the 243 entries
   __shared__ double acc[WANT_K ? 3 * 375 : 1];
   const int lane = threadIdx.x;

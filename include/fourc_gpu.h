@@ -104,7 +104,8 @@ enum fcg_material { FCG_MAT_STVK = 0, FCG_MAT_ELASTHYPER_COUPNEOHOOKE = 1 };
 
 /* Evaluation paths.  AUTO picks the hex8 row-block sweep (FCG_PATH_STRUCTURED) when the lattice
  * hint verifies -- or, without a hint, when fcg_create finds the lattice in the connectivity
- * (elements stacked like a GridGenerator box, faces shared in 4C node order; FCG_DETECT_LATTICE=0
+ * (elements stacked like a GridGenerator box, each element's local numbering any proper rotation
+ * of 4C's -- a mirrored element frame is no lattice; FCG_DETECT_LATTICE=0
  * in the environment turns the search off); other hex8 StVK meshes take FCG_PATH_GATHER (one wavefront per owned row node
  * recomputes the node's elements and writes its 3 CSR rows once: no scratch, no atomics, any
  * conforming mesh with <= 27 neighbour nodes per node); everything else GENERAL (element kernel +

@@ -374,7 +374,8 @@ def _scrambled_hex8(iv, seed, duplicate=0):
 def test_renumbered_box_takes_the_sweep_by_lattice_detection(kinem):
     """An input-file-numbered box (random node and element order, no lattice hint): AUTO finds the
     lattice in the connectivity and takes the row-block sweep -- same K, f as the oracle and as the
-    gather path on the same mesh; rotating one element's local numbering keeps it on the gather."""
+    gather path on the same mesh; with elements' local frames rotated (4C's numbering turned about
+    a local axis) the lattice is still found and K, f are unchanged."""
     _dev()
     box = fcg.BoxMesh(fcg.HEX8, (7, 6, 5), jitter=0.1, seed=12)
     dis = fcg.Discretization.renumbered(box, seed=3)
@@ -397,10 +398,13 @@ def test_renumbered_box_takes_the_sweep_by_lattice_detection(kinem):
     en = dis.ele_nodes.copy()
     en[0, :4] = np.roll(en[0, :4], 1)
     en[0, 4:] = np.roll(en[0, 4:], 1)
+    en[5] = en[5][[1, 5, 6, 2, 0, 4, 7, 3]]
+    en[9] = en[9][[4, 7, 6, 5, 0, 3, 2, 1]]
     rot = fcg.Discretization(fcg.HEX8, en, dis.node_x, dis.node_dof_col, dis.node_dof_row,
                              dis.rowptr, dis.col_lid)
-    _, _, ev = _run_gpu(rot, kinem, u, path=fcg.PATH_AUTO)
-    assert ev.info.path == fcg.PATH_GATHER
+    Kt, ft, ev = _run_gpu(rot, kinem, u, path=fcg.PATH_AUTO)
+    assert ev.info.path == fcg.PATH_STRUCTURED
+    _check(Kt, ft, Kr, fr)
 
 
 def test_lattice_detection_with_holes_matches_oracle():
@@ -453,9 +457,10 @@ def test_gather_path_unstructured_matches_oracle(kinem, iv, dup):
     assert err == 0
     for path in (fcg.PATH_AUTO, fcg.PATH_GATHER, fcg.PATH_GENERAL):
         Kg, fg, ev = _run_gpu(dis, kinem, u, path=path)
-        want = fcg.PATH_GENERAL if path == fcg.PATH_GENERAL else fcg.PATH_GATHER
-        # a single element is trivially a lattice (its rotation is its own frame)
-        assert ev.info.path == want or (path == fcg.PATH_AUTO and dis.n_ele == 1)
+        want = {fcg.PATH_GENERAL: fcg.PATH_GENERAL, fcg.PATH_GATHER: fcg.PATH_GATHER,
+                # rotated element frames still stack as a lattice; repeated elements do not
+                fcg.PATH_AUTO: fcg.PATH_GATHER if dup else fcg.PATH_STRUCTURED}[path]
+        assert ev.info.path == want
         _check(Kg, fg, Kr, fr)
     _, fi, _ = _run_gpu(dis, kinem, u, action=fcg.CALC_INTERNALFORCE, path=fcg.PATH_GATHER)
     assert rel_err(fi, fr) <= 1e-10

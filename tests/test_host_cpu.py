@@ -159,26 +159,36 @@ def test_structured_hint_is_verified_before_device_work(celltype):
 
 def test_lattice_detected_from_connectivity():
     """An input-file hex8 mesh without the lattice hint: fcg_create finds the lattice in the
-    connectivity (faces shared in 4C node order) when the elements stack like a box, and verifies it
-    like a given hint (a renumbered box passes and then needs the device); elements rotated about
-    their local zeta axis are no such lattice, so PATH_STRUCTURED is refused on the host."""
+    connectivity (shared faces, any proper rotation of an element's local numbering) when the
+    elements stack like a box, and verifies it like a given hint (a renumbered box, or one with an
+    element's local frame rotated, passes and then needs the device); an element whose local frame
+    is mirrored is no such lattice, so PATH_STRUCTURED is refused on the host."""
     import torch
     if torch.cuda.is_available():
         pytest.skip("GPU present: covered by the gpu tests")
     box = fcg.BoxMesh(fcg.HEX8, (5, 4, 3), jitter=0.1, seed=4)
     dis = fcg.Discretization.renumbered(box, seed=2)
     assert dis.ele_ijk is None
+
+    def relabel(en):
+        return fcg.Discretization(fcg.HEX8, en, dis.node_x, dis.node_dof_col, dis.node_dof_row,
+                                  dis.rowptr, dis.col_lid)
+
     with pytest.raises(fcg.FcgError) as ei:
         fcg.Evaluator(dis, path=fcg.PATH_STRUCTURED)
     assert ei.value.code == 4
     en = dis.ele_nodes.copy()
-    en[0, :4] = np.roll(en[0, :4], 1)
+    en[0, :4] = np.roll(en[0, :4], 1)   # about local zeta
     en[0, 4:] = np.roll(en[0, 4:], 1)
-    rot = fcg.Discretization(fcg.HEX8, en, dis.node_x, dis.node_dof_col, dis.node_dof_row,
-                             dis.rowptr, dis.col_lid)
+    en[7] = en[7][[1, 5, 6, 2, 0, 4, 7, 3]]  # about local eta
     with pytest.raises(fcg.FcgError) as ei:
-        fcg.Evaluator(rot, path=fcg.PATH_STRUCTURED)
-    assert ei.value.code == 3 and "lattice" in str(ei.value)
+        fcg.Evaluator(relabel(en), path=fcg.PATH_STRUCTURED)
+    assert ei.value.code == 4
+    en = dis.ele_nodes.copy()
+    en[3] = en[3][[4, 5, 6, 7, 0, 1, 2, 3]]  # top and bottom swapped: a mirrored frame
+    with pytest.raises(fcg.FcgError) as ei:
+        fcg.Evaluator(relabel(en), path=fcg.PATH_STRUCTURED)
+    assert ei.value.code == 3 and "mirrored" in str(ei.value)
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
