@@ -84,6 +84,7 @@ struct StructHost {
   std::vector<double> lat_x;        // node coordinates on the column-node lattice
   std::vector<int32_t> lat_dof;     // column LID of the node's first DOF, -1 = none
   std::vector<uint32_t> plane_rec;  // [tiles_y][tiles_x][NK][PLANE_REC_WORDS]
+  int64_t rows_unordered = 0;       // rows whose lower-plane neighbours are not their first columns
 };
 
 const int kOff8[8][3] = {{0, 0, 0}, {1, 0, 0}, {1, 1, 0}, {0, 1, 0}, {0, 0, 1}, {1, 0, 1}, {1, 1, 1},
@@ -456,6 +457,7 @@ bool build_structured_plan(const fcg_desc* d, const std::vector<int32_t>& rownod
   P.nbr_pos.assign(nrn * 27, 0xFFFF);
   std::string err;
   std::mutex err_m;
+  std::atomic<int64_t> unordered{0};
   parallel_for(nrn, [&](int64_t r) {
     const int64_t p = npos[rownodes[r]];
     const int64_t i = p % NXn, jj = (p / NXn) % NYn, k = p / (NXn * NYn);
@@ -497,7 +499,20 @@ bool build_structured_plan(const fcg_desc* d, const std::vector<int32_t>& rownod
       std::lock_guard<std::mutex> lk(err_m);
       err = "row holds columns beyond the lattice neighbours";
     }
+    // lattice order (GridGenerator numbering): the lower plane's triples open the row
+    int lo_max = -1, hi_min = 1 << 30;
+    for (int t = 0; t < 27; ++t)
+    {
+      const int q = P.nbr_pos[r * 27 + t];
+      if (q == 0xFFFF) continue;
+      if (t < 9)
+        lo_max = std::max(lo_max, q);
+      else
+        hi_min = std::min(hi_min, q);
+    }
+    if (lo_max > hi_min) unordered.fetch_add(1, std::memory_order_relaxed);
   });
+  P.rows_unordered = unordered.load();
   if (!err.empty())
   {
     why = err;
@@ -1203,6 +1218,17 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
     m.NI = sp.n[0]; m.NJ = sp.n[1]; m.NK = sp.n[2];
     m.EX0 = sp.elo[0]; m.EY0 = sp.elo[1]; m.EZ0 = sp.elo[2];
     m.EX = sp.en[0]; m.EY = sp.en[1]; m.EZ = sp.en[2];
+    // rows not in lattice order (input-file numbering): the linear sweep defers each row's
+    // lower-plane blocks by one layer (MODE 3; renumbered 1M box: 3.41 -> 2.20 GB written,
+    // 1.43 -> 1.32 ms, profiles/r03/r03_defer_*).  TotLag keeps MODE 0: its sweep is bound by the
+    // arithmetic at one workgroup per CU, and the extra LDS round trip cost 4 % there.
+    // FCG_SWEEP_DEFER=0/1 forces the choice (A/B runs, tests)
+    {
+      const char* de = std::getenv("FCG_SWEEP_DEFER");
+      m.sweep_defer = de && de[0] ? de[0] == '1'
+                                  : d->kinematics == FCG_LINEAR &&
+                                        8 * sp.rows_unordered > int64_t(rownodes.size());
+    }
     chk(upload(&m.elem_at, sp.elem_at.data(), int64_t(sp.elem_at.size()), bytes));
     chk(upload(&m.lat_x, sp.lat_x.data(), int64_t(sp.lat_x.size()), bytes));
     chk(upload(&m.lat_dof, sp.lat_dof.data(), int64_t(sp.lat_dof.size()), bytes));

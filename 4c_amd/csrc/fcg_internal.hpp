@@ -78,6 +78,7 @@ struct DeviceMesh {
   int32_t tiles_x = 0, tiles_y = 0, tiles_z = 0, seg_planes = 0;
   int32_t I0 = 0, J0 = 0, K0 = 0, NI = 0, NJ = 0, NK = 0;  // owned-node lattice box
   int32_t EX0 = 0, EY0 = 0, EZ0 = 0, EX = 0, EY = 0, EZ = 0;  // column-element lattice box
+  bool sweep_defer = false;         // rows not in lattice order: sweep MODE 3 (fcg_sweep.hip)
   int32_t* elem_at = nullptr;       // [EZ][EY][EX] column element or -1
   double* lat_x = nullptr;          // [EZ+1][EY+1][EX+1][3] node coordinates on the lattice
   int32_t* lat_dof = nullptr;       // [EZ+1][EY+1][EX+1] column LID of the node's first DOF or -1

@@ -91,7 +91,7 @@ struct SweepArgs {
 template <bool TSI>
 constexpr int node_comps() { return TSI ? 10 : 6; }
 
-template <int KIN, bool TSI, bool TH = false>
+template <int KIN, bool TSI, bool TH = false, bool DEFER = false>
 struct SweepShared {
   alignas(16) double nx[3 * 4 * NSLOT * 8 * 2];  // sqrt|fac| N_XYZ, see nx2i()
   // TotLag: F (column-major) | S (Voigt) | c = fac / sqrt|fac|  (linear kinematics: unused)
@@ -115,6 +115,10 @@ struct SweepShared {
 #else
   double hold[TX * TY][9][TSI ? (TH ? 9 : 18) : 9];
 #endif
+  // DEFER (rows not in lattice order): the blocks of node plane L+1's rows with the plane below
+  // (dz = -1, finished in layer L) wait here and are written in layer L+1 beside the row's other
+  // blocks, so that each row's cache lines are filled within one layer; ring by plane parity
+  double hold_lo[DEFER ? 2 : 1][DEFER ? TX * TY : 1][9][9];
 };
 
 __device__ inline int ring(int p) { return (p % 3 + 3) % 3; }
@@ -455,16 +459,21 @@ __device__ inline void block_k(const StVK& m, const double* acc, double* Kb)
 
 // MODE 0: structure (K, f_int); 1: fused TSI (K_SS, k_ST, k_TS, k_TT, f_S, f_T in one pass);
 // 2: the thermal-only pass that follows a MODE-0 linear sweep (k_ST, k_TS, k_TT, f_T, and
-// k_ST (T - T_0) added into f_S) -- 8 accumulators per block instead of 16, no K stores.
+// k_ST (T - T_0) added into f_S) -- 8 accumulators per block instead of 16, no K stores;
+// 3: structure with the lower-plane blocks deferred one layer (hold_lo), for meshes whose CSR
+// rows do not list the lattice neighbours plane by plane (input-file numbering): a row's 27
+// triples then land all over its 648 bytes, and writing them in two layers' halves left its
+// lines half-written in L2 between the two (1.4x the K bytes written on the renumbered 1M box).
 template <int KIN, bool WANT_K, bool OVERWRITE, int MODE>
 #ifndef FCG_SWEEP_WGS
 #define FCG_SWEEP_WGS 2
 #endif
 __global__ __launch_bounds__(256, KIN ? 1 : FCG_SWEEP_WGS) void sweep_h8_kernel(SweepArgs A)
 {
-  constexpr bool TSI = MODE != 0, TH = MODE == 2;
+  constexpr bool TSI = MODE == 1 || MODE == 2, TH = MODE == 2, DEFER = MODE == 3;
   static_assert(!TSI || (KIN == 0 && WANT_K), "TSI is geometrically linear, full tangent");
-  __shared__ SweepShared<KIN, TSI, TH> sh;
+  static_assert(!DEFER || WANT_K, "deferred blocks are K blocks");
+  __shared__ SweepShared<KIN, TSI, TH, DEFER> sh;
   constexpr int NACC = TH ? 8 : ((KIN || TSI) ? 16 : 9);
   constexpr int NC = node_comps<TSI>();
   constexpr int NLD = (NNODE * NC + 255) / 256;  // node-load items per lane
@@ -636,6 +645,11 @@ __global__ __launch_bounds__(256, KIN ? 1 : FCG_SWEEP_WGS) void sweep_h8_kernel(
         const uint32_t base_lo = WANT_K ? rec[PR_BASE + 2 * c] : 0u;
         const uint32_t base_hi = WANT_K ? rec[PR_BASE + 2 * c + 1] : 0u;
         const int32_t len32 = WANT_K ? int32_t(rec[PR_LEN + c]) : 0;
+        // DEFER: position of the lower-plane neighbour (dx, dy, -1) of an in-plane block t, whose
+        // held block this emit writes beside it (absent whenever t's neighbour is: an element
+        // coupling A with (dx, dy, -1) also holds (dx, dy, 0))
+        const uint16_t pos_lo =
+            DEFER ? reinterpret_cast<const uint16_t*>(rec + PR_NPOS)[27 * c + (t >= 9 ? t - 9 : 0)] : 0;
         if (KIN == 0)
         {
           const int dx = t % 3 - 1, dy = (t / 3) % 3 - 1, dz = t / 9 - 1;
@@ -689,6 +703,16 @@ __global__ __launch_bounds__(256, KIN ? 1 : FCG_SWEEP_WGS) void sweep_h8_kernel(
           }
         }
         if (act == kActHold || !WANT_K) return;
+        if constexpr (DEFER)
+        {
+          if (act == kActWriteL1)
+          {
+            double* h = sh.hold_lo[(L + 1) & 1][c][t];
+#pragma unroll
+            for (int i = 0; i < 9; ++i) h[i] = Kb[i];
+            return;
+          }
+        }
         if (!(to_l1 ? wl1 : wl) || row0 < 0 || pos == 0xFFFF) return;
         const int64_t base = int64_t(base_lo) | (int64_t(base_hi) << 32);
         const int64_t len = len32;
@@ -704,6 +728,24 @@ __global__ __launch_bounds__(256, KIN ? 1 : FCG_SWEEP_WGS) void sweep_h8_kernel(
               else
                 dst[r * len + qq] += Kb[3 * r + qq];
             }
+        if constexpr (DEFER)
+        {
+          if (act == kActWriteLHold && pos_lo != 0xFFFF)
+          {
+            const double* h = sh.hold_lo[L & 1][c][t - 9];
+            double* dlo = A.K + base + pos_lo;
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+              for (int qq = 0; qq < 3; ++qq)
+              {
+                if (OVERWRITE)
+                  dlo[r * len + qq] = h[3 * r + qq];
+                else
+                  dlo[r * len + qq] += h[3 * r + qq];
+              }
+          }
+        }
 #if defined(FCG_PROBE_TH_NOSTORE) || defined(FCG_PROBE_TH_1STORE)
         if (TH)
         {
@@ -929,7 +971,11 @@ hipError_t launch_sweep_h8(const DeviceMesh& m, const double* d_u_col, bool want
   const dim3 grid{static_cast<unsigned>(ntiles), 1, 1};
   const dim3 block{256, 1, 1};
 #define FCG_SWEEP(KIN)                                                                             \
-  if (want_k && overwrite)                                                                         \
+  if (want_k && m.sweep_defer && overwrite)                                                        \
+    hipLaunchKernelGGL((sweep_h8_kernel<KIN, true, true, 3>), grid, block, 0, stream, a);      \
+  else if (want_k && m.sweep_defer)                                                                \
+    hipLaunchKernelGGL((sweep_h8_kernel<KIN, true, false, 3>), grid, block, 0, stream, a);     \
+  else if (want_k && overwrite)                                                                    \
     hipLaunchKernelGGL((sweep_h8_kernel<KIN, true, true, 0>), grid, block, 0, stream, a);      \
   else if (want_k)                                                                                 \
     hipLaunchKernelGGL((sweep_h8_kernel<KIN, true, false, 0>), grid, block, 0, stream, a);     \

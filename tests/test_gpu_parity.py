@@ -407,6 +407,45 @@ def test_renumbered_box_takes_the_sweep_by_lattice_detection(kinem):
     _check(Kt, ft, Kr, fr)
 
 
+@pytest.mark.parametrize("kinem", [fcg.LINEAR, fcg.TOTLAG])
+def test_sweep_deferred_lower_plane_blocks_bitwise(kinem, monkeypatch):
+    """The sweep's MODE 3 (each row's lower-plane blocks written one layer later, beside the row's
+    other blocks -- chosen for rows not in lattice order) stores the same values as MODE 0:
+    bitwise equal K, f for OVERWRITE and ACCUMULATE on box ranks (holes at the rank faces), and on
+    a renumbered box (its default for linear kinematics) the same as the oracle."""
+    _dev()
+    for r in range(2):
+        m = fcg.BoxMesh(fcg.HEX8, (9, 7, 11), jitter=0.1, rank=r, nranks=2)
+        u = m.u_col(1e-3 if kinem == fcg.LINEAR else 5e-2)
+        rng = np.random.default_rng(r)
+        K0, f0 = rng.standard_normal(m.nnz), rng.standard_normal(m.n_rows)
+        out = {}
+        for defer in ("0", "1"):
+            monkeypatch.setenv("FCG_SWEEP_DEFER", defer)
+            K1, f1, ev = _run_gpu(m, kinem, u, path=fcg.PATH_STRUCTURED)
+            K2, f2, _ = _run_gpu(m, kinem, u, ev=ev, mode=fcg.ACCUMULATE, K0=K0, f0=f0)
+            out[defer] = (K1, f1, K2, f2)
+        for a, b in zip(out["0"], out["1"]):
+            assert np.array_equal(a, b)
+    monkeypatch.delenv("FCG_SWEEP_DEFER")
+    box = fcg.BoxMesh(fcg.HEX8, (6, 7, 5), jitter=0.1, seed=8)
+    dis = fcg.Discretization.renumbered(box, seed=5)
+    u = np.random.default_rng(4).standard_normal(dis.n_cols) * (1e-3 if kinem == fcg.LINEAR else 5e-2)
+    mesh_like = type("M", (), {})()
+    mesh_like.row_gid = mesh_like.col_gid = np.arange(dis.n_cols, dtype=np.int32)
+    mesh_like.nnz, mesh_like.n_rows, mesh_like.rowptr, mesh_like.col_lid = dis.nnz, dis.n_rows, dis.rowptr, dis.col_lid
+    mesh_like.celltype, mesh_like.n_ele, mesh_like.ele_nodes = fcg.HEX8, dis.n_ele, dis.ele_nodes
+    mesh_like.n_node, mesh_like.node_x, mesh_like.node_dof_row = dis.n_node, dis.node_x, dis.node_dof_row
+    mesh_like.node_gid = np.arange(dis.n_node, dtype=np.int64)
+    err, _, Kr, fr = oracle_evaluate(mesh_like, kinem, E, NU, u)
+    assert err == 0
+    Ks, fs, ev = _run_gpu(dis, kinem, u, path=fcg.PATH_STRUCTURED)
+    _check(Ks, fs, Kr, fr)
+    monkeypatch.setenv("FCG_SWEEP_DEFER", "0")
+    K0s, f0s, _ = _run_gpu(dis, kinem, u, path=fcg.PATH_STRUCTURED)
+    assert np.array_equal(Ks, K0s) and np.array_equal(fs, f0s)
+
+
 def test_lattice_detection_with_holes_matches_oracle():
     """Lattice detection on an input-file mesh with elements missing (a hole through the box and an
     L-shaped notch): the found lattice has empty positions, which the row-block sweep treats like
