@@ -1219,9 +1219,9 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
     m.EX0 = sp.elo[0]; m.EY0 = sp.elo[1]; m.EZ0 = sp.elo[2];
     m.EX = sp.en[0]; m.EY = sp.en[1]; m.EZ = sp.en[2];
     // rows not in lattice order (input-file numbering): the linear sweep defers each row's
-    // lower-plane blocks by one layer (MODE 3; renumbered 1M box: 3.41 -> 2.20 GB written,
-    // 1.43 -> 1.32 ms, profiles/r03/r03_defer_*).  TotLag keeps MODE 0: its sweep is bound by the
-    // arithmetic at one workgroup per CU, and the extra LDS round trip cost 4 % there.
+    // lower-plane blocks by one layer (MODE 3; renumbered 1M box: 3.41 -> 2.23 GB written,
+    // 1.45 -> 1.30-1.35 ms, profiles/r03/defer/).  TotLag keeps MODE 0: its sweep is bound by the
+    // arithmetic at one workgroup per CU, and the extra LDS round trip cost 4-6 % there.
     // FCG_SWEEP_DEFER=0/1 forces the choice (A/B runs, tests)
     {
       const char* de = std::getenv("FCG_SWEEP_DEFER");

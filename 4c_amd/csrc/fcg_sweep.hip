@@ -117,8 +117,10 @@ struct SweepShared {
 #endif
   // DEFER (rows not in lattice order): the blocks of node plane L+1's rows with the plane below
   // (dz = -1, finished in layer L) wait here and are written in layer L+1 beside the row's other
-  // blocks, so that each row's cache lines are filled within one layer; ring by plane parity
-  double hold_lo[DEFER ? 2 : 1][DEFER ? TX * TY : 1][9][9];
+  // blocks, so that each row's cache lines are filled within one layer.  Slot (column, t) belongs
+  // to the one lane that emits block t of that column every layer: it reads the held block
+  // before it holds the next one (a wavefront's LDS operations execute in order), one buffer.
+  double hold_lo[DEFER ? TX * TY : 1][9][9];
 };
 
 __device__ inline int ring(int p) { return (p % 3 + 3) % 3; }
@@ -645,11 +647,6 @@ __global__ __launch_bounds__(256, KIN ? 1 : FCG_SWEEP_WGS) void sweep_h8_kernel(
         const uint32_t base_lo = WANT_K ? rec[PR_BASE + 2 * c] : 0u;
         const uint32_t base_hi = WANT_K ? rec[PR_BASE + 2 * c + 1] : 0u;
         const int32_t len32 = WANT_K ? int32_t(rec[PR_LEN + c]) : 0;
-        // DEFER: position of the lower-plane neighbour (dx, dy, -1) of an in-plane block t, whose
-        // held block this emit writes beside it (absent whenever t's neighbour is: an element
-        // coupling A with (dx, dy, -1) also holds (dx, dy, 0))
-        const uint16_t pos_lo =
-            DEFER ? reinterpret_cast<const uint16_t*>(rec + PR_NPOS)[27 * c + (t >= 9 ? t - 9 : 0)] : 0;
         if (KIN == 0)
         {
           const int dx = t % 3 - 1, dy = (t / 3) % 3 - 1, dz = t / 9 - 1;
@@ -707,9 +704,31 @@ __global__ __launch_bounds__(256, KIN ? 1 : FCG_SWEEP_WGS) void sweep_h8_kernel(
         {
           if (act == kActWriteL1)
           {
-            double* h = sh.hold_lo[(L + 1) & 1][c][t];
+            // the block held since the previous layer belongs to plane L's row: write it now,
+            // beside that row's other blocks; hold this layer's block for plane L+1
+            const int32_t row0L = int32_t(recL[PR_ROW0 + c]);
+            const uint16_t posL = reinterpret_cast<const uint16_t*>(recL + PR_NPOS)[27 * c + t];
+            const uint32_t bloL = recL[PR_BASE + 2 * c], bhiL = recL[PR_BASE + 2 * c + 1];
+            const int64_t lenL = int32_t(recL[PR_LEN + c]);
+            double* h = sh.hold_lo[c][t];
+            double old[9];
+#pragma unroll
+            for (int i = 0; i < 9; ++i) old[i] = h[i];
+            __asm__ volatile("" ::: "memory");
 #pragma unroll
             for (int i = 0; i < 9; ++i) h[i] = Kb[i];
+            if (!wl || row0L < 0 || posL == 0xFFFF) return;
+            double* dlo = A.K + (int64_t(bloL) | (int64_t(bhiL) << 32)) + posL;
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+              for (int qq = 0; qq < 3; ++qq)
+              {
+                if (OVERWRITE)
+                  dlo[r * lenL + qq] = old[3 * r + qq];
+                else
+                  dlo[r * lenL + qq] += old[3 * r + qq];
+              }
             return;
           }
         }
@@ -728,24 +747,6 @@ __global__ __launch_bounds__(256, KIN ? 1 : FCG_SWEEP_WGS) void sweep_h8_kernel(
               else
                 dst[r * len + qq] += Kb[3 * r + qq];
             }
-        if constexpr (DEFER)
-        {
-          if (act == kActWriteLHold && pos_lo != 0xFFFF)
-          {
-            const double* h = sh.hold_lo[L & 1][c][t - 9];
-            double* dlo = A.K + base + pos_lo;
-#pragma unroll
-            for (int r = 0; r < 3; ++r)
-#pragma unroll
-              for (int qq = 0; qq < 3; ++qq)
-              {
-                if (OVERWRITE)
-                  dlo[r * len + qq] = h[3 * r + qq];
-                else
-                  dlo[r * len + qq] += h[3 * r + qq];
-              }
-          }
-        }
 #if defined(FCG_PROBE_TH_NOSTORE) || defined(FCG_PROBE_TH_1STORE)
         if (TH)
         {
