@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <climits>
 #include <cstdlib>
 #include <atomic>
@@ -150,42 +151,51 @@ bool detect_lattice_hex8(const fcg_desc* d, std::vector<int32_t>& ijk, std::vect
       if (diff == 1) partner[u][c++] = v;
     }
   }
-  struct Face {
-    int32_t v[4];
-    int32_t ef;  // element * 6 + local face
-    bool operator<(const Face& o) const
-    {
-      for (int k = 0; k < 4; ++k)
-        if (v[k] != o.v[k]) return v[k] < o.v[k];
-      return ef < o.ef;
-    }
-  };
-  std::vector<Face> faces(6 * n);
+  // faces as sorted node quadruples, bucketed by their smallest node (a counting sort: at most 12
+  // faces of a hex8 mesh start at one node), matched inside each bucket
+  std::vector<std::array<int32_t, 4>> fv(6 * n);
   parallel_for(n, [&](int64_t e) {
     const int32_t* en = d->ele_nodes + 8 * e;
     for (int f = 0; f < 6; ++f)
     {
-      Face& F = faces[6 * e + f];
-      for (int k = 0; k < 4; ++k) F.v[k] = en[kFace[f][k]];
-      std::sort(F.v, F.v + 4);
-      F.ef = int32_t(6 * e + f);
+      std::array<int32_t, 4>& F = fv[6 * e + f];
+      for (int k = 0; k < 4; ++k) F[k] = en[kFace[f][k]];
+      std::sort(F.begin(), F.end());
     }
   });
-  std::sort(faces.begin(), faces.end());
+  std::vector<int64_t> boff(d->n_node + 1, 0);
+  for (int64_t i = 0; i < 6 * n; ++i) ++boff[fv[i][0] + 1];
+  for (int64_t nd = 0; nd < d->n_node; ++nd) boff[nd + 1] += boff[nd];
+  std::vector<int32_t> bface(6 * n);
+  {
+    std::vector<int64_t> fill(boff.begin(), boff.end() - 1);
+    for (int64_t i = 0; i < 6 * n; ++i) bface[fill[fv[i][0]]++] = int32_t(i);
+  }
   std::vector<int32_t> nbr(6 * n, -1);  // element across local face f of e
-  for (size_t i = 0; i + 1 < faces.size(); ++i)
-    if (std::memcmp(faces[i].v, faces[i + 1].v, sizeof(faces[i].v)) == 0)
+  std::atomic<int> shared3{0};
+  parallel_for(d->n_node, [&](int64_t nd) {
+    for (int64_t i = boff[nd]; i < boff[nd + 1]; ++i)
     {
-      if (i + 2 < faces.size() && std::memcmp(faces[i].v, faces[i + 2].v, sizeof(faces[i].v)) == 0)
+      const int32_t fi = bface[i];
+      int matches = 0;
+      for (int64_t j = boff[nd]; j < boff[nd + 1]; ++j)
       {
-        why = "a face is shared by more than two elements";
-        return false;
+        const int32_t fj = bface[j];
+        if (fj != fi && fv[fj] == fv[fi])
+        {
+          ++matches;
+          nbr[fi] = fj / 6;
+        }
       }
-      nbr[faces[i].ef] = faces[i + 1].ef / 6;
-      nbr[faces[i + 1].ef] = faces[i].ef / 6;
-      ++i;
+      if (matches > 1) shared3 = 1;
     }
-  std::vector<Face>().swap(faces);
+  });
+  if (shared3)
+  {
+    why = "a face is shared by more than two elements";
+    return false;
+  }
+  std::vector<std::array<int32_t, 4>>().swap(fv);
 
   // node positions spread from element 0 (its local frame = the lattice axes)
   const int64_t unset = INT64_MIN;
