@@ -799,7 +799,8 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
 #pragma unroll
           for (int i = 0; i < 3; ++i)
 #pragma unroll
-            for (int j = 0; j < 3; ++j) dst[81 * i + j] = up ? v[i + 3 * j] : v[j + 3 * i];
+            for (int j = 0; j < 3; ++j)  // streamed (nt): read once, by the row assembly
+              __builtin_nontemporal_store(up ? v[i + 3 * j] : v[j + 3 * i], dst + 81 * i + j);
         }
       }
       else
