@@ -418,6 +418,8 @@ class NativeAMG:
             raise fcg.FcgError(rc, L.fcg_last_error(ev._h).decode())
         self._h = h
         self.setup_ms = []
+        # a rank of a partition: the handle preconditions the solve across ranks only
+        self.local = int(info.n_cols) != n_rows
 
     def close(self):
         if getattr(self, "_h", None):
@@ -456,6 +458,10 @@ class NativeAMG:
     def solve(self, K, b, x, rtol, max_iter=1000, setup=True):
         """K x = b from x = 0; setup=False iterates on the last setup (a constant operator)."""
         L = fcg.lib()
+        if self.local:
+            # the library refuses it too (fcg_amg_iterate: FCG_ERR_ARG); say so before any setup
+            raise fcg.FcgError(3, "NativeAMG.solve: multi-rank context -- solve across ranks with "
+                               "dsolve.NativeDFCG (fcg_dfcg_solve); this AMG is its preconditioner")
         if setup:
             self.setup(K)
         it, rel = ctypes.c_int(0), ctypes.c_double(0.0)

@@ -786,6 +786,15 @@ int fcg_amg_iterate(fcg_amg* h, const double* d_K_vals, const double* d_b_row, d
 {
   using namespace fcg_amgs;
   if (!h || !d_K_vals || !d_b_row || !d_x_row || !(rtol >= 0.0) || max_iter < 0) return FCG_ERR_ARG;
+  if (h->local)
+  {
+    // a rank of a partition: level 0 is only the owned block, so iterating here would solve the
+    // block-diagonal local system and report it converged -- the solve across ranks is
+    // fcg_dfcg_solve (this handle then serves as its preconditioner through setup / apply)
+    h->last_error = "fcg_amg_iterate: multi-rank context (ghost columns) -- solve with fcg_dfcg_solve";
+    h->ctx->last_error = h->last_error;
+    return FCG_ERR_ARG;
+  }
   if (!h->ready)
   {
     h->last_error = "fcg_amg_iterate: no numeric setup (call fcg_amg_setup first)";
@@ -818,6 +827,12 @@ int fcg_amg_solve(fcg_amg* h, const double* d_K_vals, const double* d_b_row, dou
   if (iterations) *iterations = 0;
   if (rel_residual) *rel_residual = 0.0;
   if (!h || !d_K_vals || !d_b_row || !d_x_row || !(rtol >= 0.0) || max_iter < 0) return FCG_ERR_ARG;
+  if (h->local)
+  {
+    h->last_error = "fcg_amg_solve: multi-rank context (ghost columns) -- solve with fcg_dfcg_solve";
+    h->ctx->last_error = h->last_error;
+    return FCG_ERR_ARG;
+  }
   const int rc = fcg_amg_setup(h, d_K_vals, stream);
   if (rc != FCG_OK) return rc;
   return fcg_amg_iterate(h, d_K_vals, d_b_row, d_x_row, rtol, max_iter, iterations, rel_residual, stream);

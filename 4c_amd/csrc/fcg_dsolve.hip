@@ -180,7 +180,11 @@ int fcg_dfcg_solve(fcg_ctx* ctx, fcg_amg* amg, const fcg_transport* tr, const do
     ck(hipMemsetAsync(pc, 0, sizeof(double) * size_t(std::max<int64_t>(1, nc)), s), "memset");
     // preconditioner: the rank's AMG on its owned block, or the nodal block Jacobi
     if (amg)
-      ck(fcg_amg_setup(amg, d_K, s), fcg_amg_last_error(amg));
+    {
+      // the return code first: fcg_amg_setup rewrites the handle's error string on failure
+      const int rc = fcg_amg_setup(amg, d_K, s);
+      if (rc != FCG_OK) throw Fail{rc, fcg_amg_last_error(amg)};
+    }
     else
     {
       alloc(&dinv, 9 * (n / 3));
@@ -188,7 +192,10 @@ int fcg_dfcg_solve(fcg_ctx* ctx, fcg_amg* amg, const fcg_transport* tr, const do
     }
     auto precond = [&](const double* rr, double* zz) {
       if (amg)
-        ck(fcg_amg_apply(amg, d_K, rr, zz, s), fcg_amg_last_error(amg));
+      {
+        const int rc = fcg_amg_apply(amg, d_K, rr, zz, s);
+        if (rc != FCG_OK) throw Fail{rc, fcg_amg_last_error(amg)};
+      }
       else
         ck(fcg_block_jacobi_apply(ctx, dinv, rr, zz, 1.0, 0, s), "block Jacobi apply");
     };

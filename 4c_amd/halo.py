@@ -127,6 +127,66 @@ def gloo_exchange():
     return Exchange(fn, None, keepalive=cb)
 
 
+def thread_exchanges(world):
+    """`world` fcg_alltoallv_fn callbacks for ranks that are threads of ONE process (MPI_Alltoallv
+    semantics through shared memory and a barrier): plan builds of every rank of a partition
+    from one process -- a host that evaluates the ranks of a split in turn on one device, and the
+    CPU tests.  Rank r's plan build must run in its own thread with exchanges[r] (`run_ranks`)."""
+    import threading
+    barrier = threading.Barrier(world)
+    slots = [None] * world
+    out = []
+    for rank in range(world):
+        def cb(send, scounts, recv, rcounts, item, _user, rank=rank):
+            try:
+                sc = [int(scounts[p]) for p in range(world)]
+                total = sum(sc) * item
+                slots[rank] = (ctypes.string_at(send, total) if total else b"", sc)
+                barrier.wait()
+                off = 0
+                for p in range(world):
+                    buf, psc = slots[p]
+                    start, n = sum(psc[:rank]) * item, psc[rank] * item
+                    if n != int(rcounts[p]) * item:
+                        raise ValueError("alltoallv: send and receive counts disagree")
+                    if n:
+                        ctypes.memmove(recv + off, buf[start:start + n], n)
+                    off += n
+                barrier.wait()  # every rank has read the slots before any rank reuses its own
+                return 0
+            except Exception:  # noqa: BLE001 - surfaced as an error code
+                barrier.abort()
+                return 1
+
+        fn = fcg.ALLTOALLV_FN(cb)
+        out.append(Exchange(fn, None, keepalive=cb))
+    return out
+
+
+def run_ranks(world, fn):
+    """fn(rank, exchange) for every rank, each in its own thread over thread_exchanges(world);
+    returns the results in rank order (re-raises the first failure)."""
+    import threading
+    xs = thread_exchanges(world)
+    res, err = [None] * world, [None] * world
+
+    def body(r):
+        try:
+            res[r] = fn(r, xs[r])
+        except BaseException as e:  # noqa: BLE001 - re-raised in the caller
+            err[r] = e
+
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for e in err:
+        if e is not None:
+            raise e
+    return res
+
+
 def _arr(p, n, dt):
     if n == 0:
         return np.zeros(0, dtype=dt)

@@ -407,3 +407,44 @@ def test_two_ranks_distributed_newton_pcg(kinem, path, transport):
     worst = max(abs(got[g] - uref[g]) for g in uref)
     assert worst <= 1e-8 * scale, (worst, scale)
     assert dev is not None
+
+
+def test_native_amg_refuses_to_solve_on_a_rank_of_a_partition():
+    """A NativeAMG built on a rank of a 2-rank partition covers the owned block only: solving with
+    it alone would answer the block-diagonal local system.  fcg_amg_iterate / fcg_amg_solve refuse
+    (FCG_ERR_ARG, pointing at fcg_dfcg_solve), and so does NativeAMG.solve; setup and apply -- the
+    preconditioner role inside fcg_dfcg_solve -- still work."""
+    dev = _dev()
+    amg_mod = importlib.import_module("4c_amd.amg")
+    import ctypes
+    iv, up = _solve_box(fcg.HEX8)
+    m = fcg.BoxMesh(fcg.HEX8, iv, upper=up, jitter=0.1, seed=5, rank=0, nranks=2)
+    assert m.n_cols > m.n_rows
+    ev = fcg.Evaluator(m, kinematics=fcg.LINEAR, youngs=E, poisson=NU, device=0)
+    fext, dbc = _cantilever_loads(m, up[0])
+    amg = amg_mod.NativeAMG(m, ev, dbc)
+    assert amg.local
+    K = torch.zeros(int(ev.info.nnz), dtype=torch.float64, device=dev)
+    f = torch.zeros(m.n_rows, dtype=torch.float64, device=dev)
+    u = torch.zeros(m.n_cols, dtype=torch.float64, device=dev)
+    ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u, f, K)
+    b = torch.from_numpy(fext).to(dev)
+    x = torch.zeros_like(b)
+    with pytest.raises(fcg.FcgError) as ei:
+        amg.solve(K, b, x, 1e-8)
+    assert ei.value.code == 3 and "fcg_dfcg_solve" in str(ei.value)
+    L = fcg.lib()
+    vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    it, rel = ctypes.c_int(0), ctypes.c_double(0.0)
+    s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    rc = L.fcg_amg_solve(amg._h, vp(K), vp(b), vp(x), 1e-8, 100, ctypes.byref(it), ctypes.byref(rel), s)
+    assert rc == 3 and b"fcg_dfcg_solve" in L.fcg_amg_last_error(amg._h)
+    amg.setup(K)
+    rc = L.fcg_amg_iterate(amg._h, vp(K), vp(b), vp(x), 1e-8, 100, ctypes.byref(it), ctypes.byref(rel), s)
+    assert rc == 3 and it.value == 0
+    z = torch.zeros_like(b)
+    assert L.fcg_amg_apply(amg._h, vp(K), vp(b), vp(z), s) == 0
+    torch.cuda.synchronize()
+    assert torch.isfinite(z).all() and float(z.abs().max()) > 0
+    amg.close()
+    ev.close()

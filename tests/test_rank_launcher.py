@@ -102,3 +102,38 @@ def test_bench_refuses_mismatched_world_before_importing_torch():
     assert p.returncode != 0
     assert "WORLD_SIZE=3" in p.stderr and "--gpus 2" in p.stderr
     assert "| torch" not in p.stderr  # failed before torch was imported
+
+
+def test_sigterm_to_the_launcher_stops_every_rank(tmp_path):
+    """A SIGTERM to the launcher (harness timeout) stops the ranks before it exits: no orphans."""
+    import signal
+    child = tmp_path / "child.py"
+    child.write_text(textwrap.dedent(f"""
+        import os, time
+        open(os.path.join({str(tmp_path)!r}, "pid%s" % os.environ["RANK"]), "w").write(str(os.getpid()))
+        time.sleep(120)
+        """))
+    launcher = tmp_path / "launch.py"
+    launcher.write_text(textwrap.dedent(f"""
+        import sys
+        sys.path.insert(0, {os.path.join(ROOT, "tools")!r})
+        import rank_launcher as rl
+        sys.exit(rl.spawn([sys.executable, {str(child)!r}], 2, grace_s=5.0))
+        """))
+    p = subprocess.Popen([sys.executable, str(launcher)])
+    t0 = time.time()
+    while len(list(tmp_path.glob("pid*"))) < 2 and time.time() - t0 < 30:
+        time.sleep(0.1)
+    pids = [int((tmp_path / f"pid{r}").read_text()) for r in range(2)]
+    p.send_signal(signal.SIGTERM)
+    assert p.wait(timeout=30) == 128 + signal.SIGTERM
+    for pid in pids:
+        t0 = time.time()
+        while time.time() - t0 < 10:
+            try:
+                os.kill(pid, 0)
+            except ProcessLookupError:
+                break
+            time.sleep(0.1)
+        else:
+            raise AssertionError(f"rank process {pid} outlived the launcher")

@@ -64,11 +64,30 @@ def plan(argv, environ):
     return ("spawn", n) if n > 1 else ("run", None)
 
 
+class _Signalled(Exception):
+    def __init__(self, signum):
+        super().__init__(signum)
+        self.signum = signum
+
+
+def _raise_signal(signum, _frame):
+    raise _Signalled(signum)
+
+
 def spawn(cmd, n, environ=None, poll_s=0.2, grace_s=20.0):
-    """Run `cmd` as ranks 0..n-1; return the job's exit code (0, or the first failure's)."""
+    """Run `cmd` as ranks 0..n-1; return the job's exit code (0, or the first failure's).
+    A SIGTERM / SIGINT to the launcher (a harness timeout, another launcher stopping the job)
+    stops every rank first -- children left behind would hold their GPUs, possibly blocked in a
+    collective -- and then returns 128 + the signal number."""
     environ = dict(os.environ if environ is None else environ)
     port = free_port()
     procs = []
+    old = {}
+    try:
+        for sig in (signal.SIGTERM, signal.SIGINT):
+            old[sig] = signal.signal(sig, _raise_signal)
+    except ValueError:  # not the main thread: no handlers, the finally below still stops ranks
+        pass
     try:
         for r in range(n):
             out = None if r == 0 else sys.stderr.fileno()
@@ -89,8 +108,17 @@ def spawn(cmd, n, environ=None, poll_s=0.2, grace_s=20.0):
             if live:
                 time.sleep(poll_s)
         return rc
-    finally:
+    except _Signalled as e:
+        print(f"rank_launcher: signal {e.signum}; stopping the ranks", file=sys.stderr, flush=True)
         _stop([p for p in procs if p.poll() is None], grace_s)
+        return 128 + e.signum
+    finally:
+        # no second signal may interrupt the clean-up
+        for sig in old:
+            signal.signal(sig, signal.SIG_IGN)
+        _stop([p for p in procs if p.poll() is None], grace_s)
+        for sig, h in old.items():
+            signal.signal(sig, h)
 
 
 def _stop(procs, grace_s):
