@@ -171,6 +171,71 @@ def _under_profiler():
     return "rocprof" in pre or any(k.startswith("ROCPROF") for k in os.environ)
 
 
+def measure_counters(passes, prof_args, kernel, timeout_s=150):
+    """Per-dispatch means of rocprofv3 counters for the kernels whose name contains `kernel`,
+    measured in this run: one child process per pass (tools/prof_kernel.py `prof_args`, a few
+    evaluates of the workload), each under its own time limit and with no tracing domain mixed in.
+    Returns {counter: mean per dispatch} (or a dict with "error")."""
+    import csv
+    import shutil
+    import tempfile
+    rp = shutil.which("rocprofv3")
+    if rp is None:
+        return {"error": "rocprofv3 not found"}
+    if _under_profiler():
+        return {"error": "bench.py is itself running under a profiler: no nested counter passes"}
+    work = tempfile.mkdtemp(prefix="fcg_pmc_")
+    per = {}
+    try:
+        for i, ctrs in enumerate(passes):
+            d = os.path.join(work, f"p{i}")
+            cmd = [rp, "--pmc", *ctrs.split(), "--output-format", "csv", "-d", d, "-o", "run", "--",
+                   sys.executable, os.path.join(ROOT, "tools", "prof_kernel.py"), *prof_args]
+            env = dict(os.environ, TMPDIR=work)
+            p = subprocess.run(cmd, cwd=work, env=env, capture_output=True, text=True,
+                               timeout=timeout_s)
+            if p.returncode != 0:
+                return {"error": f"pass {ctrs} exited {p.returncode}: {p.stderr[-400:]}"}
+            vals = {}
+            for fn in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+                for r in csv.DictReader(open(fn)):
+                    if kernel in r["Kernel_Name"]:
+                        key = (r["Counter_Name"], r["Dispatch_Id"])
+                        vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
+            for c in ctrs.split():
+                v = [x for (name, _), x in vals.items() if name == c]
+                if not v:
+                    return {"error": f"{c}: no {kernel} dispatch in the counter output"}
+                per[c] = sum(v) / len(v)
+        return per
+    except subprocess.TimeoutExpired:
+        return {"error": f"counter pass exceeded {timeout_s} s"}
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+
+
+def measure_mfma_h27(n, cus):
+    """Matrix-pipe use of h27_element_kernel on the config-3 element box, measured in this run:
+    SQ_VALU_MFMA_BUSY_CYCLES (summed over the SIMDs) against the SIMD-cycles of the dispatch
+    (GRBM_GUI_ACTIVE summed over the 8 XCDs -> / 8 per XCD, x 4 SIMDs x CUs), and the FP64 MFMA
+    flops it executed (SQ_INSTS_VALU_MFMA_F64 x 2048 for v_mfma_f64_16x16x4_f64)."""
+    c = measure_counters(["SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_F64 SQ_INSTS_VALU_MFMA_MOPS_F64 "
+                          "SQ_INSTS_VALU_FLOPS_FP64 GRBM_GUI_ACTIVE"],
+                         ["--n", str(n), "--celltype", "hex27", "--kinem", "totlag", "--reps", "3"],
+                         "h27_element_kernel")
+    if "error" in c:
+        return c
+    simd_cycles = c["GRBM_GUI_ACTIVE"] / 8.0 * 4.0 * cus
+    return {"mfma_busy_cycles": c["SQ_VALU_MFMA_BUSY_CYCLES"], "simd_cycles": simd_cycles,
+            "matrix_pipe_busy_frac": c["SQ_VALU_MFMA_BUSY_CYCLES"] / simd_cycles,
+            "mfma_f64_instructions": c["SQ_INSTS_VALU_MFMA_F64"],
+            "mfma_f64_mops": c["SQ_INSTS_VALU_MFMA_MOPS_F64"],
+            "mfma_f64_flop_per_evaluate": 2048.0 * c["SQ_INSTS_VALU_MFMA_F64"],
+            "valu_flops_fp64_counter": c["SQ_INSTS_VALU_FLOPS_FP64"],
+            "source": "measured in this run: rocprofv3 --pmc (one child pass of tools/prof_kernel.py, "
+                      "3 evaluates, mean per dispatch)"}
+
+
 def measure_traffic(n, kernel="sweep_h8", timeout_s=150):
     """HBM bytes per evaluate of the bench kernel, measured in this run: two rocprofv3 counter
     passes (FETCH_SIZE, then WRITE_SIZE -- they do not fit one pass), each a child process
@@ -382,6 +447,14 @@ def hex27_secondary(dev, n, steps, threads, with_cpu):
     }
     ev.close()
     del K, f, u
+    # matrix-pipe use of the element kernel (north_star: "MFMA utilisation reported against gfx950
+    # peak"), from counters of this run, beside the executed-flop fraction above
+    ms_el = out["roofline"]["ms_element_kernel"]
+    mf = measure_mfma_h27(n, torch.cuda.get_device_properties(dev).multi_processor_count)
+    if "error" not in mf:
+        mf["mfma_tflops"] = mf["mfma_f64_flop_per_evaluate"] / (ms_el * 1e-3) / 1e12
+        mf["mfma_frac_of_spec_fp64"] = mf["mfma_tflops"] / FP64_PEAK_TFS
+    out["roofline"]["mfma_counters"] = mf
     if with_cpu:
         pu = _oracle_native()
         small = fcg.BoxMesh(fcg.HEX27, (n, n, max(2, n // 10)), jitter=0.02, seed=20251015)
@@ -1040,6 +1113,13 @@ def main():
             secondary.append(amg_newton_secondary(args.n))
         except Exception as e:  # report, never hide
             secondary.append({"workload": "hex8-renumbered-newton-amg", "error": repr(e)})
+    # the hex27 element's MFMA rate against this box's measured FP64 MFMA peak as well
+    if not isinstance(peaks, Exception) and peaks is not None:
+        for sec in secondary:
+            mf = sec.get("roofline", {}).get("mfma_counters") if isinstance(sec, dict) else None
+            if mf and "mfma_tflops" in mf and peaks[2] > 0:
+                mf["measured_mfma_peak_tflops"] = peaks[2]
+                mf["mfma_frac_of_measured_peak"] = mf["mfma_tflops"] / peaks[2]
     if secondary:
         out["secondary"] = secondary
     if rank == 0:

@@ -428,7 +428,10 @@ def test_native_amg_refuses_to_solve_on_a_rank_of_a_partition():
     f = torch.zeros(m.n_rows, dtype=torch.float64, device=dev)
     u = torch.zeros(m.n_cols, dtype=torch.float64, device=dev)
     ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u, f, K)
-    b = torch.from_numpy(fext).to(dev)
+    # rank 0 holds no tip load: a random right-hand side, zero on the Dirichlet rows
+    rhs = np.random.default_rng(1).standard_normal(m.n_rows)
+    rhs[dbc] = 0.0
+    b = torch.from_numpy(rhs).to(dev)
     x = torch.zeros_like(b)
     with pytest.raises(fcg.FcgError) as ei:
         amg.solve(K, b, x, 1e-8)
