@@ -156,6 +156,8 @@ struct Level {  // coarse level (6 x 6 blocks)
   double *x = nullptr, *b = nullptr, *r = nullptr, *d = nullptr, *z = nullptr, *p = nullptr, *q = nullptr;
 };
 
+struct Coupled;
+
 }  // namespace fcg_amgs
 
 struct fcg_amg {
@@ -183,6 +185,12 @@ struct fcg_amg {
   // rank-local preconditioner of a multi-rank context: level 0 is the owned block (ghost column
   // triples dropped) and is applied through its BSR copy instead of the context's fcg_spmv
   bool local = false;
+  std::vector<double> ns1;  // level 1's near-null space [n_agg][6][6] (R factors of step 0)
+  std::vector<int64_t> full_ptr;  // local: block pattern of the rank's whole rows (column nodes)
+  std::vector<int32_t> full_col;
+  // the coarse levels coupled across ranks (fcg_dfcg_solve with a local handle): built on the
+  // first solve through its transport, see fcg_amgs::Coupled
+  fcg_amgs::Coupled* cpl = nullptr;
 };
 
 namespace fcg_amgs {
@@ -260,6 +268,72 @@ std::vector<int64_t> diag_index(const Bsr& A)
   for (int64_t v : d)
     if (v < 0) throw Fail{FCG_ERR_ARG, "AMG: block row without a diagonal block"};
   return d;
+}
+
+// aggregation hierarchy below A_start (block size bs, near-null space ns [n][bs][6]; skip: level-0
+// nodes left out of the aggregation, NULL on a coarse start): appends steps and coarse levels until
+// a level has at most coarse_max DOFs (and always one step from an empty hierarchy)
+void coarsen(fcg_amg* h, const Bsr* A_start, int bs, std::vector<double> ns, const uint8_t* skip)
+{
+  const Bsr* A = A_start;
+  bool first = skip != nullptr;
+  while ((A->n * bs > h->opt.coarse_max || h->steps.empty()) && int(h->steps.size()) + 1 < h->opt.max_levels)
+  {
+    std::vector<int32_t> agg(size_t(A->n));
+    const int64_t n_agg = fcg_amg_aggregate(A->n, A->ptr_h.data(), A->col_h.data(), first ? skip : nullptr, agg.data());
+    if (n_agg <= 0 || n_agg >= A->n) break;
+    std::vector<double> tent(size_t(A->n) * bs * 6), nsc(size_t(n_agg) * 36);
+    int64_t nd = 0;
+    ck(fcg_amg_tentative(A->n, bs, ns.data(), agg.data(), n_agg, tent.data(), nsc.data(), &nd), "fcg_amg_tentative");
+    h->steps.emplace_back();
+    Step& st = h->steps.back();
+    st.bs = bs;
+    st.n_agg = n_agg;
+    std::vector<int64_t> tptr(size_t(A->n) + 1, 0);
+    std::vector<int32_t> tcol;
+    std::vector<double> tvals;
+    for (int64_t i = 0; i < A->n; ++i)
+    {
+      tptr[size_t(i) + 1] = tptr[size_t(i)] + (agg[size_t(i)] >= 0 ? 1 : 0);
+      if (agg[size_t(i)] >= 0)
+      {
+        tcol.push_back(agg[size_t(i)]);
+        tvals.insert(tvals.end(), tent.begin() + i * bs * 6, tent.begin() + (i + 1) * bs * 6);
+      }
+    }
+    make_bsr(h, st.T, tptr, tcol, bs, 6, n_agg);
+    if (!tvals.empty())
+      ck(hipMemcpy(st.T.vals, tvals.data(), sizeof(double) * tvals.size(), hipMemcpyHostToDevice), "hipMemcpy");
+    st.agg = upload(h, agg);
+    st.tent = upload(h, tent);
+    std::vector<int64_t> pp, app, tp, cp;
+    std::vector<int32_t> pc, apc, tc, cc;
+    symbolic(*A, st.T.ptr_h, st.T.col_h, n_agg, pp, pc);
+    make_bsr(h, st.P, pp, pc, bs, 6, n_agg);
+    make_bsr(h, st.AT, pp, pc, bs, 6, n_agg);
+    symbolic(*A, pp, pc, n_agg, app, apc);
+    make_bsr(h, st.AP, app, apc, bs, 6, n_agg);
+    tp.assign(size_t(n_agg) + 1, 0);
+    tc.assign(size_t(std::max<int64_t>(pp.back(), 1)), 0);
+    std::vector<int64_t> perm(size_t(std::max<int64_t>(pp.back(), 1)));
+    ck(fcg_bsr_transpose_pattern(A->n, n_agg, pp.data(), pc.data(), tp.data(), tc.data(), perm.data()), "fcg_bsr_transpose_pattern");
+    tc.resize(size_t(pp.back()));
+    perm.resize(size_t(pp.back()));
+    make_bsr(h, st.Pt, tp, tc, 6, bs, A->n);
+    st.perm = upload(h, perm);
+    symbolic(st.Pt, app, apc, n_agg, cp, cc);
+    h->levels.emplace_back();
+    Level& c = h->levels.back();
+    make_bsr(h, c.A, cp, cc, 6, 6, n_agg);
+    c.diag = upload(h, diag_index(c.A));
+    c.dinv = dalloc<double>(h, 36 * n_agg);
+    for (double** v : {&c.x, &c.b, &c.r, &c.d, &c.z, &c.p, &c.q}) *v = dalloc<double>(h, 6 * n_agg);
+    if (first) h->ns1 = nsc;  // level 1's near-null space (the coupled coarse level gathers it)
+    ns.swap(nsc);
+    A = &c.A;
+    bs = 6;
+    first = false;
+  }
 }
 
 // ---- device helpers --------------------------------------------------------------------------
@@ -485,6 +559,8 @@ void vcycle(fcg_amg* h, int l, const double* K, const double* b, double* x, hipS
   cheb(h, o, b, x, false);
 }
 
+void galerkin_from(fcg_amg* h, size_t l0, const double* K, hipStream_t s);
+
 // numeric setup for the tangent K (level-0 values in the context's CSR order)
 void setup(fcg_amg* h, const double* K, hipStream_t s)
 {
@@ -496,9 +572,16 @@ void setup(fcg_amg* h, const double* K, hipStream_t s)
   ck(fcg_bsr_block_jacobi_setup(h->device, 3, h->nb0, h->A0.ptr, h->A0_diag, h->A0.vals, h->A0_dinv,
          h->flag, s),
       "singular nodal block of K");
-  const Bsr* A = &h->A0;
-  const double* dinv = h->A0_dinv;
-  for (size_t l = 0; l < h->steps.size(); ++l)
+  galerkin_from(h, 0, K, s);
+}
+
+// the Galerkin hierarchy below level l0 (its operator and block inverses already set): per step
+// l >= l0, P_l = (I - omega D^-1 A_l) T_l and A_{l+1} = P_l^T (A_l P_l) on the fixed patterns
+void galerkin_from(fcg_amg* h, size_t l0, const double* K, hipStream_t s)
+{
+  const Bsr* A = l0 == 0 ? &h->A0 : &h->levels[l0 - 1].A;
+  const double* dinv = l0 == 0 ? h->A0_dinv : h->levels[l0 - 1].dinv;
+  for (size_t l = l0; l < h->steps.size(); ++l)
   {
     Step& st = h->steps[l];
     const double lm = l == 0 ? h->lmax0 : h->levels[l - 1].lmax;
@@ -570,6 +653,252 @@ void run_fcg(fcg_amg* h, const double* K, const double* b, double* x, double rto
   *rel = rn / bn;
 }
 
+
+// ---- coarse levels coupled across ranks (fcg_dfcg_solve with a rank-local handle) -------------
+// 4C's MueLu hierarchy spans every rank (4C_linear_solver_preconditioner_muelu.cpp:97: one
+// Xpetra operator over the global matrix).  Here the aggregation and the prolongator smoothing of
+// level 0 stay rank-local (as MueLu's uncoupled aggregation), but level 1 is the Galerkin operator
+// of the GLOBAL matrix, A_1 = P_0^T A P_0 with every rank's ghost-column couplings, solved
+// redundantly on every rank by a hierarchy built from the gathered A_1:
+//   * P_0's rows of the ghost nodes come from their owners through the transport's import
+//     (fixed-width channels: the global aggregate id and the six columns of each of a row's
+//     M blocks, M the widest row over the ranks);
+//   * this rank's rows of A_1 = Pt_0 (A_full P_ext) by the block SpGEMM on host-built patterns;
+//   * the rows of all ranks are summed into one zero-padded buffer (the transport's all-reduce),
+//     patterns once, values per tangent;
+//   * V-cycle: local Chebyshev on level 0, the level-0 residual with the global operator (one
+//     import + the rank's SpMV), restriction into the global level-1 vector (all-reduce), the
+//     replicated hierarchy's V-cycle, prolongation of this rank's aggregates, local Chebyshev.
+struct DevBuf {
+  double* p = nullptr;
+  explicit DevBuf(int64_t n) { ck(hipMalloc(&p, sizeof(double) * size_t(std::max<int64_t>(1, n))), "hipMalloc"); }
+  ~DevBuf() { if (p) (void)hipFree(p); }
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+};
+
+struct Coupled {
+  int rank = 0, nranks = 1;
+  int64_t nc_nodes = 0;            // column nodes of the context (owned first, then ghosts)
+  int64_t off = 0, n_agg_tot = 0;  // this rank's first global aggregate; all ranks' aggregates
+  int M = 0;                       // blocks per P_0 row, widest over the ranks
+  Bsr Afull;                       // owned block rows x column nodes (3 x 3)
+  Bsr Pext;                        // column nodes x global aggregates (3 x 6)
+  Bsr AP;                          // owned block rows x global aggregates (3 x 6)
+  Bsr A1r;                         // this rank's aggregates x global aggregates (6 x 6)
+  int64_t a1_first = 0, a1_nnzb = 0;  // this rank's first block in the global A_1; its block count
+  double *chan = nullptr, *chan_col = nullptr, *q = nullptr, *gb = nullptr, *ge = nullptr;
+  fcg_amg* g = nullptr;            // the replicated hierarchy: g->levels[0].A = the global A_1
+};
+
+// element-wise sum over the ranks of a host vector, through the transport's device all-reduce
+void host_allsum(const fcg_transport* tr, std::vector<double>& v, hipStream_t s)
+{
+  DevBuf d(int64_t(v.size()));
+  if (!v.empty())
+    ck(hipMemcpyAsync(d.p, v.data(), sizeof(double) * v.size(), hipMemcpyHostToDevice, s), "hipMemcpyAsync");
+  ck(tr->allreduce_fn(tr->user, d.p, int64_t(v.size()), s), "transport all-reduce");
+  if (!v.empty())
+    ck(hipMemcpyAsync(v.data(), d.p, sizeof(double) * v.size(), hipMemcpyDeviceToHost, s), "hipMemcpyAsync");
+  ck(hipStreamSynchronize(s), "hipStreamSynchronize");
+}
+
+// channel (k, col) of P_0's rows as a DOF vector: DOF d of owned node i gets entry (d, col) of the
+// row's k-th block (col < 0: the block's global aggregate id, -1 past the row's end)
+__global__ __launch_bounds__(kBlock) void pack_channel_kernel(int64_t nb, const int64_t* __restrict__ ptr,
+    const int32_t* __restrict__ col, const double* __restrict__ vals, int k, int c, int64_t off,
+    double* out)
+{
+  const int64_t t = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (t >= 3 * nb) return;
+  const int64_t i = t / 3, d = t - 3 * i;
+  const int64_t p = ptr[i] + k;
+  const bool in = p < ptr[i + 1];
+  out[t] = c < 0 ? (in ? double(int64_t(col[p]) + off) : -1.0) : (in ? vals[p * 18 + d * 6 + c] : 0.0);
+}
+
+// ... and back into P_ext's ghost rows (column nodes nb .. nc-1)
+__global__ __launch_bounds__(kBlock) void scatter_channel_kernel(int64_t nb, int64_t nc,
+    const int64_t* __restrict__ ptr, const double* __restrict__ in, int k, int c, double* vals)
+{
+  const int64_t t = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  const int64_t i = nb + t / 3, d = t % 3;
+  if (i >= nc) return;
+  const int64_t p = ptr[i] + k;
+  if (p < ptr[i + 1]) vals[p * 18 + d * 6 + c] = in[3 * i + d];
+}
+
+void coupled_build(fcg_amg* h, const fcg_transport* tr, hipStream_t s)
+{
+  const fcg::DeviceMesh& m = h->ctx->mesh;
+  Coupled* c = new Coupled();
+  h->cpl = c;
+  c->rank = tr->rank;
+  c->nranks = tr->nranks;
+  c->nc_nodes = m.n_cols / 3;
+  const int64_t nb0 = h->nb0, nc = c->nc_nodes, R = c->nranks;
+  const Step& st0 = h->steps[0];
+  const Bsr& P = st0.P;
+  // aggregates per rank and the widest P_0 row
+  {
+    std::vector<double> v(size_t(2 * R), 0.0);
+    int64_t wmax = 0;
+    for (int64_t i = 0; i < P.n; ++i) wmax = std::max(wmax, P.ptr_h[size_t(i) + 1] - P.ptr_h[size_t(i)]);
+    v[size_t(c->rank)] = double(st0.n_agg);
+    v[size_t(R + c->rank)] = double(wmax);
+    host_allsum(tr, v, s);
+    for (int64_t q = 0; q < R; ++q)
+    {
+      if (q < c->rank) c->off += int64_t(v[size_t(q)]);
+      c->n_agg_tot += int64_t(v[size_t(q)]);
+      c->M = std::max(c->M, int(v[size_t(R + q)]));
+    }
+  }
+  c->chan = dalloc<double>(h, 3 * nb0);
+  c->chan_col = dalloc<double>(h, m.n_cols);
+  c->q = dalloc<double>(h, 3 * nb0);
+  c->gb = dalloc<double>(h, 6 * c->n_agg_tot);
+  c->ge = dalloc<double>(h, 6 * c->n_agg_tot);
+  // the ghost rows' aggregate ids, one channel per block slot
+  std::vector<std::vector<int32_t>> gid(size_t(nc - nb0));
+  std::vector<double> colv(size_t(m.n_cols));
+  const dim3 gp(blocks_for(3 * std::max<int64_t>(1, nb0))), bl(kBlock);
+  for (int k = 0; k < c->M; ++k)
+  {
+    hipLaunchKernelGGL(pack_channel_kernel, gp, bl, 0, s, nb0, P.ptr, P.col, P.vals, k, -1, c->off, c->chan);
+    ck(hipGetLastError(), "pack_channel_kernel");
+    ck(tr->import_fn(tr->user, c->chan, c->chan_col, s), "transport import (P_0 ghost ids)");
+    ck(hipMemcpyAsync(colv.data(), c->chan_col, sizeof(double) * colv.size(), hipMemcpyDeviceToHost, s), "hipMemcpyAsync");
+    ck(hipStreamSynchronize(s), "hipStreamSynchronize");
+    for (int64_t i = nb0; i < nc; ++i)
+    {
+      const double id = colv[size_t(3 * i)];
+      if (id >= 0.0) gid[size_t(i - nb0)].push_back(int32_t(id));
+    }
+  }
+  // P_ext: owned rows = P_0 with global aggregate ids, then the ghost rows as imported
+  std::vector<int64_t> pp(size_t(nc) + 1, 0);
+  std::vector<int32_t> pc;
+  for (int64_t i = 0; i < nb0; ++i)
+  {
+    for (int64_t k = P.ptr_h[size_t(i)]; k < P.ptr_h[size_t(i) + 1]; ++k) pc.push_back(int32_t(P.col_h[size_t(k)] + c->off));
+    pp[size_t(i) + 1] = int64_t(pc.size());
+  }
+  for (int64_t i = nb0; i < nc; ++i)
+  {
+    const auto& row = gid[size_t(i - nb0)];
+    for (size_t k = 0; k < row.size(); ++k)
+      if (k > 0 && row[k] <= row[k - 1]) throw Fail{FCG_ERR_ARG, "coupled AMG: ghost P_0 row not sorted"};
+    pc.insert(pc.end(), row.begin(), row.end());
+    pp[size_t(i) + 1] = int64_t(pc.size());
+  }
+  make_bsr(h, c->Pext, pp, pc, 3, 6, c->n_agg_tot);
+  make_bsr(h, c->Afull, h->full_ptr, h->full_col, 3, 3, nc);
+  std::vector<int64_t> app, a1p;
+  std::vector<int32_t> apc, a1c;
+  symbolic(c->Afull, c->Pext.ptr_h, c->Pext.col_h, c->n_agg_tot, app, apc);
+  make_bsr(h, c->AP, app, apc, 3, 6, c->n_agg_tot);
+  symbolic(st0.Pt, app, apc, c->n_agg_tot, a1p, a1c);
+  make_bsr(h, c->A1r, a1p, a1c, 6, 6, c->n_agg_tot);
+  // the global A_1 pattern on every rank: row lengths, then the columns
+  std::vector<double> lens(size_t(c->n_agg_tot), 0.0);
+  for (int64_t i = 0; i < st0.n_agg; ++i) lens[size_t(c->off + i)] = double(a1p[size_t(i) + 1] - a1p[size_t(i)]);
+  host_allsum(tr, lens, s);
+  std::vector<int64_t> gptr(size_t(c->n_agg_tot) + 1, 0);
+  for (int64_t i = 0; i < c->n_agg_tot; ++i) gptr[size_t(i) + 1] = gptr[size_t(i)] + int64_t(lens[size_t(i)]);
+  c->a1_first = gptr[size_t(c->off)];
+  c->a1_nnzb = gptr.back();
+  std::vector<double> cols(size_t(c->a1_nnzb), 0.0);
+  for (size_t k = 0; k < a1c.size(); ++k) cols[size_t(c->a1_first) + k] = double(a1c[k]);
+  host_allsum(tr, cols, s);
+  std::vector<int32_t> gcol(cols.size());
+  for (size_t k = 0; k < cols.size(); ++k) gcol[k] = int32_t(cols[k]);
+  // level 1's near-null space: the ranks' R factors of step 0
+  std::vector<double> ns(size_t(36 * c->n_agg_tot), 0.0);
+  std::copy(h->ns1.begin(), h->ns1.end(), ns.begin() + 36 * c->off);
+  host_allsum(tr, ns, s);
+  // the replicated hierarchy (identical on every rank: same input, deterministic build)
+  fcg_amg* g = new fcg_amg();
+  c->g = g;
+  g->ctx = h->ctx;
+  g->device = h->device;
+  g->opt = h->opt;
+  g->steps.emplace_back();  // step 0 (level 0 -> 1) is the ranks' own P_0
+  g->levels.emplace_back();
+  {
+    Level& L1 = g->levels[0];
+    make_bsr(g, L1.A, gptr, gcol, 6, 6, c->n_agg_tot);
+    L1.diag = upload(g, diag_index(L1.A));
+    L1.dinv = dalloc<double>(g, 36 * c->n_agg_tot);
+    for (double** v : {&L1.x, &L1.b, &L1.r, &L1.d, &L1.z, &L1.p, &L1.q}) *v = dalloc<double>(g, 6 * c->n_agg_tot);
+  }
+  coarsen(g, &g->levels[0].A, 6, std::move(ns), nullptr);
+  g->partial = dalloc<double>(g, kMaxPartials);
+  g->sc = dalloc<double>(g, 16);
+  g->flag = dalloc<int32_t>(g, 1);
+}
+
+// numeric part per tangent, after the local setup (P_0's values for this K)
+void coupled_setup(fcg_amg* h, const double* K, const fcg_transport* tr, hipStream_t s)
+{
+  Coupled* c = h->cpl;
+  const fcg::DeviceMesh& m = h->ctx->mesh;
+  const Step& st0 = h->steps[0];
+  const Bsr& P = st0.P;
+  const int64_t nb0 = h->nb0, nc = c->nc_nodes;
+  ck(fcg_bsr_from_node_csr(h->device, nb0, m.rowptr, c->Afull.ptr, K, c->Afull.vals, s), "fcg_bsr_from_node_csr (full rows)");
+  if (P.nnzb > 0)
+    ck(hipMemcpyAsync(c->Pext.vals, P.vals, sizeof(double) * size_t(P.nnzb) * 18, hipMemcpyDeviceToDevice, s), "copy");
+  const dim3 gp(blocks_for(3 * std::max<int64_t>(1, nb0))), gg(blocks_for(3 * std::max<int64_t>(1, nc - nb0))),
+      bl(kBlock);
+  for (int k = 0; k < c->M; ++k)
+    for (int col = 0; col < 6; ++col)
+    {
+      hipLaunchKernelGGL(pack_channel_kernel, gp, bl, 0, s, nb0, P.ptr, P.col, P.vals, k, col, c->off, c->chan);
+      ck(hipGetLastError(), "pack_channel_kernel");
+      ck(tr->import_fn(tr->user, c->chan, c->chan_col, s), "transport import (P_0 ghost rows)");
+      if (nc > nb0)
+        hipLaunchKernelGGL(scatter_channel_kernel, gg, bl, 0, s, nb0, nc, c->Pext.ptr, c->chan_col, k, col, c->Pext.vals);
+      ck(hipGetLastError(), "scatter_channel_kernel");
+    }
+  ck(fcg_bsr_spgemm(h->device, 3, 3, 6, nb0, c->Afull.ptr, c->Afull.col, c->Afull.vals, c->Pext.ptr,
+         c->Pext.col, c->Pext.vals, c->AP.ptr, c->AP.col, c->AP.vals, s), "fcg_bsr_spgemm (A P_ext)");
+  ck(fcg_bsr_spgemm(h->device, 6, 3, 6, st0.Pt.n, st0.Pt.ptr, st0.Pt.col, st0.Pt.vals, c->AP.ptr,
+         c->AP.col, c->AP.vals, c->A1r.ptr, c->A1r.col, c->A1r.vals, s), "fcg_bsr_spgemm (P^T A P)");
+  fcg_amg* g = c->g;
+  Level& L1 = g->levels[0];
+  ck(hipMemsetAsync(L1.A.vals, 0, sizeof(double) * size_t(std::max<int64_t>(1, c->a1_nnzb)) * 36, s), "memset");
+  if (c->A1r.nnzb > 0)
+    ck(hipMemcpyAsync(L1.A.vals + c->a1_first * 36, c->A1r.vals, sizeof(double) * size_t(c->A1r.nnzb) * 36,
+           hipMemcpyDeviceToDevice, s), "copy");
+  ck(tr->allreduce_fn(tr->user, L1.A.vals, c->a1_nnzb * 36, s), "transport all-reduce (A_1)");
+  ck(fcg_bsr_block_jacobi_setup(g->device, 6, L1.A.n, L1.A.ptr, L1.diag, L1.A.vals, L1.dinv, g->flag, s),
+      "coupled AMG level 1: singular diagonal block");
+  if (g->steps.size() > 1) estimate_lmax(Ops{g, 1, nullptr, s});
+  galerkin_from(g, 1, nullptr, s);
+}
+
+void coupled_apply(fcg_amg* h, const double* K, const fcg_transport* tr, const double* r, double* z,
+    hipStream_t s)
+{
+  Coupled* c = h->cpl;
+  const Ops o{h, 0, K, s};
+  const int64_t n = h->n0;
+  const Step& st0 = h->steps[0];
+  cheb(h, o, r, z, true);
+  // the residual with the global operator
+  ck(tr->import_fn(tr->user, z, c->chan_col, s), "transport import");
+  ck(fcg_spmv(h->ctx, K, c->chan_col, c->q, s), "fcg_spmv");
+  hipLaunchKernelGGL(rsub_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, s, r, c->q, n);
+  ck(hipMemsetAsync(c->gb, 0, sizeof(double) * size_t(std::max<int64_t>(1, 6 * c->n_agg_tot)), s), "memset");
+  ck(fcg_bsr_spmv(h->device, 6, 3, st0.Pt.n, st0.Pt.ptr, st0.Pt.col, st0.Pt.vals, c->q, c->gb + 6 * c->off,
+         1.0, 0, s), "restriction");
+  ck(tr->allreduce_fn(tr->user, c->gb, 6 * c->n_agg_tot, s), "transport all-reduce (level 1)");
+  vcycle(c->g, 1, nullptr, c->gb, c->ge, s);
+  ck(fcg_bsr_spmv(h->device, 3, 6, st0.P.n, st0.P.ptr, st0.P.col, st0.P.vals, c->ge + 6 * c->off, z, 1.0, 1, s),
+      "prolongation");
+  cheb(h, o, r, z, false);
+}
 }  // namespace fcg_amgs
 
 extern "C" {
@@ -638,6 +967,23 @@ int fcg_amg_create(fcg_ctx* ctx, const int64_t* rowptr, const int32_t* col_lid,
         bcol[size_t(bptr[size_t(b)] + k)] = c / 3;
       }
     make_bsr(h, h->A0, bptr, bcol, 3, 3, nb);
+    if (h->local)
+    {
+      // the rank's whole rows (ghost column triples included), for the coarse level coupled
+      // across ranks (A_1 = P_0^T A P_0 with the global operator): block column = column LID / 3
+      if (m.n_cols % 3 != 0) throw Fail{FCG_ERR_ARG, "fcg_amg_create: 3 DOFs per column node"};
+      h->full_ptr.assign(size_t(nb) + 1, 0);
+      for (int64_t b = 0; b < nb; ++b) h->full_ptr[size_t(b) + 1] = h->full_ptr[size_t(b)] + (rowptr[3 * b + 1] - rowptr[3 * b]) / 3;
+      h->full_col.resize(size_t(h->full_ptr.back()));
+      for (int64_t b = 0; b < nb; ++b)
+        for (int64_t k = 0; k < h->full_ptr[size_t(b) + 1] - h->full_ptr[size_t(b)]; ++k)
+        {
+          const int32_t c = col_lid[rowptr[3 * b] + 3 * k];
+          if (c < 0 || c % 3 != 0 || c >= m.n_cols)
+            throw Fail{FCG_ERR_ARG, "fcg_amg_create: column triples must start at 3 c"};
+          h->full_col[size_t(h->full_ptr[size_t(b)] + k)] = c / 3;
+        }
+    }
     h->A0_diag = upload(h, diag_index(h->A0));
     h->A0_dinv = dalloc<double>(h, 9 * nb);
     h->ctx_dinv = dalloc<double>(h, 9 * nb);
@@ -673,65 +1019,7 @@ int fcg_amg_create(fcg_ctx* ctx, const int64_t* rowptr, const int32_t* col_lid,
         }
       skip[size_t(b)] = nd == 3;
     }
-    const Bsr* A = &h->A0;
-    int bs = 3;
-    bool first = true;
-    while ((A->n * bs > h->opt.coarse_max || h->steps.empty()) && int(h->steps.size()) + 1 < h->opt.max_levels)
-    {
-      std::vector<int32_t> agg(size_t(A->n));
-      const int64_t n_agg = fcg_amg_aggregate(A->n, A->ptr_h.data(), A->col_h.data(), first ? skip.data() : nullptr, agg.data());
-      if (n_agg <= 0 || n_agg >= A->n) break;
-      std::vector<double> tent(size_t(A->n) * bs * 6), nsc(size_t(n_agg) * 36);
-      int64_t nd = 0;
-      ck(fcg_amg_tentative(A->n, bs, ns.data(), agg.data(), n_agg, tent.data(), nsc.data(), &nd), "fcg_amg_tentative");
-      h->steps.emplace_back();
-      Step& st = h->steps.back();
-      st.bs = bs;
-      st.n_agg = n_agg;
-      std::vector<int64_t> tptr(size_t(A->n) + 1, 0);
-      std::vector<int32_t> tcol;
-      std::vector<double> tvals;
-      for (int64_t i = 0; i < A->n; ++i)
-      {
-        tptr[size_t(i) + 1] = tptr[size_t(i)] + (agg[size_t(i)] >= 0 ? 1 : 0);
-        if (agg[size_t(i)] >= 0)
-        {
-          tcol.push_back(agg[size_t(i)]);
-          tvals.insert(tvals.end(), tent.begin() + i * bs * 6, tent.begin() + (i + 1) * bs * 6);
-        }
-      }
-      make_bsr(h, st.T, tptr, tcol, bs, 6, n_agg);
-      if (!tvals.empty())
-        ck(hipMemcpy(st.T.vals, tvals.data(), sizeof(double) * tvals.size(), hipMemcpyHostToDevice), "hipMemcpy");
-      st.agg = upload(h, agg);
-      st.tent = upload(h, tent);
-      std::vector<int64_t> pp, app, tp, cp;
-      std::vector<int32_t> pc, apc, tc, cc;
-      symbolic(*A, st.T.ptr_h, st.T.col_h, n_agg, pp, pc);
-      make_bsr(h, st.P, pp, pc, bs, 6, n_agg);
-      make_bsr(h, st.AT, pp, pc, bs, 6, n_agg);
-      symbolic(*A, pp, pc, n_agg, app, apc);
-      make_bsr(h, st.AP, app, apc, bs, 6, n_agg);
-      tp.assign(size_t(n_agg) + 1, 0);
-      tc.assign(size_t(std::max<int64_t>(pp.back(), 1)), 0);
-      std::vector<int64_t> perm(size_t(std::max<int64_t>(pp.back(), 1)));
-      ck(fcg_bsr_transpose_pattern(A->n, n_agg, pp.data(), pc.data(), tp.data(), tc.data(), perm.data()), "fcg_bsr_transpose_pattern");
-      tc.resize(size_t(pp.back()));
-      perm.resize(size_t(pp.back()));
-      make_bsr(h, st.Pt, tp, tc, 6, bs, A->n);
-      st.perm = upload(h, perm);
-      symbolic(st.Pt, app, apc, n_agg, cp, cc);
-      h->levels.emplace_back();
-      Level& c = h->levels.back();
-      make_bsr(h, c.A, cp, cc, 6, 6, n_agg);
-      c.diag = upload(h, diag_index(c.A));
-      c.dinv = dalloc<double>(h, 36 * n_agg);
-      for (double** v : {&c.x, &c.b, &c.r, &c.d, &c.z, &c.p, &c.q}) *v = dalloc<double>(h, 6 * n_agg);
-      ns.swap(nsc);
-      A = &c.A;
-      bs = 6;
-      first = false;
-    }
+    coarsen(h, &h->A0, 3, std::move(ns), skip.data());
     if (h->levels.empty()) throw Fail{FCG_ERR_ARG, "fcg_amg_create: no coarse level (aggregation did not coarsen)"};
     for (double** v : {&h->r0, &h->d0, &h->z0, &h->q0, &h->p0, &h->ro0, &h->fr, &h->fz, &h->fx})
       *v = dalloc<double>(h, n);
@@ -886,9 +1174,84 @@ int fcg_amg_apply(fcg_amg* h, const double* d_K_vals, const double* d_r_row, dou
   return FCG_OK;
 }
 
+// fcg_dfcg_solve's preconditioner (internal, fcg_internal.hpp): the numeric setup and one
+// application -- coupled across ranks when the handle is rank-local and the transport names more
+// than one rank (the coupled levels are built on the first call), else the handle's own V-cycle
+int fcg_amg_precond_setup(fcg_amg* h, const double* d_K, const fcg_transport* tr, void* stream)
+{
+  using namespace fcg_amgs;
+  int rc = fcg_amg_setup(h, d_K, stream);
+  if (rc != FCG_OK) return rc;
+  if (!h->local || !tr || tr->nranks <= 1) return FCG_OK;
+  try
+  {
+    ck(hipSetDevice(h->device), "hipSetDevice");
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->ctx->stream;
+    if (tr->rank < 0 || tr->rank >= tr->nranks) throw Fail{FCG_ERR_ARG, "coupled AMG: transport rank out of range"};
+    if (!h->cpl)
+    {
+      try
+      {
+        coupled_build(h, tr, s);
+      }
+      catch (const Fail&)
+      {
+        // a failed build leaves no half-built coupling behind (its device buffers stay listed
+        // in the handle's allocations until fcg_amg_destroy)
+        fcg_amg_destroy(h->cpl->g);
+        delete h->cpl;
+        h->cpl = nullptr;
+        throw;
+      }
+    }
+    else if (h->cpl->rank != tr->rank || h->cpl->nranks != tr->nranks)
+      throw Fail{FCG_ERR_ARG, "coupled AMG: the transport's rank / rank count changed"};
+    coupled_setup(h, d_K, tr, s);
+  }
+  catch (const Fail& f)
+  {
+    h->ready = false;
+    h->last_error = f.msg;
+    h->ctx->last_error = f.msg;
+    return f.code;
+  }
+  return FCG_OK;
+}
+
+int fcg_amg_precond_apply(fcg_amg* h, const double* d_K, const fcg_transport* tr, const double* d_r,
+    double* d_z, void* stream)
+{
+  using namespace fcg_amgs;
+  if (!h->cpl || !tr || tr->nranks <= 1) return fcg_amg_apply(h, d_K, d_r, d_z, stream);
+  try
+  {
+    ck(hipSetDevice(h->device), "hipSetDevice");
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->ctx->stream;
+    coupled_apply(h, d_K, tr, d_r, d_z, s);
+  }
+  catch (const Fail& f)
+  {
+    h->last_error = f.msg;
+    h->ctx->last_error = f.msg;
+    return f.code;
+  }
+  return FCG_OK;
+}
+
+int fcg_amg_coupled_levels(const fcg_amg* h)
+{
+  return h && h->cpl && h->cpl->g ? int(h->cpl->g->levels.size()) : 0;
+}
+
 int fcg_amg_destroy(fcg_amg* h)
 {
   if (!h) return FCG_OK;
+  if (h->cpl)
+  {
+    fcg_amg_destroy(h->cpl->g);
+    delete h->cpl;
+    h->cpl = nullptr;
+  }
   (void)hipSetDevice(h->device);
   for (void* p : h->allocs) (void)hipFree(p);
   delete h;

@@ -218,6 +218,15 @@ int fcg_comm_size(const fcg_comm* c, int* nranks)
   return FCG_OK;
 }
 
+int fcg_comm_rank(const fcg_comm* c, int* rank)
+{
+  if (!c || !rank) return FCG_ERR_ARG;
+  int r = 0;
+  if (ncclCommUserRank(c->nccl, &r) != ncclSuccess) return fcg_device_error();
+  *rank = r;
+  return FCG_OK;
+}
+
 int fcg_comm_allreduce(fcg_comm* c, double* d_buf, int64_t n, int op, void* stream)
 {
   if (!c || n < 0 || (n && !d_buf) || (op != FCG_OP_SUM && op != FCG_OP_MAX)) return FCG_ERR_ARG;

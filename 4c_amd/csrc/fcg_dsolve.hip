@@ -4,8 +4,11 @@
 // on the ghost-layer partition of the element evaluation (SURVEY §8e option A):
 //   * the SpMV of the rank's owned rows needs the search direction on the column map: one import
 //     per iteration (Epetra_CrsMatrix::Multiply's Importer = fcg_halo_import over RCCL);
-//   * the preconditioner is local to the rank: its fcg_amg on the owned block (a subdomain AMG --
-//     MueLu's uncoupled aggregation also aggregates within a rank) or the nodal block Jacobi;
+//   * the preconditioner: the rank's fcg_amg -- aggregation and level-0 smoothing on the owned
+//     block (MueLu's uncoupled aggregation also aggregates within a rank), the coarse levels
+//     coupled across the ranks (A_1 = P_0^T A P_0 of the global operator, gathered and solved
+//     redundantly; fcg_amgs::Coupled in fcg_amg_solver.hip) when the transport names its rank and
+//     rank count -- or the nodal block Jacobi;
 //   * the inner products are fixed-order partial sums on each rank plus one all-reduce of a small
 //     device buffer (two per iteration), so the iterates are independent of the launch geometry.
 // Flexible CG (Polak-Ribiere beta), as the single-rank fcg_amg_iterate: the V-cycle with a loose
@@ -137,6 +140,10 @@ int fcg_transport_rccl(fcg_rccl_pair* pair, fcg_transport* out)
   out->import_fn = rccl_import;
   out->allreduce_fn = rccl_allreduce;
   out->user = pair;
+  int n = 1, r = 0;
+  if (fcg_comm_size(pair->comm, &n) != FCG_OK || fcg_comm_rank(pair->comm, &r) != FCG_OK) return FCG_ERR_DEVICE;
+  out->nranks = n;
+  out->rank = r;
   return FCG_OK;
 }
 
@@ -181,8 +188,8 @@ int fcg_dfcg_solve(fcg_ctx* ctx, fcg_amg* amg, const fcg_transport* tr, const do
     // preconditioner: the rank's AMG on its owned block, or the nodal block Jacobi
     if (amg)
     {
-      // the return code first: fcg_amg_setup rewrites the handle's error string on failure
-      const int rc = fcg_amg_setup(amg, d_K, s);
+      // the return code first: the setup rewrites the handle's error string on failure
+      const int rc = fcg_amg_precond_setup(amg, d_K, tr, s);
       if (rc != FCG_OK) throw Fail{rc, fcg_amg_last_error(amg)};
     }
     else
@@ -193,7 +200,7 @@ int fcg_dfcg_solve(fcg_ctx* ctx, fcg_amg* amg, const fcg_transport* tr, const do
     auto precond = [&](const double* rr, double* zz) {
       if (amg)
       {
-        const int rc = fcg_amg_apply(amg, d_K, rr, zz, s);
+        const int rc = fcg_amg_precond_apply(amg, d_K, tr, rr, zz, s);
         if (rc != FCG_OK) throw Fail{rc, fcg_amg_last_error(amg)};
       }
       else

@@ -186,3 +186,12 @@ struct fcg_ctx {
   bool pending = false;
   hipStream_t pending_stream = nullptr;
 };
+
+// fcg_dfcg_solve's AMG preconditioner (fcg_amg_solver.hip; not part of the C ABI): numeric setup
+// and one application, with the coarse levels coupled across the ranks of the transport when the
+// handle is rank-local (fcg_amgs::Coupled), else the handle's own V-cycle
+extern "C" {
+int fcg_amg_precond_setup(fcg_amg* h, const double* d_K, const fcg_transport* tr, void* stream);
+int fcg_amg_precond_apply(fcg_amg* h, const double* d_K, const fcg_transport* tr, const double* d_r,
+    double* d_z, void* stream);
+}

@@ -140,7 +140,9 @@ class NativeDFCG:
     a Transport over RCCL (halo.Comm) or host-staged (gloo callbacks into the library).  Same
     solve(K, b, x, rtol, max_iter) interface as DistributedPCG."""
 
-    def __init__(self, evaluator, transport, amg=None):
+    def __init__(self, evaluator, transport, amg=None, coupled=True):
+        """coupled=False: the transport does not name the ranks (nranks = 0), so the AMG stays the
+        rank-local subdomain preconditioner (the round-3 behaviour, kept for comparison)."""
         self.ev, self.tr, self.amg = evaluator, transport, amg
         self.dev = torch.device("cuda", evaluator.device)
         self._keep = []
@@ -188,6 +190,12 @@ class NativeDFCG:
             t.import_fn = fcg.IMPORT_FN(import_cb)
             t.allreduce_fn = fcg.ALLREDUCE_FN(allreduce_cb)
             self._keep += [t.import_fn, t.allreduce_fn, send, recv]
+            if dist.is_initialized():
+                t.rank, t.nranks = dist.get_rank(), dist.get_world_size()
+            else:
+                t.rank, t.nranks = 0, 1
+        if not coupled:
+            t.nranks = 0
         self._t = t
         self.iterations, self.rel_residual = 0, None
 
@@ -201,6 +209,10 @@ class NativeDFCG:
             raise fcg.FcgError(rc, fcg.lib().fcg_last_error(self.ev._h).decode())
         self.iterations, self.rel_residual = it.value, rel.value
         return it.value, rel.value
+
+    def coupled_levels(self):
+        """Levels of the AMG hierarchy coupled across ranks (0: rank-local preconditioner)."""
+        return fcg.lib().fcg_amg_coupled_levels(self.amg._h) if self.amg is not None else 0
 
 
 class DistributedNewton:

@@ -91,7 +91,8 @@ ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, 
 
 
 class FcgTransport(ctypes.Structure):
-    _fields_ = [("import_fn", IMPORT_FN), ("allreduce_fn", ALLREDUCE_FN), ("user", ctypes.c_void_p)]
+    _fields_ = [("import_fn", IMPORT_FN), ("allreduce_fn", ALLREDUCE_FN), ("user", ctypes.c_void_p),
+                ("rank", ctypes.c_int32), ("nranks", ctypes.c_int32)]
 
 
 class FcgRcclPair(ctypes.Structure):
@@ -135,7 +136,7 @@ EXPORTS = ["fcg_create", "fcg_destroy", "fcg_last_error", "fcg_evaluate", "fcg_e
            "fcg_tsi_evaluate_fused",
            "fcg_box_mesh_create", "fcg_box_mesh_destroy", "fcg_box_mesh_desc", "fcg_box_mesh_maps",
            "fcg_box_mesh_counts", "fcg_box_mesh_create_ex", "fcg_box_mesh_owned_rows",
-           "fcg_comm_unique_id", "fcg_comm_create", "fcg_comm_destroy", "fcg_comm_size", "fcg_comm_allreduce",
+           "fcg_comm_unique_id", "fcg_comm_create", "fcg_comm_destroy", "fcg_comm_size", "fcg_comm_rank", "fcg_comm_allreduce",
            "fcg_comm_alltoallv", "fcg_import_plan_build", "fcg_plan_free", "fcg_halo_create",
            "fcg_halo_destroy", "fcg_halo_import", "fcg_halo_pack", "fcg_halo_unpack",
            "fcg_shared_plan_build", "fcg_shared_create", "fcg_shared_destroy", "fcg_shared_reduce",
@@ -147,7 +148,7 @@ EXPORTS = ["fcg_create", "fcg_destroy", "fcg_last_error", "fcg_evaluate", "fcg_e
            "fcg_bsr_to_dense", "fcg_amg_default_options", "fcg_amg_create", "fcg_amg_solve",
            "fcg_amg_levels", "fcg_amg_level_info", "fcg_amg_setup_ms", "fcg_amg_last_error",
            "fcg_amg_destroy", "fcg_amg_setup", "fcg_amg_iterate", "fcg_amg_apply",
-           "fcg_transport_rccl", "fcg_dfcg_solve"]
+           "fcg_amg_coupled_levels", "fcg_transport_rccl", "fcg_dfcg_solve"]
 
 _lib = None
 FUNCT_FN = ctypes.CFUNCTYPE(ctypes.c_double, ctypes.c_int, _dp, ctypes.c_double, ctypes.c_void_p)
@@ -220,6 +221,7 @@ def lib():
     L.fcg_comm_create.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
     L.fcg_comm_destroy.argtypes = [vp]
     L.fcg_comm_size.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
+    L.fcg_comm_rank.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
     L.fcg_comm_allreduce.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_int, vp]
     L.fcg_comm_alltoallv.argtypes = [vp, _i64p, vp, _i64p, ctypes.c_int64, vp]
     L.fcg_import_plan_build.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64, _i32p,
@@ -288,6 +290,7 @@ def lib():
     L.fcg_amg_last_error.restype = ctypes.c_char_p
     L.fcg_amg_destroy.argtypes = [vp]
     L.fcg_amg_apply.argtypes = [vp, vp, vp, vp, vp]
+    L.fcg_amg_coupled_levels.argtypes = [vp]
     L.fcg_transport_rccl.argtypes = [ctypes.POINTER(FcgRcclPair), ctypes.POINTER(FcgTransport)]
     L.fcg_dfcg_solve.argtypes = [vp, vp, ctypes.POINTER(FcgTransport), vp, vp, vp, c_dbl, c_int, vp,
                                  ctypes.POINTER(c_int), _dp]

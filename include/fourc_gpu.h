@@ -507,6 +507,8 @@ int fcg_comm_create(const void* id, int nranks, int rank, int device, fcg_comm**
 int fcg_comm_destroy(fcg_comm* comm);
 /* The communicator's size as RCCL reports it (ncclCommCount); Epetra_Comm::NumProc in 4C. */
 int fcg_comm_size(const fcg_comm* comm, int* nranks);
+/* This rank in the communicator (ncclCommUserRank); Epetra_Comm::MyPID in 4C. */
+int fcg_comm_rank(const fcg_comm* comm, int* rank);
 /* In-place all-reduce of n doubles in device memory (ncclAllReduce). */
 int fcg_comm_allreduce(fcg_comm* comm, double* d_buf, int64_t n, int op, void* stream);
 
@@ -606,6 +608,12 @@ typedef struct fcg_transport {
   fcg_import_fn import_fn;
   fcg_allreduce_fn allreduce_fn;
   void* user;
+  /* this rank and the rank count of the partition (MPI_Comm_rank / _size in 4C).  With
+   * nranks > 1 an AMG handle's coarse levels are coupled across the ranks (the global Galerkin
+   * operator A_1 = P_0^T A P_0, gathered by allreduce_fn and solved redundantly); nranks <= 1 (a
+   * zero-initialised struct) keeps the rank-local AMG. */
+  int32_t rank;
+  int32_t nranks;
 } fcg_transport;
 /* The RCCL transport of (comm, halo): fills *out; `pair` (caller-owned, alive while used) holds
  * the two handles the callbacks receive as `user`. */
@@ -617,6 +625,9 @@ int fcg_transport_rccl(fcg_rccl_pair* pair, fcg_transport* out);
 /* AMG as the rank's local preconditioner: one V-cycle z = M^-1 r on the owned block after
  * fcg_amg_setup (fcg_amg_create accepts a multi-rank context: ghost columns are dropped). */
 int fcg_amg_apply(fcg_amg* amg, const double* d_K_vals, const double* d_r_row, double* d_z_row, void* stream);
+/* Levels of the coarse hierarchy coupled across ranks that fcg_dfcg_solve built for this handle
+ * (level 1 = the global A_1 and its coarsenings; 0 = none: single rank, or nranks <= 1). */
+int fcg_amg_coupled_levels(const fcg_amg* amg);
 int fcg_dfcg_solve(fcg_ctx* ctx, fcg_amg* amg, const fcg_transport* tr, const double* d_K_vals,
     const double* d_b_row, double* d_x_row, double rtol, int max_iter, void* stream,
     int* iterations, double* rel_residual);

@@ -299,13 +299,14 @@ def _worker_solve(rank, world, port, q, kinem, path, transport="staged", solver=
         lin = None
         if solver != "pcg":
             amg_mod = importlib.import_module("4c_amd.amg")
-            amg = amg_mod.NativeAMG(m, ev, dbc) if solver == "native" else None
-            lin = dsolve.NativeDFCG(ev, tr, amg)
+            amg = amg_mod.NativeAMG(m, ev, dbc) if solver in ("native", "native-uncoupled") else None
+            lin = dsolve.NativeDFCG(ev, tr, amg, coupled=solver != "native-uncoupled")
         nt = dsolve.DistributedNewton(ev, tr, fext, dbc, tol_res=1e-10, tol_inc=1e-11, lin_rtol=1e-12,
                                       linear_solver=lin)
         u = nt.solve().cpu().numpy()
         q.put((rank, True, {"u": dict(zip(m.row_gid[:n_own].tolist(), u.tolist())),
-                            "iters": [r.get("lin_iter") for r in nt.history]}))
+                            "iters": [r.get("lin_iter") for r in nt.history],
+                            "coupled_levels": lin.coupled_levels() if lin is not None else 0}))
         if lin is not None and lin.amg is not None:
             lin.amg.close()
         dist.destroy_process_group()
@@ -346,6 +347,10 @@ def _run_two_rank_solve(kinem, path, transport, solver="pcg", celltype=fcg.HEX8)
         assert ok is True, (rank, ok)
         got.update(out["u"])
         iters.append(out["iters"])
+        if solver == "native":
+            assert out["coupled_levels"] >= 1, out  # the coarse levels span both ranks
+        elif solver == "native-uncoupled":
+            assert out["coupled_levels"] == 0, out
     assert set(got) == set(uref)
     scale = max(abs(v) for v in uref.values())
     assert scale > 0
@@ -365,6 +370,35 @@ def test_two_ranks_native_dfcg(celltype, kinem, solver):
     if solver == "native":
         bj = _run_two_rank_solve(kinem, fcg.PATH_AUTO, "staged", "native-bj", celltype)
         assert sum(i or 0 for i in iters[0]) < sum(i or 0 for i in bj[0]), (iters, bj)
+        # coarse levels coupled across the ranks (4C's MueLu hierarchy spans every rank,
+        # 4C_linear_solver_preconditioner_muelu.cpp:97): the 2-rank solve needs at most 1.5x the
+        # FCG iterations of the 1-rank AMG on the same problem; the rank-local subdomain AMG
+        # (round 3) is kept as "native-uncoupled" for the comparison
+        one = _one_rank_amg_iters(celltype, kinem)
+        unc = _run_two_rank_solve(kinem, fcg.PATH_AUTO, "staged", "native-uncoupled", celltype)
+        n1, n2, nu = sum(one), sum(i or 0 for i in iters[0]), sum(i or 0 for i in unc[0])
+        print(f"FCG iterations: 1 rank {one}, 2 ranks coupled {iters[0]}, 2 ranks rank-local {unc[0]}")
+        assert n2 <= 1.5 * n1, (one, iters, unc)
+        assert n2 <= nu, (iters, unc)
+
+
+def _one_rank_amg_iters(celltype, kinem):
+    """The same Newton on one rank with the native AMG (fcg_amg_iterate): FCG iterations per step."""
+    _dev()
+    newton = importlib.import_module("4c_amd.newton")
+    amg_mod = importlib.import_module("4c_amd.amg")
+    iv, up = _solve_box(celltype)
+    m = fcg.BoxMesh(celltype, iv, upper=up, jitter=0.1 if celltype == fcg.HEX8 else 0.02, seed=5)
+    fext, dbc = _cantilever_loads(m, up[0])
+    ev = fcg.Evaluator(m, kinematics=kinem, youngs=E, poisson=NU, device=0)
+    amg = amg_mod.NativeAMG(m, ev, dbc)
+    nt = newton.StaticNewton(ev, fext, dbc, tol_res=1e-10, tol_inc=1e-11, lin_rtol=1e-12,
+                             linear_solver=amg)
+    nt.solve()
+    its = [r.get("lin_iter") or 0 for r in nt.history]
+    amg.close()
+    ev.close()
+    return its
 
 
 @pytest.mark.parametrize("transport", ["staged", "rccl"])
