@@ -776,7 +776,7 @@ void free_mesh(fcg::DeviceMesh& m)
       m.ele_dof, m.ele_nodes, m.ele_gid, m.node_x, m.node_dof_col, m.inc_of, m.inc_ptr,
       m.rownode_row0, m.inc_pos, m.rowptr, m.scratch, m.err, m.elem_at, m.lat_x, m.lat_dof,
       m.plane_rec,
-      m.tables, m.stamps, m.col_lid, m.diag_pos, m.pcg_work, m.col_ele, m.ele_ft, m.inc_row0,
+      m.tables, m.stamps, m.col_lid, m.diag_pos, m.pcg_work, m.col_ele, m.ele_ft, m.inc_row0, m.ele_gp,
       m.pen_ptr, m.ele_nb};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -1401,6 +1401,9 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
       tab[4 * g + 3] = w[g];
     }
     chk(upload(&m.tables, tab.data(), int64_t(tab.size()), bytes));
+    // the Gauss points' reference Jacobians, inverted, once for the context's lifetime
+    chk(upload<double>(&m.ele_gp, nullptr, d->n_ele * 80, bytes));
+    chk(fcg::gather_precompute(m, d->n_ele, ctx->stream));
   }
   else
   {

@@ -85,6 +85,7 @@ struct GatherArgs {
   const uint32_t* rec_tmap;  // [n_rec][32] per column triple of the rows: slot s's node in nibble s
   const int32_t* ele_orig;   // [n_ele] column element index of each storage slot (error report)
   const double* ele_x;       // [n_ele][8][3]
+  const double* ele_gp;      // [n_ele][8][10] per Gauss point (gather_gp_kernel, once per context)
   const int32_t* ele_dof;    // [n_ele][8] column LID of each node's first DOF
   const double* u_col;
   const double* gp;          // Gauss points [8][4]: xi, eta, zeta, weight
@@ -193,14 +194,29 @@ __global__ __launch_bounds__(64, 2) void gather_h8_kernel(GatherArgs A)
     r.tm = A.rec_tmap[k * 32 + (lane & 31)];
     return r;
   };
-  // element data of node q of slot j
+  // element data of node q of slot j (TotLag: its reference coordinates; linear: none) and its
+  // DOF; the Gauss point q's geometric factors come one record ahead (load_g)
   auto load_x = [&](const RecRegs& r, double* x, int32_t& dof) {
     const int64_t el = max(r.ele, 0);
-    const double* p = A.ele_x + (el * 8 + q) * 3;
-    x[0] = p[0];
-    x[1] = p[1];
-    x[2] = p[2];
+    if (KIN == 1)
+    {
+      const double* p = A.ele_x + (el * 8 + q) * 3;
+      x[0] = p[0];
+      x[1] = p[1];
+      x[2] = p[2];
+    }
     dof = A.ele_dof[el * 8 + q];
+  };
+  auto load_g = [&](const RecRegs& r, double* gv) {
+    const int64_t el = max(r.ele, 0);
+    const double2* p = reinterpret_cast<const double2*>(A.ele_gp + (el * 8 + q) * 10);
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+    {
+      const double2 v = p[k];
+      gv[2 * k] = v.x;
+      gv[2 * k + 1] = v.y;
+    }
   };
   auto load_u = [&](int32_t dof, double* u) {
     u[0] = A.u_col[dof];
@@ -220,18 +236,19 @@ __global__ __launch_bounds__(64, 2) void gather_h8_kernel(GatherArgs A)
   }
 
   RecRegs cur = load_rec(R0), nx1 = load_rec(R0 + 1), nx2 = load_rec(R0 + 2);
-  double xc[3], xn1[3], uc[3];
+  double xc[3], xn1[3], uc[3], gc[10];
   int32_t dofc, dof1;
   load_x(cur, xc, dofc);
   load_x(nx1, xn1, dof1);
   load_u(dofc, uc);
+  load_g(cur, gc);
   double fA0 = 0.0, fA1 = 0.0, fA2 = 0.0;
   int bad_code = 0, bad_ele = 0x7FFFFFFF;
   // the prologue's loads have landed before the loop: the loop header then carries only the
   // previous record's stores, and the waits inside stay at their static counts
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-  const double gx = sh.gp[q][0], gy = sh.gp[q][1], gz = sh.gp[q][2], gw = sh.gp[q][3];
+  const double gx = sh.gp[q][0], gy = sh.gp[q][1], gz = sh.gp[q][2];
   // element node b = q: parametric signs (TotLag stage 3)
   const double bsx = h8_sx(q & 3), bsy = (q & 3) >= 2 ? 1.0 : -1.0, bsz = q >= 4 ? 1.0 : -1.0;
   const double bsx8 = 0.125 * bsx, bsy8 = 0.125 * bsy, bsz8 = 0.125 * bsz;
@@ -240,10 +257,11 @@ __global__ __launch_bounds__(64, 2) void gather_h8_kernel(GatherArgs A)
     // in flight while this record computes: the next record's displacements, the element data of
     // the one after, the words of the third
     const RecRegs nx3 = load_rec(i + 3);
-    double xn2[3], u1[3];
+    double xn2[3], u1[3], g1[10];
     int32_t dof2;
     load_x(nx2, xn2, dof2);
     load_u(dof1, u1);
+    load_g(nx1, g1);
 
     const bool first = (cur.meta >> 4) & 1, last = (cur.meta >> 5) & 1;
     const int64_t base = cur.base;
@@ -255,9 +273,6 @@ __global__ __launch_bounds__(64, 2) void gather_h8_kernel(GatherArgs A)
     }
     const int32_t e = cur.ele;
     const int a = cur.a;
-    sh.X(0, j)[3 * q + 0] = xc[0];
-    sh.X(0, j)[3 * q + 1] = xc[1];
-    sh.X(0, j)[3 * q + 2] = xc[2];
     if (KIN == 1)
     {
       sh.X(1, j)[3 * q + 0] = xc[0] + uc[0];
@@ -266,11 +281,12 @@ __global__ __launch_bounds__(64, 2) void gather_h8_kernel(GatherArgs A)
     }
     if (lane < 32) sh.tmap[lane] = cur.tm;
     __syncthreads();
-    // 1. trilinear coefficient q of slot j
-    if (e >= 0)
+    // 1. trilinear coefficient q of slot j (TotLag: of the current coordinates; the reference
+    // Jacobians come precomputed)
+    if (KIN == 1 && e >= 0)
     {
 #pragma unroll
-      for (int s = 0; s < (KIN ? 2 : 1); ++s)
+      for (int s = 1; s < 2; ++s)
       {
         double c0 = 0.0, c1 = 0.0, c2 = 0.0;
 #pragma unroll
@@ -292,19 +308,14 @@ __global__ __launch_bounds__(64, 2) void gather_h8_kernel(GatherArgs A)
     if (e >= 0)
     {
       int bad = 0;
+      // the Gauss point's reference Jacobian, inverted (and the nodal det J check) once per
+      // context by gather_gp_kernel: linear sqrt|fac| J^-1 | sign(fac), TotLag J^-1 | fac
       double J[9];
-      // nodal check at corner q (det J(corner) has the sign of the edge-vector determinant)
-      h8_jac(sh.C(0, j), ((q & 3) == 1 || (q & 3) == 2) ? 1.0 : -1.0, (q & 3) >= 2 ? 1.0 : -1.0,
-          q >= 4 ? 1.0 : -1.0, J);
-      const double detn = h8_det(J);
-      if (detn == 0.0) bad = 2;
-      else if (!(detn > 0)) bad = 1;
-      h8_jac(sh.C(0, j), gx, gy, gz, J);
+#pragma unroll
+      for (int k = 0; k < 9; ++k) J[k] = gc[k];
       double Jc[9];
       if (KIN == 1) h8_jac(sh.C(1, j), gx, gy, gz, Jc);  // before GP (aliasing C) is written
-      const double det = h8_invert3x3(J);
-      if (det == 0.0) bad = 2;
-      const double fac = det * gw;
+      const double fac = gc[9];
       // dN_n/dxi = sx (1 + sy eta)(1 + sz zeta) / 8, ...
       // the 12 distinct products (1 +- eta)(1 +- zeta) / 8, ...; the node's sign is a negation
       const double xp = 1.0 + gx, xm = 1.0 - gx, yp = 1.0 + gy, ym = 1.0 - gy, zp = 1.0 + gz,
@@ -349,6 +360,7 @@ __global__ __launch_bounds__(64, 2) void gather_h8_kernel(GatherArgs A)
       double* P = sh.GP(j, q);
       if (KIN == 0)
       {
+        // NX holds sqrt|fac| N_XYZ: sign(fac) sqrt|fac| N_XYZ_a . sqrt|fac| N_XYZ_b = fac a b^T
         P[0] = fac * na[0];
         P[1] = fac * na[1];
         P[2] = fac * na[2];
@@ -594,6 +606,8 @@ __global__ __launch_bounds__(64, 2) void gather_h8_kernel(GatherArgs A)
       xn1[k] = xn2[k];
       uc[k] = u1[k];
     }
+#pragma unroll
+    for (int k = 0; k < 10; ++k) gc[k] = g1[k];
     dofc = dof1;
     dof1 = dof2;
   }
@@ -604,11 +618,114 @@ __global__ __launch_bounds__(64, 2) void gather_h8_kernel(GatherArgs A)
   }
 }
 
+// The Gauss points' geometric factors of every element, from its reference coordinates (fixed for
+// the context's lifetime), one thread per (element, Gauss point): J at the point and its inverse
+// (4C_solid_3D_ele_calc_lib.hpp:380-448), fac = det J w, the nodal det J > 0 check at corner g
+// (calc_lib.hpp:475-496).  Linear kinematics store sqrt|fac| J^-1 and sign(fac) (N_XYZ then comes
+// out scaled by sqrt|fac|), TotLag J^-1 and fac.  Failures go to err[0] (max code) / err[1] (min
+// column element).
+template <int KIN>
+__global__ __launch_bounds__(256) void gather_gp_kernel(int64_t n_ele, const double* __restrict__ ele_x,
+    const int32_t* __restrict__ ele_orig, const double* __restrict__ gp, double* ele_gp, int32_t* err)
+{
+  const int64_t t = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  const int64_t e = t >> 3;
+  const int g = int(t & 7);
+  if (e >= n_ele) return;
+  double x[8][3];
+#pragma unroll
+  for (int n = 0; n < 8; ++n)
+#pragma unroll
+    for (int d = 0; d < 3; ++d) x[n][d] = ele_x[e * 24 + 3 * n + d];
+  auto jac = [&](double px, double py, double pz, double* J) {
+    const H8dN dn = h8_dn_products(px, py, pz);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) J[k] = 0.0;
+#pragma unroll
+    for (int n = 0; n < 8; ++n)
+    {
+      double d0, d1, d2;
+      h8_dn(dn, n, d0, d1, d2);
+#pragma unroll
+      for (int d = 0; d < 3; ++d)
+      {
+        J[0 + 3 * d] += d0 * x[n][d];
+        J[1 + 3 * d] += d1 * x[n][d];
+        J[2 + 3 * d] += d2 * x[n][d];
+      }
+    }
+  };
+  int bad = 0;
+  double J[9];
+  jac(((g & 3) == 1 || (g & 3) == 2) ? 1.0 : -1.0, (g & 3) >= 2 ? 1.0 : -1.0, g >= 4 ? 1.0 : -1.0, J);
+  const double detn = h8_det(J);
+  if (detn == 0.0) bad = 2;
+  else if (!(detn > 0)) bad = 1;
+  jac(gp[4 * g], gp[4 * g + 1], gp[4 * g + 2], J);
+  const double det = h8_invert3x3(J);
+  if (det == 0.0) bad = 2;
+  const double fac = det * gp[4 * g + 3];
+  double* o = ele_gp + (e * 8 + g) * 10;
+  if (KIN == 0)
+  {
+    const double sq = sqrt(fabs(fac));
+#pragma unroll
+    for (int k = 0; k < 9; ++k) o[k] = sq * J[k];
+    o[9] = fac < 0.0 ? -1.0 : 1.0;
+  }
+  else
+  {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) o[k] = J[k];
+    o[9] = fac;
+  }
+  if (bad)
+  {
+    atomicMax(&err[0], bad);
+    atomicMin(&err[1], ele_orig[e]);
+  }
+}
+
+__global__ void fold_err_kernel(int32_t* err, int code, int ele)
+{
+  atomicMax(&err[0], code);
+  atomicMin(&err[1], ele);
+}
+
 }  // namespace
+
+hipError_t gather_precompute(DeviceMesh& m, int64_t n_ele, hipStream_t stream)
+{
+  if (n_ele == 0) return hipSuccess;
+  int32_t* d_err = nullptr;
+  hipError_t e = hipMalloc(&d_err, 2 * sizeof(int32_t));
+  if (e != hipSuccess) return e;
+  const int32_t init[2] = {0, 0x7FFFFFFF};
+  e = hipMemcpyAsync(d_err, init, sizeof(init), hipMemcpyHostToDevice, stream);
+  const dim3 grid{static_cast<unsigned>((n_ele * 8 + 255) / 256), 1, 1}, block{256, 1, 1};
+  if (e == hipSuccess)
+  {
+    if (m.kinem == 0)
+      hipLaunchKernelGGL((gather_gp_kernel<0>), grid, block, 0, stream, n_ele, m.ele_x, m.ele_orig, m.tables, m.ele_gp, d_err);
+    else
+      hipLaunchKernelGGL((gather_gp_kernel<1>), grid, block, 0, stream, n_ele, m.ele_x, m.ele_orig, m.tables, m.ele_gp, d_err);
+    e = hipGetLastError();
+  }
+  int32_t h[2] = {0, 0};
+  if (e == hipSuccess) e = hipMemcpyAsync(h, d_err, sizeof(h), hipMemcpyDeviceToHost, stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(stream);
+  (void)hipFree(d_err);
+  m.gp_bad_code = h[0];
+  m.gp_bad_ele = h[1];
+  return e;
+}
 
 hipError_t launch_gather_h8(const DeviceMesh& m, const double* d_u_col, bool want_k, bool overwrite,
     double* d_K, double* d_fint, hipStream_t stream)
 {
+  // a nodal / Gauss-point Jacobian failure found when the geometric factors were made is reported
+  // by every evaluate, as 4C's element throws on every call
+  if (m.gp_bad_code) hipLaunchKernelGGL(fold_err_kernel, dim3(1), dim3(1), 0, stream, m.err, m.gp_bad_code, m.gp_bad_ele);
   GatherArgs a{};
   a.n_single = m.n_rec_single;
   a.n_multi = m.n_multi;
@@ -621,6 +738,7 @@ hipError_t launch_gather_h8(const DeviceMesh& m, const double* d_u_col, bool wan
   a.rec_tmap = m.rec_tmap;
   a.ele_orig = m.ele_orig;
   a.ele_x = m.ele_x;
+  a.ele_gp = m.ele_gp;
   a.ele_dof = m.ele_dof;
   a.u_col = d_u_col;
   a.gp = m.tables;

@@ -70,6 +70,8 @@ struct DeviceMesh {
   int32_t* asm_order = nullptr;     // [n_rownodes] row nodes in Morton order of their coordinates
   int32_t* ele_orig = nullptr;      // [n_ele] column element index of each storage slot (Morton order)
   double* ele_x = nullptr;          // [n_ele][8][3] element node coordinates (storage slot order)
+  double* ele_gp = nullptr;         // [n_ele][8][10] Gauss-point factors (gather_precompute)
+  int32_t gp_bad_code = 0, gp_bad_ele = 0;  // a Jacobian failure found by gather_precompute
   int32_t* ele_dof = nullptr;       // [n_ele][8] column LID of each element node's first DOF
   double* gather_dummy = nullptr;   // [4] store target of a row without columns
 
@@ -164,6 +166,7 @@ hipError_t launch_h27_pencil(const DeviceMesh& m, const double* d_u_col, bool wa
     bool overwrite, double* d_K, double* d_fint, hipStream_t stream);
 // Node-row gather (FCG_PATH_GATHER, hex8 StVK on any mesh): one wavefront per owned row node
 // (fcg_gather.hip).
+hipError_t gather_precompute(DeviceMesh& m, int64_t n_ele, hipStream_t stream);
 hipError_t launch_gather_h8(const DeviceMesh& m, const double* d_u_col, bool want_k, bool overwrite,
     double* d_K, double* d_fint, hipStream_t stream);
 
