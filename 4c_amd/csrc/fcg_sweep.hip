@@ -389,20 +389,42 @@ __device__ inline void sweep_visit(const SH& sh, int slot, int a, int b1, int b2
       one(acc2, q0, q1, q2);
     }
   };
+  auto load_p = [&](int p, double2* v) {
+    const int nd[3] = {a, b1, b2};
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int d = 0; d < 3; ++d) v[3 * k + d] = *reinterpret_cast<const double2*>(&sh.nx[nx2i(d, p, slot, nd[k])]);
+  };
+#ifndef FCG_VISIT_NOPIPE
+  // structural passes: software-pipelined, the nine N_XYZ pairs of Gauss-point pair p + 1 are in
+  // flight while pair p computes (the scheduling barrier keeps the loads ahead of the FMAs; the
+  // compiler otherwise issues each pair's loads after the previous pair's FMAs and waits for them,
+  // an exposed LDS round trip per pair at two waves per SIMD).  +47 VGPRs (189 -> 236, still two
+  // workgroups per CU); the TSI instantiations would spill, they keep the plain loop.
+  if constexpr (!TSI)
+  {
+  double2 buf[2][9];
+  load_p(0, buf[0]);
 #pragma unroll
   for (int p = 0; p < 4; ++p)
   {
-    const double2 ax = *reinterpret_cast<const double2*>(&sh.nx[nx2i(0, p, slot, a)]);
-    const double2 ay = *reinterpret_cast<const double2*>(&sh.nx[nx2i(1, p, slot, a)]);
-    const double2 az = *reinterpret_cast<const double2*>(&sh.nx[nx2i(2, p, slot, a)]);
-    const double2 px = *reinterpret_cast<const double2*>(&sh.nx[nx2i(0, p, slot, b1)]);
-    const double2 py = *reinterpret_cast<const double2*>(&sh.nx[nx2i(1, p, slot, b1)]);
-    const double2 pz = *reinterpret_cast<const double2*>(&sh.nx[nx2i(2, p, slot, b1)]);
-    const double2 qx = *reinterpret_cast<const double2*>(&sh.nx[nx2i(0, p, slot, b2)]);
-    const double2 qy = *reinterpret_cast<const double2*>(&sh.nx[nx2i(1, p, slot, b2)]);
-    const double2 qz = *reinterpret_cast<const double2*>(&sh.nx[nx2i(2, p, slot, b2)]);
-    gp_body(2 * p, ax.x, ay.x, az.x, px.x, py.x, pz.x, qx.x, qy.x, qz.x);
-    gp_body(2 * p + 1, ax.y, ay.y, az.y, px.y, py.y, pz.y, qx.y, qy.y, qz.y);
+    if (p < 3) load_p(p + 1, buf[(p + 1) & 1]);
+    __builtin_amdgcn_sched_barrier(0);
+    const double2* v = buf[p & 1];
+    gp_body(2 * p, v[0].x, v[1].x, v[2].x, v[3].x, v[4].x, v[5].x, v[6].x, v[7].x, v[8].x);
+    gp_body(2 * p + 1, v[0].y, v[1].y, v[2].y, v[3].y, v[4].y, v[5].y, v[6].y, v[7].y, v[8].y);
+  }
+  return;
+  }
+#endif
+#pragma unroll
+  for (int p = 0; p < 4; ++p)
+  {
+    double2 v[9];
+    load_p(p, v);
+    gp_body(2 * p, v[0].x, v[1].x, v[2].x, v[3].x, v[4].x, v[5].x, v[6].x, v[7].x, v[8].x);
+    gp_body(2 * p + 1, v[0].y, v[1].y, v[2].y, v[3].y, v[4].y, v[5].y, v[6].y, v[7].y, v[8].y);
   }
 }
 

@@ -11,6 +11,7 @@ timeout -k 10 900 python -u -m pytest -x -v -s --timeout 800 --timeout-method th
 for k in linear totlag; do
   timeout -k 10 200 python tools/eval_timing.py --n 100 --kinem $k --renumber --path gather --reps 20 | tail -1 | tee -a $O/gather_timing.jsonl || exit 1
 done
+ROUNDS=3 timeout -k 10 600 bash tools/exp_ab.sh default nopipe 2>&1 | tee $O/ab_visit_pipe.txt || exit 1
 timeout -k 10 1500 python -u -m pytest -x -v --timeout 800 --timeout-method thread -m gpu tests > $O/gpu_tests_v1.log 2>&1; rc=$?
 tail -5 $O/gpu_tests_v1.log
 [ $rc -eq 0 ] || exit $rc
