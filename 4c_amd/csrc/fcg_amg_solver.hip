@@ -666,9 +666,13 @@ void run_fcg(fcg_amg* h, const double* K, const double* b, double* x, double rto
 //   * this rank's rows of A_1 = Pt_0 (A_full P_ext) by the block SpGEMM on host-built patterns;
 //   * the rows of all ranks are summed into one zero-padded buffer (the transport's all-reduce),
 //     patterns once, values per tangent;
-//   * V-cycle: local Chebyshev on level 0, the level-0 residual with the global operator (one
-//     import + the rank's SpMV), restriction into the global level-1 vector (all-reduce), the
-//     replicated hierarchy's V-cycle, prolongation of this rank's aggregates, local Chebyshev.
+//   * application: the balancing two-level form z = Q r + (I - Q A) M (I - A Q) r with
+//     Q = P_0 A_1^-1 P_0^T (restriction into the global level-1 vector, all-reduce, the replicated
+//     hierarchy's V-cycle, prolongation of this rank's aggregates) and M the rank-local V-cycle;
+//     two imports + SpMVs of the global operator per application.  (A multiplicative cycle with
+//     rank-local post-smoothing was tried first: its residual after the coarse correction is the
+//     global one but the smoother's the local one, and the result was indefinite on the first
+//     2-rank solve.)
 struct DevBuf {
   double* p = nullptr;
   explicit DevBuf(int64_t n) { ck(hipMalloc(&p, sizeof(double) * size_t(std::max<int64_t>(1, n))), "hipMalloc"); }
@@ -687,7 +691,8 @@ struct Coupled {
   Bsr AP;                          // owned block rows x global aggregates (3 x 6)
   Bsr A1r;                         // this rank's aggregates x global aggregates (6 x 6)
   int64_t a1_first = 0, a1_nnzb = 0;  // this rank's first block in the global A_1; its block count
-  double *chan = nullptr, *chan_col = nullptr, *q = nullptr, *gb = nullptr, *ge = nullptr;
+  double *chan = nullptr, *chan_col = nullptr, *q = nullptr, *w = nullptr, *v = nullptr, *gb = nullptr,
+         *ge = nullptr;
   fcg_amg* g = nullptr;            // the replicated hierarchy: g->levels[0].A = the global A_1
 };
 
@@ -757,6 +762,8 @@ void coupled_build(fcg_amg* h, const fcg_transport* tr, hipStream_t s)
   c->chan = dalloc<double>(h, 3 * nb0);
   c->chan_col = dalloc<double>(h, m.n_cols);
   c->q = dalloc<double>(h, 3 * nb0);
+  c->w = dalloc<double>(h, 3 * nb0);
+  c->v = dalloc<double>(h, 3 * nb0);
   c->gb = dalloc<double>(h, 6 * c->n_agg_tot);
   c->ge = dalloc<double>(h, 6 * c->n_agg_tot);
   // the ghost rows' aggregate ids, one channel per block slot
@@ -878,26 +885,48 @@ void coupled_setup(fcg_amg* h, const double* K, const fcg_transport* tr, hipStre
   galerkin_from(g, 1, nullptr, s);
 }
 
+// Q x = P_0 A_1^-1 P_0^T x over all ranks: restriction of this rank's rows into its segment of the
+// global level-1 vector, the all-reduce, the replicated hierarchy's V-cycle, prolongation of this
+// rank's aggregates (overwrites y)
+void coupled_coarse(fcg_amg* h, const fcg_transport* tr, const double* x, double* y, hipStream_t s)
+{
+  Coupled* c = h->cpl;
+  const Step& st0 = h->steps[0];
+  ck(hipMemsetAsync(c->gb, 0, sizeof(double) * size_t(std::max<int64_t>(1, 6 * c->n_agg_tot)), s), "memset");
+  ck(fcg_bsr_spmv(h->device, 6, 3, st0.Pt.n, st0.Pt.ptr, st0.Pt.col, st0.Pt.vals, x, c->gb + 6 * c->off,
+         1.0, 0, s), "restriction");
+  ck(tr->allreduce_fn(tr->user, c->gb, 6 * c->n_agg_tot, s), "transport all-reduce (level 1)");
+  vcycle(c->g, 1, nullptr, c->gb, c->ge, s);
+  ck(fcg_bsr_spmv(h->device, 3, 6, st0.P.n, st0.P.ptr, st0.P.col, st0.P.vals, c->ge + 6 * c->off, y, 1.0, 0, s),
+      "prolongation");
+}
+
+// y = A x with the global operator: the import of x into the column map, the rank's SpMV
+void coupled_spmv(fcg_amg* h, const double* K, const fcg_transport* tr, const double* x, double* y, hipStream_t s)
+{
+  Coupled* c = h->cpl;
+  ck(tr->import_fn(tr->user, x, c->chan_col, s), "transport import");
+  ck(fcg_spmv(h->ctx, K, c->chan_col, y, s), "fcg_spmv");
+}
+
+// The balancing (BNN) two-level preconditioner of the global system,
+//   z = Q r + (I - Q A) M (I - A Q) r,   Q = P_0 A_1^-1 P_0^T,  M = the rank-local V-cycle
+// (symmetric positive definite for SPD A and M: the rank-local hierarchy's smoothing and coarse
+// levels act on the owned block, the coupled level 1 on the global operator)
 void coupled_apply(fcg_amg* h, const double* K, const fcg_transport* tr, const double* r, double* z,
     hipStream_t s)
 {
   Coupled* c = h->cpl;
-  const Ops o{h, 0, K, s};
   const int64_t n = h->n0;
-  const Step& st0 = h->steps[0];
-  cheb(h, o, r, z, true);
-  // the residual with the global operator
-  ck(tr->import_fn(tr->user, z, c->chan_col, s), "transport import");
-  ck(fcg_spmv(h->ctx, K, c->chan_col, c->q, s), "fcg_spmv");
-  hipLaunchKernelGGL(rsub_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, s, r, c->q, n);
-  ck(hipMemsetAsync(c->gb, 0, sizeof(double) * size_t(std::max<int64_t>(1, 6 * c->n_agg_tot)), s), "memset");
-  ck(fcg_bsr_spmv(h->device, 6, 3, st0.Pt.n, st0.Pt.ptr, st0.Pt.col, st0.Pt.vals, c->q, c->gb + 6 * c->off,
-         1.0, 0, s), "restriction");
-  ck(tr->allreduce_fn(tr->user, c->gb, 6 * c->n_agg_tot, s), "transport all-reduce (level 1)");
-  vcycle(c->g, 1, nullptr, c->gb, c->ge, s);
-  ck(fcg_bsr_spmv(h->device, 3, 6, st0.P.n, st0.P.ptr, st0.P.col, st0.P.vals, c->ge + 6 * c->off, z, 1.0, 1, s),
-      "prolongation");
-  cheb(h, o, r, z, false);
+  const dim3 g(blocks_for(n)), bl(kBlock);
+  coupled_coarse(h, tr, r, c->w, s);                                     // w = Q r
+  coupled_spmv(h, K, tr, c->w, c->q, s);                                 // q = A w
+  hipLaunchKernelGGL(rsub_kernel, g, bl, 0, s, r, c->q, n);              // q = r - A Q r
+  vcycle(h, 0, K, c->q, z, s);                                           // z = M q
+  coupled_spmv(h, K, tr, z, c->q, s);                                    // q = A z
+  coupled_coarse(h, tr, c->q, c->v, s);                                  // v = Q A z
+  hipLaunchKernelGGL(axpby_kernel, g, bl, 0, s, -1.0, c->v, 1.0, z, n);  // z -= Q A z
+  hipLaunchKernelGGL(axpby_kernel, g, bl, 0, s, 1.0, c->w, 1.0, z, n);   // z += Q r
 }
 }  // namespace fcg_amgs
 

@@ -786,7 +786,14 @@ def main():
                     help="committed PMC file to fall back on (default: newest profiles/pmc_rNN_vM.json)")
     ap.add_argument("--no-gather", action="store_true",
                     help="skip the unstructured (renumbered) hex8 line")
+    ap.add_argument("--only-primary", action="store_true",
+                    help="the primary line alone (no secondary lines, no CPU baseline, no counter "
+                         "passes): the command whose rocprofv3 kernel statistics are committed")
     args = ap.parse_args()
+    if args.only_primary:
+        for k in ("no_cpu_baseline", "no_hex27", "no_tsi", "no_newton", "no_amg", "no_optionb",
+                  "no_host", "no_pmc", "no_gather"):
+            setattr(args, k, True)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
