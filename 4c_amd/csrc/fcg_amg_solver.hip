@@ -365,15 +365,23 @@ void apply_A0(fcg_amg* h, const double* K, const double* x, double* y, hipStream
 }
 
 // a level's operator and smoother pieces: l = 0 the context, l >= 1 levels[l - 1]
+void coupled_spmv(fcg_amg* h, const double* K, const fcg_transport* tr, const double* x, double* y, hipStream_t s);
+double& coupled_lmax0_ref(fcg_amg* h);
+
 struct Ops {
   fcg_amg* h;
   int l;
   const double* K;  // level 0 values
   hipStream_t s;
+  // level 0 of a rank-local handle with coupled coarse levels: the global operator (import + the
+  // rank's SpMV) and its lambda_max instead of the owned block's
+  const fcg_transport* tr = nullptr;
   int64_t n() const { return l == 0 ? h->n0 : h->levels[size_t(l - 1)].A.n * 6; }
   void spmv(const double* x, double* y) const
   {
-    if (l == 0)
+    if (l == 0 && tr)
+      coupled_spmv(h, K, tr, x, y, s);
+    else if (l == 0)
       apply_A0(h, K, x, y, s);
     else
     {
@@ -392,7 +400,7 @@ struct Ops {
           "fcg_bsr_block_jacobi_apply");
     }
   }
-  double& lmax() const { return l == 0 ? h->lmax0 : h->levels[size_t(l - 1)].lmax; }
+  double& lmax() const { return l == 0 ? (tr ? coupled_lmax0_ref(h) : h->lmax0) : h->levels[size_t(l - 1)].lmax; }
   double* r() const { return l == 0 ? h->r0 : h->levels[size_t(l - 1)].r; }
   double* d() const { return l == 0 ? h->d0 : h->levels[size_t(l - 1)].d; }
   double* z() const { return l == 0 ? h->z0 : h->levels[size_t(l - 1)].z; }
@@ -400,12 +408,22 @@ struct Ops {
   double* q() const { return l == 0 ? h->q0 : h->levels[size_t(l - 1)].q; }
 };
 
-// largest eigenvalue of D^-1 A from a 10-step Lanczos (block-Jacobi CG on a random vector)
+// largest eigenvalue of D^-1 A from a 10-step Lanczos (block-Jacobi CG on a random vector); with
+// o.tr the operator is the global one and the inner products are summed over the ranks
 void estimate_lmax(const Ops& o)
 {
   fcg_amg* h = o.h;
   const int64_t n = o.n();
   double *b = o.d(), *r = o.r(), *z = o.z(), *p = o.p(), *q = o.q();
+  auto dot_host = [&](fcg_amg* hh, const double* x, const double* y, int64_t nn, hipStream_t ss) {
+    if (!o.tr) return fcg_amgs::dot_host(hh, x, y, nn, ss);
+    dot_dev(hh, x, y, nn, hh->sc + 6, ss);
+    ck(o.tr->allreduce_fn(o.tr->user, hh->sc + 6, 1, ss), "transport all-reduce (Lanczos)");
+    double v = 0.0;
+    ck(hipMemcpyAsync(&v, hh->sc + 6, sizeof(double), hipMemcpyDeviceToHost, ss), "hipMemcpyAsync");
+    ck(hipStreamSynchronize(ss), "hipStreamSynchronize");
+    return v;
+  };
   hipLaunchKernelGGL(random_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, o.s, b, o.l == 0 ? h->mask0 : nullptr, n, 20251015u);
   ck(hipMemcpyAsync(r, b, sizeof(double) * size_t(n), hipMemcpyDeviceToDevice, o.s), "copy");
   o.dinv(r, z, 1.0, false);
@@ -666,13 +684,10 @@ void run_fcg(fcg_amg* h, const double* K, const double* b, double* x, double rto
 //   * this rank's rows of A_1 = Pt_0 (A_full P_ext) by the block SpGEMM on host-built patterns;
 //   * the rows of all ranks are summed into one zero-padded buffer (the transport's all-reduce),
 //     patterns once, values per tangent;
-//   * application: the balancing two-level form z = Q r + (I - Q A) M (I - A Q) r with
-//     Q = P_0 A_1^-1 P_0^T (restriction into the global level-1 vector, all-reduce, the replicated
-//     hierarchy's V-cycle, prolongation of this rank's aggregates) and M the rank-local V-cycle;
-//     two imports + SpMVs of the global operator per application.  (A multiplicative cycle with
-//     rank-local post-smoothing was tried first: its residual after the coarse correction is the
-//     global one but the smoother's the local one, and the result was indefinite on the first
-//     2-rank solve.)
+//   * application: one V-cycle of the global system -- Chebyshev on the global operator (each of
+//     its SpMVs one import + the rank's rows; lambda_max by a Lanczos over the ranks), the
+//     residual restricted into the global level-1 vector (all-reduce), the replicated hierarchy,
+//     prolongation of this rank's aggregates, Chebyshev again (coupled_apply).
 struct DevBuf {
   double* p = nullptr;
   explicit DevBuf(int64_t n) { ck(hipMalloc(&p, sizeof(double) * size_t(std::max<int64_t>(1, n))), "hipMalloc"); }
@@ -691,10 +706,12 @@ struct Coupled {
   Bsr AP;                          // owned block rows x global aggregates (3 x 6)
   Bsr A1r;                         // this rank's aggregates x global aggregates (6 x 6)
   int64_t a1_first = 0, a1_nnzb = 0;  // this rank's first block in the global A_1; its block count
-  double *chan = nullptr, *chan_col = nullptr, *q = nullptr, *w = nullptr, *v = nullptr, *gb = nullptr,
-         *ge = nullptr;
+  double *chan = nullptr, *chan_col = nullptr, *q = nullptr, *w = nullptr, *gb = nullptr, *ge = nullptr;
   fcg_amg* g = nullptr;            // the replicated hierarchy: g->levels[0].A = the global A_1
+  double lmax0 = 0.0;              // lambda_max of D^-1 A for the global operator (Chebyshev)
 };
+
+double& coupled_lmax0_ref(fcg_amg* h) { return h->cpl->lmax0; }
 
 // element-wise sum over the ranks of a host vector, through the transport's device all-reduce
 void host_allsum(const fcg_transport* tr, std::vector<double>& v, hipStream_t s)
@@ -763,7 +780,6 @@ void coupled_build(fcg_amg* h, const fcg_transport* tr, hipStream_t s)
   c->chan_col = dalloc<double>(h, m.n_cols);
   c->q = dalloc<double>(h, 3 * nb0);
   c->w = dalloc<double>(h, 3 * nb0);
-  c->v = dalloc<double>(h, 3 * nb0);
   c->gb = dalloc<double>(h, 6 * c->n_agg_tot);
   c->ge = dalloc<double>(h, 6 * c->n_agg_tot);
   // the ghost rows' aggregate ids, one channel per block slot
@@ -883,6 +899,8 @@ void coupled_setup(fcg_amg* h, const double* K, const fcg_transport* tr, hipStre
       "coupled AMG level 1: singular diagonal block");
   if (g->steps.size() > 1) estimate_lmax(Ops{g, 1, nullptr, s});
   galerkin_from(g, 1, nullptr, s);
+  // the level-0 smoother runs on the global operator: its lambda_max from a Lanczos over the ranks
+  estimate_lmax(Ops{h, 0, K, s, tr});
 }
 
 // Q x = P_0 A_1^-1 P_0^T x over all ranks: restriction of this rank's rows into its segment of the
@@ -909,25 +927,26 @@ void coupled_spmv(fcg_amg* h, const double* K, const fcg_transport* tr, const do
   ck(fcg_spmv(h->ctx, K, c->chan_col, y, s), "fcg_spmv");
 }
 
-// The balancing (BNN) two-level preconditioner of the global system,
-//   z = Q r + (I - Q A) M (I - A Q) r,   Q = P_0 A_1^-1 P_0^T,  M = the rank-local V-cycle
-// (symmetric positive definite for SPD A and M: the rank-local hierarchy's smoothing and coarse
-// levels act on the owned block, the coupled level 1 on the global operator)
+// One V-cycle of the global system: Chebyshev smoothing with the global operator (D = the owned
+// nodal blocks, lambda_max of the global D^-1 A), the residual restricted by this rank's P_0 into
+// the global level 1, the replicated hierarchy there, prolongation, Chebyshev again -- the
+// single-rank cycle, with P_0 from the rank-local aggregation.  (Tried before: a multiplicative
+// cycle with rank-local smoothing, indefinite; the balancing form Q r + (I - Q A) M (I - A Q) r with
+// M the rank-local V-cycle, 64 FCG iterations against 33 on one rank for the 2-rank test box.)
 void coupled_apply(fcg_amg* h, const double* K, const fcg_transport* tr, const double* r, double* z,
     hipStream_t s)
 {
   Coupled* c = h->cpl;
   const int64_t n = h->n0;
-  const dim3 g(blocks_for(n)), bl(kBlock);
-  coupled_coarse(h, tr, r, c->w, s);                                     // w = Q r
-  coupled_spmv(h, K, tr, c->w, c->q, s);                                 // q = A w
-  hipLaunchKernelGGL(rsub_kernel, g, bl, 0, s, r, c->q, n);              // q = r - A Q r
-  vcycle(h, 0, K, c->q, z, s);                                           // z = M q
-  coupled_spmv(h, K, tr, z, c->q, s);                                    // q = A z
-  coupled_coarse(h, tr, c->q, c->v, s);                                  // v = Q A z
-  hipLaunchKernelGGL(axpby_kernel, g, bl, 0, s, -1.0, c->v, 1.0, z, n);  // z -= Q A z
-  hipLaunchKernelGGL(axpby_kernel, g, bl, 0, s, 1.0, c->w, 1.0, z, n);   // z += Q r
+  const Ops o{h, 0, K, s, tr};
+  cheb(h, o, r, z, true);
+  coupled_spmv(h, K, tr, z, c->q, s);
+  hipLaunchKernelGGL(rsub_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, s, r, c->q, n);
+  coupled_coarse(h, tr, c->q, c->w, s);
+  hipLaunchKernelGGL(axpby_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, s, 1.0, c->w, 1.0, z, n);
+  cheb(h, o, r, z, false);
 }
+
 }  // namespace fcg_amgs
 
 extern "C" {
