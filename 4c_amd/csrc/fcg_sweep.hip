@@ -402,7 +402,11 @@ __device__ inline void sweep_visit(const SH& sh, int slot, int a, int b1, int b2
   // compiler otherwise issues each pair's loads after the previous pair's FMAs and waits for them,
   // an exposed LDS round trip per pair at two waves per SIMD).  +47 VGPRs (189 -> 236, still two
   // workgroups per CU); the TSI instantiations would spill, they keep the plain loop.
+#ifdef FCG_VISIT_PIPE_TSI
+  if constexpr (true)
+#else
   if constexpr (!TSI)
+#endif
   {
   double2 buf[2][9];
   load_p(0, buf[0]);
