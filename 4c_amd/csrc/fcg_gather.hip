@@ -749,7 +749,13 @@ hipError_t launch_gather_h8(const DeviceMesh& m, const double* d_u_col, bool wan
   a.mat = StVK{m.lambda, m.mu, m.cdiag};
   // one-wave workgroups, as many as the LDS keeps resident on every CU, a multiple of the 8 XCDs,
   // each a contiguous block of records / nodes
-  const int64_t want = int64_t(256) * 8;  // two waves per SIMD (VGPRs), LDS fits nine
+  // workgroups per CU: linear kinematics (158 VGPRs since the Gauss-point factors are precomputed:
+  // three waves per SIMD by registers) as many as the LDS keeps resident (16.2 KB each: nine);
+  // TotLag (220 VGPRs) two waves per SIMD
+#ifndef FCG_GATHER_WPC_LINEAR
+#define FCG_GATHER_WPC_LINEAR 9
+#endif
+  const int64_t want = int64_t(256) * (m.kinem == 0 ? FCG_GATHER_WPC_LINEAR : 8);
   const dim3 block{64, 1, 1};
   auto grid_of = [&](int64_t work) {
     return dim3{static_cast<unsigned>(std::max<int64_t>(8, std::min<int64_t>(want, (work + 7) / 8 * 8))), 1, 1};
