@@ -174,8 +174,21 @@ __global__ __launch_bounds__(64, 2) void gather_h8_kernel(GatherArgs A)
   const int64_t rank = blockIdx.x >> 3;
   const int64_t chunk = (nwork + 7) / 8;
   const int64_t x0 = min(nwork, int64_t(xcd) * chunk), x1 = min(nwork, x0 + chunk);
+  // nodes with <= 8 elements: the XCD's workgroups take its records round robin (workgroup k
+  // records x0 + k, x0 + k + per_xcd, ...), so that at any time they work on neighbouring row nodes
+  // (Morton order) and share the elements' data in the XCD's L2 -- with a contiguous block each,
+  // 256 workgroups streamed 256 separate regions through 4 MB of L2 and re-fetched every element's
+  // Gauss-point factors for each of its row nodes.  Nodes with more records (MULTI) keep one
+  // contiguous block of nodes each.
   const int64_t sub = (x1 - x0 + per_xcd - 1) / per_xcd;
-  const int64_t n0 = min(x1, x0 + rank * sub), n1 = min(x1, n0 + sub);
+#ifdef FCG_GATHER_CONTIGUOUS
+  constexpr bool RR = false;  // A/B probe: one contiguous block of records per workgroup
+#else
+  constexpr bool RR = !MULTI;
+#endif
+  const int64_t n0 = RR ? x0 + rank : min(x1, x0 + rank * sub);
+  const int64_t n1 = RR ? x1 : min(x1, n0 + sub);
+  const int64_t step = RR ? per_xcd : 1;
   const int64_t R0 = MULTI ? A.multi_ptr[n0] : n0, R1 = MULTI ? A.multi_ptr[n1] : n1;
   if (R0 >= R1) return;
 
@@ -184,7 +197,7 @@ __global__ __launch_bounds__(64, 2) void gather_h8_kernel(GatherArgs A)
   // wait counts stay static: record i's words arrive three records ahead, its element data two,
   // its displacements one, and no wait covers the stores of the record before.
   auto load_rec = [&](int64_t i) -> RecRegs {
-    const int64_t k = min(i, R1 - 1);
+    const int64_t k = min(i, R1 - 1);  // past the end: re-reads a valid record, unused
     RecRegs r;
     r.row0 = A.rec_row0[k];
     r.meta = A.rec_meta[k];
@@ -235,7 +248,7 @@ __global__ __launch_bounds__(64, 2) void gather_h8_kernel(GatherArgs A)
     negmask |= uint32_t(neg) << n;
   }
 
-  RecRegs cur = load_rec(R0), nx1 = load_rec(R0 + 1), nx2 = load_rec(R0 + 2);
+  RecRegs cur = load_rec(R0), nx1 = load_rec(R0 + step), nx2 = load_rec(R0 + 2 * step);
   double xc[3], xn1[3], uc[3], gc[10];
   int32_t dofc, dof1;
   load_x(cur, xc, dofc);
@@ -252,11 +265,11 @@ __global__ __launch_bounds__(64, 2) void gather_h8_kernel(GatherArgs A)
   // element node b = q: parametric signs (TotLag stage 3)
   const double bsx = h8_sx(q & 3), bsy = (q & 3) >= 2 ? 1.0 : -1.0, bsz = q >= 4 ? 1.0 : -1.0;
   const double bsx8 = 0.125 * bsx, bsy8 = 0.125 * bsy, bsz8 = 0.125 * bsz;
-  for (int64_t i = R0; i < R1; ++i)
+  for (int64_t i = R0; i < R1; i += step)
   {
     // in flight while this record computes: the next record's displacements, the element data of
     // the one after, the words of the third
-    const RecRegs nx3 = load_rec(i + 3);
+    const RecRegs nx3 = load_rec(i + 3 * step);
     double xn2[3], u1[3], g1[10];
     int32_t dof2;
     load_x(nx2, xn2, dof2);
@@ -749,11 +762,10 @@ hipError_t launch_gather_h8(const DeviceMesh& m, const double* d_u_col, bool wan
   a.mat = StVK{m.lambda, m.mu, m.cdiag};
   // one-wave workgroups, as many as the LDS keeps resident on every CU, a multiple of the 8 XCDs,
   // each a contiguous block of records / nodes
-  // workgroups per CU: linear kinematics (158 VGPRs since the Gauss-point factors are precomputed:
-  // three waves per SIMD by registers) as many as the LDS keeps resident (16.2 KB each: nine);
-  // TotLag (220 VGPRs) two waves per SIMD
+  // workgroups per CU: two waves per SIMD.  (Linear kinematics would fit nine by LDS and registers
+  // since the Gauss-point factors are precomputed -- measured 10 % slower: more streams in L2.)
 #ifndef FCG_GATHER_WPC_LINEAR
-#define FCG_GATHER_WPC_LINEAR 9
+#define FCG_GATHER_WPC_LINEAR 8
 #endif
   const int64_t want = int64_t(256) * (m.kinem == 0 ? FCG_GATHER_WPC_LINEAR : 8);
   const dim3 block{64, 1, 1};
