@@ -319,9 +319,9 @@ def _solve_box(celltype):
     return ((8, 4, 4), (8.0, 4.0, 4.0)) if celltype == fcg.HEX8 else ((6, 2, 2), (6.0, 2.0, 2.0))
 
 
-def _run_two_rank_solve(kinem, path, transport, solver="pcg", celltype=fcg.HEX8):
-    """The 2-rank DistributedNewton of the clamped, tip-loaded box against the 1-rank StaticNewton
-    (by DOF GID); returns the ranks' linear iteration counts."""
+def _run_two_rank_solve(kinem, path, transport, solver="pcg", celltype=fcg.HEX8, world=2):
+    """The `world`-rank DistributedNewton of the clamped, tip-loaded box against the 1-rank
+    StaticNewton (by DOF GID); returns the ranks' linear iteration counts."""
     dev = _dev()
     newton = importlib.import_module("4c_amd.newton")
     iv, up = _solve_box(celltype)
@@ -335,11 +335,11 @@ def _run_two_rank_solve(kinem, path, transport, solver="pcg", celltype=fcg.HEX8)
     ctx = mp.get_context("spawn")
     qq = ctx.Queue()
     port = 29700 + os.getpid() % 1000
-    procs = [ctx.Process(target=_worker_solve, args=(r, 2, port, qq, kinem, path, transport, solver,
-                                                     celltype)) for r in range(2)]
+    procs = [ctx.Process(target=_worker_solve, args=(r, world, port, qq, kinem, path, transport, solver,
+                                                     celltype)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [qq.get(timeout=240) for _ in range(2)]
+    res = [qq.get(timeout=240) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
     got, iters = {}, []
@@ -380,6 +380,18 @@ def test_two_ranks_native_dfcg(celltype, kinem, solver):
         print(f"FCG iterations: 1 rank {one}, 2 ranks coupled {iters[0]}, 2 ranks rank-local {unc[0]}")
         assert n2 <= 1.5 * n1, (one, iters, unc)
         assert n2 <= nu, (iters, unc)
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_many_ranks_coupled_amg_iterations(world):
+    """The coupled coarse levels at 4 and 8 ranks (host-staged on one GPU, hex8 linear box): the
+    solution by GID matches one rank, and the FCG iterations stay within 1.5x of the 1-rank AMG's
+    (the rank-local AMG grows with the rank count)."""
+    one = _one_rank_amg_iters(fcg.HEX8, fcg.LINEAR)
+    iters = _run_two_rank_solve(fcg.LINEAR, fcg.PATH_AUTO, "staged", "native", fcg.HEX8, world=world)
+    n1, nR = sum(one), sum(i or 0 for i in iters[0])
+    print(f"FCG iterations: 1 rank {one}, {world} ranks coupled {iters[0]}")
+    assert nR <= 1.5 * n1, (one, iters)
 
 
 def _one_rank_amg_iters(celltype, kinem):

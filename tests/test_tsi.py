@@ -445,6 +445,8 @@ def test_tsi_config5_eight_rank_split_full_size():
     sp = pytest.importorskip("scipy.sparse")
     n = 126
 
+    from parity_util import oracle_tsi_evaluate
+
     def run(rank, nranks):
         mesh = fcg.BoxMesh(fcg.HEX8, (n, n, n), rank=rank, nranks=nranks)
         u, v, Tn = _fields_xyz(mesh)
@@ -454,6 +456,15 @@ def test_tsi_config5_eight_rank_split_full_size():
         r = _gpu_fused(mesh, tev, ev, u, v, Tn)
         ev.close()
         tev.close()
+        if nranks > 1:
+            # the rank's four blocks and residual rows against the oracle's TSI::Monolithic loop on
+            # the same rank (its column elements, its owned rows; 16 workers)
+            err, *ref = oracle_tsi_evaluate(mesh, g, E, NU, ALPHA, T0, COND, 1.0, 1.0 / DT, u, v, Tn,
+                                            nworkers=16)
+            assert err == 0
+            for k, x in zip(("Kss", "Kst", "Kts", "Ktt", "fs", "fT"), ref):
+                tol = 1e-10 if k in ("fs", "fT") else 1e-12
+                assert _rel(r[k], x) <= tol, (rank, k, _rel(r[k], x))
         Ktt = sp.csr_matrix((r["Ktt"], g.col_tt, g.rowptr_tt), shape=(g.n_rows_t, g.n_cols_t))
         Kss = sp.csr_matrix((r["Kss"], mesh.col_lid, mesh.rowptr), shape=(mesh.n_rows, mesh.n_cols))
         Kst = sp.csr_matrix((r["Kst"], g.col_st, g.rowptr_st), shape=(mesh.n_rows, g.n_cols_t))
@@ -477,6 +488,32 @@ def test_tsi_config5_eight_rank_split_full_size():
     ok_s, ok_t = ~np.isnan(S1), ~np.isnan(T1)
     assert np.linalg.norm(S8[ok_s] - S1[ok_s]) <= 1e-12 * np.linalg.norm(S1[ok_s])
     assert np.linalg.norm(T8[ok_t] - T1[ok_t]) <= 1e-12 * np.linalg.norm(T1[ok_t])
+
+
+@pytest.mark.gpu
+def test_tsi_config5_full_size_against_oracle():
+    """Config 5's 126^3 box (2M hex8) at its stated size, one rank: the fused pass's four blocks
+    (K_SS, k_ST, k_TS, k_TT) and both residuals against the oracle's TSI::Monolithic element loop
+    on the whole mesh (orc_tsi_discretization_evaluate, 16 workers): 1e-12 / 1e-10."""
+    torch, dev = _dev()
+    from parity_util import oracle_tsi_evaluate
+    n = 126
+    mesh = fcg.BoxMesh(fcg.HEX8, (n, n, n), jitter=0.1, seed=20251015)
+    u, v, Tn = _fields_xyz(mesh)
+    ev = fcg.Evaluator(mesh, kinematics=fcg.LINEAR, youngs=E, poisson=NU, path=fcg.PATH_STRUCTURED)
+    tev = fcg.TsiEvaluator(mesh, E, NU, ALPHA, T0, COND)
+    g = tev.graph
+    r = _gpu_fused(mesh, tev, ev, u, v, Tn)
+    ev.close()
+    tev.close()
+    err, *ref = oracle_tsi_evaluate(mesh, g, E, NU, ALPHA, T0, COND, 1.0, 1.0 / DT, u, v, Tn, nworkers=16)
+    assert err == 0 and mesh.n_ele == 2_000_376
+    for k, x in zip(("Kss", "Kst", "Kts", "Ktt", "fs", "fT"), ref):
+        tol = 1e-10 if k in ("fs", "fT") else 1e-12
+        assert np.all(np.isfinite(r[k])), k
+        assert _rel(r[k], x) <= tol, (k, _rel(r[k], x))
+        if tol == 1e-12:
+            assert np.abs(r[k] - x).max() <= 1e-12 * np.abs(x).max(), k
 
 
 @pytest.mark.parametrize("nranks,nworkers", [(1, 1), (1, 4), (2, 3)])
