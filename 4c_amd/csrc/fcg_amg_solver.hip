@@ -674,20 +674,24 @@ void run_fcg(fcg_amg* h, const double* K, const double* b, double* x, double rto
 
 // ---- coarse levels coupled across ranks (fcg_dfcg_solve with a rank-local handle) -------------
 // 4C's MueLu hierarchy spans every rank (4C_linear_solver_preconditioner_muelu.cpp:97: one
-// Xpetra operator over the global matrix).  Here the aggregation and the prolongator smoothing of
-// level 0 stay rank-local (as MueLu's uncoupled aggregation), but level 1 is the Galerkin operator
-// of the GLOBAL matrix, A_1 = P_0^T A P_0 with every rank's ghost-column couplings, solved
-// redundantly on every rank by a hierarchy built from the gathered A_1:
-//   * P_0's rows of the ghost nodes come from their owners through the transport's import
-//     (fixed-width channels: the global aggregate id and the six columns of each of a row's
-//     M blocks, M the widest row over the ranks);
-//   * this rank's rows of A_1 = Pt_0 (A_full P_ext) by the block SpGEMM on host-built patterns;
-//   * the rows of all ranks are summed into one zero-padded buffer (the transport's all-reduce),
-//     patterns once, values per tangent;
+// Xpetra operator over the global matrix).  Here the aggregation stays rank-local (as MueLu's
+// uncoupled aggregation), everything else is of the GLOBAL matrix, solved redundantly on every rank
+// below level 1:
+//   * T_0's rows of the ghost nodes come from their owners through the transport's import (the
+//     global aggregate id, then the 3 x 6 block's six columns), so that the prolongator is smoothed
+//     with the global operator, P = (I - omega D^-1 A) T_ext, lambda_max of D^-1 A by a Lanczos over
+//     the ranks: P's rows near a rank boundary reach the neighbours' aggregates;
+//   * P's ghost rows the same way (fixed-width channels per block slot, M the widest row over the
+//     ranks), then this rank's part of A_1 = P^T (A_full P_ext) by the block SpGEMM on host-built
+//     patterns (A_full: the rank's whole rows, ghost columns included);
+//   * the global A_1 pattern is the union of the ranks' parts (their (row, column) pairs gathered
+//     once, sorted identically everywhere); per tangent each rank scatters its blocks into a zeroed
+//     global buffer and the transport's all-reduce sums them;
+//   * a hierarchy built from the gathered A_1 by the same aggregation code (coarsen), replicated and
+//     identical on every rank (same input, deterministic build and kernels);
 //   * application: one V-cycle of the global system -- Chebyshev on the global operator (each of
-//     its SpMVs one import + the rank's rows; lambda_max by a Lanczos over the ranks), the
-//     residual restricted into the global level-1 vector (all-reduce), the replicated hierarchy,
-//     prolongation of this rank's aggregates, Chebyshev again (coupled_apply).
+//     its SpMVs one import + the rank's rows), the residual restricted into the global level-1
+//     vector (all-reduce), the replicated hierarchy, prolongation, Chebyshev again (coupled_apply).
 struct DevBuf {
   double* p = nullptr;
   explicit DevBuf(int64_t n) { ck(hipMalloc(&p, sizeof(double) * size_t(std::max<int64_t>(1, n))), "hipMalloc"); }
@@ -700,15 +704,22 @@ struct Coupled {
   int rank = 0, nranks = 1;
   int64_t nc_nodes = 0;            // column nodes of the context (owned first, then ghosts)
   int64_t off = 0, n_agg_tot = 0;  // this rank's first global aggregate; all ranks' aggregates
-  int M = 0;                       // blocks per P_0 row, widest over the ranks
+  int M = 0;                       // blocks per row of P, widest over the ranks
   Bsr Afull;                       // owned block rows x column nodes (3 x 3)
-  Bsr Pext;                        // column nodes x global aggregates (3 x 6)
+  Bsr Text;                        // column nodes x global aggregates: T_0 rows, ghosts imported
+  Bsr AT;                          // owned block rows x global aggregates (3 x 6)
+  Bsr P;                           // owned block rows x global aggregates: (I - w D^-1 A) T
+  Bsr Pt;                          // its transpose: global aggregates x owned block rows
+  int64_t* p_perm = nullptr;       // P^T block -> P block
+  int32_t* agg = nullptr;          // [nb0] global aggregate of each owned node (-1 = none)
+  Bsr Pext;                        // column nodes x global aggregates: P rows, ghosts imported
   Bsr AP;                          // owned block rows x global aggregates (3 x 6)
-  Bsr A1r;                         // this rank's aggregates x global aggregates (6 x 6)
-  int64_t a1_first = 0, a1_nnzb = 0;  // this rank's first block in the global A_1; its block count
+  Bsr C;                           // this rank's part of A_1 = P^T A P (global rows touched)
+  int64_t* c_pos = nullptr;        // [C.nnzb] block position of each of C's blocks in the global A_1
+  int64_t a1_nnzb = 0;             // blocks of the global A_1
   double *chan = nullptr, *chan_col = nullptr, *q = nullptr, *w = nullptr, *gb = nullptr, *ge = nullptr;
   fcg_amg* g = nullptr;            // the replicated hierarchy: g->levels[0].A = the global A_1
-  double lmax0 = 0.0;              // lambda_max of D^-1 A for the global operator (Chebyshev)
+  double lmax0 = 0.0;              // lambda_max of D^-1 A for the global operator
 };
 
 double& coupled_lmax0_ref(fcg_amg* h) { return h->cpl->lmax0; }
@@ -725,8 +736,8 @@ void host_allsum(const fcg_transport* tr, std::vector<double>& v, hipStream_t s)
   ck(hipStreamSynchronize(s), "hipStreamSynchronize");
 }
 
-// channel (k, col) of P_0's rows as a DOF vector: DOF d of owned node i gets entry (d, col) of the
-// row's k-th block (col < 0: the block's global aggregate id, -1 past the row's end)
+// channel (k, col) of a 3 x 6 BSR's rows as a DOF vector: DOF d of owned node i gets entry
+// (d, col) of the row's k-th block (col < 0: the block's column id + off, -1 past the row's end)
 __global__ __launch_bounds__(kBlock) void pack_channel_kernel(int64_t nb, const int64_t* __restrict__ ptr,
     const int32_t* __restrict__ col, const double* __restrict__ vals, int k, int c, int64_t off,
     double* out)
@@ -739,7 +750,7 @@ __global__ __launch_bounds__(kBlock) void pack_channel_kernel(int64_t nb, const 
   out[t] = c < 0 ? (in ? double(int64_t(col[p]) + off) : -1.0) : (in ? vals[p * 18 + d * 6 + c] : 0.0);
 }
 
-// ... and back into P_ext's ghost rows (column nodes nb .. nc-1)
+// ... and back into the ghost rows (column nodes nb .. nc-1) of an extended BSR
 __global__ __launch_bounds__(kBlock) void scatter_channel_kernel(int64_t nb, int64_t nc,
     const int64_t* __restrict__ ptr, const double* __restrict__ in, int k, int c, double* vals)
 {
@@ -748,6 +759,88 @@ __global__ __launch_bounds__(kBlock) void scatter_channel_kernel(int64_t nb, int
   if (i >= nc) return;
   const int64_t p = ptr[i] + k;
   if (p < ptr[i + 1]) vals[p * 18 + d * 6 + c] = in[3 * i + d];
+}
+
+// out[pos[k]] = vals[k] (36 doubles per block): this rank's blocks into the global A_1 buffer
+__global__ __launch_bounds__(kBlock) void scatter_blocks_kernel(int64_t nnzb, const int64_t* __restrict__ pos,
+    const double* __restrict__ vals, double* out)
+{
+  const int64_t t = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (t >= nnzb * 36) return;
+  const int64_t k = t / 36, q = t - 36 * k;
+  out[pos[k] * 36 + q] = vals[t];
+}
+
+// the owned rows of a 3 x 6 BSR (ids + off) followed by the ghost rows' ids, imported from their
+// owners one block slot at a time (M slots); returns the extended pattern
+void extend_pattern(fcg_amg* h, Coupled* c, const Bsr& B, int64_t off, int M, const fcg_transport* tr,
+    hipStream_t s, std::vector<int64_t>& pp, std::vector<int32_t>& pc)
+{
+  const fcg::DeviceMesh& m = h->ctx->mesh;
+  const int64_t nb0 = h->nb0, nc = c->nc_nodes;
+  std::vector<std::vector<int32_t>> gid(size_t(nc - nb0));
+  std::vector<double> colv(size_t(m.n_cols));
+  const dim3 gp(blocks_for(3 * std::max<int64_t>(1, nb0))), bl(kBlock);
+  for (int k = 0; k < M; ++k)
+  {
+    hipLaunchKernelGGL(pack_channel_kernel, gp, bl, 0, s, nb0, B.ptr, B.col, B.vals, k, -1, off, c->chan);
+    ck(hipGetLastError(), "pack_channel_kernel");
+    ck(tr->import_fn(tr->user, c->chan, c->chan_col, s), "transport import (ghost row ids)");
+    ck(hipMemcpyAsync(colv.data(), c->chan_col, sizeof(double) * colv.size(), hipMemcpyDeviceToHost, s), "hipMemcpyAsync");
+    ck(hipStreamSynchronize(s), "hipStreamSynchronize");
+    for (int64_t i = nb0; i < nc; ++i)
+    {
+      const double id = colv[size_t(3 * i)];
+      if (id >= 0.0) gid[size_t(i - nb0)].push_back(int32_t(id));
+    }
+  }
+  pp.assign(size_t(nc) + 1, 0);
+  pc.clear();
+  for (int64_t i = 0; i < nb0; ++i)
+  {
+    for (int64_t k = B.ptr_h[size_t(i)]; k < B.ptr_h[size_t(i) + 1]; ++k) pc.push_back(int32_t(B.col_h[size_t(k)] + off));
+    pp[size_t(i) + 1] = int64_t(pc.size());
+  }
+  for (int64_t i = nb0; i < nc; ++i)
+  {
+    const auto& row = gid[size_t(i - nb0)];
+    for (size_t k = 1; k < row.size(); ++k)
+      if (row[k] <= row[k - 1]) throw Fail{FCG_ERR_ARG, "coupled AMG: ghost row not sorted"};
+    pc.insert(pc.end(), row.begin(), row.end());
+    pp[size_t(i) + 1] = int64_t(pc.size());
+  }
+}
+
+// the ghost rows' values of an extended BSR (pattern from extend_pattern), 6 channels per slot
+void extend_values(fcg_amg* h, Coupled* c, const Bsr& B, Bsr& E, int M, const fcg_transport* tr, hipStream_t s)
+{
+  const int64_t nb0 = h->nb0, nc = c->nc_nodes;
+  if (B.nnzb > 0)
+    ck(hipMemcpyAsync(E.vals, B.vals, sizeof(double) * size_t(B.nnzb) * 18, hipMemcpyDeviceToDevice, s), "copy");
+  const dim3 gp(blocks_for(3 * std::max<int64_t>(1, nb0))), gg(blocks_for(3 * std::max<int64_t>(1, nc - nb0))),
+      bl(kBlock);
+  for (int k = 0; k < M; ++k)
+    for (int col = 0; col < 6; ++col)
+    {
+      hipLaunchKernelGGL(pack_channel_kernel, gp, bl, 0, s, nb0, B.ptr, B.col, B.vals, k, col, int64_t(0), c->chan);
+      ck(hipGetLastError(), "pack_channel_kernel");
+      ck(tr->import_fn(tr->user, c->chan, c->chan_col, s), "transport import (ghost rows)");
+      if (nc > nb0)
+        hipLaunchKernelGGL(scatter_channel_kernel, gg, bl, 0, s, nb0, nc, E.ptr, c->chan_col, k, col, E.vals);
+      ck(hipGetLastError(), "scatter_channel_kernel");
+    }
+}
+
+int widest_over_ranks(const Bsr& B, int rank, int R, const fcg_transport* tr, hipStream_t s)
+{
+  std::vector<double> v(size_t(R), 0.0);
+  int64_t w = 0;
+  for (int64_t i = 0; i < B.n; ++i) w = std::max(w, B.ptr_h[size_t(i) + 1] - B.ptr_h[size_t(i)]);
+  v[size_t(rank)] = double(w);
+  host_allsum(tr, v, s);
+  int M = 0;
+  for (double x : v) M = std::max(M, int(x));
+  return M;
 }
 
 void coupled_build(fcg_amg* h, const fcg_transport* tr, hipStream_t s)
@@ -760,20 +853,15 @@ void coupled_build(fcg_amg* h, const fcg_transport* tr, hipStream_t s)
   c->nc_nodes = m.n_cols / 3;
   const int64_t nb0 = h->nb0, nc = c->nc_nodes, R = c->nranks;
   const Step& st0 = h->steps[0];
-  const Bsr& P = st0.P;
-  // aggregates per rank and the widest P_0 row
+  // aggregates per rank: the global numbering by rank offsets
   {
-    std::vector<double> v(size_t(2 * R), 0.0);
-    int64_t wmax = 0;
-    for (int64_t i = 0; i < P.n; ++i) wmax = std::max(wmax, P.ptr_h[size_t(i) + 1] - P.ptr_h[size_t(i)]);
+    std::vector<double> v(size_t(R), 0.0);
     v[size_t(c->rank)] = double(st0.n_agg);
-    v[size_t(R + c->rank)] = double(wmax);
     host_allsum(tr, v, s);
     for (int64_t q = 0; q < R; ++q)
     {
       if (q < c->rank) c->off += int64_t(v[size_t(q)]);
       c->n_agg_tot += int64_t(v[size_t(q)]);
-      c->M = std::max(c->M, int(v[size_t(R + q)]));
     }
   }
   c->chan = dalloc<double>(h, 3 * nb0);
@@ -782,61 +870,84 @@ void coupled_build(fcg_amg* h, const fcg_transport* tr, hipStream_t s)
   c->w = dalloc<double>(h, 3 * nb0);
   c->gb = dalloc<double>(h, 6 * c->n_agg_tot);
   c->ge = dalloc<double>(h, 6 * c->n_agg_tot);
-  // the ghost rows' aggregate ids, one channel per block slot
-  std::vector<std::vector<int32_t>> gid(size_t(nc - nb0));
-  std::vector<double> colv(size_t(m.n_cols));
-  const dim3 gp(blocks_for(3 * std::max<int64_t>(1, nb0))), bl(kBlock);
-  for (int k = 0; k < c->M; ++k)
-  {
-    hipLaunchKernelGGL(pack_channel_kernel, gp, bl, 0, s, nb0, P.ptr, P.col, P.vals, k, -1, c->off, c->chan);
-    ck(hipGetLastError(), "pack_channel_kernel");
-    ck(tr->import_fn(tr->user, c->chan, c->chan_col, s), "transport import (P_0 ghost ids)");
-    ck(hipMemcpyAsync(colv.data(), c->chan_col, sizeof(double) * colv.size(), hipMemcpyDeviceToHost, s), "hipMemcpyAsync");
-    ck(hipStreamSynchronize(s), "hipStreamSynchronize");
-    for (int64_t i = nb0; i < nc; ++i)
-    {
-      const double id = colv[size_t(3 * i)];
-      if (id >= 0.0) gid[size_t(i - nb0)].push_back(int32_t(id));
-    }
-  }
-  // P_ext: owned rows = P_0 with global aggregate ids, then the ghost rows as imported
-  std::vector<int64_t> pp(size_t(nc) + 1, 0);
-  std::vector<int32_t> pc;
-  for (int64_t i = 0; i < nb0; ++i)
-  {
-    for (int64_t k = P.ptr_h[size_t(i)]; k < P.ptr_h[size_t(i) + 1]; ++k) pc.push_back(int32_t(P.col_h[size_t(k)] + c->off));
-    pp[size_t(i) + 1] = int64_t(pc.size());
-  }
-  for (int64_t i = nb0; i < nc; ++i)
-  {
-    const auto& row = gid[size_t(i - nb0)];
-    for (size_t k = 0; k < row.size(); ++k)
-      if (k > 0 && row[k] <= row[k - 1]) throw Fail{FCG_ERR_ARG, "coupled AMG: ghost P_0 row not sorted"};
-    pc.insert(pc.end(), row.begin(), row.end());
-    pp[size_t(i) + 1] = int64_t(pc.size());
-  }
-  make_bsr(h, c->Pext, pp, pc, 3, 6, c->n_agg_tot);
   make_bsr(h, c->Afull, h->full_ptr, h->full_col, 3, 3, nc);
-  std::vector<int64_t> app, a1p;
-  std::vector<int32_t> apc, a1c;
-  symbolic(c->Afull, c->Pext.ptr_h, c->Pext.col_h, c->n_agg_tot, app, apc);
-  make_bsr(h, c->AP, app, apc, 3, 6, c->n_agg_tot);
-  symbolic(st0.Pt, app, apc, c->n_agg_tot, a1p, a1c);
-  make_bsr(h, c->A1r, a1p, a1c, 6, 6, c->n_agg_tot);
-  // the global A_1 pattern on every rank: row lengths, then the columns
-  std::vector<double> lens(size_t(c->n_agg_tot), 0.0);
-  for (int64_t i = 0; i < st0.n_agg; ++i) lens[size_t(c->off + i)] = double(a1p[size_t(i) + 1] - a1p[size_t(i)]);
-  host_allsum(tr, lens, s);
+  {
+    std::vector<int32_t> ag(static_cast<size_t>(nb0));
+    ck(hipMemcpy(ag.data(), st0.agg, sizeof(int32_t) * ag.size(), hipMemcpyDeviceToHost), "hipMemcpy");
+    for (auto& a : ag)
+      if (a >= 0) a = int32_t(a + c->off);
+    c->agg = upload(h, ag);
+  }
+  // T_0 with the ghost rows of its owners (one block per row), then P = (I - w D^-1 A) T_ext on
+  // the pattern of A_full T_ext: P's rows reach the neighbour ranks' aggregates
+  std::vector<int64_t> pp, ap, tp, cp;
+  std::vector<int32_t> pc, apc, tc, cc;
+  extend_pattern(h, c, st0.T, c->off, widest_over_ranks(st0.T, c->rank, int(R), tr, s), tr, s, pp, pc);
+  make_bsr(h, c->Text, pp, pc, 3, 6, c->n_agg_tot);
+  symbolic(c->Afull, c->Text.ptr_h, c->Text.col_h, c->n_agg_tot, ap, apc);
+  make_bsr(h, c->AT, ap, apc, 3, 6, c->n_agg_tot);
+  make_bsr(h, c->P, ap, apc, 3, 6, c->n_agg_tot);
+  tp.assign(size_t(c->n_agg_tot) + 1, 0);
+  tc.assign(size_t(std::max<int64_t>(ap.back(), 1)), 0);
+  std::vector<int64_t> perm(size_t(std::max<int64_t>(ap.back(), 1)));
+  ck(fcg_bsr_transpose_pattern(nb0, c->n_agg_tot, ap.data(), apc.data(), tp.data(), tc.data(), perm.data()),
+      "fcg_bsr_transpose_pattern");
+  tc.resize(size_t(ap.back()));
+  perm.resize(size_t(ap.back()));
+  make_bsr(h, c->Pt, tp, tc, 6, 3, nb0);
+  c->p_perm = upload(h, perm);
+  // P's ghost rows from their owners, then this rank's part of A_1 = P^T (A P)
+  c->M = widest_over_ranks(c->P, c->rank, int(R), tr, s);
+  extend_pattern(h, c, c->P, 0, c->M, tr, s, pp, pc);
+  make_bsr(h, c->Pext, pp, pc, 3, 6, c->n_agg_tot);
+  symbolic(c->Afull, c->Pext.ptr_h, c->Pext.col_h, c->n_agg_tot, ap, apc);
+  make_bsr(h, c->AP, ap, apc, 3, 6, c->n_agg_tot);
+  symbolic(c->Pt, ap, apc, c->n_agg_tot, cp, cc);
+  make_bsr(h, c->C, cp, cc, 6, 6, c->n_agg_tot);
+  // the global A_1 pattern = the union of the ranks' parts: every rank's (row, column) pairs
+  // gathered (counts, then the pairs in rank order), sorted and deduplicated identically everywhere
+  std::vector<int64_t> keys;
+  {
+    std::vector<double> cnt(size_t(R), 0.0);
+    cnt[size_t(c->rank)] = double(cc.size());
+    host_allsum(tr, cnt, s);
+    int64_t first = 0, total = 0;
+    for (int64_t q = 0; q < R; ++q)
+    {
+      if (q < c->rank) first += int64_t(cnt[size_t(q)]);
+      total += int64_t(cnt[size_t(q)]);
+    }
+    std::vector<double> pairs(size_t(2 * total), 0.0);
+    for (int64_t i = 0; i < c->n_agg_tot; ++i)
+      for (int64_t k = cp[size_t(i)]; k < cp[size_t(i) + 1]; ++k)
+      {
+        pairs[size_t(2 * (first + k))] = double(i);
+        pairs[size_t(2 * (first + k) + 1)] = double(cc[size_t(k)]);
+      }
+    host_allsum(tr, pairs, s);
+    keys.resize(size_t(total));
+    for (int64_t k = 0; k < total; ++k)
+      keys[size_t(k)] = int64_t(pairs[size_t(2 * k)]) * c->n_agg_tot + int64_t(pairs[size_t(2 * k + 1)]);
+    std::sort(keys.begin(), keys.end());
+    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+  }
+  c->a1_nnzb = int64_t(keys.size());
   std::vector<int64_t> gptr(size_t(c->n_agg_tot) + 1, 0);
-  for (int64_t i = 0; i < c->n_agg_tot; ++i) gptr[size_t(i) + 1] = gptr[size_t(i)] + int64_t(lens[size_t(i)]);
-  c->a1_first = gptr[size_t(c->off)];
-  c->a1_nnzb = gptr.back();
-  std::vector<double> cols(size_t(c->a1_nnzb), 0.0);
-  for (size_t k = 0; k < a1c.size(); ++k) cols[size_t(c->a1_first) + k] = double(a1c[k]);
-  host_allsum(tr, cols, s);
-  std::vector<int32_t> gcol(cols.size());
-  for (size_t k = 0; k < cols.size(); ++k) gcol[k] = int32_t(cols[k]);
-  // level 1's near-null space: the ranks' R factors of step 0
+  std::vector<int32_t> gcol(keys.size());
+  for (size_t k = 0; k < keys.size(); ++k)
+  {
+    gptr[size_t(keys[k] / c->n_agg_tot) + 1] += 1;
+    gcol[k] = int32_t(keys[k] % c->n_agg_tot);
+  }
+  for (int64_t i = 0; i < c->n_agg_tot; ++i) gptr[size_t(i) + 1] += gptr[size_t(i)];
+  {
+    std::vector<int64_t> pos(cc.size());
+    for (int64_t i = 0; i < c->n_agg_tot; ++i)
+      for (int64_t k = cp[size_t(i)]; k < cp[size_t(i) + 1]; ++k)
+        pos[size_t(k)] = int64_t(std::lower_bound(keys.begin(), keys.end(), i * c->n_agg_tot + cc[size_t(k)]) - keys.begin());
+    c->c_pos = upload(h, pos);
+  }
+  // level 1's near-null space: each aggregate's R factor from its owner
   std::vector<double> ns(size_t(36 * c->n_agg_tot), 0.0);
   std::copy(h->ns1.begin(), h->ns1.end(), ns.begin() + 36 * c->off);
   host_allsum(tr, ns, s);
@@ -846,7 +957,7 @@ void coupled_build(fcg_amg* h, const fcg_transport* tr, hipStream_t s)
   g->ctx = h->ctx;
   g->device = h->device;
   g->opt = h->opt;
-  g->steps.emplace_back();  // step 0 (level 0 -> 1) is the ranks' own P_0
+  g->steps.emplace_back();  // step 0 (level 0 -> 1) is the ranks' P
   g->levels.emplace_back();
   {
     Level& L1 = g->levels[0];
@@ -861,62 +972,52 @@ void coupled_build(fcg_amg* h, const fcg_transport* tr, hipStream_t s)
   g->flag = dalloc<int32_t>(g, 1);
 }
 
-// numeric part per tangent, after the local setup (P_0's values for this K)
+// numeric part per tangent, after the local setup (T_0, the nodal block inverses)
 void coupled_setup(fcg_amg* h, const double* K, const fcg_transport* tr, hipStream_t s)
 {
   Coupled* c = h->cpl;
   const fcg::DeviceMesh& m = h->ctx->mesh;
   const Step& st0 = h->steps[0];
-  const Bsr& P = st0.P;
-  const int64_t nb0 = h->nb0, nc = c->nc_nodes;
+  const int64_t nb0 = h->nb0;
   ck(fcg_bsr_from_node_csr(h->device, nb0, m.rowptr, c->Afull.ptr, K, c->Afull.vals, s), "fcg_bsr_from_node_csr (full rows)");
-  if (P.nnzb > 0)
-    ck(hipMemcpyAsync(c->Pext.vals, P.vals, sizeof(double) * size_t(P.nnzb) * 18, hipMemcpyDeviceToDevice, s), "copy");
-  const dim3 gp(blocks_for(3 * std::max<int64_t>(1, nb0))), gg(blocks_for(3 * std::max<int64_t>(1, nc - nb0))),
-      bl(kBlock);
-  for (int k = 0; k < c->M; ++k)
-    for (int col = 0; col < 6; ++col)
-    {
-      hipLaunchKernelGGL(pack_channel_kernel, gp, bl, 0, s, nb0, P.ptr, P.col, P.vals, k, col, c->off, c->chan);
-      ck(hipGetLastError(), "pack_channel_kernel");
-      ck(tr->import_fn(tr->user, c->chan, c->chan_col, s), "transport import (P_0 ghost rows)");
-      if (nc > nb0)
-        hipLaunchKernelGGL(scatter_channel_kernel, gg, bl, 0, s, nb0, nc, c->Pext.ptr, c->chan_col, k, col, c->Pext.vals);
-      ck(hipGetLastError(), "scatter_channel_kernel");
-    }
+  // lambda_max of the global D^-1 A (Lanczos over the ranks): the smoother's and P's
+  estimate_lmax(Ops{h, 0, K, s, tr});
+  extend_values(h, c, st0.T, c->Text, 1, tr, s);
+  ck(fcg_bsr_spgemm(h->device, 3, 3, 6, nb0, c->Afull.ptr, c->Afull.col, c->Afull.vals, c->Text.ptr,
+         c->Text.col, c->Text.vals, c->AT.ptr, c->AT.col, c->AT.vals, s), "fcg_bsr_spgemm (A T_ext)");
+  ck(fcg_amg_smooth_prolongator(h->device, 3, nb0, c->P.ptr, c->P.col, c->agg, st0.tent, h->A0_dinv,
+         c->AT.vals, h->opt.omega / c->lmax0, c->P.vals, s), "fcg_amg_smooth_prolongator (global)");
+  ck(fcg_bsr_transpose_values(h->device, 3, 6, c->P.nnzb, c->p_perm, c->P.vals, c->Pt.vals, s),
+      "fcg_bsr_transpose_values");
+  extend_values(h, c, c->P, c->Pext, c->M, tr, s);
   ck(fcg_bsr_spgemm(h->device, 3, 3, 6, nb0, c->Afull.ptr, c->Afull.col, c->Afull.vals, c->Pext.ptr,
          c->Pext.col, c->Pext.vals, c->AP.ptr, c->AP.col, c->AP.vals, s), "fcg_bsr_spgemm (A P_ext)");
-  ck(fcg_bsr_spgemm(h->device, 6, 3, 6, st0.Pt.n, st0.Pt.ptr, st0.Pt.col, st0.Pt.vals, c->AP.ptr,
-         c->AP.col, c->AP.vals, c->A1r.ptr, c->A1r.col, c->A1r.vals, s), "fcg_bsr_spgemm (P^T A P)");
+  ck(fcg_bsr_spgemm(h->device, 6, 3, 6, c->Pt.n, c->Pt.ptr, c->Pt.col, c->Pt.vals, c->AP.ptr, c->AP.col,
+         c->AP.vals, c->C.ptr, c->C.col, c->C.vals, s), "fcg_bsr_spgemm (P^T A P)");
   fcg_amg* g = c->g;
   Level& L1 = g->levels[0];
   ck(hipMemsetAsync(L1.A.vals, 0, sizeof(double) * size_t(std::max<int64_t>(1, c->a1_nnzb)) * 36, s), "memset");
-  if (c->A1r.nnzb > 0)
-    ck(hipMemcpyAsync(L1.A.vals + c->a1_first * 36, c->A1r.vals, sizeof(double) * size_t(c->A1r.nnzb) * 36,
-           hipMemcpyDeviceToDevice, s), "copy");
+  if (c->C.nnzb > 0)
+    hipLaunchKernelGGL(scatter_blocks_kernel, dim3(blocks_for(c->C.nnzb * 36)), dim3(kBlock), 0, s, c->C.nnzb,
+        c->c_pos, c->C.vals, L1.A.vals);
+  ck(hipGetLastError(), "scatter_blocks_kernel");
   ck(tr->allreduce_fn(tr->user, L1.A.vals, c->a1_nnzb * 36, s), "transport all-reduce (A_1)");
   ck(fcg_bsr_block_jacobi_setup(g->device, 6, L1.A.n, L1.A.ptr, L1.diag, L1.A.vals, L1.dinv, g->flag, s),
       "coupled AMG level 1: singular diagonal block");
   if (g->steps.size() > 1) estimate_lmax(Ops{g, 1, nullptr, s});
   galerkin_from(g, 1, nullptr, s);
-  // the level-0 smoother runs on the global operator: its lambda_max from a Lanczos over the ranks
-  estimate_lmax(Ops{h, 0, K, s, tr});
 }
 
-// Q x = P_0 A_1^-1 P_0^T x over all ranks: restriction of this rank's rows into its segment of the
-// global level-1 vector, the all-reduce, the replicated hierarchy's V-cycle, prolongation of this
-// rank's aggregates (overwrites y)
+// Q x = P A_1^-1 P^T x over all ranks: this rank's rows restricted into the global level-1 vector
+// (every rank adds to the aggregates its rows reach), the all-reduce, the replicated hierarchy's
+// V-cycle, prolongation into this rank's rows (overwrites y)
 void coupled_coarse(fcg_amg* h, const fcg_transport* tr, const double* x, double* y, hipStream_t s)
 {
   Coupled* c = h->cpl;
-  const Step& st0 = h->steps[0];
-  ck(hipMemsetAsync(c->gb, 0, sizeof(double) * size_t(std::max<int64_t>(1, 6 * c->n_agg_tot)), s), "memset");
-  ck(fcg_bsr_spmv(h->device, 6, 3, st0.Pt.n, st0.Pt.ptr, st0.Pt.col, st0.Pt.vals, x, c->gb + 6 * c->off,
-         1.0, 0, s), "restriction");
+  ck(fcg_bsr_spmv(h->device, 6, 3, c->Pt.n, c->Pt.ptr, c->Pt.col, c->Pt.vals, x, c->gb, 1.0, 0, s), "restriction");
   ck(tr->allreduce_fn(tr->user, c->gb, 6 * c->n_agg_tot, s), "transport all-reduce (level 1)");
   vcycle(c->g, 1, nullptr, c->gb, c->ge, s);
-  ck(fcg_bsr_spmv(h->device, 3, 6, st0.P.n, st0.P.ptr, st0.P.col, st0.P.vals, c->ge + 6 * c->off, y, 1.0, 0, s),
-      "prolongation");
+  ck(fcg_bsr_spmv(h->device, 3, 6, c->P.n, c->P.ptr, c->P.col, c->P.vals, c->ge, y, 1.0, 0, s), "prolongation");
 }
 
 // y = A x with the global operator: the import of x into the column map, the rank's SpMV
