@@ -41,7 +41,7 @@ NATIVE = os.path.join(CXX, "_build", "config3_native")
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,ranks", [(8, 2), (40, 2)])
+@pytest.mark.parametrize("n,ranks", [(8, 2), (40, 2), (32, 4)])
 def test_config3_native_cxx_host(n, ranks):
     """BASELINE config 3's problem (hex27 StVK TotLag cube, x- clamped, traction -1 on x+) solved by
     a C++ host through the C ABI alone (tests/cxx/config3_native.cpp): Newton with fcg_dfcg_solve
