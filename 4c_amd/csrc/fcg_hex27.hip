@@ -952,6 +952,278 @@ __global__ __launch_bounds__(64) void h27_assemble_kernel(H27AsmArgs A)
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Matrix-free tangent action y = K(u) x (fcg_tangent_apply): the operator the assembled tangent
+// of this element would apply, B^T C B + K_geo over the Gauss points (calc_lib.hpp:872-927),
+// without forming the element or global matrix.  At Gauss point g with H = grad_X x:
+//   linear  P = fac C sym(H)                                  (F = I, no geometric part)
+//   TotLag  P = fac (F C sym(F^T H) + H S),  S = C E(u)       (material + geometric part)
+// and y_a = sum_g P N_XYZ_a = sum_g (P J^-1) dN_a(xi_g) -- the same folding as f_a = sum_g R_g d_a
+// in emit_f.  One workgroup pass takes kApE elements: lanes (element, Gauss point) form J,
+// du/dxi and dx/dxi from the element's nodal X | u | x in LDS and the shape derivatives built
+// from the 1-D Lagrange factors of their point (registers, no table reads), then Q = P J^-1 into
+// LDS; lanes (element, node) sum Q_g dN_a(xi_g) over the points and write y_a at the node's
+// incidence; h27_inc_sum_kernel adds a row node's incidences in incidence order.  Per element
+// 81 + 81 doubles of X, u (TotLag) and x are read instead of the 6,561 stored entries an SpMV
+// with the assembled element matrices reads.
+constexpr int kApE = 9;  // elements per workgroup pass (243 of 256 lanes)
+__constant__ double c_L1[9], c_dL1[9];  // 1-D Lagrange L_p(x_m), L'_p(x_m) at the rule's points: [3 m + p]
+
+struct H27ApplyArgs {
+  int64_t n_ele;
+  const int32_t* ele_nodes;
+  const double* node_x;
+  const int32_t* node_dof_col;
+  const double* u_col;
+  const double* x_col;
+  const int32_t* inc_of;
+  double* ye;  // [n_inc][3]
+  double lambda, mu, cdiag;
+};
+
+template <int KIN>
+__global__ __launch_bounds__(256, 2) void h27_apply_kernel(H27ApplyArgs A)
+{
+  __shared__ double nd[kApE][3][81];  // X | u | x of the pass's elements (node-major xyz)
+  __shared__ double Qs[kApE][27][9];  // Q = P J^-1 per Gauss point, row-major 3 x 3
+  __shared__ double tL[9], tdL[9];    // c_L1, c_dL1
+  __shared__ uint8_t lat[27];         // node (= Gauss point) at lattice position i0 + 3 i1 + 9 i2
+  const int tid = threadIdx.x;
+  if (tid < 9)
+  {
+    tL[tid] = c_L1[tid];
+    tdL[tid] = c_dL1[tid];
+  }
+  if (tid < 27) lat[tid] = c_latnode[tid];
+  const bool act = tid < 27 * kApE;
+  const int s = tid / 27, g = tid - 27 * s;  // (element slot, Gauss point | node)
+  // lattice position of this lane's Gauss point g (gauss phase) = of its node a = g (node phase)
+  const uint32_t pg = c_loc[act ? g : 0];
+  const int p0 = pg & 3, p1 = (pg >> 2) & 3, p2 = pg >> 4;
+  const double w = c_w[act ? g : 0];
+  const double lam = A.lambda, mu = A.mu, cd = A.cdiag;
+  constexpr int NSRC = KIN == 0 ? 2 : 3;  // X | x (linear) or X | u | x
+  constexpr int NLD = (kApE * 81 * NSRC + 255) / 256;
+  double pre[NLD];
+  auto load = [&](int64_t e0) {
+#pragma unroll
+    for (int q = 0; q < NLD; ++q)
+    {
+      const int t = tid + 256 * q;
+      pre[q] = 0.0;
+      if (t >= kApE * 81 * NSRC) continue;
+      const int sl = t / (81 * NSRC), r = t - 81 * NSRC * sl;
+      const int src = r / 81, rr = r - 81 * src, a = rr / 3, d = rr - 3 * a;
+      const int64_t e = e0 + sl;
+      if (e0 < 0 || e >= A.n_ele) continue;
+      const int32_t node = A.ele_nodes[e * 27 + a];
+      const double* base = src == 0 ? A.node_x : (src == NSRC - 1 ? A.x_col : A.u_col);
+      pre[q] = src == 0 ? base[3 * int64_t(node) + d] : base[A.node_dof_col[node] + d];
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int q = 0; q < NLD; ++q)
+    {
+      const int t = tid + 256 * q;
+      if (t >= kApE * 81 * NSRC) continue;
+      const int sl = t / (81 * NSRC), r = t - 81 * NSRC * sl;
+      const int src = r / 81, rr = r - 81 * src;
+      nd[sl][src == NSRC - 1 ? 2 : src][rr] = pre[q];
+    }
+  };
+  const int64_t stride = int64_t(gridDim.x) * kApE;
+  int64_t e0 = int64_t(blockIdx.x) * kApE;
+  load(e0 < A.n_ele ? e0 : -1);
+  for (; e0 < A.n_ele; e0 += stride)
+  {
+    store();
+    __syncthreads();
+    load(e0 + stride < A.n_ele ? e0 + stride : -1);  // next pass's gathers in flight
+    const int64_t e = e0 + s;
+    if (act && e < A.n_ele)
+    {
+      // J (col-major, J[d + 3k] = dX_k/dxi_d), du_i/dxi_d and dx_i/dxi_d at point g.  Nodes by
+      // lattice position (i0, i1, i2): the 1-D factors of the point along x in registers, along y
+      // and z read per (i1, i2); the products in shape_deriv's order (fcg_shape.hpp), so dN is
+      // the element kernel's table value bit for bit.
+      double J[9], Gu[9], Gx[9];
+#pragma unroll
+      for (int q = 0; q < 9; ++q) J[q] = Gu[q] = Gx[q] = 0.0;
+      double Lx[3], dLx[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+      {
+        Lx[i] = tL[3 * p0 + i];
+        dLx[i] = tdL[3 * p0 + i];
+      }
+#pragma unroll 1
+      for (int i12 = 0; i12 < 9; ++i12)
+      {
+        const int i1 = i12 % 3, i2 = i12 / 3;
+        const double Ly = tL[3 * p1 + i1], dLy = tdL[3 * p1 + i1];
+        const double Lz = tL[3 * p2 + i2], dLz = tdL[3 * p2 + i2];
+        const double yz = Ly * Lz;
+#pragma unroll
+        for (int i0 = 0; i0 < 3; ++i0)
+        {
+          const int c = lat[i0 + 3 * i12];
+          const double d0 = yz * dLx[i0];
+          const double d1 = Lx[i0] * Lz * dLy;
+          const double d2 = Lx[i0] * Ly * dLz;
+#pragma unroll
+          for (int k = 0; k < 3; ++k)
+          {
+            const double xk = nd[s][0][3 * c + k], vk = nd[s][2][3 * c + k];
+            J[3 * k + 0] += d0 * xk;
+            J[3 * k + 1] += d1 * xk;
+            J[3 * k + 2] += d2 * xk;
+            Gx[3 * k + 0] += d0 * vk;
+            Gx[3 * k + 1] += d1 * vk;
+            Gx[3 * k + 2] += d2 * vk;
+            if (KIN == 1)
+            {
+              const double uk = nd[s][1][3 * c + k];
+              Gu[3 * k + 0] += d0 * uk;
+              Gu[3 * k + 1] += d1 * uk;
+              Gu[3 * k + 2] += d2 * uk;
+            }
+          }
+        }
+      }
+      double iJ[9];
+#pragma unroll
+      for (int q = 0; q < 9; ++q) iJ[q] = J[q];
+      const double fac = inv3(iJ) * w;  // det == 0 was reported by the evaluate of this state
+      // grad_X of x and u: H(i, j) = sum_k J^-1(j, k) d(.)_i / dxi_k
+      double Hx[3][3], F[3][3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+        {
+          Hx[i][j] = iJ[j] * Gx[3 * i] + iJ[j + 3] * Gx[3 * i + 1] + iJ[j + 6] * Gx[3 * i + 2];
+          F[i][j] = KIN == 0 ? 0.0
+                             : iJ[j] * Gu[3 * i] + iJ[j + 3] * Gu[3 * i + 1] + iJ[j + 6] * Gu[3 * i + 2];
+        }
+      double P[3][3];
+      auto cmat = [&](const double* ev, double Sm[3][3]) {  // S = C e (fill_cmat), e engineering Voigt
+        Sm[0][0] = cd * ev[0] + lam * (ev[1] + ev[2]);
+        Sm[1][1] = cd * ev[1] + lam * (ev[0] + ev[2]);
+        Sm[2][2] = cd * ev[2] + lam * (ev[0] + ev[1]);
+        Sm[0][1] = Sm[1][0] = mu * ev[3];
+        Sm[1][2] = Sm[2][1] = mu * ev[4];
+        Sm[0][2] = Sm[2][0] = mu * ev[5];
+      };
+      if (KIN == 0)
+      {
+        const double ev[6] = {Hx[0][0], Hx[1][1], Hx[2][2], Hx[0][1] + Hx[1][0], Hx[1][2] + Hx[2][1],
+                              Hx[0][2] + Hx[2][0]};
+        double dS[3][3];
+        cmat(ev, dS);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) P[i][j] = fac * dS[i][j];
+      }
+      else
+      {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) F[i][i] += 1.0;
+        double C[3][3], Ah[3][3];  // C = F^T F, Ah = F^T H
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j)
+          {
+            C[i][j] = F[0][i] * F[0][j] + F[1][i] * F[1][j] + F[2][i] * F[2][j];
+            Ah[i][j] = F[0][i] * Hx[0][j] + F[1][i] * Hx[1][j] + F[2][i] * Hx[2][j];
+          }
+        const double E[6] = {0.5 * (C[0][0] - 1.0), 0.5 * (C[1][1] - 1.0), 0.5 * (C[2][2] - 1.0),
+                             C[0][1], C[1][2], C[0][2]};
+        const double dE[6] = {Ah[0][0], Ah[1][1], Ah[2][2], Ah[0][1] + Ah[1][0], Ah[1][2] + Ah[2][1],
+                              Ah[0][2] + Ah[2][0]};
+        double S[3][3], dS[3][3];
+        cmat(E, S);
+        cmat(dE, dS);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j)
+            P[i][j] = fac * (F[i][0] * dS[0][j] + F[i][1] * dS[1][j] + F[i][2] * dS[2][j] +
+                             Hx[i][0] * S[0][j] + Hx[i][1] * S[1][j] + Hx[i][2] * S[2][j]);
+      }
+      double* Q = Qs[s][g];
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          Q[3 * i + k] = P[i][0] * iJ[3 * k] + P[i][1] * iJ[3 * k + 1] + P[i][2] * iJ[3 * k + 2];
+    }
+    __syncthreads();
+    if (act && e < A.n_ele)
+    {
+      // node a = g at lattice position (p0, p1, p2): y_a = sum_g Q_g dN_a(xi_g), the points by
+      // lattice position (m0, m1, m2), dN_a(xi_g) from L_{p_d}(x_{m_d}) = tL[3 m_d + p_d]
+      const int32_t k = A.inc_of[e * 27 + g];
+      double La0[3], dLa0[3];
+#pragma unroll
+      for (int m = 0; m < 3; ++m)
+      {
+        La0[m] = tL[3 * m + p0];
+        dLa0[m] = tdL[3 * m + p0];
+      }
+      double y0 = 0.0, y1 = 0.0, y2 = 0.0;
+#pragma unroll 1
+      for (int m12 = 0; m12 < 9; ++m12)
+      {
+        const int m1 = m12 % 3, m2 = m12 / 3;
+        const double Ly = tL[3 * m1 + p1], dLy = tdL[3 * m1 + p1];
+        const double Lz = tL[3 * m2 + p2], dLz = tdL[3 * m2 + p2];
+        const double yz = Ly * Lz;
+#pragma unroll
+        for (int m0 = 0; m0 < 3; ++m0)
+        {
+          const double d0 = yz * dLa0[m0];
+          const double d1 = La0[m0] * Lz * dLy;
+          const double d2 = La0[m0] * Ly * dLz;
+          const double* Q = Qs[s][lat[m0 + 3 * m12]];
+          y0 += Q[0] * d0 + Q[1] * d1 + Q[2] * d2;
+          y1 += Q[3] * d0 + Q[4] * d1 + Q[5] * d2;
+          y2 += Q[6] * d0 + Q[7] * d1 + Q[8] * d2;
+        }
+      }
+      if (k >= 0)
+      {
+        double* o = A.ye + 3 * int64_t(k);
+        o[0] = y0;
+        o[1] = y1;
+        o[2] = y2;
+      }
+    }
+  }
+}
+
+// y_row of each owned row node = the sum of its incidences' parts in incidence order
+__global__ __launch_bounds__(256) void h27_inc_sum_kernel(int64_t n_rownodes,
+    const int64_t* __restrict__ inc_ptr, const int32_t* __restrict__ rownode_row0,
+    const double* __restrict__ ye, double* __restrict__ y)
+{
+  const int64_t r = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (r >= n_rownodes) return;
+  double y0 = 0.0, y1 = 0.0, y2 = 0.0;
+  for (int64_t k = inc_ptr[r]; k < inc_ptr[r + 1]; ++k)
+  {
+    y0 += ye[3 * k];
+    y1 += ye[3 * k + 1];
+    y2 += ye[3 * k + 2];
+  }
+  const int32_t row0 = rownode_row0[r];
+  y[row0] = y0;
+  y[row0 + 1] = y1;
+  y[row0 + 2] = y2;
+}
+
 }  // namespace
 
 void upload_h27_tables()
@@ -974,6 +1246,20 @@ void upload_h27_tables()
     dLn[3 * p + 2] = t + 0.5;
   }
   (void)hipMemcpyToSymbol(HIP_SYMBOL(c_dLn), dLn, sizeof(dLn));
+  // 1-D factors at the rule's points (the same r as gauss_rule, the same L / dL as shape_deriv)
+  double L1[9], dL1[9];
+  for (int m = 0; m < 3; ++m)
+  {
+    const double r = xi[3 * (m == 0 ? 0 : (m == 1 ? 8 : 1))];  // points 0, 8, 1: x = -a, 0, +a
+    L1[3 * m + 0] = 0.5 * r * (r - 1.0);
+    L1[3 * m + 1] = 1.0 - r * r;
+    L1[3 * m + 2] = 0.5 * r * (r + 1.0);
+    dL1[3 * m + 0] = r - 0.5;
+    dL1[3 * m + 1] = -2.0 * r;
+    dL1[3 * m + 2] = r + 0.5;
+  }
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(c_L1), L1, sizeof(L1));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(c_dL1), dL1, sizeof(dL1));
   uint8_t loc[27], latnode[27];
   for (int a = 0; a < 27; ++a)
   {
@@ -1102,6 +1388,39 @@ hipError_t launch_h27_assemble(const DeviceMesh& m, bool want_k, bool overwrite,
     hipLaunchKernelGGL((h27_assemble_kernel<false, true>), grid, block, 0, stream, a);
   else
     hipLaunchKernelGGL((h27_assemble_kernel<false, false>), grid, block, 0, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_h27_apply(const DeviceMesh& m, const double* d_u_col, const double* d_x_col,
+    double* d_y_row, hipStream_t stream)
+{
+  if (m.n_ele > 0)
+  {
+    H27ApplyArgs a{};
+    a.n_ele = m.n_ele;
+    a.ele_nodes = m.ele_nodes;
+    a.node_x = m.node_x;
+    a.node_dof_col = m.node_dof_col;
+    a.u_col = d_u_col;
+    a.x_col = d_x_col;
+    a.inc_of = m.inc_of;
+    a.ye = m.apply_ye;
+    a.lambda = m.lambda;
+    a.mu = m.mu;
+    a.cdiag = m.cdiag;
+    const int64_t passes = (m.n_ele + kApE - 1) / kApE;
+    const dim3 grid(unsigned(std::min<int64_t>(passes, 256 * 2 * 4))), block(256);
+    if (m.kinem == 0)
+      hipLaunchKernelGGL((h27_apply_kernel<0>), grid, block, 0, stream, a);
+    else
+      hipLaunchKernelGGL((h27_apply_kernel<1>), grid, block, 0, stream, a);
+    const hipError_t he = hipGetLastError();
+    if (he != hipSuccess) return he;
+  }
+  if (m.n_rownodes == 0) return hipSuccess;
+  const dim3 grid(unsigned((m.n_rownodes + 255) / 256)), block(256);
+  hipLaunchKernelGGL(h27_inc_sum_kernel, grid, block, 0, stream, m.n_rownodes, m.inc_ptr,
+      m.rownode_row0, m.apply_ye, d_y_row);
   return hipGetLastError();
 }
 

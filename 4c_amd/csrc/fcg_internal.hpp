@@ -74,6 +74,7 @@ struct DeviceMesh {
   int32_t gp_bad_code = 0, gp_bad_ele = 0;  // a Jacobian failure found by gather_precompute
   int32_t* ele_dof = nullptr;       // [n_ele][8] column LID of each element node's first DOF
   double* gather_dummy = nullptr;   // [4] store target of a row without columns
+  double* apply_ye = nullptr;       // [n_inc][3] fcg_tangent_apply's node parts (allocated on first use)
 
   // structured (row-block sweep) plan, hex8 only
   int path = FCG_PATH_GENERAL;
@@ -164,6 +165,10 @@ hipError_t launch_h27_assemble(const DeviceMesh& m, bool want_k, bool overwrite,
 // CSR rows, four colour launches of pencils (runs of elements along x, one workgroup each)
 hipError_t launch_h27_pencil(const DeviceMesh& m, const double* d_u_col, bool want_k,
     bool overwrite, double* d_K, double* d_fint, hipStream_t stream);
+// Matrix-free tangent action y_row = K(u) x_col of hex27 StVK (fcg_tangent_apply): the element
+// kernel writes each owned incidence's 3 values to m.apply_ye, a row-node pass sums them.
+hipError_t launch_h27_apply(const DeviceMesh& m, const double* d_u_col, const double* d_x_col,
+    double* d_y_row, hipStream_t stream);
 // Node-row gather (FCG_PATH_GATHER, hex8 StVK on any mesh): one wavefront per owned row node
 // (fcg_gather.hip).
 hipError_t gather_precompute(DeviceMesh& m, int64_t n_ele, hipStream_t stream);

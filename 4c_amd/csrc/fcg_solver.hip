@@ -441,6 +441,40 @@ int fcg_spmv_f32(fcg_ctx* ctx, const float* d_K32, const double* d_x_col, double
   return FCG_OK;
 }
 
+int fcg_tangent_apply(fcg_ctx* ctx, const double* d_u_col, const double* d_x_col, double* d_y_row,
+    void* stream)
+{
+  if (!ctx) return FCG_ERR_ARG;
+  fcg::DeviceMesh& m = ctx->mesh;
+  if (m.npe != 27 || m.material != FCG_MAT_STVK || !m.inc_of || !m.inc_ptr || !m.rownode_row0)
+  {
+    ctx->last_error = "fcg_tangent_apply: hex27 St.Venant-Kirchhoff contexts only";
+    return FCG_ERR_ARG;
+  }
+  if (m.n_rows > 0 && (!d_x_col || !d_y_row || (m.kinem != 0 && !d_u_col))) return FCG_ERR_ARG;
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  if (!m.apply_ye && m.n_inc > 0)
+  {
+    const size_t bytes = size_t(m.n_inc) * 3 * sizeof(double);
+    const hipError_t he = hipMalloc(&m.apply_ye, bytes);
+    if (he != hipSuccess)
+    {
+      m.apply_ye = nullptr;
+      ctx->last_error = std::string("fcg_tangent_apply: hipMalloc: ") + hipGetErrorString(he);
+      return fcg_device_error();
+    }
+    ctx->device_bytes += int64_t(bytes);
+  }
+  const hipError_t he = fcg::launch_h27_apply(m, d_u_col, d_x_col, d_y_row, s);
+  if (he != hipSuccess)
+  {
+    ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
+    return fcg_device_error();
+  }
+  return FCG_OK;
+}
+
 int fcg_dirichlet_apply(fcg_ctx* ctx, int64_t n_dbc, const int32_t* d_rows, double* d_K_vals,
     double* d_rhs_row, double* d_freact_row, void* stream)
 {

@@ -129,7 +129,7 @@ EXPORTS = ["fcg_create", "fcg_destroy", "fcg_last_error", "fcg_evaluate", "fcg_e
            "fcg_device_alloc", "fcg_device_free", "fcg_memcpy_h2d", "fcg_memcpy_d2h",
            "fcg_memset_device", "fcg_set_timing", "fcg_get_timing", "fcg_get_info",
            "fcg_get_diagnostics", "fcg_measure_peaks", "fcg_measure_hbm", "fcg_spmv", "fcg_dirichlet_apply",
-           "fcg_pcg_solve", "fcg_spmv_f32", "fcg_block_jacobi_setup", "fcg_block_jacobi_apply", "fcg_node_transfer",
+           "fcg_pcg_solve", "fcg_spmv_f32", "fcg_tangent_apply", "fcg_block_jacobi_setup", "fcg_block_jacobi_apply", "fcg_node_transfer",
            "fcg_neumann_surface", "fcg_neumann_volume",
            "fcg_graph_build_device", "fcg_get_graph",
            "fcg_tsi_create", "fcg_tsi_destroy", "fcg_tsi_last_error", "fcg_tsi_evaluate_device",
@@ -198,6 +198,7 @@ def lib():
     L.fcg_pcg_solve.argtypes = [vp, vp, vp, vp, ctypes.c_double, ctypes.c_int,
                                 ctypes.POINTER(ctypes.c_int), _dp, vp]
     L.fcg_spmv_f32.argtypes = [vp, vp, vp, vp, vp]
+    L.fcg_tangent_apply.argtypes = [vp, vp, vp, vp, vp]
     L.fcg_block_jacobi_setup.argtypes = [vp, vp, vp, vp]
     L.fcg_block_jacobi_apply.argtypes = [vp, vp, vp, vp, ctypes.c_double, ctypes.c_int, vp]
     L.fcg_node_transfer.argtypes = [ctypes.c_int, ctypes.c_int64, vp, vp, vp, vp, vp, vp,
@@ -616,6 +617,7 @@ class Evaluator:
             self._mesh = None
             desc = desc_or_mesh
         self.device = desc.device
+        self.kinematics = int(desc.kinematics)
         h = ctypes.c_void_p()
         rc = L.fcg_create(ctypes.byref(desc), ctypes.byref(h))
         if rc != 0:
@@ -709,6 +711,15 @@ class Evaluator:
         """y = K x with an FP32 copy of the matrix values (asynchronous)."""
         rc = lib().fcg_spmv_f32(self._h, _tensor_ptr(K32), _tensor_ptr(x_col), _tensor_ptr(y_row),
                                 self._stream(stream))
+        if rc != 0:
+            self._raise(rc, -1)
+
+    def tangent_apply(self, u_col, x_col, y_row, stream=None):
+        """y = K(u) x without a matrix (fcg_tangent_apply; hex27 StVK): the tangent the evaluate
+        assembles at u, before Dirichlet rows, applied element by element (asynchronous).  u_col
+        may be None for linear kinematics."""
+        rc = lib().fcg_tangent_apply(self._h, _tensor_ptr(u_col), _tensor_ptr(x_col),
+                                     _tensor_ptr(y_row), self._stream(stream))
         if rc != 0:
             self._raise(rc, -1)
 

@@ -135,6 +135,10 @@ class _LevelOps:
     """What the Chebyshev smoother and the Lanczos estimate need of a level: n, dev, mask, the
     work vectors r and z, spmv(x, y) and apply_dinv(r, z, scale, accumulate)."""
 
+    def spmv_cycle(self, x, y):
+        """The operator of the V-cycle's residual before restriction (FP64)."""
+        self.spmv_exact(x, y)
+
     def estimate_lmax(self, iters=10, seed=20251015):
         """Largest eigenvalue of D^-1 K from the Lanczos tridiagonal of a short block-Jacobi PCG
         run on a random right-hand side (the CG estimate of hypre / AmgX Chebyshev smoothers;
@@ -189,6 +193,11 @@ class _Level(_LevelOps):
         self.x, self.b, self.r, self.d, self.z = (torch.zeros(self.n, **f64) for _ in range(5))
         self.lmax = None
         self.K32 = None  # FP32 copy of K for the smoother and the V-cycle residual (mixed=True)
+        # matrix-free operator (Multigrid(matrix_free=True), hex27 StVK): K(u) x by
+        # fcg_tangent_apply at the state set_state gave, the Dirichlet rows as unit rows
+        self.matrix_free = False
+        self.mf_u = None
+        self.mf_dbc = torch.as_tensor(np.asarray(dbc_rows, dtype=np.int64), device=device)
 
     def stream(self):
         return torch.cuda.current_stream(self.dev)
@@ -207,14 +216,32 @@ class _Level(_LevelOps):
             self.ev._raise(rc, -1)
 
     def spmv(self, x, y):
-        """The V-cycle's operator: K, or its FP32 copy when the level has one."""
-        if self.K32 is not None:
+        """The V-cycle's operator: K, its FP32 copy when the level has one, or (matrix_free) the
+        element-by-element tangent action."""
+        if self.matrix_free:
+            self.apply_matrix_free(x, y)
+        elif self.K32 is not None:
             self.ev.spmv_f32(self.K32, x, y, stream=self.stream())
         else:
             self.ev.spmv(self.K, x, y, stream=self.stream())
 
     def spmv_exact(self, x, y):
         self.ev.spmv(self.K, x, y, stream=self.stream())
+
+    def spmv_cycle(self, x, y):
+        """The V-cycle's residual operator: FP64 -- K, or the matrix-free action."""
+        if self.matrix_free:
+            self.apply_matrix_free(x, y)
+        else:
+            self.spmv_exact(x, y)
+
+    def apply_matrix_free(self, x, y):
+        """y = K x for the Dirichlet-modified K: K(u) x, then y = x on the unit rows."""
+        if self.mf_u is None and self.ev.kinematics != fcg.LINEAR:
+            raise RuntimeError("matrix-free level: set_state(u) before the solve")
+        self.ev.tangent_apply(self.mf_u, x, y, stream=self.stream())
+        if self.mf_dbc.numel():
+            y.index_copy_(0, self.mf_dbc, x.index_select(0, self.mf_dbc))
 
 
 class _Indefinite(Exception):
@@ -277,7 +304,7 @@ class CycleFCG:
             self._coarse_solve(lvl, b, x)
             return
         self._cheb(lvl, b, x, x_zero=True)
-        lvl.spmv_exact(x, lvl.r)  # the restricted residual stays FP64 (mixed: smoother only)
+        lvl.spmv_cycle(x, lvl.r)  # the restricted residual stays FP64 (mixed: smoother only)
         torch.sub(b, lvl.r, out=lvl.r)
         c = self.levels[l + 1]
         self._restrict(l, lvl.r, c.b)
@@ -367,8 +394,10 @@ class Multigrid(CycleFCG):
 
     def __init__(self, fine_mesh, fine_ev, dbc_nodes, youngs, poisson, nu=2, min_intervals=4,
                  max_levels=8, ratio=10.0, boost=1.1, coarse_rtol=1e-2, coarse_max_iter=2000,
-                 mixed=False, coarse_solver="pcg", fine_post=True):
+                 mixed=False, coarse_solver="pcg", fine_post=True, matrix_free=False):
         self.fine_post = bool(fine_post)
+        if matrix_free and (mixed or fine_mesh.celltype != fcg.HEX27):
+            raise ValueError("matrix_free: hex27 fine levels in FP64 only (mixed=False)")
         if coarse_solver not in ("pcg", "amg"):
             raise ValueError(f"coarse_solver must be 'pcg' or 'amg', not {coarse_solver!r}")
         box = getattr(fine_mesh, "box", None)
@@ -403,6 +432,7 @@ class Multigrid(CycleFCG):
             return np.sort((mesh.node_dof_row[nodes][:, None] + np.arange(3)).ravel()).astype(np.int32)
 
         self.levels = [_Level(fine_mesh, fine_ev, None, dbc_rows(fine_mesh), dev)]
+        self.levels[0].matrix_free = bool(matrix_free)
         self.P, self.R = [], []
         prev = fine_mesh
         for ivc in meshes:
@@ -438,6 +468,11 @@ class Multigrid(CycleFCG):
         return [{"celltype": "hex27" if l.mesh.celltype == fcg.HEX27 else "hex8",
                  "intervals": [int(l.mesh.box.interval[d]) for d in range(3)], "dofs": l.n,
                  "lmax": l.lmax} for l in self.levels]
+
+    def set_state(self, u_col):
+        """The displacement the next solve's tangent was evaluated at (the matrix-free fine
+        level applies K(u); StaticNewton calls this before each linear solve)."""
+        self.levels[0].mf_u = u_col
 
     def _prepare(self, K):
         """lambda_max of D^-1 K barely moves between Newton iterations: it is estimated on the

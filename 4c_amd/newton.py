@@ -154,6 +154,8 @@ class StaticNewton:
                 return u
             torch.neg(self.r, out=self.r)
             eta = self.forcing.compute(it, nr, nr_old, lin_abs)
+            if hasattr(self.linear_solver, "set_state"):
+                self.linear_solver.set_state(u)  # a matrix-free level applies K(u)
             lin_it, lin_res = accept_linear_solve(lambda: self.linear_solve(self.r, self.du, eta),
                                                   eta, it, self.rescue, rec)
             nr_old, lin_abs = nr, lin_res * nr  # ‖F_k + J_k d_k‖ (full step, no line search)

@@ -224,6 +224,17 @@ int fcg_dirichlet_apply(fcg_ctx* ctx, int64_t n_dbc, const int32_t* d_rows, doub
  * fcg_spmv.  Asynchronous on `stream` like fcg_spmv. */
 int fcg_spmv_f32(fcg_ctx* ctx, const float* d_K32, const double* d_x_col, double* d_y_row,
     void* stream);
+/* y_row = K(u) x_col without a matrix: the tangent the context's evaluate assembles at the
+ * displacement u_col (before Dirichlet rows), applied element by element from X, u and x
+ * (B^T C B + K_geo per Gauss point, 4C_solid_3D_ele_calc_lib.hpp:872-927) and summed per owned
+ * row node in incidence order -- deterministic, equal to fcg_spmv on that K to rounding.  hex27
+ * St.Venant-Kirchhoff contexts only (else FCG_ERR_ARG); u_col may be NULL for linear kinematics.
+ * The multigrid smoother's level-0 operator (4c_amd/multigrid.py, matrix_free=True): 81 + 162
+ * doubles of input per element instead of the 6,561 matrix entries an SpMV reads.  Uses a
+ * per-context buffer (3 doubles per owned incidence, allocated on the first call): calls on one
+ * context must not run concurrently.  Asynchronous on `stream` like fcg_spmv. */
+int fcg_tangent_apply(fcg_ctx* ctx, const double* d_u_col, const double* d_x_col, double* d_y_row,
+    void* stream);
 int fcg_pcg_solve(fcg_ctx* ctx, const double* d_K_vals, const double* d_b_row, double* d_x_row,
     double rtol, int max_iter, int* iterations, double* rel_residual, void* stream);
 /* Pieces of the geometric multigrid preconditioner (4c_amd/multigrid.py; the MueLu

@@ -39,6 +39,9 @@ ap.add_argument("--mg-ratio", type=float, default=None,
 ap.add_argument("--mg-mixed", action="store_true", help="FP32 copy of K in the fine smoother")
 ap.add_argument("--mg-no-fine-post", action="store_true",
                 help="no post-smoothing on the finest level (pre-smoothing V-cycle there)")
+ap.add_argument("--mg-matrix-free", action="store_true",
+                help="hex27: the fine level's smoother and V-cycle residual apply K(u) element by "
+                     "element (fcg_tangent_apply) instead of reading the assembled K")
 ap.add_argument("--mg-coarse", default="pcg", choices=["pcg", "amg"],
                 help="coarsest-level solver of the geometric multigrid")
 ap.add_argument("--amg", action="store_true",
@@ -104,6 +107,8 @@ class Timed(newton.StaticNewton):
             hb.start()
             try:
                 eta = self.forcing.compute(it, nr, nr_old, lin_abs)
+                if hasattr(self.linear_solver, "set_state"):
+                    self.linear_solver.set_state(u)
                 li, lr = self.linear_solve(self.r, self.du, eta)
                 nr_old, lin_abs = nr, lr * nr
             finally:
@@ -127,7 +132,7 @@ if a.mg:
     mg = importlib.import_module("4c_amd.multigrid").Multigrid(
         mesh, ev, lambda m: np.isclose(m.node_x[:, 0], 0.0), 210.0, 0.3, nu=a.mg_nu,
         coarse_rtol=a.mg_coarse_rtol, mixed=a.mg_mixed, coarse_solver=a.mg_coarse,
-        fine_post=not a.mg_no_fine_post,
+        fine_post=not a.mg_no_fine_post, matrix_free=a.mg_matrix_free,
         **({"ratio": a.mg_ratio} if a.mg_ratio else {}))
     print(f"multigrid setup {time.perf_counter() - t_mg:.1f} s: {json.dumps(mg.describe())}",
           file=sys.stderr, flush=True)
@@ -166,7 +171,8 @@ del xv, yv, Kx, Ky
 out = {"config": f"{a.celltype}-{a.kinem}-{a.n}^3-cantilever", "forcing": a.forcing,
        "converged": True, "tangent_symmetry_rel": sym,
        "residual_rel_incl_dbc_rows": r_final,
-       "linear_solver": (f"multigrid-FCG (Chebyshev {a.mg_nu})" if a.mg else
+       "linear_solver": (f"multigrid-FCG (Chebyshev {a.mg_nu}"
+                         + (", matrix-free fine smoother)" if a.mg_matrix_free else ")") if a.mg else
                          f"SA-AMG-FCG (Chebyshev {a.mg_nu})" if a.amg else
                          f"SA-AMG-FCG native C ABI (Chebyshev {a.mg_nu})" if a.amg_native else
                          "block-Jacobi PCG"),
