@@ -45,6 +45,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <string>
 
 #include "fcg_internal.hpp"
 #include "fcg_shape.hpp"
@@ -1204,6 +1205,241 @@ __global__ __launch_bounds__(256, 2) void h27_apply_kernel(H27ApplyArgs A)
   }
 }
 
+// The same action sum-factorised over the tensor-product structure of hex27 (the default; the
+// kernel above stays as FCG_H27_APPLY=direct).  With L_p(x_m), L'_p(x_m) the 1-D factors and
+// nodes / points by lattice position:
+//   gradients  lanes (element, point line (m1, m2), source X | u | x): per component the node
+//              values contracted over (i1, i2) with L L, L' L, L L' of the line, then over i0 with
+//              L' | L | L for the three points of the line -- 108 FMA per component and line
+//              instead of 243;
+//   points     lanes (element, point): J, F, S, P and Q = P J^-1 from the gradients in LDS;
+//   nodes      lanes (element, node line (a1, a2), component i): Q contracted over (m1, m2) with
+//              the line's factors, then over m0 for the line's three nodes -- 99 FMA instead of 729.
+// Four barriers per pass (Q reuses the nodal values' LDS).
+template <int KIN>
+__global__ __launch_bounds__(256, 2) void h27_apply_sf_kernel(H27ApplyArgs A)
+{
+  constexpr int NSRC = KIN == 0 ? 2 : 3;  // X | x (linear) or X | u | x
+  constexpr int NND = 81 * NSRC > 243 ? 81 * NSRC : 243;
+  __shared__ double nq[kApE][NND];               // nodal X | (u) | x, then Q[g][9]
+  __shared__ double gr[kApE][27][NSRC][3][3];     // d(src)_k / dxi_d at point g: [g][src][k][d]
+  __shared__ double tL[9], tdL[9];
+  __shared__ uint8_t lat[27];
+  const int tid = threadIdx.x;
+  if (tid < 9)
+  {
+    tL[tid] = c_L1[tid];
+    tdL[tid] = c_dL1[tid];
+  }
+  if (tid < 27) lat[tid] = c_latnode[tid];
+  const double lam = A.lambda, mu = A.mu, cd = A.cdiag;
+  constexpr int NLD = (kApE * 81 * NSRC + 255) / 256;
+  double pre[NLD];
+  auto load = [&](int64_t e0) {
+#pragma unroll
+    for (int q = 0; q < NLD; ++q)
+    {
+      int t = tid + 256 * q;
+      __asm__ volatile("" : "+v"(t));  // index math per pass, not hoisted into live registers
+      pre[q] = 0.0;
+      if (t >= kApE * 81 * NSRC) continue;
+      const int sl = t / (81 * NSRC), r = t - 81 * NSRC * sl;
+      const int src = r / 81, rr = r - 81 * src, a = rr / 3, d = rr - 3 * a;
+      const int64_t e = e0 + sl;
+      if (e0 < 0 || e >= A.n_ele) continue;
+      const int32_t node = A.ele_nodes[e * 27 + a];
+      const double* base = src == 0 ? A.node_x : (src == NSRC - 1 ? A.x_col : A.u_col);
+      pre[q] = src == 0 ? base[3 * int64_t(node) + d] : base[A.node_dof_col[node] + d];
+    }
+  };
+  // lane roles: gradients (s, line, src), points (s, g), nodes (s, line, i)
+  const int s27 = tid / 27, r27 = tid - 27 * s27;
+  const int sg = tid / (9 * NSRC), rg = tid - 9 * NSRC * sg;
+  const int64_t stride = int64_t(gridDim.x) * kApE;
+  int64_t e0 = int64_t(blockIdx.x) * kApE;
+  load(e0 < A.n_ele ? e0 : -1);
+  for (; e0 < A.n_ele; e0 += stride)
+  {
+    __syncthreads();  // the previous pass's node phase has read Q
+#pragma unroll
+    for (int q = 0; q < NLD; ++q)
+    {
+      const int t = tid + 256 * q;
+      if (t < kApE * 81 * NSRC)
+      {
+        const int sl = t / (81 * NSRC);
+        nq[sl][t - 81 * NSRC * sl] = pre[q];
+      }
+    }
+    __syncthreads();
+    load(e0 + stride < A.n_ele ? e0 + stride : -1);  // next pass's gathers in flight
+    // ---- gradients at the points of line (m1, m2), one source
+    if (sg < kApE && e0 + sg < A.n_ele)
+    {
+      const int line = rg / NSRC, src = rg - NSRC * (rg / NSRC);
+      const int m1 = line % 3, m2 = line / 3;
+      double f0[9], f1[9], f2[9];  // L L, L' L, L L' of (i1, i2)
+#pragma unroll
+      for (int i2 = 0; i2 < 3; ++i2)
+#pragma unroll
+        for (int i1 = 0; i1 < 3; ++i1)
+        {
+          const double ly = tL[3 * m1 + i1], dly = tdL[3 * m1 + i1];
+          const double lz = tL[3 * m2 + i2], dlz = tdL[3 * m2 + i2];
+          f0[i1 + 3 * i2] = ly * lz;
+          f1[i1 + 3 * i2] = dly * lz;
+          f2[i1 + 3 * i2] = ly * dlz;
+        }
+      double lx[3][3], dlx[3][3];  // [m0][i0]
+#pragma unroll
+      for (int m0 = 0; m0 < 3; ++m0)
+#pragma unroll
+        for (int i0 = 0; i0 < 3; ++i0)
+        {
+          lx[m0][i0] = tL[3 * m0 + i0];
+          dlx[m0][i0] = tdL[3 * m0 + i0];
+        }
+#pragma unroll
+      for (int j = 0; j < 9; ++j)
+        __asm__ volatile("" : "+v"(f0[j]), "+v"(f1[j]), "+v"(f2[j]));  // rebuilt per pass, not kept live
+      const double* v = nq[sg] + 81 * src;
+#pragma unroll 1
+      for (int k = 0; k < 3; ++k)
+      {
+        double w0[3] = {0.0, 0.0, 0.0}, w1[3] = {0.0, 0.0, 0.0}, w2[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+        for (int j = 0; j < 9; ++j)
+#pragma unroll
+          for (int i0 = 0; i0 < 3; ++i0)
+          {
+            const double x = v[3 * lat[i0 + 3 * j] + k];
+            w0[i0] += f0[j] * x;
+            w1[i0] += f1[j] * x;
+            w2[i0] += f2[j] * x;
+          }
+#pragma unroll
+        for (int m0 = 0; m0 < 3; ++m0)
+        {
+          double* o = &gr[sg][lat[m0 + 3 * line]][src][k][0];
+          o[0] = dlx[m0][0] * w0[0] + dlx[m0][1] * w0[1] + dlx[m0][2] * w0[2];
+          o[1] = lx[m0][0] * w1[0] + lx[m0][1] * w1[1] + lx[m0][2] * w1[2];
+          o[2] = lx[m0][0] * w2[0] + lx[m0][1] * w2[1] + lx[m0][2] * w2[2];
+        }
+      }
+    }
+    __syncthreads();
+    // ---- point algebra: lanes (s27, g)
+    if (s27 < kApE && e0 + s27 < A.n_ele)
+    {
+      const int g = r27;
+      const double* G = &gr[s27][g][0][0][0];
+      double iJ[9];
+#pragma unroll
+      for (int q = 0; q < 9; ++q) iJ[q] = G[q];  // [k][d] row-major = J[d + 3k] col-major
+      const double fac = inv3(iJ) * c_w[g];
+      const double* Gx = G + 9 * (NSRC - 1);
+      double Hx[3][3], F[3][3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+        {
+          Hx[i][j] = iJ[j] * Gx[3 * i] + iJ[j + 3] * Gx[3 * i + 1] + iJ[j + 6] * Gx[3 * i + 2];
+          F[i][j] = KIN == 0 ? 0.0
+                             : iJ[j] * G[9 + 3 * i] + iJ[j + 3] * G[9 + 3 * i + 1] + iJ[j + 6] * G[9 + 3 * i + 2];
+        }
+      double P[3][3];
+      auto cmat = [&](const double* ev, double Sm[3][3]) {
+        Sm[0][0] = cd * ev[0] + lam * (ev[1] + ev[2]);
+        Sm[1][1] = cd * ev[1] + lam * (ev[0] + ev[2]);
+        Sm[2][2] = cd * ev[2] + lam * (ev[0] + ev[1]);
+        Sm[0][1] = Sm[1][0] = mu * ev[3];
+        Sm[1][2] = Sm[2][1] = mu * ev[4];
+        Sm[0][2] = Sm[2][0] = mu * ev[5];
+      };
+      if (KIN == 0)
+      {
+        const double ev[6] = {Hx[0][0], Hx[1][1], Hx[2][2], Hx[0][1] + Hx[1][0], Hx[1][2] + Hx[2][1],
+                              Hx[0][2] + Hx[2][0]};
+        double dS[3][3];
+        cmat(ev, dS);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) P[i][j] = fac * dS[i][j];
+      }
+      else
+      {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) F[i][i] += 1.0;
+        double C[3][3], Ah[3][3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j)
+          {
+            C[i][j] = F[0][i] * F[0][j] + F[1][i] * F[1][j] + F[2][i] * F[2][j];
+            Ah[i][j] = F[0][i] * Hx[0][j] + F[1][i] * Hx[1][j] + F[2][i] * Hx[2][j];
+          }
+        const double E[6] = {0.5 * (C[0][0] - 1.0), 0.5 * (C[1][1] - 1.0), 0.5 * (C[2][2] - 1.0),
+                             C[0][1], C[1][2], C[0][2]};
+        const double dE[6] = {Ah[0][0], Ah[1][1], Ah[2][2], Ah[0][1] + Ah[1][0], Ah[1][2] + Ah[2][1],
+                              Ah[0][2] + Ah[2][0]};
+        double S[3][3], dS[3][3];
+        cmat(E, S);
+        cmat(dE, dS);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j)
+            P[i][j] = fac * (F[i][0] * dS[0][j] + F[i][1] * dS[1][j] + F[i][2] * dS[2][j] +
+                             Hx[i][0] * S[0][j] + Hx[i][1] * S[1][j] + Hx[i][2] * S[2][j]);
+      }
+      double* Q = nq[s27] + 9 * g;  // the nodal values are dead: the gradients are in gr
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          Q[3 * i + k] = P[i][0] * iJ[3 * k] + P[i][1] * iJ[3 * k + 1] + P[i][2] * iJ[3 * k + 2];
+    }
+    __syncthreads();
+    // ---- node lines: lanes (s27, line (a1, a2), component i)
+    if (s27 < kApE && e0 + s27 < A.n_ele)
+    {
+      const int line = r27 / 3, i = r27 - 3 * (r27 / 3);
+      const int a1 = line % 3, a2 = line / 3;
+      const double* Q = nq[s27];
+      double z0[3] = {0.0, 0.0, 0.0}, z12[3] = {0.0, 0.0, 0.0};
+#pragma unroll 1
+      for (int m2 = 0; m2 < 3; ++m2)
+#pragma unroll
+        for (int m1 = 0; m1 < 3; ++m1)
+        {
+          const double ly = tL[3 * m1 + a1], dly = tdL[3 * m1 + a1];
+          const double lz = tL[3 * m2 + a2], dlz = tdL[3 * m2 + a2];
+          const double c0 = ly * lz, c1 = dly * lz, c2 = ly * dlz;
+#pragma unroll
+          for (int m0 = 0; m0 < 3; ++m0)
+          {
+            const double* q = Q + 9 * lat[m0 + 3 * m1 + 9 * m2] + 3 * i;
+            z0[m0] += c0 * q[0];
+            z12[m0] += c1 * q[1] + c2 * q[2];
+          }
+        }
+      const int64_t e = e0 + s27;
+#pragma unroll
+      for (int a0 = 0; a0 < 3; ++a0)
+      {
+        const int a = lat[a0 + 3 * line];
+        const int32_t k = A.inc_of[e * 27 + a];
+        const double y = tdL[a0] * z0[0] + tdL[3 + a0] * z0[1] + tdL[6 + a0] * z0[2] +
+                         tL[a0] * z12[0] + tL[3 + a0] * z12[1] + tL[6 + a0] * z12[2];
+        if (k >= 0) A.ye[3 * int64_t(k) + i] = y;
+      }
+    }
+  }
+}
+
 // y_row of each owned row node = the sum of its incidences' parts in incidence order
 __global__ __launch_bounds__(256) void h27_inc_sum_kernel(int64_t n_rownodes,
     const int64_t* __restrict__ inc_ptr, const int32_t* __restrict__ rownode_row0,
@@ -1410,10 +1646,22 @@ hipError_t launch_h27_apply(const DeviceMesh& m, const double* d_u_col, const do
     a.cdiag = m.cdiag;
     const int64_t passes = (m.n_ele + kApE - 1) / kApE;
     const dim3 grid(unsigned(std::min<int64_t>(passes, 256 * 2 * 4))), block(256);
-    if (m.kinem == 0)
-      hipLaunchKernelGGL((h27_apply_kernel<0>), grid, block, 0, stream, a);
+    // FCG_H27_APPLY=direct: the per-point kernel without sum factorisation (A/B runs)
+    static const bool direct = [] {
+      const char* e = std::getenv("FCG_H27_APPLY");
+      return e && std::string(e) == "direct";
+    }();
+    if (direct)
+    {
+      if (m.kinem == 0)
+        hipLaunchKernelGGL((h27_apply_kernel<0>), grid, block, 0, stream, a);
+      else
+        hipLaunchKernelGGL((h27_apply_kernel<1>), grid, block, 0, stream, a);
+    }
+    else if (m.kinem == 0)
+      hipLaunchKernelGGL((h27_apply_sf_kernel<0>), grid, block, 0, stream, a);
     else
-      hipLaunchKernelGGL((h27_apply_kernel<1>), grid, block, 0, stream, a);
+      hipLaunchKernelGGL((h27_apply_sf_kernel<1>), grid, block, 0, stream, a);
     const hipError_t he = hipGetLastError();
     if (he != hipSuccess) return he;
   }

@@ -2,6 +2,7 @@
 # rocprofv3 counter passes of one workload (each pass its own run, no tracing domains mixed in),
 # summarised for the kernels whose name contains PATTERN.
 #   tools/pmc_kernel.sh TAG PATTERN [SETS] -- <args of tools/prof_kernel.py>
+# (PMC_SCRIPT=<repo-relative .py> profiles another workload script with those arguments)
 # SETS (comma list): occ (wave / issue cycles), inst (instruction mix, LDS), flop (FP64 VALU and
 # MFMA counts, matrix-pipe busy), mem (FETCH_SIZE, WRITE_SIZE, GRBM)
 set -o pipefail
@@ -19,7 +20,7 @@ declare -a P
 i=0
 for C in "${P[@]}"; do
   i=$((i+1))
-  (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d "$OUT/p$i" -o run -- python3 "$GRAFT_REPO_ROOT/tools/prof_kernel.py" "$@") > "$OUT/p$i.log" 2>&1
+  (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d "$OUT/p$i" -o run -- python3 "$GRAFT_REPO_ROOT/${PMC_SCRIPT:-tools/prof_kernel.py}" "$@") > "$OUT/p$i.log" 2>&1
   rc=$?
   echo "pass $i rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 "$OUT/p$i.log"; exit $rc; fi

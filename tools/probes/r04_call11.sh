@@ -1,0 +1,11 @@
+#!/bin/bash
+# round 4, call 11: where the matrix-free hex27 action spends its time (kernel stats + counters)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 2
+O=gpurun_out/r04
+mkdir -p $O/apply_stats
+export TMPDIR=/tmp
+(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$O/apply_stats" -o run -- \
+  python3 "$GRAFT_REPO_ROOT/tools/probes/apply_timing.py" --n 100 --kinem totlag --reps 10) > $O/apply_stats.log 2>&1 || exit 1
+f=$(find $O/apply_stats -name "*kernel_stats.csv" | head -1); head -12 "$f"
+PMC_SCRIPT=tools/probes/apply_timing.py timeout -k 10 600 bash tools/pmc_kernel.sh r04/apply_pmc apply_sf occ,inst,mem -- --n 60 --kinem totlag --reps 3 || exit 1
