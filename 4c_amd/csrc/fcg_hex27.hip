@@ -1222,16 +1222,23 @@ __global__ __launch_bounds__(256, 2) void h27_apply_sf_kernel(H27ApplyArgs A)
   constexpr int NSRC = KIN == 0 ? 2 : 3;  // X | x (linear) or X | u | x
   constexpr int NND = 81 * NSRC > 243 ? 81 * NSRC : 243;
   __shared__ double nq[kApE][NND];               // nodal X | (u) | x, then Q[g][9]
-  __shared__ double gr[kApE][27][NSRC][3][3];     // d(src)_k / dxi_d at point g: [g][src][k][d]
-  __shared__ double tL[9], tdL[9];
-  __shared__ uint8_t lat[27];
+  __shared__ double gr[kApE][27][NSRC][3][3];     // d(src)_k / dxi_d at point l: [l][src][k][d]
+  __shared__ double tL[9], tdL[9], wl[27];
+  __shared__ uint8_t lat[27], posl[27];  // lattice position -> node (= point) number, and back
+  // every LDS array is indexed by lattice position l = p0 + 3 p1 + 9 p2 (nodes and points alike)
   const int tid = threadIdx.x;
   if (tid < 9)
   {
     tL[tid] = c_L1[tid];
     tdL[tid] = c_dL1[tid];
   }
-  if (tid < 27) lat[tid] = c_latnode[tid];
+  if (tid < 27)
+  {
+    lat[tid] = c_latnode[tid];
+    const uint32_t pc = c_loc[tid];
+    posl[tid] = uint8_t((pc & 3) + 3 * ((pc >> 2) & 3) + 9 * (pc >> 4));
+    wl[tid] = c_w[c_latnode[tid]];
+  }
   const double lam = A.lambda, mu = A.mu, cd = A.cdiag;
   constexpr int NLD = (kApE * 81 * NSRC + 255) / 256;
   double pre[NLD];
@@ -1267,8 +1274,9 @@ __global__ __launch_bounds__(256, 2) void h27_apply_sf_kernel(H27ApplyArgs A)
       const int t = tid + 256 * q;
       if (t < kApE * 81 * NSRC)
       {
-        const int sl = t / (81 * NSRC);
-        nq[sl][t - 81 * NSRC * sl] = pre[q];
+        const int sl = t / (81 * NSRC), r = t - 81 * NSRC * sl;
+        const int src = r / 81, rr = r - 81 * src, a = rr / 3;
+        nq[sl][81 * src + 3 * posl[a] + rr - 3 * a] = pre[q];
       }
     }
     __syncthreads();
@@ -1312,7 +1320,7 @@ __global__ __launch_bounds__(256, 2) void h27_apply_sf_kernel(H27ApplyArgs A)
 #pragma unroll
           for (int i0 = 0; i0 < 3; ++i0)
           {
-            const double x = v[3 * lat[i0 + 3 * j] + k];
+            const double x = v[3 * (i0 + 3 * j) + k];
             w0[i0] += f0[j] * x;
             w1[i0] += f1[j] * x;
             w2[i0] += f2[j] * x;
@@ -1320,7 +1328,7 @@ __global__ __launch_bounds__(256, 2) void h27_apply_sf_kernel(H27ApplyArgs A)
 #pragma unroll
         for (int m0 = 0; m0 < 3; ++m0)
         {
-          double* o = &gr[sg][lat[m0 + 3 * line]][src][k][0];
+          double* o = &gr[sg][m0 + 3 * line][src][k][0];
           o[0] = dlx[m0][0] * w0[0] + dlx[m0][1] * w0[1] + dlx[m0][2] * w0[2];
           o[1] = lx[m0][0] * w1[0] + lx[m0][1] * w1[1] + lx[m0][2] * w1[2];
           o[2] = lx[m0][0] * w2[0] + lx[m0][1] * w2[1] + lx[m0][2] * w2[2];
@@ -1331,12 +1339,12 @@ __global__ __launch_bounds__(256, 2) void h27_apply_sf_kernel(H27ApplyArgs A)
     // ---- point algebra: lanes (s27, g)
     if (s27 < kApE && e0 + s27 < A.n_ele)
     {
-      const int g = r27;
+      const int g = r27;  // lattice position of the point
       const double* G = &gr[s27][g][0][0][0];
       double iJ[9];
 #pragma unroll
       for (int q = 0; q < 9; ++q) iJ[q] = G[q];  // [k][d] row-major = J[d + 3k] col-major
-      const double fac = inv3(iJ) * c_w[g];
+      const double fac = inv3(iJ) * wl[g];
       const double* Gx = G + 9 * (NSRC - 1);
       double Hx[3][3], F[3][3];
 #pragma unroll
@@ -1421,7 +1429,7 @@ __global__ __launch_bounds__(256, 2) void h27_apply_sf_kernel(H27ApplyArgs A)
 #pragma unroll
           for (int m0 = 0; m0 < 3; ++m0)
           {
-            const double* q = Q + 9 * lat[m0 + 3 * m1 + 9 * m2] + 3 * i;
+            const double* q = Q + 9 * (m0 + 3 * m1 + 9 * m2) + 3 * i;
             z0[m0] += c0 * q[0];
             z12[m0] += c1 * q[1] + c2 * q[2];
           }

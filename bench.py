@@ -316,10 +316,12 @@ def cpu_topology():
 def newton_secondary(n, timeout_s=900):
     """BASELINE config 3: StVK TotLag on the 1M-hex27 cube (x- clamped, traction -1 in z on x+),
     full static Newton on this GPU (fcg_evaluate_device + Dirichlet + multigrid-preconditioned
-    flexible CG, 4c_amd/newton.py + multigrid.py), run by tools/newton_bench.py in a child process
-    so that its ~60 GB of device buffers are released when it ends."""
+    flexible CG, 4c_amd/newton.py + multigrid.py; the fine level's smoother applies K(u) element
+    by element, fcg_tangent_apply, the outer FCG the assembled K), run by tools/newton_bench.py in
+    a child process so that its ~60 GB of device buffers are released when it ends."""
     cmd = [sys.executable, os.path.join(ROOT, "tools", "newton_bench.py"), "--celltype", "hex27",
-           "--kinem", "totlag", "--n", str(n), "--length", "1", "--load", "-1", "--mg"]
+           "--kinem", "totlag", "--n", str(n), "--length", "1", "--load", "-1", "--mg",
+           "--mg-matrix-free"]
     t = time.perf_counter()
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s)
     wall = time.perf_counter() - t

@@ -67,6 +67,18 @@ def test_multigrid_rejects_meshes_without_a_hierarchy():
         mgm.Multigrid(object(), None, None, E, NU)
 
 
+def test_matrix_free_fine_level_needs_hex27_fp64():
+    """Multigrid(matrix_free=True) applies fcg_tangent_apply (hex27 only) and is exact FP64: a hex8
+    fine level or mixed=True is refused before any device work."""
+    m8 = fcg.BoxMesh(fcg.HEX8, (4, 4, 4))
+    m27 = fcg.BoxMesh(fcg.HEX27, (4, 4, 4))
+    with pytest.raises(ValueError):
+        mgm.Multigrid(m8, None, lambda mm: np.zeros(mm.n_node, bool), E, NU, matrix_free=True)
+    with pytest.raises(ValueError):
+        mgm.Multigrid(m27, None, lambda mm: np.zeros(mm.n_node, bool), E, NU, matrix_free=True,
+                      mixed=True)
+
+
 def _dev():
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
