@@ -8,7 +8,8 @@ the BASELINE configs the hierarchy is known in advance, so it is built geometric
 
   level 0   the tangent K being solved (hex27 or hex8, any kinematics, Dirichlet unit rows)
   level 1   hex27 -> hex8 on the same elements (p-coarsening), if level 0 is hex27
-  level l+1 hex8 n -> hex8 n/2 (h-coarsening) while n stays even and >= min_intervals
+  level l+1 hex8 n -> hex8 (n+1)/2 (h-coarsening) while that stays >= min_intervals (an odd n
+            gives a non-nested level: trilinear interpolation at general weights)
 
 Coarse operators are rediscretised: linear-elastic StVK hex8 assembled by the library's own
 evaluate (for affine boxes and linear kinematics this is exactly the Galerkin product P^T K P,
@@ -57,22 +58,27 @@ def node_lattice(mesh):
 
 def transfer_tables(fine, coarse):
     """Prolongation fine <- coarse (trilinear nodal interpolation) and its transpose, as
-    node-block tables for fcg_node_transfer: (ptr, src_row0, w, dst_row0) each."""
+    node-block tables for fcg_node_transfer: (ptr, src_row0, w, dst_row0) each.  Both meshes
+    span the same GridGenerator box; a fine node at lattice index f of N_f points sits at coarse
+    lattice coordinate f (N_c - 1) / (N_f - 1) -- on a 2:1 refinement the weights are 1 or 1/2,
+    otherwise (an odd interval count halved to (n + 1) / 2) the general linear weights."""
     fl, cl = node_lattice(fine), node_lattice(coarse)
     cdim = cl.max(axis=0) + 1
-    if not np.array_equal(fl.max(axis=0), 2 * (cdim - 1)):
-        raise ValueError("fine lattice is not the 2:1 refinement of the coarse one")
+    fdim = fl.max(axis=0) + 1
+    if (cdim > fdim).any() or (cdim < 2).any():
+        raise ValueError("coarse lattice is not coarser than the fine one")
     crow = np.full(tuple(cdim), -1, dtype=np.int64)
     crow[cl[:, 0], cl[:, 1], cl[:, 2]] = coarse.node_dof_row
     nf = len(fl)
     lo, hi, wl, wh = [], [], [], []
     for d in range(3):
-        f = fl[:, d]
-        odd = (f & 1).astype(bool)
-        lo.append(f // 2)
-        hi.append(np.where(odd, f // 2 + 1, f // 2))
-        wl.append(np.where(odd, 0.5, 1.0))
-        wh.append(np.where(odd, 0.5, 0.0))
+        c = fl[:, d] * float(cdim[d] - 1) / float(fdim[d] - 1)
+        i0 = np.minimum(np.floor(c).astype(np.int64), cdim[d] - 2)
+        t = c - i0
+        lo.append(i0)
+        hi.append(i0 + 1)
+        wl.append(1.0 - t)
+        wh.append(t)
     fidx, cidx, w = [], [], []
     for cx in range(2):
         for cy in range(2):
@@ -408,12 +414,13 @@ class Multigrid(CycleFCG):
         if fine_mesh.celltype == fcg.HEX27:
             meshes.append(tuple(iv))
         n = list(iv)
-        while len(meshes) + 1 < max_levels and all(v % 2 == 0 and v // 2 >= min_intervals for v in n):
-            n = [v // 2 for v in n]
+        # halve (odd counts to (n + 1) / 2, a non-nested level with general interpolation weights)
+        while len(meshes) + 1 < max_levels and all((v + 1) // 2 >= min_intervals for v in n):
+            n = [(v + 1) // 2 for v in n]
             meshes.append(tuple(n))
         if not meshes:
-            raise ValueError(f"no coarse level for intervals {iv}: hex8 boxes need even intervals "
-                             f"with n/2 >= min_intervals ({min_intervals})")
+            raise ValueError(f"no coarse level for intervals {iv}: hex8 boxes need (n + 1) / 2 >= "
+                             f"min_intervals ({min_intervals})")
         dev = torch.device("cuda", fine_ev.device)
         self.dev, self.nu, self.ratio, self.boost = dev, nu, ratio, boost
         # mixed: the fine level's Chebyshev smoother uses an FP32 copy of K (half the bytes of

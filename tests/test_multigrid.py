@@ -1,7 +1,7 @@
 """Geometric multigrid preconditioner of the Newton solve (4c_amd/multigrid.py).
 
-Host (no GPU): the transfer tables of GridGenerator boxes -- hex27 -> hex8 on the same elements and
-hex8 n -> n/2 -- interpolate linear fields exactly and the restriction is the transpose of the
+Host (no GPU): the transfer tables of GridGenerator boxes -- hex27 -> hex8 on the same elements,
+hex8 n -> n/2 and the non-nested odd n -> (n + 1)/2 -- interpolate linear fields exactly and the restriction is the transpose of the
 prolongation.  GPU: fcg_node_transfer and fcg_block_jacobi_apply against numpy on the same tables,
 and Newton solves with the multigrid-preconditioned flexible CG converging to the block-Jacobi
 PCG's displacement (the preconditioner changes the path, not the solution: 1e-8 relative at
@@ -37,10 +37,13 @@ def _pairs():
     f27 = fcg.BoxMesh(fcg.HEX27, (4, 2, 6), upper=up)
     c8 = fcg.BoxMesh(fcg.HEX8, (4, 2, 6), upper=up)
     c8h = fcg.BoxMesh(fcg.HEX8, (2, 1, 3), upper=up)
-    return [(f27, c8), (c8, c8h)]
+    # odd interval counts halved to (n + 1) / 2: a non-nested coarse level
+    o8 = fcg.BoxMesh(fcg.HEX8, (5, 3, 7), upper=up)
+    o8h = fcg.BoxMesh(fcg.HEX8, (3, 2, 4), upper=up)
+    return [(f27, c8), (c8, c8h), (o8, o8h)]
 
 
-@pytest.mark.parametrize("k", [0, 1])
+@pytest.mark.parametrize("k", [0, 1, 2])
 def test_transfer_tables_host(k):
     fine, coarse = _pairs()[k]
     P, R = mgm.transfer_tables(fine, coarse)
@@ -87,7 +90,7 @@ def _dev():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("k", [0, 1])
+@pytest.mark.parametrize("k", [0, 1, 2])
 def test_node_transfer_device(k):
     torch, dev = _dev()
     fine, coarse = _pairs()[k]
