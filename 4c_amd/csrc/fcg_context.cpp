@@ -772,7 +772,7 @@ bool build_colored_plan(const fcg_desc* d, ColorHost& P, std::string& why)
 
 void free_mesh(fcg::DeviceMesh& m)
 {
-  void* ptrs[] = {m.apply_ye, m.gather_dummy, m.multi_ptr, m.rec_row0, m.rec_meta, m.rec_base, m.rec_ele, m.rec_a, m.rec_tmap, m.ele_orig, m.inc_ele, m.inc_a, m.asm_order, m.ele_x,
+  void* ptrs[] = {m.apply_ye, m.apply_dof, m.gather_dummy, m.multi_ptr, m.rec_row0, m.rec_meta, m.rec_base, m.rec_ele, m.rec_a, m.rec_tmap, m.ele_orig, m.inc_ele, m.inc_a, m.asm_order, m.ele_x,
       m.ele_dof, m.ele_nodes, m.ele_gid, m.node_x, m.node_dof_col, m.inc_of, m.inc_ptr,
       m.rownode_row0, m.inc_pos, m.rowptr, m.scratch, m.err, m.elem_at, m.lat_x, m.lat_dof,
       m.plane_rec,

@@ -978,6 +978,7 @@ struct H27ApplyArgs {
   const double* u_col;
   const double* x_col;
   const int32_t* inc_of;
+  const int32_t* ele_dof;  // [n_ele][27] column LID of each element node's first DOF
   double* ye;  // [n_inc][3]
   double lambda, mu, cdiag;
 };
@@ -1241,32 +1242,57 @@ __global__ __launch_bounds__(256, 2) void h27_apply_sf_kernel(H27ApplyArgs A)
   }
   const double lam = A.lambda, mu = A.mu, cd = A.cdiag;
   constexpr int NLD = (kApE * 81 * NSRC + 255) / 256;
+  // the gathers in two stages, one pass apart, so that no wait on a dependent load falls inside a
+  // pass: stage 1 reads the element's node / DOF index of each item for the pass after next
+  // (ele_nodes, apply_dof: independent loads), stage 2 the values for the next pass at the
+  // indices stage 1 read one pass earlier
   double pre[NLD];
-  auto load = [&](int64_t e0) {
+  int32_t ix1[NLD], ix2[NLD];
+  auto index_of = [&](int64_t e0, int32_t* ix) {
 #pragma unroll
     for (int q = 0; q < NLD; ++q)
     {
       int t = tid + 256 * q;
       __asm__ volatile("" : "+v"(t));  // index math per pass, not hoisted into live registers
-      pre[q] = 0.0;
+      ix[q] = -1;
       if (t >= kApE * 81 * NSRC) continue;
       const int sl = t / (81 * NSRC), r = t - 81 * NSRC * sl;
       const int src = r / 81, rr = r - 81 * src, a = rr / 3, d = rr - 3 * a;
       const int64_t e = e0 + sl;
       if (e0 < 0 || e >= A.n_ele) continue;
-      const int32_t node = A.ele_nodes[e * 27 + a];
+      ix[q] = src == 0 ? 3 * A.ele_nodes[e * 27 + a] + d : A.ele_dof[e * 27 + a] + d;
+    }
+  };
+  auto value_of = [&](const int32_t* ix) {
+#pragma unroll
+    for (int q = 0; q < NLD; ++q)
+    {
+      int t = tid + 256 * q;
+      __asm__ volatile("" : "+v"(t));
+      const int src = (t - 81 * NSRC * (t / (81 * NSRC))) / 81;
       const double* base = src == 0 ? A.node_x : (src == NSRC - 1 ? A.x_col : A.u_col);
-      pre[q] = src == 0 ? base[3 * int64_t(node) + d] : base[A.node_dof_col[node] + d];
+      pre[q] = ix[q] >= 0 ? base[ix[q]] : 0.0;
     }
   };
   // lane roles: gradients (s, line, src), points (s, g), nodes (s, line, i)
   const int s27 = tid / 27, r27 = tid - 27 * s27;
   const int sg = tid / (9 * NSRC), rg = tid - 9 * NSRC * sg;
-  const int64_t stride = int64_t(gridDim.x) * kApE;
-  int64_t e0 = int64_t(blockIdx.x) * kApE;
-  load(e0 < A.n_ele ? e0 : -1);
-  for (; e0 < A.n_ele; e0 += stride)
+  // XCD-contiguous passes: workgroup b runs on XCD b % 8 (round-robin dispatch); XCD x takes its
+  // own eighth of the element chunks, its workgroups interleaved, so that elements sharing nodes
+  // are gathered through one L2
+  const int64_t nch = (A.n_ele + kApE - 1) / kApE;
+  const int xcd = int(blockIdx.x & 7u);
+  const int64_t per_xcd = (int64_t(gridDim.x) + 7 - xcd) / 8;
+  const int64_t span = (nch + 7) / 8;
+  const int64_t c0 = min(nch, int64_t(xcd) * span), c1 = min(nch, c0 + span);
+  auto first_of = [&](int64_t c) { return c < c1 ? c * kApE : int64_t(-1); };
+  int64_t ch = c0 + (blockIdx.x >> 3);
+  index_of(first_of(ch), ix1);
+  value_of(ix1);
+  index_of(first_of(ch + per_xcd), ix1);
+  for (; ch < c1; ch += per_xcd)
   {
+    const int64_t e0 = ch * kApE;
     __syncthreads();  // the previous pass's node phase has read Q
 #pragma unroll
     for (int q = 0; q < NLD; ++q)
@@ -1280,7 +1306,10 @@ __global__ __launch_bounds__(256, 2) void h27_apply_sf_kernel(H27ApplyArgs A)
       }
     }
     __syncthreads();
-    load(e0 + stride < A.n_ele ? e0 + stride : -1);  // next pass's gathers in flight
+    index_of(first_of(ch + 2 * per_xcd), ix2);  // pass after next: indices
+    value_of(ix1);                               // next pass: values at last pass's indices
+#pragma unroll
+    for (int q = 0; q < NLD; ++q) ix1[q] = ix2[q];
     // ---- gradients at the points of line (m1, m2), one source
     if (sg < kApE && e0 + sg < A.n_ele)
     {
@@ -1446,6 +1475,14 @@ __global__ __launch_bounds__(256, 2) void h27_apply_sf_kernel(H27ApplyArgs A)
       }
     }
   }
+}
+
+// apply_dof[e][a] = node_dof_col[ele_nodes[e][a]] (the matrix-free action's gather plan)
+__global__ __launch_bounds__(256) void h27_apply_plan_kernel(int64_t n, const int32_t* __restrict__ ele_nodes,
+    const int32_t* __restrict__ node_dof_col, int32_t* __restrict__ out)
+{
+  const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = node_dof_col[ele_nodes[i]];
 }
 
 // y_row of each owned row node = the sum of its incidences' parts in incidence order
@@ -1635,6 +1672,15 @@ hipError_t launch_h27_assemble(const DeviceMesh& m, bool want_k, bool overwrite,
   return hipGetLastError();
 }
 
+hipError_t launch_h27_apply_plan(const DeviceMesh& m, hipStream_t stream)
+{
+  const int64_t n = m.n_ele * 27;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(h27_apply_plan_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, stream,
+      n, m.ele_nodes, m.node_dof_col, m.apply_dof);
+  return hipGetLastError();
+}
+
 hipError_t launch_h27_apply(const DeviceMesh& m, const double* d_u_col, const double* d_x_col,
     double* d_y_row, hipStream_t stream)
 {
@@ -1648,12 +1694,19 @@ hipError_t launch_h27_apply(const DeviceMesh& m, const double* d_u_col, const do
     a.u_col = d_u_col;
     a.x_col = d_x_col;
     a.inc_of = m.inc_of;
+    a.ele_dof = m.apply_dof;
     a.ye = m.apply_ye;
     a.lambda = m.lambda;
     a.mu = m.mu;
     a.cdiag = m.cdiag;
     const int64_t passes = (m.n_ele + kApE - 1) / kApE;
-    const dim3 grid(unsigned(std::min<int64_t>(passes, 256 * 2 * 4))), block(256);
+    // persistent: two resident workgroups per CU (LDS), so that each XCD's workgroups walk its
+    // element range together (FCG_H27_APPLY_GRID overrides, for A/B runs)
+    static const int64_t cap = [] {
+      const char* e = std::getenv("FCG_H27_APPLY_GRID");
+      return e ? std::max<int64_t>(8, std::atoll(e)) : int64_t(256 * 2);
+    }();
+    const dim3 grid(unsigned(std::min<int64_t>(passes, cap))), block(256);
     // FCG_H27_APPLY=direct: the per-point kernel without sum factorisation (A/B runs)
     static const bool direct = [] {
       const char* e = std::getenv("FCG_H27_APPLY");

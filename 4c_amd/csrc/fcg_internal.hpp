@@ -75,6 +75,7 @@ struct DeviceMesh {
   int32_t* ele_dof = nullptr;       // [n_ele][8] column LID of each element node's first DOF
   double* gather_dummy = nullptr;   // [4] store target of a row without columns
   double* apply_ye = nullptr;       // [n_inc][3] fcg_tangent_apply's node parts (allocated on first use)
+  int32_t* apply_dof = nullptr;     // [n_ele][27] column LID of each element node's first DOF (idem)
 
   // structured (row-block sweep) plan, hex8 only
   int path = FCG_PATH_GENERAL;
@@ -169,6 +170,7 @@ hipError_t launch_h27_pencil(const DeviceMesh& m, const double* d_u_col, bool wa
 // kernel writes each owned incidence's 3 values to m.apply_ye, a row-node pass sums them.
 hipError_t launch_h27_apply(const DeviceMesh& m, const double* d_u_col, const double* d_x_col,
     double* d_y_row, hipStream_t stream);
+hipError_t launch_h27_apply_plan(const DeviceMesh& m, hipStream_t stream);  // fills m.apply_dof
 // Node-row gather (FCG_PATH_GATHER, hex8 StVK on any mesh): one wavefront per owned row node
 // (fcg_gather.hip).
 hipError_t gather_precompute(DeviceMesh& m, int64_t n_ele, hipStream_t stream);

@@ -466,6 +466,20 @@ int fcg_tangent_apply(fcg_ctx* ctx, const double* d_u_col, const double* d_x_col
     }
     ctx->device_bytes += int64_t(bytes);
   }
+  if (!m.apply_dof && m.n_ele > 0)
+  {
+    const size_t bytes = size_t(m.n_ele) * 27 * sizeof(int32_t);
+    hipError_t he = hipMalloc(&m.apply_dof, bytes);
+    if (he == hipSuccess) he = fcg::launch_h27_apply_plan(m, s);
+    if (he != hipSuccess)
+    {
+      if (m.apply_dof) (void)hipFree(m.apply_dof);
+      m.apply_dof = nullptr;
+      ctx->last_error = std::string("fcg_tangent_apply: gather plan: ") + hipGetErrorString(he);
+      return fcg_device_error();
+    }
+    ctx->device_bytes += int64_t(bytes);
+  }
   const hipError_t he = fcg::launch_h27_apply(m, d_u_col, d_x_col, d_y_row, s);
   if (he != hipSuccess)
   {
