@@ -344,10 +344,16 @@ class CycleFCG:
         what = "after a lambda_max re-estimate" if self.retry_lmax else "(no retry)"
         raise MultigridError(f"multigrid FCG failed {what}: {why}", *last)
 
+    # a V-cycle that never waits on the host (Multigrid with the dense coarsest solve) lets an
+    # FCG iteration run as one captured HIP graph (FCG_MG_GRAPH=0: eager launches)
+    graph_ok = False
+
     def _fcg(self, f0, b, x, rtol, max_iter):
         """Flexible CG with the scalars kept on the device: one host read per iteration (|r|,
         r.z and z.r_old together, after the V-cycle of the new residual -- the last iteration's
         V-cycle is spent for nothing, every other read would stall the queue)."""
+        if self.graph_ok and os.environ.get("FCG_MG_GRAPH", "1") != "0" and not self.trace:
+            return self._fcg_graph(f0, b, x, rtol, max_iter)
         if self.trace:
             print(f"  levels: {self.describe()}", file=sys.stderr, flush=True)
         bn = float(torch.linalg.vector_norm(b))
@@ -391,6 +397,76 @@ class CycleFCG:
             rz, rz_t = rz_new, st[1]
         return it, rn / bn
 
+    def _fcg_graph(self, f0, b, x, rtol, max_iter):
+        """_fcg with one iteration -- the fine operator, the vector updates, the V-cycle and the
+        dots, ~10^2 launches on 7 levels -- captured once into a HIP graph and replayed: the host
+        launches one graph and reads |r|, r.z back per iteration, and the GPU no longer idles
+        while Python issues the coarse levels' microsecond kernels.  alpha and the Polak-Ribiere
+        beta stay device scalars.  The graph is rebuilt when what it baked in changes: the
+        buffers of K, b, x, the state u of a matrix-free level, or a lambda_max."""
+        bn = float(torch.linalg.vector_norm(b))
+        x.zero_()
+        if bn == 0.0:
+            return 0, 0.0
+        key = (b.data_ptr(), x.data_ptr(), b.numel(), f0.K.data_ptr(),
+               None if f0.mf_u is None else f0.mf_u.data_ptr(),
+               tuple(l.lmax for l in self.levels))
+        g = getattr(self, "_graph", None)
+        if g is None or g["key"] != key:
+            f64 = dict(dtype=torch.float64, device=b.device)
+            g = {"key": key, "graph": None}
+            for name in ("r", "z", "q", "r_old", "p"):
+                g[name] = torch.empty_like(b)
+            for name in ("rz", "pq", "alpha", "beta", "rr", "rzn", "zro"):
+                g[name] = torch.zeros((), **f64)
+            g["st"] = torch.zeros(3, **f64)
+            self._graph = g
+        r, z, q, r_old, p = g["r"], g["z"], g["q"], g["r_old"], g["p"]
+
+        def body():
+            f0.spmv_exact(p, q)
+            torch.dot(p, q, out=g["pq"])
+            torch.div(g["rz"], g["pq"], out=g["alpha"])
+            x.addcmul_(p, g["alpha"])
+            r_old.copy_(r)  # z . r_old enters the Polak-Ribiere beta
+            r.addcmul_(q, g["alpha"], value=-1.0)
+            torch.dot(r, r, out=g["rr"])
+            self._vcycle(0, r, z)
+            torch.dot(r, z, out=g["rzn"])
+            torch.dot(z, r_old, out=g["zro"])
+            torch.div(g["rzn"] - g["zro"], g["rz"], out=g["beta"])
+            p.mul_(g["beta"]).add_(z)
+            g["rz"].copy_(g["rzn"])
+            torch.stack((g["rr"], g["rzn"], g["zro"]), out=g["st"])
+
+        r.copy_(b)
+        self._vcycle(0, r, z)
+        p.copy_(z)
+        torch.dot(r, z, out=g["rz"])
+        if not float(g["rz"]) > 0.0:
+            raise _Indefinite()
+        rn = bn
+        it = 0
+        while it < max_iter:
+            it += 1
+            if g["graph"] is not None:
+                g["graph"].replay()
+            else:
+                body()  # the first iteration runs eagerly (warm-up), then the capture
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    body()
+                g["graph"] = graph
+            s3 = g["st"].cpu().numpy()
+            rn = float(np.sqrt(s3[0]))
+            if not np.isfinite(rn):
+                raise FloatingPointError("multigrid FCG diverged (non-finite residual)")
+            if rn <= rtol * bn:
+                break
+            if not float(s3[1]) > 0.0:
+                raise _Indefinite()
+        return it, rn / bn
+
 
 class Multigrid(CycleFCG):
     """Flexible-CG solver preconditioned by a geometric multigrid V-cycle (see module doc).
@@ -400,12 +476,12 @@ class Multigrid(CycleFCG):
 
     def __init__(self, fine_mesh, fine_ev, dbc_nodes, youngs, poisson, nu=2, min_intervals=4,
                  max_levels=8, ratio=10.0, boost=1.1, coarse_rtol=1e-2, coarse_max_iter=2000,
-                 mixed=False, coarse_solver="pcg", fine_post=True, matrix_free=False):
+                 mixed=False, coarse_solver="auto", fine_post=True, matrix_free=False):
         self.fine_post = bool(fine_post)
         if matrix_free and (mixed or fine_mesh.celltype != fcg.HEX27):
             raise ValueError("matrix_free: hex27 fine levels in FP64 only (mixed=False)")
-        if coarse_solver not in ("pcg", "amg"):
-            raise ValueError(f"coarse_solver must be 'pcg' or 'amg', not {coarse_solver!r}")
+        if coarse_solver not in ("auto", "dense", "pcg", "amg"):
+            raise ValueError(f"coarse_solver must be 'auto', 'dense', 'pcg' or 'amg', not {coarse_solver!r}")
         box = getattr(fine_mesh, "box", None)
         if box is None or getattr(fine_mesh, "nranks", 1) != 1:
             raise ValueError("Multigrid needs a single-rank GridGenerator box (fcg.BoxMesh)")
@@ -440,6 +516,10 @@ class Multigrid(CycleFCG):
 
         self.levels = [_Level(fine_mesh, fine_ev, None, dbc_rows(fine_mesh), dev)]
         self.levels[0].matrix_free = bool(matrix_free)
+        if matrix_free:  # the action's per-context buffers and gather plan are set up here
+            zc = torch.zeros(fine_mesh.n_cols, dtype=torch.float64, device=dev)
+            fine_ev.tangent_apply(zc, zc, torch.empty(fine_mesh.n_rows, dtype=torch.float64, device=dev))
+            del zc
         self.P, self.R = [], []
         prev = fine_mesh
         for ivc in meshes:
@@ -462,9 +542,24 @@ class Multigrid(CycleFCG):
             prev = m
         for lvl in self.levels[1:-1]:
             lvl.estimate_lmax()
-        # coarsest level: block-Jacobi PCG (fcg_pcg_solve), or the native smoothed-aggregation AMG
-        # set up once on it (its rediscretised linear operator does not change between tangents)
+        # coarsest level: its rediscretised linear operator does not change between tangents, so
+        # it is factored once -- "dense": the inverse of the (small) matrix, one matrix-vector
+        # product per V-cycle, exact and without the host round trips of an iterative solve;
+        # "pcg": block-Jacobi PCG to coarse_rtol (fcg_pcg_solve); "amg": the native
+        # smoothed-aggregation AMG set up on it.  "auto": dense up to 6,000 DOFs, else PCG.
         self.coarse_amg = None
+        self.coarse_inv = None
+        last = self.levels[-1]
+        if coarse_solver == "auto":
+            coarse_solver = "dense" if last.n <= 6000 else "pcg"
+        self.coarse_solver = coarse_solver
+        self.graph_ok = coarse_solver == "dense"  # the V-cycle never waits on the host
+        if coarse_solver == "dense":
+            Kh = last.K.cpu().numpy()
+            A = np.zeros((last.n, last.n))
+            rows = np.repeat(np.arange(last.n), np.diff(last.mesh.rowptr))
+            A[rows, last.mesh.col_lid] = Kh
+            self.coarse_inv = torch.from_numpy(np.linalg.inv(A)).to(dev)
         if coarse_solver == "amg":
             from .amg import NativeAMG
             last = self.levels[-1]
@@ -472,9 +567,13 @@ class Multigrid(CycleFCG):
             self.coarse_amg.setup(last.K)
 
     def describe(self):
-        return [{"celltype": "hex27" if l.mesh.celltype == fcg.HEX27 else "hex8",
-                 "intervals": [int(l.mesh.box.interval[d]) for d in range(3)], "dofs": l.n,
-                 "lmax": l.lmax} for l in self.levels]
+        out = [{"celltype": "hex27" if l.mesh.celltype == fcg.HEX27 else "hex8",
+                "intervals": [int(l.mesh.box.interval[d]) for d in range(3)], "dofs": l.n,
+                "lmax": l.lmax} for l in self.levels]
+        out[-1]["coarse_solver"] = self.coarse_solver
+        if self.levels[0].matrix_free:
+            out[0]["operator"] = "matrix-free (fcg_tangent_apply)"
+        return out
 
     def set_state(self, u_col):
         """The displacement the next solve's tangent was evaluated at (the matrix-free fine
@@ -503,6 +602,9 @@ class Multigrid(CycleFCG):
         x.mul_(self.levels[l].mask)
 
     def _coarse_solve(self, lvl, b, x):
+        if self.coarse_inv is not None:
+            torch.mv(self.coarse_inv, b, out=x)
+            return
         if self.coarse_amg is not None:
             self.coarse_amg.solve(lvl.K, b, x, self.coarse_rtol, self.coarse_max_iter, setup=False)
             return

@@ -42,7 +42,7 @@ ap.add_argument("--mg-no-fine-post", action="store_true",
 ap.add_argument("--mg-matrix-free", action="store_true",
                 help="hex27: the fine level's smoother and V-cycle residual apply K(u) element by "
                      "element (fcg_tangent_apply) instead of reading the assembled K")
-ap.add_argument("--mg-coarse", default="pcg", choices=["pcg", "amg"],
+ap.add_argument("--mg-coarse", default="auto", choices=["auto", "dense", "pcg", "amg"],
                 help="coarsest-level solver of the geometric multigrid")
 ap.add_argument("--amg", action="store_true",
                 help="smoothed-aggregation AMG preconditioned flexible CG (4c_amd/amg.py)")
