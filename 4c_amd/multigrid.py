@@ -32,6 +32,7 @@ on the hex27 TotLag cantilever of tests/test_multigrid.py it raised the FCG iter
 import ctypes
 import os
 import sys
+import time
 
 import numpy as np
 import torch
@@ -149,8 +150,10 @@ class _LevelOps:
         """Largest eigenvalue of D^-1 K from the Lanczos tridiagonal of a short block-Jacobi PCG
         run on a random right-hand side (the CG estimate of hypre / AmgX Chebyshev smoothers;
         power iteration converges from below too slowly on these spectra)."""
-        g = torch.Generator(device="cpu").manual_seed(seed)
-        b = (torch.rand(self.n, generator=g, dtype=torch.float64) - 0.5).to(self.dev) * self.mask
+        # the random start vector is drawn on the device (a host draw of 24M values and its
+        # upload took ~0.2 s of config 3's first solve)
+        g = torch.Generator(device=self.dev).manual_seed(seed)
+        b = (torch.rand(self.n, generator=g, dtype=torch.float64, device=self.dev) - 0.5) * self.mask
         r = b.clone()
         z, q = self.z, self.r
         self.apply_dinv(r, z)
@@ -453,10 +456,14 @@ class CycleFCG:
                 g["graph"].replay()
             else:
                 body()  # the first iteration runs eagerly (warm-up), then the capture
+                t_cap = time.perf_counter()
                 graph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(graph):
                     body()
                 g["graph"] = graph
+                if os.environ.get("FCG_MG_GRAPH_TIMING"):
+                    print(f"  fcg graph captured in {1e3 * (time.perf_counter() - t_cap):.1f} ms",
+                          file=sys.stderr, flush=True)
             s3 = g["st"].cpu().numpy()
             rn = float(np.sqrt(s3[0]))
             if not np.isfinite(rn):
@@ -583,6 +590,7 @@ class Multigrid(CycleFCG):
     def _prepare(self, K):
         """lambda_max of D^-1 K barely moves between Newton iterations: it is estimated on the
         first solve and kept (re-estimated by CycleFCG.solve's restart)."""
+        t0 = time.perf_counter()
         f0 = self.levels[0]
         f0.K = K
         if self.mixed:
@@ -592,6 +600,9 @@ class Multigrid(CycleFCG):
         f0.setup_diag()
         if f0.lmax is None:
             f0.estimate_lmax()
+            if os.environ.get("FCG_MG_GRAPH_TIMING"):
+                print(f"  fine lambda_max estimate {1e3 * (time.perf_counter() - t0):.1f} ms",
+                      file=sys.stderr, flush=True)
 
     def _restrict(self, l, r, cb):
         self.R[l](r, cb, accumulate=False)
