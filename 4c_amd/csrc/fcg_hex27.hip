@@ -1217,13 +1217,22 @@ __global__ __launch_bounds__(256, 2) void h27_apply_kernel(H27ApplyArgs A)
 //   nodes      lanes (element, node line (a1, a2), component i): Q contracted over (m1, m2) with
 //              the line's factors, then over m0 for the line's three nodes -- 99 FMA instead of 729.
 // Four barriers per pass (Q reuses the nodal values' LDS).
-template <int KIN>
-__global__ __launch_bounds__(256, 2) void h27_apply_sf_kernel(H27ApplyArgs A)
+template <int KIN, int BT, int NE>
+__global__ __launch_bounds__(BT, BT == 64 ? 2 : 2) void h27_apply_sf_kernel(H27ApplyArgs A)
 {
+  // BT = 64: one wavefront holds whole elements (NE = 2, 54 of 64 lanes) and its phases are
+  // ordered by the wavefront's in-order LDS accesses, no workgroup barrier; BT = 256: NE = 9
+  // elements, the phases separated by __syncthreads
+  auto phase_sync = [&]() {
+    if constexpr (BT == 64)
+      __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    else
+      __syncthreads();
+  };
   constexpr int NSRC = KIN == 0 ? 2 : 3;  // X | x (linear) or X | u | x
   constexpr int NND = 81 * NSRC > 243 ? 81 * NSRC : 243;
-  __shared__ double nq[kApE][NND];               // nodal X | (u) | x, then Q[g][9]
-  __shared__ double gr[kApE][27][NSRC][3][3];     // d(src)_k / dxi_d at point l: [l][src][k][d]
+  __shared__ double nq[NE][NND];               // nodal X | (u) | x, then Q[g][9]
+  __shared__ double gr[NE][27][NSRC][3][3];     // d(src)_k / dxi_d at point l: [l][src][k][d]
   __shared__ double tL[9], tdL[9], wl[27];
   __shared__ uint8_t lat[27], posl[27];  // lattice position -> node (= point) number, and back
   // every LDS array is indexed by lattice position l = p0 + 3 p1 + 9 p2 (nodes and points alike)
@@ -1241,7 +1250,7 @@ __global__ __launch_bounds__(256, 2) void h27_apply_sf_kernel(H27ApplyArgs A)
     wl[tid] = c_w[c_latnode[tid]];
   }
   const double lam = A.lambda, mu = A.mu, cd = A.cdiag;
-  constexpr int NLD = (kApE * 81 * NSRC + 255) / 256;
+  constexpr int NLD = (NE * 81 * NSRC + BT - 1) / BT;
   // the gathers in two stages, one pass apart, so that no wait on a dependent load falls inside a
   // pass: stage 1 reads the element's node / DOF index of each item for the pass after next
   // (ele_nodes, apply_dof: independent loads), stage 2 the values for the next pass at the
@@ -1252,10 +1261,10 @@ __global__ __launch_bounds__(256, 2) void h27_apply_sf_kernel(H27ApplyArgs A)
 #pragma unroll
     for (int q = 0; q < NLD; ++q)
     {
-      int t = tid + 256 * q;
+      int t = tid + BT * q;
       __asm__ volatile("" : "+v"(t));  // index math per pass, not hoisted into live registers
       ix[q] = -1;
-      if (t >= kApE * 81 * NSRC) continue;
+      if (t >= NE * 81 * NSRC) continue;
       const int sl = t / (81 * NSRC), r = t - 81 * NSRC * sl;
       const int src = r / 81, rr = r - 81 * src, a = rr / 3, d = rr - 3 * a;
       const int64_t e = e0 + sl;
@@ -1267,7 +1276,7 @@ __global__ __launch_bounds__(256, 2) void h27_apply_sf_kernel(H27ApplyArgs A)
 #pragma unroll
     for (int q = 0; q < NLD; ++q)
     {
-      int t = tid + 256 * q;
+      int t = tid + BT * q;
       __asm__ volatile("" : "+v"(t));
       const int src = (t - 81 * NSRC * (t / (81 * NSRC))) / 81;
       const double* base = src == 0 ? A.node_x : (src == NSRC - 1 ? A.x_col : A.u_col);
@@ -1280,38 +1289,38 @@ __global__ __launch_bounds__(256, 2) void h27_apply_sf_kernel(H27ApplyArgs A)
   // XCD-contiguous passes: workgroup b runs on XCD b % 8 (round-robin dispatch); XCD x takes its
   // own eighth of the element chunks, its workgroups interleaved, so that elements sharing nodes
   // are gathered through one L2
-  const int64_t nch = (A.n_ele + kApE - 1) / kApE;
+  const int64_t nch = (A.n_ele + NE - 1) / NE;
   const int xcd = int(blockIdx.x & 7u);
   const int64_t per_xcd = (int64_t(gridDim.x) + 7 - xcd) / 8;
   const int64_t span = (nch + 7) / 8;
   const int64_t c0 = min(nch, int64_t(xcd) * span), c1 = min(nch, c0 + span);
-  auto first_of = [&](int64_t c) { return c < c1 ? c * kApE : int64_t(-1); };
+  auto first_of = [&](int64_t c) { return c < c1 ? c * NE : int64_t(-1); };
   int64_t ch = c0 + (blockIdx.x >> 3);
   index_of(first_of(ch), ix1);
   value_of(ix1);
   index_of(first_of(ch + per_xcd), ix1);
   for (; ch < c1; ch += per_xcd)
   {
-    const int64_t e0 = ch * kApE;
-    __syncthreads();  // the previous pass's node phase has read Q
+    const int64_t e0 = ch * NE;
+    phase_sync();  // the previous pass's node phase has read Q
 #pragma unroll
     for (int q = 0; q < NLD; ++q)
     {
-      const int t = tid + 256 * q;
-      if (t < kApE * 81 * NSRC)
+      const int t = tid + BT * q;
+      if (t < NE * 81 * NSRC)
       {
         const int sl = t / (81 * NSRC), r = t - 81 * NSRC * sl;
         const int src = r / 81, rr = r - 81 * src, a = rr / 3;
         nq[sl][81 * src + 3 * posl[a] + rr - 3 * a] = pre[q];
       }
     }
-    __syncthreads();
+    phase_sync();
     index_of(first_of(ch + 2 * per_xcd), ix2);  // pass after next: indices
     value_of(ix1);                               // next pass: values at last pass's indices
 #pragma unroll
     for (int q = 0; q < NLD; ++q) ix1[q] = ix2[q];
     // ---- gradients at the points of line (m1, m2), one source
-    if (sg < kApE && e0 + sg < A.n_ele)
+    if (sg < NE && e0 + sg < A.n_ele)
     {
       const int line = rg / NSRC, src = rg - NSRC * (rg / NSRC);
       const int m1 = line % 3, m2 = line / 3;
@@ -1364,9 +1373,9 @@ __global__ __launch_bounds__(256, 2) void h27_apply_sf_kernel(H27ApplyArgs A)
         }
       }
     }
-    __syncthreads();
+    phase_sync();
     // ---- point algebra: lanes (s27, g)
-    if (s27 < kApE && e0 + s27 < A.n_ele)
+    if (s27 < NE && e0 + s27 < A.n_ele)
     {
       const int g = r27;  // lattice position of the point
       const double* G = &gr[s27][g][0][0][0];
@@ -1439,9 +1448,9 @@ __global__ __launch_bounds__(256, 2) void h27_apply_sf_kernel(H27ApplyArgs A)
         for (int k = 0; k < 3; ++k)
           Q[3 * i + k] = P[i][0] * iJ[3 * k] + P[i][1] * iJ[3 * k + 1] + P[i][2] * iJ[3 * k + 2];
     }
-    __syncthreads();
+    phase_sync();
     // ---- node lines: lanes (s27, line (a1, a2), component i)
-    if (s27 < kApE && e0 + s27 < A.n_ele)
+    if (s27 < NE && e0 + s27 < A.n_ele)
     {
       const int line = r27 / 3, i = r27 - 3 * (r27 / 3);
       const int a1 = line % 3, a2 = line / 3;
@@ -1708,9 +1717,15 @@ hipError_t launch_h27_apply(const DeviceMesh& m, const double* d_u_col, const do
     }();
     const dim3 grid(unsigned(std::min<int64_t>(passes, cap))), block(256);
     // FCG_H27_APPLY=direct: the per-point kernel without sum factorisation (A/B runs)
-    static const bool direct = [] {
+    // FCG_H27_APPLY=sf: the 256-lane sum-factorised kernel (9 elements per pass, barriers)
+    static const std::string variant = [] {
       const char* e = std::getenv("FCG_H27_APPLY");
-      return e && std::string(e) == "direct";
+      return std::string(e ? e : "wave");
+    }();
+    const bool direct = variant == "direct", workgroup = variant == "sf";
+    static const int64_t cap_w = [] {
+      const char* e = std::getenv("FCG_H27_APPLY_GRID");
+      return e ? std::max<int64_t>(8, std::atoll(e)) : int64_t(256 * 8);
     }();
     if (direct)
     {
@@ -1719,10 +1734,22 @@ hipError_t launch_h27_apply(const DeviceMesh& m, const double* d_u_col, const do
       else
         hipLaunchKernelGGL((h27_apply_kernel<1>), grid, block, 0, stream, a);
     }
-    else if (m.kinem == 0)
-      hipLaunchKernelGGL((h27_apply_sf_kernel<0>), grid, block, 0, stream, a);
+    else if (workgroup)
+    {
+      if (m.kinem == 0)
+        hipLaunchKernelGGL((h27_apply_sf_kernel<0, 256, kApE>), grid, block, 0, stream, a);
+      else
+        hipLaunchKernelGGL((h27_apply_sf_kernel<1, 256, kApE>), grid, block, 0, stream, a);
+    }
     else
-      hipLaunchKernelGGL((h27_apply_sf_kernel<1>), grid, block, 0, stream, a);
+    {
+      // one wavefront per workgroup, 8 resident per CU (LDS 15.7 KB, <= 256 VGPRs)
+      const dim3 gw(unsigned(std::min<int64_t>((m.n_ele + 1) / 2, cap_w))), bw(64);
+      if (m.kinem == 0)
+        hipLaunchKernelGGL((h27_apply_sf_kernel<0, 64, 2>), gw, bw, 0, stream, a);
+      else
+        hipLaunchKernelGGL((h27_apply_sf_kernel<1, 64, 2>), gw, bw, 0, stream, a);
+    }
     const hipError_t he = hipGetLastError();
     if (he != hipSuccess) return he;
   }
