@@ -979,7 +979,8 @@ struct H27ApplyArgs {
   const double* x_col;
   const int32_t* inc_of;
   const int32_t* ele_dof;  // [n_ele][27] column LID of each element node's first DOF
-  double* ye;  // [n_inc][3]
+  double* ye;  // [n_inc + 1][3] (the last triple: target of the unowned nodes' stores)
+  int64_t n_inc;
   double lambda, mu, cdiag;
 };
 
@@ -1235,6 +1236,7 @@ __global__ __launch_bounds__(BT, BT == 64 ? 2 : 2) void h27_apply_sf_kernel(H27A
   __shared__ double gr[NE][27][NSRC][3][3];     // d(src)_k / dxi_d at point l: [l][src][k][d]
   __shared__ double tL[9], tdL[9], wl[27];
   __shared__ uint8_t lat[27], posl[27];  // lattice position -> node (= point) number, and back
+  __shared__ int32_t incs[NE][27];        // the pass's incidences of (element, node), -1 = unowned
   // every LDS array is indexed by lattice position l = p0 + 3 p1 + 9 p2 (nodes and points alike)
   const int tid = threadIdx.x;
   if (tid < 9)
@@ -1256,31 +1258,45 @@ __global__ __launch_bounds__(BT, BT == 64 ? 2 : 2) void h27_apply_sf_kernel(H27A
   // (ele_nodes, apply_dof: independent loads), stage 2 the values for the next pass at the
   // indices stage 1 read one pass earlier
   double pre[NLD];
-  int32_t ix1[NLD], ix2[NLD];
+  int32_t ix1[NLD];
+  // Every gather is unconditional (a clamped address; validity is re-derived from the pass's
+  // first element where the value is consumed), so each pass issues a fixed number of memory
+  // operations and the compiler's wait before a use can skip what was issued after it.  Per
+  // pass: value_of for the next pass (at the indices index_of loaded one pass earlier), then
+  // index_of for the pass after next, then the compute phases and the node stores.
+  auto item_ok = [&](int t, int64_t e0) {
+    return t < NE * 81 * NSRC && e0 >= 0 && e0 + t / (81 * NSRC) < A.n_ele;
+  };
   auto index_of = [&](int64_t e0, int32_t* ix) {
 #pragma unroll
     for (int q = 0; q < NLD; ++q)
     {
       int t = tid + BT * q;
       __asm__ volatile("" : "+v"(t));  // index math per pass, not hoisted into live registers
-      ix[q] = -1;
-      if (t >= NE * 81 * NSRC) continue;
       const int sl = t / (81 * NSRC), r = t - 81 * NSRC * sl;
-      const int src = r / 81, rr = r - 81 * src, a = rr / 3, d = rr - 3 * a;
-      const int64_t e = e0 + sl;
-      if (e0 < 0 || e >= A.n_ele) continue;
-      ix[q] = src == 0 ? 3 * A.ele_nodes[e * 27 + a] + d : A.ele_dof[e * 27 + a] + d;
+      const int src = r / 81, a = (r - 81 * src) / 3;
+      const int64_t e = item_ok(t, e0) ? e0 + sl : 0;
+      const int32_t* tab = src == 0 ? A.ele_nodes : A.ele_dof;
+      ix[q] = tab[e * 27 + (t < NE * 81 * NSRC ? a : 0)];
     }
   };
-  auto value_of = [&](const int32_t* ix) {
+  int32_t incp = 0;  // lane < 27 NE: incidence of (element, node) of the next pass
+  auto value_of = [&](const int32_t* ix, int64_t e0n) {
+    {
+      const int sl = tid / 27;
+      const bool ok = tid < 27 * NE && e0n >= 0 && e0n + sl < A.n_ele;
+      incp = A.inc_of[ok ? (e0n + sl) * 27 + tid - 27 * sl : 0];
+    }
 #pragma unroll
     for (int q = 0; q < NLD; ++q)
     {
       int t = tid + BT * q;
       __asm__ volatile("" : "+v"(t));
-      const int src = (t - 81 * NSRC * (t / (81 * NSRC))) / 81;
+      const int r = t - 81 * NSRC * (t / (81 * NSRC));
+      const int src = r / 81, d = r - 81 * src - 3 * ((r - 81 * src) / 3);
       const double* base = src == 0 ? A.node_x : (src == NSRC - 1 ? A.x_col : A.u_col);
-      pre[q] = ix[q] >= 0 ? base[ix[q]] : 0.0;
+      const int32_t at = (src == 0 ? 3 * ix[q] : ix[q]) + d;
+      pre[q] = base[item_ok(t, e0n) ? at : 0];
     }
   };
   // lane roles: gradients (s, line, src), points (s, g), nodes (s, line, i)
@@ -1297,8 +1313,9 @@ __global__ __launch_bounds__(BT, BT == 64 ? 2 : 2) void h27_apply_sf_kernel(H27A
   auto first_of = [&](int64_t c) { return c < c1 ? c * NE : int64_t(-1); };
   int64_t ch = c0 + (blockIdx.x >> 3);
   index_of(first_of(ch), ix1);
-  value_of(ix1);
+  value_of(ix1, first_of(ch));
   index_of(first_of(ch + per_xcd), ix1);
+  int64_t e0pre = first_of(ch);  // the pass whose values sit in pre / incp
   for (; ch < c1; ch += per_xcd)
   {
     const int64_t e0 = ch * NE;
@@ -1314,11 +1331,11 @@ __global__ __launch_bounds__(BT, BT == 64 ? 2 : 2) void h27_apply_sf_kernel(H27A
         nq[sl][81 * src + 3 * posl[a] + rr - 3 * a] = pre[q];
       }
     }
+    if (tid < 27 * NE) incs[tid / 27][tid - 27 * (tid / 27)] = incp;
     phase_sync();
-    index_of(first_of(ch + 2 * per_xcd), ix2);  // pass after next: indices
-    value_of(ix1);                               // next pass: values at last pass's indices
-#pragma unroll
-    for (int q = 0; q < NLD; ++q) ix1[q] = ix2[q];
+    e0pre = first_of(ch + per_xcd);
+    value_of(ix1, e0pre);                        // next pass: values at last pass's indices
+    index_of(first_of(ch + 2 * per_xcd), ix1);  // pass after next: indices
     // ---- gradients at the points of line (m1, m2), one source
     if (sg < NE && e0 + sg < A.n_ele)
     {
@@ -1472,15 +1489,16 @@ __global__ __launch_bounds__(BT, BT == 64 ? 2 : 2) void h27_apply_sf_kernel(H27A
             z12[m0] += c1 * q[1] + c2 * q[2];
           }
         }
-      const int64_t e = e0 + s27;
 #pragma unroll
       for (int a0 = 0; a0 < 3; ++a0)
       {
         const int a = lat[a0 + 3 * line];
-        const int32_t k = A.inc_of[e * 27 + a];
+        const int32_t k = incs[s27][a];
         const double y = tdL[a0] * z0[0] + tdL[3 + a0] * z0[1] + tdL[6 + a0] * z0[2] +
                          tL[a0] * z12[0] + tL[3 + a0] * z12[1] + tL[6 + a0] * z12[2];
-        if (k >= 0) A.ye[3 * int64_t(k) + i] = y;
+        // unconditional (an unowned node's value goes to the spare triple): a static store count
+        // per pass lets the next pass's wait skip these stores
+        A.ye[3 * (k >= 0 ? int64_t(k) : A.n_inc) + i] = y;
       }
     }
   }
@@ -1705,6 +1723,7 @@ hipError_t launch_h27_apply(const DeviceMesh& m, const double* d_u_col, const do
     a.inc_of = m.inc_of;
     a.ele_dof = m.apply_dof;
     a.ye = m.apply_ye;
+    a.n_inc = m.n_inc;
     a.lambda = m.lambda;
     a.mu = m.mu;
     a.cdiag = m.cdiag;

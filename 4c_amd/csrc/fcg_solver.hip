@@ -456,7 +456,7 @@ int fcg_tangent_apply(fcg_ctx* ctx, const double* d_u_col, const double* d_x_col
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   if (!m.apply_ye && m.n_inc > 0)
   {
-    const size_t bytes = size_t(m.n_inc) * 3 * sizeof(double);
+    const size_t bytes = size_t(m.n_inc + 1) * 3 * sizeof(double);  // + the spare triple
     const hipError_t he = hipMalloc(&m.apply_ye, bytes);
     if (he != hipSuccess)
     {
