@@ -375,6 +375,50 @@ inline unsigned spmv_grid(const DeviceMesh& m, int lpn, bool partials)
   return partials ? capped_blocks(m.n_rownodes * lpn, kBlock) : blocks_for(m.n_rownodes * lpn, kBlock);
 }
 
+// y = K x on a GridGenerator hex8 box whose elements are all the same parallelepiped (the
+// multigrid's rediscretised coarse levels): a 27-point stencil of 3 x 3 blocks per node class
+// (low face / interior / high face along each axis: 27 classes), S[class][offset][3 x 3] summed
+// from the one element matrix; rows of clamped nodes are unit rows (y = x).  One thread per node,
+// its 27 neighbours' DOF triples read through the lattice's row table.
+__global__ __launch_bounds__(kBlock) void box_stencil_kernel(int nx, int ny, int nz,
+    const int32_t* __restrict__ row_of, const uint8_t* __restrict__ clamped,
+    const double* __restrict__ S, const double* __restrict__ x, double* __restrict__ y)
+{
+  const int64_t n = int64_t(nx) * ny * nz;
+  const int64_t id = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (id >= n) return;
+  const int i = int(id % nx), j = int((id / nx) % ny), k = int(id / (int64_t(nx) * ny));
+  const int32_t r0 = row_of[id];
+  if (r0 < 0) return;
+  if (clamped[id])
+  {
+    y[r0] = x[r0];
+    y[r0 + 1] = x[r0 + 1];
+    y[r0 + 2] = x[r0 + 2];
+    return;
+  }
+  const int cls = (i == 0 ? 0 : (i == nx - 1 ? 2 : 1)) + 3 * (j == 0 ? 0 : (j == ny - 1 ? 2 : 1)) +
+                  9 * (k == 0 ? 0 : (k == nz - 1 ? 2 : 1));
+  const double* Sc = S + 243 * cls;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+#pragma unroll 3
+  for (int o = 0; o < 27; ++o)
+  {
+    const int di = o % 3 - 1, dj = (o / 3) % 3 - 1, dk = o / 9 - 1;
+    const int ii = i + di, jj = j + dj, kk = k + dk;
+    if (ii < 0 || ii >= nx || jj < 0 || jj >= ny || kk < 0 || kk >= nz) continue;
+    const int32_t c = row_of[(int64_t(kk) * ny + jj) * nx + ii];
+    const double x0 = x[c], x1 = x[c + 1], x2 = x[c + 2];
+    const double* B = Sc + 9 * o;
+    a0 += B[0] * x0 + B[1] * x1 + B[2] * x2;
+    a1 += B[3] * x0 + B[4] * x1 + B[5] * x2;
+    a2 += B[6] * x0 + B[7] * x1 + B[8] * x2;
+  }
+  y[r0] = a0;
+  y[r0 + 1] = a1;
+  y[r0 + 2] = a2;
+}
+
 // partial[blockIdx] = sum over the block's rows of p . q (grid-stride, fixed assignment)
 __global__ __launch_bounds__(kBlock) void dot_kernel(const double* __restrict__ p,
     const double* __restrict__ q, int64_t n, double* partial)
@@ -722,6 +766,18 @@ int fcg_node_transfer(int device, int64_t n_out, const int64_t* d_ptr, const int
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(fcg::node_transfer_kernel, dim3(fcg::blocks_for(n_out, fcg::kBlock)), dim3(fcg::kBlock), 0, s,
       d_ptr, d_src_row0, d_w, d_dst_row0, d_x, d_y, n_out, accumulate);
+  return hipGetLastError() == hipSuccess ? FCG_OK : fcg_device_error();
+}
+
+int fcg_box_stencil_apply(int device, int nx, int ny, int nz, const int32_t* d_row_of,
+    const uint8_t* d_clamped, const double* d_S, const double* d_x, double* d_y, void* stream)
+{
+  const int64_t n = int64_t(nx) * ny * nz;
+  if (nx < 2 || ny < 2 || nz < 2 || !d_row_of || !d_clamped || !d_S || !d_x || !d_y) return FCG_ERR_ARG;
+  if (!fcg_use_device(device)) return fcg_device_error();
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(fcg::box_stencil_kernel, dim3(fcg::blocks_for(n, fcg::kBlock)), dim3(fcg::kBlock), 0, s,
+      nx, ny, nz, d_row_of, d_clamped, d_S, d_x, d_y);
   return hipGetLastError() == hipSuccess ? FCG_OK : fcg_device_error();
 }
 

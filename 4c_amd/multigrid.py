@@ -119,6 +119,68 @@ def transfer_tables(fine, coarse):
     return P, R
 
 
+def box_stencil(mesh, youngs, poisson, device, dbc_rows):
+    """The 27-point stencil of a rediscretised hex8 GridGenerator box (all elements the same
+    parallelepiped, linear StVK) for fcg_box_stencil_apply: (nx, ny, nz, row_of, clamped, S) with
+    S[27 node classes][27 offsets][3 x 3] summed from the element matrix, which the library
+    assembles on a one-element box of the same size and rotation."""
+    box = mesh.box
+    iv = [int(box.interval[d]) for d in range(3)]
+    if min(iv) < 1:
+        raise ValueError("box stencil: empty box")
+    h = [(box.upper[d] - box.lower[d]) / iv[d] for d in range(3)]
+    one = fcg.BoxMesh(fcg.HEX8, (1, 1, 1), lower=(0.0, 0.0, 0.0), upper=tuple(h),
+                      rotation=tuple(box.rotation[d] for d in range(3)))
+    ev = fcg.Evaluator(one, kinematics=fcg.LINEAR, youngs=youngs, poisson=poisson, device=device.index or 0)
+    f64 = dict(dtype=torch.float64, device=device)
+    K = torch.zeros(one.nnz, **f64)
+    ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, torch.zeros(one.n_cols, **f64),
+                       torch.zeros(one.n_rows, **f64), K)
+    Kh = K.cpu().numpy()
+    ev.close()
+    A = np.zeros((one.n_rows, one.n_cols))
+    A[np.repeat(np.arange(one.n_rows), np.diff(one.rowptr)), one.col_lid] = Kh
+    lat1 = node_lattice(one)
+    row1 = {tuple(int(v) for v in lat1[n]): int(one.node_dof_row[n]) for n in range(len(lat1))}
+    S = np.zeros((27, 27, 3, 3))
+    for cls in range(27):
+        c = (cls % 3, (cls // 3) % 3, cls // 9)
+        for ea in range(2):
+            for eb in range(2):
+                for ec in range(2):
+                    e = (ea, eb, ec)
+                    if any((c[d] == 0 and e[d] == 0) or (c[d] == 2 and e[d] == 1) for d in range(3)):
+                        continue
+                    rn = row1[(1 - ea, 1 - eb, 1 - ec)]
+                    for p in range(2):
+                        for q in range(2):
+                            for r in range(2):
+                                o = (ea - 1 + p) + 1 + 3 * ((eb - 1 + q) + 1) + 9 * ((ec - 1 + r) + 1)
+                                rm = row1[(p, q, r)]
+                                S[cls, o] += A[rn:rn + 3, rm:rm + 3]
+    lat = node_lattice(mesh)
+    nx, ny, nz = iv[0] + 1, iv[1] + 1, iv[2] + 1
+    row_of = np.full(nx * ny * nz, -1, dtype=np.int32)
+    idx = lat[:, 0] + nx * (lat[:, 1] + ny * lat[:, 2])
+    row_of[idx] = mesh.node_dof_row
+    clamped = np.zeros(nx * ny * nz, dtype=np.uint8)
+    dbc = np.asarray(dbc_rows, dtype=np.int64)
+    if len(dbc):
+        is_dbc = np.zeros(mesh.n_rows, dtype=bool)
+        is_dbc[dbc] = True
+        ok = mesh.node_dof_row >= 0
+        full = np.zeros(len(lat), dtype=bool)
+        r0 = mesh.node_dof_row[ok]
+        full[ok] = is_dbc[r0] & is_dbc[r0 + 1] & is_dbc[r0 + 2]
+        part = np.zeros(len(lat), dtype=bool)
+        part[ok] = (is_dbc[r0] | is_dbc[r0 + 1] | is_dbc[r0 + 2]) & ~full[ok]
+        if part.any():
+            return None  # a node with some of its DOFs clamped: no unit-row node class for it
+        clamped[idx[full]] = 1
+    return (nx, ny, nz, torch.from_numpy(row_of).to(device), torch.from_numpy(clamped).to(device),
+            torch.from_numpy(S.ravel()).to(device))
+
+
 class _Transfer:
     def __init__(self, tab, device):
         ptr, src, w, dst = tab
@@ -206,6 +268,7 @@ class _Level(_LevelOps):
         # fcg_tangent_apply at the state set_state gave, the Dirichlet rows as unit rows
         self.matrix_free = False
         self.mf_u = None
+        self.stencil = None  # rediscretised box levels: fcg_box_stencil_apply instead of K
         self.mf_dbc = torch.as_tensor(np.asarray(dbc_rows, dtype=np.int64), device=device)
 
     def stream(self):
@@ -225,16 +288,26 @@ class _Level(_LevelOps):
             self.ev._raise(rc, -1)
 
     def spmv(self, x, y):
-        """The V-cycle's operator: K, its FP32 copy when the level has one, or (matrix_free) the
-        element-by-element tangent action."""
+        """The V-cycle's operator: K, its FP32 copy when the level has one, (matrix_free) the
+        element-by-element tangent action, or (stencil) the box's 27-point stencil."""
         if self.matrix_free:
             self.apply_matrix_free(x, y)
+        elif self.stencil is not None:
+            self.spmv_exact(x, y)
         elif self.K32 is not None:
             self.ev.spmv_f32(self.K32, x, y, stream=self.stream())
         else:
             self.ev.spmv(self.K, x, y, stream=self.stream())
 
     def spmv_exact(self, x, y):
+        if self.stencil is not None:
+            nx, ny, nz, row_of, clamped, S = self.stencil
+            rc = fcg.lib().fcg_box_stencil_apply(self.dev.index or 0, nx, ny, nz, _ptr(row_of),
+                                                 _ptr(clamped), _ptr(S), _ptr(x), _ptr(y),
+                                                 ctypes.c_void_p(self.stream().cuda_stream))
+            if rc != 0:
+                raise fcg.FcgError(rc, "fcg_box_stencil_apply failed")
+            return
         self.ev.spmv(self.K, x, y, stream=self.stream())
 
     def spmv_cycle(self, x, y):
@@ -542,6 +615,10 @@ class Multigrid(CycleFCG):
             ev.dirichlet_apply(torch.as_tensor(rows, device=dev), K)
             lvl = _Level(m, ev, K, rows, dev)
             lvl.setup_diag()
+            # every element of a rediscretised box is the same parallelepiped: the level applies
+            # its 27-point stencil instead of reading K (FCG_MG_STENCIL=0: the assembled K)
+            if os.environ.get("FCG_MG_STENCIL", "1") != "0" and min(ivc) >= 1:
+                lvl.stencil = box_stencil(m, youngs, poisson, dev, rows)
             P, R = transfer_tables(prev, m)
             self.P.append(_Transfer(P, dev))
             self.R.append(_Transfer(R, dev))

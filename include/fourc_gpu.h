@@ -251,6 +251,15 @@ int fcg_block_jacobi_apply(fcg_ctx* ctx, const double* d_dinv, const double* d_r
 int fcg_node_transfer(int device, int64_t n_out, const int64_t* d_ptr, const int32_t* d_src_row0,
     const double* d_w, const int32_t* d_dst_row0, const double* d_x, double* d_y, int accumulate,
     void* stream);
+/* y = K x of a hex8 GridGenerator box whose elements are all the same parallelepiped (the
+ * multigrid's rediscretised coarse levels, 4c_amd/multigrid.py): nx x ny x nz nodes (x fastest,
+ * each >= 2), d_row_of[node] = row LID of its first DOF (-1: no row), d_clamped[node] != 0 makes
+ * the node's rows unit rows (fcg_dirichlet_apply's), d_S[27 classes][27 offsets][3 x 3] the
+ * stencil blocks summed from the element matrix (class = low face / interior / high face per axis,
+ * offset (dx, dy, dz) in {-1, 0, 1}^3, both x fastest).  Equal to fcg_spmv on that box's assembled
+ * K to rounding, without reading K.  Asynchronous on `stream`. */
+int fcg_box_stencil_apply(int device, int nx, int ny, int nz, const int32_t* d_row_of,
+    const uint8_t* d_clamped, const double* d_S, const double* d_x, double* d_y, void* stream);
 
 /* Smoothed-aggregation AMG for meshes without a box hierarchy (replaces the MueLu preconditioner
  * 4C builds in 4C_linear_solver_preconditioner_muelu.cpp; algorithm in fcg_amg_setup.cpp).

@@ -120,6 +120,36 @@ def _cantilever(ct, n, kin, load, length=2.0, jitter=0.0):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("iv,rot", [((5, 4, 3), (0.0, 0.0, 0.0)), ((3, 6, 2), (0.3, -0.2, 0.5))])
+def test_box_stencil_matches_assembled_operator(iv, rot):
+    """fcg_box_stencil_apply (the coarse levels' operator) = fcg_spmv on the same box's assembled,
+    Dirichlet-modified K, every node class (faces, edges, corners, interior) and unit rows."""
+    torch, dev = _dev()
+    mesh = fcg.BoxMesh(fcg.HEX8, iv, upper=(2.0, 1.0, 1.5), rotation=rot)
+    clamp = np.isclose(mgm.node_lattice(mesh)[:, 0], 0)
+    nodes = np.nonzero(clamp)[0]
+    rows = np.sort((mesh.node_dof_row[nodes][:, None] + np.arange(3)).ravel()).astype(np.int32)
+    ev = fcg.Evaluator(mesh, kinematics=fcg.LINEAR, youngs=E, poisson=NU)
+    f64 = dict(dtype=torch.float64, device=dev)
+    K = torch.zeros(mesh.nnz, **f64)
+    ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, torch.zeros(mesh.n_cols, **f64),
+                       torch.zeros(mesh.n_rows, **f64), K)
+    ev.dirichlet_apply(torch.as_tensor(rows, device=dev), K)
+    lvl = mgm._Level(mesh, ev, K, rows, dev)
+    x = torch.from_numpy(np.random.default_rng(2).standard_normal(mesh.n_rows)).to(dev)
+    y0, y1 = torch.empty_like(x), torch.empty_like(x)
+    lvl.spmv_exact(x, y0)
+    lvl.stencil = mgm.box_stencil(mesh, E, NU, dev, rows)
+    assert lvl.stencil is not None
+    lvl.spmv_exact(x, y1)
+    torch.cuda.synchronize()
+    a, b = y0.cpu().numpy(), y1.cpu().numpy()
+    assert np.linalg.norm(a - b) <= 1e-13 * np.linalg.norm(a)
+    assert np.array_equal(b[rows], x.cpu().numpy()[rows])
+    ev.close()
+
+
+@pytest.mark.gpu
 def test_block_jacobi_apply_device():
     torch, dev = _dev()
     mesh, clamp, dbc, fext = _cantilever(fcg.HEX8, 4, fcg.LINEAR, -1e-2)
