@@ -419,6 +419,84 @@ __global__ __launch_bounds__(kBlock) void box_stencil_kernel(int nx, int ny, int
   y[r0 + 2] = a2;
 }
 
+// Multigrid transfer between a GridGenerator box lattice and its 2:1 coarsening (fine lattice
+// 2 (n_c - 1) + 1 points per axis: hex27 -> hex8 on the same elements, hex8 n -> n / 2), weights
+// implicit (1 on a coincident point, 1/2 to both neighbours of a midpoint, products over the
+// axes) instead of read from tables.  mode 0, prolongation, one thread per fine node:
+// y_f (+)= sum_c w x_c; mode 1, restriction (the transpose), one thread per coarse node:
+// y_c = sum_f w x_f.  Rows whose node is flagged in zero_out are set to 0 (the level's Dirichlet
+// mask).  Fixed summation order: deterministic.
+__global__ __launch_bounds__(kBlock) void box_transfer_kernel(int mode, int fnx, int fny, int fnz,
+    int cnx, int cny, int cnz, const int32_t* __restrict__ frow, const int32_t* __restrict__ crow,
+    const uint8_t* __restrict__ zero_out, const double* __restrict__ x, double* __restrict__ y,
+    int accumulate)
+{
+  const int64_t id = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (mode == 0)
+  {
+    if (id >= int64_t(fnx) * fny * fnz) return;
+    const int i = int(id % fnx), j = int((id / fnx) % fny), k = int(id / (int64_t(fnx) * fny));
+    const int32_t r = frow[id];
+    if (r < 0) return;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+    if (!zero_out[id])
+    {
+      const int ni = 1 + (i & 1), nj = 1 + (j & 1), nk = 1 + (k & 1);
+      const double wi = (i & 1) ? 0.5 : 1.0, wj = (j & 1) ? 0.5 : 1.0, wk = (k & 1) ? 0.5 : 1.0;
+      for (int c = 0; c < nk; ++c)
+        for (int b = 0; b < nj; ++b)
+          for (int a = 0; a < ni; ++a)
+          {
+            const int32_t s = crow[(int64_t((k >> 1) + c) * cny + (j >> 1) + b) * cnx + (i >> 1) + a];
+            const double w = wi * wj * wk;
+            a0 += w * x[s];
+            a1 += w * x[s + 1];
+            a2 += w * x[s + 2];
+          }
+      if (accumulate)
+      {
+        a0 += y[r];
+        a1 += y[r + 1];
+        a2 += y[r + 2];
+      }
+    }
+    y[r] = a0;
+    y[r + 1] = a1;
+    y[r + 2] = a2;
+    return;
+  }
+  if (id >= int64_t(cnx) * cny * cnz) return;
+  const int I = int(id % cnx), J = int((id / cnx) % cny), K = int(id / (int64_t(cnx) * cny));
+  const int32_t r = crow[id];
+  if (r < 0) return;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+  if (!zero_out[id])
+    for (int dk = -1; dk <= 1; ++dk)
+    {
+      const int k = 2 * K + dk;
+      if (k < 0 || k >= fnz) continue;
+      for (int dj = -1; dj <= 1; ++dj)
+      {
+        const int j = 2 * J + dj;
+        if (j < 0 || j >= fny) continue;
+        for (int di = -1; di <= 1; ++di)
+        {
+          const int i = 2 * I + di;
+          if (i < 0 || i >= fnx) continue;
+          const int32_t s = frow[(int64_t(k) * fny + j) * fnx + i];
+          if (s < 0) continue;
+          const double w = (di ? 0.5 : 1.0) * (dj ? 0.5 : 1.0) * (dk ? 0.5 : 1.0);
+          a0 += w * x[s];
+          a1 += w * x[s + 1];
+          a2 += w * x[s + 2];
+        }
+      }
+    }
+  y[r] = a0;
+  y[r + 1] = a1;
+  y[r + 2] = a2;
+}
+
 // partial[blockIdx] = sum over the block's rows of p . q (grid-stride, fixed assignment)
 __global__ __launch_bounds__(kBlock) void dot_kernel(const double* __restrict__ p,
     const double* __restrict__ q, int64_t n, double* partial)
@@ -766,6 +844,22 @@ int fcg_node_transfer(int device, int64_t n_out, const int64_t* d_ptr, const int
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(fcg::node_transfer_kernel, dim3(fcg::blocks_for(n_out, fcg::kBlock)), dim3(fcg::kBlock), 0, s,
       d_ptr, d_src_row0, d_w, d_dst_row0, d_x, d_y, n_out, accumulate);
+  return hipGetLastError() == hipSuccess ? FCG_OK : fcg_device_error();
+}
+
+int fcg_box_transfer(int device, int mode, int fnx, int fny, int fnz, int cnx, int cny, int cnz,
+    const int32_t* d_fine_row_of, const int32_t* d_coarse_row_of, const uint8_t* d_zero_out,
+    const double* d_x, double* d_y, int accumulate, void* stream)
+{
+  if ((mode != 0 && mode != 1) || cnx < 2 || cny < 2 || cnz < 2 || fnx != 2 * cnx - 1 ||
+      fny != 2 * cny - 1 || fnz != 2 * cnz - 1 || !d_fine_row_of || !d_coarse_row_of || !d_zero_out ||
+      !d_x || !d_y)
+    return FCG_ERR_ARG;
+  if (!fcg_use_device(device)) return fcg_device_error();
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t n = mode == 0 ? int64_t(fnx) * fny * fnz : int64_t(cnx) * cny * cnz;
+  hipLaunchKernelGGL(fcg::box_transfer_kernel, dim3(fcg::blocks_for(n, fcg::kBlock)), dim3(fcg::kBlock), 0, s,
+      mode, fnx, fny, fnz, cnx, cny, cnz, d_fine_row_of, d_coarse_row_of, d_zero_out, d_x, d_y, accumulate);
   return hipGetLastError() == hipSuccess ? FCG_OK : fcg_device_error();
 }
 

@@ -200,6 +200,55 @@ class _Transfer:
             raise fcg.FcgError(rc, "fcg_node_transfer failed")
 
 
+def _lattice_rows(mesh, rows):
+    """(dims, row_of[lattice], node_dirichlet[lattice]) of a box mesh: the row LID of each lattice
+    point's first DOF and whether all its DOFs are Dirichlet rows (None when some node is only
+    partly constrained)."""
+    lat = node_lattice(mesh)
+    dims = lat.max(axis=0) + 1
+    idx = lat[:, 0] + dims[0] * (lat[:, 1] + dims[1] * lat[:, 2])
+    row_of = np.full(int(np.prod(dims)), -1, dtype=np.int32)
+    row_of[idx] = mesh.node_dof_row
+    is_dbc = np.zeros(mesh.n_rows, dtype=bool)
+    is_dbc[np.asarray(rows, dtype=np.int64)] = True
+    ok = mesh.node_dof_row >= 0
+    r0 = mesh.node_dof_row[ok]
+    cnt = is_dbc[r0].astype(int) + is_dbc[r0 + 1] + is_dbc[r0 + 2]
+    if ((cnt > 0) & (cnt < 3)).any():
+        return None
+    zero = np.zeros(len(row_of), dtype=np.uint8)
+    zero[idx[ok][cnt == 3]] = 1
+    return dims, row_of, zero
+
+
+class _BoxTransfer:
+    """fcg_box_transfer between a box level and its 2:1 coarsening, the level masks applied in the
+    kernel (prolong: the fine level's Dirichlet rows, restrict: the coarse level's)."""
+
+    def __init__(self, fine, frows, coarse, crows, device):
+        f, c = _lattice_rows(fine, frows), _lattice_rows(coarse, crows)
+        if f is None or c is None or not np.array_equal(f[0], 2 * c[0] - 1) or (c[0] < 2).any():
+            raise ValueError("not a 2:1 box pair with node-wise Dirichlet rows")
+        self.fd, self.cd = [int(v) for v in f[0]], [int(v) for v in c[0]]
+        self.frow, self.fzero = (torch.from_numpy(a).to(device) for a in f[1:])
+        self.crow, self.czero = (torch.from_numpy(a).to(device) for a in c[1:])
+        self.device = device.index or 0
+
+    def _run(self, mode, zero, x, y, accumulate):
+        rc = fcg.lib().fcg_box_transfer(self.device, mode, *self.fd, *self.cd, _ptr(self.frow),
+                                        _ptr(self.crow), _ptr(zero), _ptr(x), _ptr(y),
+                                        1 if accumulate else 0,
+                                        ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream))
+        if rc != 0:
+            raise fcg.FcgError(rc, "fcg_box_transfer failed")
+
+    def prolong(self, xc, xf):
+        self._run(0, self.fzero, xc, xf, True)
+
+    def restrict(self, rf, bc):
+        self._run(1, self.czero, rf, bc, False)
+
+
 class _LevelOps:
     """What the Chebyshev smoother and the Lanczos estimate need of a level: n, dev, mask, the
     work vectors r and z, spmv(x, y) and apply_dinv(r, z, scale, accumulate)."""
@@ -600,7 +649,7 @@ class Multigrid(CycleFCG):
             zc = torch.zeros(fine_mesh.n_cols, dtype=torch.float64, device=dev)
             fine_ev.tangent_apply(zc, zc, torch.empty(fine_mesh.n_rows, dtype=torch.float64, device=dev))
             del zc
-        self.P, self.R = [], []
+        self.P, self.R, self.BT = [], [], []
         prev = fine_mesh
         for ivc in meshes:
             m = fcg.BoxMesh(fcg.HEX8, ivc, lower=lower, upper=upper, rotation=rot,
@@ -622,6 +671,15 @@ class Multigrid(CycleFCG):
             P, R = transfer_tables(prev, m)
             self.P.append(_Transfer(P, dev))
             self.R.append(_Transfer(R, dev))
+            # a 2:1 pair (hex27 -> hex8 on the same elements, hex8 n -> n/2): weights implicit
+            # (FCG_MG_BOXT=0: the tables)
+            bt = None
+            if os.environ.get("FCG_MG_BOXT", "1") != "0":
+                try:
+                    bt = _BoxTransfer(prev, self.levels[-1].rows, m, rows, dev)
+                except ValueError:
+                    bt = None
+            self.BT.append(bt)
             self.levels.append(lvl)
             prev = m
         for lvl in self.levels[1:-1]:
@@ -682,10 +740,16 @@ class Multigrid(CycleFCG):
                       file=sys.stderr, flush=True)
 
     def _restrict(self, l, r, cb):
+        if self.BT[l] is not None:
+            self.BT[l].restrict(r, cb)
+            return
         self.R[l](r, cb, accumulate=False)
         cb.mul_(self.levels[l + 1].mask)
 
     def _prolong(self, l, cx, x):
+        if self.BT[l] is not None:
+            self.BT[l].prolong(cx, x)
+            return
         self.P[l](cx, x, accumulate=True)
         x.mul_(self.levels[l].mask)
 

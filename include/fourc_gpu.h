@@ -260,6 +260,14 @@ int fcg_node_transfer(int device, int64_t n_out, const int64_t* d_ptr, const int
  * K to rounding, without reading K.  Asynchronous on `stream`. */
 int fcg_box_stencil_apply(int device, int nx, int ny, int nz, const int32_t* d_row_of,
     const uint8_t* d_clamped, const double* d_S, const double* d_x, double* d_y, void* stream);
+/* The multigrid's transfer between a box lattice and its 2:1 coarsening (fine = 2 coarse - 1
+ * points per axis: hex27 -> hex8 on the same elements, hex8 n -> n / 2) with the trilinear weights
+ * implicit: mode 0 prolongation y_fine (+)= P x_coarse, mode 1 restriction y_coarse = P^T x_fine;
+ * rows of nodes flagged in d_zero_out (the output level's lattice) are set to 0.  Row tables as
+ * fcg_box_stencil_apply's.  The same operator as fcg_node_transfer on multigrid.transfer_tables. */
+int fcg_box_transfer(int device, int mode, int fnx, int fny, int fnz, int cnx, int cny, int cnz,
+    const int32_t* d_fine_row_of, const int32_t* d_coarse_row_of, const uint8_t* d_zero_out,
+    const double* d_x, double* d_y, int accumulate, void* stream);
 
 /* Smoothed-aggregation AMG for meshes without a box hierarchy (replaces the MueLu preconditioner
  * 4C builds in 4C_linear_solver_preconditioner_muelu.cpp; algorithm in fcg_amg_setup.cpp).

@@ -106,6 +106,44 @@ def test_node_transfer_device(k):
         assert np.abs(y.cpu().numpy() - ref).max() <= 1e-13 * max(1.0, np.abs(ref).max())
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [0, 1])
+def test_box_transfer_matches_tables(k):
+    """fcg_box_transfer (implicit 2:1 weights, the level masks in the kernel) = fcg_node_transfer on
+    the tables followed by the mask, both directions, with clamped nodes on both levels."""
+    torch, dev = _dev()
+    fine, coarse = _pairs()[k]
+    P, R = mgm.transfer_tables(fine, coarse)
+
+    def dbc(m):
+        nodes = np.nonzero(mgm.node_lattice(m)[:, 0] == 0)[0]
+        return np.sort((m.node_dof_row[nodes][:, None] + np.arange(3)).ravel()).astype(np.int32)
+
+    fr, cr = dbc(fine), dbc(coarse)
+    bt = mgm._BoxTransfer(fine, fr, coarse, cr, dev)
+    rng = np.random.default_rng(11)
+    xc = torch.from_numpy(rng.standard_normal(coarse.n_rows)).to(dev)
+    xf = torch.from_numpy(rng.standard_normal(fine.n_rows)).to(dev)
+    mf = torch.ones(fine.n_rows, dtype=torch.float64, device=dev)
+    mf[torch.as_tensor(fr.astype(np.int64), device=dev)] = 0.0
+    mc = torch.ones(coarse.n_rows, dtype=torch.float64, device=dev)
+    mc[torch.as_tensor(cr.astype(np.int64), device=dev)] = 0.0
+    y0 = torch.full((fine.n_rows,), 3.0, dtype=torch.float64, device=dev)
+    y1 = y0.clone()
+    mgm._Transfer(P, dev)(xc, y0, accumulate=True)
+    y0.mul_(mf)
+    bt.prolong(xc, y1)
+    b0 = torch.empty(coarse.n_rows, dtype=torch.float64, device=dev)
+    b1 = torch.empty_like(b0)
+    mgm._Transfer(R, dev)(xf, b0, accumulate=False)
+    b0.mul_(mc)
+    bt.restrict(xf, b1)
+    torch.cuda.synchronize()
+    for a, b in ((y0, y1), (b0, b1)):
+        a, b = a.cpu().numpy(), b.cpu().numpy()
+        assert np.abs(a - b).max() <= 1e-14 * max(1.0, np.abs(a).max())
+
+
 def _cantilever(ct, n, kin, load, length=2.0, jitter=0.0):
     mesh = fcg.BoxMesh(ct, (n, n, n), upper=(length, 1.0, 1.0), jitter=jitter)
     X = mesh.node_x
