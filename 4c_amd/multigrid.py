@@ -405,7 +405,14 @@ class CycleFCG:
     retry_lmax = True
 
     # -- smoother ---------------------------------------------------------------------------
-    def _cheb(self, lvl, b, x, x_zero):
+    # Chebyshev degree on the coarse levels (None: nu) and the cycle below the fine level
+    # ("W": two coarse corrections per visit of a coarse level, which the cheap stencil levels
+    # afford); the fine level is visited once per application either way
+    coarse_nu = None
+    cycle = "V"
+
+    def _cheb(self, lvl, b, x, x_zero, nu=None):
+        nu = self.nu if nu is None else nu
         lmax = self.boost * lvl.lmax
         lmin = lmax / self.ratio
         theta, delta = 0.5 * (lmax + lmin), 0.5 * (lmax - lmin)
@@ -420,7 +427,7 @@ class CycleFCG:
             torch.sub(b, r, out=r)
             lvl.apply_dinv(r, d, 1.0 / theta)
             x.add_(d)
-        for _ in range(self.nu - 1):
+        for _ in range(nu - 1):
             lvl.spmv(x, r)
             torch.sub(b, r, out=r)
             rho_n = 1.0 / (2.0 * sigma - rho)
@@ -434,15 +441,17 @@ class CycleFCG:
         if l == len(self.levels) - 1:
             self._coarse_solve(lvl, b, x)
             return
-        self._cheb(lvl, b, x, x_zero=True)
-        lvl.spmv_cycle(x, lvl.r)  # the restricted residual stays FP64 (mixed: smoother only)
-        torch.sub(b, lvl.r, out=lvl.r)
+        nu = None if l == 0 or self.coarse_nu is None else self.coarse_nu
+        self._cheb(lvl, b, x, x_zero=True, nu=nu)
         c = self.levels[l + 1]
-        self._restrict(l, lvl.r, c.b)
-        self._vcycle(l + 1, c.b, c.x)
-        self._prolong(l, c.x, x)
+        for _ in range(2 if l > 0 and self.cycle == "W" else 1):
+            lvl.spmv_cycle(x, lvl.r)  # the restricted residual stays FP64 (mixed: smoother only)
+            torch.sub(b, lvl.r, out=lvl.r)
+            self._restrict(l, lvl.r, c.b)
+            self._vcycle(l + 1, c.b, c.x)
+            self._prolong(l, c.x, x)
         if l > 0 or self.fine_post:
-            self._cheb(lvl, b, x, x_zero=False)
+            self._cheb(lvl, b, x, x_zero=False, nu=nu)
 
     # -- outer solve ------------------------------------------------------------------------
     def solve(self, K, b, x, rtol, max_iter=1000):
@@ -607,6 +616,10 @@ class Multigrid(CycleFCG):
                  max_levels=8, ratio=10.0, boost=1.1, coarse_rtol=1e-2, coarse_max_iter=2000,
                  mixed=False, coarse_solver="auto", fine_post=True, matrix_free=False):
         self.fine_post = bool(fine_post)
+        if os.environ.get("FCG_MG_COARSE_NU"):
+            self.coarse_nu = int(os.environ["FCG_MG_COARSE_NU"])
+        if os.environ.get("FCG_MG_CYCLE"):
+            self.cycle = os.environ["FCG_MG_CYCLE"]
         if matrix_free and (mixed or fine_mesh.celltype != fcg.HEX27):
             raise ValueError("matrix_free: hex27 fine levels in FP64 only (mixed=False)")
         if coarse_solver not in ("auto", "dense", "pcg", "amg"):
