@@ -630,6 +630,15 @@ __global__ __launch_bounds__(256, KIN ? 1 : FCG_SWEEP_WGS) void sweep_h8_kernel(
 #pragma unroll
     for (int j = 0; j < NLD; ++j)
     {
+#ifdef FCG_PROBE_TH_NOPREFETCH
+      if (TH)
+      {
+        // timing probe only (wrong results): the thermal pass without its plane prefetch
+        node_nxt[j] = 0.0;
+        dof_nn[j] = -1;
+        continue;
+      }
+#endif
       node_nxt[j] = n_lane[j] ? load_val(j, L + 2, dof_nxt[j]) : 0.0;
       dof_nn[j] = n_lane[j] ? load_dof(j, L + 3) : -1;
     }
@@ -936,7 +945,11 @@ __global__ __launch_bounds__(256, KIN ? 1 : FCG_SWEEP_WGS) void sweep_h8_kernel(
 #pragma unroll
           for (int d = 0; d < 3; ++d)
           {
+#ifdef FCG_PROBE_TH_NORMW
+            if (OVERWRITE)  // timing probe only (wrong f_S): no read-modify-write in the thermal pass
+#else
             if (OVERWRITE && !TH)  // the thermal pass adds k_ST (T - T_0) to the structural f_S
+#endif
               A.fint[row0 + d] = fp[d] + f[d];
             else
               A.fint[row0 + d] += fp[d] + f[d];
