@@ -48,7 +48,7 @@ def _apply(ev, u, x, torch, dev):
 
 
 @pytest.mark.parametrize("kin,amp", [(fcg.LINEAR, 0.0), (fcg.TOTLAG, 2e-2)])
-@pytest.mark.parametrize("shape,jitter", [((3, 2, 2), 0.1), ((2, 3, 1), 0.0)])
+@pytest.mark.parametrize("shape,jitter", [((3, 2, 2), 0.1), ((2, 3, 1), 0.0), ((3, 3, 1), 0.05), ((5, 5, 5), 0.05)])
 def test_tangent_apply_box_matches_oracle(kin, amp, shape, jitter):
     torch, dev = _dev()
     mesh = fcg.BoxMesh(fcg.HEX27, shape, jitter=jitter, seed=11)
