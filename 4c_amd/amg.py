@@ -446,6 +446,12 @@ class NativeAMG:
             out.append({"level": l, "dofs": d.value, "blocks": b.value, "lmax": lm.value})
         return out
 
+    def stats(self):
+        """fcg_amg_stats: whether the coarsest level is a dense inverse, graph-replayed iterations."""
+        dense, launches = ctypes.c_int(0), ctypes.c_int(0)
+        fcg.lib().fcg_amg_stats(self._h, ctypes.byref(dense), ctypes.byref(launches))
+        return {"coarse_dense": bool(dense.value), "graph_launches": launches.value}
+
     def setup(self, K):
         """Numeric setup for the tangent K (fcg_amg_setup)."""
         L = fcg.lib()

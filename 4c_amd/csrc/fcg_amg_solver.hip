@@ -5,10 +5,11 @@
 // hierarchy and cycle are those of 4c_amd/amg.py (which stays the Python-side mirror and test
 // reference): graph setup on the host once (fcg_amg_setup.cpp), numeric setup per tangent and the
 // flexible-CG / V-cycle / Chebyshev iteration on the device (fcg_amg.hip kernels, the context's
-// fcg_spmv / block-Jacobi on level 0).  Differences from amg.py: the coarsest level is solved by
-// block-Jacobi CG to a loose tolerance on the device (no dense factor: no solver library is linked)
-// and the scalars of every iteration stay on the device except one read per FCG iteration (and one
-// per 8 coarse CG iterations).
+// fcg_spmv / block-Jacobi on level 0).  Differences from amg.py: the coarsest level is inverted
+// densely on the device per tangent (Gauss-Jordan, up to kDenseMax DOFs; above that, or when a
+// pivot fails, block-Jacobi CG to a loose tolerance), the scalars of every iteration stay on the
+// device except one read per FCG iteration, and with the dense coarsest level one FCG iteration can
+// be replayed as a captured HIP graph (FCG_AMG_GRAPH=1).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -25,6 +26,7 @@ namespace fcg_amgs {
 
 constexpr int kBlock = 256;
 constexpr int kMaxPartials = 1024;
+constexpr int64_t kDenseMax = 4096;  // largest coarsest level inverted densely (2 x 134 MB)
 inline unsigned blocks_for(int64_t n) { return unsigned((n + kBlock - 1) / kBlock); }
 inline unsigned capped(int64_t n) { return unsigned(std::max<int64_t>(1, std::min<int64_t>(kMaxPartials, (n + kBlock - 1) / kBlock))); }
 
@@ -80,17 +82,159 @@ __global__ __launch_bounds__(kBlock) void axpby_kernel(double a, const double* _
   if (i < n) y[i] = a * x[i] + b * y[i];
 }
 
-// FCG step: alpha = rz / (p.q); x += alpha p; r_old = r; r -= alpha q
-__global__ __launch_bounds__(kBlock) void fcg_step_kernel(double rz, const double* __restrict__ pq,
+// FCG step, scalars on the device (sc[0] = r.z, sc[1] = p.q): alpha = r.z / p.q; x += alpha p;
+// r_old = r; r -= alpha q
+__global__ __launch_bounds__(kBlock) void fcg_step_kernel(const double* __restrict__ sc,
     const double* __restrict__ p, const double* __restrict__ q, double* x, double* r, double* r_old,
     int64_t n)
 {
   const int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x;
   if (i >= n) return;
-  const double alpha = rz / *pq;
+  const double alpha = sc[0] / sc[1];
   x[i] += alpha * p[i];
   r_old[i] = r[i];
   r[i] -= alpha * q[i];
+}
+// FCG direction (Polak-Ribiere): p = z + beta p, beta = (r.z new - z.r_old) / r.z (sc[2], sc[5], sc[0])
+__global__ __launch_bounds__(kBlock) void fcg_dir_kernel(const double* __restrict__ sc,
+    const double* __restrict__ z, double* p, int64_t n)
+{
+  const int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const double beta = (sc[2] - sc[5]) / sc[0];
+  p[i] = z[i] + beta * p[i];
+}
+
+// ---- the coarsest level as a dense inverse ------------------------------------------------------
+// (4C's MueLu coarsest level is a direct solve, Amesos/KLU: 4C_linear_solver_preconditioner_muelu.cpp
+// via the xml's "coarse: type"; here the coarsest level has at most coarse_max DOFs, so its inverse
+// is formed densely once per tangent and applied as one matrix-vector product per V-cycle)
+
+// D = the 6 x 6 BSR matrix as dense row-major n x n (n = 6 nb; D zeroed before): one thread per
+// (block row, block entry)
+__global__ __launch_bounds__(kBlock) void bsr6_dense_kernel(int64_t nb, const int64_t* __restrict__ ptr,
+    const int32_t* __restrict__ col, const double* __restrict__ vals, double* D)
+{
+  const int64_t t = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (t >= nb * 36) return;
+  const int64_t i = t / 36;
+  const int e = int(t - 36 * i), a = e / 6, b = e % 6;
+  const int64_t n = 6 * nb;
+  for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k)
+    D[(6 * i + a) * n + 6 * int64_t(col[k]) + b] = vals[36 * k + e];
+}
+
+// Block Gauss-Jordan inversion (no pivoting: the coarsest Galerkin operator is symmetric positive
+// definite), kGJ pivots per step, A -> B out of place.  With the pivot block P = A[K, K], its row
+// panel R = A[K, :] and column panel C = A[:, K]:
+//   B[K, K] = P^-1,  B[K, j] = P^-1 R_j,  B[i, K] = -C_i P^-1,  B[i, j] = A_ij - C_i P^-1 R_j;
+// after ceil(n / kGJ) steps the buffer holds A^-1.  Step part 1 (gj_panel_kernel): every
+// workgroup inverts P in LDS (scalar Gauss-Jordan; a pivot that is not positive sets *bad), then
+// W = P^-1 R for its 256 columns and the copy C of the column panel for its 256 rows (both zero
+// beyond the last pivot of a short final block); workgroup 0 stores P^-1.  Part 2 (gj_update_kernel)
+// forms B.
+constexpr int kGJ = 32;
+
+__global__ __launch_bounds__(kBlock) void gj_panel_kernel(const double* __restrict__ A, int64_t n, int64_t k0,
+    double* __restrict__ Pinv, double* __restrict__ W, double* __restrict__ C, int32_t* bad)
+{
+  __shared__ double P[kGJ][kGJ + 1];
+  const int t = threadIdx.x;
+  const int b = int(min<int64_t>(kGJ, n - k0));
+  for (int e = t; e < kGJ * kGJ; e += kBlock)
+  {
+    const int r = e / kGJ, c = e % kGJ;
+    P[r][c] = (r < b && c < b) ? A[(k0 + r) * n + k0 + c] : (r == c ? 1.0 : 0.0);
+  }
+  __syncthreads();
+  for (int m = 0; m < kGJ; ++m)
+  {
+    const double piv = P[m][m];
+    double v[kGJ * kGJ / kBlock];
+    const double inv = 1.0 / piv;
+#pragma unroll
+    for (int u = 0; u < kGJ * kGJ / kBlock; ++u)
+    {
+      const int e = t + kBlock * u, r = e / kGJ, c = e % kGJ;
+      if (r == m) v[u] = c == m ? inv : P[m][c] * inv;
+      else if (c == m) v[u] = -P[r][m] * inv;
+      else v[u] = P[r][c] - P[r][m] * (P[m][c] * inv);
+    }
+    if (blockIdx.x == 0 && t == 0 && !(piv > 0.0)) *bad = 1;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kGJ * kGJ / kBlock; ++u)
+    {
+      const int e = t + kBlock * u;
+      P[e / kGJ][e % kGJ] = v[u];
+    }
+    __syncthreads();
+  }
+  if (blockIdx.x == 0)
+    for (int e = t; e < kGJ * kGJ; e += kBlock) Pinv[e] = P[e / kGJ][e % kGJ];
+  const int64_t j = int64_t(blockIdx.x) * kBlock + t;
+  if (j >= n) return;
+  double w[kGJ];
+#pragma unroll
+  for (int m = 0; m < kGJ; ++m) w[m] = 0.0;
+  for (int q = 0; q < b; ++q)
+  {
+    const double r = A[(k0 + q) * n + j];
+#pragma unroll
+    for (int m = 0; m < kGJ; ++m) w[m] += P[m][q] * r;
+  }
+#pragma unroll
+  for (int m = 0; m < kGJ; ++m) W[int64_t(m) * n + j] = w[m];
+#pragma unroll
+  for (int m = 0; m < kGJ; ++m) C[j * kGJ + m] = m < b ? A[j * n + k0 + m] : 0.0;
+}
+
+// grid (ceil(n / kBlock), n): blockIdx.y = row i (its C_i is uniform over the workgroup)
+__global__ __launch_bounds__(kBlock) void gj_update_kernel(const double* __restrict__ A, double* __restrict__ B,
+    int64_t n, int64_t k0, const double* __restrict__ Pinv, const double* __restrict__ W,
+    const double* __restrict__ C)
+{
+  const int64_t i = blockIdx.y;
+  const int64_t j = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= n) return;
+  const int64_t ik = i - k0, jk = j - k0;
+  const bool i_in = ik >= 0 && ik < kGJ && i < n, j_in = jk >= 0 && jk < kGJ;
+  double v;
+  if (i_in)
+    v = j_in ? Pinv[ik * kGJ + jk] : W[ik * n + j];
+  else
+  {
+    const double* c = C + i * kGJ;
+    double s = 0.0;
+    if (j_in)
+    {
+#pragma unroll
+      for (int m = 0; m < kGJ; ++m) s += c[m] * Pinv[m * kGJ + jk];
+      v = -s;
+    }
+    else
+    {
+#pragma unroll
+      for (int m = 0; m < kGJ; ++m) s += c[m] * W[int64_t(m) * n + j];
+      v = A[i * n + j] - s;
+    }
+  }
+  B[i * n + j] = v;
+}
+
+// y = D x, D dense row-major n x n: one wavefront per row (fixed-order reduction)
+__global__ __launch_bounds__(kBlock) void dense_mv_kernel(const double* __restrict__ D,
+    const double* __restrict__ x, double* y, int64_t n)
+{
+  const int64_t row = int64_t(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= n) return;
+  const double* d = D + row * n;
+  double t = 0.0;
+  for (int64_t j = lane; j < n; j += 64) t += d[j] * x[j];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o);
+  if (lane == 0) y[row] = t;
 }
 
 // coarse CG, scalars on the device: sc[0] = r.z, sc[1] = p.q, sc[2] = r.z new, sc[3] = r.r
@@ -191,6 +335,24 @@ struct fcg_amg {
   // the coarse levels coupled across ranks (fcg_dfcg_solve with a local handle): built on the
   // first solve through its transport, see fcg_amgs::Coupled
   fcg_amgs::Coupled* cpl = nullptr;
+  // the coarsest level's dense inverse (coarse_solve applies it when set; else block-Jacobi CG):
+  // formed per tangent by block Gauss-Jordan between the two buffers when the level has at most
+  // kDenseMax DOFs (FCG_AMG_DENSE=0: never)
+  double* cbuf[2] = {nullptr, nullptr};
+  double* cwork = nullptr;  // the block elimination's pivot inverse and panels
+  double* cinv = nullptr;
+  int64_t cn = 0;
+  // one FCG iteration of fcg_amg_iterate captured as a HIP graph on a private stream (re-captured
+  // after every numeric setup and when K or x move), opt-in with FCG_AMG_GRAPH=1: at the 1M-element
+  // scale the kernels leave no launch gaps to remove and the replay measured 1-2 % slower.  Only
+  // with the dense coarsest inverse: the CG coarse solve reads its residual on the host.
+  hipStream_t gs = nullptr;
+  hipEvent_t gev[2] = {nullptr, nullptr};
+  hipGraphExec_t gexec = nullptr;
+  const double* g_K = nullptr;
+  double* g_x = nullptr;
+  bool graph_off = false;
+  int graph_launches = 0;
 };
 
 namespace fcg_amgs {
@@ -521,6 +683,13 @@ void cheb(const fcg_amg* hc, const Ops& o, const double* b, double* x, bool x_ze
 void coarse_solve(fcg_amg* h, const Ops& o, const double* b, double* x)
 {
   const int64_t n = o.n();
+  if (h->cinv && h->cn == n)
+  {
+    hipLaunchKernelGGL(dense_mv_kernel, dim3(unsigned((n + kBlock / 64 - 1) / (kBlock / 64))), dim3(kBlock), 0,
+        o.s, h->cinv, b, x, n);
+    ck(hipGetLastError(), "dense_mv_kernel");
+    return;
+  }
   double *r = o.r(), *z = o.z(), *p = o.p(), *q = o.q();
   // its own scalars (the outer FCG keeps r.r in sc[3] across the V-cycle): 0 r.z, 1 p.q,
   // 2 r.z new, 3 r.r, 4 b.b
@@ -578,6 +747,7 @@ void vcycle(fcg_amg* h, int l, const double* K, const double* b, double* x, hipS
 }
 
 void galerkin_from(fcg_amg* h, size_t l0, const double* K, hipStream_t s);
+void coarse_factor(fcg_amg* h, hipStream_t s);
 
 // numeric setup for the tangent K (level-0 values in the context's CSR order)
 void setup(fcg_amg* h, const double* K, hipStream_t s)
@@ -623,6 +793,50 @@ void galerkin_from(fcg_amg* h, size_t l0, const double* K, hipStream_t s)
     A = &c.A;
     dinv = c.dinv;
   }
+  coarse_factor(h, s);
+}
+
+bool env_off(const char* name)
+{
+  const char* v = std::getenv(name);
+  return v && std::strcmp(v, "0") == 0;
+}
+
+// the coarsest level's dense inverse (h->cinv), or none (the CG coarse solve) when the level is
+// larger than kDenseMax DOFs, FCG_AMG_DENSE=0 or a pivot is not positive
+void coarse_factor(fcg_amg* h, hipStream_t s)
+{
+  h->cinv = nullptr;
+  if (h->levels.empty() || env_off("FCG_AMG_DENSE")) return;
+  const Bsr& A = h->levels.back().A;
+  const int64_t n = 6 * A.n;
+  if (n == 0 || n > kDenseMax) return;
+  if (h->cn != n)
+  {
+    h->cbuf[0] = dalloc<double>(h, n * n);
+    h->cbuf[1] = dalloc<double>(h, n * n);
+    h->cwork = dalloc<double>(h, 2 * kGJ * n + kGJ * kGJ);
+    h->cn = n;
+  }
+  double *Pinv = h->cwork, *W = Pinv + kGJ * kGJ, *C = W + kGJ * n;
+  ck(hipMemsetAsync(h->cbuf[0], 0, sizeof(double) * size_t(n * n), s), "memset");
+  ck(hipMemsetAsync(h->flag, 0, sizeof(int32_t), s), "memset");
+  hipLaunchKernelGGL(bsr6_dense_kernel, dim3(blocks_for(A.n * 36)), dim3(kBlock), 0, s, A.n, A.ptr, A.col,
+      A.vals, h->cbuf[0]);
+  const int64_t steps = (n + kGJ - 1) / kGJ;
+  for (int64_t t = 0; t < steps; ++t)
+  {
+    const double* src = h->cbuf[t & 1];
+    hipLaunchKernelGGL(gj_panel_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, s, src, n, t * kGJ, Pinv, W, C,
+        h->flag);
+    hipLaunchKernelGGL(gj_update_kernel, dim3(blocks_for(n), unsigned(n)), dim3(kBlock), 0, s, src,
+        h->cbuf[(t + 1) & 1], n, t * kGJ, Pinv, W, C);
+  }
+  ck(hipGetLastError(), "gj_update_kernel");
+  int32_t bad = 0;
+  ck(hipMemcpyAsync(&bad, h->flag, sizeof(bad), hipMemcpyDeviceToHost, s), "hipMemcpyAsync");
+  ck(hipStreamSynchronize(s), "hipStreamSynchronize");
+  if (!bad) h->cinv = h->cbuf[steps & 1];
 }
 
 // flexible CG (Polak-Ribiere) preconditioned by one V-cycle; one host read per iteration
@@ -633,39 +847,110 @@ void run_fcg(fcg_amg* h, const double* K, const double* b, double* x, double rto
   const dim3 g(blocks_for(n)), bl(kBlock);
   // FCG vectors (the V-cycle's level-0 work vectors r0 / d0 are separate)
   double *r = h->fr, *z = h->fz, *pp = h->fx, *q = h->q0, *ro = h->ro0;
-  ck(hipMemsetAsync(x, 0, sizeof(double) * size_t(n), s), "memset");
-  const double bn = std::sqrt(dot_host(h, b, b, n, s));
+  double* sc = h->sc;
+  // device scalars: 0 r.z, 1 p.q, 2 r.z new, 3 r.r, 5 z.r_old
+  auto body = [&](hipStream_t q_s) {
+    apply_A0(h, K, pp, q, q_s);
+    dot_dev(h, pp, q, n, sc + 1, q_s);
+    hipLaunchKernelGGL(fcg_step_kernel, g, bl, 0, q_s, sc, pp, q, x, r, ro, n);
+    dot_dev(h, r, r, n, sc + 3, q_s);
+    vcycle(h, 0, K, r, z, q_s);
+    dot_dev(h, r, z, n, sc + 2, q_s);
+    dot_dev(h, z, ro, n, sc + 5, q_s);
+  };
+  // the graph (the iteration body has no host synchronisation once the coarsest solve is dense):
+  // its kernel arguments bake in K, x and the setup's lambda_max values
+  const char* ge = std::getenv("FCG_AMG_GRAPH");
+  const bool use_graph = !h->graph_off && h->cinv && ge && std::strcmp(ge, "1") == 0;
+  hipStream_t w = s;
+  if (use_graph)
+  {
+    if (!h->gs)
+    {
+      ck(hipStreamCreateWithFlags(&h->gs, hipStreamNonBlocking), "hipStreamCreateWithFlags");
+      ck(hipEventCreateWithFlags(&h->gev[0], hipEventDisableTiming), "hipEventCreate");
+      ck(hipEventCreateWithFlags(&h->gev[1], hipEventDisableTiming), "hipEventCreate");
+    }
+    ck(hipEventRecord(h->gev[0], s), "hipEventRecord");
+    ck(hipStreamWaitEvent(h->gs, h->gev[0], 0), "hipStreamWaitEvent");
+    w = h->gs;
+    if (h->gexec && (h->g_K != K || h->g_x != x))
+    {
+      (void)hipGraphExecDestroy(h->gexec);
+      h->gexec = nullptr;
+    }
+  }
+  // the caller's stream waits for the private one on every exit
+  struct Join {
+    fcg_amg* h;
+    hipStream_t s, w;
+    ~Join()
+    {
+      if (w != s && hipEventRecord(h->gev[1], w) == hipSuccess) (void)hipStreamWaitEvent(s, h->gev[1], 0);
+    }
+  } join{h, s, w};
+  ck(hipMemsetAsync(x, 0, sizeof(double) * size_t(n), w), "memset");
+  const double bn = std::sqrt(dot_host(h, b, b, n, w));
   *iterations = 0;
   *rel = 0.0;
   if (bn == 0.0) return;
-  ck(hipMemcpyAsync(r, b, sizeof(double) * size_t(n), hipMemcpyDeviceToDevice, s), "copy");
-  vcycle(h, 0, K, r, z, s);
-  ck(hipMemcpyAsync(pp, z, sizeof(double) * size_t(n), hipMemcpyDeviceToDevice, s), "copy");
-  double rz = dot_host(h, r, z, n, s);
+  ck(hipMemcpyAsync(r, b, sizeof(double) * size_t(n), hipMemcpyDeviceToDevice, w), "copy");
+  vcycle(h, 0, K, r, z, w);
+  ck(hipMemcpyAsync(pp, z, sizeof(double) * size_t(n), hipMemcpyDeviceToDevice, w), "copy");
+  dot_dev(h, r, z, n, sc + 0, w);
+  double rz = 0.0;
+  ck(hipMemcpyAsync(&rz, sc, sizeof(double), hipMemcpyDeviceToHost, w), "hipMemcpyAsync");
+  ck(hipStreamSynchronize(w), "hipStreamSynchronize");
   if (!(rz > 0.0)) throw Fail{FCG_ERR_SINGULAR, "AMG: indefinite V-cycle (r.z <= 0)"};
   double rn = bn;
   int it = 0;
-  double* sc = h->sc;
   while (it < max_iter)
   {
     ++it;
-    apply_A0(h, K, pp, q, s);
-    dot_dev(h, pp, q, n, sc + 1, s);
-    hipLaunchKernelGGL(fcg_step_kernel, g, bl, 0, s, rz, sc + 1, pp, q, x, r, ro, n);
-    dot_dev(h, r, r, n, sc + 3, s);
-    vcycle(h, 0, K, r, z, s);
-    dot_dev(h, r, z, n, sc + 2, s);
-    dot_dev(h, z, ro, n, sc + 5, s);
+    if (use_graph && !h->gexec && !h->graph_off)
+    {
+      hipGraph_t graph = nullptr;
+      bool ok = hipStreamBeginCapture(w, hipStreamCaptureModeRelaxed) == hipSuccess;
+      if (ok)
+      {
+        try
+        {
+          body(w);
+        }
+        catch (const Fail&)
+        {
+          ok = false;
+        }
+        ok = hipStreamEndCapture(w, &graph) == hipSuccess && ok && graph;
+        ok = ok && hipGraphInstantiate(&h->gexec, graph, nullptr, nullptr, 0) == hipSuccess;
+        if (graph) (void)hipGraphDestroy(graph);
+      }
+      if (!ok)
+      {
+        (void)hipGetLastError();
+        if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
+        h->gexec = nullptr;
+        h->graph_off = true;  // eager from here on
+      }
+      h->g_K = K;
+      h->g_x = x;
+    }
+    if (h->gexec)
+    {
+      ck(hipGraphLaunch(h->gexec, w), "hipGraphLaunch");
+      ++h->graph_launches;
+    }
+    else
+      body(w);
     double hs[6];
-    ck(hipMemcpyAsync(hs, sc, sizeof(hs), hipMemcpyDeviceToHost, s), "hipMemcpyAsync");
-    ck(hipStreamSynchronize(s), "hipStreamSynchronize");
+    ck(hipMemcpyAsync(hs, sc, sizeof(hs), hipMemcpyDeviceToHost, w), "hipMemcpyAsync");
+    ck(hipStreamSynchronize(w), "hipStreamSynchronize");
     rn = std::sqrt(hs[3]);
     if (!std::isfinite(rn)) throw Fail{FCG_ERR_SINGULAR, "AMG FCG: non-finite residual"};
     if (rn <= rtol * bn) break;
     if (!(hs[2] > 0.0)) throw Fail{FCG_ERR_SINGULAR, "AMG: indefinite V-cycle (r.z <= 0)"};
-    const double beta = (hs[2] - hs[5]) / rz;
-    hipLaunchKernelGGL(axpby_kernel, g, bl, 0, s, 1.0, z, beta, pp, n);
-    rz = hs[2];
+    hipLaunchKernelGGL(fcg_dir_kernel, g, bl, 0, w, sc, z, pp, n);
+    hipLaunchKernelGGL(shift_kernel, dim3(1), dim3(1), 0, w, sc);
   }
   *iterations = it;
   *rel = rn / bn;
@@ -1198,6 +1483,11 @@ int fcg_amg_setup(fcg_amg* h, const double* d_K_vals, void* stream)
     ck(hipEventCreate(&e0), "hipEventCreate");
     ck(hipEventCreate(&e1), "hipEventCreate");
     ck(hipEventRecord(e0, s), "hipEventRecord");
+    if (h->gexec)  // its kernel arguments hold the previous setup's lambda_max values
+    {
+      (void)hipGraphExecDestroy(h->gexec);
+      h->gexec = nullptr;
+    }
     setup(h, d_K_vals, s);
     ck(hipEventRecord(e1, s), "hipEventRecord");
     ck(hipEventSynchronize(e1), "hipEventSynchronize");
@@ -1295,6 +1585,14 @@ int fcg_amg_level_info(const fcg_amg* h, int level, int64_t* dofs, int64_t* bloc
 int fcg_amg_levels(const fcg_amg* h) { return h ? int(h->levels.size()) + 1 : 0; }
 
 double fcg_amg_setup_ms(const fcg_amg* h) { return h ? h->setup_ms : -1.0; }
+
+int fcg_amg_stats(const fcg_amg* h, int* coarse_dense, int* graph_launches)
+{
+  if (!h) return FCG_ERR_ARG;
+  if (coarse_dense) *coarse_dense = h->cinv ? 1 : 0;
+  if (graph_launches) *graph_launches = h->graph_launches;
+  return FCG_OK;
+}
 
 const char* fcg_amg_last_error(const fcg_amg* h) { return h ? h->last_error.c_str() : ""; }
 
@@ -1402,6 +1700,14 @@ int fcg_amg_destroy(fcg_amg* h)
     h->cpl = nullptr;
   }
   (void)hipSetDevice(h->device);
+  if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
+  if (h->gs)
+  {
+    (void)hipStreamSynchronize(h->gs);
+    (void)hipStreamDestroy(h->gs);
+  }
+  for (hipEvent_t e : h->gev)
+    if (e) (void)hipEventDestroy(e);
   for (void* p : h->allocs) (void)hipFree(p);
   delete h;
   return FCG_OK;

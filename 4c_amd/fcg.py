@@ -146,7 +146,7 @@ EXPORTS = ["fcg_create", "fcg_destroy", "fcg_last_error", "fcg_evaluate", "fcg_e
            "fcg_bsr_spmv", "fcg_bsr_spgemm", "fcg_bsr_transpose_values", "fcg_bsr_from_node_csr",
            "fcg_bsr_block_jacobi_setup", "fcg_bsr_block_jacobi_apply", "fcg_amg_smooth_prolongator",
            "fcg_bsr_to_dense", "fcg_amg_default_options", "fcg_amg_create", "fcg_amg_solve",
-           "fcg_amg_levels", "fcg_amg_level_info", "fcg_amg_setup_ms", "fcg_amg_last_error",
+           "fcg_amg_levels", "fcg_amg_level_info", "fcg_amg_setup_ms", "fcg_amg_stats", "fcg_amg_last_error",
            "fcg_amg_destroy", "fcg_amg_setup", "fcg_amg_iterate", "fcg_amg_apply",
            "fcg_amg_coupled_levels", "fcg_transport_rccl", "fcg_dfcg_solve"]
 
@@ -289,6 +289,7 @@ def lib():
     L.fcg_amg_level_info.argtypes = [vp, c_int, _i64p, _i64p, _dp]
     L.fcg_amg_setup_ms.argtypes = [vp]
     L.fcg_amg_setup_ms.restype = c_dbl
+    L.fcg_amg_stats.argtypes = [vp, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]
     L.fcg_amg_last_error.argtypes = [vp]
     L.fcg_amg_last_error.restype = ctypes.c_char_p
     L.fcg_amg_destroy.argtypes = [vp]

@@ -351,6 +351,12 @@ int fcg_amg_iterate(fcg_amg* amg, const double* d_K_vals, const double* d_b_row,
 int fcg_amg_levels(const fcg_amg* amg);
 int fcg_amg_level_info(const fcg_amg* amg, int level, int64_t* dofs, int64_t* blocks, double* lmax);
 double fcg_amg_setup_ms(const fcg_amg* amg);
+/* How the last numeric setup / iterations ran: *coarse_dense = 1 when the coarsest level is
+ * applied as its dense inverse (formed per tangent, at most 4096 DOFs; 0: block-Jacobi CG),
+ * *graph_launches = FCG iterations replayed from the captured HIP graph since creation (opt-in:
+ * FCG_AMG_GRAPH=1 in the environment; FCG_AMG_DENSE=0 keeps the CG coarse solve).  (Either
+ * pointer may be NULL.) */
+int fcg_amg_stats(const fcg_amg* amg, int* coarse_dense, int* graph_launches);
 const char* fcg_amg_last_error(const fcg_amg* amg);
 int fcg_amg_destroy(fcg_amg* amg);
 

@@ -334,6 +334,46 @@ def test_amg_reported_residual_is_the_true_one(cls):
 
 
 @pytest.mark.gpu
+def test_native_amg_dense_coarse_and_graph(monkeypatch):
+    """The coarsest level as its dense inverse (Gauss-Jordan per tangent) and the FCG iteration
+    replayed from a captured HIP graph: the graph gives bit-identical iterates to eager launches,
+    the exact coarse solve needs no more iterations than the block-Jacobi CG one, and all three
+    reach the same solution."""
+    torch, dev = _dev()
+    dis, kin, load = _case("renumbered-totlag")
+    dbc, fext = _loads(dis, load)
+    ev = fcg.Evaluator(dis, kinematics=fcg.LINEAR, youngs=E, poisson=NU)
+    f64 = dict(dtype=torch.float64, device=dev)
+    K = torch.zeros(dis.nnz, **f64)
+    ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, torch.zeros(dis.n_cols, **f64),
+                       torch.zeros(dis.n_rows, **f64), K)
+    b = torch.from_numpy(fext).to(dev)
+    ev.dirichlet_apply(torch.from_numpy(dbc).to(dev), K, b)
+    solver = amg.NativeAMG(dis, ev, dbc)
+    runs = {}
+    for name, env in (("graph", {"FCG_AMG_GRAPH": "1"}), ("eager", {}), ("cg", {"FCG_AMG_DENSE": "0"})):
+        for k in ("FCG_AMG_GRAPH", "FCG_AMG_DENSE"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        before = solver.stats()["graph_launches"]
+        x = torch.empty_like(b)
+        it, rel = solver.solve(K, b, x, 1e-9, 500)
+        st = solver.stats()
+        runs[name] = (it, rel, x.cpu().numpy(), st["coarse_dense"], st["graph_launches"] - before)
+    it_g, rel_g, x_g, dense_g, launches_g = runs["graph"]
+    it_e, rel_e, x_e, dense_e, launches_e = runs["eager"]
+    it_c, rel_c, x_c, dense_c, launches_c = runs["cg"]
+    assert dense_g and dense_e and not dense_c
+    assert launches_g >= it_g - 1 > 0 and launches_e == 0 and launches_c == 0
+    assert it_g == it_e and rel_g == rel_e and np.array_equal(x_g, x_e)
+    assert it_g <= it_c, (it_g, it_c)
+    assert np.linalg.norm(x_g - x_c) <= 1e-7 * np.linalg.norm(x_c)
+    solver.close()
+    ev.close()
+
+
+@pytest.mark.gpu
 def test_native_amg_rejects_bad_input():
     torch, dev = _dev()
     dis, kin, load = _case("renumbered-totlag")

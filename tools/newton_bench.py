@@ -187,5 +187,6 @@ out = {"config": f"{a.celltype}-{a.kinem}-{a.n}^3-cantilever", "forcing": a.forc
        "tip_uz": float(u[mesh.node_dof_row[np.argmax(mesh.node_x.sum(axis=1))] + 2]),
        "amg_graph_setup_s": t_amg_setup if (a.amg or a.amg_native) else None,
        "amg_numeric_setup_ms": mg.setup_ms if (a.amg or a.amg_native) else None,
+       "amg_stats": mg.stats() if a.amg_native else None,
        "history": h}
 print(json.dumps(out))
