@@ -316,12 +316,15 @@ def cpu_topology():
 def newton_secondary(n, timeout_s=900):
     """BASELINE config 3: StVK TotLag on the 1M-hex27 cube (x- clamped, traction -1 in z on x+),
     full static Newton on this GPU (fcg_evaluate_device + Dirichlet + multigrid-preconditioned
-    flexible CG, 4c_amd/newton.py + multigrid.py; the fine level's smoother applies K(u) element
-    by element, fcg_tangent_apply, the outer FCG the assembled K), run by tools/newton_bench.py in
+    flexible CG, 4c_amd/newton.py + multigrid.py; the fine level's smoother and the outer FCG apply
+    the Dirichlet-modified tangent K(u) element by element, fcg_tangent_apply -- the assembled K,
+    formed every Newton step, sets the block-Jacobi smoother and equals that action at 1e-13 --
+    same FCG iterations and tip displacement as with the assembled outer operator, profiles/r04/
+    r04_config3_newton_outer_*.json), run by tools/newton_bench.py in
     a child process so that its ~60 GB of device buffers are released when it ends."""
     cmd = [sys.executable, os.path.join(ROOT, "tools", "newton_bench.py"), "--celltype", "hex27",
            "--kinem", "totlag", "--n", str(n), "--length", "1", "--load", "-1", "--mg",
-           "--mg-matrix-free"]
+           "--mg-matrix-free", "--mg-outer-matrix-free"]
     t = time.perf_counter()
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s)
     wall = time.perf_counter() - t

@@ -80,6 +80,8 @@ def test_matrix_free_fine_level_needs_hex27_fp64():
     with pytest.raises(ValueError):
         mgm.Multigrid(m27, None, lambda mm: np.zeros(mm.n_node, bool), E, NU, matrix_free=True,
                       mixed=True)
+    with pytest.raises(ValueError):  # the outer operator matrix-free needs the fine level's action
+        mgm.Multigrid(m27, None, lambda mm: np.zeros(mm.n_node, bool), E, NU, outer_matrix_free=True)
 
 
 def _dev():

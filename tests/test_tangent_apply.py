@@ -116,17 +116,21 @@ def test_newton_multigrid_matrix_free_fine_smoother():
     fcg.neumann_surface(fcg.HEX27, faces, mesh.node_x, mesh.node_dof_row, [1, 1, 1],
                         [0.0, 0.0, -2.0], fext)
     res = {}
-    for mf in (False, True):
+    # (fine smoother matrix-free, outer FCG operator matrix-free)
+    for mf, outer in ((False, False), (True, False), (True, True)):
         ev = fcg.Evaluator(mesh, kinematics=fcg.TOTLAG, youngs=E, poisson=NU)
-        mg = mgm.Multigrid(mesh, ev, clamp, E, NU, min_intervals=2, matrix_free=mf)
+        mg = mgm.Multigrid(mesh, ev, clamp, E, NU, min_intervals=2, matrix_free=mf,
+                           outer_matrix_free=outer)
         nt = newton.StaticNewton(ev, fext, dbc, tol_res=1e-10 * np.linalg.norm(fext), tol_inc=1e-9,
                                  lin_rtol=1e-10, linear_solver=mg)
-        res[mf] = (nt.solve().cpu().numpy(), [h.get("lin_iter") for h in nt.history])
+        res[mf, outer] = (nt.solve().cpu().numpy(), [h.get("lin_iter") for h in nt.history])
         ev.close()
-    (u0, it0), (u1, it1) = res[False], res[True]
-    assert np.linalg.norm(u1 - u0) <= 1e-9 * np.linalg.norm(u0)
-    # the same operator to rounding: the iteration path differs only through those last bits,
-    # amplified by the loose coarsest solve (1e-2)
-    assert len(it0) == len(it1)
-    n0, n1 = sum(i for i in it0 if i), sum(i for i in it1 if i)
-    assert abs(n1 - n0) <= 0.1 * n0, (it0, it1)
+    u0, it0 = res[False, False]
+    for key in ((True, False), (True, True)):
+        u1, it1 = res[key]
+        assert np.linalg.norm(u1 - u0) <= 1e-9 * np.linalg.norm(u0), key
+        # the same operator to rounding: the iteration path differs only through those last bits,
+        # amplified by the loose coarsest solve (1e-2)
+        assert len(it0) == len(it1), key
+        n0, n1 = sum(i for i in it0 if i), sum(i for i in it1 if i)
+        assert abs(n1 - n0) <= 0.1 * n0, (key, it0, it1)

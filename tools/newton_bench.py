@@ -42,6 +42,9 @@ ap.add_argument("--mg-no-fine-post", action="store_true",
 ap.add_argument("--mg-matrix-free", action="store_true",
                 help="hex27: the fine level's smoother and V-cycle residual apply K(u) element by "
                      "element (fcg_tangent_apply) instead of reading the assembled K")
+ap.add_argument("--mg-outer-matrix-free", action="store_true",
+                help="with --mg-matrix-free: the outer flexible CG applies the same tangent "
+                     "element by element too (the assembled K still sets the smoother's blocks)")
 ap.add_argument("--mg-coarse", default="auto", choices=["auto", "dense", "pcg", "amg"],
                 help="coarsest-level solver of the geometric multigrid")
 ap.add_argument("--amg", action="store_true",
@@ -133,6 +136,7 @@ if a.mg:
         mesh, ev, lambda m: np.isclose(m.node_x[:, 0], 0.0), 210.0, 0.3, nu=a.mg_nu,
         coarse_rtol=a.mg_coarse_rtol, mixed=a.mg_mixed, coarse_solver=a.mg_coarse,
         fine_post=not a.mg_no_fine_post, matrix_free=a.mg_matrix_free,
+        outer_matrix_free=a.mg_outer_matrix_free,
         **({"ratio": a.mg_ratio} if a.mg_ratio else {}))
     print(f"multigrid setup {time.perf_counter() - t_mg:.1f} s: {json.dumps(mg.describe())}",
           file=sys.stderr, flush=True)
@@ -172,7 +176,8 @@ out = {"config": f"{a.celltype}-{a.kinem}-{a.n}^3-cantilever", "forcing": a.forc
        "converged": True, "tangent_symmetry_rel": sym,
        "residual_rel_incl_dbc_rows": r_final,
        "linear_solver": (f"multigrid-FCG (Chebyshev {a.mg_nu}"
-                         + (", matrix-free fine smoother)" if a.mg_matrix_free else ")") if a.mg else
+                         + (", matrix-free fine smoother and outer operator)" if a.mg_outer_matrix_free else
+                            ", matrix-free fine smoother)" if a.mg_matrix_free else ")") if a.mg else
                          f"SA-AMG-FCG (Chebyshev {a.mg_nu})" if a.amg else
                          f"SA-AMG-FCG native C ABI (Chebyshev {a.mg_nu})" if a.amg_native else
                          "block-Jacobi PCG"),
