@@ -325,7 +325,30 @@ __global__ __launch_bounds__(kBlock) void bj_apply_kernel(const int32_t* __restr
   for (int d = 0; d < 3; ++d) ri[d] = r[i + d];
   bj_apply(dinv + 9 * k, ri, zi);
 #pragma unroll
-  for (int d = 0; d < 3; ++d) z[i + d] = (accumulate ? z[i + d] : 0.0) + scale * zi[d];
+  for (int d = 0; d < 3; ++d) z[i + d] = __fma_rn(scale, zi[d], accumulate ? z[i + d] : 0.0);
+}
+
+// fcg_chebyshev_step: the smoother update per node (fourc_gpu.h); d = c_d d first, then the
+// block-Jacobi term added as in bj_apply_kernel, so the result equals the separate passes
+__global__ __launch_bounds__(kBlock) void cheb_step_kernel(const int32_t* __restrict__ row0_of,
+    const double* __restrict__ dinv, const double* __restrict__ b, const double* __restrict__ y, double* dv,
+    double* x, int64_t n_nodes, double c_d, double c_r, int mode)
+{
+  const int64_t k = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (k >= n_nodes) return;
+  const int32_t i = row0_of[k];
+  double ri[3], zi[3];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) ri[d] = mode == 2 ? b[i + d] : b[i + d] - y[i + d];
+  bj_apply(dinv + 9 * k, ri, zi);
+#pragma unroll
+  for (int d = 0; d < 3; ++d)
+  {
+    // the rounded c_d d, then one fused multiply-add (as the accumulating bj_apply_kernel)
+    const double dn = __fma_rn(c_r, zi[d], mode == 1 ? __dmul_rn(c_d, dv[i + d]) : 0.0);
+    dv[i + d] = dn;
+    x[i + d] = mode == 2 ? dn : x[i + d] + dn;
+  }
 }
 
 // Node-block transfer between two discretizations of one box (multigrid prolongation and its
@@ -824,6 +847,27 @@ int fcg_block_jacobi_apply(fcg_ctx* ctx, const double* d_dinv, const double* d_r
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   hipLaunchKernelGGL(fcg::bj_apply_kernel, dim3(fcg::blocks_for(nn, fcg::kBlock)), dim3(fcg::kBlock), 0, s,
       m.rownode_row0, d_dinv, d_r_row, d_z_row, nn, scale, accumulate);
+  const hipError_t he = hipGetLastError();
+  if (he != hipSuccess)
+  {
+    ctx->last_error = std::string("HIP: ") + hipGetErrorString(he);
+    return fcg_device_error();
+  }
+  return FCG_OK;
+}
+
+int fcg_chebyshev_step(fcg_ctx* ctx, const double* d_dinv, const double* d_b_row, const double* d_y_row,
+    double* d_d_row, double* d_x_row, double c_d, double c_r, int mode, void* stream)
+{
+  if (!ctx || !d_dinv || !d_b_row || (!d_y_row && mode != 2) || !d_d_row || !d_x_row || mode < 0 || mode > 2)
+    return FCG_ERR_ARG;
+  fcg::DeviceMesh& m = ctx->mesh;
+  const int64_t nn = m.n_rownodes;
+  if (nn == 0) return FCG_OK;
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  hipLaunchKernelGGL(fcg::cheb_step_kernel, dim3(fcg::blocks_for(nn, fcg::kBlock)), dim3(fcg::kBlock), 0, s,
+      m.rownode_row0, d_dinv, d_b_row, mode == 2 ? d_b_row : d_y_row, d_d_row, d_x_row, nn, c_d, c_r, mode);
   const hipError_t he = hipGetLastError();
   if (he != hipSuccess)
   {

@@ -129,7 +129,7 @@ EXPORTS = ["fcg_create", "fcg_destroy", "fcg_last_error", "fcg_evaluate", "fcg_e
            "fcg_device_alloc", "fcg_device_free", "fcg_memcpy_h2d", "fcg_memcpy_d2h",
            "fcg_memset_device", "fcg_set_timing", "fcg_get_timing", "fcg_get_info",
            "fcg_get_diagnostics", "fcg_measure_peaks", "fcg_measure_hbm", "fcg_spmv", "fcg_dirichlet_apply",
-           "fcg_pcg_solve", "fcg_spmv_f32", "fcg_tangent_apply", "fcg_box_stencil_apply", "fcg_box_transfer", "fcg_block_jacobi_setup", "fcg_block_jacobi_apply", "fcg_node_transfer",
+           "fcg_pcg_solve", "fcg_spmv_f32", "fcg_tangent_apply", "fcg_box_stencil_apply", "fcg_box_transfer", "fcg_block_jacobi_setup", "fcg_block_jacobi_apply", "fcg_chebyshev_step", "fcg_node_transfer",
            "fcg_neumann_surface", "fcg_neumann_volume",
            "fcg_graph_build_device", "fcg_get_graph",
            "fcg_tsi_create", "fcg_tsi_destroy", "fcg_tsi_last_error", "fcg_tsi_evaluate_device",
@@ -203,6 +203,7 @@ def lib():
     L.fcg_box_transfer.argtypes = [ctypes.c_int] * 8 + [vp, vp, vp, vp, vp, ctypes.c_int, vp]
     L.fcg_block_jacobi_setup.argtypes = [vp, vp, vp, vp]
     L.fcg_block_jacobi_apply.argtypes = [vp, vp, vp, vp, ctypes.c_double, ctypes.c_int, vp]
+    L.fcg_chebyshev_step.argtypes = [vp, vp, vp, vp, vp, vp, ctypes.c_double, ctypes.c_double, ctypes.c_int, vp]
     L.fcg_node_transfer.argtypes = [ctypes.c_int, ctypes.c_int64, vp, vp, vp, vp, vp, vp,
                                     ctypes.c_int, vp]
     neu = [ctypes.c_int, ctypes.c_int64, _i32p, _dp, _i32p, _i32p, _dp, _i32p, FUNCT_FN,

@@ -336,6 +336,15 @@ class _Level(_LevelOps):
         if rc != 0:
             self.ev._raise(rc, -1)
 
+    def cheb_step(self, b, y, d, x, c_d, c_r, mode):
+        """One Chebyshev update of d and x from r = b - y (fcg_chebyshev_step; mode 2: from x = 0)."""
+        rc = fcg.lib().fcg_chebyshev_step(self.ev._h, _ptr(self.dinv), _ptr(b),
+                                          None if y is None else _ptr(y), _ptr(d), _ptr(x),
+                                          ctypes.c_double(c_d), ctypes.c_double(c_r), int(mode),
+                                          ctypes.c_void_p(self.stream().cuda_stream))
+        if rc != 0:
+            self.ev._raise(rc, -1)
+
     def spmv(self, x, y):
         """The V-cycle's operator: K, its FP32 copy when the level has one, (matrix_free) the
         element-by-element tangent action, or (stencil) the box's 27-point stencil."""
@@ -419,6 +428,19 @@ class CycleFCG:
         sigma = theta / delta
         rho = 1.0 / sigma
         r, d = lvl.r, lvl.d
+        if getattr(lvl, "cheb_step", None) is not None and os.environ.get("FCG_MG_FUSED", "1") != "0":
+            # the same steps, each update one fused pass (fcg_chebyshev_step), bit-identical
+            if x_zero:
+                lvl.cheb_step(b, None, d, x, 0.0, 1.0 / theta, 2)
+            else:
+                lvl.spmv(x, r)
+                lvl.cheb_step(b, r, d, x, 0.0, 1.0 / theta, 0)
+            for _ in range(nu - 1):
+                lvl.spmv(x, r)
+                rho_n = 1.0 / (2.0 * sigma - rho)
+                lvl.cheb_step(b, r, d, x, rho_n * rho, 2.0 * rho_n / delta, 1)
+                rho = rho_n
+            return
         if x_zero:
             lvl.apply_dinv(b, d, 1.0 / theta)
             x.copy_(d)

@@ -248,6 +248,16 @@ int fcg_pcg_solve(fcg_ctx* ctx, const double* d_K_vals, const double* d_b_row, d
 int fcg_block_jacobi_setup(fcg_ctx* ctx, const double* d_K_vals, double* d_dinv, void* stream);
 int fcg_block_jacobi_apply(fcg_ctx* ctx, const double* d_dinv, const double* d_r_row, double* d_z_row,
     double scale, int accumulate, void* stream);
+/* One Chebyshev smoothing step with the block-Jacobi preconditioner, fused per node (the update of
+ * the multigrid smoother, 4c_amd/multigrid.py CycleFCG._cheb): with r = b - y (y = A x, computed
+ * by the caller) and z = D^-1 r,
+ *   mode 0: d = c_r z,           x += d
+ *   mode 1: d = c_d d + c_r z,   x += d
+ *   mode 2: d = c_r D^-1 b,      x  = d   (first step from x = 0; y is not read)
+ * -- the arithmetic of the separate r = b - y, d *= c_d, d += c_r D^-1 r, x += d passes in one
+ * read of b, y, d, x and the nodal inverses. */
+int fcg_chebyshev_step(fcg_ctx* ctx, const double* d_dinv, const double* d_b_row, const double* d_y_row,
+    double* d_d_row, double* d_x_row, double c_d, double c_r, int mode, void* stream);
 int fcg_node_transfer(int device, int64_t n_out, const int64_t* d_ptr, const int32_t* d_src_row0,
     const double* d_w, const int32_t* d_dst_row0, const double* d_x, double* d_y, int accumulate,
     void* stream);

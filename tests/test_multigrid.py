@@ -267,6 +267,26 @@ def test_multigrid_pre_smoothing_only_on_the_finest_level():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("ct", [fcg.HEX8, fcg.HEX27])
+def test_fused_chebyshev_step_is_bit_identical(monkeypatch, ct):
+    """fcg_chebyshev_step (r = b - y, d = c_d d + c_r D^-1 r, x += d in one pass) against the
+    separate torch / block-Jacobi passes: the same Newton iterates bit for bit."""
+    torch, dev = _dev()
+    mesh, clamp, dbc, fext = _cantilever(ct, 6, fcg.TOTLAG, -2.0)
+    res = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("FCG_MG_FUSED", fused)
+        ev = fcg.Evaluator(mesh, kinematics=fcg.TOTLAG, youngs=E, poisson=NU)
+        mg = mgm.Multigrid(mesh, ev, clamp, E, NU, min_intervals=2)
+        nt = newton.StaticNewton(ev, fext, dbc, tol_res=1e-10 * np.linalg.norm(fext), tol_inc=1e-9,
+                                 lin_rtol=1e-10, linear_solver=mg)
+        res[fused] = (nt.solve().cpu().numpy(), [h.get("lin_iter") for h in nt.history])
+        ev.close()
+    assert res["1"][1] == res["0"][1]
+    assert np.array_equal(res["1"][0], res["0"][0])
+
+
+@pytest.mark.gpu
 def test_multigrid_with_native_amg_coarsest_level():
     """coarse_solver="amg": the coarsest hex8 level solved by the native AMG set up once."""
     torch, dev = _dev()
