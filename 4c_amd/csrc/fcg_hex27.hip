@@ -1520,7 +1520,32 @@ __global__ __launch_bounds__(256) void h27_inc_sum_kernel(int64_t n_rownodes,
   const int64_t r = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (r >= n_rownodes) return;
   double y0 = 0.0, y1 = 0.0, y2 = 0.0;
-  for (int64_t k = inc_ptr[r]; k < inc_ptr[r + 1]; ++k)
+  const int64_t p0 = inc_ptr[r], p1 = inc_ptr[r + 1];
+  const int64_t cnt = p1 - p0;
+#ifndef FCG_PROBE_INCSUM_LOOP
+  // the first 8 incidences (a lattice node's most) loaded unconditionally -- addresses clamped to
+  // the node's last one, all 24 loads in flight at once -- and summed in order by selects
+  // (bit-identical to the loop); a node with more incidences continues in the loop
+  double v[8][3];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+  {
+    const int64_t k = p0 + (j < cnt ? j : (cnt > 0 ? cnt - 1 : 0));  // ye has a spare last triple
+    v[j][0] = ye[3 * k];
+    v[j][1] = ye[3 * k + 1];
+    v[j][2] = ye[3 * k + 2];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+  {
+    y0 = j < cnt ? y0 + v[j][0] : y0;
+    y1 = j < cnt ? y1 + v[j][1] : y1;
+    y2 = j < cnt ? y2 + v[j][2] : y2;
+  }
+  for (int64_t k = p0 + 8; k < p1; ++k)
+#else
+  for (int64_t k = p0; k < p1; ++k)
+#endif
   {
     y0 += ye[3 * k];
     y1 += ye[3 * k + 1];
