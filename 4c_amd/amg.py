@@ -96,6 +96,25 @@ def symbolic(a_ptr, a_col, b_ptr, b_col, n_cols):
     return c_ptr, c_col[:nnz]
 
 
+def product_plan(a_ptr, a_col, b_ptr, b_col, c_ptr, c_col, n_cols):
+    """fcg_bsr_product_plan: per block of C = A B on C's pattern its (A block, B block) pairs in
+    A's row order -> (pair_ptr, pair_a, pair_b)."""
+    L = fcg.lib()
+    a_ptr, b_ptr, c_ptr = (np.ascontiguousarray(p, dtype=np.int64) for p in (a_ptr, b_ptr, c_ptr))
+    a_col, b_col, c_col = (np.ascontiguousarray(c, dtype=np.int32) for c in (a_col, b_col, c_col))
+    n = len(a_ptr) - 1
+    pp = np.empty(int(c_ptr[-1]) + 1, dtype=np.int64)
+    npairs = L.fcg_bsr_product_plan(n, _vp(a_ptr), _vp(a_col), _vp(b_ptr), _vp(b_col), _vp(c_ptr),
+                                    _vp(c_col), n_cols, _vp(pp), None, None)
+    if npairs < 0:
+        raise ValueError("fcg_bsr_product_plan: bad pattern")
+    pa, pb = np.empty(max(npairs, 1), dtype=np.int32), np.empty(max(npairs, 1), dtype=np.int32)
+    if L.fcg_bsr_product_plan(n, _vp(a_ptr), _vp(a_col), _vp(b_ptr), _vp(b_col), _vp(c_ptr),
+                              _vp(c_col), n_cols, _vp(pp), _vp(pa), _vp(pb)) != npairs:
+        raise ValueError("fcg_bsr_product_plan: fill pass disagrees with the count pass")
+    return pp, pa[:npairs], pb[:npairs]
+
+
 def transpose_pattern(ptr, col, n_cols):
     """Pattern of A^T and perm (transposed block -> A's block index)."""
     ptr = np.ascontiguousarray(ptr, dtype=np.int64)

@@ -116,6 +116,39 @@ __global__ __launch_bounds__(kBlock) void bsr_spgemm_kernel(int64_t n,
   }
 }
 
+// C = A B from a product plan (fcg_bsr_spgemm_planned): the (A block, B block) pairs of every C
+// block, listed once on the host in A's row order -- the pairs bsr_spgemm_kernel finds by its
+// searches, so the same products in the same order (bitwise equal).  One thread per C block.
+template <int BR, int BK, int BC>
+__global__ __launch_bounds__(kBlock) void bsr_spgemm_plan_kernel(int64_t n_out,
+    const int64_t* __restrict__ pptr, const int32_t* __restrict__ pa, const int32_t* __restrict__ pb,
+    const double* __restrict__ a_vals, const double* __restrict__ b_vals, double* c_vals)
+{
+  const int64_t ci = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (ci >= n_out) return;
+  double acc[BR * BC];
+#pragma unroll
+  for (int q = 0; q < BR * BC; ++q) acc[q] = 0.0;
+  const int64_t t1 = pptr[ci + 1];
+  for (int64_t t = pptr[ci]; t < t1; ++t)
+  {
+    const double* A = a_vals + int64_t(pa[t]) * (BR * BK);
+    const double* B = b_vals + int64_t(pb[t]) * (BK * BC);
+#pragma unroll
+    for (int r = 0; r < BR; ++r)
+#pragma unroll
+      for (int q = 0; q < BK; ++q)
+      {
+        const double av = A[r * BK + q];
+#pragma unroll
+        for (int c = 0; c < BC; ++c) acc[r * BC + c] += av * B[q * BC + c];
+      }
+  }
+  double* out = c_vals + ci * (BR * BC);
+#pragma unroll
+  for (int q = 0; q < BR * BC; ++q) out[q] = acc[q];
+}
+
 // t_vals[t] = vals[perm[t]]^T (BR x BC -> BC x BR)
 template <int BR, int BC>
 __global__ __launch_bounds__(kBlock) void bsr_transpose_kernel(int64_t nnzb,
@@ -348,6 +381,29 @@ int fcg_bsr_spgemm(int device, int br, int bk, int bc, int64_t n_brows, const in
   else if (br == 3 && bk == 3 && bc == 3) FCG_SPGEMM(3, 3, 3);
   else return FCG_ERR_ARG;
 #undef FCG_SPGEMM
+  return status(hipGetLastError());
+}
+
+int fcg_bsr_spgemm_planned(int device, int br, int bk, int bc, int64_t nnzb_c, const int64_t* d_pair_ptr,
+    const int32_t* d_pair_a, const int32_t* d_pair_b, const double* d_a_vals, const double* d_b_vals,
+    double* d_c_vals, void* stream)
+{
+  using namespace fcg_bsrk;
+  if (nnzb_c < 0 || (nnzb_c > 0 && (!d_pair_ptr || !d_pair_a || !d_pair_b || !d_a_vals || !d_b_vals || !d_c_vals)))
+    return FCG_ERR_ARG;
+  if (nnzb_c == 0) return FCG_OK;
+  if (!fcg_use_device(device)) return fcg_device_error();
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const dim3 g(blocks_for(nnzb_c, kBlock)), b(kBlock);
+#define FCG_SPGEMM_P(R, K, C)                                                                      \
+  hipLaunchKernelGGL((bsr_spgemm_plan_kernel<R, K, C>), g, b, 0, s, nnzb_c, d_pair_ptr, d_pair_a,  \
+      d_pair_b, d_a_vals, d_b_vals, d_c_vals)
+  if (br == 3 && bk == 3 && bc == 6) FCG_SPGEMM_P(3, 3, 6);
+  else if (br == 6 && bk == 3 && bc == 6) FCG_SPGEMM_P(6, 3, 6);
+  else if (br == 6 && bk == 6 && bc == 6) FCG_SPGEMM_P(6, 6, 6);
+  else if (br == 3 && bk == 3 && bc == 3) FCG_SPGEMM_P(3, 3, 3);
+  else return FCG_ERR_ARG;
+#undef FCG_SPGEMM_P
   return status(hipGetLastError());
 }
 

@@ -21,6 +21,7 @@
 //    sorted ascending -- the device product binary-searches them) and of P^T.
 // The numeric half (products, smoothing, block inverses, the cycle's operators) is fcg_amg.hip.
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -219,6 +220,57 @@ int64_t fcg_bsr_symbolic(int64_t n_rows, const int64_t* a_ptr, const int32_t* a_
     std::copy(row.begin(), row.end(), c_col + c_ptr[i]);
   }
   return c_ptr[n_rows];
+}
+
+// Product plan of C = A B on C's pattern: for every block of C, the pairs (A block, B block) whose
+// product lands there, in A's row order -- what the searching SpGEMM kernel finds per call, listed
+// once.  Count pass (pair_a = NULL): pair_ptr[0..nnzb_c]; fill pass: pair_a / pair_b.  Returns the
+// pair count, -1 on bad input (block indices past int32).
+int64_t fcg_bsr_product_plan(int64_t n_rows, const int64_t* a_ptr, const int32_t* a_col,
+    const int64_t* b_ptr, const int32_t* b_col, const int64_t* c_ptr, const int32_t* c_col,
+    int64_t n_cols, int64_t* pair_ptr, int32_t* pair_a, int32_t* pair_b)
+{
+  if (n_rows < 0 || n_cols < 0 || !pair_ptr || (n_rows > 0 && (!a_ptr || !a_col || !b_ptr || !b_col || !c_ptr)))
+    return -1;
+  if ((pair_a == nullptr) != (pair_b == nullptr)) return -1;
+  const int64_t nnzb_c = n_rows ? c_ptr[n_rows] : 0;
+  if ((n_rows && a_ptr[n_rows] > INT32_MAX) || nnzb_c < 0) return -1;
+  const bool fill = pair_a != nullptr;
+  std::vector<int64_t> pos(size_t(n_cols), -1);  // C's block index of column c in the current row
+  std::vector<int64_t> cur;
+  if (fill) cur.assign(pair_ptr, pair_ptr + nnzb_c);
+  else std::fill(pair_ptr, pair_ptr + nnzb_c + 1, int64_t(0));
+  for (int64_t i = 0; i < n_rows; ++i)
+  {
+    for (int64_t ci = c_ptr[i]; ci < c_ptr[i + 1]; ++ci)
+    {
+      if (c_col[ci] < 0 || c_col[ci] >= n_cols) return -1;
+      pos[size_t(c_col[ci])] = ci;
+    }
+    for (int64_t ak = a_ptr[i]; ak < a_ptr[i + 1]; ++ak)
+    {
+      const int32_t k = a_col[ak];
+      for (int64_t bk = b_ptr[k]; bk < b_ptr[k + 1]; ++bk)
+      {
+        const int32_t c = b_col[bk];
+        if (c < 0 || c >= n_cols || bk > INT32_MAX) return -1;
+        const int64_t ci = pos[size_t(c)];
+        if (ci < 0) continue;  // a product outside C's pattern is not formed (as the search kernel)
+        if (fill)
+        {
+          const int64_t t = cur[size_t(ci)]++;
+          pair_a[t] = int32_t(ak);
+          pair_b[t] = int32_t(bk);
+        }
+        else
+          ++pair_ptr[ci + 1];
+      }
+    }
+    for (int64_t ci = c_ptr[i]; ci < c_ptr[i + 1]; ++ci) pos[size_t(c_col[ci])] = -1;
+  }
+  if (!fill)
+    for (int64_t ci = 0; ci < nnzb_c; ++ci) pair_ptr[ci + 1] += pair_ptr[ci];
+  return pair_ptr[nnzb_c];
 }
 
 // Pattern of A^T (n_cols block rows): t_col ascending per row, perm[t] = A's block index.

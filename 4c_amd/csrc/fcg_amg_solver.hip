@@ -283,10 +283,17 @@ struct Bsr {
   double* vals = nullptr;
 };
 
+// product plan of one Galerkin SpGEMM (fcg_bsr_product_plan): per C block its (A, B) block pairs
+struct Plan {
+  int64_t* ptr = nullptr;
+  int32_t *a = nullptr, *b = nullptr;
+};
+
 struct Step {  // level l -> l + 1
   int bs = 3;
   int64_t n_agg = 0;
   Bsr T, P, AT, AP, Pt;
+  Plan pAT, pAP, pC;  // A T, A P, P^T (A P); empty: the searching kernel (FCG_AMG_PLAN=0)
   int32_t* agg = nullptr;
   double* tent = nullptr;   // [n][bs][6], every row's T_i
   int64_t* perm = nullptr;  // P^T block -> P block
@@ -432,6 +439,27 @@ std::vector<int64_t> diag_index(const Bsr& A)
   return d;
 }
 
+bool env_off(const char* name);
+
+// the pairs of C = X Y on C's pattern, listed on the host and uploaded (the numeric SpGEMM per
+// tangent then streams them instead of searching Y's rows for every C block)
+Plan make_plan(fcg_amg* h, const Bsr& X, const Bsr& Y, const Bsr& C)
+{
+  Plan pl;
+  std::vector<int64_t> ptr(size_t(C.nnzb) + 1, 0);
+  const int64_t np = fcg_bsr_product_plan(X.n, X.ptr_h.data(), X.col_h.data(), Y.ptr_h.data(),
+      Y.col_h.data(), C.ptr_h.data(), C.col_h.data(), C.n_cols, ptr.data(), nullptr, nullptr);
+  if (np < 0) throw Fail{FCG_ERR_ARG, "AMG: product plan (count)"};
+  std::vector<int32_t> a(size_t(std::max<int64_t>(np, 1))), b(size_t(std::max<int64_t>(np, 1)));
+  if (fcg_bsr_product_plan(X.n, X.ptr_h.data(), X.col_h.data(), Y.ptr_h.data(), Y.col_h.data(),
+          C.ptr_h.data(), C.col_h.data(), C.n_cols, ptr.data(), a.data(), b.data()) != np)
+    throw Fail{FCG_ERR_ARG, "AMG: product plan (fill)"};
+  pl.ptr = upload(h, ptr);
+  pl.a = upload(h, a);
+  pl.b = upload(h, b);
+  return pl;
+}
+
 // aggregation hierarchy below A_start (block size bs, near-null space ns [n][bs][6]; skip: level-0
 // nodes left out of the aggregation, NULL on a coarse start): appends steps and coarse levels until
 // a level has at most coarse_max DOFs (and always one step from an empty hierarchy)
@@ -484,9 +512,16 @@ void coarsen(fcg_amg* h, const Bsr* A_start, int bs, std::vector<double> ns, con
     make_bsr(h, st.Pt, tp, tc, 6, bs, A->n);
     st.perm = upload(h, perm);
     symbolic(st.Pt, app, apc, n_agg, cp, cc);
+    const bool plans = !env_off("FCG_AMG_PLAN");
+    if (plans)  // (before the level list grows: A may point into it)
+    {
+      st.pAT = make_plan(h, *A, st.T, st.AT);
+      st.pAP = make_plan(h, *A, st.P, st.AP);
+    }
     h->levels.emplace_back();
     Level& c = h->levels.back();
     make_bsr(h, c.A, cp, cc, 6, 6, n_agg);
+    if (plans) st.pC = make_plan(h, st.Pt, st.AP, c.A);
     c.diag = upload(h, diag_index(c.A));
     c.dinv = dalloc<double>(h, 36 * n_agg);
     for (double** v : {&c.x, &c.b, &c.r, &c.d, &c.z, &c.p, &c.q}) *v = dalloc<double>(h, 6 * n_agg);
@@ -773,20 +808,25 @@ void galerkin_from(fcg_amg* h, size_t l0, const double* K, hipStream_t s)
   {
     Step& st = h->steps[l];
     const double lm = l == 0 ? h->lmax0 : h->levels[l - 1].lmax;
-    auto product = [&](Bsr& C, const Bsr& X, const Bsr& Y) {
-      ck(fcg_bsr_spgemm(h->device, X.br, X.bc, Y.bc, X.n, X.ptr, X.col, X.vals, Y.ptr, Y.col, Y.vals,
-             C.ptr, C.col, C.vals, s),
-          "fcg_bsr_spgemm");
+    auto product = [&](Bsr& C, const Bsr& X, const Bsr& Y, const Plan& pl) {
+      if (pl.ptr)
+        ck(fcg_bsr_spgemm_planned(h->device, X.br, X.bc, Y.bc, C.nnzb, pl.ptr, pl.a, pl.b, X.vals,
+               Y.vals, C.vals, s),
+            "fcg_bsr_spgemm_planned");
+      else
+        ck(fcg_bsr_spgemm(h->device, X.br, X.bc, Y.bc, X.n, X.ptr, X.col, X.vals, Y.ptr, Y.col, Y.vals,
+               C.ptr, C.col, C.vals, s),
+            "fcg_bsr_spgemm");
     };
-    product(st.AT, *A, st.T);
+    product(st.AT, *A, st.T, st.pAT);
     ck(fcg_amg_smooth_prolongator(h->device, st.bs, A->n, st.P.ptr, st.P.col, st.agg, st.tent, dinv,
            st.AT.vals, h->opt.omega / lm, st.P.vals, s),
         "fcg_amg_smooth_prolongator");
-    product(st.AP, *A, st.P);
+    product(st.AP, *A, st.P, st.pAP);
     ck(fcg_bsr_transpose_values(h->device, st.bs, 6, st.P.nnzb, st.perm, st.P.vals, st.Pt.vals, s),
         "fcg_bsr_transpose_values");
     Level& c = h->levels[l];
-    product(c.A, st.Pt, st.AP);
+    product(c.A, st.Pt, st.AP, st.pC);
     ck(fcg_bsr_block_jacobi_setup(h->device, 6, c.A.n, c.A.ptr, c.diag, c.A.vals, c.dinv, h->flag, s),
         "AMG coarse level: singular diagonal block");
     if (l + 1 < h->steps.size()) estimate_lmax(Ops{h, int(l) + 1, K, s});

@@ -143,7 +143,7 @@ EXPORTS = ["fcg_create", "fcg_destroy", "fcg_last_error", "fcg_evaluate", "fcg_e
            "fcg_shared_pack", "fcg_shared_unpack", "fcg_norm2", "fcg_set_async", "fcg_check_error",
            "fcg_evaluate_host",
            "fcg_amg_aggregate", "fcg_amg_tentative", "fcg_bsr_symbolic", "fcg_bsr_transpose_pattern",
-           "fcg_bsr_spmv", "fcg_bsr_spgemm", "fcg_bsr_transpose_values", "fcg_bsr_from_node_csr",
+           "fcg_bsr_spmv", "fcg_bsr_spgemm", "fcg_bsr_product_plan", "fcg_bsr_spgemm_planned", "fcg_bsr_transpose_values", "fcg_bsr_from_node_csr",
            "fcg_bsr_block_jacobi_setup", "fcg_bsr_block_jacobi_apply", "fcg_amg_smooth_prolongator",
            "fcg_bsr_to_dense", "fcg_amg_default_options", "fcg_amg_create", "fcg_amg_solve",
            "fcg_amg_levels", "fcg_amg_level_info", "fcg_amg_setup_ms", "fcg_amg_stats", "fcg_amg_last_error",
@@ -272,6 +272,9 @@ def lib():
     L.fcg_bsr_spmv.argtypes = [c_int, c_int, c_int, i64, vp, vp, vp, vp, vp, c_dbl, c_int, vp]
     L.fcg_bsr_spgemm.argtypes = [c_int, c_int, c_int, c_int, i64, vp, vp, vp, vp, vp, vp, vp, vp,
                                  vp, vp]
+    L.fcg_bsr_product_plan.argtypes = [i64, vp, vp, vp, vp, vp, vp, i64, vp, vp, vp]
+    L.fcg_bsr_product_plan.restype = i64
+    L.fcg_bsr_spgemm_planned.argtypes = [c_int, c_int, c_int, c_int, i64, vp, vp, vp, vp, vp, vp, vp]
     L.fcg_bsr_transpose_values.argtypes = [c_int, c_int, c_int, i64, vp, vp, vp, vp]
     L.fcg_bsr_from_node_csr.argtypes = [c_int, i64, vp, vp, vp, vp, vp]
     L.fcg_bsr_block_jacobi_setup.argtypes = [c_int, c_int, i64, vp, vp, vp, vp, vp, vp]

@@ -296,7 +296,12 @@ int fcg_box_transfer(int device, int mode, int fnx, int fny, int fnz, int cnx, i
  * scalar row empty across its block row first gets a unit diagonal in d_vals) and returns
  * FCG_ERR_SINGULAR for a missing or singular block; fcg_bsr_block_jacobi_apply z = scale D^-1 r
  * (+ z); fcg_amg_smooth_prolongator P = T - omega D^-1 (A T) on P's pattern (br = 3, 6; 6
- * columns); fcg_bsr_to_dense fills a zeroed row-major dense matrix. */
+ * columns); fcg_bsr_to_dense fills a zeroed row-major dense matrix.
+ * fcg_bsr_product_plan (host) lists once, per block of C = A B on C's pattern, the (A block,
+ * B block) pairs whose products land there, in A's row order (count pass with pair_a = pair_b =
+ * NULL fills pair_ptr[0..nnzb_c]; returns the pair count, -1 on bad input);
+ * fcg_bsr_spgemm_planned forms C from such a plan -- the same products in the same order as
+ * fcg_bsr_spgemm, without its per-block column searches. */
 int64_t fcg_amg_aggregate(int64_t n, const int64_t* ptr, const int32_t* adj, const uint8_t* skip,
     int32_t* agg);
 int fcg_amg_tentative(int64_t n, int bs, const double* ns, const int32_t* agg, int64_t n_agg,
@@ -312,6 +317,12 @@ int fcg_bsr_spgemm(int device, int br, int bk, int bc, int64_t n_brows, const in
     const int32_t* d_a_col, const double* d_a_vals, const int64_t* d_b_ptr, const int32_t* d_b_col,
     const double* d_b_vals, const int64_t* d_c_ptr, const int32_t* d_c_col, double* d_c_vals,
     void* stream);
+int64_t fcg_bsr_product_plan(int64_t n_rows, const int64_t* a_ptr, const int32_t* a_col,
+    const int64_t* b_ptr, const int32_t* b_col, const int64_t* c_ptr, const int32_t* c_col,
+    int64_t n_cols, int64_t* pair_ptr, int32_t* pair_a, int32_t* pair_b);
+int fcg_bsr_spgemm_planned(int device, int br, int bk, int bc, int64_t nnzb_c, const int64_t* d_pair_ptr,
+    const int32_t* d_pair_a, const int32_t* d_pair_b, const double* d_a_vals, const double* d_b_vals,
+    double* d_c_vals, void* stream);
 int fcg_bsr_transpose_values(int device, int br, int bc, int64_t nnzb, const int64_t* d_perm,
     const double* d_vals, double* d_t_vals, void* stream);
 int fcg_bsr_from_node_csr(int device, int64_t n_brows, const int64_t* d_rowptr,

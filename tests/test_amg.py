@@ -100,6 +100,33 @@ def test_symbolic_and_transpose_patterns_match_scipy():
     del rng
 
 
+def test_product_plan_lists_the_pairs_in_row_order():
+    """fcg_bsr_product_plan against a direct listing: per C block, the (A block, B block) pairs whose
+    product lands on its column, in A's row order; a C pattern with a column dropped and one added
+    (no product) lists none for them."""
+    A = sp.random(40, 30, density=0.12, random_state=3, format="csr")
+    B = sp.random(30, 25, density=0.15, random_state=4, format="csr")
+    A.sort_indices()
+    B.sort_indices()
+    p, c = amg.symbolic(A.indptr, A.indices, B.indptr, B.indices, 25)
+    rows = [list(c[p[i]:p[i + 1]]) for i in range(40)]
+    rows[3] = rows[3][1:]  # drop a column
+    rows[5] = sorted(set(rows[5]) | {24, 0})  # columns no product reaches (maybe)
+    cp = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int64)
+    cc = np.concatenate([np.asarray(r, dtype=np.int32) for r in rows])
+    pp, pa, pb = amg.product_plan(A.indptr, A.indices, B.indptr, B.indices, cp, cc, 25)
+    for i in range(40):
+        for ci in range(cp[i], cp[i + 1]):
+            want = []
+            for ak in range(A.indptr[i], A.indptr[i + 1]):
+                k = A.indices[ak]
+                for bk in range(B.indptr[k], B.indptr[k + 1]):
+                    if B.indices[bk] == cc[ci]:
+                        want.append((ak, bk))
+            got = list(zip(pa[pp[ci]:pp[ci + 1]], pb[pp[ci]:pp[ci + 1]]))
+            assert got == want, (i, ci)
+
+
 def test_amg_rejects_bad_input():
     with pytest.raises(ValueError):
         amg.aggregate(np.array([0, 1]), np.array([5]))
@@ -153,6 +180,53 @@ def test_bsr_kernels_match_numpy(br, bk, bc):
         assert rc == 0
         torch.cuda.synchronize()
         assert np.array_equal(T.to_numpy(), C.to_numpy().T)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("br,bk,bc", [(3, 3, 6), (6, 3, 6), (6, 6, 6), (3, 3, 3)])
+def test_planned_spgemm_equals_searching_spgemm(br, bk, bc):
+    """fcg_bsr_spgemm_planned from fcg_bsr_product_plan: bit-identical to fcg_bsr_spgemm."""
+    torch, dev = _dev()
+    rng = np.random.default_rng(br * 7 + bk * 3 + bc)
+    A = _rand_bsr(rng, 60, 45, br, bk, 0.1, dev)
+    B = _rand_bsr(rng, 45, 35, bk, bc, 0.12, dev)
+    p, c = amg.symbolic(A.ptr_h, A.col_h, B.ptr_h, B.col_h, 35)
+    C1, C2 = amg.Bsr(p, c, br, bc, 35, dev), amg.Bsr(p, c, br, bc, 35, dev)
+    C1.product(A, B)
+    pp, pa, pb = amg.product_plan(A.ptr_h, A.col_h, B.ptr_h, B.col_h, p, c, 35)
+    t = [torch.from_numpy(v).to(dev) for v in (pp, pa, pb)]
+    assert fcg.lib().fcg_bsr_spgemm_planned(0, br, bk, bc, C2.nnzb, amg._vp(t[0]), amg._vp(t[1]),
+                                            amg._vp(t[2]), amg._vp(A.vals), amg._vp(B.vals),
+                                            amg._vp(C2.vals), None) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(C1.vals, C2.vals)
+
+
+@pytest.mark.gpu
+def test_native_amg_planned_products_are_bit_identical(monkeypatch):
+    """The native AMG's Galerkin products from product plans (default) and by the searching kernel
+    (FCG_AMG_PLAN=0, read at fcg_amg_create): the same iterations and solution bit for bit."""
+    torch, dev = _dev()
+    dis, kin, load = _case("renumbered-totlag")
+    dbc, fext = _loads(dis, load)
+    ev = fcg.Evaluator(dis, kinematics=fcg.LINEAR, youngs=E, poisson=NU)
+    f64 = dict(dtype=torch.float64, device=dev)
+    K = torch.zeros(dis.nnz, **f64)
+    ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, torch.zeros(dis.n_cols, **f64),
+                       torch.zeros(dis.n_rows, **f64), K)
+    b = torch.from_numpy(fext).to(dev)
+    ev.dirichlet_apply(torch.from_numpy(dbc).to(dev), K, b)
+    out = {}
+    for plan in ("1", "0"):
+        monkeypatch.setenv("FCG_AMG_PLAN", plan)
+        solver = amg.NativeAMG(dis, ev, dbc)
+        x = torch.empty_like(b)
+        it, rel = solver.solve(K, b, x, 1e-10, 500)
+        out[plan] = (it, rel, x.cpu().numpy())
+        solver.close()
+    assert out["1"][0] == out["0"][0] and out["1"][1] == out["0"][1]
+    assert np.array_equal(out["1"][2], out["0"][2])
+    ev.close()
 
 
 @pytest.mark.gpu
