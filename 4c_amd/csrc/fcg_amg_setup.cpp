@@ -21,6 +21,8 @@
 //    sorted ascending -- the device product binary-searches them) and of P^T.
 // The numeric half (products, smoothing, block inverses, the cycle's operators) is fcg_amg.hip.
 #include <algorithm>
+#include <thread>
+#include <atomic>
 #include <climits>
 #include <cmath>
 #include <cstdint>
@@ -236,38 +238,67 @@ int64_t fcg_bsr_product_plan(int64_t n_rows, const int64_t* a_ptr, const int32_t
   const int64_t nnzb_c = n_rows ? c_ptr[n_rows] : 0;
   if ((n_rows && a_ptr[n_rows] > INT32_MAX) || nnzb_c < 0) return -1;
   const bool fill = pair_a != nullptr;
-  std::vector<int64_t> pos(size_t(n_cols), -1);  // C's block index of column c in the current row
-  std::vector<int64_t> cur;
-  if (fill) cur.assign(pair_ptr, pair_ptr + nnzb_c);
-  else std::fill(pair_ptr, pair_ptr + nnzb_c + 1, int64_t(0));
-  for (int64_t i = 0; i < n_rows; ++i)
-  {
-    for (int64_t ci = c_ptr[i]; ci < c_ptr[i + 1]; ++ci)
+  if (!fill) std::fill(pair_ptr, pair_ptr + nnzb_c + 1, int64_t(0));
+  // rows are independent (each C block belongs to one row): threads over row ranges, each with its
+  // own column -> C block map
+  std::atomic<bool> bad{false};
+  auto rows = [&](int64_t r0, int64_t r1) {
+    std::vector<int64_t> pos(size_t(n_cols), -1);  // C's block index of column c in the current row
+    std::vector<int64_t> cursor;
+    for (int64_t i = r0; i < r1 && !bad.load(std::memory_order_relaxed); ++i)
     {
-      if (c_col[ci] < 0 || c_col[ci] >= n_cols) return -1;
-      pos[size_t(c_col[ci])] = ci;
-    }
-    for (int64_t ak = a_ptr[i]; ak < a_ptr[i + 1]; ++ak)
-    {
-      const int32_t k = a_col[ak];
-      for (int64_t bk = b_ptr[k]; bk < b_ptr[k + 1]; ++bk)
+      for (int64_t ci = c_ptr[i]; ci < c_ptr[i + 1]; ++ci)
       {
-        const int32_t c = b_col[bk];
-        if (c < 0 || c >= n_cols || bk > INT32_MAX) return -1;
-        const int64_t ci = pos[size_t(c)];
-        if (ci < 0) continue;  // a product outside C's pattern is not formed (as the search kernel)
-        if (fill)
+        if (c_col[ci] < 0 || c_col[ci] >= n_cols)
         {
-          const int64_t t = cur[size_t(ci)]++;
-          pair_a[t] = int32_t(ak);
-          pair_b[t] = int32_t(bk);
+          bad = true;
+          return;
         }
-        else
-          ++pair_ptr[ci + 1];
+        pos[size_t(c_col[ci])] = ci;
       }
+      // (fill pass: a cursor per C block of the row; the count pass checked the indices)
+      std::vector<int64_t>& cur = cursor;
+      if (fill)
+      {
+        cur.clear();
+        for (int64_t ci = c_ptr[i]; ci < c_ptr[i + 1]; ++ci) cur.push_back(pair_ptr[ci]);
+      }
+      for (int64_t ak = a_ptr[i]; ak < a_ptr[i + 1]; ++ak)
+      {
+        const int32_t k = a_col[ak];
+        for (int64_t bk = b_ptr[k]; bk < b_ptr[k + 1]; ++bk)
+        {
+          const int32_t c = b_col[bk];
+          if (!fill && (c < 0 || c >= n_cols || bk > INT32_MAX))
+          {
+            bad = true;
+            return;
+          }
+          const int64_t ci = pos[size_t(c)];
+          if (ci < 0) continue;  // a product outside C's pattern is not formed (as the search kernel)
+          if (fill)
+          {
+            const int64_t t = cur[size_t(ci - c_ptr[i])]++;
+            pair_a[t] = int32_t(ak);
+            pair_b[t] = int32_t(bk);
+          }
+          else
+            ++pair_ptr[ci + 1];
+        }
+      }
+      for (int64_t ci = c_ptr[i]; ci < c_ptr[i + 1]; ++ci) pos[size_t(c_col[ci])] = -1;
     }
-    for (int64_t ci = c_ptr[i]; ci < c_ptr[i + 1]; ++ci) pos[size_t(c_col[ci])] = -1;
+  };
+  const int64_t nt = std::max<int64_t>(1, std::min<int64_t>({16, int64_t(std::thread::hardware_concurrency()), n_rows / 4096}));
+  if (nt == 1)
+    rows(0, n_rows);
+  else
+  {
+    std::vector<std::thread> th;
+    for (int64_t t = 0; t < nt; ++t) th.emplace_back(rows, n_rows * t / nt, n_rows * (t + 1) / nt);
+    for (auto& x : th) x.join();
   }
+  if (bad) return -1;
   if (!fill)
     for (int64_t ci = 0; ci < nnzb_c; ++ci) pair_ptr[ci + 1] += pair_ptr[ci];
   return pair_ptr[nnzb_c];

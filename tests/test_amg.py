@@ -127,6 +127,33 @@ def test_product_plan_lists_the_pairs_in_row_order():
             assert got == want, (i, ci)
 
 
+def test_product_plan_threaded_rows():
+    """The plan over enough rows that the library splits them across threads: every pair lands on
+    its block (A row = C row, A column = B row, B column = C column), in A's row order, and every
+    structural product into C's pattern is listed once."""
+    rng = np.random.default_rng(5)
+
+    def pattern(n, m, per_row):  # (scipy.sparse.random samples slowly at these sizes)
+        M = sp.csr_matrix((np.ones(n * per_row), rng.integers(0, m, n * per_row),
+                           np.arange(0, n * per_row + 1, per_row)), shape=(n, m))
+        M.sum_duplicates()
+        M.sort_indices()
+        return M
+
+    A, B = pattern(30000, 20000, 6), pattern(20000, 9000, 4)
+    p, c = amg.symbolic(A.indptr, A.indices, B.indptr, B.indices, 9000)
+    pp, pa, pb = amg.product_plan(A.indptr, A.indices, B.indptr, B.indices, p, c, 9000)
+    a_row = np.repeat(np.arange(30000), np.diff(A.indptr))
+    b_row = np.repeat(np.arange(20000), np.diff(B.indptr))
+    c_row = np.repeat(np.arange(30000), np.diff(p))
+    owner = np.repeat(np.arange(len(c)), np.diff(pp))
+    assert np.array_equal(a_row[pa], c_row[owner])
+    assert np.array_equal(A.indices[pa], b_row[pb])
+    assert np.array_equal(B.indices[pb], c[owner])
+    assert np.all((np.diff(pa) > 0) | (np.diff(owner) != 0))
+    assert len(pa) == int((abs(A).astype(bool).astype(np.int64) @ abs(B).astype(bool).astype(np.int64)).sum())
+
+
 def test_amg_rejects_bad_input():
     with pytest.raises(ValueError):
         amg.aggregate(np.array([0, 1]), np.array([5]))
