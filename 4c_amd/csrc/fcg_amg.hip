@@ -122,10 +122,12 @@ __global__ __launch_bounds__(kBlock) void bsr_spgemm_kernel(int64_t n,
 template <int BR, int BK, int BC>
 __global__ __launch_bounds__(kBlock) void bsr_spgemm_plan_kernel(int64_t n_out,
     const int64_t* __restrict__ pptr, const int32_t* __restrict__ pa, const int32_t* __restrict__ pb,
-    const double* __restrict__ a_vals, const double* __restrict__ b_vals, double* c_vals)
+    const double* __restrict__ a_vals, const double* __restrict__ b_vals, double* c_vals,
+    const int64_t* __restrict__ order)
 {
-  const int64_t ci = int64_t(blockIdx.x) * kBlock + threadIdx.x;
-  if (ci >= n_out) return;
+  const int64_t t0 = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (t0 >= n_out) return;
+  const int64_t ci = order ? order[t0] : t0;
   double acc[BR * BC];
 #pragma unroll
   for (int q = 0; q < BR * BC; ++q) acc[q] = 0.0;
@@ -386,7 +388,7 @@ int fcg_bsr_spgemm(int device, int br, int bk, int bc, int64_t n_brows, const in
 
 int fcg_bsr_spgemm_planned(int device, int br, int bk, int bc, int64_t nnzb_c, const int64_t* d_pair_ptr,
     const int32_t* d_pair_a, const int32_t* d_pair_b, const double* d_a_vals, const double* d_b_vals,
-    double* d_c_vals, void* stream)
+    double* d_c_vals, const int64_t* d_order, void* stream)
 {
   using namespace fcg_bsrk;
   if (nnzb_c < 0 || (nnzb_c > 0 && (!d_pair_ptr || !d_pair_a || !d_pair_b || !d_a_vals || !d_b_vals || !d_c_vals)))
@@ -397,7 +399,7 @@ int fcg_bsr_spgemm_planned(int device, int br, int bk, int bc, int64_t nnzb_c, c
   const dim3 g(blocks_for(nnzb_c, kBlock)), b(kBlock);
 #define FCG_SPGEMM_P(R, K, C)                                                                      \
   hipLaunchKernelGGL((bsr_spgemm_plan_kernel<R, K, C>), g, b, 0, s, nnzb_c, d_pair_ptr, d_pair_a,  \
-      d_pair_b, d_a_vals, d_b_vals, d_c_vals)
+      d_pair_b, d_a_vals, d_b_vals, d_c_vals, d_order)
   if (br == 3 && bk == 3 && bc == 6) FCG_SPGEMM_P(3, 3, 6);
   else if (br == 6 && bk == 3 && bc == 6) FCG_SPGEMM_P(6, 3, 6);
   else if (br == 6 && bk == 6 && bc == 6) FCG_SPGEMM_P(6, 6, 6);

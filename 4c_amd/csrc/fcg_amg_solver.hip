@@ -287,6 +287,7 @@ struct Bsr {
 struct Plan {
   int64_t* ptr = nullptr;
   int32_t *a = nullptr, *b = nullptr;
+  int64_t* order = nullptr;  // C blocks by (aggregate of the row, row), or NULL
 };
 
 struct Step {  // level l -> l + 1
@@ -443,9 +444,24 @@ bool env_off(const char* name);
 
 // the pairs of C = X Y on C's pattern, listed on the host and uploaded (the numeric SpGEMM per
 // tangent then streams them instead of searching Y's rows for every C block)
-Plan make_plan(fcg_amg* h, const Bsr& X, const Bsr& Y, const Bsr& C)
+Plan make_plan(fcg_amg* h, const Bsr& X, const Bsr& Y, const Bsr& C, const std::vector<int32_t>* agg = nullptr)
 {
   Plan pl;
+  if (agg)
+  {
+    // rows of one aggregate are neighbours: forming their blocks together re-reads the Y rows of
+    // their shared neighbours from cache (on a renumbered mesh storage order scatters them)
+    std::vector<int64_t> rows(size_t(C.n));
+    for (int64_t i = 0; i < C.n; ++i) rows[size_t(i)] = i;
+    std::stable_sort(rows.begin(), rows.end(), [&](int64_t p, int64_t q) {
+      return (*agg)[size_t(p)] < (*agg)[size_t(q)];  // unaggregated rows (-1) first
+    });
+    std::vector<int64_t> ord;
+    ord.reserve(size_t(C.nnzb));
+    for (int64_t i : rows)
+      for (int64_t ci = C.ptr_h[size_t(i)]; ci < C.ptr_h[size_t(i) + 1]; ++ci) ord.push_back(ci);
+    pl.order = upload(h, ord);
+  }
   std::vector<int64_t> ptr(size_t(C.nnzb) + 1, 0);
   const int64_t np = fcg_bsr_product_plan(X.n, X.ptr_h.data(), X.col_h.data(), Y.ptr_h.data(),
       Y.col_h.data(), C.ptr_h.data(), C.col_h.data(), C.n_cols, ptr.data(), nullptr, nullptr);
@@ -515,8 +531,9 @@ void coarsen(fcg_amg* h, const Bsr* A_start, int bs, std::vector<double> ns, con
     const bool plans = !env_off("FCG_AMG_PLAN");
     if (plans)  // (before the level list grows: A may point into it)
     {
-      st.pAT = make_plan(h, *A, st.T, st.AT);
-      st.pAP = make_plan(h, *A, st.P, st.AP);
+      const bool by_agg = !env_off("FCG_AMG_PLAN_ORDER");
+      st.pAT = make_plan(h, *A, st.T, st.AT, by_agg ? &agg : nullptr);
+      st.pAP = make_plan(h, *A, st.P, st.AP, by_agg ? &agg : nullptr);
     }
     h->levels.emplace_back();
     Level& c = h->levels.back();
@@ -811,7 +828,7 @@ void galerkin_from(fcg_amg* h, size_t l0, const double* K, hipStream_t s)
     auto product = [&](Bsr& C, const Bsr& X, const Bsr& Y, const Plan& pl) {
       if (pl.ptr)
         ck(fcg_bsr_spgemm_planned(h->device, X.br, X.bc, Y.bc, C.nnzb, pl.ptr, pl.a, pl.b, X.vals,
-               Y.vals, C.vals, s),
+               Y.vals, C.vals, pl.order, s),
             "fcg_bsr_spgemm_planned");
       else
         ck(fcg_bsr_spgemm(h->device, X.br, X.bc, Y.bc, X.n, X.ptr, X.col, X.vals, Y.ptr, Y.col, Y.vals,

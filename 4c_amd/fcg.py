@@ -274,7 +274,7 @@ def lib():
                                  vp, vp]
     L.fcg_bsr_product_plan.argtypes = [i64, vp, vp, vp, vp, vp, vp, i64, vp, vp, vp]
     L.fcg_bsr_product_plan.restype = i64
-    L.fcg_bsr_spgemm_planned.argtypes = [c_int, c_int, c_int, c_int, i64, vp, vp, vp, vp, vp, vp, vp]
+    L.fcg_bsr_spgemm_planned.argtypes = [c_int, c_int, c_int, c_int, i64, vp, vp, vp, vp, vp, vp, vp, vp]
     L.fcg_bsr_transpose_values.argtypes = [c_int, c_int, c_int, i64, vp, vp, vp, vp]
     L.fcg_bsr_from_node_csr.argtypes = [c_int, i64, vp, vp, vp, vp, vp]
     L.fcg_bsr_block_jacobi_setup.argtypes = [c_int, c_int, i64, vp, vp, vp, vp, vp, vp]

@@ -301,7 +301,9 @@ int fcg_box_transfer(int device, int mode, int fnx, int fny, int fnz, int cnx, i
  * B block) pairs whose products land there, in A's row order (count pass with pair_a = pair_b =
  * NULL fills pair_ptr[0..nnzb_c]; returns the pair count, -1 on bad input);
  * fcg_bsr_spgemm_planned forms C from such a plan -- the same products in the same order as
- * fcg_bsr_spgemm, without its per-block column searches. */
+ * fcg_bsr_spgemm, without its per-block column searches; d_order (or NULL = storage order) is the
+ * order in which the C blocks are formed (thread t forms block d_order[t]: e.g. rows grouped by
+ * aggregate, so that the B rows of neighbouring rows are re-read from cache). */
 int64_t fcg_amg_aggregate(int64_t n, const int64_t* ptr, const int32_t* adj, const uint8_t* skip,
     int32_t* agg);
 int fcg_amg_tentative(int64_t n, int bs, const double* ns, const int32_t* agg, int64_t n_agg,
@@ -322,7 +324,7 @@ int64_t fcg_bsr_product_plan(int64_t n_rows, const int64_t* a_ptr, const int32_t
     int64_t n_cols, int64_t* pair_ptr, int32_t* pair_a, int32_t* pair_b);
 int fcg_bsr_spgemm_planned(int device, int br, int bk, int bc, int64_t nnzb_c, const int64_t* d_pair_ptr,
     const int32_t* d_pair_a, const int32_t* d_pair_b, const double* d_a_vals, const double* d_b_vals,
-    double* d_c_vals, void* stream);
+    double* d_c_vals, const int64_t* d_order, void* stream);
 int fcg_bsr_transpose_values(int device, int br, int bc, int64_t nnzb, const int64_t* d_perm,
     const double* d_vals, double* d_t_vals, void* stream);
 int fcg_bsr_from_node_csr(int device, int64_t n_brows, const int64_t* d_rowptr,

@@ -224,9 +224,15 @@ def test_planned_spgemm_equals_searching_spgemm(br, bk, bc):
     t = [torch.from_numpy(v).to(dev) for v in (pp, pa, pb)]
     assert fcg.lib().fcg_bsr_spgemm_planned(0, br, bk, bc, C2.nnzb, amg._vp(t[0]), amg._vp(t[1]),
                                             amg._vp(t[2]), amg._vp(A.vals), amg._vp(B.vals),
-                                            amg._vp(C2.vals), None) == 0
+                                            amg._vp(C2.vals), None, None) == 0
+    # the same blocks formed in a shuffled order
+    C3 = amg.Bsr(p, c, br, bc, 35, dev)
+    order = torch.from_numpy(rng.permutation(C3.nnzb).astype(np.int64)).to(dev)
+    assert fcg.lib().fcg_bsr_spgemm_planned(0, br, bk, bc, C3.nnzb, amg._vp(t[0]), amg._vp(t[1]),
+                                            amg._vp(t[2]), amg._vp(A.vals), amg._vp(B.vals),
+                                            amg._vp(C3.vals), amg._vp(order), None) == 0
     torch.cuda.synchronize()
-    assert torch.equal(C1.vals, C2.vals)
+    assert torch.equal(C1.vals, C2.vals) and torch.equal(C1.vals, C3.vals)
 
 
 @pytest.mark.gpu
