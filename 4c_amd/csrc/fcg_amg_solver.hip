@@ -273,6 +273,44 @@ __global__ __launch_bounds__(kBlock) void random_kernel(double* v, const double*
   v[i] = mask ? u * mask[i] : u;
 }
 
+// the context's node-triple K into the reordered BSR copy: block m of level-0 row p is triple
+// old_k of context row new2old[p] (16 lanes per row, as node_csr_to_bsr_kernel)
+__global__ __launch_bounds__(kBlock) void perm_csr_to_bsr_kernel(int64_t n, const int64_t* __restrict__ rowptr,
+    const int64_t* __restrict__ b_ptr, const int32_t* __restrict__ new2old, const int32_t* __restrict__ old_k,
+    const double* __restrict__ K, double* b_vals)
+{
+  const int64_t p = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> 4;
+  const int lane = threadIdx.x & 15;
+  if (p >= n) return;
+  const int64_t r = new2old[p];
+  const int64_t r0 = rowptr[3 * r], r1 = rowptr[3 * r + 1], r2 = rowptr[3 * r + 2];
+  for (int64_t q = b_ptr[p] + lane; q < b_ptr[p + 1]; q += 16)
+  {
+    const int64_t k3 = 3 * int64_t(old_k[q]);
+    double* o = b_vals + q * 9;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+    {
+      o[c] = K[r0 + k3 + c];
+      o[3 + c] = K[r1 + k3 + c];
+      o[6 + c] = K[r2 + k3 + c];
+    }
+  }
+}
+
+// node triples between the context's order and level 0's: gather dst[3p + d] = src[3 new2old[p] + d]
+// (to_ctx = 0) or scatter dst[3 new2old[p] + d] = src[3p + d] (to_ctx = 1)
+__global__ __launch_bounds__(kBlock) void node_perm_kernel(int64_t nb, const int32_t* __restrict__ new2old,
+    const double* __restrict__ src, double* __restrict__ dst, int to_ctx)
+{
+  const int64_t t = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (t >= 3 * nb) return;
+  const int64_t p = t / 3, d = t - 3 * p;
+  const int64_t o = 3 * int64_t(new2old[p]) + d;
+  if (to_ctx) dst[o] = src[t];
+  else dst[t] = src[o];
+}
+
 struct Bsr {
   int64_t n = 0, nnzb = 0, n_cols = 0;
   int br = 0, bc = 0;
@@ -361,6 +399,13 @@ struct fcg_amg {
   double* g_x = nullptr;
   bool graph_off = false;
   int graph_launches = 0;
+  // single rank: level 0 renumbered in the Morton order of the node coordinates (a renumbered
+  // mesh's input order scatters every row's neighbours over the vectors; FCG_AMG_REORDER=0 keeps
+  // the context's order).  Level 0 is then the BSR copy A0 in that order: its SpMV and block
+  // Jacobi run on A0, the iteration's vectors are permuted on entry and exit.
+  int32_t* new2old = nullptr;  // [nb0] context node of level-0 node p (NULL: no reordering)
+  int32_t* old_k = nullptr;    // [A0.nnzb] triple index of each A0 block in its context row
+  double *pb = nullptr, *px = nullptr;  // permuted right-hand side / solution
 };
 
 namespace fcg_amgs {
@@ -571,7 +616,7 @@ void dot_dev(fcg_amg* h, const double* a, const double* b, int64_t n, double* ou
 // level 0: the context's SpMV (single rank), or the owned block's BSR copy (local)
 void apply_A0(fcg_amg* h, const double* K, const double* x, double* y, hipStream_t s)
 {
-  if (h->local)
+  if (h->local || h->new2old)
     ck(fcg_bsr_spmv(h->device, 3, 3, h->A0.n, h->A0.ptr, h->A0.col, h->A0.vals, x, y, 1.0, 0, s),
         "fcg_bsr_spmv (level 0)");
   else
@@ -605,7 +650,10 @@ struct Ops {
   }
   void dinv(const double* r, double* z, double scale, bool acc) const
   {
-    if (l == 0)
+    if (l == 0 && h->new2old)  // reordered level 0: its BSR block inverses
+      ck(fcg_bsr_block_jacobi_apply(h->device, 3, h->nb0, h->A0_dinv, r, z, scale, acc ? 1 : 0, s),
+          "fcg_bsr_block_jacobi_apply (level 0)");
+    else if (l == 0)
       ck(fcg_block_jacobi_apply(h->ctx, h->ctx_dinv, r, z, scale, acc ? 1 : 0, s), "fcg_block_jacobi_apply");
     else
     {
@@ -804,6 +852,22 @@ void coarse_factor(fcg_amg* h, hipStream_t s);
 // numeric setup for the tangent K (level-0 values in the context's CSR order)
 void setup(fcg_amg* h, const double* K, hipStream_t s)
 {
+  if (h->new2old)
+  {
+    // the context's nodal blocks first, for their singularity check (4C's block Jacobi throws on a
+    // singular block; the BSR setup below completes empty rows with a unit diagonal instead)
+    ck(fcg_block_jacobi_setup(h->ctx, K, h->ctx_dinv, s), "singular nodal block of K (block Jacobi)");
+    // reordered level 0: the BSR copy in level 0's order, its block inverses (the smoother's too)
+    hipLaunchKernelGGL(perm_csr_to_bsr_kernel, dim3(blocks_for(h->nb0 * 16)), dim3(kBlock), 0, s, h->nb0,
+        h->ctx->mesh.rowptr, h->A0.ptr, h->new2old, h->old_k, K, h->A0.vals);
+    ck(hipGetLastError(), "perm_csr_to_bsr_kernel");
+    ck(fcg_bsr_block_jacobi_setup(h->device, 3, h->nb0, h->A0.ptr, h->A0_diag, h->A0.vals, h->A0_dinv,
+           h->flag, s),
+        "singular nodal block of K");
+    estimate_lmax(Ops{h, 0, K, s});
+    galerkin_from(h, 0, K, s);
+    return;
+  }
   ck(fcg_block_jacobi_setup(h->ctx, K, h->ctx_dinv, s), "singular nodal block of K (block Jacobi)");
   // the BSR copy first: the local level 0 applies it in the lambda_max estimate
   ck(fcg_bsr_from_node_csr(h->device, h->nb0, h->ctx->mesh.rowptr, h->A0.ptr, K, h->A0.vals, s),
@@ -897,7 +961,27 @@ void coarse_factor(fcg_amg* h, hipStream_t s)
 }
 
 // flexible CG (Polak-Ribiere) preconditioned by one V-cycle; one host read per iteration
+void run_fcg_ordered(fcg_amg* h, const double* K, const double* b, double* x, double rtol, int max_iter,
+    int* iterations, double* rel, hipStream_t s);
+
+// level 0 reordered: the iteration runs on permuted copies of b and x
 void run_fcg(fcg_amg* h, const double* K, const double* b, double* x, double rtol, int max_iter,
+    int* iterations, double* rel, hipStream_t s)
+{
+  if (!h->new2old)
+  {
+    run_fcg_ordered(h, K, b, x, rtol, max_iter, iterations, rel, s);
+    return;
+  }
+  const dim3 g(blocks_for(h->n0)), bl(kBlock);
+  hipLaunchKernelGGL(node_perm_kernel, g, bl, 0, s, h->nb0, h->new2old, b, h->pb, 0);
+  ck(hipGetLastError(), "node_perm_kernel");
+  run_fcg_ordered(h, K, h->pb, h->px, rtol, max_iter, iterations, rel, s);
+  hipLaunchKernelGGL(node_perm_kernel, g, bl, 0, s, h->nb0, h->new2old, h->px, x, 1);
+  ck(hipGetLastError(), "node_perm_kernel");
+}
+
+void run_fcg_ordered(fcg_amg* h, const double* K, const double* b, double* x, double rtol, int max_iter,
     int* iterations, double* rel, hipStream_t s)
 {
   const int64_t n = h->n0;
@@ -1457,6 +1541,62 @@ int fcg_amg_create(fcg_ctx* ctx, const int64_t* rowptr, const int32_t* col_lid,
         if (c < 0 || c % 3 != 0 || c >= n) throw Fail{FCG_ERR_ARG, "fcg_amg_create: column triples must start at 3 c"};
         bcol[size_t(bptr[size_t(b)] + k)] = c / 3;
       }
+    // single rank: level 0 in the Morton order of the node coordinates (21 bits per axis)
+    std::vector<int32_t> new2old;
+    if (!h->local && !env_off("FCG_AMG_REORDER") && nb > 1)
+    {
+      double lo[3] = {node_x[0], node_x[1], node_x[2]}, hi[3] = {node_x[0], node_x[1], node_x[2]};
+      for (int64_t b = 0; b < nb; ++b)
+        for (int d = 0; d < 3; ++d)
+        {
+          lo[d] = std::min(lo[d], node_x[3 * b + d]);
+          hi[d] = std::max(hi[d], node_x[3 * b + d]);
+        }
+      std::vector<uint64_t> key(static_cast<size_t>(nb));
+      for (int64_t b = 0; b < nb; ++b)
+      {
+        uint64_t m = 0;
+        uint32_t q[3];
+        for (int d = 0; d < 3; ++d)
+        {
+          const double ext = hi[d] - lo[d];
+          const double f = ext > 0.0 ? (node_x[3 * b + d] - lo[d]) / ext : 0.0;
+          q[d] = uint32_t(std::min(2097151.0, std::max(0.0, f * 2097151.0)));
+        }
+        for (int bit = 20; bit >= 0; --bit)
+          for (int d = 0; d < 3; ++d) m = (m << 1) | ((q[d] >> bit) & 1u);
+        key[size_t(b)] = m;
+      }
+      new2old.resize(size_t(nb));
+      for (int64_t b = 0; b < nb; ++b) new2old[size_t(b)] = int32_t(b);
+      std::stable_sort(new2old.begin(), new2old.end(),
+          [&](int32_t a, int32_t c) { return key[size_t(a)] < key[size_t(c)]; });
+      std::vector<int32_t> old2new(static_cast<size_t>(nb));
+      for (int64_t p = 0; p < nb; ++p) old2new[size_t(new2old[size_t(p)])] = int32_t(p);
+      std::vector<int64_t> pptr(size_t(nb) + 1, 0);
+      std::vector<int32_t> pcol(bcol.size()), pk(bcol.size());
+      std::vector<std::pair<int32_t, int32_t>> row;
+      for (int64_t p = 0; p < nb; ++p)
+      {
+        const int64_t r = new2old[size_t(p)];
+        row.clear();
+        for (int64_t k = bptr[size_t(r)]; k < bptr[size_t(r) + 1]; ++k)
+          row.emplace_back(old2new[size_t(bcol[size_t(k)])], int32_t(k - bptr[size_t(r)]));
+        std::sort(row.begin(), row.end());
+        pptr[size_t(p) + 1] = pptr[size_t(p)] + int64_t(row.size());
+        for (size_t m = 0; m < row.size(); ++m)
+        {
+          pcol[size_t(pptr[size_t(p)]) + m] = row[m].first;
+          pk[size_t(pptr[size_t(p)]) + m] = row[m].second;
+        }
+      }
+      bptr.swap(pptr);
+      bcol.swap(pcol);
+      h->new2old = upload(h, new2old);
+      h->old_k = upload(h, pk);
+      h->pb = dalloc<double>(h, n);
+      h->px = dalloc<double>(h, n);
+    }
     make_bsr(h, h->A0, bptr, bcol, 3, 3, nb);
     if (h->local)
     {
@@ -1484,18 +1624,34 @@ int fcg_amg_create(fcg_ctx* ctx, const int64_t* rowptr, const int32_t* col_lid,
       if (dbc_rows[k] < 0 || dbc_rows[k] >= n) throw Fail{FCG_ERR_ARG, "fcg_amg_create: Dirichlet row out of range"};
       dbc[size_t(dbc_rows[k])] = 1;
     }
+    // level 0's order (identity without reordering)
+    std::vector<double> xl;
+    const double* X0 = node_x;
+    if (!new2old.empty())
+    {
+      std::vector<uint8_t> dp(static_cast<size_t>(n));
+      xl.resize(size_t(3 * nb));
+      for (int64_t p = 0; p < nb; ++p)
+        for (int d = 0; d < 3; ++d)
+        {
+          dp[size_t(3 * p + d)] = dbc[size_t(3 * int64_t(new2old[size_t(p)]) + d)];
+          xl[size_t(3 * p + d)] = node_x[3 * int64_t(new2old[size_t(p)]) + d];
+        }
+      dbc.swap(dp);
+      X0 = xl.data();
+    }
     std::vector<double> mask(static_cast<size_t>(n));
     for (int64_t i = 0; i < n; ++i) mask[size_t(i)] = dbc[size_t(i)] ? 0.0 : 1.0;
     h->mask0 = upload(h, mask);
     // near-null space: rigid-body modes about the centroid, Dirichlet rows zeroed
     double cen[3] = {0, 0, 0};
     for (int64_t b = 0; b < nb; ++b)
-      for (int d = 0; d < 3; ++d) cen[d] += node_x[3 * b + d] / double(nb);
+      for (int d = 0; d < 3; ++d) cen[d] += X0[3 * b + d] / double(nb);
     std::vector<double> ns(size_t(nb) * 18, 0.0);
     std::vector<uint8_t> skip(size_t(nb), 0);
     for (int64_t b = 0; b < nb; ++b)
     {
-      const double x = node_x[3 * b] - cen[0], y = node_x[3 * b + 1] - cen[1], z = node_x[3 * b + 2] - cen[2];
+      const double x = X0[3 * b] - cen[0], y = X0[3 * b + 1] - cen[1], z = X0[3 * b + 2] - cen[2];
       double* B = ns.data() + 18 * b;  // [3][6]
       B[0 * 6 + 0] = B[1 * 6 + 1] = B[2 * 6 + 2] = 1.0;
       B[0 * 6 + 3] = -y; B[1 * 6 + 3] = x;
@@ -1667,7 +1823,16 @@ int fcg_amg_apply(fcg_amg* h, const double* d_K_vals, const double* d_r_row, dou
   {
     ck(hipSetDevice(h->device), "hipSetDevice");
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->ctx->stream;
-    vcycle(h, 0, d_K_vals, d_r_row, d_z_row, s);
+    if (h->new2old)
+    {
+      const dim3 g(blocks_for(h->n0)), bl(kBlock);
+      hipLaunchKernelGGL(node_perm_kernel, g, bl, 0, s, h->nb0, h->new2old, d_r_row, h->pb, 0);
+      vcycle(h, 0, d_K_vals, h->pb, h->px, s);
+      hipLaunchKernelGGL(node_perm_kernel, g, bl, 0, s, h->nb0, h->new2old, h->px, d_z_row, 1);
+      ck(hipGetLastError(), "node_perm_kernel");
+    }
+    else
+      vcycle(h, 0, d_K_vals, d_r_row, d_z_row, s);
   }
   catch (const Fail& f)
   {

@@ -481,6 +481,48 @@ def test_native_amg_dense_coarse_and_graph(monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("case", ["renumbered-totlag", "tiled-beam"])
+def test_native_amg_morton_level0_matches_context_order(monkeypatch, case):
+    """Level 0 renumbered in the Morton order of the node coordinates (default; the BSR copy in
+    that order, vectors permuted on entry and exit) against the context's order
+    (FCG_AMG_REORDER=0): the same solution to the solve tolerance, iteration counts alike, and
+    fcg_amg_apply's V-cycle in the caller's order (a symmetric positive preconditioner)."""
+    torch, dev = _dev()
+    if case == "tiled-beam":
+        dis, load = tiled_input_mesh(load_fixture(FX), (3, 6, 2), jitter=0.15, seed=11), -1e-3
+    else:
+        dis, _, load = _case(case)
+    dbc, fext = _loads(dis, load)
+    ev = fcg.Evaluator(dis, kinematics=fcg.LINEAR, youngs=E, poisson=NU)
+    f64 = dict(dtype=torch.float64, device=dev)
+    K = torch.zeros(dis.nnz, **f64)
+    ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, torch.zeros(dis.n_cols, **f64),
+                       torch.zeros(dis.n_rows, **f64), K)
+    b = torch.from_numpy(fext).to(dev)
+    ev.dirichlet_apply(torch.from_numpy(dbc).to(dev), K, b)
+    out = {}
+    for reorder in ("1", "0"):
+        monkeypatch.setenv("FCG_AMG_REORDER", reorder)
+        solver = amg.NativeAMG(dis, ev, dbc)
+        x = torch.empty_like(b)
+        it, rel = solver.solve(K, b, x, 1e-10, 500)
+        # the V-cycle through fcg_amg_apply: r . M r > 0 for a random r (caller's order in and out)
+        r = torch.randn(dis.n_rows, generator=torch.Generator().manual_seed(3), dtype=torch.float64).to(dev)
+        r[torch.from_numpy(dbc.astype(np.int64)).to(dev)] = 0.0
+        z = torch.empty_like(r)
+        L = fcg.lib()
+        assert L.fcg_amg_apply(solver._h, amg._vp(K), amg._vp(r), amg._vp(z), None) == 0
+        torch.cuda.synchronize()
+        out[reorder] = (it, rel, x.cpu().numpy(), float(torch.dot(r, z)))
+        solver.close()
+    (i1, r1, x1, q1), (i0, r0, x0, q0) = out["1"], out["0"]
+    assert r1 <= 1e-10 and r0 <= 1e-10 and q1 > 0 and q0 > 0
+    assert np.linalg.norm(x1 - x0) <= 1e-8 * np.linalg.norm(x0)
+    assert abs(i1 - i0) <= max(2, 0.25 * i0), (i1, i0)
+    ev.close()
+
+
+@pytest.mark.gpu
 def test_native_amg_rejects_bad_input():
     torch, dev = _dev()
     dis, kin, load = _case("renumbered-totlag")
