@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "fourc_gpu.h"
 #include "fcg_status.hpp"
@@ -23,13 +24,12 @@ constexpr int kBlock = 256;
 
 inline unsigned blocks_for(int64_t n, int per_block) { return unsigned((n + per_block - 1) / per_block); }
 
-// y = alpha A x (+ y): 8 lanes per block row, blocks strided over the lanes, butterfly sum
-template <int BR, int BC>
+// y = alpha A x (+ y): LPN lanes per block row, blocks strided over the lanes, butterfly sum
+template <int BR, int BC, int LPN = 8>
 __global__ __launch_bounds__(kBlock) void bsr_spmv_kernel(int64_t n, const int64_t* __restrict__ ptr,
     const int32_t* __restrict__ col, const double* __restrict__ vals, const double* __restrict__ x,
     double* y, double alpha, int accumulate)
 {
-  constexpr int LPN = 8;
   const int64_t row = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / LPN;
   const int lane = threadIdx.x % LPN;
   double acc[BR];
@@ -348,8 +348,21 @@ int fcg_bsr_spmv(int device, int br, int bc, int64_t n_brows, const int64_t* d_p
   if (!fcg_use_device(device)) return fcg_device_error();
   hipStream_t s = static_cast<hipStream_t>(stream);
   const dim3 g(blocks_for(n_brows * 8, kBlock)), b(kBlock);
-  if (br == 3 && bc == 3)
+  // 3 x 3 (an AMG level 0: ~27 blocks per row): 32 lanes per row, about one block each (renumbered
+  // 1M hex8 AMG Newton 0.350 / 0.341 / 0.330 s at 8 / 16 / 32 lanes, profiles/r04/r04_bsr_lpn_ab.txt;
+  // FCG_BSR_LPN33 = 4, 8, 16 for A/B)
+  static const int lpn33 = [] {
+    const char* e = std::getenv("FCG_BSR_LPN33");
+    return e ? std::atoi(e) : 32;
+  }();
+  if (br == 3 && bc == 3 && lpn33 == 4)
+    hipLaunchKernelGGL((bsr_spmv_kernel<3, 3, 4>), dim3(blocks_for(n_brows * 4, kBlock)), b, 0, s, n_brows, d_ptr, d_col, d_vals, d_x, d_y, alpha, accumulate);
+  else if (br == 3 && bc == 3 && lpn33 == 16)
+    hipLaunchKernelGGL((bsr_spmv_kernel<3, 3, 16>), dim3(blocks_for(n_brows * 16, kBlock)), b, 0, s, n_brows, d_ptr, d_col, d_vals, d_x, d_y, alpha, accumulate);
+  else if (br == 3 && bc == 3 && lpn33 == 8)
     hipLaunchKernelGGL((bsr_spmv_kernel<3, 3>), g, b, 0, s, n_brows, d_ptr, d_col, d_vals, d_x, d_y, alpha, accumulate);
+  else if (br == 3 && bc == 3)
+    hipLaunchKernelGGL((bsr_spmv_kernel<3, 3, 32>), dim3(blocks_for(n_brows * 32, kBlock)), b, 0, s, n_brows, d_ptr, d_col, d_vals, d_x, d_y, alpha, accumulate);
   else if (br == 3 && bc == 6)
     hipLaunchKernelGGL((bsr_spmv_kernel<3, 6>), g, b, 0, s, n_brows, d_ptr, d_col, d_vals, d_x, d_y, alpha, accumulate);
   else if (br == 6 && bc == 3)
