@@ -355,6 +355,10 @@ int fcg_bsr_spmv(int device, int br, int bc, int64_t n_brows, const int64_t* d_p
     const char* e = std::getenv("FCG_BSR_LPN33");
     return e ? std::atoi(e) : 32;
   }();
+  static const int lpn63 = [] {  // restriction P^T (an aggregate's row holds ~10^2 blocks): 32 lanes
+    const char* e = std::getenv("FCG_BSR_LPN63");
+    return e ? std::atoi(e) : 32;
+  }();
   static const int lpn66 = [] {  // 6 x 6 coarse levels: 32 lanes (0.329 -> 0.321 s, r04_bsr_lpn66_ab.txt)
     const char* e = std::getenv("FCG_BSR_LPN66");
     return e ? std::atoi(e) : 32;
@@ -369,8 +373,10 @@ int fcg_bsr_spmv(int device, int br, int bc, int64_t n_brows, const int64_t* d_p
     hipLaunchKernelGGL((bsr_spmv_kernel<3, 3, 32>), dim3(blocks_for(n_brows * 32, kBlock)), b, 0, s, n_brows, d_ptr, d_col, d_vals, d_x, d_y, alpha, accumulate);
   else if (br == 3 && bc == 6)
     hipLaunchKernelGGL((bsr_spmv_kernel<3, 6>), g, b, 0, s, n_brows, d_ptr, d_col, d_vals, d_x, d_y, alpha, accumulate);
-  else if (br == 6 && bc == 3)
+  else if (br == 6 && bc == 3 && lpn63 == 8)
     hipLaunchKernelGGL((bsr_spmv_kernel<6, 3>), g, b, 0, s, n_brows, d_ptr, d_col, d_vals, d_x, d_y, alpha, accumulate);
+  else if (br == 6 && bc == 3)
+    hipLaunchKernelGGL((bsr_spmv_kernel<6, 3, 32>), dim3(blocks_for(n_brows * 32, kBlock)), b, 0, s, n_brows, d_ptr, d_col, d_vals, d_x, d_y, alpha, accumulate);
   else if (br == 6 && bc == 6 && lpn66 == 16)
     hipLaunchKernelGGL((bsr_spmv_kernel<6, 6, 16>), dim3(blocks_for(n_brows * 16, kBlock)), b, 0, s, n_brows, d_ptr, d_col, d_vals, d_x, d_y, alpha, accumulate);
   else if (br == 6 && bc == 6 && lpn66 == 8)
