@@ -355,9 +355,9 @@ int fcg_bsr_spmv(int device, int br, int bc, int64_t n_brows, const int64_t* d_p
     const char* e = std::getenv("FCG_BSR_LPN33");
     return e ? std::atoi(e) : 32;
   }();
-  static const int lpn63 = [] {  // restriction P^T (an aggregate's row holds ~10^2 blocks): 32 lanes
+  static const int lpn63 = [] {  // restriction P^T: 8 lanes (32: no difference, r04_bsr_lpn63_ab.txt)
     const char* e = std::getenv("FCG_BSR_LPN63");
-    return e ? std::atoi(e) : 32;
+    return e ? std::atoi(e) : 8;
   }();
   static const int lpn66 = [] {  // 6 x 6 coarse levels: 32 lanes (0.329 -> 0.321 s, r04_bsr_lpn66_ab.txt)
     const char* e = std::getenv("FCG_BSR_LPN66");
