@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -368,6 +369,7 @@ struct fcg_amg {
   double* partial = nullptr;  // dot partials
   double* sc = nullptr;       // device scalars
   int32_t* flag = nullptr;
+  double* agree = nullptr;    // [2] fcg_amg_precond_setup's go/no-go all-reduce
   std::string last_error;
   std::vector<void*> allocs;
   double setup_ms = 0.0;
@@ -1849,13 +1851,64 @@ int fcg_amg_apply(fcg_amg* h, const double* d_K_vals, const double* d_r_row, dou
 int fcg_amg_precond_setup(fcg_amg* h, const double* d_K, const fcg_transport* tr, void* stream)
 {
   using namespace fcg_amgs;
+  // test hook: FCG_AMG_INJECT_FAIL_RANK=r makes rank r's local setup fail (tests/test_multigpu.py)
+  static const int inject = [] {
+    const char* e = std::getenv("FCG_AMG_INJECT_FAIL_RANK");
+    return e ? std::atoi(e) : -1;
+  }();
   int rc = fcg_amg_setup(h, d_K, stream);
-  if (rc != FCG_OK) return rc;
-  if (!h->local || !tr || tr->nranks <= 1) return FCG_OK;
+  if (rc == FCG_OK && tr && tr->nranks > 1 && tr->rank == inject)
+  {
+    h->ready = false;
+    h->last_error = "coupled AMG: injected setup failure (FCG_AMG_INJECT_FAIL_RANK)";
+    rc = FCG_ERR_SINGULAR;
+  }
+  if (!tr || tr->nranks <= 1) return rc;
+  // Every rank of the transport enters the coupled levels' chain of collectives (imports, the
+  // A_1 all-reduce) or none does: a go/no-go all-reduce of {local setup failed, handle not
+  // rank-local} first, a status all-reduce after the build and numeric setup.  A rank that fails
+  // alone would otherwise leave the others waiting in their next collective.
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->ctx->stream;
+  auto agree = [&](double bad, double nonlocal, double* out) -> int {
+    try
+    {
+      if (!h->agree) h->agree = dalloc<double>(h, 2);
+      const double v[2] = {bad, nonlocal};
+      ck(hipMemcpyAsync(h->agree, v, sizeof(v), hipMemcpyHostToDevice, s), "hipMemcpyAsync");
+      ck(tr->allreduce_fn(tr->user, h->agree, 2, s), "transport all-reduce (go/no-go)");
+      ck(hipMemcpyAsync(out, h->agree, 2 * sizeof(double), hipMemcpyDeviceToHost, s), "hipMemcpyAsync");
+      ck(hipStreamSynchronize(s), "hipStreamSynchronize");
+    }
+    catch (const Fail& f)
+    {
+      h->last_error = f.msg;
+      h->ctx->last_error = f.msg;
+      return f.code;
+    }
+    return FCG_OK;
+  };
+  double g[2] = {0.0, 0.0};
+  const int ra = agree(rc != FCG_OK ? 1.0 : 0.0, h->local ? 0.0 : 1.0, g);
+  if (ra != FCG_OK) return ra;
+  auto others_failed = [&](int code) {
+    h->ready = false;
+    h->last_error = "coupled AMG: the setup failed on another rank of the transport";
+    h->ctx->last_error = h->last_error;
+    return code;
+  };
+  if (g[0] > 0.0) return rc != FCG_OK ? rc : others_failed(FCG_ERR_DEVICE);
+  if (g[1] > 0.0 && g[1] < double(tr->nranks))
+  {
+    h->last_error = "coupled AMG: the ranks disagree on whether their handles are rank-local";
+    h->ctx->last_error = h->last_error;
+    h->ready = false;
+    return FCG_ERR_ARG;
+  }
+  if (!h->local) return FCG_OK;  // no rank's handle is rank-local: each keeps its own V-cycle
+  int code = FCG_OK;
   try
   {
     ck(hipSetDevice(h->device), "hipSetDevice");
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->ctx->stream;
     if (tr->rank < 0 || tr->rank >= tr->nranks) throw Fail{FCG_ERR_ARG, "coupled AMG: transport rank out of range"};
     if (!h->cpl)
     {
@@ -1867,7 +1920,7 @@ int fcg_amg_precond_setup(fcg_amg* h, const double* d_K, const fcg_transport* tr
       {
         // a failed build leaves no half-built coupling behind (its device buffers stay listed
         // in the handle's allocations until fcg_amg_destroy)
-        fcg_amg_destroy(h->cpl->g);
+        if (h->cpl) fcg_amg_destroy(h->cpl->g);
         delete h->cpl;
         h->cpl = nullptr;
         throw;
@@ -1882,8 +1935,12 @@ int fcg_amg_precond_setup(fcg_amg* h, const double* d_K, const fcg_transport* tr
     h->ready = false;
     h->last_error = f.msg;
     h->ctx->last_error = f.msg;
-    return f.code;
+    code = f.code;
   }
+  const int rb = agree(code != FCG_OK ? 1.0 : 0.0, 0.0, g);
+  if (code != FCG_OK) return code;
+  if (rb != FCG_OK) return rb;
+  if (g[0] > 0.0) return others_failed(FCG_ERR_DEVICE);
   return FCG_OK;
 }
 

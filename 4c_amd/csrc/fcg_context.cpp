@@ -770,6 +770,92 @@ bool build_colored_plan(const fcg_desc* d, ColorHost& P, std::string& why)
   return true;
 }
 
+// hex27 slab schedule (DeviceMesh::h27_*): elements in slabs of S consecutive elements; a row
+// node is assembled after the slab of its last incident element (its completing slab c), and its
+// records occupy consecutive ring slots from the moment its first element is evaluated (slab smin)
+// until that assembly.  Rows are laid out in the ring in assembly order (by c, then Morton order),
+// so a slot is reused by a later row; the smallest ring is the one in which every row's slots were
+// last held by rows assembled at least 1 + lag slabs before the row's first writer slab (element
+// and assembly launches alternate on one stream: lag 0).
+struct H27Ring {
+  int64_t nslab = 0, ring = 0;
+  std::vector<int64_t> asm_ptr;
+  std::vector<int32_t> rows, rslot0, slot;
+};
+
+void build_h27_ring(int64_t n_ele, int64_t S, int lag, const std::vector<int64_t>& inc_ptr,
+    const std::vector<int32_t>& inc_ele, const std::vector<uint8_t>& inc_a,
+    const std::vector<int64_t>& morton, H27Ring& R)
+{
+  const int64_t nrn = int64_t(inc_ptr.size()) - 1;
+  R.nslab = (n_ele + S - 1) / S;
+  std::vector<int32_t> smin(nrn, 0), cmax(nrn, 0);
+  parallel_for(nrn, [&](int64_t r) {
+    int64_t lo = INT64_MAX, hi = 0;
+    for (int64_t k = inc_ptr[r]; k < inc_ptr[r + 1]; ++k)
+    {
+      const int64_t sl = int64_t(inc_ele[k]) / S;
+      lo = std::min(lo, sl);
+      hi = std::max(hi, sl);
+    }
+    smin[r] = int32_t(lo == INT64_MAX ? 0 : lo);
+    cmax[r] = int32_t(hi);
+  });
+  // rows by completing slab, Morton order inside a slab (a stable counting sort of the Morton list)
+  R.asm_ptr.assign(R.nslab + 1, 0);
+  for (int64_t r = 0; r < nrn; ++r) R.asm_ptr[cmax[r] + 1]++;
+  for (int64_t c = 0; c < R.nslab; ++c) R.asm_ptr[c + 1] += R.asm_ptr[c];
+  R.rows.assign(nrn, 0);
+  {
+    std::vector<int64_t> fill(R.asm_ptr.begin(), R.asm_ptr.end() - 1);
+    for (int64_t i = 0; i < nrn; ++i)
+    {
+      const int64_t r = morton[i];
+      R.rows[fill[cmax[r]]++] = int32_t(r);
+    }
+  }
+  std::vector<int64_t> P(nrn + 1, 0);  // first ring position (unwrapped) of the j-th row
+  int64_t maxn = 1;
+  for (int64_t j = 0; j < nrn; ++j)
+  {
+    const int64_t n = inc_ptr[R.rows[j] + 1] - inc_ptr[R.rows[j]];
+    P[j + 1] = P[j] + n;
+    maxn = std::max(maxn, n);
+  }
+  const int64_t n_inc = P[nrn];
+  // does a ring of `ring` slots keep every row's slots free until its first writer slab?
+  auto fits = [&](int64_t ring) {
+    int64_t jp = 0;  // the row holding position P[j] + n - 1 - ring, found by a forward scan
+    for (int64_t j = 0; j < nrn; ++j)
+    {
+      const int64_t last = P[j + 1] - 1 - ring;
+      if (last < 0) continue;
+      while (P[jp + 1] <= last) ++jp;
+      if (cmax[R.rows[jp]] > smin[R.rows[j]] - 1 - lag) return false;
+    }
+    return true;
+  };
+  int64_t lo = maxn, hi = std::max<int64_t>(maxn, n_inc);
+  while (lo < hi)
+  {
+    const int64_t mid = lo + (hi - lo) / 2;
+    if (fits(mid))
+      hi = mid;
+    else
+      lo = mid + 1;
+  }
+  R.ring = lo;
+  R.rslot0.assign(nrn, 0);
+  R.slot.assign(size_t(n_ele) * 27, -1);
+  for (int64_t j = 0; j < nrn; ++j)
+  {
+    const int64_t r = R.rows[j];
+    R.rslot0[r] = int32_t(P[j] % R.ring);
+    for (int64_t k = inc_ptr[r]; k < inc_ptr[r + 1]; ++k)
+      R.slot[size_t(inc_ele[k]) * 27 + inc_a[k]] = int32_t((P[j] + (k - inc_ptr[r])) % R.ring);
+  }
+}
+
 void free_mesh(fcg::DeviceMesh& m)
 {
   void* ptrs[] = {m.apply_ye, m.apply_dof, m.gather_dummy, m.multi_ptr, m.rec_row0, m.rec_meta, m.rec_base, m.rec_ele, m.rec_a, m.rec_tmap, m.ele_orig, m.inc_ele, m.inc_a, m.asm_order, m.ele_x,
@@ -777,7 +863,7 @@ void free_mesh(fcg::DeviceMesh& m)
       m.rownode_row0, m.inc_pos, m.rowptr, m.scratch, m.err, m.elem_at, m.lat_x, m.lat_dof,
       m.plane_rec,
       m.tables, m.stamps, m.col_lid, m.diag_pos, m.pcg_work, m.col_ele, m.ele_ft, m.inc_row0, m.ele_gp,
-      m.pen_ptr, m.ele_nb};
+      m.pen_ptr, m.ele_nb, m.h27_rows, m.h27_rslot0, m.h27_slot};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (m.err_host) (void)hipHostFree(m.err_host);
@@ -1437,8 +1523,46 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
       // FCG_H27_SYMREC=1: one symmetric record per element (blocks a <= b) and h27_assemble_kernel
       const char* sym = std::getenv("FCG_H27_SYMREC");
       m.h27_increc = !(sym && sym[0] == '1');
+      // slab schedule of the incidence records (DeviceMesh::h27_*): FCG_H27_SLAB elements per
+      // slab (0 = one slab); by default only when one record per incidence would take more than a
+      // quarter of the device's memory (1M hex27: 53 GB of 288 GB -> one slab; the schedule costs
+      // ~10 % there, measured, but shrinks the scratch to ~1 GB, so that meshes of several million
+      // hex27 elements fit one GPU beside their tangent)
+      const char* sl = std::getenv("FCG_H27_SLAB");
+      int64_t S = sl ? std::atoll(sl) : 0;
+      int n_cu = 256;
+      size_t mem_total = 0;
+      {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, d->device) == hipSuccess)
+        {
+          if (prop.multiProcessorCount > 0) n_cu = prop.multiProcessorCount;
+          mem_total = prop.totalGlobalMem;
+        }
+        else
+          (void)hipGetLastError();
+      }
+      const char* eg = std::getenv("FCG_H27_EL_GRID");
+      m.h27_el_grid = eg ? std::max(1, std::atoi(eg)) : 2 * n_cu;  // the resident workgroups
+      const double full = double(n_inc) * double(fcg::record_doubles(npe)) * sizeof(double);
+      if (!sl && mem_total > 0 && full > 0.25 * double(mem_total))
+        S = std::max<int64_t>(8192, d->n_ele / 50);
+      int64_t n_slots = n_inc;
+      if (m.h27_increc && S > 0 && S < d->n_ele)
+      {
+        H27Ring R;
+        build_h27_ring(d->n_ele, S, 0, inc_ptr, inc_ele, inc_a, ord, R);
+        m.h27_nslab = R.nslab;
+        m.h27_slab = S;
+        m.h27_ring = R.ring;
+        m.h27_asm_ptr = R.asm_ptr;
+        n_slots = R.ring;
+        chk(upload(&m.h27_rows, R.rows.data(), nrn, bytes));
+        chk(upload(&m.h27_rslot0, R.rslot0.data(), nrn, bytes));
+        chk(upload(&m.h27_slot, R.slot.data(), d->n_ele * 27, bytes));
+      }
       chk(upload<double>(&m.scratch, nullptr,
-          m.h27_increc ? n_inc * fcg::record_doubles(npe) : d->n_ele * fcg::kH27RecDoubles, bytes));
+          m.h27_increc ? n_slots * fcg::record_doubles(npe) : d->n_ele * fcg::kH27RecDoubles, bytes));
     }
     else
       chk(upload<double>(&m.scratch, nullptr, n_inc * fcg::record_doubles(npe), bytes));
@@ -1659,6 +1783,18 @@ int fcg_evaluate_device(fcg_ctx* ctx, int action, int mode, const double* d_u_co
       he = fcg::launch_gather_h8(m, d_u_col, want_k, mode == FCG_OVERWRITE, d_K_vals, d_fint_row, s);
     if (T.enabled && he == hipSuccess) he = hipEventRecord(T.ev[1], s);
   }
+  else if (m.h27_nslab > 1)
+  {
+    // hex27 slab schedule: slab s's elements, then the rows whose last element it holds
+    for (int64_t sl = 0; sl < m.h27_nslab && he == hipSuccess; ++sl)
+    {
+      he = fcg::launch_h27_element(m, d_u_col, want_k, s, sl * m.h27_slab,
+          std::min(m.n_ele, (sl + 1) * m.h27_slab));
+      if (he == hipSuccess)
+        he = fcg::launch_assemble27_slab(m, sl, want_k, mode == FCG_OVERWRITE, d_K_vals, d_fint_row, s);
+    }
+    if (T.enabled && he == hipSuccess) he = hipEventRecord(T.ev[1], s);
+  }
   else
   {
     if (he == hipSuccess)
@@ -1824,7 +1960,8 @@ int fcg_get_info(const fcg_ctx* ctx, fcg_info* info)
   info->n_incidences = m.n_inc;
   info->scratch_bytes = !m.scratch ? 0
                         : m.h27s && !m.h27_increc ? m.n_ele * fcg::kH27RecDoubles * int64_t(sizeof(double))
-                                   : m.n_inc * fcg::record_doubles(m.npe) * int64_t(sizeof(double));
+                        : (m.h27_nslab > 1 ? m.h27_ring : m.n_inc) * fcg::record_doubles(m.npe) *
+                              int64_t(sizeof(double));
   info->device_bytes = ctx->device_bytes;
   info->path = m.path;
   return FCG_OK;

@@ -137,8 +137,11 @@ struct H27Args {
   const int32_t* node_dof_col;
   const double* u_col;
   double* rec;
-  const int32_t* inc_of;  // increc: [n_ele][27] incidence of (e, a), -1 = a not owned
-  int increc;             // 1: per-incidence block rows [n_inc][246] (assembled by assemble27_kernel)
+  const int32_t* inc_of;  // increc: [n_ele][27] record slot of (e, a) (the incidence, or its ring
+                          // slot under the slab schedule), -1 = a not owned
+  int increc;             // 1: per-incidence block rows [slots][246] (assembled by assemble27_kernel)
+  int64_t e_end;          // ASM 0: elements [blockIdx.x-th of e_begin.., e_end) (a slab)
+  int64_t e_begin;
   int32_t* err;
   double lambda, mu, cdiag;
   int want_k;
@@ -229,7 +232,7 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
   // the same sequence.
   int64_t pen = A.pen_begin + blockIdx.x, pos = -1, pend = -1;
   auto first_element = [&]() -> int64_t {
-    if (!ASM) return blockIdx.x < A.n_ele ? int64_t(blockIdx.x) : -1;
+    if (!ASM) return A.e_begin + blockIdx.x < A.e_end ? A.e_begin + blockIdx.x : -1;
     if (pen >= A.pen_end) return -1;
     pos = A.pen_ptr[pen];
     pend = A.pen_ptr[pen + 1];
@@ -237,7 +240,7 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
   };
   auto next_element = [&](int64_t e) -> int64_t {
     if (e < 0) return -1;
-    if (!ASM) return e + gridDim.x < A.n_ele ? e + gridDim.x : -1;
+    if (!ASM) return e + gridDim.x < A.e_end ? e + gridDim.x : -1;
     if (++pos < pend) return A.col_ele[pos];
     pen += gridDim.x;
     if (pen >= A.pen_end) return -1;
@@ -1605,17 +1608,21 @@ void upload_h27_tables()
 }
 
 hipError_t launch_h27_element(const DeviceMesh& m, const double* d_u_col, bool want_k,
-    hipStream_t stream)
+    hipStream_t stream, int64_t e_begin, int64_t e_end)
 {
-  if (m.n_ele == 0) return hipSuccess;
+  if (e_end < 0) e_end = m.n_ele;
+  const int64_t n = e_end - e_begin;
+  if (n <= 0) return hipSuccess;
   H27Args a{};
   a.n_ele = m.n_ele;
+  a.e_begin = e_begin;
+  a.e_end = e_end;
   a.ele_nodes = m.ele_nodes;
   a.node_x = m.node_x;
   a.node_dof_col = m.node_dof_col;
   a.u_col = d_u_col;
   a.rec = m.scratch;
-  a.inc_of = m.inc_of;
+  a.inc_of = m.h27_slot ? m.h27_slot : m.inc_of;  // slab schedule: the ring slot of each incidence
   a.increc = m.h27_increc ? 1 : 0;
   a.err = m.err;
   a.lambda = m.lambda;
@@ -1623,8 +1630,10 @@ hipError_t launch_h27_element(const DeviceMesh& m, const double* d_u_col, bool w
   a.cdiag = m.cdiag;
   a.want_k = want_k ? 1 : 0;
   a.stamps = m.stamps;
-  const int64_t cap = 256 * 8;
-  const dim3 grid(unsigned(m.n_ele < cap ? m.n_ele : cap)), block(kBlk);
+  // the whole mesh: 4 workgroups per CU queued (2 resident); a slab: at most the resident ones,
+  // so that every workgroup keeps several elements in its two-element pipeline
+  const int64_t cap = m.h27_nslab > 1 ? m.h27_el_grid : 256 * 8;
+  const dim3 grid(unsigned(n < cap ? n : cap)), block(kBlk);
   if (m.kinem == 0)
     hipLaunchKernelGGL((h27_element_kernel<0, 0>), grid, block, 0, stream, a);
   else

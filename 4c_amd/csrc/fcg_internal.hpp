@@ -6,6 +6,7 @@
 
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include "fourc_gpu.h"
 
@@ -76,6 +77,16 @@ struct DeviceMesh {
   double* gather_dummy = nullptr;   // [4] store target of a row without columns
   double* apply_ye = nullptr;       // [n_inc][3] fcg_tangent_apply's node parts (allocated on first use)
   int32_t* apply_dof = nullptr;     // [n_ele][27] column LID of each element node's first DOF (idem)
+  // hex27 slab schedule (FCG_H27_SLAB): the elements run in slabs of h27_slab consecutive
+  // elements; after slab s the row nodes whose last incident element lies in slab s are assembled,
+  // so an incidence record lives only from its slab to its row's slab, in a ring of h27_ring
+  // records (instead of one record per incidence)
+  int64_t h27_nslab = 0, h27_slab = 0, h27_ring = 0;
+  int h27_el_grid = 512;             // element workgroups per slab launch (the resident ones)
+  std::vector<int64_t> h27_asm_ptr;  // [h27_nslab + 1] range of h27_rows assembled after slab s
+  int32_t* h27_rows = nullptr;       // [n_rownodes] row nodes by completing slab, then Morton order
+  int32_t* h27_rslot0 = nullptr;     // [n_rownodes] ring slot of the row node's first record
+  int32_t* h27_slot = nullptr;       // [n_ele][27] ring slot of incidence (e, a), -1 = not owned
 
   // structured (row-block sweep) plan, hex8 only
   int path = FCG_PATH_GENERAL;
@@ -159,7 +170,10 @@ hipError_t launch_assemble(const DeviceMesh& m, bool want_k, bool overwrite, dou
 void upload_h27_tables();
 constexpr int64_t kH27RecDoubles = 378 * 9 + 81 + 1;  // even: 16-byte aligned records
 hipError_t launch_h27_element(const DeviceMesh& m, const double* d_u_col, bool want_k,
-    hipStream_t stream);
+    hipStream_t stream, int64_t e_begin = 0, int64_t e_end = -1);
+// hex27 slab schedule: the row assembly of the row nodes completed by slab s
+hipError_t launch_assemble27_slab(const DeviceMesh& m, int64_t s, bool want_k, bool overwrite,
+    double* d_K, double* d_fint, hipStream_t stream);
 hipError_t launch_h27_assemble(const DeviceMesh& m, bool want_k, bool overwrite, double* d_K,
     double* d_fint, hipStream_t stream);
 // hex27 StVK on a verified lattice: the same element kernel adding its blocks straight into the

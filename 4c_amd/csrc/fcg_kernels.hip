@@ -1237,6 +1237,12 @@ struct AssembleArgs {
   const int64_t* rowptr;
   double* K;
   double* fint;
+  // hex27 slab schedule (assemble27_kernel): rows[j_begin, j_end) (NULL: row nodes j directly),
+  // the records of row node r at slots rslot0[r] + i (mod ring); ring 0: at the incidence index
+  const int32_t* rows;
+  int64_t j_begin, j_end;
+  const int32_t* rslot0;
+  int64_t ring;
 };
 
 // hex27 rows: one wavefront per owned row node as assemble_kernel, the incidence records read as
@@ -1253,8 +1259,9 @@ __global__ __launch_bounds__(64) void assemble27_kernel(AssembleArgs A)
   constexpr int NV2 = 2;  // double2 pieces per lane and record: 122 pieces of the 243 entries
   __shared__ double acc[WANT_K ? 3 * 375 : 1];
   const int lane = threadIdx.x;
-  for (int64_t r = blockIdx.x; r < A.n_rownodes; r += gridDim.x)
+  for (int64_t jj = A.j_begin + blockIdx.x; jj < A.j_end; jj += gridDim.x)
   {
+    const int64_t r = A.rows ? int64_t(A.rows[jj]) : jj;
     const int32_t row0 = A.rownode_row0[r];
     const int64_t base = A.rowptr[row0];
     const int rowlen = int(A.rowptr[row0 + 1] - base);
@@ -1262,6 +1269,7 @@ __global__ __launch_bounds__(64) void assemble27_kernel(AssembleArgs A)
       for (int v = lane; v < 3 * rowlen; v += 64) acc[v] = 0.0;
     double f = 0.0;
     const int64_t k0 = A.inc_ptr[r], k1 = A.inc_ptr[r + 1];
+    const int64_t s0 = A.ring ? int64_t(A.rslot0[r]) : k0;  // record slot of incidence k0
     for (int64_t kb = k0; kb < k1; kb += NB)
     {
       double2 val[NB][NV2];
@@ -1279,7 +1287,9 @@ __global__ __launch_bounds__(64) void assemble27_kernel(AssembleArgs A)
           dst[q][s][0] = dst[q][s][1] = -1;
         }
         if (k >= k1) continue;
-        const double* src = A.scratch + k * REC;
+        int64_t slot = s0 + (k - k0);
+        if (A.ring && slot >= A.ring) slot -= A.ring;
+        const double* src = A.scratch + slot * REC;
         if (lane < 3) fv[q] = src[243 + lane];
         if (!WANT_K) continue;
         const uint16_t* pos = A.inc_pos + k * NPE;
@@ -1567,6 +1577,11 @@ hipError_t launch_assemble(const DeviceMesh& m, bool want_k, bool overwrite, dou
   a.rowptr = m.rowptr;
   a.K = d_K;
   a.fint = d_fint;
+  a.rows = nullptr;
+  a.j_begin = 0;
+  a.j_end = m.n_rownodes;
+  a.rslot0 = nullptr;
+  a.ring = 0;
   const int grid = grid_for(m.n_rownodes, 256 * 32);
 #define FCG_ASM(NPE)                                                                               \
   if (want_k && overwrite)                                                                         \
@@ -1593,6 +1608,37 @@ hipError_t launch_assemble(const DeviceMesh& m, bool want_k, bool overwrite, dou
       hipLaunchKernelGGL((assemble27_kernel<false, false>), dim3(grid), dim3(64), 0, stream, a);
   }
 #undef FCG_ASM
+  return hipGetLastError();
+}
+
+// hex27 slab schedule: the row nodes completed by slab s (m.h27_asm_ptr), records in the ring
+hipError_t launch_assemble27_slab(const DeviceMesh& m, int64_t s, bool want_k, bool overwrite,
+    double* d_K, double* d_fint, hipStream_t stream)
+{
+  AssembleArgs a;
+  a.n_rownodes = m.n_rownodes;
+  a.inc_ptr = m.inc_ptr;
+  a.rownode_row0 = m.rownode_row0;
+  a.inc_pos = m.inc_pos;
+  a.scratch = m.scratch;
+  a.rowptr = m.rowptr;
+  a.K = d_K;
+  a.fint = d_fint;
+  a.rows = m.h27_rows;
+  a.j_begin = m.h27_asm_ptr[s];
+  a.j_end = m.h27_asm_ptr[s + 1];
+  a.rslot0 = m.h27_rslot0;
+  a.ring = m.h27_ring;
+  if (a.j_end <= a.j_begin) return hipSuccess;
+  const int grid = grid_for(a.j_end - a.j_begin, 256 * 32);
+  if (want_k && overwrite)
+    hipLaunchKernelGGL((assemble27_kernel<true, true>), dim3(grid), dim3(64), 0, stream, a);
+  else if (want_k)
+    hipLaunchKernelGGL((assemble27_kernel<true, false>), dim3(grid), dim3(64), 0, stream, a);
+  else if (overwrite)
+    hipLaunchKernelGGL((assemble27_kernel<false, true>), dim3(grid), dim3(64), 0, stream, a);
+  else
+    hipLaunchKernelGGL((assemble27_kernel<false, false>), dim3(grid), dim3(64), 0, stream, a);
   return hipGetLastError();
 }
 

@@ -127,13 +127,17 @@ def gloo_exchange():
     return Exchange(fn, None, keepalive=cb)
 
 
-def thread_exchanges(world):
+def thread_exchanges(world, timeout=None, barrier_out=None):
     """`world` fcg_alltoallv_fn callbacks for ranks that are threads of ONE process (MPI_Alltoallv
     semantics through shared memory and a barrier): plan builds of every rank of a partition
     from one process -- a host that evaluates the ranks of a split in turn on one device, and the
-    CPU tests.  Rank r's plan build must run in its own thread with exchanges[r] (`run_ranks`)."""
+    CPU tests.  Rank r's plan build must run in its own thread with exchanges[r] (`run_ranks`).
+    `timeout` (s) bounds every barrier wait; `barrier_out` (a list) receives the barrier, so that
+    a caller can abort it when a rank fails outside its exchanges."""
     import threading
-    barrier = threading.Barrier(world)
+    barrier = threading.Barrier(world, timeout=timeout)
+    if barrier_out is not None:
+        barrier_out.append(barrier)
     slots = [None] * world
     out = []
     for rank in range(world):
@@ -163,11 +167,14 @@ def thread_exchanges(world):
     return out
 
 
-def run_ranks(world, fn):
+def run_ranks(world, fn, timeout=600.0):
     """fn(rank, exchange) for every rank, each in its own thread over thread_exchanges(world);
-    returns the results in rank order (re-raises the first failure)."""
+    returns the results in rank order (re-raises the first failure).  A rank that raises (or
+    calls its exchange a different number of times than the others) aborts the shared barrier, so
+    the other ranks fail instead of waiting forever; every wait is bounded by `timeout` seconds."""
     import threading
-    xs = thread_exchanges(world)
+    bar = []
+    xs = thread_exchanges(world, timeout=timeout, barrier_out=bar)
     res, err = [None] * world, [None] * world
 
     def body(r):
@@ -175,6 +182,7 @@ def run_ranks(world, fn):
             res[r] = fn(r, xs[r])
         except BaseException as e:  # noqa: BLE001 - re-raised in the caller
             err[r] = e
+            bar[0].abort()
 
     ts = [threading.Thread(target=body, args=(r,)) for r in range(world)]
     for t in ts:

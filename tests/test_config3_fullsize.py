@@ -36,9 +36,13 @@ def _straddling_row(rowptr, offset):
     return int(np.searchsorted(rowptr, offset, side="right") - 1)
 
 
-def test_config3_rows_past_int32_offsets_against_oracle():
+@pytest.mark.parametrize("slab", [0, 20000])
+def test_config3_rows_past_int32_offsets_against_oracle(monkeypatch, slab):
+    """slab 20000: the slab schedule of the incidence records -- the records live in
+    a ring of about 1 GB instead of one 1,968-byte record per incidence (53 GB)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    monkeypatch.setenv("FCG_H27_SLAB", str(slab))
     dev = torch.device("cuda:0")
     mesh = fcg.BoxMesh(fcg.HEX27, (N, N, N), jitter=0.02, seed=20251015)
     assert mesh.nnz > 2 ** 31
@@ -46,6 +50,8 @@ def test_config3_rows_past_int32_offsets_against_oracle():
         assert mesh.nnz == 4_625_301_609 and mesh.n_rows == 24_361_803
     u = mesh.u_col(5e-2)
     ev = fcg.Evaluator(mesh, kinematics=fcg.TOTLAG, youngs=E, poisson=NU)
+    if slab and N == 100:
+        assert ev.info.scratch_bytes < 1e9, ev.info.scratch_bytes
     f = torch.zeros(mesh.n_rows, dtype=torch.float64, device=dev)
     K = torch.full((mesh.nnz,), float("nan"), dtype=torch.float64, device=dev)
     u_d = torch.from_numpy(u).to(dev)

@@ -206,3 +206,25 @@ def test_thread_exchange_plans_match_the_global_maps(world):
         own = parts[r][:m.n_owned_rows]
         gi = np.array([grow[int(g)] for g in m.row_gid[:m.n_owned_rows]])
         assert np.abs(own - fg[gi]).max() <= 1e-12 * np.abs(fg).max(), r
+
+
+def test_run_ranks_fails_instead_of_hanging_when_a_rank_raises():
+    """A rank that raises before its exchange aborts the shared barrier: the other rank's plan
+    build fails (its exchange returns an error code) and run_ranks re-raises, no hang."""
+    import time
+    fcg = importlib.import_module("4c_amd").fcg
+    halo = importlib.import_module("4c_amd.halo")
+    world = 2
+    meshes = [fcg.BoxMesh(0, (4, 2, 2), rank=r, nranks=world) for r in range(world)]
+
+    def fn(r, x):
+        if r == 1:
+            time.sleep(0.2)  # rank 0 is already waiting in its exchange
+            raise ValueError("rank 1 failed before its exchange")
+        return halo.ImportPlan(r, world, meshes[r].row_gid, meshes[r].col_gid,
+                               halo.col_owner_of(meshes[r]), x)
+
+    t0 = time.time()
+    with pytest.raises(Exception):
+        halo.run_ranks(world, fn, timeout=60.0)
+    assert time.time() - t0 < 30.0

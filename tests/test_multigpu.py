@@ -382,6 +382,53 @@ def test_two_ranks_native_dfcg(celltype, kinem, solver):
         assert n2 <= nu, (iters, unc)
 
 
+def test_two_ranks_native_dfcg_rccl():
+    """The coupled AMG path of fcg_dfcg_solve over the library's RCCL transport (fcg_transport_rccl
+    names rank / nranks, so every RCCL solve with an AMG handle couples its coarse levels): one GPU
+    per rank, the 1-rank solution, coupled levels >= 1 and the 1.5x iteration bound."""
+    _dev()
+    if torch.cuda.device_count() < 2:
+        pytest.skip("RCCL transport needs two GPUs (RCCL refuses two ranks on one device)")
+    iters = _run_two_rank_solve(fcg.LINEAR, fcg.PATH_AUTO, "rccl", "native", fcg.HEX8)
+    one = _one_rank_amg_iters(fcg.HEX8, fcg.LINEAR)
+    assert sum(i or 0 for i in iters[0]) <= 1.5 * sum(one), (one, iters)
+
+
+def test_coupled_amg_setup_failure_on_one_rank_fails_every_rank():
+    """A rank whose local AMG setup fails (injected on rank 1) must not leave rank 0 waiting in the
+    coupled levels' collectives: fcg_amg_precond_setup all-reduces a go/no-go flag first, so both
+    ranks' solves raise."""
+    _dev()
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    qq = ctx.Queue()
+    port = 29700 + (os.getpid() + 7) % 1000
+    old = os.environ.get("FCG_AMG_INJECT_FAIL_RANK")
+    os.environ["FCG_AMG_INJECT_FAIL_RANK"] = "1"
+    try:
+        procs = [ctx.Process(target=_worker_solve, args=(r, 2, port, qq, fcg.LINEAR, fcg.PATH_AUTO,
+                                                         "staged", "native")) for r in range(2)]
+        for p in procs:
+            p.start()
+    finally:
+        if old is None:
+            del os.environ["FCG_AMG_INJECT_FAIL_RANK"]
+        else:
+            os.environ["FCG_AMG_INJECT_FAIL_RANK"] = old
+    try:
+        res = sorted(qq.get(timeout=180) for _ in range(2))
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.terminate()
+    assert [r for r, _, _ in res] == [0, 1]
+    for rank, ok, _ in res:
+        assert ok is not True, (rank, ok)
+    assert "another rank" in res[0][1], res[0][1][-400:]
+    assert "injected" in res[1][1], res[1][1][-400:]
+
+
 @pytest.mark.parametrize("world", [4, 8])
 def test_many_ranks_coupled_amg_iterations(world):
     """The coupled coarse levels at 4 and 8 ranks (host-staged on one GPU, hex8 linear box): the

@@ -51,4 +51,4 @@ print(json.dumps({"config": f"{a.celltype}-{a.kinem}-{a.material}-{a.n}^3-{a.act
                   "elements": m.n_ele, "nnz": m.nnz, "ms_evaluate": ms,
                   "ms_element": sorted(ts)[len(ts) // 2][0], "ms_assemble": sorted(ts)[len(ts) // 2][1],
                   "elem_per_s": m.n_ele / (ms * 1e-3), "mesh_s": t1 - t0, "create_s": t2 - t1,
-                  "device_bytes": int(ev.info.device_bytes)}))
+                  "device_bytes": int(ev.info.device_bytes), "scratch_bytes": int(ev.info.scratch_bytes)}))

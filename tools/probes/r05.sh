@@ -1,0 +1,78 @@
+#!/bin/bash
+# Round-5 GPU probe runner (one parameterised script instead of one file per gpurun call).
+# usage (on the GPU box, from the repo root): tools/probes/r05.sh <step> [<step> ...]
+# Every step runs under its own time limit; the first failing step ends the call.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 2
+O=gpurun_out/r05
+mkdir -p $O
+export TMPDIR=/tmp
+ET="tools/eval_timing.py"
+run() {  # run <seconds> <log> <cmd...>: time-limited, output appended to $O/<log>
+  local t=$1 log=$2; shift 2
+  echo "== $*" >> $O/$log
+  timeout -k 10 "$t" "$@" >> $O/$log 2>&1 || { echo "step failed ($?): $*"; tail -30 $O/$log; exit 1; }
+}
+for step in "$@"; do
+  case $step in
+    h27)  # hex27 evaluate timing (element + assembly split), 40^3 linear / TotLag, 100^3 TotLag
+      for k in linear totlag; do run 200 h27.jsonl python3 $ET --celltype hex27 --kinem $k --n 40 --reps 9; done
+      run 300 h27.jsonl python3 $ET --celltype hex27 --kinem totlag --n 100 --reps 5
+      grep '^{' $O/h27.jsonl | tail -3 ;;
+    h27q)  # hex27 40^3 only
+      for k in linear totlag; do run 200 h27.jsonl python3 $ET --celltype hex27 --kinem $k --n 40 --reps 9; done
+      grep '^{' $O/h27.jsonl | tail -2 ;;
+    slab)  # hex27 slab schedule: FCG_H27_SLAB x FCG_H27_STREAMS sweep, 40^3 TotLag / linear, 100^3 TotLag
+      for k in totlag linear; do
+        for sl in 0 800 1600 3200 6400; do for st in 1 2; do
+          [ $sl = 0 ] && [ $st = 2 ] && continue
+          echo "slab=$sl streams=$st $(FCG_H27_SLAB=$sl FCG_H27_STREAMS=$st timeout -k 10 120 python3 $ET --celltype hex27 --kinem $k --n 40 --reps 9 | tail -1)" >> $O/slab.txt || exit 1
+        done; done
+      done
+      for sl in 0 5000 10000 20000; do for st in 1 2; do
+        [ $sl = 0 ] && [ $st = 2 ] && continue
+        echo "slab=$sl streams=$st $(FCG_H27_SLAB=$sl FCG_H27_STREAMS=$st timeout -k 10 300 python3 $ET --celltype hex27 --kinem totlag --n 100 --reps 5 | tail -1)" >> $O/slab.txt || exit 1
+      done; done
+      python3 -c "
+import json
+for l in open('$O/slab.txt'):
+    h, j = l.split(' {', 1); d = json.loads('{' + j)
+    print(h, d['config'], round(d['ms_evaluate'], 3), round(d['device_bytes'] / 1e9, 2))" ;;
+    h27ab)  # same-box A/B of lib variants (FCG_LIB), hex27 40^3: h27ab with LIBS="default recw1"
+      for r in 1 2; do for v in ${LIBS:-default}; do for k in linear totlag; do
+        if [ "$v" = default ]; then unset FCG_LIB; else export FCG_LIB=$v; fi
+        echo "$v $k $(timeout -k 10 120 python3 $ET --celltype hex27 --kinem $k --n 40 --reps 9 | tail -1)" >> $O/h27ab.txt || exit 1
+      done; done; done; unset FCG_LIB
+      python3 -c "
+import json
+for l in open('$O/h27ab.txt'):
+    v, k, j = l.split(' ', 2); d = json.loads(j)
+    print(v, k, round(d['ms_evaluate'], 3), round(d['ms_element'], 3), round(d['ms_assemble'], 3))" ;;
+    slabprof)  # per-kernel durations of the slab schedule (rocprofv3 kernel trace)
+      for sl in 0 1600 6400; do
+        mkdir -p $O/slabprof_$sl
+        (cd /tmp && FCG_H27_SLAB=$sl timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$O/slabprof_$sl" -o run -- python3 "$GRAFT_REPO_ROOT/$ET" --celltype hex27 --kinem totlag --n 40 --reps 9) > $O/slabprof_$sl.log 2>&1 || { tail -20 $O/slabprof_$sl.log; exit 1; }
+        f=$(find $O/slabprof_$sl -name "*kernel_stats.csv" | head -1)
+        echo "slab=$sl"; grep -E "h27_element|assemble27" "$f" | cut -d, -f1-8
+      done ;;
+    scratch)  # hex27 100^3 TotLag: evaluate time and ring size per slab size
+      for sl in ${SLABS:-0 5000 10000 20000}; do
+        echo "slab=$sl $(FCG_H27_SLAB=$sl timeout -k 10 300 python3 $ET --celltype hex27 --kinem totlag --n 100 --reps 5 | tail -1)" >> $O/scratch.txt || exit 1
+      done
+      python3 -c "
+import json
+for l in open('$O/scratch.txt'):
+    h, j = l.split(' {', 1); d = json.loads('{' + j)
+    print(h, round(d['ms_evaluate'], 2), 'scratch GB', round(d['scratch_bytes'] / 1e9, 3), 'device GB', round(d['device_bytes'] / 1e9, 2))" ;;
+    tests)  # the whole GPU suite
+      run 1500 gpu_tests.log python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests
+      tail -3 $O/gpu_tests.log ;;
+    t:*)  # one test file / node id: t:tests/test_x.py::name
+      run 900 gpu_tests_part.log python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu "${step#t:}"
+      tail -3 $O/gpu_tests_part.log ;;
+    bench)
+      run 900 bench.log python3 bench.py --gpus 1 --steps 20 --warmup 5
+      grep '^{' $O/bench.log | tail -1 > $O/bench.json ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done

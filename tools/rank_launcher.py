@@ -109,6 +109,9 @@ def spawn(cmd, n, environ=None, poll_s=0.2, grace_s=20.0):
                 time.sleep(poll_s)
         return rc
     except _Signalled as e:
+        # a second signal must not interrupt the clean-up either
+        for sig in old:
+            signal.signal(sig, signal.SIG_IGN)
         print(f"rank_launcher: signal {e.signum}; stopping the ranks", file=sys.stderr, flush=True)
         _stop([p for p in procs if p.poll() is None], grace_s)
         return 128 + e.signum
