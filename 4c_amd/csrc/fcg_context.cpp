@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <array>
 #include <climits>
 #include <cstdlib>
@@ -949,6 +950,15 @@ const char* fcg_last_error(const fcg_ctx* ctx)
 
 int fcg_create(const fcg_desc* d, fcg_ctx** out)
 {
+  // phase clock (fcg_get_create_phases)
+  double ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const auto t_start = std::chrono::steady_clock::now();
+  auto t_last = t_start;
+  auto phase = [&](int i) {
+    const auto now = std::chrono::steady_clock::now();
+    ph[i] += std::chrono::duration<double>(now - t_last).count();
+    t_last = now;
+  };
   if (!d || !out) return FCG_ERR_ARG;
   *out = nullptr;
   if (d->abi_version != FCG_ABI_VERSION)
@@ -1017,6 +1027,7 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
       return FCG_ERR_ARG;
     }
   }
+  phase(0);
   fcg_desc dg;
   std::vector<int64_t> g_rowptr;
   std::vector<int32_t> g_col;
@@ -1035,6 +1046,7 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
     d = &dg;
   }
 
+  phase(1);
   // --- owned row nodes, ascending by row LID
   std::vector<int32_t> rownodes;
   for (int64_t n = 0; n < d->n_node; ++n)
@@ -1079,6 +1091,7 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
     return FCG_ERR_ARG;
   }
 
+  phase(2);
   // --- structured (row-block sweep) plan when a verified lattice hint is present
   StructHost sp;
   std::string why;
@@ -1151,6 +1164,7 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
   bool gather = !structured && d->celltype == FCG_HEX8 && d->material == FCG_MAT_STVK &&
                 (d->path == FCG_PATH_GATHER || d->path == FCG_PATH_AUTO);
 
+  phase(3);
   // --- incidences grouped by owned node (general path)
   std::vector<int64_t> inc_ptr(nrn + 1, 0);
   for (int64_t i = 0; i < (structured ? 0 : d->n_ele * npe); ++i)
@@ -1184,6 +1198,7 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
         if (colored) inc_row0[k] = row0[rn];
       }
   }
+  phase(4);
   // --- positions of every element node's DOF triple inside the row (stride fast path)
   std::vector<uint16_t> inc_pos(n_inc * npe);
   parallel_for(structured ? 0 : nrn, [&](int64_t r) {
@@ -1226,6 +1241,7 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
     return FCG_ERR_ARG;
   }
 
+  phase(5);
   // --- device
   fcg_ctx* ctx = new fcg_ctx();
   ctx->device = d->device;
@@ -1525,9 +1541,11 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
       m.h27_increc = !(sym && sym[0] == '1');
       // slab schedule of the incidence records (DeviceMesh::h27_*): FCG_H27_SLAB elements per
       // slab (0 = one slab); by default only when one record per incidence would take more than a
-      // quarter of the device's memory (1M hex27: 53 GB of 288 GB -> one slab; the schedule costs
-      // ~10 % there, measured, but shrinks the scratch to ~1 GB, so that meshes of several million
-      // hex27 elements fit one GPU beside their tangent)
+      // quarter of the device's memory (1M hex27: 53 GB of 288 GB -> one slab).  Measured at 1M
+      // hex27 TotLag: slabs of 5,000 / 10,000 / 20,000 elements keep a ring of 1.18 /
+      // 1.24 / 2.30 GB instead of 53 GB, at 64.5 / 59.9 / 56.9 ms per evaluate instead of 51.5 ms
+      // (every slab boundary drains the element kernel's two-element pipeline), so that meshes of
+      // several million hex27 elements fit one GPU beside their tangent
       const char* sl = std::getenv("FCG_H27_SLAB");
       int64_t S = sl ? std::atoll(sl) : 0;
       int n_cu = 256;
@@ -1546,7 +1564,7 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
       m.h27_el_grid = eg ? std::max(1, std::atoi(eg)) : 2 * n_cu;  // the resident workgroups
       const double full = double(n_inc) * double(fcg::record_doubles(npe)) * sizeof(double);
       if (!sl && mem_total > 0 && full > 0.25 * double(mem_total))
-        S = std::max<int64_t>(8192, d->n_ele / 50);
+        S = std::max<int64_t>(4096, d->n_ele / 200);
       int64_t n_slots = n_inc;
       if (m.h27_increc && S > 0 && S < d->n_ele)
       {
@@ -1584,6 +1602,9 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
     fcg_destroy(ctx);
     return fcg_device_error();
   }
+  phase(6);
+  ph[7] = std::chrono::duration<double>(t_last - t_start).count();
+  for (int i = 0; i < 8; ++i) ctx->create_phase_s[i] = ph[i];
   *out = ctx;
   return FCG_OK;
 }
@@ -1946,6 +1967,13 @@ int fcg_get_diagnostics(const fcg_ctx* ctx, uint64_t* out, int n)
     return fcg_device_error();
   for (int i = 0; i < n && i < 16; ++i) out[i] = v[i];
   return m.stamps ? 16 : 0;
+}
+
+int fcg_get_create_phases(const fcg_ctx* ctx, double* out, int n)
+{
+  if (!ctx || (!out && n > 0)) return FCG_ERR_ARG;
+  for (int i = 0; i < n && i < 8; ++i) out[i] = ctx->create_phase_s[i];
+  return 8;
 }
 
 int fcg_get_info(const fcg_ctx* ctx, fcg_info* info)

@@ -209,6 +209,7 @@ struct fcg_ctx {
   bool async = false;
   bool pending = false;
   hipStream_t pending_stream = nullptr;
+  double create_phase_s[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // fcg_get_create_phases
 };
 
 // fcg_dfcg_solve's AMG preconditioner (fcg_amg_solver.hip; not part of the C ABI): numeric setup

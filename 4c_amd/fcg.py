@@ -128,7 +128,7 @@ class FcgAmgOptions(ctypes.Structure):
 EXPORTS = ["fcg_create", "fcg_destroy", "fcg_last_error", "fcg_evaluate", "fcg_evaluate_device",
            "fcg_device_alloc", "fcg_device_free", "fcg_memcpy_h2d", "fcg_memcpy_d2h",
            "fcg_memset_device", "fcg_set_timing", "fcg_get_timing", "fcg_get_info",
-           "fcg_get_diagnostics", "fcg_measure_peaks", "fcg_measure_hbm", "fcg_spmv", "fcg_dirichlet_apply",
+           "fcg_get_diagnostics", "fcg_get_create_phases", "fcg_measure_peaks", "fcg_measure_hbm", "fcg_spmv", "fcg_dirichlet_apply",
            "fcg_pcg_solve", "fcg_spmv_f32", "fcg_tangent_apply", "fcg_box_stencil_apply", "fcg_box_transfer", "fcg_block_jacobi_setup", "fcg_block_jacobi_apply", "fcg_chebyshev_step", "fcg_node_transfer",
            "fcg_neumann_surface", "fcg_neumann_volume",
            "fcg_graph_build_device", "fcg_get_graph",
@@ -191,6 +191,7 @@ def lib():
     L.fcg_get_timing.argtypes = [vp, _dp, _dp]
     L.fcg_get_info.argtypes = [vp, ctypes.POINTER(FcgInfo)]
     L.fcg_get_diagnostics.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
+    L.fcg_get_create_phases.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
     L.fcg_spmv.argtypes = [vp, vp, vp, vp, vp]
     L.fcg_measure_peaks.argtypes = [ctypes.c_int, _dp, _dp, _dp]
     L.fcg_measure_hbm.argtypes = [ctypes.c_int, _dp, _dp]
@@ -756,6 +757,15 @@ class Evaluator:
         buf = (ctypes.c_uint64 * 16)()
         n = lib().fcg_get_diagnostics(self._h, buf, 16)
         return list(buf) if n > 0 else None
+
+    CREATE_PHASES = ("checks", "graph_device", "node_rows", "lattice_plans", "incidences",
+                     "incidence_positions", "device_plans", "total")
+
+    def create_phases(self):
+        """fcg_create's phase wall times (s) by name (fcg_get_create_phases)."""
+        buf = (ctypes.c_double * 8)()
+        lib().fcg_get_create_phases(self._h, buf, 8)
+        return dict(zip(self.CREATE_PHASES, list(buf)))
 
     def timing(self):
         a, b = ctypes.c_double(), ctypes.c_double()

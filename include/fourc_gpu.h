@@ -200,6 +200,14 @@ int fcg_measure_hbm(int device, double* copy_gbs, double* write_gbs);
  * kernel's layout is in fcg_hex27.hip.  Returns the number of counters (0 when off). */
 int fcg_get_diagnostics(const fcg_ctx* ctx, uint64_t* out, int n);
 
+/* Wall time (seconds) of fcg_create's phases, the setup counterpart of 4C's FillComplete and
+ * DofSet numbering (4C_linalg_sparsematrix.cpp:843-865, 4C_fem_dofset.cpp:128-366): out[i] for
+ * i < n of 0 checks, 1 graph on the device (rowptr = col_lid = NULL), 2 node rows and their CSR
+ * pattern, 3 lattice / colour plans, 4 incidences, 5 incidence column positions, 6 device
+ * buffers and path plans (uploads, Morton orders, gather records, hex27 ring), 7 total.
+ * Returns the number of phases (8). */
+int fcg_get_create_phases(const fcg_ctx* ctx, double* out, int n);
+
 /* ------------------------------------------------------------------------------------------
  * Around the assembly: what one Newton step of Solid statics needs on the device
  * (NOX full Newton, 4C_solver_nonlin_nox_linearsystem.cpp:275-353, with the structure's

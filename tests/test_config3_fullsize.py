@@ -36,10 +36,10 @@ def _straddling_row(rowptr, offset):
     return int(np.searchsorted(rowptr, offset, side="right") - 1)
 
 
-@pytest.mark.parametrize("slab", [0, 20000])
+@pytest.mark.parametrize("slab", [0, 5000])
 def test_config3_rows_past_int32_offsets_against_oracle(monkeypatch, slab):
-    """slab 20000: the slab schedule of the incidence records -- the records live in
-    a ring of about 1 GB instead of one 1,968-byte record per incidence (53 GB)."""
+    """slab 5000: the slab schedule of the incidence records -- the records live in
+    a ring of 1.18 GB instead of one 1,968-byte record per incidence (53 GB)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     monkeypatch.setenv("FCG_H27_SLAB", str(slab))
@@ -51,7 +51,7 @@ def test_config3_rows_past_int32_offsets_against_oracle(monkeypatch, slab):
     u = mesh.u_col(5e-2)
     ev = fcg.Evaluator(mesh, kinematics=fcg.TOTLAG, youngs=E, poisson=NU)
     if slab and N == 100:
-        assert ev.info.scratch_bytes < 1e9, ev.info.scratch_bytes
+        assert ev.info.scratch_bytes < 1.25e9, ev.info.scratch_bytes
     f = torch.zeros(mesh.n_rows, dtype=torch.float64, device=dev)
     K = torch.full((mesh.nnz,), float("nan"), dtype=torch.float64, device=dev)
     u_d = torch.from_numpy(u).to(dev)

@@ -74,9 +74,13 @@ if a.renumber:
     f2[newrow] = fext
     fext = f2
     dbc = np.sort(newrow[dbc]).astype(np.int32)
-print(f"mesh {time.perf_counter() - t0:.1f} s: {mesh.n_ele} elements, {mesh.nnz} nonzeros", file=sys.stderr, flush=True)
+t_mesh = time.perf_counter() - t0
+print(f"mesh {t_mesh:.1f} s: {mesh.n_ele} elements, {mesh.nnz} nonzeros", file=sys.stderr, flush=True)
 ev = fcg.Evaluator(mesh, kinematics=kin, youngs=210.0, poisson=0.3, path=path)
 t_setup = time.perf_counter() - t0
+setup_phases = {"mesh_s": t_mesh, "create_s": t_setup - t_mesh,
+                "create_phases_s": ev.create_phases()}
+print(f"fcg_create {t_setup - t_mesh:.1f} s: {json.dumps(setup_phases['create_phases_s'])}", file=sys.stderr, flush=True)
 
 
 class Timed(newton.StaticNewton):
@@ -138,6 +142,7 @@ if a.mg:
         fine_post=not a.mg_no_fine_post, matrix_free=a.mg_matrix_free,
         outer_matrix_free=a.mg_outer_matrix_free,
         **({"ratio": a.mg_ratio} if a.mg_ratio else {}))
+    setup_phases["multigrid_s"] = time.perf_counter() - t_mg
     print(f"multigrid setup {time.perf_counter() - t_mg:.1f} s: {json.dumps(mg.describe())}",
           file=sys.stderr, flush=True)
     t_setup = time.perf_counter() - t0
@@ -148,6 +153,7 @@ if a.amg or a.amg_native:
     mg = (amg_mod.NativeAMG(mesh, ev, dbc, nu=a.mg_nu, **kw) if a.amg_native
           else amg_mod.AMG(mesh, ev, dbc, nu=a.mg_nu, **kw))
     t_amg_setup = time.perf_counter() - t_mg
+    setup_phases["amg_s"] = t_amg_setup
     print(f"AMG setup (host graph) {t_amg_setup:.1f} s: {json.dumps(mg.describe())}",
           file=sys.stderr, flush=True)
     t_setup = time.perf_counter() - t0
@@ -183,7 +189,7 @@ out = {"config": f"{a.celltype}-{a.kinem}-{a.n}^3-cantilever", "forcing": a.forc
                          "block-Jacobi PCG"),
        "mesh": "renumbered (input-file order, no lattice)" if a.renumber else "GridGenerator box",
        "mg_levels": mg.describe() if mg else None, "elements": mesh.n_ele,
-       "dofs": mesh.n_rows, "nnz": mesh.nnz, "setup_s": t_setup, "newton_s": t_newton,
+       "dofs": mesh.n_rows, "nnz": mesh.nnz, "setup_s": t_setup, "setup_phases": setup_phases, "newton_s": t_newton,
        "newton_iterations": len(h) - 1,
        "assembly_ms_mean": float(np.mean([r["assembly_ms"] for r in h])),
        "assembly_elem_per_s": mesh.n_ele / (1e-3 * float(np.median([r["assembly_ms"] for r in h]))),
