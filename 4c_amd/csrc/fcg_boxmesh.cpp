@@ -12,7 +12,12 @@
 //   matrix graph: row = owned DOF, columns = DOFs of every node sharing an element, column map
 //                 ordered like Epetra's FillComplete (own DOFs first, then remote by owner, gid)
 #include <algorithm>
+#include <sys/mman.h>
+
 #include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <thread>
@@ -96,6 +101,48 @@ void parallel_for(int64_t n, F f)
   for (auto& t : th) t.join();
 }
 
+// std::vector without value-initialisation (the CSR arrays are written in full right after
+// their allocation: no serial zero-fill of 18.5 GB of column indices at 1M hex27)
+template <class T>
+struct DefaultInitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = DefaultInitAlloc<U>;
+  };
+  using std::allocator<T>::allocator;
+  // large arrays on transparent huge pages where the kernel offers them (madvise mode): the
+  // first-touch page faults of 18.5 GB of column indices dominate the graph fill otherwise
+  T* allocate(std::size_t n)
+  {
+    const std::size_t bytes = n * sizeof(T);
+    if (bytes < (std::size_t(64) << 20)) return std::allocator<T>::allocate(n);
+    constexpr std::size_t kHuge = std::size_t(2) << 20;
+    void* p = std::aligned_alloc(kHuge, (bytes + kHuge - 1) / kHuge * kHuge);
+    if (!p) throw std::bad_alloc();
+    (void)madvise(p, bytes, MADV_HUGEPAGE);
+    return static_cast<T*>(p);
+  }
+  void deallocate(T* p, std::size_t n)
+  {
+    if (n * sizeof(T) < (std::size_t(64) << 20))
+      std::allocator<T>::deallocate(p, n);
+    else
+      std::free(p);
+  }
+  template <class U>
+  void construct(U* p) noexcept
+  {
+    ::new (static_cast<void*>(p)) U;
+  }
+  template <class U, class... A>
+  void construct(U* p, A&&... a)
+  {
+    ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+  }
+};
+template <class T>
+using RawVec = std::vector<T, DefaultInitAlloc<T>>;
+
 }  // namespace
 
 struct fcg_box_mesh {
@@ -108,8 +155,8 @@ struct fcg_box_mesh {
   std::vector<int64_t> node_gid;
   std::vector<int32_t> node_owner, node_dof_col, node_dof_row;
   std::vector<int32_t> row_gid, col_gid;
-  std::vector<int64_t> rowptr;
-  std::vector<int32_t> col_lid;
+  RawVec<int64_t> rowptr;
+  RawVec<int32_t> col_lid;
 };
 
 extern "C" {
@@ -131,6 +178,14 @@ int fcg_box_mesh_create_ex(const fcg_box* box, int rank, int nranks, int flags, 
   std::vector<Section> secs;
   if (!box_sections(box->interval, nranks, secs)) return FCG_ERR_ARG;
 
+  const bool tmr = std::getenv("FCG_BOX_TIMING") != nullptr;
+  auto t_prev = std::chrono::steady_clock::now();
+  auto tick = [&](const char* what) {
+    if (!tmr) return;
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "box %-12s %.3f s\n", what, std::chrono::duration<double>(now - t_prev).count());
+    t_prev = now;
+  };
   auto* m = new fcg_box_mesh();
   m->box = *box;
   m->rank = rank;
@@ -170,62 +225,98 @@ int fcg_box_mesh_create_ex(const fcg_box* box, int rank, int nranks, int flags, 
     clo[d] = strict ? my.lo[d] : std::max<int64_t>(0, my.lo[d] - 1);
     chi[d] = strict ? my.hi[d] : std::min<int64_t>(box->interval[d], my.hi[d] + 1);
   }
+  const int64_t cex = std::max<int64_t>(0, chi[0] - clo[0]), cey = std::max<int64_t>(0, chi[1] - clo[1]),
+                cez = std::max<int64_t>(0, chi[2] - clo[2]);
+  std::vector<uint8_t> has(cex * cey * cez, strict ? 1 : 0);
+  if (!strict)
+    parallel_for(cex * cey * cez, [&](int64_t c) {
+      const int64_t ex = clo[0] + c % cex, ey = clo[1] + (c / cex) % cey, ez = clo[2] + c / (cex * cey);
+      bool h = false;
+      for (int a = 0; a < npe && !h; ++a)
+        h = owner_of(2 * ex + off27[a][0], 2 * ey + off27[a][1], 2 * ez + off27[a][2]) == rank;
+      has[c] = h ? 1 : 0;
+    });
   std::vector<int64_t> col_ele;
-  for (int64_t ez = clo[2]; ez < chi[2]; ++ez)
-    for (int64_t ey = clo[1]; ey < chi[1]; ++ey)
-      for (int64_t ex = clo[0]; ex < chi[0]; ++ex)
-      {
-        bool has = strict;
-        for (int a = 0; a < npe && !has; ++a)
-          has = owner_of(2 * ex + off27[a][0], 2 * ey + off27[a][1], 2 * ez + off27[a][2]) == rank;
-        if (has) col_ele.push_back((ez * IY + ey) * IX + ex);
-      }
+  for (int64_t c = 0; c < cex * cey * cez; ++c)
+    if (has[c])
+    {
+      const int64_t ex = clo[0] + c % cex, ey = clo[1] + (c / cex) % cey, ez = clo[2] + c / (cex * cey);
+      col_ele.push_back((ez * IY + ey) * IX + ex);
+    }
   const int64_t nce = int64_t(col_ele.size());
+  tick("elements");
 
-  // column nodes: lattice index -> local id
-  std::vector<int64_t> lat;  // lattice linear index of every node touched
-  lat.reserve(nce * npe);
-  for (int64_t e : col_ele)
-  {
+  // column nodes: the lattice nodes of the column elements, marked in the node box of the grown
+  // section and enumerated in lattice (GID) order
+  const int64_t bx = 2 * cex + 1, by = 2 * cey + 1, bz = 2 * cez + 1;
+  const int64_t bn = nce > 0 ? bx * by * bz : 0;
+  std::vector<uint8_t> used(bn, 0);
+  auto box_of = [&](int64_t e, int a) -> int64_t {
     const int64_t ex = e % IX, ey = (e / IX) % IY, ez = e / (IX * IY);
+    return ((2 * (ez - clo[2]) + off27[a][2]) * by + 2 * (ey - clo[1]) + off27[a][1]) * bx +
+           2 * (ex - clo[0]) + off27[a][0];
+  };
+  // distinct elements may mark the same node: relaxed byte stores of the same value
+  parallel_for(nce, [&](int64_t i) {
     for (int a = 0; a < npe; ++a)
-      lat.push_back(((2 * ez + off27[a][2]) * NY + 2 * ey + off27[a][1]) * NX + 2 * ex + off27[a][0]);
-  }
-  std::vector<int64_t> uniq(lat);
-  std::sort(uniq.begin(), uniq.end());
-  uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
-  const int64_t ncn = int64_t(uniq.size());
+      reinterpret_cast<std::atomic<uint8_t>*>(used.data())[box_of(col_ele[i], a)].store(1, std::memory_order_relaxed);
+  });
+  std::vector<int64_t> plane_cnt(bz + 1, 0);
+  parallel_for(bz, [&](int64_t k) {
+    int64_t c = 0;
+    for (int64_t q = k * bx * by; q < (k + 1) * bx * by; ++q) c += used[q];
+    plane_cnt[k + 1] = c;
+  });
+  for (int64_t k = 0; k < bz; ++k) plane_cnt[k + 1] += plane_cnt[k];
+  const int64_t ncn = plane_cnt[bz];
+  std::vector<int64_t> uniq(ncn);   // lattice linear index of every column node, ascending
+  std::vector<int32_t> slot(bn, -1);  // node box position -> index into uniq
+  parallel_for(bz, [&](int64_t k) {
+    int64_t w = plane_cnt[k];
+    for (int64_t q = k * bx * by; q < (k + 1) * bx * by; ++q)
+      if (used[q])
+      {
+        const int64_t i = q % bx, j = (q / bx) % by;
+        uniq[w] = ((2 * clo[2] + k) * NY + 2 * clo[1] + j) * NX + 2 * clo[0] + i;
+        slot[q] = int32_t(w++);
+      }
+  });
+  tick("nodes");
   std::vector<int32_t> own(ncn);
-  for (int64_t n = 0; n < ncn; ++n)
-  {
+  parallel_for(ncn, [&](int64_t n) {
     const int64_t L = uniq[n];
     own[n] = owner_of(L % NX, (L / NX) % NY, L / (NX * NY));
-  }
-  // order: owned by gid, then ghosts by (owner, gid)  (Epetra column-map order)
-  std::vector<int64_t> order(ncn);
-  for (int64_t n = 0; n < ncn; ++n) order[n] = n;
-  std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
-    const int oa = own[a] == rank ? -1 : own[a], ob = own[b] == rank ? -1 : own[b];
-    if (oa != ob) return oa < ob;
-    return uniq[a] < uniq[b];
   });
+  // order: owned by gid, then ghosts by (owner, gid)  (Epetra column-map order): a stable
+  // counting sort by owner class of the gid-ordered nodes
+  std::vector<int64_t> cls_ptr(nranks + 2, 0);
+  for (int64_t n = 0; n < ncn; ++n) cls_ptr[(own[n] == rank ? 0 : own[n] + 1) + 1]++;
+  for (int q = 0; q <= nranks; ++q) cls_ptr[q + 1] += cls_ptr[q];
+  std::vector<int64_t> order(ncn);
   std::vector<int32_t> newid(ncn);
-  for (int64_t i = 0; i < ncn; ++i) newid[order[i]] = int32_t(i);
+  {
+    std::vector<int64_t> fill(cls_ptr.begin(), cls_ptr.end() - 1);
+    for (int64_t n = 0; n < ncn; ++n)
+    {
+      const int64_t i = fill[own[n] == rank ? 0 : own[n] + 1]++;
+      order[i] = n;
+      newid[n] = int32_t(i);
+    }
+  }
 
   m->node_gid.resize(ncn);
   m->node_owner.resize(ncn);
   m->node_x.resize(3 * ncn);
   m->node_dof_col.resize(ncn);
   m->node_dof_row.resize(ncn, -1);
-  int64_t n_owned = 0;
-  for (int64_t i = 0; i < ncn; ++i)
-  {
+  const int64_t n_owned = cls_ptr[1];
+  parallel_for(ncn, [&](int64_t i) {
     const int64_t n = order[i];
     const int64_t L = uniq[n];
     m->node_gid[i] = box->first_node_gid + L;
     m->node_owner[i] = own[n];
     m->node_dof_col[i] = int32_t(3 * i);
-    if (own[n] == rank) m->node_dof_row[i] = int32_t(3 * n_owned++);
+    if (own[n] == rank) m->node_dof_row[i] = int32_t(3 * i);  // owned nodes come first, in gid order
     else if (strict) m->node_dof_row[i] = int32_t(3 * i);  // extended row (owned nodes come first)
     // coordinates (4C_io_gridgenerator.cpp:283-317)
     const int64_t ii = L % NX, jj = (L / NX) % NY, kk = L / (NX * NY);
@@ -259,85 +350,109 @@ int fcg_box_mesh_create_ex(const fcg_box* box, int rank, int nranks, int flags, 
       c[ax] += dx[ax];
     }
     for (int d = 0; d < 3; ++d) m->node_x[3 * i + d] = c[d];
-  }
+  });
+  tick("node data");
   // element connectivity in local column-node ids
   m->ele_nodes.resize(nce * npe);
   m->ele_gid.resize(nce);
   m->ele_ijk.resize(3 * nce);
-  for (int64_t e = 0; e < nce; ++e)
-  {
+  parallel_for(nce, [&](int64_t e) {
     // lattice position of the element (4C_io_gridgenerator.cpp:336-338)
     m->ele_ijk[3 * e + 0] = int32_t(col_ele[e] % IX);
     m->ele_ijk[3 * e + 1] = int32_t((col_ele[e] / IX) % IY);
     m->ele_ijk[3 * e + 2] = int32_t(col_ele[e] / (IX * IY));
-  }
-  for (int64_t e = 0; e < nce; ++e)
-  {
     m->ele_gid[e] = int32_t(col_ele[e]);
-    for (int a = 0; a < npe; ++a)
-    {
-      const int64_t L = lat[e * npe + a];
-      const int64_t n = std::lower_bound(uniq.begin(), uniq.end(), L) - uniq.begin();
-      m->ele_nodes[e * npe + a] = newid[n];
-    }
-  }
+    for (int a = 0; a < npe; ++a) m->ele_nodes[e * npe + a] = newid[slot[box_of(col_ele[e], a)]];
+  });
   m->n_owned_rows = 3 * n_owned;
   // rows: the owned nodes, plus (strict) the extended rows of every other touched node
   const int64_t n_rn = strict ? ncn : n_owned;
   // dof gids of the maps
   m->row_gid.resize(3 * n_rn);
   m->col_gid.resize(3 * ncn);
-  for (int64_t i = 0; i < ncn; ++i)
-  {
+  parallel_for(ncn, [&](int64_t i) {
     const int64_t dof0 = 3 * (m->node_gid[i] - box->first_node_gid);
     for (int d = 0; d < 3; ++d) m->col_gid[3 * i + d] = int32_t(dof0 + d);
     if (m->node_dof_row[i] >= 0)
       for (int d = 0; d < 3; ++d) m->row_gid[m->node_dof_row[i] + d] = int32_t(dof0 + d);
-  }
-  // graph: row node -> incident column elements -> neighbour nodes
-  std::vector<int64_t> adj_ptr(n_rn + 1, 0);
-  for (int64_t i = 0; i < nce * npe; ++i)
-  {
-    const int32_t n = m->ele_nodes[i];
-    if (n < n_rn) adj_ptr[n + 1]++;  // row nodes are the first n_rn local ids
-  }
-  for (int64_t n = 0; n < n_rn; ++n) adj_ptr[n + 1] += adj_ptr[n];
-  std::vector<int32_t> adj(adj_ptr[n_rn]);
-  {
-    std::vector<int64_t> fill(adj_ptr.begin(), adj_ptr.end() - 1);
-    for (int64_t e = 0; e < nce; ++e)
-      for (int a = 0; a < npe; ++a)
-      {
-        const int32_t n = m->ele_nodes[e * npe + a];
-        if (n < n_rn) adj[fill[n]++] = int32_t(e);
-      }
-  }
-  std::vector<int32_t> nnb(n_rn);
-  std::vector<std::vector<int32_t>> nb(n_rn);
-  parallel_for(n_rn, [&](int64_t n) {
-    std::vector<int32_t>& v = nb[n];
-    v.reserve(8 * npe);
-    for (int64_t k = adj_ptr[n]; k < adj_ptr[n + 1]; ++k)
-      for (int a = 0; a < npe; ++a) v.push_back(m->ele_nodes[int64_t(adj[k]) * npe + a]);
-    std::sort(v.begin(), v.end());
-    v.erase(std::unique(v.begin(), v.end()), v.end());
-    nnb[n] = int32_t(v.size());
   });
+  tick("connectivity");
+  // graph (the FillComplete'd Epetra graph of the owned / extended rows): the column elements
+  // holding a row node are the elements of the candidate box whose node box holds the node's
+  // lattice position -- a box of elements per node, all of them column elements (a row node is
+  // owned, so every element touching it is a column element; strict: the section's elements),
+  // and the node's neighbours are the lattice nodes of those elements' node boxes (hex8: the
+  // even positions, its corners).  Rows list them in column-LID order; with ghosts the LIDs are
+  // not in lattice order and each list is sorted.
+  std::vector<int64_t> pos_of(ncn);  // node box position of uniq index w
+  parallel_for(bn, [&](int64_t q) {
+    if (slot[q] >= 0) pos_of[slot[q]] = q;
+  });
+  const bool sorted_lids = ncn == n_owned;  // no ghosts: column LIDs follow the lattice order
+  const int step = h27 ? 1 : 2;
+  // neighbour LIDs of row node n into nbr (returns the count), the candidate element box checked
+  auto neighbours = [&](int64_t n, int32_t* nbr) -> int {
+    const int64_t q = pos_of[order[n]];
+    const int64_t p[3] = {q % bx, (q / bx) % by, q / (bx * by)};
+    const int64_t ce[3] = {cex, cey, cez};
+    int64_t lo[3], hi[3];
+    for (int d = 0; d < 3; ++d)
+    {
+      const int64_t elo = std::max<int64_t>(0, (p[d] - 1) / 2), ehi = std::min<int64_t>(ce[d] - 1, p[d] / 2);
+      lo[d] = 2 * elo;
+      hi[d] = 2 * ehi + 2;
+    }
+    int c = 0;
+    for (int64_t k = lo[2]; k <= hi[2]; k += step)
+      for (int64_t j = lo[1]; j <= hi[1]; j += step)
+        for (int64_t i = lo[0]; i <= hi[0]; i += step)
+          nbr[c++] = newid[slot[(k * by + j) * bx + i]];
+    if (!sorted_lids) std::sort(nbr, nbr + c);
+    return c;
+  };
+  // every element of a row node's element box must be a column element (else the lattice rule
+  // above does not describe the graph)
+  std::atomic<bool> box_ok{true};
+  std::vector<int32_t> nnb(n_rn);
+  parallel_for(n_rn, [&](int64_t n) {
+    const int64_t q = pos_of[order[n]];
+    const int64_t p[3] = {q % bx, (q / bx) % by, q / (bx * by)};
+    const int64_t ce[3] = {cex, cey, cez};
+    int64_t elo[3], ehi[3], cnt = 1;
+    for (int d = 0; d < 3; ++d)
+    {
+      elo[d] = std::max<int64_t>(0, (p[d] - 1) / 2);
+      ehi[d] = std::min<int64_t>(ce[d] - 1, p[d] / 2);
+      cnt *= (2 * (ehi[d] - elo[d]) + 2) / step + 1;
+    }
+    for (int64_t ez = elo[2]; ez <= ehi[2]; ++ez)
+      for (int64_t ey = elo[1]; ey <= ehi[1]; ++ey)
+        for (int64_t ex = elo[0]; ex <= ehi[0]; ++ex)
+          if (!has[(ez * cey + ey) * cex + ex]) box_ok.store(false, std::memory_order_relaxed);
+    nnb[n] = int32_t(cnt);
+  });
+  if (!box_ok.load())
+  {
+    delete m;
+    return FCG_ERR_ARG;  // not reached for GridGenerator sections
+  }
+  tick("neighbours");
   m->rowptr.resize(3 * n_rn + 1);
   m->rowptr[0] = 0;
   for (int64_t n = 0; n < n_rn; ++n)
     for (int d = 0; d < 3; ++d) m->rowptr[3 * n + d + 1] = m->rowptr[3 * n + d] + 3 * int64_t(nnb[n]);
   m->col_lid.resize(m->rowptr[3 * n_rn]);
   parallel_for(n_rn, [&](int64_t n) {
-    const std::vector<int32_t>& v = nb[n];
+    int32_t v[125];
+    const int c = neighbours(n, v);
     for (int d = 0; d < 3; ++d)
     {
-      int32_t* c = m->col_lid.data() + m->rowptr[3 * n + d];
-      for (size_t k = 0; k < v.size(); ++k)
-        for (int j = 0; j < 3; ++j) c[3 * k + j] = 3 * v[k] + j;  // node_dof_col == 3 * local id
+      int32_t* cl = m->col_lid.data() + m->rowptr[3 * n + d];
+      for (int k = 0; k < c; ++k)
+        for (int j = 0; j < 3; ++j) cl[3 * k + j] = 3 * v[k] + j;  // node_dof_col == 3 * local id
     }
-    std::vector<int32_t>().swap(nb[n]);
   });
+  tick("csr");
   *out = m;
   return FCG_OK;
 }

@@ -191,7 +191,8 @@ def lib():
     L.fcg_get_timing.argtypes = [vp, _dp, _dp]
     L.fcg_get_info.argtypes = [vp, ctypes.POINTER(FcgInfo)]
     L.fcg_get_diagnostics.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
-    L.fcg_get_create_phases.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
+    if hasattr(L, "fcg_get_create_phases"):  # absent from older A/B builds (FCG_LIB)
+        L.fcg_get_create_phases.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
     L.fcg_spmv.argtypes = [vp, vp, vp, vp, vp]
     L.fcg_measure_peaks.argtypes = [ctypes.c_int, _dp, _dp, _dp]
     L.fcg_measure_hbm.argtypes = [ctypes.c_int, _dp, _dp]
@@ -507,6 +508,18 @@ def _tensor_ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
+class _NativeBoxMesh:
+    """Owner of an fcg_box_mesh: destroyed when the last numpy view of its arrays goes."""
+
+    def __init__(self, h):
+        self.h = h
+
+    def __del__(self):
+        if self.h:
+            lib().fcg_box_mesh_destroy(self.h)
+            self.h = None
+
+
 class BoxMesh:
     """One rank of a GridGenerator box (the fcg_box_mesh_* builder), as numpy views."""
 
@@ -542,10 +555,17 @@ class BoxMesh:
         self.n_ele, self.n_node = d.n_ele, d.n_node
         self.n_rows, self.n_cols = d.n_rows, d.n_cols
 
+        # zero-copy views of the builder's arrays; the native mesh is released when the last
+        # view is (a 1M-hex27 box holds 18.5 GB of column indices: no second copy)
+        keeper = _NativeBoxMesh(h)
+        ctype_of = {np.int32: ctypes.c_int32, np.int64: ctypes.c_int64, np.float64: ctypes.c_double}
+
         def view(p, n, dt):
             if n == 0:
                 return np.zeros(0, dtype=dt)
-            return np.ctypeslib.as_array(p, shape=(n,)).astype(dt, copy=True)
+            buf = (ctype_of[dt] * n).from_address(ctypes.cast(p, ctypes.c_void_p).value)
+            buf._keep = keeper
+            return np.frombuffer(buf, dtype=dt)
 
         self.ele_nodes = view(d.ele_nodes, d.n_ele * self.npe, np.int32).reshape(-1, self.npe)
         self.ele_gid = view(d.ele_gid, d.n_ele, np.int32)
@@ -568,9 +588,7 @@ class BoxMesh:
         no_ = ctypes.c_int64()
         L.fcg_box_mesh_owned_rows(h, ctypes.byref(no_))
         self.n_owned_rows = no_.value
-        # the builder's arrays are copied; release the native mesh
-        L.fcg_box_mesh_destroy(h)
-        self._h = None
+        self._h = None  # owned by the views' keeper
 
     def desc(self, kinematics, youngs, poisson, device=0, path=PATH_AUTO, material=MAT_STVK):
         d = FcgDesc()
