@@ -701,7 +701,9 @@ class Multigrid(CycleFCG):
             del zc
         self.P, self.R, self.BT = [], [], []
         prev = fine_mesh
+        tmr = bool(os.environ.get("FCG_MG_SETUP_TIMING"))
         for ivc in meshes:
+            t_l = time.perf_counter()
             m = fcg.BoxMesh(fcg.HEX8, ivc, lower=lower, upper=upper, rotation=rot,
                             first_node_gid=int(box.first_node_gid))
             ev = fcg.Evaluator(m, kinematics=fcg.LINEAR, youngs=youngs, poisson=poisson,
@@ -718,11 +720,9 @@ class Multigrid(CycleFCG):
             # its 27-point stencil instead of reading K (FCG_MG_STENCIL=0: the assembled K)
             if os.environ.get("FCG_MG_STENCIL", "1") != "0" and min(ivc) >= 1:
                 lvl.stencil = box_stencil(m, youngs, poisson, dev, rows)
-            P, R = transfer_tables(prev, m)
-            self.P.append(_Transfer(P, dev))
-            self.R.append(_Transfer(R, dev))
             # a 2:1 pair (hex27 -> hex8 on the same elements, hex8 n -> n/2): weights implicit
-            # (FCG_MG_BOXT=0: the tables)
+            # (FCG_MG_BOXT=0: the tables); the node-block tables only where that does not apply
+            # (at 1M hex27 they took most of this setup's time, unused)
             bt = None
             if os.environ.get("FCG_MG_BOXT", "1") != "0":
                 try:
@@ -730,10 +730,23 @@ class Multigrid(CycleFCG):
                 except ValueError:
                     bt = None
             self.BT.append(bt)
+            if bt is None:
+                P, R = transfer_tables(prev, m)
+                self.P.append(_Transfer(P, dev))
+                self.R.append(_Transfer(R, dev))
+            else:
+                self.P.append(None)
+                self.R.append(None)
             self.levels.append(lvl)
             prev = m
+            if tmr:
+                torch.cuda.synchronize()
+                print(f"  multigrid level {ivc}: {time.perf_counter() - t_l:.2f} s", file=sys.stderr, flush=True)
+        t_l = time.perf_counter()
         for lvl in self.levels[1:-1]:
             lvl.estimate_lmax()
+        if tmr:
+            print(f"  multigrid lambda_max estimates: {time.perf_counter() - t_l:.2f} s", file=sys.stderr, flush=True)
         # coarsest level: its rediscretised linear operator does not change between tangents, so
         # it is factored once -- "dense": the inverse of the (small) matrix, one matrix-vector
         # product per V-cycle, exact and without the host round trips of an iterative solve;
