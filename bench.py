@@ -313,7 +313,15 @@ def cpu_topology():
     return out
 
 
-def newton_secondary(n, timeout_s=900):
+# the matrix-free hex27 action (fcg_tangent_apply) per element and application, algorithmic
+# bytes: the element's 27 nodes' X, u and x (3 x 81 doubles) and 27 DOF column indices read, the
+# 81 incidence values written and read back once by the row-node sum, 81 values of y written
+# (every value counted once per element: the minimum traffic of an element-by-element action
+# without cross-element reuse)
+ALG_BYTES_PER_ELE_H27_APPLY = 8.0 * 3 * 81 + 4.0 * 27 + 8.0 * 81 * 2 + 8.0 * 81
+
+
+def newton_secondary(n, timeout_s=900, cpu_rate=None):
     """BASELINE config 3: StVK TotLag on the 1M-hex27 cube (x- clamped, traction -1 in z on x+),
     full static Newton on this GPU (fcg_evaluate_device + Dirichlet + multigrid-preconditioned
     flexible CG, 4c_amd/newton.py + multigrid.py; the fine level's smoother and the outer FCG apply
@@ -341,10 +349,36 @@ def newton_secondary(n, timeout_s=900):
         "linear_solver": d["linear_solver"], "forcing": d["forcing"],
         "norm_res": [h["norm_res"] for h in d["history"]],
         "assembly_ms_mean": d["assembly_ms_mean"], "assembly_elem_per_s": d["assembly_elem_per_s"],
-        "solve_ms_total": d["solve_ms_total"], "setup_s": d["setup_s"], "wall_s": wall,
+        "solve_ms_total": d["solve_ms_total"], "setup_s": d["setup_s"],
+        "setup_phases": d.get("setup_phases"), "wall_s": wall,
         "elements": d["elements"], "dofs": d["dofs"], "nnz": d["nnz"], "tip_uz": d["tip_uz"],
         "tangent_symmetry_rel": d.get("tangent_symmetry_rel"),
     }
+    # the loop's two device phases against the HBM roof: the K + r assembly of every Newton
+    # iteration (SURVEY §8d's 37,695 B per hex27 element) and the matrix-free tangent action the
+    # solve applies (ALG_BYTES_PER_ELE_H27_APPLY per element)
+    ne = d["elements"]
+    asm = float(np.median(d["assembly_ms"])) if d.get("assembly_ms") else d["assembly_ms_mean"]
+    gbs = ALG_BYTES_PER_ELE_H27 * ne / (asm * 1e-3) / 1e9
+    rl = {"bound": "hbm", "kernel": "assembly: h27_element_kernel + assemble27_kernel",
+          "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+          "alg_bytes_per_element": ALG_BYTES_PER_ELE_H27, "ms_assembly_median": asm}
+    if d.get("tangent_apply_ms"):
+        ag = ALG_BYTES_PER_ELE_H27_APPLY * ne / (d["tangent_apply_ms"] * 1e-3) / 1e9
+        rl["tangent_apply"] = {"kernel": "h27_apply_sf_kernel + h27_inc_sum_kernel (fcg_tangent_apply)",
+                               "ms": d["tangent_apply_ms"], "achieved": ag, "unit": "GB/s",
+                               "frac": ag / HBM_PEAK_GBS,
+                               "alg_bytes_per_element": ALG_BYTES_PER_ELE_H27_APPLY}
+    out["roofline"] = rl
+    if cpu_rate:
+        # the CPU leg: the oracle's K + r assembly rate of the hex27 line (a bounded slab), scaled
+        # to this loop's assemblies; the reference's CPU solve (Belos + MueLu, not vendored) has no
+        # counterpart in the oracle and is not timed
+        nasm = len(d.get("assembly_ms") or []) or (d["newton_iterations"] + 1)
+        out["cpu_baseline"] = dict(cpu_rate, kind="port",
+                                   assembly_s_per_newton_loop_extrapolated=nasm * ne / cpu_rate["value"],
+                                   note="assembly only: the oracle has no CPU linear solve")
+    return out
 
 
 def amg_newton_secondary(n, timeout_s=600):
@@ -364,7 +398,7 @@ def amg_newton_secondary(n, timeout_s=600):
     d = json.loads(p.stdout.strip().splitlines()[-1])
     if not d.get("converged"):
         return {"workload": name, "error": "Newton did not converge"}
-    return {
+    out = {
         "workload": name,
         "baseline_config": "BASELINE.json configs[1] mesh without lattice, full Newton (SURVEY §8f row 2)",
         "value": d["newton_s"], "unit": "s (Newton loop, setup excluded)", "higher_is_better": False,
@@ -374,7 +408,17 @@ def amg_newton_secondary(n, timeout_s=600):
         "assembly_ms_mean": d["assembly_ms_mean"], "solve_ms_total": d["solve_ms_total"],
         "norm_res": [h["norm_res"] for h in d["history"]], "wall_s": wall,
         "elements": d["elements"], "dofs": d["dofs"], "nnz": d["nnz"],
+        "setup_phases": d.get("setup_phases"),
     }
+    # the K + r assembly of each Newton iteration (node-row gather, TotLag) against the HBM roof,
+    # SURVEY §8d's 2,069 B per hex8 element
+    asm = float(np.median(d["assembly_ms"])) if d.get("assembly_ms") else d["assembly_ms_mean"]
+    gbs = ALG_BYTES_PER_ELE * d["elements"] / (asm * 1e-3) / 1e9
+    out["roofline"] = {"bound": "hbm", "kernel": "assembly: gather_h8_kernel<TotLag>",
+                       "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": gbs / HBM_PEAK_GBS, "alg_bytes_per_element": ALG_BYTES_PER_ELE,
+                       "ms_assembly_median": asm}
+    return out
 
 
 # SURVEY.md §8d algorithmic figures for hex27 TotLag K + r (per element)
@@ -1116,7 +1160,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_newton:
         torch.cuda.empty_cache()
         try:
-            secondary.append(newton_secondary(args.newton_n))
+            h27cpu = next((x.get("cpu_baseline") for x in secondary
+                           if str(x.get("workload", "")).startswith("hex27-totlag-") and
+                           isinstance(x.get("cpu_baseline"), dict) and x["cpu_baseline"].get("value")), None)
+            secondary.append(newton_secondary(args.newton_n, cpu_rate=h27cpu))
         except Exception as e:  # report, never hide
             secondary.append({"workload": "hex27-totlag-newton", "error": repr(e)})
     if rank == 0 and world == 1 and not args.no_amg:

@@ -177,6 +177,18 @@ ev.spmv(nt.K, yv, Ky)
 sym = abs(float(torch.dot(xv, Ky)) - float(torch.dot(yv, Kx))) / float(
     torch.linalg.vector_norm(xv) * torch.linalg.vector_norm(Ky))
 r_final = float(torch.linalg.vector_norm(nt.fint - nt.fext)) / max(np.linalg.norm(fext), 1e-300)
+# the matrix-free tangent action the multigrid's smoother and outer FCG apply (hex27 StVK):
+# its device time per application at the solution, hipEvents over 20 back-to-back applications
+apply_ms = None
+if a.mg and a.mg_matrix_free:
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev.tangent_apply(u, xv, Kx)
+    e0.record()
+    for _ in range(20):
+        ev.tangent_apply(u, xv, Kx)
+    e1.record()
+    torch.cuda.synchronize()
+    apply_ms = e0.elapsed_time(e1) / 20
 del xv, yv, Kx, Ky
 out = {"config": f"{a.celltype}-{a.kinem}-{a.n}^3-cantilever", "forcing": a.forcing,
        "converged": True, "tangent_symmetry_rel": sym,
@@ -194,6 +206,7 @@ out = {"config": f"{a.celltype}-{a.kinem}-{a.n}^3-cantilever", "forcing": a.forc
        "assembly_ms_mean": float(np.mean([r["assembly_ms"] for r in h])),
        "assembly_elem_per_s": mesh.n_ele / (1e-3 * float(np.median([r["assembly_ms"] for r in h]))),
        "solve_ms_total": float(sum(r.get("solve_ms", 0.0) for r in h)),
+       "assembly_ms": [r["assembly_ms"] for r in h], "tangent_apply_ms": apply_ms,
        "pcg_iterations": [r.get("pcg_iter") for r in h[:-1]],
        "tip_uz": float(u[mesh.node_dof_row[np.argmax(mesh.node_x.sum(axis=1))] + 2]),
        "amg_graph_setup_s": t_amg_setup if (a.amg or a.amg_native) else None,
