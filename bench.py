@@ -341,7 +341,7 @@ def newton_secondary(n, timeout_s=900, cpu_rate=None):
     d = json.loads(p.stdout.strip().splitlines()[-1])
     if not d.get("converged"):
         return {"workload": f"hex27-totlag-{n}^3-newton", "error": "Newton did not converge"}
-    return {
+    out = {
         "workload": f"hex27-totlag-{n}^3-full-newton",
         "baseline_config": "BASELINE.json configs[2] (StVK, 1M hex27, full Newton loop on 1 MI355X)",
         "value": d["newton_s"], "unit": "s (Newton loop, setup excluded)", "higher_is_better": False,
