@@ -84,6 +84,27 @@ import json
 for l in open('$O/gab.txt'):
     v, k, j = l.split(' ', 2); d = json.loads(j)
     print(v, k, round(d['ms_evaluate'], 3))" ;;
+    sab)  # same-box A/B of lib variants on the structured sweep: 1M hex8 linear (+ TotLag), LIBS=...
+      for r in 1 2 3; do for v in ${LIBS:-default}; do for k in ${KINS:-linear}; do
+        if [ "$v" = default ]; then unset FCG_LIB; else export FCG_LIB=$v; fi
+        echo "$v $k $(timeout -k 10 200 python3 $ET --celltype hex8 --kinem $k --n 100 --reps 21 | tail -1)" >> $O/sab.txt || exit 1
+      done; done; done; unset FCG_LIB
+      python3 -c "
+import json, collections
+t = collections.defaultdict(list)
+for l in open('$O/sab.txt'):
+    v, k, j = l.split(' ', 2); d = json.loads(j); t[(v, k)].append(round(d['ms_evaluate'], 4))
+for key, x in t.items(): print(key, x)" ;;
+    tab)  # same-box A/B of lib variants on the TSI tangent (126^3), LIBS=...
+      for r in 1 2; do for v in ${LIBS:-default}; do
+        if [ "$v" = default ]; then unset FCG_LIB; else export FCG_LIB=$v; fi
+        echo "$v $(timeout -k 10 300 python3 tools/tsi_bench.py --n 126 --reps 10 | tail -1)" >> $O/tab.txt || exit 1
+      done; done; unset FCG_LIB
+      python3 -c "
+import json
+for l in open('$O/tab.txt'):
+    v, j = l.split(' ', 1); d = json.loads(j)
+    print(v, 'split', round(d['ms_structure'], 3), '+', round(d['ms_tsi_blocks'], 3), 'fused', round(d['ms_fused'], 3))" ;;
     tests)  # the whole GPU suite
       run 1500 gpu_tests.log python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests
       tail -3 $O/gpu_tests.log ;;
