@@ -881,6 +881,20 @@ void setup(fcg_amg* h, const double* K, hipStream_t s)
   galerkin_from(h, 0, K, s);
 }
 
+// The numeric setup a rank-local handle needs when its coarse levels are coupled across ranks
+// (fcg_amg_precond_setup): the nodal block inverses of the smoother and of P_0's smoothing only --
+// the coupled path builds its own lambda_max, P_0, A_1 and hierarchy, so the rank-local Galerkin
+// products, their Lanczos estimates and the dense coarsest inverse are skipped
+void setup_coupled_local(fcg_amg* h, const double* K, hipStream_t s)
+{
+  ck(fcg_block_jacobi_setup(h->ctx, K, h->ctx_dinv, s), "singular nodal block of K (block Jacobi)");
+  ck(fcg_bsr_from_node_csr(h->device, h->nb0, h->ctx->mesh.rowptr, h->A0.ptr, K, h->A0.vals, s),
+      "fcg_bsr_from_node_csr");
+  ck(fcg_bsr_block_jacobi_setup(h->device, 3, h->nb0, h->A0.ptr, h->A0_diag, h->A0.vals, h->A0_dinv,
+         h->flag, s),
+      "singular nodal block of K");
+}
+
 // the Galerkin hierarchy below level l0 (its operator and block inverses already set): per step
 // l >= l0, P_l = (I - omega D^-1 A_l) T_l and A_{l+1} = P_l^T (A_l P_l) on the fixed patterns
 void galerkin_from(fcg_amg* h, size_t l0, const double* K, hipStream_t s)
@@ -1395,6 +1409,8 @@ void coupled_build(fcg_amg* h, const fcg_transport* tr, hipStream_t s)
     for (double** v : {&L1.x, &L1.b, &L1.r, &L1.d, &L1.z, &L1.p, &L1.q}) *v = dalloc<double>(g, 6 * c->n_agg_tot);
   }
   coarsen(g, &g->levels[0].A, 6, std::move(ns), nullptr);
+  // T_0's ghost rows: the tentative prolongator is fixed at create, so they are imported once
+  extend_values(h, c, st0.T, c->Text, 1, tr, s);
   g->partial = dalloc<double>(g, kMaxPartials);
   g->sc = dalloc<double>(g, 16);
   g->flag = dalloc<int32_t>(g, 1);
@@ -1410,7 +1426,6 @@ void coupled_setup(fcg_amg* h, const double* K, const fcg_transport* tr, hipStre
   ck(fcg_bsr_from_node_csr(h->device, nb0, m.rowptr, c->Afull.ptr, K, c->Afull.vals, s), "fcg_bsr_from_node_csr (full rows)");
   // lambda_max of the global D^-1 A (Lanczos over the ranks): the smoother's and P's
   estimate_lmax(Ops{h, 0, K, s, tr});
-  extend_values(h, c, st0.T, c->Text, 1, tr, s);
   ck(fcg_bsr_spgemm(h->device, 3, 3, 6, nb0, c->Afull.ptr, c->Afull.col, c->Afull.vals, c->Text.ptr,
          c->Text.col, c->Text.vals, c->AT.ptr, c->AT.col, c->AT.vals, s), "fcg_bsr_spgemm (A T_ext)");
   ck(fcg_amg_smooth_prolongator(h->device, 3, nb0, c->P.ptr, c->P.col, c->agg, st0.tent, h->A0_dinv,
@@ -1856,7 +1871,25 @@ int fcg_amg_precond_setup(fcg_amg* h, const double* d_K, const fcg_transport* tr
     const char* e = std::getenv("FCG_AMG_INJECT_FAIL_RANK");
     return e ? std::atoi(e) : -1;
   }();
-  int rc = fcg_amg_setup(h, d_K, stream);
+  int rc = FCG_OK;
+  if (tr && tr->nranks > 1 && h->local)
+  {
+    try
+    {
+      ck(hipSetDevice(h->device), "hipSetDevice");
+      setup_coupled_local(h, d_K, stream ? static_cast<hipStream_t>(stream) : h->ctx->stream);
+      h->ready = true;
+    }
+    catch (const Fail& f)
+    {
+      h->ready = false;
+      h->last_error = f.msg;
+      h->ctx->last_error = f.msg;
+      rc = f.code;
+    }
+  }
+  else
+    rc = fcg_amg_setup(h, d_K, stream);
   if (rc == FCG_OK && tr && tr->nranks > 1 && tr->rank == inject)
   {
     h->ready = false;
