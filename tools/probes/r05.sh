@@ -105,6 +105,15 @@ import json
 for l in open('$O/tab.txt'):
     v, j = l.split(' ', 1); d = json.loads(j)
     print(v, 'split', round(d['ms_structure'], 3), '+', round(d['ms_tsi_blocks'], 3), 'fused', round(d['ms_fused'], 3))" ;;
+    tsplit)  # TSI fused tangent: split (default) vs one fused pass, same box, alternating
+      for r in 1 2 3; do for sp in 1 0; do
+        echo "split=$sp $(FCG_TSI_SPLIT=$sp timeout -k 10 300 python3 tools/tsi_bench.py --n 126 --reps 10 | tail -1)" >> $O/tsplit.txt || exit 1
+      done; done
+      python3 -c "
+import json
+for l in open('$O/tsplit.txt'):
+    v, j = l.split(' ', 1); d = json.loads(j)
+    print(v, 'fused-entry', round(d['ms_fused'], 3))" ;;
     tests)  # the whole GPU suite
       run 1500 gpu_tests.log python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests
       tail -3 $O/gpu_tests.log ;;
