@@ -520,6 +520,40 @@ def hex27_secondary(dev, n, steps, threads, with_cpu):
     return out
 
 
+def hex27_slab_secondary(dev, n, steps, slab):
+    """Config 3's mesh (n^3 hex27, StVK TotLag) assembled under the slab schedule of the incidence
+    records: the records live in a ring instead of one per incidence -- the memory
+    mode for meshes whose full scratch would not fit beside the tangent.  Same K and f bitwise as
+    the one-slab path (tests/test_h27_slab.py); reported: time per evaluate and the bytes."""
+    os.environ["FCG_H27_SLAB"] = str(slab)
+    try:
+        mesh = fcg.BoxMesh(fcg.HEX27, (n, n, n), jitter=0.02, seed=20251015)
+        ev = fcg.Evaluator(mesh, kinematics=fcg.TOTLAG, youngs=210.0, poisson=0.3, device=dev.index)
+    finally:
+        del os.environ["FCG_H27_SLAB"]
+    info = ev.info
+    u = torch.from_numpy(mesh.u_col(5e-2)).to(dev)
+    f = torch.zeros(mesh.n_rows, dtype=torch.float64, device=dev)
+    K = torch.zeros(mesh.nnz, dtype=torch.float64, device=dev)
+    ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u, f, K)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u, f, K)
+    torch.cuda.synchronize(dev)
+    ms = 1e3 * (time.perf_counter() - t0) / steps
+    full = int(info.n_incidences) * (9 * 27 + 3) * 8
+    out = {"workload": f"hex27-totlag-{n}^3-slab-schedule",
+           "baseline_config": "BASELINE.json configs[2] mesh, incidence records in a ring",
+           "value": mesh.n_ele / (ms * 1e-3), "unit": "element-evaluations/s", "ms_per_step": ms,
+           "slab_elements": slab, "scratch_bytes": int(info.scratch_bytes),
+           "scratch_bytes_one_record_per_incidence": full, "device_bytes": int(info.device_bytes),
+           "tangent_bytes": 8 * mesh.nnz}
+    ev.close()
+    del K, f, u
+    return out
+
+
 def tsi_cpu_baseline(n, nz, threads):
     """The oracle's TSI::Monolithic element loop (orc_tsi_discretization_evaluate: the four
     blocks and both residuals, owned rows, `threads` workers as ranks) on an n x n x nz slab of the
@@ -822,6 +856,8 @@ def main():
     ap.add_argument("--no-amg", action="store_true",
                     help="skip the unstructured-mesh Newton line (native AMG)")
     ap.add_argument("--newton-n", type=int, default=100)
+    ap.add_argument("--no-slab", action="store_true",
+                    help="skip the config-3 mesh under the slab schedule of the hex27 records")
     ap.add_argument("--no-optionb", action="store_true", help="skip the option-B (shared-DOF) line")
     ap.add_argument("--no-host", action="store_true", help="skip the host-buffer drop-in line")
     ap.add_argument("--timing-after", dest="timing_before", action="store_false",
@@ -841,7 +877,7 @@ def main():
     args = ap.parse_args()
     if args.only_primary:
         for k in ("no_cpu_baseline", "no_hex27", "no_tsi", "no_newton", "no_amg", "no_optionb",
-                  "no_host", "no_pmc", "no_gather"):
+                  "no_host", "no_pmc", "no_gather", "no_slab"):
             setattr(args, k, True)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -1157,6 +1193,13 @@ def main():
                                              cpu_threads(args.cpu_threads), not args.no_cpu_baseline))
         except Exception as e:  # report, never hide
             secondary.append({"workload": "hex27-totlag", "error": repr(e)})
+    if rank == 0 and world == 1 and not args.no_slab:
+        torch.cuda.empty_cache()
+        try:
+            secondary.append(hex27_slab_secondary(dev, args.newton_n, 3, 5000))
+        except Exception as e:  # report, never hide
+            secondary.append({"workload": "hex27-slab-schedule", "error": repr(e)})
+        torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_newton:
         torch.cuda.empty_cache()
         try:
