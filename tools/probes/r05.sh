@@ -114,6 +114,15 @@ import json
 for l in open('$O/tsplit.txt'):
     v, j = l.split(' ', 1); d = json.loads(j)
     print(v, 'fused-entry', round(d['ms_fused'], 3))" ;;
+    h27pmc)  # HEAD counter sets of both hex27 kernels (40^3 TotLag) and of the 1M sweep
+      timeout -k 10 900 tools/pmc_kernel.sh r05/h27pmc h27_element occ,inst,flop,mem -- --celltype hex27 --kinem totlag --n 40 --reps 3 > $O/h27pmc.log 2>&1 || { tail -20 $O/h27pmc.log; exit 1; }
+      python3 tools/pmc_summary.py gpurun_out/r05/h27pmc assemble27 > gpurun_out/r05/h27pmc/summary_assemble27.txt
+      tail -12 gpurun_out/r05/h27pmc/summary.txt; tail -12 gpurun_out/r05/h27pmc/summary_assemble27.txt ;;
+    primprof)  # rocprofv3 kernel statistics of bench.py --only-primary (the headline's kernels)
+      mkdir -p $O/primprof
+      (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$O/primprof" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --only-primary --steps 20 --warmup 5) > $O/primprof.log 2>&1 || { tail -20 $O/primprof.log; exit 1; }
+      grep '^{' $O/primprof.log | tail -1 > $O/primprof_bench.json
+      f=$(find $O/primprof -name "*kernel_stats.csv" | head -1); head -4 "$f" | cut -c1-220 ;;
     tests)  # the whole GPU suite
       run 1500 gpu_tests.log python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests
       tail -3 $O/gpu_tests.log ;;
