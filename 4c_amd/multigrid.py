@@ -771,6 +771,38 @@ class Multigrid(CycleFCG):
             self.coarse_amg = NativeAMG(last.mesh, last.ev, last.rows)
             self.coarse_amg.setup(last.K)
 
+    def warm_up(self):
+        """Launch every kernel of a solve once on scratch data, so that the first Newton step
+        does not pay the process's one-time costs (HIP loads a kernel's code object at its first
+        launch; config 3's first solve took ~0.3 s longer than the others).  Keeps no state: the
+        fine level's lambda_max stays unestimated, its block inverses are recomputed by the next
+        solve's _prepare, no graph is captured."""
+        f0 = self.levels[0]
+        f64 = dict(dtype=torch.float64, device=self.dev)
+        saved = (f0.lmax, f0.mf_u)
+        f0.dinv.zero_()
+        f0.lmax = 1.0
+        if f0.matrix_free:
+            f0.mf_u = torch.zeros(f0.mesh.n_cols, **f64)
+        try:
+            b = torch.zeros(f0.n, **f64)
+            x = torch.zeros(f0.n, **f64)
+            self._vcycle(0, b, x)
+            if self.outer_matrix_free:
+                self._outer(f0, b, x)
+            sc = torch.zeros((), **f64)
+            torch.dot(b, x, out=sc)
+            torch.div(sc, sc + 1.0, out=sc)
+            x.addcmul_(b, sc)
+            x.mul_(sc).add_(b)
+            st = torch.zeros(3, **f64)
+            torch.stack((sc, sc, sc), out=st)
+            st.cpu()
+            float(torch.linalg.vector_norm(b))
+        finally:
+            f0.lmax, f0.mf_u = saved
+        torch.cuda.synchronize(self.dev)
+
     def describe(self):
         out = [{"celltype": "hex27" if l.mesh.celltype == fcg.HEX27 else "hex8",
                 "intervals": [int(l.mesh.box.interval[d]) for d in range(3)], "dofs": l.n,

@@ -130,6 +130,17 @@ class StaticNewton:
             linear_solver.check_dirichlet(dbc_rows)
         self.history = []
 
+    def warm_up(self):
+        """The torch operations of a Newton step launched once on scratch vectors (their code
+        objects load at the first launch); no state is kept."""
+        t = torch.zeros(16, dtype=torch.float64, device=self.dev)
+        w = torch.zeros_like(t)
+        torch.sub(t, w, out=w)
+        torch.neg(w, out=w)
+        t += w
+        float(torch.linalg.vector_norm(t))
+        torch.cuda.synchronize(self.dev)
+
     def linear_solve(self, b, x, rtol):
         """K x = b to |r| <= rtol |b| from x = 0; returns (iterations, relative residual)."""
         if self.linear_solver is not None:

@@ -157,10 +157,18 @@ if a.amg or a.amg_native:
     print(f"AMG setup (host graph) {t_amg_setup:.1f} s: {json.dumps(mg.describe())}",
           file=sys.stderr, flush=True)
     t_setup = time.perf_counter() - t0
-print(f"setup {t_setup:.1f} s", file=sys.stderr, flush=True)
 nt = Timed(ev, fext, dbc, lin_max_iter=a.lin_max_iter, tol_res=a.tol * max(np.linalg.norm(fext), 1e-300), tol_inc=a.tol,
            lin_rtol=a.lin_rtol, max_iter=40,
            forcing=newton.ForcingTerm(a.forcing, constant=a.lin_rtol), linear_solver=mg)
+# the kernels of the Newton step launched once on scratch data (setup: HIP loads a kernel's code
+# object at its first launch, ~0.3 s of config 3's first Newton step otherwise)
+t_w = time.perf_counter()
+if hasattr(mg, "warm_up"):
+    mg.warm_up()
+nt.warm_up()
+setup_phases["warm_up_s"] = time.perf_counter() - t_w
+t_setup = time.perf_counter() - t0
+print(f"setup {t_setup:.1f} s (warm-up {setup_phases['warm_up_s']:.2f} s)", file=sys.stderr, flush=True)
 t1 = time.perf_counter()
 u = nt.solve()
 torch.cuda.synchronize()

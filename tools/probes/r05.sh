@@ -65,7 +65,7 @@ for l in open('$O/scratch.txt'):
     h, j = l.split(' {', 1); d = json.loads('{' + j)
     print(h, round(d['ms_evaluate'], 2), 'scratch GB', round(d['scratch_bytes'] / 1e9, 3), 'device GB', round(d['device_bytes'] / 1e9, 2))" ;;
     c3)  # config 3 Newton (bench.py's secondary line): setup phases and Newton time
-      run 600 c3.log env FCG_MG_SETUP_TIMING=1 python3 tools/newton_bench.py --celltype hex27 --kinem totlag --n 100 --length 1 --load -1 --mg --mg-matrix-free --mg-outer-matrix-free
+      run 600 c3.log env FCG_MG_SETUP_TIMING=1 FCG_MG_GRAPH_TIMING=1 python3 tools/newton_bench.py --celltype hex27 --kinem totlag --n 100 --length 1 --load -1 --mg --mg-matrix-free --mg-outer-matrix-free
       grep '^{' $O/c3.log | tail -1 > $O/c3.json
       python3 -c "
 import json; d = json.load(open('$O/c3.json'))
