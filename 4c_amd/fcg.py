@@ -516,7 +516,10 @@ class _NativeBoxMesh:
 
     def __del__(self):
         if self.h:
-            lib().fcg_box_mesh_destroy(self.h)
+            try:
+                lib().fcg_box_mesh_destroy(self.h)
+            except Exception:  # noqa: BLE001 - interpreter shutdown: the process frees it anyway
+                pass
             self.h = None
 
 
