@@ -1843,7 +1843,9 @@ int fcg_evaluate_device(fcg_ctx* ctx, int action, int mode, const double* d_u_co
     T.pending = true;
     T.path = m.path;
   }
-  if (he == hipSuccess)
+  // async: the flags stay sticky on the device across queued evaluates and fcg_check_error reads
+  // them once (a read-back per evaluate would put a copy between every two evaluates' kernels)
+  if (he == hipSuccess && !ctx->async)
     he = hipMemcpyAsync(m.err_host, m.err, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, s);
   if (he == hipSuccess && ctx->async)
   {
@@ -1883,7 +1885,9 @@ int fcg_check_error(fcg_ctx* ctx, int32_t* bad_ele_gid)
   if (!ctx->pending) return FCG_OK;
   (void)hipSetDevice(ctx->device);
   ctx->pending = false;
-  if (hipStreamSynchronize(ctx->pending_stream) != hipSuccess)
+  if (hipMemcpyAsync(ctx->mesh.err_host, ctx->mesh.err, 2 * sizeof(int32_t), hipMemcpyDeviceToHost,
+          ctx->pending_stream) != hipSuccess ||
+      hipStreamSynchronize(ctx->pending_stream) != hipSuccess)
   {
     ctx->mesh.err_clean = false;
     ctx->last_error = "HIP: stream failed";

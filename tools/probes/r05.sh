@@ -123,6 +123,23 @@ for l in open('$O/tsplit.txt'):
       (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$O/primprof" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --only-primary --steps 20 --warmup 5) > $O/primprof.log 2>&1 || { tail -20 $O/primprof.log; exit 1; }
       grep '^{' $O/primprof.log | tail -1 > $O/primprof_bench.json
       f=$(find $O/primprof -name "*kernel_stats.csv" | head -1); head -4 "$f" | cut -c1-220 ;;
+    gloo2)  # bench.py --gpus 2 on one GPU over the host-staged (gloo) transport: the multi-rank flow
+      FCG_DIST_BACKEND=gloo timeout -k 10 600 python -u bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu-baseline --no-newton --no-amg --no-slab > $O/bench_gloo2.json 2> $O/bench_gloo2.err || { tail -20 $O/bench_gloo2.err; exit 1; }
+      python3 -c "
+import json; d = json.loads(open('$O/bench_gloo2.json').read().strip().splitlines()[-1])
+print(d['n_gpus'], d['value'], d['ms_per_step'], d['config'])
+for s in d.get('secondary', []): print(s.get('workload'), s.get('value'), s.get('error', '')[:300])" ;;
+    bab)  # same-box A/B of the headline step (bench.py --only-primary): bab with LIBS="default head"
+      for rep in 1 2 3; do for v in ${LIBS:-default head}; do
+        if [ "$v" = default ]; then unset FCG_LIB; else export FCG_LIB=$v; fi
+        timeout -k 10 300 python3 bench.py --only-primary --steps 50 --warmup 5 --no-cpu-baseline > $O/bab_$v.log 2>&1 || { tail -20 $O/bab_$v.log; exit 1; }
+        echo "$v $(grep '^{' $O/bab_$v.log | tail -1)" >> $O/bab.jsonl
+      done; done; unset FCG_LIB
+      python3 -c "
+import json
+for l in open('$O/bab.jsonl'):
+    v, j = l.split(' ', 1); d = json.loads(j)
+    print(v, round(d['value'] / 1e6, 1), round(d['ms_per_step'], 4), round(d['roofline']['frac'], 4))" ;;
     tests)  # the whole GPU suite
       run 1500 gpu_tests.log python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests
       tail -3 $O/gpu_tests.log ;;
