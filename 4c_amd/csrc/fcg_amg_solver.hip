@@ -628,6 +628,13 @@ void apply_A0(fcg_amg* h, const double* K, const double* x, double* y, hipStream
 // a level's operator and smoother pieces: l = 0 the context, l >= 1 levels[l - 1]
 void coupled_spmv(fcg_amg* h, const double* K, const fcg_transport* tr, const double* x, double* y, hipStream_t s);
 double& coupled_lmax0_ref(fcg_amg* h);
+// level 1 distributed across the ranks (struct Dist below)
+struct Dist;
+int64_t dist_n(const Dist* d);
+void dist_spmv(fcg_amg* h, Dist* d, const fcg_transport* tr, const double* x, double* y, hipStream_t s);
+void dist_dinv(fcg_amg* h, const Dist* d, const double* r, double* z, double scale, bool acc, hipStream_t s);
+double& dist_lmax(Dist* d);
+double* dist_vec(Dist* d, int which);  // 0 r, 1 d, 2 z, 3 p, 4 q
 
 struct Ops {
   fcg_amg* h;
@@ -637,10 +644,13 @@ struct Ops {
   // level 0 of a rank-local handle with coupled coarse levels: the global operator (import + the
   // rank's SpMV) and its lambda_max instead of the owned block's
   const fcg_transport* tr = nullptr;
-  int64_t n() const { return l == 0 ? h->n0 : h->levels[size_t(l - 1)].A.n * 6; }
+  Dist* dl = nullptr;  // the distributed level 1 (tr: its imports and inner products)
+  int64_t n() const { return dl ? dist_n(dl) : l == 0 ? h->n0 : h->levels[size_t(l - 1)].A.n * 6; }
   void spmv(const double* x, double* y) const
   {
-    if (l == 0 && tr)
+    if (dl)
+      dist_spmv(h, dl, tr, x, y, s);
+    else if (l == 0 && tr)
       coupled_spmv(h, K, tr, x, y, s);
     else if (l == 0)
       apply_A0(h, K, x, y, s);
@@ -652,7 +662,9 @@ struct Ops {
   }
   void dinv(const double* r, double* z, double scale, bool acc) const
   {
-    if (l == 0 && h->new2old)  // reordered level 0: its BSR block inverses
+    if (dl)
+      dist_dinv(h, dl, r, z, scale, acc, s);
+    else if (l == 0 && h->new2old)  // reordered level 0: its BSR block inverses
       ck(fcg_bsr_block_jacobi_apply(h->device, 3, h->nb0, h->A0_dinv, r, z, scale, acc ? 1 : 0, s),
           "fcg_bsr_block_jacobi_apply (level 0)");
     else if (l == 0)
@@ -664,12 +676,15 @@ struct Ops {
           "fcg_bsr_block_jacobi_apply");
     }
   }
-  double& lmax() const { return l == 0 ? (tr ? coupled_lmax0_ref(h) : h->lmax0) : h->levels[size_t(l - 1)].lmax; }
-  double* r() const { return l == 0 ? h->r0 : h->levels[size_t(l - 1)].r; }
-  double* d() const { return l == 0 ? h->d0 : h->levels[size_t(l - 1)].d; }
-  double* z() const { return l == 0 ? h->z0 : h->levels[size_t(l - 1)].z; }
-  double* p() const { return l == 0 ? h->p0 : h->levels[size_t(l - 1)].p; }
-  double* q() const { return l == 0 ? h->q0 : h->levels[size_t(l - 1)].q; }
+  double& lmax() const
+  {
+    return dl ? dist_lmax(dl) : l == 0 ? (tr ? coupled_lmax0_ref(h) : h->lmax0) : h->levels[size_t(l - 1)].lmax;
+  }
+  double* r() const { return dl ? dist_vec(dl, 0) : l == 0 ? h->r0 : h->levels[size_t(l - 1)].r; }
+  double* d() const { return dl ? dist_vec(dl, 1) : l == 0 ? h->d0 : h->levels[size_t(l - 1)].d; }
+  double* z() const { return dl ? dist_vec(dl, 2) : l == 0 ? h->z0 : h->levels[size_t(l - 1)].z; }
+  double* p() const { return dl ? dist_vec(dl, 3) : l == 0 ? h->p0 : h->levels[size_t(l - 1)].p; }
+  double* q() const { return dl ? dist_vec(dl, 4) : l == 0 ? h->q0 : h->levels[size_t(l - 1)].q; }
 };
 
 // largest eigenvalue of D^-1 A from a 10-step Lanczos (block-Jacobi CG on a random vector); with
@@ -688,7 +703,8 @@ void estimate_lmax(const Ops& o)
     ck(hipStreamSynchronize(ss), "hipStreamSynchronize");
     return v;
   };
-  hipLaunchKernelGGL(random_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, o.s, b, o.l == 0 ? h->mask0 : nullptr, n, 20251015u);
+  hipLaunchKernelGGL(random_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, o.s, b,
+      o.l == 0 && !o.dl ? h->mask0 : nullptr, n, 20251015u);
   ck(hipMemcpyAsync(r, b, sizeof(double) * size_t(n), hipMemcpyDeviceToDevice, o.s), "copy");
   o.dinv(r, z, 1.0, false);
   ck(hipMemcpyAsync(p, z, sizeof(double) * size_t(n), hipMemcpyDeviceToDevice, o.s), "copy");
@@ -1142,29 +1158,105 @@ struct DevBuf {
   DevBuf& operator=(const DevBuf&) = delete;
 };
 
+// a fixed point-to-point exchange pattern of the distributed level: items per rank in rank
+// order (the width of an item is chosen per call)
+struct Xch {
+  std::vector<int64_t> scnt, rcnt;  // items to / from each rank
+  int64_t ns = 0, nr = 0;
+  std::vector<int64_t> sd, rd;      // the current call's doubles per rank
+  void finish()
+  {
+    ns = nr = 0;
+    for (int64_t v : scnt) ns += v;
+    for (int64_t v : rcnt) nr += v;
+  }
+};
+
+// Level 1 distributed across the ranks (fcg_transport::exchange_fn; MueLu keeps every level of its
+// hierarchy a distributed Xpetra operator, 4C_linear_solver_preconditioner_muelu.cpp:97).  Global
+// aggregate ids are numbered by rank (rank q owns [agg_off[q], agg_off[q + 1])).  Each rank keeps
+//   * LA: the aggregates its P_0 rows and their ghost rows reach, ascending global id (its own at
+//     [own0, own0 + na)); P_0, P_0^T, P_ext and this rank's partial A_1 = P^T A P_ext (C) use it;
+//   * A: the owned rows of A_1, columns DA = ascending global ids (own at [d0, d0 + na)), summed
+//     from C's own rows and the partial rows the other ranks send to the owner (fixed order: own
+//     blocks, then the senders in rank order -- bitwise reproducible);
+//   * three exchange patterns: the partial rows (36 doubles per block, per numeric setup), the
+//     import of A's ghost columns (per level-1 SpMV), and LA's other-rank entries with their owners
+//     (restriction: sent and added by the owner; prolongation: the reverse);
+//   * level 2: the tentative prolongator T_1 of a rank-local aggregation of A's owned block
+//     (unsmoothed), A_2 = T_1^T (A T_1,ext) with complete rows on their owners, gathered and solved
+//     redundantly by the replicated hierarchy (the replication moves down one level).
+struct Dist {
+  int R = 1, me = 0;
+  std::vector<int64_t> agg_off;  // [R + 1]
+  int64_t na = 0, off = 0;
+  int64_t NL = 0, own0 = 0;
+  int64_t NA = 0, d0 = 0;
+  Bsr A;
+  int64_t* diag = nullptr;
+  double* dinv = nullptr;
+  double lmax = 0.0;
+  int64_t c_lo = 0, c_hi = 0;  // C's owned-row blocks
+  int64_t* pos_own = nullptr;  // [c_hi - c_lo] their blocks of A
+  Xch rows;
+  int64_t* pos_recv = nullptr;  // [rows.nr] A block of each received partial block
+  double *rows_s = nullptr, *rows_r = nullptr;
+  Xch imp;
+  int32_t* imp_idx = nullptr;  // [imp.ns] owned aggregate of each item sent
+  std::vector<int32_t> imp_idx_h;
+  double *imp_s = nullptr, *imp_r = nullptr, *xe = nullptr;
+  Xch pex;
+  int32_t* pex_idx = nullptr;  // [pex.nr] owned aggregate of each item received (restriction)
+  double *pex_s = nullptr, *pex_r = nullptr, *y = nullptr;
+  double *x = nullptr, *b = nullptr, *r = nullptr, *dd = nullptr, *z = nullptr, *p = nullptr, *q = nullptr;
+  int64_t n2 = 0, off2 = 0, n2_tot = 0;
+  Bsr T1;     // na x n2 (own level-2 aggregates)
+  Bsr T1t;    // n2 x na
+  Bsr T1ext;  // NA x n2_tot (global level-2 ids)
+  Bsr AT1;    // na x n2_tot
+  Bsr C2;     // n2 x n2_tot: this rank's rows of A_2
+};
+
 struct Coupled {
   int rank = 0, nranks = 1;
   int64_t nc_nodes = 0;            // column nodes of the context (owned first, then ghosts)
   int64_t off = 0, n_agg_tot = 0;  // this rank's first global aggregate; all ranks' aggregates
   int M = 0;                       // blocks per row of P, widest over the ranks
   Bsr Afull;                       // owned block rows x column nodes (3 x 3)
-  Bsr Text;                        // column nodes x global aggregates: T_0 rows, ghosts imported
-  Bsr AT;                          // owned block rows x global aggregates (3 x 6)
-  Bsr P;                           // owned block rows x global aggregates: (I - w D^-1 A) T
-  Bsr Pt;                          // its transpose: global aggregates x owned block rows
+  Bsr Text;                        // column nodes x aggregates: T_0 rows, ghosts imported
+  Bsr AT;                          // owned block rows x aggregates (3 x 6)
+  Bsr P;                           // owned block rows x aggregates: (I - w D^-1 A) T
+  Bsr Pt;                          // its transpose: aggregates x owned block rows
   int64_t* p_perm = nullptr;       // P^T block -> P block
-  int32_t* agg = nullptr;          // [nb0] global aggregate of each owned node (-1 = none)
-  Bsr Pext;                        // column nodes x global aggregates: P rows, ghosts imported
-  Bsr AP;                          // owned block rows x global aggregates (3 x 6)
-  Bsr C;                           // this rank's part of A_1 = P^T A P (global rows touched)
-  int64_t* c_pos = nullptr;        // [C.nnzb] block position of each of C's blocks in the global A_1
-  int64_t a1_nnzb = 0;             // blocks of the global A_1
+  int32_t* agg = nullptr;          // [nb0] aggregate of each owned node in P's numbering (-1 = none)
+  Bsr Pext;                        // column nodes x aggregates: P rows, ghosts imported
+  Bsr AP;                          // owned block rows x aggregates (3 x 6)
+  Bsr C;                           // this rank's part of A_1 = P^T A P
+  // the replicated level (A_1, or A_2 with a distributed level 1): this rank's blocks and their
+  // positions in the replicated operator, which the all-reduce sums
+  const Bsr* rep_part = nullptr;
+  int64_t* rep_pos = nullptr;      // [rep_part->nnzb] block position in the replicated operator
+  int64_t rep_nnzb = 0, rep_n = 0; // replicated operator: blocks, block rows
   double *chan = nullptr, *chan_col = nullptr, *q = nullptr, *w = nullptr, *gb = nullptr, *ge = nullptr;
-  fcg_amg* g = nullptr;            // the replicated hierarchy: g->levels[0].A = the global A_1
+  fcg_amg* g = nullptr;            // the replicated hierarchy: g->levels[0].A = the replicated operator
   double lmax0 = 0.0;              // lambda_max of D^-1 A for the global operator
+  Dist* d = nullptr;               // level 1 distributed (with exchange_fn), else NULL (A_1 replicated)
+  // collective traffic (doubles; fcg_amg_coupled_stats): counters of the running phase, and the
+  // last numeric setup's and preconditioner application's totals
+  int64_t ctr_ar = 0, ctr_x = 0;
+  int64_t ar_setup = 0, ar_apply = 0, x_setup = 0, x_apply = 0;
+  ~Coupled() { delete d; }
 };
 
 double& coupled_lmax0_ref(fcg_amg* h) { return h->cpl->lmax0; }
+
+int64_t dist_n(const Dist* d) { return 6 * d->na; }
+double& dist_lmax(Dist* d) { return d->lmax; }
+double* dist_vec(Dist* d, int which)
+{
+  double* v[5] = {d->r, d->dd, d->z, d->p, d->q};
+  return v[which];
+}
 
 // element-wise sum over the ranks of a host vector, through the transport's device all-reduce
 void host_allsum(const fcg_transport* tr, std::vector<double>& v, hipStream_t s)
@@ -1178,8 +1270,76 @@ void host_allsum(const fcg_transport* tr, std::vector<double>& v, hipStream_t s)
   ck(hipStreamSynchronize(s), "hipStreamSynchronize");
 }
 
+// the all-reduce of the coupled levels, counted
+void allreduce_counted(Coupled* c, const fcg_transport* tr, double* p, int64_t n, hipStream_t s, const char* what)
+{
+  ck(tr->allreduce_fn(tr->user, p, n, s), what);
+  c->ctr_ar += n;
+}
+
+// one exchange of w-double items on pattern x (reverse: the owner -> requester direction), counted
+void exchange_counted(Coupled* c, const fcg_transport* tr, Xch& x, int w, bool reverse, const double* sb,
+    double* rb, hipStream_t s, const char* what)
+{
+  const std::vector<int64_t>& sc = reverse ? x.rcnt : x.scnt;
+  const std::vector<int64_t>& rc = reverse ? x.scnt : x.rcnt;
+  x.sd.assign(sc.size(), 0);
+  x.rd.assign(rc.size(), 0);
+  for (size_t q = 0; q < sc.size(); ++q)
+  {
+    x.sd[q] = sc[q] * w;
+    x.rd[q] = rc[q] * w;
+    c->ctr_x += x.sd[q];
+  }
+  ck(tr->exchange_fn(tr->user, sb, x.sd.data(), rb, x.rd.data(), s), what);
+}
+
+// build-time exchange of host vectors: out[q] goes to rank q (out[me] empty), returns what every
+// rank sent to this one (counts first, then the payload, both through exchange_fn)
+std::vector<std::vector<double>> host_exchange(const fcg_transport* tr, const std::vector<std::vector<double>>& out,
+    hipStream_t s)
+{
+  const int R = tr->nranks, me = tr->rank;
+  std::vector<int64_t> one(static_cast<size_t>(R), 1);
+  one[static_cast<size_t>(me)] = 0;
+  std::vector<double> cnt_s, cnt_r(static_cast<size_t>(R - 1), 0.0);
+  for (int q = 0; q < R; ++q)
+    if (q != me) cnt_s.push_back(double(out[static_cast<size_t>(q)].size()));
+  DevBuf ds(R), dr(R);
+  ck(hipMemcpyAsync(ds.p, cnt_s.data(), sizeof(double) * cnt_s.size(), hipMemcpyHostToDevice, s), "hipMemcpyAsync");
+  ck(tr->exchange_fn(tr->user, ds.p, one.data(), dr.p, one.data(), s), "transport exchange (counts)");
+  ck(hipMemcpyAsync(cnt_r.data(), dr.p, sizeof(double) * cnt_r.size(), hipMemcpyDeviceToHost, s), "hipMemcpyAsync");
+  ck(hipStreamSynchronize(s), "hipStreamSynchronize");
+  std::vector<int64_t> sc(static_cast<size_t>(R), 0), rc(static_cast<size_t>(R), 0);
+  std::vector<double> flat;
+  for (int q = 0, k = 0; q < R; ++q)
+  {
+    if (q == me) continue;
+    sc[static_cast<size_t>(q)] = int64_t(out[static_cast<size_t>(q)].size());
+    rc[static_cast<size_t>(q)] = int64_t(cnt_r[static_cast<size_t>(k++)]);
+    flat.insert(flat.end(), out[static_cast<size_t>(q)].begin(), out[static_cast<size_t>(q)].end());
+  }
+  int64_t nr = 0;
+  for (int64_t v : rc) nr += v;
+  DevBuf ps(int64_t(flat.size())), pr(nr);
+  if (!flat.empty())
+    ck(hipMemcpyAsync(ps.p, flat.data(), sizeof(double) * flat.size(), hipMemcpyHostToDevice, s), "hipMemcpyAsync");
+  ck(tr->exchange_fn(tr->user, ps.p, sc.data(), pr.p, rc.data(), s), "transport exchange (build)");
+  std::vector<double> got(static_cast<size_t>(nr));
+  if (nr) ck(hipMemcpyAsync(got.data(), pr.p, sizeof(double) * static_cast<size_t>(nr), hipMemcpyDeviceToHost, s), "hipMemcpyAsync");
+  ck(hipStreamSynchronize(s), "hipStreamSynchronize");
+  std::vector<std::vector<double>> in(static_cast<size_t>(R));
+  for (int q = 0, o = 0; q < R; ++q)
+  {
+    in[static_cast<size_t>(q)].assign(got.begin() + o, got.begin() + o + rc[static_cast<size_t>(q)]);
+    o += int(rc[static_cast<size_t>(q)]);
+  }
+  return in;
+}
+
 // channel (k, col) of a 3 x 6 BSR's rows as a DOF vector: DOF d of owned node i gets entry
-// (d, col) of the row's k-th block (col < 0: the block's column id + off, -1 past the row's end)
+// (d, col) of the row's k-th block (col < 0: the block's global column id -- l2g[col] or col +
+// off --, -1 past the row's end)
 __global__ __launch_bounds__(kBlock) void pack_channel_kernel(int64_t nb, const int64_t* __restrict__ ptr,
     const int32_t* __restrict__ col, const double* __restrict__ vals, int k, int c, int64_t off,
     double* out)
@@ -1203,7 +1363,7 @@ __global__ __launch_bounds__(kBlock) void scatter_channel_kernel(int64_t nb, int
   if (p < ptr[i + 1]) vals[p * 18 + d * 6 + c] = in[3 * i + d];
 }
 
-// out[pos[k]] = vals[k] (36 doubles per block): this rank's blocks into the global A_1 buffer
+// out[pos[k]] = vals[k] (36 doubles per block): this rank's blocks into the replicated operator
 __global__ __launch_bounds__(kBlock) void scatter_blocks_kernel(int64_t nnzb, const int64_t* __restrict__ pos,
     const double* __restrict__ vals, double* out)
 {
@@ -1213,15 +1373,50 @@ __global__ __launch_bounds__(kBlock) void scatter_blocks_kernel(int64_t nnzb, co
   out[pos[k] * 36 + q] = vals[t];
 }
 
-// the owned rows of a 3 x 6 BSR (ids + off) followed by the ghost rows' ids, imported from their
-// owners one block slot at a time (M slots); returns the extended pattern
+// out[pos[k]] += vals[k] (36 doubles per block; pos unique within one launch)
+__global__ __launch_bounds__(kBlock) void add_blocks_kernel(int64_t nnzb, const int64_t* __restrict__ pos,
+    const double* __restrict__ vals, double* out)
+{
+  const int64_t t = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (t >= nnzb * 36) return;
+  const int64_t k = t / 36, q = t - 36 * k;
+  out[pos[k] * 36 + q] += vals[t];
+}
+
+// dst[k] = src[idx[k]] (6 doubles per item)
+__global__ __launch_bounds__(kBlock) void gather_items_kernel(int64_t n, const int32_t* __restrict__ idx,
+    const double* __restrict__ src, double* dst)
+{
+  const int64_t t = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (t >= n * 6) return;
+  const int64_t k = t / 6, c = t - 6 * k;
+  dst[t] = src[int64_t(idx[k]) * 6 + c];
+}
+
+// dst[idx[k]] += src[k] (6 doubles per item; idx unique within one launch)
+__global__ __launch_bounds__(kBlock) void add_items_kernel(int64_t n, const int32_t* __restrict__ idx,
+    const double* __restrict__ src, double* dst)
+{
+  const int64_t t = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (t >= n * 6) return;
+  const int64_t k = t / 6, c = t - 6 * k;
+  dst[int64_t(idx[k]) * 6 + c] += src[t];
+}
+
+void copy_dd(double* dst, const double* src, int64_t n, hipStream_t s)
+{
+  if (n > 0) ck(hipMemcpyAsync(dst, src, sizeof(double) * static_cast<size_t>(n), hipMemcpyDeviceToDevice, s), "copy");
+}
+
+// the owned rows of a 3 x 6 BSR (global ids) followed by the ghost rows' ids, imported from their
+// owners one block slot at a time (M slots); returns the extended pattern in global ids
 void extend_pattern(fcg_amg* h, Coupled* c, const Bsr& B, int64_t off, int M, const fcg_transport* tr,
     hipStream_t s, std::vector<int64_t>& pp, std::vector<int32_t>& pc)
 {
   const fcg::DeviceMesh& m = h->ctx->mesh;
   const int64_t nb0 = h->nb0, nc = c->nc_nodes;
-  std::vector<std::vector<int32_t>> gid(size_t(nc - nb0));
-  std::vector<double> colv(size_t(m.n_cols));
+  std::vector<std::vector<int32_t>> gid(static_cast<size_t>(nc - nb0));
+  std::vector<double> colv(static_cast<size_t>(m.n_cols));
   const dim3 gp(blocks_for(3 * std::max<int64_t>(1, nb0))), bl(kBlock);
   for (int k = 0; k < M; ++k)
   {
@@ -1232,24 +1427,24 @@ void extend_pattern(fcg_amg* h, Coupled* c, const Bsr& B, int64_t off, int M, co
     ck(hipStreamSynchronize(s), "hipStreamSynchronize");
     for (int64_t i = nb0; i < nc; ++i)
     {
-      const double id = colv[size_t(3 * i)];
-      if (id >= 0.0) gid[size_t(i - nb0)].push_back(int32_t(id));
+      const double id = colv[static_cast<size_t>(3 * i)];
+      if (id >= 0.0) gid[static_cast<size_t>(i - nb0)].push_back(int32_t(id));
     }
   }
-  pp.assign(size_t(nc) + 1, 0);
+  pp.assign(static_cast<size_t>(nc) + 1, 0);
   pc.clear();
   for (int64_t i = 0; i < nb0; ++i)
   {
-    for (int64_t k = B.ptr_h[size_t(i)]; k < B.ptr_h[size_t(i) + 1]; ++k) pc.push_back(int32_t(B.col_h[size_t(k)] + off));
-    pp[size_t(i) + 1] = int64_t(pc.size());
+    for (int64_t k = B.ptr_h[static_cast<size_t>(i)]; k < B.ptr_h[static_cast<size_t>(i) + 1]; ++k) pc.push_back(int32_t(B.col_h[static_cast<size_t>(k)] + off));
+    pp[static_cast<size_t>(i) + 1] = int64_t(pc.size());
   }
   for (int64_t i = nb0; i < nc; ++i)
   {
-    const auto& row = gid[size_t(i - nb0)];
+    const auto& row = gid[static_cast<size_t>(i - nb0)];
     for (size_t k = 1; k < row.size(); ++k)
       if (row[k] <= row[k - 1]) throw Fail{FCG_ERR_ARG, "coupled AMG: ghost row not sorted"};
     pc.insert(pc.end(), row.begin(), row.end());
-    pp[size_t(i) + 1] = int64_t(pc.size());
+    pp[static_cast<size_t>(i) + 1] = int64_t(pc.size());
   }
 }
 
@@ -1258,7 +1453,7 @@ void extend_values(fcg_amg* h, Coupled* c, const Bsr& B, Bsr& E, int M, const fc
 {
   const int64_t nb0 = h->nb0, nc = c->nc_nodes;
   if (B.nnzb > 0)
-    ck(hipMemcpyAsync(E.vals, B.vals, sizeof(double) * size_t(B.nnzb) * 18, hipMemcpyDeviceToDevice, s), "copy");
+    ck(hipMemcpyAsync(E.vals, B.vals, sizeof(double) * static_cast<size_t>(B.nnzb) * 18, hipMemcpyDeviceToDevice, s), "copy");
   const dim3 gp(blocks_for(3 * std::max<int64_t>(1, nb0))), gg(blocks_for(3 * std::max<int64_t>(1, nc - nb0))),
       bl(kBlock);
   for (int k = 0; k < M; ++k)
@@ -1275,15 +1470,131 @@ void extend_values(fcg_amg* h, Coupled* c, const Bsr& B, Bsr& E, int M, const fc
 
 int widest_over_ranks(const Bsr& B, int rank, int R, const fcg_transport* tr, hipStream_t s)
 {
-  std::vector<double> v(size_t(R), 0.0);
+  std::vector<double> v(static_cast<size_t>(R), 0.0);
   int64_t w = 0;
-  for (int64_t i = 0; i < B.n; ++i) w = std::max(w, B.ptr_h[size_t(i) + 1] - B.ptr_h[size_t(i)]);
-  v[size_t(rank)] = double(w);
+  for (int64_t i = 0; i < B.n; ++i) w = std::max(w, B.ptr_h[static_cast<size_t>(i) + 1] - B.ptr_h[static_cast<size_t>(i)]);
+  v[static_cast<size_t>(rank)] = double(w);
   host_allsum(tr, v, s);
   int M = 0;
   for (double x : v) M = std::max(M, int(x));
   return M;
 }
+
+// a BSR whose device arrays hold the pattern only (no values), freed with the object
+struct TmpPattern {
+  Bsr b;
+  TmpPattern(const std::vector<int64_t>& ptr, const std::vector<int32_t>& col)
+  {
+    b.n = int64_t(ptr.size()) - 1;
+    b.nnzb = ptr.back();
+    b.ptr_h = ptr;
+    b.col_h = col;
+    ck(hipMalloc(&b.ptr, sizeof(int64_t) * ptr.size()), "hipMalloc");
+    ck(hipMalloc(&b.col, sizeof(int32_t) * std::max<size_t>(1, col.size())), "hipMalloc");
+    ck(hipMemcpy(b.ptr, ptr.data(), sizeof(int64_t) * ptr.size(), hipMemcpyHostToDevice), "hipMemcpy");
+    if (!col.empty()) ck(hipMemcpy(b.col, col.data(), sizeof(int32_t) * col.size(), hipMemcpyHostToDevice), "hipMemcpy");
+  }
+  ~TmpPattern()
+  {
+    if (b.ptr) (void)hipFree(b.ptr);
+    if (b.col) (void)hipFree(b.col);
+  }
+  TmpPattern(const TmpPattern&) = delete;
+  TmpPattern& operator=(const TmpPattern&) = delete;
+};
+
+// the replicated operator's pattern: the union of every rank's blocks (rows row_off + i of its
+// part, global columns), gathered once, sorted and deduplicated identically everywhere; pos =
+// each of this rank's blocks in it
+void gather_replicated(Coupled* c, const fcg_transport* tr, const std::vector<int64_t>& cp,
+    const std::vector<int32_t>& cc, int64_t row_off, int64_t n_tot, hipStream_t s,
+    std::vector<int64_t>& gptr, std::vector<int32_t>& gcol, std::vector<int64_t>& pos)
+{
+  const int64_t R = c->nranks;
+  std::vector<int64_t> keys;
+  {
+    std::vector<double> cnt(static_cast<size_t>(R), 0.0);
+    cnt[static_cast<size_t>(c->rank)] = double(cc.size());
+    host_allsum(tr, cnt, s);
+    int64_t first = 0, total = 0;
+    for (int64_t q = 0; q < R; ++q)
+    {
+      if (q < c->rank) first += int64_t(cnt[static_cast<size_t>(q)]);
+      total += int64_t(cnt[static_cast<size_t>(q)]);
+    }
+    std::vector<double> pairs(static_cast<size_t>(2 * total), 0.0);
+    const int64_t nrows = int64_t(cp.size()) - 1;
+    for (int64_t i = 0; i < nrows; ++i)
+      for (int64_t k = cp[static_cast<size_t>(i)]; k < cp[static_cast<size_t>(i) + 1]; ++k)
+      {
+        pairs[static_cast<size_t>(2 * (first + k))] = double(row_off + i);
+        pairs[static_cast<size_t>(2 * (first + k) + 1)] = double(cc[static_cast<size_t>(k)]);
+      }
+    host_allsum(tr, pairs, s);
+    keys.resize(static_cast<size_t>(total));
+    for (int64_t k = 0; k < total; ++k)
+      keys[static_cast<size_t>(k)] = int64_t(pairs[static_cast<size_t>(2 * k)]) * n_tot + int64_t(pairs[static_cast<size_t>(2 * k + 1)]);
+    std::sort(keys.begin(), keys.end());
+    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+  }
+  gptr.assign(static_cast<size_t>(n_tot) + 1, 0);
+  gcol.assign(keys.size(), 0);
+  for (size_t k = 0; k < keys.size(); ++k)
+  {
+    gptr[static_cast<size_t>(keys[k] / n_tot) + 1] += 1;
+    gcol[k] = int32_t(keys[k] % n_tot);
+  }
+  for (int64_t i = 0; i < n_tot; ++i) gptr[static_cast<size_t>(i) + 1] += gptr[static_cast<size_t>(i)];
+  pos.assign(cc.size(), 0);
+  const int64_t nrows = int64_t(cp.size()) - 1;
+  for (int64_t i = 0; i < nrows; ++i)
+    for (int64_t k = cp[static_cast<size_t>(i)]; k < cp[static_cast<size_t>(i) + 1]; ++k)
+      pos[static_cast<size_t>(k)] = int64_t(std::lower_bound(keys.begin(), keys.end(), (row_off + i) * n_tot + cc[static_cast<size_t>(k)]) - keys.begin());
+}
+
+// the replicated hierarchy below the replicated operator (pattern gptr / gcol, near-null space ns)
+void build_replicated(fcg_amg* h, Coupled* c, std::vector<int64_t> gptr, std::vector<int32_t> gcol,
+    int64_t n_tot, std::vector<double> ns)
+{
+  fcg_amg* g = new fcg_amg();
+  c->g = g;
+  g->ctx = h->ctx;
+  g->device = h->device;
+  g->opt = h->opt;
+  g->steps.emplace_back();  // step 0 (into the replicated level) is the ranks' prolongator
+  g->levels.emplace_back();
+  {
+    Level& L1 = g->levels[0];
+    make_bsr(g, L1.A, std::move(gptr), std::move(gcol), 6, 6, n_tot);
+    L1.diag = upload(g, diag_index(L1.A));
+    L1.dinv = dalloc<double>(g, 36 * n_tot);
+    for (double** v : {&L1.x, &L1.b, &L1.r, &L1.d, &L1.z, &L1.p, &L1.q}) *v = dalloc<double>(g, 6 * n_tot);
+  }
+  c->rep_nnzb = g->levels[0].A.nnzb;
+  c->rep_n = n_tot;
+  coarsen(g, &g->levels[0].A, 6, std::move(ns), nullptr);
+  g->partial = dalloc<double>(g, kMaxPartials);
+  g->sc = dalloc<double>(g, 16);
+  g->flag = dalloc<int32_t>(g, 1);
+  c->gb = dalloc<double>(h, 6 * n_tot);
+  c->ge = dalloc<double>(h, 6 * n_tot);
+}
+
+// FCG_AMG_DIST=1: distribute level 1 whenever the transport can exchange; 0: never; default: when
+// its global size passes FCG_AMG_DIST_MIN DOFs (50000).  The inputs are the same on every rank.
+bool distribute_level1(const fcg_transport* tr, int64_t n_agg_tot, int64_t min_agg_per_rank)
+{
+  if (!tr->exchange_fn || min_agg_per_rank < 1) return false;
+  const char* e = std::getenv("FCG_AMG_DIST");
+  if (e && e[0] == '0') return false;
+  if (e && e[0] == '1') return true;
+  const char* m = std::getenv("FCG_AMG_DIST_MIN");
+  const int64_t min_dofs = m ? std::atoll(m) : 50000;
+  return 6 * n_agg_tot > min_dofs;
+}
+
+void build_dist(fcg_amg* h, Coupled* c, const fcg_transport* tr, const std::vector<int64_t>& counts,
+    const std::vector<int64_t>& LA, hipStream_t s);
 
 void coupled_build(fcg_amg* h, const fcg_transport* tr, hipStream_t s)
 {
@@ -1296,130 +1607,479 @@ void coupled_build(fcg_amg* h, const fcg_transport* tr, hipStream_t s)
   const int64_t nb0 = h->nb0, nc = c->nc_nodes, R = c->nranks;
   const Step& st0 = h->steps[0];
   // aggregates per rank: the global numbering by rank offsets
+  std::vector<int64_t> counts(static_cast<size_t>(R), 0);
+  int64_t min_agg = 0;
   {
-    std::vector<double> v(size_t(R), 0.0);
-    v[size_t(c->rank)] = double(st0.n_agg);
+    std::vector<double> v(static_cast<size_t>(R), 0.0);
+    v[static_cast<size_t>(c->rank)] = double(st0.n_agg);
     host_allsum(tr, v, s);
+    min_agg = int64_t(v[0]);
     for (int64_t q = 0; q < R; ++q)
     {
-      if (q < c->rank) c->off += int64_t(v[size_t(q)]);
-      c->n_agg_tot += int64_t(v[size_t(q)]);
+      counts[static_cast<size_t>(q)] = int64_t(v[static_cast<size_t>(q)]);
+      if (q < c->rank) c->off += counts[static_cast<size_t>(q)];
+      c->n_agg_tot += counts[static_cast<size_t>(q)];
+      min_agg = std::min(min_agg, counts[static_cast<size_t>(q)]);
     }
   }
+  const bool dist = distribute_level1(tr, c->n_agg_tot, min_agg);
   c->chan = dalloc<double>(h, 3 * nb0);
   c->chan_col = dalloc<double>(h, m.n_cols);
   c->q = dalloc<double>(h, 3 * nb0);
   c->w = dalloc<double>(h, 3 * nb0);
-  c->gb = dalloc<double>(h, 6 * c->n_agg_tot);
-  c->ge = dalloc<double>(h, 6 * c->n_agg_tot);
   make_bsr(h, c->Afull, h->full_ptr, h->full_col, 3, 3, nc);
-  {
-    std::vector<int32_t> ag(static_cast<size_t>(nb0));
-    ck(hipMemcpy(ag.data(), st0.agg, sizeof(int32_t) * ag.size(), hipMemcpyDeviceToHost), "hipMemcpy");
-    for (auto& a : ag)
-      if (a >= 0) a = int32_t(a + c->off);
-    c->agg = upload(h, ag);
-  }
   // T_0 with the ghost rows of its owners (one block per row), then P = (I - w D^-1 A) T_ext on
-  // the pattern of A_full T_ext: P's rows reach the neighbour ranks' aggregates
+  // the pattern of A_full T_ext: P's rows reach the neighbour ranks' aggregates (global ids)
   std::vector<int64_t> pp, ap, tp, cp;
   std::vector<int32_t> pc, apc, tc, cc;
   extend_pattern(h, c, st0.T, c->off, widest_over_ranks(st0.T, c->rank, int(R), tr, s), tr, s, pp, pc);
-  make_bsr(h, c->Text, pp, pc, 3, 6, c->n_agg_tot);
-  symbolic(c->Afull, c->Text.ptr_h, c->Text.col_h, c->n_agg_tot, ap, apc);
-  make_bsr(h, c->AT, ap, apc, 3, 6, c->n_agg_tot);
-  make_bsr(h, c->P, ap, apc, 3, 6, c->n_agg_tot);
-  tp.assign(size_t(c->n_agg_tot) + 1, 0);
-  tc.assign(size_t(std::max<int64_t>(ap.back(), 1)), 0);
-  std::vector<int64_t> perm(size_t(std::max<int64_t>(ap.back(), 1)));
-  ck(fcg_bsr_transpose_pattern(nb0, c->n_agg_tot, ap.data(), apc.data(), tp.data(), tc.data(), perm.data()),
+  std::vector<int64_t> LA;  // P's aggregate numbering: global ids (replicated) or LA (distributed)
+  int64_t n_p_cols = c->n_agg_tot;
+  std::vector<int64_t> pp2;
+  std::vector<int32_t> pc2;
+  {
+    // P's pattern and its ghost rows (global ids)
+    symbolic(c->Afull, pp, pc, c->n_agg_tot, ap, apc);
+    TmpPattern Pg(ap, apc);
+    c->M = widest_over_ranks(Pg.b, c->rank, int(R), tr, s);
+    extend_pattern(h, c, Pg.b, 0, c->M, tr, s, pp2, pc2);
+  }
+  std::vector<int32_t> agg_h(static_cast<size_t>(nb0));
+  ck(hipMemcpy(agg_h.data(), st0.agg, sizeof(int32_t) * agg_h.size(), hipMemcpyDeviceToHost), "hipMemcpy");
+  if (dist)
+  {
+    // LA: the aggregates P_ext reaches, ascending (the order of every pattern row is kept)
+    LA.assign(pc2.begin(), pc2.end());
+    std::sort(LA.begin(), LA.end());
+    LA.erase(std::unique(LA.begin(), LA.end()), LA.end());
+    auto g2l = [&](int32_t g) {
+      const auto it = std::lower_bound(LA.begin(), LA.end(), int64_t(g));
+      if (it == LA.end() || *it != g) throw Fail{FCG_ERR_ARG, "coupled AMG: aggregate outside P_ext's columns"};
+      return int32_t(it - LA.begin());
+    };
+    for (auto* v : {&pc, &apc, &pc2})
+      for (auto& x : *v) x = g2l(x);
+    n_p_cols = int64_t(LA.size());
+    const int64_t own0 = int64_t(std::lower_bound(LA.begin(), LA.end(), c->off) - LA.begin());
+    for (auto& a : agg_h)
+      if (a >= 0) a = int32_t(a + own0);
+  }
+  else
+    for (auto& a : agg_h)
+      if (a >= 0) a = int32_t(a + c->off);
+  c->agg = upload(h, agg_h);
+  make_bsr(h, c->Text, pp, pc, 3, 6, n_p_cols);
+  make_bsr(h, c->AT, ap, apc, 3, 6, n_p_cols);
+  make_bsr(h, c->P, ap, apc, 3, 6, n_p_cols);
+  tp.assign(static_cast<size_t>(n_p_cols) + 1, 0);
+  tc.assign(static_cast<size_t>(std::max<int64_t>(ap.back(), 1)), 0);
+  std::vector<int64_t> perm(static_cast<size_t>(std::max<int64_t>(ap.back(), 1)));
+  ck(fcg_bsr_transpose_pattern(nb0, n_p_cols, ap.data(), apc.data(), tp.data(), tc.data(), perm.data()),
       "fcg_bsr_transpose_pattern");
-  tc.resize(size_t(ap.back()));
-  perm.resize(size_t(ap.back()));
+  tc.resize(static_cast<size_t>(ap.back()));
+  perm.resize(static_cast<size_t>(ap.back()));
   make_bsr(h, c->Pt, tp, tc, 6, 3, nb0);
   c->p_perm = upload(h, perm);
-  // P's ghost rows from their owners, then this rank's part of A_1 = P^T (A P)
-  c->M = widest_over_ranks(c->P, c->rank, int(R), tr, s);
-  extend_pattern(h, c, c->P, 0, c->M, tr, s, pp, pc);
-  make_bsr(h, c->Pext, pp, pc, 3, 6, c->n_agg_tot);
-  symbolic(c->Afull, c->Pext.ptr_h, c->Pext.col_h, c->n_agg_tot, ap, apc);
-  make_bsr(h, c->AP, ap, apc, 3, 6, c->n_agg_tot);
-  symbolic(c->Pt, ap, apc, c->n_agg_tot, cp, cc);
-  make_bsr(h, c->C, cp, cc, 6, 6, c->n_agg_tot);
-  // the global A_1 pattern = the union of the ranks' parts: every rank's (row, column) pairs
-  // gathered (counts, then the pairs in rank order), sorted and deduplicated identically everywhere
-  std::vector<int64_t> keys;
+  // this rank's part of A_1 = P^T (A P_ext)
+  make_bsr(h, c->Pext, pp2, pc2, 3, 6, n_p_cols);
+  std::vector<int64_t> app;
+  std::vector<int32_t> appc;
+  symbolic(c->Afull, c->Pext.ptr_h, c->Pext.col_h, n_p_cols, app, appc);
+  make_bsr(h, c->AP, app, appc, 3, 6, n_p_cols);
+  symbolic(c->Pt, app, appc, n_p_cols, cp, cc);
+  make_bsr(h, c->C, cp, cc, 6, 6, n_p_cols);
+  if (dist)
+    build_dist(h, c, tr, counts, LA, s);
+  else
   {
-    std::vector<double> cnt(size_t(R), 0.0);
-    cnt[size_t(c->rank)] = double(cc.size());
-    host_allsum(tr, cnt, s);
-    int64_t first = 0, total = 0;
-    for (int64_t q = 0; q < R; ++q)
-    {
-      if (q < c->rank) first += int64_t(cnt[size_t(q)]);
-      total += int64_t(cnt[size_t(q)]);
-    }
-    std::vector<double> pairs(size_t(2 * total), 0.0);
-    for (int64_t i = 0; i < c->n_agg_tot; ++i)
-      for (int64_t k = cp[size_t(i)]; k < cp[size_t(i) + 1]; ++k)
-      {
-        pairs[size_t(2 * (first + k))] = double(i);
-        pairs[size_t(2 * (first + k) + 1)] = double(cc[size_t(k)]);
-      }
-    host_allsum(tr, pairs, s);
-    keys.resize(size_t(total));
-    for (int64_t k = 0; k < total; ++k)
-      keys[size_t(k)] = int64_t(pairs[size_t(2 * k)]) * c->n_agg_tot + int64_t(pairs[size_t(2 * k + 1)]);
-    std::sort(keys.begin(), keys.end());
-    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+    std::vector<int64_t> gptr, pos;
+    std::vector<int32_t> gcol;
+    gather_replicated(c, tr, cp, cc, 0, c->n_agg_tot, s, gptr, gcol, pos);
+    c->rep_part = &c->C;
+    c->rep_pos = upload(h, pos);
+    // level 1's near-null space: each aggregate's R factor from its owner
+    std::vector<double> ns(static_cast<size_t>(36 * c->n_agg_tot), 0.0);
+    std::copy(h->ns1.begin(), h->ns1.end(), ns.begin() + 36 * c->off);
+    host_allsum(tr, ns, s);
+    build_replicated(h, c, std::move(gptr), std::move(gcol), c->n_agg_tot, std::move(ns));
   }
-  c->a1_nnzb = int64_t(keys.size());
-  std::vector<int64_t> gptr(size_t(c->n_agg_tot) + 1, 0);
-  std::vector<int32_t> gcol(keys.size());
-  for (size_t k = 0; k < keys.size(); ++k)
-  {
-    gptr[size_t(keys[k] / c->n_agg_tot) + 1] += 1;
-    gcol[k] = int32_t(keys[k] % c->n_agg_tot);
-  }
-  for (int64_t i = 0; i < c->n_agg_tot; ++i) gptr[size_t(i) + 1] += gptr[size_t(i)];
-  {
-    std::vector<int64_t> pos(cc.size());
-    for (int64_t i = 0; i < c->n_agg_tot; ++i)
-      for (int64_t k = cp[size_t(i)]; k < cp[size_t(i) + 1]; ++k)
-        pos[size_t(k)] = int64_t(std::lower_bound(keys.begin(), keys.end(), i * c->n_agg_tot + cc[size_t(k)]) - keys.begin());
-    c->c_pos = upload(h, pos);
-  }
-  // level 1's near-null space: each aggregate's R factor from its owner
-  std::vector<double> ns(size_t(36 * c->n_agg_tot), 0.0);
-  std::copy(h->ns1.begin(), h->ns1.end(), ns.begin() + 36 * c->off);
-  host_allsum(tr, ns, s);
-  // the replicated hierarchy (identical on every rank: same input, deterministic build)
-  fcg_amg* g = new fcg_amg();
-  c->g = g;
-  g->ctx = h->ctx;
-  g->device = h->device;
-  g->opt = h->opt;
-  g->steps.emplace_back();  // step 0 (level 0 -> 1) is the ranks' P
-  g->levels.emplace_back();
-  {
-    Level& L1 = g->levels[0];
-    make_bsr(g, L1.A, gptr, gcol, 6, 6, c->n_agg_tot);
-    L1.diag = upload(g, diag_index(L1.A));
-    L1.dinv = dalloc<double>(g, 36 * c->n_agg_tot);
-    for (double** v : {&L1.x, &L1.b, &L1.r, &L1.d, &L1.z, &L1.p, &L1.q}) *v = dalloc<double>(g, 6 * c->n_agg_tot);
-  }
-  coarsen(g, &g->levels[0].A, 6, std::move(ns), nullptr);
   // T_0's ghost rows: the tentative prolongator is fixed at create, so they are imported once
   extend_values(h, c, st0.T, c->Text, 1, tr, s);
-  g->partial = dalloc<double>(g, kMaxPartials);
-  g->sc = dalloc<double>(g, 16);
-  g->flag = dalloc<int32_t>(g, 1);
+}
+
+void build_dist(fcg_amg* h, Coupled* c, const fcg_transport* tr, const std::vector<int64_t>& counts,
+    const std::vector<int64_t>& LA, hipStream_t s)
+{
+  Dist* d = new Dist();
+  c->d = d;
+  const int R = c->nranks, me = c->rank;
+  d->R = R;
+  d->me = me;
+  d->agg_off.assign(static_cast<size_t>(R) + 1, 0);
+  for (int q = 0; q < R; ++q) d->agg_off[static_cast<size_t>(q) + 1] = d->agg_off[static_cast<size_t>(q)] + counts[static_cast<size_t>(q)];
+  d->off = c->off;
+  d->na = counts[static_cast<size_t>(me)];
+  d->NL = int64_t(LA.size());
+  d->own0 = int64_t(std::lower_bound(LA.begin(), LA.end(), d->off) - LA.begin());
+  const int64_t na = d->na, own0 = d->own0, off = d->off;
+  if (own0 + na > d->NL || LA[static_cast<size_t>(own0)] != off || LA[static_cast<size_t>(own0 + na - 1)] != off + na - 1)
+    throw Fail{FCG_ERR_ARG, "coupled AMG: an owned aggregate is missing from P's columns"};
+  auto owner = [&](int64_t gid) {
+    return int(std::upper_bound(d->agg_off.begin(), d->agg_off.end(), gid) - d->agg_off.begin()) - 1;
+  };
+  const Bsr& C = c->C;
+  d->c_lo = C.ptr_h[static_cast<size_t>(own0)];
+  d->c_hi = C.ptr_h[static_cast<size_t>(own0 + na)];
+  // 1. the partial rows of the other ranks' aggregates go to their owners: (row, column) pairs once
+  std::vector<std::vector<double>> out(static_cast<size_t>(R));
+  d->rows.scnt.assign(static_cast<size_t>(R), 0);
+  for (int64_t r = 0; r < d->NL; ++r)
+  {
+    if (r >= own0 && r < own0 + na) continue;
+    const int q = owner(LA[static_cast<size_t>(r)]);
+    for (int64_t k = C.ptr_h[static_cast<size_t>(r)]; k < C.ptr_h[static_cast<size_t>(r) + 1]; ++k)
+    {
+      out[static_cast<size_t>(q)].push_back(double(LA[static_cast<size_t>(r)]));
+      out[static_cast<size_t>(q)].push_back(double(LA[static_cast<size_t>(C.col_h[static_cast<size_t>(k)])]));
+    }
+    d->rows.scnt[static_cast<size_t>(q)] += C.ptr_h[static_cast<size_t>(r) + 1] - C.ptr_h[static_cast<size_t>(r)];
+  }
+  std::vector<std::vector<double>> in = host_exchange(tr, out, s);
+  d->rows.rcnt.assign(static_cast<size_t>(R), 0);
+  std::vector<std::vector<int64_t>> rowcols(static_cast<size_t>(na));
+  for (int64_t i = 0; i < na; ++i)
+  {
+    rowcols[static_cast<size_t>(i)].push_back(off + i);  // the diagonal block
+    for (int64_t k = C.ptr_h[static_cast<size_t>(own0 + i)]; k < C.ptr_h[static_cast<size_t>(own0 + i) + 1]; ++k)
+      rowcols[static_cast<size_t>(i)].push_back(LA[static_cast<size_t>(C.col_h[static_cast<size_t>(k)])]);
+  }
+  for (int q = 0; q < R; ++q)
+  {
+    const auto& v = in[static_cast<size_t>(q)];
+    d->rows.rcnt[static_cast<size_t>(q)] = int64_t(v.size() / 2);
+    for (size_t k = 0; k + 1 < v.size(); k += 2)
+    {
+      const int64_t rg = int64_t(v[k]);
+      if (rg < off || rg >= off + na) throw Fail{FCG_ERR_ARG, "coupled AMG: partial row sent to the wrong rank"};
+      rowcols[static_cast<size_t>(rg - off)].push_back(int64_t(v[k + 1]));
+    }
+  }
+  d->rows.finish();
+  std::vector<int64_t> DA;
+  for (auto& row : rowcols)
+  {
+    std::sort(row.begin(), row.end());
+    row.erase(std::unique(row.begin(), row.end()), row.end());
+    DA.insert(DA.end(), row.begin(), row.end());
+  }
+  std::sort(DA.begin(), DA.end());
+  DA.erase(std::unique(DA.begin(), DA.end()), DA.end());
+  d->NA = int64_t(DA.size());
+  d->d0 = int64_t(std::lower_bound(DA.begin(), DA.end(), off) - DA.begin());
+  auto da = [&](int64_t g) { return int32_t(std::lower_bound(DA.begin(), DA.end(), g) - DA.begin()); };
+  std::vector<int64_t> aptr(static_cast<size_t>(na) + 1, 0);
+  std::vector<int32_t> acol;
+  for (int64_t i = 0; i < na; ++i)
+  {
+    for (int64_t g : rowcols[static_cast<size_t>(i)]) acol.push_back(da(g));
+    aptr[static_cast<size_t>(i) + 1] = int64_t(acol.size());
+  }
+  make_bsr(h, d->A, aptr, acol, 6, 6, d->NA);
+  auto block_of = [&](int64_t i, int32_t col) {
+    const auto b = acol.begin() + aptr[static_cast<size_t>(i)], e = acol.begin() + aptr[static_cast<size_t>(i) + 1];
+    const auto it = std::lower_bound(b, e, col);
+    if (it == e || *it != col) throw Fail{FCG_ERR_ARG, "coupled AMG: level-1 block not in the pattern"};
+    return int64_t(it - acol.begin());
+  };
+  {
+    std::vector<int64_t> diag(static_cast<size_t>(na)), po(static_cast<size_t>(d->c_hi - d->c_lo)), pr(static_cast<size_t>(d->rows.nr));
+    for (int64_t i = 0; i < na; ++i)
+    {
+      diag[static_cast<size_t>(i)] = block_of(i, int32_t(d->d0 + i));
+      for (int64_t k = C.ptr_h[static_cast<size_t>(own0 + i)]; k < C.ptr_h[static_cast<size_t>(own0 + i) + 1]; ++k)
+        po[static_cast<size_t>(k - d->c_lo)] = block_of(i, da(LA[static_cast<size_t>(C.col_h[static_cast<size_t>(k)])]));
+    }
+    int64_t o = 0;
+    for (int q = 0; q < R; ++q)
+    {
+      const auto& v = in[static_cast<size_t>(q)];
+      for (size_t k = 0; k + 1 < v.size(); k += 2)
+        pr[static_cast<size_t>(o++)] = block_of(int64_t(v[k]) - off, da(int64_t(v[k + 1])));
+    }
+    d->diag = upload(h, diag);
+    d->pos_own = upload(h, po);
+    d->pos_recv = upload(h, pr);
+  }
+  d->dinv = dalloc<double>(h, 36 * na);
+  d->rows_s = dalloc<double>(h, 36 * d->rows.ns);
+  d->rows_r = dalloc<double>(h, 36 * d->rows.nr);
+  // 2. the level-1 import: A's ghost columns (DA outside [d0, d0 + na)) from their owners
+  {
+    std::vector<std::vector<double>> req(static_cast<size_t>(R));
+    d->imp.rcnt.assign(static_cast<size_t>(R), 0);
+    for (int64_t j = 0; j < d->NA; ++j)
+    {
+      if (j >= d->d0 && j < d->d0 + na) continue;
+      const int q = owner(DA[static_cast<size_t>(j)]);
+      req[static_cast<size_t>(q)].push_back(double(DA[static_cast<size_t>(j)]));
+      d->imp.rcnt[static_cast<size_t>(q)] += 1;
+    }
+    std::vector<std::vector<double>> want = host_exchange(tr, req, s);
+    d->imp.scnt.assign(static_cast<size_t>(R), 0);
+    std::vector<int32_t> idx;
+    for (int q = 0; q < R; ++q)
+    {
+      d->imp.scnt[static_cast<size_t>(q)] = int64_t(want[static_cast<size_t>(q)].size());
+      for (double g : want[static_cast<size_t>(q)])
+      {
+        const int64_t l = int64_t(g) - off;
+        if (l < 0 || l >= na) throw Fail{FCG_ERR_ARG, "coupled AMG: import request for a foreign aggregate"};
+        idx.push_back(int32_t(l));
+      }
+    }
+    d->imp.finish();
+    d->imp_idx = upload(h, idx);
+    d->imp_idx_h = std::move(idx);
+    d->imp_s = dalloc<double>(h, 6 * d->imp.ns);
+    d->imp_r = dalloc<double>(h, 6 * d->imp.nr);
+    d->xe = dalloc<double>(h, 6 * d->NA);
+  }
+  // 3. restriction / prolongation: LA's other-rank aggregates with their owners
+  {
+    std::vector<std::vector<double>> req(static_cast<size_t>(R));
+    d->pex.scnt.assign(static_cast<size_t>(R), 0);
+    for (int64_t r = 0; r < d->NL; ++r)
+    {
+      if (r >= own0 && r < own0 + na) continue;
+      const int q = owner(LA[static_cast<size_t>(r)]);
+      req[static_cast<size_t>(q)].push_back(double(LA[static_cast<size_t>(r)]));
+      d->pex.scnt[static_cast<size_t>(q)] += 1;
+    }
+    std::vector<std::vector<double>> got = host_exchange(tr, req, s);
+    d->pex.rcnt.assign(static_cast<size_t>(R), 0);
+    std::vector<int32_t> idx;
+    for (int q = 0; q < R; ++q)
+    {
+      d->pex.rcnt[static_cast<size_t>(q)] = int64_t(got[static_cast<size_t>(q)].size());
+      for (double g : got[static_cast<size_t>(q)])
+      {
+        const int64_t l = int64_t(g) - off;
+        if (l < 0 || l >= na) throw Fail{FCG_ERR_ARG, "coupled AMG: restriction entry for a foreign aggregate"};
+        idx.push_back(int32_t(l));
+      }
+    }
+    d->pex.finish();
+    d->pex_idx = upload(h, idx);
+    d->pex_s = dalloc<double>(h, 6 * d->pex.ns);
+    d->pex_r = dalloc<double>(h, 6 * d->pex.nr);
+    d->y = dalloc<double>(h, 6 * d->NL);
+  }
+  for (double** v : {&d->x, &d->b, &d->r, &d->dd, &d->z, &d->p, &d->q}) *v = dalloc<double>(h, 6 * na);
+  // 4. level 2: a rank-local aggregation of A's owned block, its tentative prolongator T_1
+  std::vector<int32_t> agg1(static_cast<size_t>(na), -1);
+  std::vector<double> tent(static_cast<size_t>(na) * 36), ns2;
+  {
+    std::vector<int64_t> optr(static_cast<size_t>(na) + 1, 0);
+    std::vector<int32_t> ocol;
+    for (int64_t i = 0; i < na; ++i)
+    {
+      for (int64_t k = aptr[static_cast<size_t>(i)]; k < aptr[static_cast<size_t>(i) + 1]; ++k)
+        if (acol[static_cast<size_t>(k)] >= d->d0 && acol[static_cast<size_t>(k)] < d->d0 + na) ocol.push_back(int32_t(acol[static_cast<size_t>(k)] - d->d0));
+      optr[static_cast<size_t>(i) + 1] = int64_t(ocol.size());
+    }
+    d->n2 = fcg_amg_aggregate(na, optr.data(), ocol.data(), nullptr, agg1.data());
+    if (d->n2 <= 0) throw Fail{FCG_ERR_ARG, "coupled AMG: level-1 aggregation failed"};
+    ns2.assign(static_cast<size_t>(d->n2) * 36, 0.0);
+    int64_t nd = 0;
+    ck(fcg_amg_tentative(na, 6, h->ns1.data(), agg1.data(), d->n2, tent.data(), ns2.data(), &nd),
+        "fcg_amg_tentative (level 1)");
+  }
+  std::vector<int64_t> counts2(static_cast<size_t>(R), 0);
+  {
+    std::vector<double> v(static_cast<size_t>(R), 0.0);
+    v[static_cast<size_t>(me)] = double(d->n2);
+    host_allsum(tr, v, s);
+    for (int q = 0; q < R; ++q)
+    {
+      counts2[static_cast<size_t>(q)] = int64_t(v[static_cast<size_t>(q)]);
+      if (q < me) d->off2 += counts2[static_cast<size_t>(q)];
+      d->n2_tot += counts2[static_cast<size_t>(q)];
+    }
+  }
+  {
+    std::vector<int64_t> tptr(static_cast<size_t>(na) + 1, 0);
+    std::vector<int32_t> tcol;
+    std::vector<double> tv;
+    for (int64_t i = 0; i < na; ++i)
+    {
+      if (agg1[static_cast<size_t>(i)] >= 0)
+      {
+        tcol.push_back(agg1[static_cast<size_t>(i)]);
+        tv.insert(tv.end(), tent.begin() + 36 * i, tent.begin() + 36 * (i + 1));
+      }
+      tptr[static_cast<size_t>(i) + 1] = int64_t(tcol.size());
+    }
+    make_bsr(h, d->T1, tptr, tcol, 6, 6, d->n2);
+    if (!tv.empty())
+      ck(hipMemcpy(d->T1.vals, tv.data(), sizeof(double) * tv.size(), hipMemcpyHostToDevice), "hipMemcpy");
+    std::vector<int64_t> ttp(static_cast<size_t>(d->n2) + 1, 0), perm(std::max<size_t>(1, tcol.size()));
+    std::vector<int32_t> ttc(std::max<size_t>(1, tcol.size()), 0);
+    ck(fcg_bsr_transpose_pattern(na, d->n2, tptr.data(), tcol.data(), ttp.data(), ttc.data(), perm.data()),
+        "fcg_bsr_transpose_pattern (T_1)");
+    ttc.resize(tcol.size());
+    perm.resize(tcol.size());
+    make_bsr(h, d->T1t, ttp, ttc, 6, 6, na);
+    const int64_t* dperm = upload(h, perm);
+    if (d->T1.nnzb > 0)
+      ck(fcg_bsr_transpose_values(h->device, 6, 6, d->T1.nnzb, dperm, d->T1.vals, d->T1t.vals, s),
+          "fcg_bsr_transpose_values (T_1)");
+  }
+  // T_1,ext: A's column rows of T_1 (global level-2 ids), the ghost ones from their owners once
+  {
+    std::vector<std::vector<double>> rowsout(static_cast<size_t>(R));
+    for (int q = 0, o = 0; q < R; ++q)
+      for (int64_t k = 0; k < d->imp.scnt[static_cast<size_t>(q)]; ++k)
+      {
+        const int32_t l = d->imp_idx_h[static_cast<size_t>(o++)];
+        const int32_t a = agg1[static_cast<size_t>(l)];
+        rowsout[static_cast<size_t>(q)].push_back(a >= 0 ? double(d->off2 + a) : -1.0);
+        for (int t = 0; t < 36; ++t) rowsout[static_cast<size_t>(q)].push_back(a >= 0 ? tent[static_cast<size_t>(36 * l + t)] : 0.0);
+      }
+    std::vector<std::vector<double>> rin = host_exchange(tr, rowsout, s);
+    std::vector<double> gh;  // the ghost rows in DA order (ascending global id = rank order)
+    for (int q = 0; q < R; ++q) gh.insert(gh.end(), rin[static_cast<size_t>(q)].begin(), rin[static_cast<size_t>(q)].end());
+    if (int64_t(gh.size()) != 37 * d->imp.nr) throw Fail{FCG_ERR_ARG, "coupled AMG: T_1 ghost rows incomplete"};
+    std::vector<int64_t> eptr(static_cast<size_t>(d->NA) + 1, 0);
+    std::vector<int32_t> ecol;
+    std::vector<double> ev;
+    for (int64_t j = 0, gi = 0; j < d->NA; ++j)
+    {
+      if (j >= d->d0 && j < d->d0 + na)
+      {
+        const int64_t l = j - d->d0;
+        if (agg1[static_cast<size_t>(l)] >= 0)
+        {
+          ecol.push_back(int32_t(d->off2 + agg1[static_cast<size_t>(l)]));
+          ev.insert(ev.end(), tent.begin() + 36 * l, tent.begin() + 36 * (l + 1));
+        }
+      }
+      else
+      {
+        const double* row = gh.data() + 37 * gi++;
+        if (row[0] >= 0.0)
+        {
+          ecol.push_back(int32_t(row[0]));
+          ev.insert(ev.end(), row + 1, row + 37);
+        }
+      }
+      eptr[static_cast<size_t>(j) + 1] = int64_t(ecol.size());
+    }
+    make_bsr(h, d->T1ext, eptr, ecol, 6, 6, d->n2_tot);
+    if (!ev.empty())
+      ck(hipMemcpy(d->T1ext.vals, ev.data(), sizeof(double) * ev.size(), hipMemcpyHostToDevice), "hipMemcpy");
+  }
+  // A T_1,ext and this rank's (complete) rows of A_2 = T_1^T A T_1,ext
+  std::vector<int64_t> a1p, c2p;
+  std::vector<int32_t> a1c, c2c;
+  symbolic(d->A, d->T1ext.ptr_h, d->T1ext.col_h, d->n2_tot, a1p, a1c);
+  make_bsr(h, d->AT1, a1p, a1c, 6, 6, d->n2_tot);
+  symbolic(d->T1t, a1p, a1c, d->n2_tot, c2p, c2c);
+  make_bsr(h, d->C2, c2p, c2c, 6, 6, d->n2_tot);
+  std::vector<int64_t> gptr, pos;
+  std::vector<int32_t> gcol;
+  gather_replicated(c, tr, c2p, c2c, d->off2, d->n2_tot, s, gptr, gcol, pos);
+  c->rep_part = &d->C2;
+  c->rep_pos = upload(h, pos);
+  std::vector<double> nsg(static_cast<size_t>(36 * d->n2_tot), 0.0);
+  std::copy(ns2.begin(), ns2.end(), nsg.begin() + 36 * d->off2);
+  host_allsum(tr, nsg, s);
+  build_replicated(h, c, std::move(gptr), std::move(gcol), d->n2_tot, std::move(nsg));
+}
+
+// y = A_1 x on the owned rows: x into the extended vector, its ghost entries imported
+void dist_spmv(fcg_amg* h, Dist* d, const fcg_transport* tr, const double* x, double* y, hipStream_t s)
+{
+  Coupled* c = h->cpl;
+  copy_dd(d->xe + 6 * d->d0, x, 6 * d->na, s);
+  if (d->imp.ns > 0)
+    hipLaunchKernelGGL(gather_items_kernel, dim3(blocks_for(6 * d->imp.ns)), dim3(kBlock), 0, s, d->imp.ns,
+        d->imp_idx, x, d->imp_s);
+  ck(hipGetLastError(), "gather_items_kernel");
+  exchange_counted(c, tr, d->imp, 6, false, d->imp_s, d->imp_r, s, "transport exchange (level-1 import)");
+  copy_dd(d->xe, d->imp_r, 6 * d->d0, s);
+  copy_dd(d->xe + 6 * (d->d0 + d->na), d->imp_r + 6 * d->d0, 6 * (d->NA - d->d0 - d->na), s);
+  ck(fcg_bsr_spmv(h->device, 6, 6, d->A.n, d->A.ptr, d->A.col, d->A.vals, d->xe, y, 1.0, 0, s), "fcg_bsr_spmv (level 1)");
+}
+
+void dist_dinv(fcg_amg* h, const Dist* d, const double* r, double* z, double scale, bool acc, hipStream_t s)
+{
+  ck(fcg_bsr_block_jacobi_apply(h->device, 6, d->na, d->dinv, r, z, scale, acc ? 1 : 0, s),
+      "fcg_bsr_block_jacobi_apply (level 1)");
+}
+
+// numeric: A_1's owned rows from this rank's blocks and the partial rows of the other ranks, its
+// block Jacobi and lambda_max, then A_2's rows
+void dist_setup(fcg_amg* h, const fcg_transport* tr, hipStream_t s)
+{
+  Coupled* c = h->cpl;
+  Dist* d = c->d;
+  const Bsr& C = c->C;
+  ck(hipMemsetAsync(d->A.vals, 0, sizeof(double) * static_cast<size_t>(std::max<int64_t>(1, d->A.nnzb)) * 36, s), "memset");
+  if (d->c_hi > d->c_lo)
+    hipLaunchKernelGGL(add_blocks_kernel, dim3(blocks_for((d->c_hi - d->c_lo) * 36)), dim3(kBlock), 0, s,
+        d->c_hi - d->c_lo, d->pos_own, C.vals + 36 * d->c_lo, d->A.vals);
+  ck(hipGetLastError(), "add_blocks_kernel");
+  copy_dd(d->rows_s, C.vals, 36 * d->c_lo, s);
+  copy_dd(d->rows_s + 36 * d->c_lo, C.vals + 36 * d->c_hi, 36 * (C.nnzb - d->c_hi), s);
+  exchange_counted(c, tr, d->rows, 36, false, d->rows_s, d->rows_r, s, "transport exchange (partial level-1 rows)");
+  for (int q = 0, o = 0; q < d->R; ++q)
+  {
+    const int64_t n = d->rows.rcnt[static_cast<size_t>(q)];
+    if (n > 0)
+      hipLaunchKernelGGL(add_blocks_kernel, dim3(blocks_for(n * 36)), dim3(kBlock), 0, s, n, d->pos_recv + o,
+          d->rows_r + 36 * o, d->A.vals);
+    o += int(n);
+  }
+  ck(hipGetLastError(), "add_blocks_kernel");
+  ck(fcg_bsr_block_jacobi_setup(h->device, 6, d->na, d->A.ptr, d->diag, d->A.vals, d->dinv, h->flag, s),
+      "coupled AMG level 1: singular diagonal block");
+  Ops o{h, 1, nullptr, s, tr};
+  o.dl = d;
+  estimate_lmax(o);
+  ck(fcg_bsr_spgemm(h->device, 6, 6, 6, d->A.n, d->A.ptr, d->A.col, d->A.vals, d->T1ext.ptr, d->T1ext.col,
+         d->T1ext.vals, d->AT1.ptr, d->AT1.col, d->AT1.vals, s), "fcg_bsr_spgemm (A_1 T_1,ext)");
+  ck(fcg_bsr_spgemm(h->device, 6, 6, 6, d->T1t.n, d->T1t.ptr, d->T1t.col, d->T1t.vals, d->AT1.ptr,
+         d->AT1.col, d->AT1.vals, d->C2.ptr, d->C2.col, d->C2.vals, s), "fcg_bsr_spgemm (T_1^T A_1 T_1)");
+}
+
+// one V-cycle of the distributed level 1: Chebyshev with A_1, the residual restricted by T_1 into
+// the replicated level 2 (each rank fills its own aggregates, the all-reduce completes the vector),
+// the replicated hierarchy, T_1 back, Chebyshev again
+void dist_vcycle(fcg_amg* h, const fcg_transport* tr, const double* b, double* x, hipStream_t s)
+{
+  Coupled* c = h->cpl;
+  Dist* d = c->d;
+  Ops o{h, 1, nullptr, s, tr};
+  o.dl = d;
+  cheb(h, o, b, x, true);
+  o.spmv(x, d->r);
+  const int64_t n = 6 * d->na;
+  hipLaunchKernelGGL(rsub_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, s, b, d->r, n);
+  ck(hipMemsetAsync(c->gb, 0, sizeof(double) * static_cast<size_t>(6 * d->n2_tot), s), "memset");
+  ck(fcg_bsr_spmv(h->device, 6, 6, d->T1t.n, d->T1t.ptr, d->T1t.col, d->T1t.vals, d->r, c->gb + 6 * d->off2,
+         1.0, 0, s), "restriction (level 1)");
+  allreduce_counted(c, tr, c->gb, 6 * d->n2_tot, s, "transport all-reduce (level 2)");
+  vcycle(c->g, 1, nullptr, c->gb, c->ge, s);
+  ck(fcg_bsr_spmv(h->device, 6, 6, d->T1.n, d->T1.ptr, d->T1.col, d->T1.vals, c->ge + 6 * d->off2, x, 1.0, 1, s),
+      "prolongation (level 1)");
+  cheb(h, o, b, x, false);
 }
 
 // numeric part per tangent, after the local setup (T_0, the nodal block inverses)
 void coupled_setup(fcg_amg* h, const double* K, const fcg_transport* tr, hipStream_t s)
 {
   Coupled* c = h->cpl;
+  c->ctr_ar = c->ctr_x = 0;
   const fcg::DeviceMesh& m = h->ctx->mesh;
   const Step& st0 = h->steps[0];
   const int64_t nb0 = h->nb0;
@@ -1437,30 +2097,66 @@ void coupled_setup(fcg_amg* h, const double* K, const fcg_transport* tr, hipStre
          c->Pext.col, c->Pext.vals, c->AP.ptr, c->AP.col, c->AP.vals, s), "fcg_bsr_spgemm (A P_ext)");
   ck(fcg_bsr_spgemm(h->device, 6, 3, 6, c->Pt.n, c->Pt.ptr, c->Pt.col, c->Pt.vals, c->AP.ptr, c->AP.col,
          c->AP.vals, c->C.ptr, c->C.col, c->C.vals, s), "fcg_bsr_spgemm (P^T A P)");
+  if (c->d) dist_setup(h, tr, s);
+  // the replicated operator: every rank's blocks scattered into a zeroed buffer, summed
   fcg_amg* g = c->g;
   Level& L1 = g->levels[0];
-  ck(hipMemsetAsync(L1.A.vals, 0, sizeof(double) * size_t(std::max<int64_t>(1, c->a1_nnzb)) * 36, s), "memset");
-  if (c->C.nnzb > 0)
-    hipLaunchKernelGGL(scatter_blocks_kernel, dim3(blocks_for(c->C.nnzb * 36)), dim3(kBlock), 0, s, c->C.nnzb,
-        c->c_pos, c->C.vals, L1.A.vals);
+  ck(hipMemsetAsync(L1.A.vals, 0, sizeof(double) * static_cast<size_t>(std::max<int64_t>(1, c->rep_nnzb)) * 36, s), "memset");
+  if (c->rep_part->nnzb > 0)
+    hipLaunchKernelGGL(scatter_blocks_kernel, dim3(blocks_for(c->rep_part->nnzb * 36)), dim3(kBlock), 0, s,
+        c->rep_part->nnzb, c->rep_pos, c->rep_part->vals, L1.A.vals);
   ck(hipGetLastError(), "scatter_blocks_kernel");
-  ck(tr->allreduce_fn(tr->user, L1.A.vals, c->a1_nnzb * 36, s), "transport all-reduce (A_1)");
+  allreduce_counted(c, tr, L1.A.vals, c->rep_nnzb * 36, s, c->d ? "transport all-reduce (A_2)" : "transport all-reduce (A_1)");
   ck(fcg_bsr_block_jacobi_setup(g->device, 6, L1.A.n, L1.A.ptr, L1.diag, L1.A.vals, L1.dinv, g->flag, s),
-      "coupled AMG level 1: singular diagonal block");
+      c->d ? "coupled AMG level 2: singular diagonal block" : "coupled AMG level 1: singular diagonal block");
   if (g->steps.size() > 1) estimate_lmax(Ops{g, 1, nullptr, s});
   galerkin_from(g, 1, nullptr, s);
+  c->ar_setup = c->ctr_ar;
+  c->x_setup = c->ctr_x;
 }
 
-// Q x = P A_1^-1 P^T x over all ranks: this rank's rows restricted into the global level-1 vector
-// (every rank adds to the aggregates its rows reach), the all-reduce, the replicated hierarchy's
-// V-cycle, prolongation into this rank's rows (overwrites y)
+// Q x = P A_1^-1 P^T x over all ranks.  Replicated level 1: this rank's rows restricted into the
+// global level-1 vector (every rank adds to the aggregates its rows reach), the all-reduce, the
+// replicated hierarchy's V-cycle, prolongation into this rank's rows (overwrites y).  Distributed
+// level 1: the restriction over LA, whose other-rank entries go to their owners and are added
+// there (senders in rank order), the level-1 V-cycle, and the reverse exchange before P.
 void coupled_coarse(fcg_amg* h, const fcg_transport* tr, const double* x, double* y, hipStream_t s)
 {
   Coupled* c = h->cpl;
-  ck(fcg_bsr_spmv(h->device, 6, 3, c->Pt.n, c->Pt.ptr, c->Pt.col, c->Pt.vals, x, c->gb, 1.0, 0, s), "restriction");
-  ck(tr->allreduce_fn(tr->user, c->gb, 6 * c->n_agg_tot, s), "transport all-reduce (level 1)");
-  vcycle(c->g, 1, nullptr, c->gb, c->ge, s);
-  ck(fcg_bsr_spmv(h->device, 3, 6, c->P.n, c->P.ptr, c->P.col, c->P.vals, c->ge, y, 1.0, 0, s), "prolongation");
+  Dist* d = c->d;
+  if (!d)
+  {
+    ck(fcg_bsr_spmv(h->device, 6, 3, c->Pt.n, c->Pt.ptr, c->Pt.col, c->Pt.vals, x, c->gb, 1.0, 0, s), "restriction");
+    allreduce_counted(c, tr, c->gb, 6 * c->n_agg_tot, s, "transport all-reduce (level 1)");
+    vcycle(c->g, 1, nullptr, c->gb, c->ge, s);
+    ck(fcg_bsr_spmv(h->device, 3, 6, c->P.n, c->P.ptr, c->P.col, c->P.vals, c->ge, y, 1.0, 0, s), "prolongation");
+    return;
+  }
+  const int64_t na = d->na, own0 = d->own0, tail = d->NL - own0 - na;
+  ck(fcg_bsr_spmv(h->device, 6, 3, c->Pt.n, c->Pt.ptr, c->Pt.col, c->Pt.vals, x, d->y, 1.0, 0, s), "restriction");
+  copy_dd(d->b, d->y + 6 * own0, 6 * na, s);
+  copy_dd(d->pex_s, d->y, 6 * own0, s);
+  copy_dd(d->pex_s + 6 * own0, d->y + 6 * (own0 + na), 6 * tail, s);
+  exchange_counted(c, tr, d->pex, 6, false, d->pex_s, d->pex_r, s, "transport exchange (restriction)");
+  for (int q = 0, o = 0; q < d->R; ++q)
+  {
+    const int64_t n = d->pex.rcnt[static_cast<size_t>(q)];
+    if (n > 0)
+      hipLaunchKernelGGL(add_items_kernel, dim3(blocks_for(6 * n)), dim3(kBlock), 0, s, n, d->pex_idx + o,
+          d->pex_r + 6 * o, d->b);
+    o += int(n);
+  }
+  ck(hipGetLastError(), "add_items_kernel");
+  dist_vcycle(h, tr, d->b, d->x, s);
+  if (d->pex.nr > 0)
+    hipLaunchKernelGGL(gather_items_kernel, dim3(blocks_for(6 * d->pex.nr)), dim3(kBlock), 0, s, d->pex.nr,
+        d->pex_idx, d->x, d->pex_r);
+  ck(hipGetLastError(), "gather_items_kernel");
+  exchange_counted(c, tr, d->pex, 6, true, d->pex_r, d->pex_s, s, "transport exchange (prolongation)");
+  copy_dd(d->y + 6 * own0, d->x, 6 * na, s);
+  copy_dd(d->y, d->pex_s, 6 * own0, s);
+  copy_dd(d->y + 6 * (own0 + na), d->pex_s + 6 * own0, 6 * tail, s);
+  ck(fcg_bsr_spmv(h->device, 3, 6, c->P.n, c->P.ptr, c->P.col, c->P.vals, d->y, y, 1.0, 0, s), "prolongation");
 }
 
 // y = A x with the global operator: the import of x into the column map, the rank's SpMV
@@ -1473,14 +2169,15 @@ void coupled_spmv(fcg_amg* h, const double* K, const fcg_transport* tr, const do
 
 // One V-cycle of the global system: Chebyshev smoothing with the global operator (D = the owned
 // nodal blocks, lambda_max of the global D^-1 A), the residual restricted by this rank's P_0 into
-// the global level 1, the replicated hierarchy there, prolongation, Chebyshev again -- the
-// single-rank cycle, with P_0 from the rank-local aggregation.  (Tried before: a multiplicative
-// cycle with rank-local smoothing, indefinite; the balancing form Q r + (I - Q A) M (I - A Q) r with
-// M the rank-local V-cycle, 64 FCG iterations against 33 on one rank for the 2-rank test box.)
+// level 1, the coarse levels there, prolongation, Chebyshev again -- the single-rank cycle, with
+// P_0 from the rank-local aggregation.  (Tried before: a multiplicative cycle with rank-local
+// smoothing, indefinite; the balancing form Q r + (I - Q A) M (I - A Q) r with M the rank-local
+// V-cycle, 64 FCG iterations against 33 on one rank for the 2-rank test box.)
 void coupled_apply(fcg_amg* h, const double* K, const fcg_transport* tr, const double* r, double* z,
     hipStream_t s)
 {
   Coupled* c = h->cpl;
+  c->ctr_ar = c->ctr_x = 0;
   const int64_t n = h->n0;
   const Ops o{h, 0, K, s, tr};
   cheb(h, o, r, z, true);
@@ -1489,6 +2186,19 @@ void coupled_apply(fcg_amg* h, const double* K, const fcg_transport* tr, const d
   coupled_coarse(h, tr, c->q, c->w, s);
   hipLaunchKernelGGL(axpby_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, s, 1.0, c->w, 1.0, z, n);
   cheb(h, o, r, z, false);
+  c->ar_apply = c->ctr_ar;
+  c->x_apply = c->ctr_x;
+}
+
+// bytes of a hierarchy's matrices (fcg_amg_coupled_stats)
+int64_t hierarchy_bytes(const fcg_amg* g)
+{
+  int64_t b = 0;
+  for (const Level& L : g->levels) b += L.A.nnzb * 36 * 8;
+  for (const Step& st : g->steps)
+    for (const Bsr* M : {&st.T, &st.P, &st.AT, &st.AP, &st.Pt}) b += M->nnzb * M->br * M->bc * 8;
+  b += g->cn * g->cn * 8;
+  return b;
 }
 
 }  // namespace fcg_amgs
@@ -1999,7 +2709,28 @@ int fcg_amg_precond_apply(fcg_amg* h, const double* d_K, const fcg_transport* tr
 
 int fcg_amg_coupled_levels(const fcg_amg* h)
 {
-  return h && h->cpl && h->cpl->g ? int(h->cpl->g->levels.size()) : 0;
+  return h && h->cpl && h->cpl->g ? int(h->cpl->g->levels.size()) + (h->cpl->d ? 1 : 0) : 0;
+}
+
+int fcg_amg_coupled_stats(const fcg_amg* h, int64_t* out, int n)
+{
+  if (!h || !out || n < 0) return FCG_ERR_ARG;
+  const fcg_amgs::Coupled* c = h->cpl;
+  int64_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (c && c->g)
+  {
+    v[0] = c->d ? 1 : 0;
+    v[1] = c->d ? c->d->na : c->n_agg_tot;
+    v[2] = c->n_agg_tot;
+    v[3] = c->ar_setup;
+    v[4] = c->ar_apply;
+    v[5] = c->x_setup;
+    v[6] = c->x_apply;
+    v[7] = fcg_amgs::hierarchy_bytes(c->g);
+  }
+  const int k = std::min(n, 8);
+  for (int i = 0; i < k; ++i) out[i] = v[i];
+  return k;
 }
 
 int fcg_amg_destroy(fcg_amg* h)

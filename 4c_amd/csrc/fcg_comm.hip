@@ -285,6 +285,27 @@ int fcg_comm_alltoallv(const void* send_buf, const int64_t* send_counts, void* r
   return rc;
 }
 
+int fcg_comm_exchange_device(void* comm, const double* d_send, const int64_t* send_counts,
+    double* d_recv, const int64_t* recv_counts, void* stream)
+{
+  auto* c = static_cast<fcg_comm*>(comm);
+  if (!c || !send_counts || !recv_counts) return FCG_ERR_ARG;
+  (void)hipSetDevice(c->device);
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+  int64_t so = 0, ro = 0;
+  ncclResult_t r = ncclGroupStart();
+  for (int p = 0; p < c->nranks && r == ncclSuccess; ++p)
+  {
+    if (send_counts[p] > 0) r = ncclSend(d_send + so, size_t(send_counts[p]), ncclFloat64, p, c->nccl, s);
+    if (r == ncclSuccess && recv_counts[p] > 0)
+      r = ncclRecv(d_recv + ro, size_t(recv_counts[p]), ncclFloat64, p, c->nccl, s);
+    so += send_counts[p];
+    ro += recv_counts[p];
+  }
+  const ncclResult_t r2 = ncclGroupEnd();
+  return (r == ncclSuccess && r2 == ncclSuccess) ? FCG_OK : fcg_device_error();
+}
+
 int fcg_halo_create(const fcg_import_plan* p, int device, fcg_halo** out)
 {
   if (!p || !out || p->nranks < 1 || p->rank < 0 || p->rank >= p->nranks || p->n_same < 0 ||

@@ -130,6 +130,13 @@ int rccl_allreduce(void* user, double* d_vals, int64_t n, void* stream)
   return fcg_comm_allreduce(p->comm, d_vals, n, FCG_OP_SUM, stream);
 }
 
+int rccl_exchange(void* user, const double* d_send, const int64_t* send_counts, double* d_recv,
+    const int64_t* recv_counts, void* stream)
+{
+  auto* p = static_cast<fcg_rccl_pair*>(user);
+  return fcg_comm_exchange_device(p->comm, d_send, send_counts, d_recv, recv_counts, stream);
+}
+
 }  // namespace
 
 extern "C" {
@@ -139,6 +146,7 @@ int fcg_transport_rccl(fcg_rccl_pair* pair, fcg_transport* out)
   if (!pair || !out || !pair->comm || !pair->halo) return FCG_ERR_ARG;
   out->import_fn = rccl_import;
   out->allreduce_fn = rccl_allreduce;
+  out->exchange_fn = rccl_exchange;
   out->user = pair;
   int n = 1, r = 0;
   if (fcg_comm_size(pair->comm, &n) != FCG_OK || fcg_comm_rank(pair->comm, &r) != FCG_OK) return FCG_ERR_DEVICE;

@@ -187,9 +187,30 @@ class NativeDFCG:
                 except Exception:  # noqa: BLE001
                     return fcg.FCG_ERR_DEVICE
 
+            def exchange_cb(_user, d_send, scnt, d_recv, rcnt, _stream):
+                # the distributed coarse level's point-to-point exchange: MPI_Alltoallv of doubles
+                try:
+                    Lb = fcg.lib()
+                    world = dist.get_world_size()
+                    sc = [int(scnt[q]) for q in range(world)]
+                    rc = [int(rcnt[q]) for q in range(world)]
+                    torch.cuda.synchronize(self.dev)
+                    hs = np.zeros(max(1, sum(sc)))
+                    if sum(sc) and Lb.fcg_memcpy_d2h(hs.ctypes.data_as(ctypes.c_void_p), d_send, 8 * sum(sc)) != 0:
+                        return fcg.FCG_ERR_DEVICE
+                    hr = torch.empty(sum(rc), dtype=torch.float64)
+                    dist.all_to_all_single(hr, torch.from_numpy(hs[:sum(sc)]), output_split_sizes=rc,
+                                           input_split_sizes=sc)
+                    if sum(rc):
+                        return Lb.fcg_memcpy_h2d(d_recv, hr.numpy().ctypes.data_as(ctypes.c_void_p), 8 * sum(rc))
+                    return 0
+                except Exception:  # noqa: BLE001 - surfaced as an error code
+                    return fcg.FCG_ERR_DEVICE
+
             t.import_fn = fcg.IMPORT_FN(import_cb)
             t.allreduce_fn = fcg.ALLREDUCE_FN(allreduce_cb)
-            self._keep += [t.import_fn, t.allreduce_fn, send, recv]
+            t.exchange_fn = fcg.EXCHANGE_FN(exchange_cb)
+            self._keep += [t.import_fn, t.allreduce_fn, t.exchange_fn, send, recv]
             if dist.is_initialized():
                 t.rank, t.nranks = dist.get_rank(), dist.get_world_size()
             else:
@@ -213,6 +234,18 @@ class NativeDFCG:
     def coupled_levels(self):
         """Levels of the AMG hierarchy coupled across ranks (0: rank-local preconditioner)."""
         return fcg.lib().fcg_amg_coupled_levels(self.amg._h) if self.amg is not None else 0
+
+    COUPLED_STATS = ("distributed_levels", "level1_rows_here", "level1_rows_global",
+                     "allreduce_doubles_setup", "allreduce_doubles_apply", "exchange_doubles_setup",
+                     "exchange_doubles_apply", "replicated_bytes")
+
+    def coupled_stats(self):
+        """fcg_amg_coupled_stats: what the coupled coarse levels store and move on this rank."""
+        if self.amg is None:
+            return {}
+        out = (ctypes.c_int64 * 8)()
+        n = fcg.lib().fcg_amg_coupled_stats(self.amg._h, out, 8)
+        return {k: int(out[i]) for i, k in enumerate(self.COUPLED_STATS[:max(0, n)])}
 
 
 class DistributedNewton:

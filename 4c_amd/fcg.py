@@ -88,11 +88,15 @@ IMPORT_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, cty
                              ctypes.c_void_p)
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                 ctypes.c_void_p)
+# (user, d_send, send_counts[nranks], d_recv, recv_counts[nranks], stream): MPI_Alltoallv of doubles
+EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                               ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p,
+                               ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p)
 
 
 class FcgTransport(ctypes.Structure):
     _fields_ = [("import_fn", IMPORT_FN), ("allreduce_fn", ALLREDUCE_FN), ("user", ctypes.c_void_p),
-                ("rank", ctypes.c_int32), ("nranks", ctypes.c_int32)]
+                ("rank", ctypes.c_int32), ("nranks", ctypes.c_int32), ("exchange_fn", EXCHANGE_FN)]
 
 
 class FcgRcclPair(ctypes.Structure):
@@ -148,7 +152,8 @@ EXPORTS = ["fcg_create", "fcg_destroy", "fcg_last_error", "fcg_evaluate", "fcg_e
            "fcg_bsr_to_dense", "fcg_amg_default_options", "fcg_amg_create", "fcg_amg_solve",
            "fcg_amg_levels", "fcg_amg_level_info", "fcg_amg_setup_ms", "fcg_amg_stats", "fcg_amg_last_error",
            "fcg_amg_destroy", "fcg_amg_setup", "fcg_amg_iterate", "fcg_amg_apply",
-           "fcg_amg_coupled_levels", "fcg_transport_rccl", "fcg_dfcg_solve"]
+           "fcg_amg_coupled_levels", "fcg_amg_coupled_stats", "fcg_comm_exchange_device",
+           "fcg_transport_rccl", "fcg_dfcg_solve"]
 
 _lib = None
 FUNCT_FN = ctypes.CFUNCTYPE(ctypes.c_double, ctypes.c_int, _dp, ctypes.c_double, ctypes.c_void_p)
@@ -301,6 +306,8 @@ def lib():
     L.fcg_amg_destroy.argtypes = [vp]
     L.fcg_amg_apply.argtypes = [vp, vp, vp, vp, vp]
     L.fcg_amg_coupled_levels.argtypes = [vp]
+    if hasattr(L, "fcg_amg_coupled_stats"):  # absent from older A/B builds (FCG_LIB)
+        L.fcg_amg_coupled_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), c_int]
     L.fcg_transport_rccl.argtypes = [ctypes.POINTER(FcgRcclPair), ctypes.POINTER(FcgTransport)]
     L.fcg_dfcg_solve.argtypes = [vp, vp, ctypes.POINTER(FcgTransport), vp, vp, vp, c_dbl, c_int, vp,
                                  ctypes.POINTER(c_int), _dp]

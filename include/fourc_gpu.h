@@ -669,16 +669,27 @@ int fcg_norm2(fcg_comm* comm, const double* d_x, int64_t n, void* stream, double
  * ---------------------------------------------------------------------------------------- */
 typedef int (*fcg_import_fn)(void* user, const double* d_x_row, double* d_x_col, void* stream);
 typedef int (*fcg_allreduce_fn)(void* user, double* d_vals, int64_t n, void* stream);  /* in place, sum */
+/* Point-to-point exchange of device doubles with MPI_Alltoallv semantics (the Epetra_Import /
+ * Export of a distributed coarse level): send_counts[p] doubles to rank p, packed in rank order in
+ * d_send, recv_counts[p] from rank p into d_recv in rank order; counts are host arrays of nranks
+ * entries, this rank's own entries 0.  Ordered after the work already queued on `stream`. */
+typedef int (*fcg_exchange_fn)(void* user, const double* d_send, const int64_t* send_counts,
+    double* d_recv, const int64_t* recv_counts, void* stream);
 typedef struct fcg_transport {
   fcg_import_fn import_fn;
   fcg_allreduce_fn allreduce_fn;
   void* user;
   /* this rank and the rank count of the partition (MPI_Comm_rank / _size in 4C).  With
-   * nranks > 1 an AMG handle's coarse levels are coupled across the ranks (the global Galerkin
-   * operator A_1 = P_0^T A P_0, gathered by allreduce_fn and solved redundantly); nranks <= 1 (a
-   * zero-initialised struct) keeps the rank-local AMG. */
+   * nranks > 1 an AMG handle's coarse levels are coupled across the ranks; nranks <= 1 (a
+   * zero-initialised struct) keeps the rank-local AMG.  Without exchange_fn the global Galerkin
+   * operator A_1 = P_0^T A P_0 is gathered by allreduce_fn and solved redundantly on every rank;
+   * with it, level 1 is distributed (each rank owns the rows of its aggregates, its own import
+   * plan, the partial rows of the other ranks' aggregates sent to their owners) once its global
+   * size passes FCG_AMG_DIST_MIN DOFs (default 50000; FCG_AMG_DIST=1 always, 0 never), and the
+   * replication moves down to level 2 = T_1^T A_1 T_1 (fcg_amg_coupled_stats). */
   int32_t rank;
   int32_t nranks;
+  fcg_exchange_fn exchange_fn;  /* may be NULL */
 } fcg_transport;
 /* The RCCL transport of (comm, halo): fills *out; `pair` (caller-owned, alive while used) holds
  * the two handles the callbacks receive as `user`. */
@@ -693,6 +704,21 @@ int fcg_amg_apply(fcg_amg* amg, const double* d_K_vals, const double* d_r_row, d
 /* Levels of the coarse hierarchy coupled across ranks that fcg_dfcg_solve built for this handle
  * (level 1 = the global A_1 and its coarsenings; 0 = none: single rank, or nranks <= 1). */
 int fcg_amg_coupled_levels(const fcg_amg* amg);
+/* What the coupled coarse levels cost this rank (after the first fcg_dfcg_solve), out[0..n):
+ *   0 distributed levels (0: A_1 replicated, 1: A_1 distributed and A_2 replicated)
+ *   1 level-1 block rows (6 DOFs each) this rank stores: its own (distributed) or all (replicated)
+ *   2 level-1 block rows over all ranks
+ *   3 doubles all-reduced per numeric setup (the replicated level's Galerkin operator)
+ *   4 doubles all-reduced per preconditioner application (the replicated level's right-hand side)
+ *   5 doubles this rank sends per numeric setup through exchange_fn (partial level-1 rows)
+ *   6 doubles this rank sends per application through exchange_fn (level-1 imports, restriction
+ *     and prolongation)
+ *   7 bytes of the replicated hierarchy's matrices on this rank
+ * Returns the number of entries written (<= n). */
+int fcg_amg_coupled_stats(const fcg_amg* amg, int64_t* out, int n);
+/* fcg_exchange_fn over RCCL (user = fcg_comm*): grouped ncclSend / ncclRecv on `stream`. */
+int fcg_comm_exchange_device(void* comm, const double* d_send, const int64_t* send_counts,
+    double* d_recv, const int64_t* recv_counts, void* stream);
 int fcg_dfcg_solve(fcg_ctx* ctx, fcg_amg* amg, const fcg_transport* tr, const double* d_K_vals,
     const double* d_b_row, double* d_x_row, double rtol, int max_iter, void* stream,
     int* iterations, double* rel_residual);

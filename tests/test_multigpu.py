@@ -306,7 +306,8 @@ def _worker_solve(rank, world, port, q, kinem, path, transport="staged", solver=
         u = nt.solve().cpu().numpy()
         q.put((rank, True, {"u": dict(zip(m.row_gid[:n_own].tolist(), u.tolist())),
                             "iters": [r.get("lin_iter") for r in nt.history],
-                            "coupled_levels": lin.coupled_levels() if lin is not None else 0}))
+                            "coupled_levels": lin.coupled_levels() if lin is not None else 0,
+                            "stats": lin.coupled_stats() if lin is not None else {}}))
         if lin is not None and lin.amg is not None:
             lin.amg.close()
         dist.destroy_process_group()
@@ -316,12 +317,17 @@ def _worker_solve(rank, world, port, q, kinem, path, transport="staged", solver=
 
 
 def _solve_box(celltype):
+    box = os.environ.get("FCG_TEST_SOLVE_BOX")  # "nx,ny,nz": a larger hex8 box for the stats tests
+    if box and celltype == fcg.HEX8:
+        n = tuple(int(v) for v in box.split(","))
+        return n, tuple(float(v) for v in n)
     return ((8, 4, 4), (8.0, 4.0, 4.0)) if celltype == fcg.HEX8 else ((6, 2, 2), (6.0, 2.0, 2.0))
 
 
-def _run_two_rank_solve(kinem, path, transport, solver="pcg", celltype=fcg.HEX8, world=2):
+def _run_two_rank_solve(kinem, path, transport, solver="pcg", celltype=fcg.HEX8, world=2, stats=None):
     """The `world`-rank DistributedNewton of the clamped, tip-loaded box against the 1-rank
-    StaticNewton (by DOF GID); returns the ranks' linear iteration counts."""
+    StaticNewton (by DOF GID); returns the ranks' linear iteration counts (and appends each rank's
+    fcg_amg_coupled_stats to `stats`)."""
     dev = _dev()
     newton = importlib.import_module("4c_amd.newton")
     iv, up = _solve_box(celltype)
@@ -343,10 +349,12 @@ def _run_two_rank_solve(kinem, path, transport, solver="pcg", celltype=fcg.HEX8,
     for p in procs:
         p.join(timeout=60)
     got, iters = {}, []
-    for rank, ok, out in res:
+    for rank, ok, out in sorted(res, key=lambda t: t[0]):
         assert ok is True, (rank, ok)
         got.update(out["u"])
         iters.append(out["iters"])
+        if stats is not None:
+            stats.append(out["stats"])
         if solver == "native":
             assert out["coupled_levels"] >= 1, out  # the coarse levels span both ranks
         elif solver == "native-uncoupled":
@@ -439,6 +447,75 @@ def test_many_ranks_coupled_amg_iterations(world):
     n1, nR = sum(one), sum(i or 0 for i in iters[0])
     print(f"FCG iterations: 1 rank {one}, {world} ranks coupled {iters[0]}")
     assert nR <= 1.5 * n1, (one, iters)
+
+
+class _env:
+    """Environment variables for the spawned ranks (they inherit os.environ at start)."""
+
+    def __init__(self, **kv):
+        self.kv, self.old = kv, {}
+
+    def __enter__(self):
+        for k, v in self.kv.items():
+            self.old[k] = os.environ.get(k)
+            os.environ[k] = v
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_distributed_level1_coupled_amg(world):
+    """Level 1 of the coupled AMG distributed across the ranks (FCG_AMG_DIST=1: each rank owns the
+    rows of its aggregates, the partial rows of the others' aggregates go to their owners through
+    the transport's exchange, its own level-1 import plan; A_2 = T_1^T A_1 T_1 replicated): the
+    1-rank solution by GID, the FCG iterations within 1.5x of one rank, and the stats -- the rank
+    stores only its own level-1 rows, and the all-reduces carry level 2, not level 1."""
+    one = _one_rank_amg_iters(fcg.HEX8, fcg.LINEAR)
+    st_d, st_r = [], []
+    with _env(FCG_AMG_DIST="1"):
+        it_d = _run_two_rank_solve(fcg.LINEAR, fcg.PATH_AUTO, "staged", "native", fcg.HEX8, world=world,
+                                   stats=st_d)
+    with _env(FCG_AMG_DIST="0"):
+        it_r = _run_two_rank_solve(fcg.LINEAR, fcg.PATH_AUTO, "staged", "native", fcg.HEX8, world=world,
+                                   stats=st_r)
+    n1, nd, nr = sum(one), sum(i or 0 for i in it_d[0]), sum(i or 0 for i in it_r[0])
+    print(f"FCG iterations: 1 rank {one}, {world} ranks distributed level 1 {it_d[0]}, replicated {it_r[0]}")
+    print("stats distributed", st_d, "replicated", st_r)
+    assert nd <= 1.5 * n1, (one, it_d, it_r)
+    glob = st_r[0]["level1_rows_global"]
+    assert sum(s["level1_rows_here"] for s in st_d) == glob  # every level-1 row on exactly one rank
+    for sd, sr in zip(st_d, st_r):
+        assert sd["distributed_levels"] == 1 and sr["distributed_levels"] == 0
+        assert sd["level1_rows_global"] == glob and sr["level1_rows_here"] == glob
+        assert sd["exchange_doubles_apply"] > 0 and sr["exchange_doubles_apply"] == 0
+        assert sr["allreduce_doubles_apply"] == 6 * glob
+        assert sd["allreduce_doubles_apply"] < sr["allreduce_doubles_apply"]
+        assert sd["allreduce_doubles_setup"] < sr["allreduce_doubles_setup"]
+        assert sd["replicated_bytes"] < sr["replicated_bytes"]
+
+
+def test_distributed_level1_weak_scaling_stats():
+    """Weak scaling of the distributed level 1 (a box of 8 x 8 x 8 hex8 per rank along x, 2 and 4
+    ranks): the level-1 rows and the exchange volume per rank stay put (within the boundary ranks'
+    difference), while the replicated path's per-rank level-1 storage doubles with the ranks."""
+    per = {}
+    for world in (2, 4):
+        st_d, st_r = [], []
+        with _env(FCG_AMG_DIST="1", FCG_TEST_SOLVE_BOX=f"{8 * world},8,8"):
+            _run_two_rank_solve(fcg.LINEAR, fcg.PATH_AUTO, "staged", "native", fcg.HEX8, world=world, stats=st_d)
+        with _env(FCG_AMG_DIST="0", FCG_TEST_SOLVE_BOX=f"{8 * world},8,8"):
+            _run_two_rank_solve(fcg.LINEAR, fcg.PATH_AUTO, "staged", "native", fcg.HEX8, world=world, stats=st_r)
+        per[world] = (max(s["level1_rows_here"] for s in st_d), max(s["exchange_doubles_apply"] for s in st_d),
+                      max(s["level1_rows_here"] for s in st_r))
+        print(world, "distributed", st_d, "replicated", st_r)
+    (r2, x2, g2), (r4, x4, g4) = per[2], per[4]
+    assert r4 <= 1.25 * r2 and x4 <= 2.25 * x2, per  # interior ranks exchange on two faces
+    assert g4 >= 1.8 * g2, per
 
 
 def _one_rank_amg_iters(celltype, kinem):
