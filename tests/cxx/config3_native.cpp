@@ -148,7 +148,27 @@ int tr_sum(void* user, double* d_vals, int64_t n, void*)
   return fcg_memcpy_h2d(d_vals, h.data(), n * 8);
 }
 
+// the distributed coarse level's point-to-point exchange (MPI_Alltoallv of doubles in 4C)
+int tr_exchange(void* user, const double* d_send, const int64_t* sc, double* d_recv, const int64_t* rc, void*)
+{
+  auto* t = static_cast<HostTransport*>(user);
+  const int R = t->rc.tc->n;
+  int64_t ns = 0, nr = 0;
+  for (int q = 0; q < R; ++q)
+  {
+    ns += sc[q];
+    nr += rc[q];
+  }
+  std::vector<double> hs(static_cast<size_t>(std::max<int64_t>(1, ns))), hr(static_cast<size_t>(std::max<int64_t>(1, nr)));
+  int rcode = ns ? fcg_memcpy_d2h(hs.data(), d_send, ns * 8) : FCG_OK;
+  if (rcode != FCG_OK) return rcode;
+  t->rc.tc->alltoallv(t->rc.rank, hs.data(), sc, hr.data(), rc, 8);
+  if (!t->rc.tc->ok()) return FCG_ERR_DEVICE;
+  return nr ? fcg_memcpy_h2d(d_recv, hr.data(), nr * 8) : FCG_OK;
+}
+
 struct RankResult {
+  std::vector<int64_t> coupled;  // fcg_amg_coupled_stats
   std::map<int32_t, double> u;  // DOF GID -> displacement
   std::vector<double> norm_res;
   std::vector<int> lin_iters;
@@ -212,7 +232,7 @@ void run_rank(int n, int nranks, int rank, ThreadComm* tc, RankResult* out)
   ht.d_send = static_cast<double*>(d_send);
   ht.d_recv = static_cast<double*>(d_recv);
   // rank and rank count: the AMG's coarse levels are coupled across the ranks
-  fcg_transport tr{tr_import, tr_sum, &ht, int32_t(rank), int32_t(nranks)};
+  fcg_transport tr{tr_import, tr_sum, &ht, int32_t(rank), int32_t(nranks), tr_exchange};
 
   // external load: traction (0, 0, -1) on the x = 1 face (quad9 faces of the last element layer)
   std::vector<int32_t> faces;
@@ -301,6 +321,8 @@ void run_rank(int n, int nranks, int rank, ThreadComm* tc, RankResult* out)
     ndu = std::sqrt(dd);
   }
   for (int64_t i = 0; i < nr; ++i) out->u[row_gid[i]] = u[size_t(i)];
+  out->coupled.assign(8, 0);
+  out->coupled.resize(size_t(std::max(0, fcg_amg_coupled_stats(amg, out->coupled.data(), 8))));
   out->ok = conv;
   if (!conv) out->err = "Newton did not converge";
   for (void* p : {dK, du_row, du_col, df, drhs, ddu, ddbc, d_send, d_recv}) fcg_device_free(p);
@@ -311,7 +333,8 @@ void run_rank(int n, int nranks, int rank, ThreadComm* tc, RankResult* out)
   fcg_box_mesh_destroy(bm);
 }
 
-bool solve(int n, int nranks, std::map<int32_t, double>& u, std::vector<double>& res, std::vector<int>& lin)
+bool solve(int n, int nranks, std::map<int32_t, double>& u, std::vector<double>& res, std::vector<int>& lin,
+    std::vector<std::vector<int64_t>>* coupled = nullptr)
 {
   ThreadComm tc(nranks);
   std::vector<RankResult> rr(static_cast<size_t>(nranks));
@@ -330,6 +353,8 @@ bool solve(int n, int nranks, std::map<int32_t, double>& u, std::vector<double>&
   }
   res = rr[0].norm_res;
   lin = rr[0].lin_iters;
+  if (coupled)
+    for (const auto& r : rr) coupled->push_back(r.coupled);
   return ok;
 }
 
@@ -358,8 +383,18 @@ int main(int argc, char** argv)
   if (res1.size() < 3 || res1.size() > 9 || !(res1.back() <= 1e-12 * res1.front())) ++failures;
   if (nranks > 1)
   {
-    failures += !solve(n, nranks, uR, resR, linR);
+    std::vector<std::vector<int64_t>> cst;
+    failures += !solve(n, nranks, uR, resR, linR, &cst);
     report(nranks, resR, linR, uR);
+    // fcg_amg_coupled_stats per rank: distributed levels, level-1 rows here / global, doubles
+    // all-reduced per setup / application, doubles exchanged per setup / application, bytes of
+    // the replicated hierarchy
+    for (size_t r = 0; r < cst.size(); ++r)
+    {
+      std::printf("coupled AMG rank %zu:", r);
+      for (int64_t v : cst[r]) std::printf(" %lld", static_cast<long long>(v));
+      std::printf("\n");
+    }
     double worst = 0.0, scale = 0.0;
     bool same = uR.size() == u1.size();
     for (const auto& kv : u1)

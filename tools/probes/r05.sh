@@ -140,6 +140,13 @@ import json
 for l in open('$O/bab.jsonl'):
     v, j = l.split(' ', 1); d = json.loads(j)
     print(v, round(d['value'] / 1e6, 1), round(d['ms_per_step'], 4), round(d['roofline']['frac'], 4))" ;;
+    s:*)  # one test file / node id with its prints (-s): s:tests/test_x.py::name
+      run 900 gpu_tests_s.log python -u -m pytest -x -v -s --timeout 600 --timeout-method thread -m gpu "${step#s:}"
+      grep -E "PASSED|FAILED|iterations|stats|passed|failed" $O/gpu_tests_s.log | cut -c1-900 | tail -40 ;;
+    cxx:*)  # the C++ host's config-3 Newton (tests/cxx/config3_native N RANKS): cxx:40,2
+      a=${step#cxx:}
+      run 900 cxx_${a/,/_}.log tests/cxx/_build/config3_native ${a/,/ }
+      tail -12 $O/cxx_${a/,/_}.log ;;
     tests)  # the whole GPU suite
       run 1500 gpu_tests.log python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests
       tail -3 $O/gpu_tests.log ;;
