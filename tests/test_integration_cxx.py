@@ -41,14 +41,29 @@ NATIVE = os.path.join(CXX, "_build", "config3_native")
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,ranks", [(8, 2), (40, 2), (32, 4)])
-def test_config3_native_cxx_host(n, ranks):
+@pytest.mark.parametrize("n,ranks,dist", [(8, 2, "auto"), (40, 2, "auto"), (32, 4, "auto"), (40, 2, "1"),
+                                          (32, 4, "1")])
+def test_config3_native_cxx_host(n, ranks, dist):
     """BASELINE config 3's problem (hex27 StVK TotLag cube, x- clamped, traction -1 on x+) solved by
     a C++ host through the C ABI alone (tests/cxx/config3_native.cpp): Newton with fcg_dfcg_solve
     and each rank's fcg_amg; ranks as threads with a host exchange on one GPU.  1 rank and `ranks`
-    ranks converge quadratically to the same displacement by DOF GID (n = 40: config 3 at 40^3)."""
+    ranks converge quadratically to the same displacement by DOF GID (n = 40: config 3 at 40^3)
+    within 1.5x the 1-rank FCG iterations.  dist "1": the AMG's level 1 distributed across the
+    ranks (FCG_AMG_DIST=1; the host transport's exchange_fn) -- each rank then stores only its own
+    level-1 rows and all-reduces only level 2."""
     if not os.path.exists(NATIVE):
         subprocess.run(["make", "-s", "-C", CXX], check=True)
-    p = subprocess.run([NATIVE, str(n), str(ranks)], capture_output=True, text=True, timeout=600)
+    env = dict(os.environ)
+    if dist != "auto":
+        env["FCG_AMG_DIST"] = dist
+    p = subprocess.run([NATIVE, str(n), str(ranks)], capture_output=True, text=True, timeout=600, env=env)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "PASS" in p.stdout, p.stdout
+    stats = [[int(v) for v in line.split(":")[1].split()] for line in p.stdout.splitlines()
+             if line.startswith("coupled AMG rank")]
+    assert len(stats) == ranks, p.stdout
+    if dist == "1":
+        glob = stats[0][2]
+        assert all(st[0] == 1 for st in stats), p.stdout
+        assert sum(st[1] for st in stats) == glob, p.stdout  # each level-1 row on one rank
+        assert all(st[4] < 6 * glob for st in stats), p.stdout  # level 2 all-reduced, not level 1
