@@ -390,14 +390,19 @@ def test_two_ranks_native_dfcg(celltype, kinem, solver):
         assert n2 <= nu, (iters, unc)
 
 
-def test_two_ranks_native_dfcg_rccl():
+@pytest.mark.parametrize("dist", ["0", "1"])
+def test_two_ranks_native_dfcg_rccl(dist):
     """The coupled AMG path of fcg_dfcg_solve over the library's RCCL transport (fcg_transport_rccl
     names rank / nranks, so every RCCL solve with an AMG handle couples its coarse levels): one GPU
-    per rank, the 1-rank solution, coupled levels >= 1 and the 1.5x iteration bound."""
+    per rank, the 1-rank solution, coupled levels >= 1 and the 1.5x iteration bound (ADVICE r4);
+    dist "1": level 1 distributed, its exchanges through fcg_comm_exchange_device."""
     _dev()
     if torch.cuda.device_count() < 2:
         pytest.skip("RCCL transport needs two GPUs (RCCL refuses two ranks on one device)")
-    iters = _run_two_rank_solve(fcg.LINEAR, fcg.PATH_AUTO, "rccl", "native", fcg.HEX8)
+    st = []
+    with _env(FCG_AMG_DIST=dist):
+        iters = _run_two_rank_solve(fcg.LINEAR, fcg.PATH_AUTO, "rccl", "native", fcg.HEX8, stats=st)
+    assert all(s_["distributed_levels"] == int(dist) for s_ in st), st
     one = _one_rank_amg_iters(fcg.HEX8, fcg.LINEAR)
     assert sum(i or 0 for i in iters[0]) <= 1.5 * sum(one), (one, iters)
 
