@@ -248,8 +248,9 @@ int fcg_box_mesh_create_ex(const fcg_box* box, int rank, int nranks, int flags, 
 
   // column nodes: the lattice nodes of the column elements, marked in the node box of the grown
   // section and enumerated in lattice (GID) order
-  const int64_t bx = 2 * cex + 1, by = 2 * cey + 1, bz = 2 * cez + 1;
-  const int64_t bn = nce > 0 ? bx * by * bz : 0;
+  // (a rank without column elements -- more ranks than element layers -- has an empty node box)
+  const int64_t bx = nce > 0 ? 2 * cex + 1 : 0, by = nce > 0 ? 2 * cey + 1 : 0, bz = nce > 0 ? 2 * cez + 1 : 0;
+  const int64_t bn = bx * by * bz;
   std::vector<uint8_t> used(bn, 0);
   auto box_of = [&](int64_t e, int a) -> int64_t {
     const int64_t ex = e % IX, ey = (e / IX) % IY, ez = e / (IX * IY);

@@ -162,6 +162,44 @@ def test_multirank_rows_sum_to_global():
                 assert abs(mine[c] - ref[c]) <= 1e-12 * np.abs(Kg).max()
 
 
+@pytest.mark.parametrize("celltype,kinem", [(fcg.HEX8, fcg.LINEAR), (fcg.HEX8, fcg.TOTLAG), (fcg.HEX27, fcg.TOTLAG)])
+def test_more_ranks_than_elements_empty_ranks_evaluate(celltype, kinem):
+    """A 2 x 1 x 1 box over 5 ranks: the ranks GridGenerator gives no elements create empty
+    contexts whose evaluates (device, host, internal force, async check) are no-ops, and the other
+    ranks' owned rows still equal the single-rank assembly."""
+    iv, nranks = (2, 1, 1), 5
+    glob = fcg.BoxMesh(celltype, iv, jitter=0.05)
+    ug = glob.u_col(1e-3)
+    Kg, fg, _ = _run_gpu(glob, kinem, ug)
+    grow = {int(g): i for i, g in enumerate(glob.row_gid)}
+    gcol = {int(g): i for i, g in enumerate(glob.col_gid)}
+    empty = 0
+    for r in range(nranks):
+        m = fcg.BoxMesh(celltype, iv, jitter=0.05, rank=r, nranks=nranks)
+        u = np.array([ug[gcol[int(g)]] for g in m.col_gid], dtype=np.float64)
+        K, f, ev = _run_gpu(m, kinem, u)
+        if m.n_ele == 0:
+            empty += 1
+            assert K.size == 0 and f.size == 0
+            ev.evaluate(fcg.CALC_INTERNALFORCE, u, np.zeros(0), None)
+            ev.set_async(True)
+            _run_gpu(m, kinem, u, ev=ev)
+            ev.check_error()
+            ev.set_async(False)
+        for i in range(m.n_owned_rows):
+            gi = grow[int(m.row_gid[i])]
+            assert abs(f[i] - fg[gi]) <= 1e-12 * np.abs(fg).max()
+            cols = m.col_gid[m.col_lid[m.rowptr[i]:m.rowptr[i + 1]]]
+            gcols = glob.col_gid[glob.col_lid[glob.rowptr[gi]:glob.rowptr[gi + 1]]]
+            mine = dict(zip(cols.tolist(), K[m.rowptr[i]:m.rowptr[i + 1]].tolist()))
+            ref = dict(zip(gcols.tolist(), Kg[glob.rowptr[gi]:glob.rowptr[gi + 1]].tolist()))
+            assert mine.keys() == ref.keys()
+            for c in mine:
+                assert abs(mine[c] - ref[c]) <= 1e-12 * np.abs(Kg).max()
+        ev.close()
+    assert empty > 0
+
+
 def test_full_size_linear_properties():
     """1M hex8 (BASELINE config 2) at full size: K u == f_int for linear kinematics (linearity),
     K symmetric by gid, and a z-slab of rows against the oracle."""

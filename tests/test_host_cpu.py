@@ -108,6 +108,27 @@ def test_partition_rows_and_ghost_layer(nranks):
     assert set(allrows.tolist()) == set(glob.row_gid.tolist())
 
 
+@pytest.mark.parametrize("celltype", [fcg.HEX8, fcg.HEX27])
+@pytest.mark.parametrize("strict", [False, True])
+def test_more_ranks_than_elements_leaves_empty_ranks(celltype, strict):
+    """A split with more ranks than the box has element layers (GridGenerator gives some ranks no
+    elements): those ranks get an empty mesh -- no elements, rows, columns or graph -- and the other
+    ranks' rows still cover the global rows exactly once (this used to crash the builder)."""
+    for iv, nranks in (((1, 1, 1), 3), ((2, 1, 1), 5), ((2, 2, 1), 8)):
+        glob = fcg.BoxMesh(celltype, iv)
+        rows, empty = [], 0
+        for r in range(nranks):
+            m = fcg.BoxMesh(celltype, iv, rank=r, nranks=nranks, strict=strict)
+            if m.n_ele == 0:
+                empty += 1
+                assert m.n_rows == m.n_cols == m.nnz == m.n_owned_rows == 0
+                assert len(m.rowptr) == 1 and m.rowptr[0] == 0
+            rows.append(m.row_gid[:m.n_owned_rows])
+        assert empty > 0, (iv, nranks)
+        allrows = np.concatenate(rows)
+        assert len(allrows) == glob.n_rows and set(allrows.tolist()) == set(glob.row_gid.tolist())
+
+
 def test_create_without_gpu_fails_loudly():
     import torch
     if torch.cuda.is_available():
