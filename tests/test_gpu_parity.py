@@ -200,6 +200,41 @@ def test_more_ranks_than_elements_empty_ranks_evaluate(celltype, kinem):
     assert empty > 0
 
 
+def test_random_splits_owned_rows_equal_global():
+    """Seeded random boxes (1-4 elements per direction), rank counts 1-7 (empty ranks included),
+    both cell types and kinematics, hex8 through each path: every rank's owned rows equal the
+    single-rank assembly's rows by GID."""
+    rng = np.random.default_rng(20251018)
+    paths = [fcg.PATH_AUTO, fcg.PATH_GATHER, fcg.PATH_GENERAL]
+    for trial in range(14):
+        ct = fcg.HEX8 if trial % 3 else fcg.HEX27
+        kinem = fcg.LINEAR if trial % 2 else fcg.TOTLAG
+        path = paths[trial % 3] if ct == fcg.HEX8 else fcg.PATH_AUTO
+        iv = tuple(int(v) for v in rng.integers(1, 5, 3))
+        nranks = int(rng.integers(1, 8))
+        glob = fcg.BoxMesh(ct, iv, jitter=0.05, seed=trial)
+        ug = glob.u_col(1e-3)
+        Kg, fg, evg = _run_gpu(glob, kinem, ug)
+        evg.close()
+        grow = {int(g): i for i, g in enumerate(glob.row_gid)}
+        gcol = {int(g): i for i, g in enumerate(glob.col_gid)}
+        tolK, tolf = 1e-12 * np.abs(Kg).max(), 1e-12 * np.abs(fg).max()
+        for r in range(nranks):
+            m = fcg.BoxMesh(ct, iv, jitter=0.05, seed=trial, rank=r, nranks=nranks)
+            u = np.array([ug[gcol[int(g)]] for g in m.col_gid], dtype=np.float64)
+            K, f, ev = _run_gpu(m, kinem, u, path=path)
+            ev.close()
+            for i in range(m.n_owned_rows):
+                gi = grow[int(m.row_gid[i])]
+                assert abs(f[i] - fg[gi]) <= tolf, (trial, iv, nranks, r, path)
+                cols = m.col_gid[m.col_lid[m.rowptr[i]:m.rowptr[i + 1]]]
+                gcols = glob.col_gid[glob.col_lid[glob.rowptr[gi]:glob.rowptr[gi + 1]]]
+                mine = dict(zip(cols.tolist(), K[m.rowptr[i]:m.rowptr[i + 1]].tolist()))
+                ref = dict(zip(gcols.tolist(), Kg[glob.rowptr[gi]:glob.rowptr[gi + 1]].tolist()))
+                assert mine.keys() == ref.keys(), (trial, iv, nranks, r, path)
+                assert max(abs(mine[c] - ref[c]) for c in mine) <= tolK, (trial, iv, nranks, r, path)
+
+
 def test_full_size_linear_properties():
     """1M hex8 (BASELINE config 2) at full size: K u == f_int for linear kinematics (linearity),
     K symmetric by gid, and a z-slab of rows against the oracle."""
