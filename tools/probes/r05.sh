@@ -70,10 +70,6 @@ for l in open('$O/scratch.txt'):
       python3 -c "
 import json; d = json.load(open('$O/c3.json'))
 print('setup_s', round(d['setup_s'], 2), 'newton_s', round(d['newton_s'], 3), json.dumps(d['setup_phases']))" ;;
-    pcs)  # PC sampling (host trap, beta) of the 1M hex8 linear sweep
-      mkdir -p $O/pcs
-      (cd /tmp && timeout -k 10 180 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method host_trap --pc-sampling-unit time --pc-sampling-interval 1 --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/$O/pcs" -o run -- python3 "$GRAFT_REPO_ROOT/$ET" --celltype hex8 --kinem linear --n 100 --reps 20) > $O/pcs.log 2>&1 || { tail -20 $O/pcs.log; exit 1; }
-      find $O/pcs -type f | head; tail -5 $O/pcs.log ;;
     gab)  # same-box A/B of lib variants on the gather path: renumbered 1M hex8, LIBS="default head ..."
       for r in 1 2; do for v in ${LIBS:-default}; do for k in linear totlag; do
         if [ "$v" = default ]; then unset FCG_LIB; else export FCG_LIB=$v; fi
