@@ -143,6 +143,28 @@ for l in open('$O/bab.jsonl'):
       a=${step#cxx:}
       run 900 cxx_${a/,/_}.log tests/cxx/_build/config3_native ${a/,/ }
       tail -12 $O/cxx_${a/,/_}.log ;;
+    c3lib)  # config-3 Newton, same-box A/B of lib variants: c3lib with LIBS="default x"
+      for rep in 1 2; do for v in ${LIBS:-default}; do
+        if [ "$v" = default ]; then unset FCG_LIB; else export FCG_LIB=$v; fi
+        timeout -k 10 300 python3 tools/newton_bench.py --celltype hex27 --kinem totlag --n 100 --length 1 --load -1 --mg --mg-matrix-free --mg-outer-matrix-free > $O/c3lib_$v.log 2>&1 || { tail -20 $O/c3lib_$v.log; exit 1; }
+        echo "$v $(grep '^{' $O/c3lib_$v.log | tail -1)" >> $O/c3lib.jsonl
+      done; done; unset FCG_LIB
+      python3 -c "
+import json
+for l in open('$O/c3lib.jsonl'):
+    v, j = l.split(' ', 1); d = json.loads(j)
+    print(v, 'newton_s', round(d['newton_s'], 3), 'solve_ms', round(d['solve_ms_total'], 1), 'asm_ms', round(d['assembly_ms_mean'], 2), 'apply_ms', round(d['tangent_apply_ms'], 3), 'its', d['pcg_iterations'])" ;;
+    amglib)  # renumbered 1M hex8 TotLag Newton with the native AMG (bench.py's secondary), LIBS=...
+      for rep in 1 2; do for v in ${LIBS:-default}; do
+        if [ "$v" = default ]; then unset FCG_LIB; else export FCG_LIB=$v; fi
+        timeout -k 10 300 python3 tools/newton_bench.py --celltype hex8 --kinem totlag --n 100 --length 1 --load=-1e-2 --renumber --amg-native > $O/amglib_$v.log 2>&1 || { tail -20 $O/amglib_$v.log; exit 1; }
+        echo "$v $(grep '^{' $O/amglib_$v.log | tail -1)" >> $O/amglib.jsonl
+      done; done; unset FCG_LIB
+      python3 -c "
+import json
+for l in open('$O/amglib.jsonl'):
+    v, j = l.split(' ', 1); d = json.loads(j)
+    print(v, 'newton_s', round(d['newton_s'], 3), 'solve_ms', round(d['solve_ms_total'], 1), 'asm_ms', round(d['assembly_ms_mean'], 2), 'its', d['pcg_iterations'])" ;;
     tests)  # the whole GPU suite
       run 1500 gpu_tests.log python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests
       tail -3 $O/gpu_tests.log ;;
