@@ -1002,14 +1002,6 @@ SweepArgs sweep_args(const DeviceMesh& m, const double* d_u_col, double* d_K, do
 }
 }  // namespace
 
-hipError_t launch_sweep_h8(const DeviceMesh& m, const double* d_u_col, bool want_k,
-    bool overwrite, double* d_K, double* d_fint, hipStream_t stream)
-{
-  const int64_t ntiles = int64_t(m.tiles_x) * m.tiles_y * m.tiles_z;
-  if (ntiles == 0) return hipSuccess;
-  const SweepArgs a = sweep_args(m, d_u_col, d_K, d_fint);
-  const dim3 grid{static_cast<unsigned>(ntiles), 1, 1};
-  const dim3 block{256, 1, 1};
 #define FCG_SWEEP(KIN)                                                                             \
   if (want_k && m.sweep_defer && overwrite)                                                        \
     hipLaunchKernelGGL((sweep_h8_kernel<KIN, true, true, 3>), grid, block, 0, stream, a);      \
@@ -1023,15 +1015,37 @@ hipError_t launch_sweep_h8(const DeviceMesh& m, const double* d_u_col, bool want
     hipLaunchKernelGGL((sweep_h8_kernel<KIN, false, true, 0>), grid, block, 0, stream, a);     \
   else                                                                                             \
     hipLaunchKernelGGL((sweep_h8_kernel<KIN, false, false, 0>), grid, block, 0, stream, a);
-  if (m.kinem == 0)
-  {
-    FCG_SWEEP(0)
-  }
-  else
-  {
-    FCG_SWEEP(1)
-  }
-#undef FCG_SWEEP
+
+// The TotLag instantiations live in their own translation unit, fcg_sweep_totlag.hip (this file
+// with FCG_SWEEP_TOTLAG_TU), compiled without the SLP vectorizer: its pairing of the F / S
+// arithmetic into 2-wide vectors costs the TotLag sweep 7-10 % (same-box A/B, 1M hex8: 3.09 ->
+// 2.79 ms; profiles/r05/r05_noslp_sweep_ab.txt), while the linear and TSI sweeps gain nothing.
+hipError_t launch_sweep_h8_totlag(const DeviceMesh& m, const double* d_u_col, bool want_k,
+    bool overwrite, double* d_K, double* d_fint, hipStream_t stream);
+
+#ifdef FCG_SWEEP_TOTLAG_TU
+hipError_t launch_sweep_h8_totlag(const DeviceMesh& m, const double* d_u_col, bool want_k,
+    bool overwrite, double* d_K, double* d_fint, hipStream_t stream)
+{
+  const int64_t ntiles = int64_t(m.tiles_x) * m.tiles_y * m.tiles_z;
+  if (ntiles == 0) return hipSuccess;
+  const SweepArgs a = sweep_args(m, d_u_col, d_K, d_fint);
+  const dim3 grid{static_cast<unsigned>(ntiles), 1, 1};
+  const dim3 block{256, 1, 1};
+  FCG_SWEEP(1)
+  return hipGetLastError();
+}
+#else
+hipError_t launch_sweep_h8(const DeviceMesh& m, const double* d_u_col, bool want_k,
+    bool overwrite, double* d_K, double* d_fint, hipStream_t stream)
+{
+  if (m.kinem != 0) return launch_sweep_h8_totlag(m, d_u_col, want_k, overwrite, d_K, d_fint, stream);
+  const int64_t ntiles = int64_t(m.tiles_x) * m.tiles_y * m.tiles_z;
+  if (ntiles == 0) return hipSuccess;
+  const SweepArgs a = sweep_args(m, d_u_col, d_K, d_fint);
+  const dim3 grid{static_cast<unsigned>(ntiles), 1, 1};
+  const dim3 block{256, 1, 1};
+  FCG_SWEEP(0)
   return hipGetLastError();
 }
 
@@ -1075,5 +1089,7 @@ hipError_t launch_sweep_h8_tsi(const DeviceMesh& m, const double* d_u_col, bool 
   }
   return hipGetLastError();
 }
+#endif  // FCG_SWEEP_TOTLAG_TU
+#undef FCG_SWEEP
 
 }  // namespace fcg

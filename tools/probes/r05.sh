@@ -165,6 +165,17 @@ import json
 for l in open('$O/amglib.jsonl'):
     v, j = l.split(' ', 1); d = json.loads(j)
     print(v, 'newton_s', round(d['newton_s'], 3), 'solve_ms', round(d['solve_ms_total'], 1), 'asm_ms', round(d['assembly_ms_mean'], 2), 'its', d['pcg_iterations'])" ;;
+    rab)  # renumbered 1M hex8 through AUTO (lattice detection -> sweep MODE 3), LIBS=..., KINS=...
+      for r in 1 2 3; do for v in ${LIBS:-default}; do for k in ${KINS:-linear}; do
+        if [ "$v" = default ]; then unset FCG_LIB; else export FCG_LIB=$v; fi
+        echo "$v $k $(timeout -k 10 300 python3 $ET --celltype hex8 --kinem $k --n 100 --renumber --reps 9 | tail -1)" >> $O/rab.txt || exit 1
+      done; done; done; unset FCG_LIB
+      python3 -c "
+import json, collections
+t = collections.defaultdict(list)
+for l in open('$O/rab.txt'):
+    v, k, j = l.split(' ', 2); d = json.loads(j); t[(v, k)].append(round(d['ms_evaluate'], 4))
+for key, x in t.items(): print(key, x)" ;;
     tests)  # the whole GPU suite
       run 1500 gpu_tests.log python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests
       tail -3 $O/gpu_tests.log ;;
