@@ -665,7 +665,9 @@ int fcg_norm2(fcg_comm* comm, const double* d_x, int64_t n, void* stream, double
  * Data movement goes through an fcg_transport: fcg_transport_rccl (fcg_halo_import + ncclAllReduce
  * of a device buffer), or caller callbacks (MPI, or a host-staged rehearsal).  K holds the
  * Dirichlet unit rows (fcg_dirichlet_apply); the context's column map must start with its owned
- * DOFs in row order (Epetra's local-first column maps).  Blocking; x starts at 0.
+ * DOFs in row order (Epetra's local-first column maps).  Collective: every rank calls it, and
+ * either every rank passes an AMG handle or none does (fcg_amg_create refuses a rank without
+ * rows; such a partition solves with the block Jacobi, amg = NULL).  Blocking; x starts at 0.
  * ---------------------------------------------------------------------------------------- */
 typedef int (*fcg_import_fn)(void* user, const double* d_x_row, double* d_x_col, void* stream);
 typedef int (*fcg_allreduce_fn)(void* user, double* d_vals, int64_t n, void* stream);  /* in place, sum */
