@@ -91,13 +91,27 @@ struct SweepArgs {
 template <bool TSI>
 constexpr int node_comps() { return TSI ? 10 : 6; }
 
+// Record strides (doubles) of the per-(Gauss point, slot) arrays gp and tg below.  Stage A's lane
+// (slot s, Gauss point g) stores record 25 g + s; with 16 doubles (32 dwords) every record began on
+// bank 0 (mod 32), so a 16-lane ds_write_b64 group was a 16-way conflict and the visit loads at one
+// Gauss point saw two distinct banks.  18 (36 dwords) starts record r on bank 4 (g + s) mod 32
+// for the stores and 36 s mod 64 for the loads, 16-byte aligned for ds_*_b128 (1M hex8 TotLag
+// 2.76 -> 2.40 ms, profiles/r05/r05_gp_stride_ab.txt).  tg (TSI) at 6 instead of 4 measured the
+// same (4.31-4.40 vs 4.31-4.35 ms fused), so it stays at 4.
+#ifndef FCG_GP_STRIDE
+#define FCG_GP_STRIDE 18
+#endif
+#ifndef FCG_TG_STRIDE
+#define FCG_TG_STRIDE 4
+#endif
+
 template <int KIN, bool TSI, bool TH = false, bool DEFER = false>
 struct SweepShared {
   alignas(16) double nx[3 * 4 * NSLOT * 8 * 2];  // sqrt|fac| N_XYZ, see nx2i()
-  // TotLag: F (column-major) | S (Voigt) | c = fac / sqrt|fac|  (linear kinematics: unused)
-  double gp[KIN ? 8 : 1][KIN ? NSLOT : 1][16];
+  // TotLag: F (column-major) | S (Voigt) | c = fac / sqrt|fac| | pad  (linear kinematics: unused)
+  alignas(16) double gp[KIN ? 8 : 1][KIN ? NSLOT : 1][KIN ? FCG_GP_STRIDE : 16];
   // TSI: c = fac / sqrt|fac| | T_g | m c sqrt|fac| tr(B_L v)_g = m fac tr(e')_g | pad
-  alignas(16) double tg[TSI ? 8 : 1][TSI ? NSLOT : 1][4];
+  alignas(16) double tg[TSI ? 8 : 1][TSI ? NSLOT : 1][TSI ? FCG_TG_STRIDE : 4];
   double node[3][NNODE][node_comps<TSI>()];  // node columns of the 6 x 6 grid, ring by plane mod 3
   uint32_t prec[3][PLANE_REC_WORDS];  // plane records, ring by plane mod 3
   double gxi[8][4];  // Gauss point coordinates (stage A forms the shape derivatives from them)

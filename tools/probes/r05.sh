@@ -114,6 +114,12 @@ for l in open('$O/tsplit.txt'):
       timeout -k 10 900 tools/pmc_kernel.sh r05/h27pmc h27_element occ,inst,flop,mem -- --celltype hex27 --kinem totlag --n 40 --reps 3 > $O/h27pmc.log 2>&1 || { tail -20 $O/h27pmc.log; exit 1; }
       python3 tools/pmc_summary.py gpurun_out/r05/h27pmc assemble27 > gpurun_out/r05/h27pmc/summary_assemble27.txt
       tail -12 gpurun_out/r05/h27pmc/summary.txt; tail -12 gpurun_out/r05/h27pmc/summary_assemble27.txt ;;
+    tlpmc)  # counter sets of the 1M hex8 TotLag sweep for the default build and LIBS=... variants
+      for v in default ${LIBS:-}; do
+        if [ "$v" = default ]; then unset FCG_LIB; else export FCG_LIB=$v; fi
+        timeout -k 10 600 tools/pmc_kernel.sh r05/tlpmc_$v sweep_h8 occ,inst,flop,mem -- --celltype hex8 --kinem totlag --n 100 --reps 3 > $O/tlpmc_$v.log 2>&1 || { tail -20 $O/tlpmc_$v.log; exit 1; }
+        echo "== $v"; tail -12 gpurun_out/r05/tlpmc_$v/summary.txt
+      done; unset FCG_LIB ;;
     primprof)  # rocprofv3 kernel statistics of bench.py --only-primary (the headline's kernels)
       mkdir -p $O/primprof
       (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$O/primprof" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --only-primary --steps 20 --warmup 5) > $O/primprof.log 2>&1 || { tail -20 $O/primprof.log; exit 1; }
