@@ -541,7 +541,9 @@ bool build_structured_plan(const fcg_desc* d, const std::vector<int32_t>& rownod
   // FCG_SWEEP_WGS_PER_CU: occupancy probes (tools/exp_lib.sh builds with another launch bound)
   const char* wenv = std::getenv("FCG_SWEEP_WGS_PER_CU");
   const int wpc = wenv ? std::max(1, std::atoi(wenv)) : 2;
-  const int64_t slots = int64_t(std::max(1, cus)) * (d->kinematics == FCG_TOTLAG ? 1 : wpc);
+  const char* tenv = std::getenv("FCG_SWEEP_TOTLAG_WGS_PER_CU");  // the same, TotLag
+  const int tpc = tenv ? std::max(1, std::atoi(tenv)) : 1;
+  const int64_t slots = int64_t(std::max(1, cus)) * (d->kinematics == FCG_TOTLAG ? tpc : wpc);
   int64_t nseg = 1;
   double best = 0.0;
   for (int64_t k = 1; k <= std::min<int64_t>(P.n[2], 64); ++k)

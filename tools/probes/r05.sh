@@ -114,6 +114,16 @@ for l in open('$O/tsplit.txt'):
       timeout -k 10 900 tools/pmc_kernel.sh r05/h27pmc h27_element occ,inst,flop,mem -- --celltype hex27 --kinem totlag --n 40 --reps 3 > $O/h27pmc.log 2>&1 || { tail -20 $O/h27pmc.log; exit 1; }
       python3 tools/pmc_summary.py gpurun_out/r05/h27pmc assemble27 > gpurun_out/r05/h27pmc/summary_assemble27.txt
       tail -12 gpurun_out/r05/h27pmc/summary.txt; tail -12 gpurun_out/r05/h27pmc/summary_assemble27.txt ;;
+    tseg)  # TotLag sweep segmentation: the slot model at 1 / 2 / 3 / 4 workgroups per CU
+      for r in 1 2 3; do for w in 1 2 3 4; do
+        echo "wpc=$w $(FCG_SWEEP_TOTLAG_WGS_PER_CU=$w timeout -k 10 200 python3 $ET --celltype hex8 --kinem totlag --n 100 --reps 21 | tail -1)" >> $O/tseg.txt || exit 1
+      done; done
+      python3 -c "
+import json, collections
+t = collections.defaultdict(list)
+for l in open('$O/tseg.txt'):
+    v, j = l.split(' ', 1); t[v].append(round(json.loads(j)['ms_evaluate'], 4))
+for k, x in t.items(): print(k, x)" ;;
     tlpmc)  # counter sets of the 1M hex8 TotLag sweep for the default build and LIBS=... variants
       for v in default ${LIBS:-}; do
         if [ "$v" = default ]; then unset FCG_LIB; else export FCG_LIB=$v; fi
