@@ -373,7 +373,11 @@ struct fcg_amg {
   std::string last_error;
   std::vector<void*> allocs;
   double setup_ms = 0.0;
-  bool ready = false;  // a numeric setup has been made (fcg_amg_setup)
+  bool ready = false;  // a numeric setup has been made (fcg_amg_setup or the coupled setup)
+  // the rank-local hierarchy (lmax0, the Galerkin levels, the coarse inverse) matches the last K:
+  // set by fcg_amg_setup, cleared by the coupled numeric setup, which refreshes only the block
+  // inverses the coupled V-cycle smooths with -- fcg_amg_apply / fcg_amg_iterate need it
+  bool local_ready = false;
   // rank-local preconditioner of a multi-rank context: level 0 is the owned block (ghost column
   // triples dropped) and is applied through its BSR copy instead of the context's fcg_spmv
   bool local = false;
@@ -2284,6 +2288,78 @@ int64_t hierarchy_bytes(const fcg_amg* g)
   return b;
 }
 
+// A transport whose every collective is preceded by a status all-reduce (one double: 0 on a rank
+// still going).  The coupled build and numeric setup run over it, so a rank that throws between
+// two collectives (a malformed pattern, a singular level-1 block found by dist_setup, a HIP error)
+// joins the other ranks at their next collective with its status 1 instead of its payload
+// (guard_fail below); every rank then stops there together and returns an error.  The status
+// all-reduce is a host round trip per collective of the setup, never of the application.
+struct Guard {
+  const fcg_transport* in = nullptr;
+  fcg_amg* h = nullptr;
+  hipStream_t s = nullptr;
+  bool remote = false;   // a checkpoint saw another rank's failure (this rank joined it)
+  int64_t checkpoints = 0;
+  int64_t fail_at = -1;  // test hook: throw on reaching this checkpoint (a failure inside the build)
+};
+
+// all-reduced status: true when some rank reported a failure
+bool guard_checkpoint(Guard* g, double mine)
+{
+  if (!g->h->agree) g->h->agree = dalloc<double>(g->h, 2);
+  const double v[2] = {mine, 0.0};
+  double out[2] = {0.0, 0.0};
+  ck(hipMemcpyAsync(g->h->agree, v, sizeof(v), hipMemcpyHostToDevice, g->s), "hipMemcpyAsync");
+  ck(g->in->allreduce_fn(g->in->user, g->h->agree, 2, g->s), "transport all-reduce (status)");
+  ck(hipMemcpyAsync(out, g->h->agree, sizeof(out), hipMemcpyDeviceToHost, g->s), "hipMemcpyAsync");
+  ck(hipStreamSynchronize(g->s), "hipStreamSynchronize");
+  ++g->checkpoints;
+  return out[0] > 0.0;
+}
+
+int guard_enter(Guard* g)
+{
+  if (g->fail_at >= 0 && g->checkpoints >= g->fail_at)
+  {
+    g->fail_at = -1;
+    throw Fail{FCG_ERR_ARG, "coupled AMG: injected failure inside the build (FCG_AMG_INJECT_BUILD_FAIL)"};
+  }
+  if (!guard_checkpoint(g, 0.0)) return FCG_OK;
+  g->remote = true;
+  return FCG_ERR_DEVICE;
+}
+
+int guard_allreduce(void* u, double* d, int64_t n, void* s)
+{
+  Guard* g = static_cast<Guard*>(u);
+  const int rc = guard_enter(g);
+  return rc != FCG_OK ? rc : g->in->allreduce_fn(g->in->user, d, n, s);
+}
+
+int guard_import(void* u, const double* x_row, double* x_col, void* s)
+{
+  Guard* g = static_cast<Guard*>(u);
+  const int rc = guard_enter(g);
+  return rc != FCG_OK ? rc : g->in->import_fn(g->in->user, x_row, x_col, s);
+}
+
+int guard_exchange(void* u, const double* sb, const int64_t* sc, double* rb, const int64_t* rc_, void* s)
+{
+  Guard* g = static_cast<Guard*>(u);
+  const int rc = guard_enter(g);
+  return rc != FCG_OK ? rc : g->in->exchange_fn(g->in->user, sb, sc, rb, rc_, s);
+}
+
+fcg_transport guarded(const fcg_transport* tr, Guard* g)
+{
+  fcg_transport t = *tr;
+  t.user = g;
+  t.allreduce_fn = guard_allreduce;
+  t.import_fn = guard_import;
+  t.exchange_fn = tr->exchange_fn ? guard_exchange : nullptr;
+  return t;
+}
+
 }  // namespace fcg_amgs
 
 extern "C" {
@@ -2520,10 +2596,12 @@ int fcg_amg_setup(fcg_amg* h, const double* d_K_vals, void* stream)
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     h->ready = true;
+    h->local_ready = true;
   }
   catch (const Fail& f)
   {
     h->ready = false;
+    h->local_ready = false;
     h->last_error = f.msg;
     h->ctx->last_error = f.msg;
     return f.code;
@@ -2545,9 +2623,9 @@ int fcg_amg_iterate(fcg_amg* h, const double* d_K_vals, const double* d_b_row, d
     h->ctx->last_error = h->last_error;
     return FCG_ERR_ARG;
   }
-  if (!h->ready)
+  if (!h->ready || !h->local_ready)
   {
-    h->last_error = "fcg_amg_iterate: no numeric setup (call fcg_amg_setup first)";
+    h->last_error = "fcg_amg_iterate: no numeric setup of the handle's own hierarchy for this K (call fcg_amg_setup first)";
     return FCG_ERR_ARG;
   }
   int it = 0;
@@ -2624,9 +2702,10 @@ int fcg_amg_apply(fcg_amg* h, const double* d_K_vals, const double* d_r_row, dou
 {
   using namespace fcg_amgs;
   if (!h || !d_K_vals || !d_r_row || !d_z_row) return FCG_ERR_ARG;
-  if (!h->ready)
+  if (!h->ready || !h->local_ready)
   {
-    h->last_error = "fcg_amg_apply: no numeric setup (call fcg_amg_setup first)";
+    // after fcg_dfcg_solve's coupled setup only the coupled application is valid on this handle
+    h->last_error = "fcg_amg_apply: no numeric setup of the handle's own hierarchy for this K (call fcg_amg_setup first)";
     return FCG_ERR_ARG;
   }
   try
@@ -2670,6 +2749,7 @@ int fcg_amg_precond_setup(fcg_amg* h, const double* d_K, const fcg_transport* tr
     try
     {
       ck(hipSetDevice(h->device), "hipSetDevice");
+      h->local_ready = false;  // only the block inverses follow this K
       setup_coupled_local(h, d_K, stream ? static_cast<hipStream_t>(stream) : h->ctx->stream);
       h->ready = true;
     }
@@ -2732,6 +2812,21 @@ int fcg_amg_precond_setup(fcg_amg* h, const double* d_K, const fcg_transport* tr
   }
   if (!h->local) return FCG_OK;  // no rank's handle is rank-local: each keeps its own V-cycle
   int code = FCG_OK;
+  // the build and the numeric setup over the guarded transport: a rank failing inside them meets
+  // the others at their next collective (or at the final status below) and all stop together
+  Guard G;
+  G.in = tr;
+  G.h = h;
+  G.s = s;
+  const fcg_transport gt = guarded(tr, &G);
+  // test hook: FCG_AMG_INJECT_BUILD_FAIL="r:k" makes rank r throw inside coupled_build when it
+  // reaches its k-th guarded collective (tests/test_multigpu.py, tests/cxx/config3_native.cpp)
+  static const std::pair<int, int64_t> inject_build = [] {
+    const char* e = std::getenv("FCG_AMG_INJECT_BUILD_FAIL");
+    const char* c = e ? std::strchr(e, ':') : nullptr;
+    return e ? std::make_pair(std::atoi(e), c ? int64_t(std::atoll(c + 1)) : int64_t(0))
+             : std::make_pair(-1, int64_t(0));
+  }();
   try
   {
     ck(hipSetDevice(h->device), "hipSetDevice");
@@ -2740,7 +2835,9 @@ int fcg_amg_precond_setup(fcg_amg* h, const double* d_K, const fcg_transport* tr
     {
       try
       {
-        coupled_build(h, tr, s);
+        if (tr->rank == inject_build.first) G.fail_at = inject_build.second;
+        coupled_build(h, &gt, s);
+        G.fail_at = -1;
       }
       catch (const Fail&)
       {
@@ -2754,19 +2851,33 @@ int fcg_amg_precond_setup(fcg_amg* h, const double* d_K, const fcg_transport* tr
     }
     else if (h->cpl->rank != tr->rank || h->cpl->nranks != tr->nranks)
       throw Fail{FCG_ERR_ARG, "coupled AMG: the transport's rank / rank count changed"};
-    coupled_setup(h, d_K, tr, s);
+    coupled_setup(h, d_K, &gt, s);
+  }
+  catch (const Fail& f)
+  {
+    h->ready = false;
+    if (G.remote)
+      return others_failed(FCG_ERR_DEVICE);  // met another rank's failure at a collective: done
+    h->last_error = f.msg;
+    h->ctx->last_error = f.msg;
+    code = f.code;
+  }
+  // the final status: the ranks that finished and the ranks that failed on their own meet here (a
+  // rank that failed is at the same count of checkpoints as the others' next one)
+  bool any = false;
+  try
+  {
+    any = guard_checkpoint(&G, code != FCG_OK ? 1.0 : 0.0);
   }
   catch (const Fail& f)
   {
     h->ready = false;
     h->last_error = f.msg;
     h->ctx->last_error = f.msg;
-    code = f.code;
+    return code != FCG_OK ? code : f.code;
   }
-  const int rb = agree(code != FCG_OK ? 1.0 : 0.0, 0.0, g);
   if (code != FCG_OK) return code;
-  if (rb != FCG_OK) return rb;
-  if (g[0] > 0.0) return others_failed(FCG_ERR_DEVICE);
+  if (any) return others_failed(FCG_ERR_DEVICE);
   return FCG_OK;
 }
 

@@ -1328,7 +1328,7 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
     chk(upload_big(&m.col_lid, d->col_lid, m.nnz));
     chk(upload(&m.diag_pos, diag.data(), d->n_rows, bytes));
   }
-  chk(upload<int32_t>(&m.err, nullptr, 2, bytes));
+  chk(upload<int32_t>(&m.err, nullptr, 3, bytes));
   if (he == hipSuccess) he = hipHostMalloc(reinterpret_cast<void**>(&m.err_host), 2 * sizeof(int32_t),
       hipHostMallocDefault);
   if (structured)
@@ -1574,8 +1574,18 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
       }
       const char* eg = std::getenv("FCG_H27_EL_GRID");
       m.h27_el_grid = eg ? std::max(1, std::atoi(eg)) : 2 * n_cu;  // the resident workgroups
+      // the full scratch whenever it fits: the slab schedule costs about +25 % per evaluate, so
+      // it is taken only when the records plus the caller's K values (and 4 GB of headroom for the
+      // vectors and the solver) would not fit the device's free memory now
       const double full = double(n_inc) * double(fcg::record_doubles(npe)) * sizeof(double);
-      if (!sl && mem_total > 0 && full > 0.25 * double(mem_total))
+      size_t mem_free = 0, mem_tot2 = 0;
+      if (hipMemGetInfo(&mem_free, &mem_tot2) != hipSuccess)
+      {
+        (void)hipGetLastError();
+        mem_free = mem_total;
+      }
+      const double need = full + double(m.nnz) * sizeof(double) + double(int64_t(4) << 30);
+      if (!sl && mem_free > 0 && need > double(mem_free))
         S = std::max<int64_t>(4096, d->n_ele / 200);
       int64_t n_slots = n_inc;
       if (m.h27_increc && S > 0 && S < d->n_ele)
@@ -1667,7 +1677,9 @@ void read_timing(fcg::Timing& T)
   (void)hipEventElapsedTime(&a, T.ev[0], T.ev[1]);
   (void)hipEventElapsedTime(&b, T.ev[1], T.ev[2]);
   T.ms_element = a;
-  T.ms_assemble = T.path == FCG_PATH_GENERAL ? b : 0.0;  // fused: evaluate + assembly in ms_element
+  // fused kernels and the hex27 slab schedule: evaluate + assembly in ms_element
+  T.ms_element = T.fused ? a + b : a;
+  T.ms_assemble = T.path == FCG_PATH_GENERAL && !T.fused ? b : 0.0;
 }
 
 }  // namespace
@@ -1844,6 +1856,7 @@ int fcg_evaluate_device(fcg_ctx* ctx, int action, int mode, const double* d_u_co
     he = hipEventRecord(T.ev[2], s);
     T.pending = true;
     T.path = m.path;
+    T.fused = m.path == FCG_PATH_GENERAL && m.h27_nslab > 1;
   }
   // async: the flags stay sticky on the device across queued evaluates and fcg_check_error reads
   // them once (a read-back per evaluate would put a copy between every two evaluates' kernels)
@@ -2008,6 +2021,9 @@ int fcg_get_info(const fcg_ctx* ctx, fcg_info* info)
                               int64_t(sizeof(double));
   info->device_bytes = ctx->device_bytes;
   info->path = m.path;
+  info->h27_slabs = m.path == FCG_PATH_GENERAL && m.h27s && m.h27_increc
+                        ? int32_t(std::max<int64_t>(1, m.h27_nslab))
+                        : 0;
   return FCG_OK;
 }
 

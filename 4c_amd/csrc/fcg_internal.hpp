@@ -34,7 +34,9 @@ struct DeviceMesh {
   uint16_t* inc_pos = nullptr;      // [n_inc][npe] column position of node b in the row
   int64_t* rowptr = nullptr;        // [n_rows+1]
   double* scratch = nullptr;        // [n_inc][record_doubles(npe)]
-  int32_t* err = nullptr;           // [2]: code, min failing element index
+  int32_t* err = nullptr;           // [3]: code, min failing element index; [2] the solver flag
+  // (Dirichlet / block-Jacobi / PCG kernels write only err[2], so a failed element's flags from an
+  // async evaluate survive them until fcg_check_error reads them)
   // evaluate's error-flag protocol: err holds {0, INT32_MAX} between calls while err_clean is set
   // (no per-call re-initialisation); whatever else writes err clears err_clean.  The flags come
   // back through the pinned err_host (a DMA, not a staged pageable copy).
@@ -138,6 +140,7 @@ struct Timing {
   bool enabled = false;
   bool pending = false;  // events recorded, durations not read yet (async evaluate)
   int path = 0;
+  bool fused = false;  // ev[1] marks no element/assembly boundary (hex27 slab schedule)
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
   double ms_element = 0.0, ms_assemble = 0.0;
 };

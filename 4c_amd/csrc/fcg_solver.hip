@@ -643,17 +643,17 @@ int fcg_dirichlet_apply(fcg_ctx* ctx, int64_t n_dbc, const int32_t* d_rows, doub
   (void)hipSetDevice(ctx->device);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   const int32_t zero = 0;
-  m.err_clean = false;  // err[0] becomes this call's flag
-  hipError_t he = hipMemcpyAsync(m.err, &zero, sizeof(zero), hipMemcpyHostToDevice, s);
+  int32_t* flag = m.err + 2;  // the solver flag word: evaluate's sticky flags are left alone
+  hipError_t he = hipMemcpyAsync(flag, &zero, sizeof(zero), hipMemcpyHostToDevice, s);
   if (he == hipSuccess)
   {
     hipLaunchKernelGGL(fcg::dirichlet_kernel, dim3(fcg::blocks_for(n_dbc * 64, fcg::kBlock)),
         dim3(fcg::kBlock), 0, s, m.rowptr, m.diag_pos, d_rows, n_dbc, m.n_rows, d_K_vals, d_rhs_row,
-        d_freact_row, m.err);
+        d_freact_row, flag);
     he = hipGetLastError();
   }
   int32_t bad = 0;
-  if (he == hipSuccess) he = hipMemcpyAsync(&bad, m.err, sizeof(bad), hipMemcpyDeviceToHost, s);
+  if (he == hipSuccess) he = hipMemcpyAsync(&bad, flag, sizeof(bad), hipMemcpyDeviceToHost, s);
   if (he == hipSuccess) he = hipStreamSynchronize(s);
   if (he != hipSuccess)
   {
@@ -718,12 +718,12 @@ int fcg_pcg_solve(fcg_ctx* ctx, const double* d_K_vals, const double* d_b_row, d
   double* pc = pb + nb;
   double* sc = pc + nb;
   const int32_t zero = 0;
-  m.err_clean = false;  // err[0] becomes this call's flag
-  he = hipMemcpyAsync(m.err, &zero, sizeof(zero), hipMemcpyHostToDevice, s);
+  int32_t* flag = m.err + 2;  // the solver flag word: evaluate's sticky flags are left alone
+  he = hipMemcpyAsync(flag, &zero, sizeof(zero), hipMemcpyHostToDevice, s);
   if (he == hipSuccess)
   {
     hipLaunchKernelGGL(fcg::block_jacobi_kernel, dim3(fcg::blocks_for(nn, fcg::kBlock)), dim3(fcg::kBlock), 0, s,
-        m.rownode_row0, m.diag_pos, d_K_vals, dinv, nn, m.err);
+        m.rownode_row0, m.diag_pos, d_K_vals, dinv, nn, flag);
     hipLaunchKernelGGL(fcg::pcg_init_kernel, dim3(nb_node), dim3(fcg::kBlock), 0, s, m.rownode_row0,
         d_b_row, dinv, d_x_row, r, z, p, nn, pa, pb);
     hipLaunchKernelGGL(fcg::reduce_kernel, dim3(1), dim3(fcg::kBlock), 0, s, pa, nb_node, sc,
@@ -733,7 +733,7 @@ int fcg_pcg_solve(fcg_ctx* ctx, const double* d_K_vals, const double* d_b_row, d
   double hsc[fcg::SC_N] = {0};
   int32_t bad = 0;
   if (he == hipSuccess) he = hipMemcpyAsync(hsc, sc, sizeof(hsc), hipMemcpyDeviceToHost, s);
-  if (he == hipSuccess) he = hipMemcpyAsync(&bad, m.err, sizeof(bad), hipMemcpyDeviceToHost, s);
+  if (he == hipSuccess) he = hipMemcpyAsync(&bad, flag, sizeof(bad), hipMemcpyDeviceToHost, s);
   if (he == hipSuccess) he = hipStreamSynchronize(s);
   if (he != hipSuccess)
   {
@@ -813,15 +813,15 @@ int fcg_block_jacobi_setup(fcg_ctx* ctx, const double* d_K_vals, double* d_dinv,
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   const int32_t zero = 0;
   int32_t bad = 0;
-  m.err_clean = false;
-  hipError_t he = hipMemcpyAsync(m.err, &zero, sizeof(zero), hipMemcpyHostToDevice, s);
+  int32_t* flag = m.err + 2;  // the solver flag word: evaluate's sticky flags are left alone
+  hipError_t he = hipMemcpyAsync(flag, &zero, sizeof(zero), hipMemcpyHostToDevice, s);
   if (he == hipSuccess && nn > 0)
   {
     hipLaunchKernelGGL(fcg::block_jacobi_kernel, dim3(fcg::blocks_for(nn, fcg::kBlock)), dim3(fcg::kBlock), 0, s,
-        m.rownode_row0, m.diag_pos, d_K_vals, d_dinv, nn, m.err);
+        m.rownode_row0, m.diag_pos, d_K_vals, d_dinv, nn, flag);
     he = hipGetLastError();
   }
-  if (he == hipSuccess) he = hipMemcpyAsync(&bad, m.err, sizeof(bad), hipMemcpyDeviceToHost, s);
+  if (he == hipSuccess) he = hipMemcpyAsync(&bad, flag, sizeof(bad), hipMemcpyDeviceToHost, s);
   if (he == hipSuccess) he = hipStreamSynchronize(s);
   if (he != hipSuccess)
   {

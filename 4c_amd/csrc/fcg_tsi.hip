@@ -876,6 +876,13 @@ int fcg_tsi_evaluate_fused(fcg_ctx* sctx, fcg_tsi_ctx* ctx, int mode, const doub
     return FCG_ERR_ARG;
   }
   (void)hipSetDevice(ctx->device);
+  // the fused pass re-initialises the structural context's flags: a queued (async) evaluate's
+  // failure is reported first, as fcg_evaluate_host does, instead of being overwritten
+  if (sctx->pending)
+  {
+    const int rc = fcg_check_error(sctx, bad_ele_gid);
+    if (rc != FCG_OK) return rc;
+  }
   hipStream_t s = stream_ptr ? static_cast<hipStream_t>(stream_ptr) : ctx->stream;
   hipError_t he = hipSuccess;
   if (d.fused_with != static_cast<const void*>(sctx))

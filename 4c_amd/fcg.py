@@ -25,7 +25,7 @@ PATH_AUTO, PATH_GENERAL, PATH_STRUCTURED, PATH_COLORED, PATH_GATHER = 0, 1, 2, 3
 MAT_STVK, MAT_ELASTHYPER_COUPNEOHOOKE = 0, 1
 TSI_STRUCT_FORCE, TSI_STIFFTEMP, TSI_THERMO_FINTCOND, TSI_COUPLTANG = 1, 2, 4, 8
 TSI_ALL = 15
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 FCG_OK, FCG_ERR_NODAL_DETJ, FCG_ERR_SINGULAR, FCG_ERR_ARG, FCG_ERR_DEVICE = 0, 1, 2, 3, 4
 STATUS = {0: "FCG_OK", 1: "FCG_ERR_NODAL_DETJ", 2: "FCG_ERR_SINGULAR", 3: "FCG_ERR_ARG",
@@ -59,7 +59,7 @@ class FcgInfo(ctypes.Structure):
                 ("n_cols", ctypes.c_int64), ("nnz", ctypes.c_int64),
                 ("n_incidences", ctypes.c_int64), ("scratch_bytes", ctypes.c_int64),
                 ("device_bytes", ctypes.c_int64), ("path", ctypes.c_int32),
-                ("reserved", ctypes.c_int32)]
+                ("h27_slabs", ctypes.c_int32)]
 
 
 class FcgImportPlan(ctypes.Structure):

@@ -236,7 +236,7 @@ def measure_mfma_h27(n, cus):
                       "3 evaluates, mean per dispatch)"}
 
 
-def measure_traffic(n, kernel="sweep_h8", timeout_s=150):
+def measure_traffic(n, kernel="sweep_h8", timeout_s=150, extra=()):
     """HBM bytes per evaluate of the bench kernel, measured in this run: two rocprofv3 counter
     passes (FETCH_SIZE, then WRITE_SIZE -- they do not fit one pass), each a child process
     (tools/prof_kernel.py: the same n^3 mesh, seed and kernel, 3 evaluates) under its own time
@@ -257,7 +257,7 @@ def measure_traffic(n, kernel="sweep_h8", timeout_s=150):
             d = os.path.join(work, ctr)
             cmd = [rp, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "run", "--",
                    sys.executable, os.path.join(ROOT, "tools", "prof_kernel.py"), "--n", str(n),
-                   "--seed", "20251015", "--reps", "3"]
+                   "--seed", "20251015", "--reps", "3", *extra]
             env = dict(os.environ, TMPDIR=work)
             p = subprocess.run(cmd, cwd=work, env=env, capture_output=True, text=True,
                                timeout=timeout_s)
@@ -352,6 +352,7 @@ def newton_secondary(n, timeout_s=900, cpu_rate=None):
         "solve_ms_total": d["solve_ms_total"], "setup_s": d["setup_s"],
         "setup_phases": d.get("setup_phases"), "wall_s": wall,
         "elements": d["elements"], "dofs": d["dofs"], "nnz": d["nnz"], "tip_uz": d["tip_uz"],
+        "h27_slabs": d.get("h27_slabs"), "scratch_bytes": d.get("scratch_bytes"),
         "tangent_symmetry_rel": d.get("tangent_symmetry_rel"),
     }
     # the loop's two device phases against the HBM roof: the K + r assembly of every Newton
@@ -477,7 +478,7 @@ def hex27_secondary(dev, n, steps, threads, with_cpu):
     out = {
         "workload": f"hex27-totlag-{n}^3", "baseline_config": "BASELINE.json configs[2] element",
         "value": mesh.n_ele / wall, "unit": "element-evaluations/s", "ms_per_step": 1e3 * wall,
-        "elements": mesh.n_ele, "nnz": mesh.nnz,
+        "elements": mesh.n_ele, "nnz": mesh.nnz, "h27_slabs": int(ev.info.h27_slabs),
         "path": ("general: h27_element_kernel (two elements in flight per workgroup: wave 3 forms "
                  "the next element's Jacobians (MFMA) and Gauss-point factors while waves 0-2 put "
                  "this one's G, c_ab, geo on v_mfma_f64_16x16x4_f64) writing the owned incidences' "
@@ -546,7 +547,8 @@ def hex27_slab_secondary(dev, n, steps, slab):
     out = {"workload": f"hex27-totlag-{n}^3-slab-schedule",
            "baseline_config": "BASELINE.json configs[2] mesh, incidence records in a ring",
            "value": mesh.n_ele / (ms * 1e-3), "unit": "element-evaluations/s", "ms_per_step": ms,
-           "slab_elements": slab, "scratch_bytes": int(info.scratch_bytes),
+           "slab_elements": slab, "h27_slabs": int(info.h27_slabs),
+           "scratch_bytes": int(info.scratch_bytes),
            "scratch_bytes_one_record_per_incidence": full, "device_bytes": int(info.device_bytes),
            "tangent_bytes": 8 * mesh.nnz}
     ev.close()
@@ -839,6 +841,58 @@ def gather_secondary(dev, n, steps):
         return {"workload": "hex8 renumbered (gather path)", "error": repr(e)}
 
 
+def totlag_sweep_secondary(dev, n, steps, with_pmc):
+    """Config 2's mesh (n^3 hex8 GridGenerator box) with StVK total-Lagrangian kinematics
+    (4C_solid_3D_ele_calc_displacement_based.hpp:45-72: F from the current coordinates, E, S, B_NL,
+    K_geo) on the structured row-block sweep (sweep_h8_kernel<TotLag>): K + r per step, kernel time
+    by hipEvents, HBM fraction by SURVEY §8d's bytes per element and the HBM traffic from counters
+    of this run."""
+    try:
+        mesh = fcg.BoxMesh(fcg.HEX8, (n, n, n), jitter=0.1, seed=20251015)
+        ev = fcg.Evaluator(mesh, kinematics=fcg.TOTLAG, youngs=210.0, poisson=0.3, device=dev.index)
+        u = torch.from_numpy(mesh.u_col(5e-2)).to(dev)
+        f = torch.zeros(mesh.n_rows, dtype=torch.float64, device=dev)
+        K = torch.zeros(mesh.nnz, dtype=torch.float64, device=dev)
+        for _ in range(5):
+            ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u, f, K)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u, f, K)
+        torch.cuda.synchronize(dev)
+        wall = (time.perf_counter() - t0) / steps
+        ev.set_timing(True)
+        ts = []
+        for _ in range(steps):
+            ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u, f, K)
+            ts.append(sum(ev.timing()))
+        ms_kern = float(np.mean(ts))
+        alg = ALG_BYTES_PER_ELE * mesh.n_ele
+        gbs = alg / (ms_kern * 1e-3) / 1e9
+        path = int(ev.info.path)
+        out = {"workload": f"hex8-totlag-{n}^3 structured (sweep)",
+               "baseline_config": "BASELINE.json configs[1] mesh, StVK total Lagrangian",
+               "value": mesh.n_ele / wall, "unit": "element-evaluations/s", "ms_per_step": 1e3 * wall,
+               "ms_kernel": ms_kern, "elements": mesh.n_ele, "nnz": mesh.nnz,
+               "path": "structured" if path == fcg.PATH_STRUCTURED else path,
+               "roofline": {"bound": "hbm", "kernel": "sweep_h8_kernel<1,...> (TotLag)",
+                            "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": gbs / HBM_PEAK_GBS, "alg_bytes_per_element": ALG_BYTES_PER_ELE,
+                            "alg_bytes_per_launch": alg}}
+        ev.close()
+        del K, f, u
+        torch.cuda.empty_cache()
+        if with_pmc:
+            tr = measure_traffic(n, kernel="sweep_h8_kernel<1", extra=("--kinem", "totlag"))
+            if "error" not in tr:
+                tr["ratio_to_algorithmic"] = tr["hbm_bytes_per_evaluate"] / alg
+                out["roofline"]["traffic"] = tr["hbm_bytes_per_evaluate"]
+            out["roofline"]["traffic_detail"] = tr
+        return out
+    except Exception as e:  # report, never hide
+        return {"workload": "hex8-totlag structured (sweep)", "error": repr(e)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -856,6 +910,8 @@ def main():
     ap.add_argument("--no-amg", action="store_true",
                     help="skip the unstructured-mesh Newton line (native AMG)")
     ap.add_argument("--newton-n", type=int, default=100)
+    ap.add_argument("--no-totlag", action="store_true",
+                    help="skip the structured hex8 TotLag sweep line")
     ap.add_argument("--no-slab", action="store_true",
                     help="skip the config-3 mesh under the slab schedule of the hex27 records")
     ap.add_argument("--no-optionb", action="store_true", help="skip the option-B (shared-DOF) line")
@@ -877,7 +933,7 @@ def main():
     args = ap.parse_args()
     if args.only_primary:
         for k in ("no_cpu_baseline", "no_hex27", "no_tsi", "no_newton", "no_amg", "no_optionb",
-                  "no_host", "no_pmc", "no_gather", "no_slab"):
+                  "no_host", "no_pmc", "no_gather", "no_slab", "no_totlag"):
             setattr(args, k, True)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -1186,6 +1242,9 @@ def main():
         secondary.append(host_secondary(dev, args.n, 3))
     if rank == 0 and world == 1 and not args.no_gather:
         secondary.append(gather_secondary(dev, args.n, max(3, min(args.steps, 10))))
+    if rank == 0 and world == 1 and not args.no_totlag:
+        secondary.append(totlag_sweep_secondary(dev, args.n, max(3, min(args.steps, 10)),
+                                                not args.no_pmc))
         torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_hex27:
         try:

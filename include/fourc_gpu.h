@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define FCG_ABI_VERSION 1
+#define FCG_ABI_VERSION 2  /* 2: fcg_transport gained exchange_fn */
 
 /* Cell types (Core::FE::CellType::hex8 / hex27) */
 enum fcg_celltype { FCG_HEX8 = 0, FCG_HEX27 = 1 };
@@ -160,7 +160,9 @@ int fcg_memset_device(void* d_dst, int value, int64_t bytes);
 
 /* Per-kernel timing of the last evaluate on the launch stream, measured with hipEvents
  * (enable before the call).  GENERAL path: element kernel, assemble kernel.  STRUCTURED path:
- * the fused kernel in ms_element, 0 in ms_assemble.  Returns the number of kernels timed. */
+ * the fused kernel in ms_element, 0 in ms_assemble.  hex27 slab schedule (fcg_info.h27_slabs > 1):
+ * the slabs' element and row launches interleave, so ms_element holds both and ms_assemble is 0.
+ * Returns the number of kernels timed. */
 int fcg_set_timing(fcg_ctx* ctx, int enable);
 int fcg_get_timing(const fcg_ctx* ctx, double* ms_element, double* ms_assemble);
 
@@ -171,7 +173,12 @@ typedef struct fcg_info {
   int64_t scratch_bytes;    /* device scratch for element block-rows */
   int64_t device_bytes;     /* total device memory held by the context */
   int32_t path;             /* fcg_path actually used (GENERAL, STRUCTURED or COLORED) */
-  int32_t reserved;
+  /* hex27 incidence records (GENERAL path): 1 = one record per incidence (the full scratch, the
+   * fast mode), > 1 = the slab schedule with that many slabs (a ring of records, DESIGN §7e: less
+   * memory, about +25 % per evaluate), 0 = not the hex27 record path.  By default the slab
+   * schedule is taken only when the full scratch plus the K values would not fit the device's free
+   * memory at fcg_create; FCG_H27_SLAB = elements per slab forces it (0 = one slab). */
+  int32_t h27_slabs;
 } fcg_info;
 int fcg_get_info(const fcg_ctx* ctx, fcg_info* info);
 
@@ -677,6 +684,8 @@ typedef int (*fcg_allreduce_fn)(void* user, double* d_vals, int64_t n, void* str
  * entries, this rank's own entries 0.  Ordered after the work already queued on `stream`. */
 typedef int (*fcg_exchange_fn)(void* user, const double* d_send, const int64_t* send_counts,
     double* d_recv, const int64_t* recv_counts, void* stream);
+/* Zero-initialise the struct (`fcg_transport t = {0};` / `{}`) before filling it field by field:
+ * members added in later ABI versions (exchange_fn in version 2) must read NULL, not garbage. */
 typedef struct fcg_transport {
   fcg_import_fn import_fn;
   fcg_allreduce_fn allreduce_fn;
@@ -729,7 +738,9 @@ int fcg_dfcg_solve(fcg_ctx* ctx, fcg_amg* amg, const fcg_transport* tr, const do
  * Deferred error check.  With fcg_set_async(ctx, 1), fcg_evaluate_device returns once the work is
  * queued on the stream (no drain, no host round trip per call); 4C's throws (FCG_ERR_NODAL_DETJ,
  * FCG_ERR_SINGULAR) are then reported by fcg_check_error, which waits for the queued evaluates
- * and returns the first failure since the last check (sticky until checked).
+ * and returns the first failure since the last check (sticky until checked: fcg_dirichlet_apply,
+ * fcg_pcg_solve and fcg_block_jacobi_setup report through a flag word of their own, and
+ * fcg_evaluate_host / fcg_tsi_evaluate_fused report a pending failure before they start).
  * ---------------------------------------------------------------------------------------- */
 int fcg_set_async(fcg_ctx* ctx, int enable);
 int fcg_check_error(fcg_ctx* ctx, int32_t* bad_ele_gid);

@@ -13,6 +13,9 @@
 // quadratically as the reference's full Newton does.
 //
 // usage: config3_native N R     (N elements per direction, R ranks; prints PASS / FAIL)
+//        config3_native N R inject   with FCG_AMG_INJECT_BUILD_FAIL="r:k" in the environment: rank r
+//        fails inside the coupled AMG build; every rank's fcg_dfcg_solve must return an error (no
+//        rank is left waiting in a collective -- this mode never releases the barriers for them)
 #include <algorithm>
 #include <atomic>
 #include <cmath>
@@ -177,6 +180,7 @@ struct RankResult {
 };
 
 std::mutex g_create;  // contexts are created one at a time (library setup is per process)
+bool g_inject = false;  // fault-injection run: a failed solve does not release the other ranks
 
 void run_rank(int n, int nranks, int rank, ThreadComm* tc, RankResult* out)
 {
@@ -308,7 +312,16 @@ void run_rank(int n, int nranks, int rank, ThreadComm* tc, RankResult* out)
     double rel = 0.0;
     if (fcg_dfcg_solve(ctx, amg, &tr, static_cast<double*>(dK), static_cast<double*>(drhs),
             static_cast<double*>(ddu), 1e-10, 500, nullptr, &li, &rel) != FCG_OK)
+    {
+      if (g_inject)
+      {
+        // the library must have stopped every rank by itself: no tc->fail() here
+        out->err = std::string("fcg_dfcg_solve: ") + fcg_last_error(ctx);
+        out->ok = false;
+        return;
+      }
       return fail(std::string("fcg_dfcg_solve: ") + fcg_last_error(ctx));
+    }
     out->lin_iters.push_back(li);
     fcg_memcpy_d2h(du.data(), ddu, nr * 8);
     double dd = 0.0;
@@ -364,6 +377,28 @@ int main(int argc, char** argv)
 {
   const int n = argc > 1 ? std::atoi(argv[1]) : 8;
   const int nranks = argc > 2 ? std::atoi(argv[2]) : 2;
+  if (argc > 3 && std::strcmp(argv[3], "inject") == 0)
+  {
+    g_inject = true;
+    const char* e = std::getenv("FCG_AMG_INJECT_BUILD_FAIL");
+    const int bad = e ? std::atoi(e) : -1;
+    ThreadComm tc(nranks);
+    std::vector<RankResult> rr(static_cast<size_t>(nranks));
+    std::vector<std::thread> th;
+    for (int r = 0; r < nranks; ++r) th.emplace_back(run_rank, n, nranks, r, &tc, &rr[size_t(r)]);
+    for (auto& t : th) t.join();
+    int failures = 0;
+    for (int r = 0; r < nranks; ++r)
+    {
+      const std::string& m = rr[size_t(r)].err;
+      std::printf("rank %d/%d: %s\n", r, nranks, m.empty() ? "(no error)" : m.c_str());
+      const bool want = r == bad ? m.find("injected") != std::string::npos
+                                 : m.find("another rank") != std::string::npos;
+      failures += rr[size_t(r)].ok || !want;
+    }
+    std::printf(failures ? "FAIL (%d)\n" : "PASS\n", failures);
+    return failures ? 1 : 0;
+  }
   int failures = 0;
   std::map<int32_t, double> u1, uR;
   std::vector<double> res1, resR;

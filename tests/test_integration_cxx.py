@@ -67,3 +67,19 @@ def test_config3_native_cxx_host(n, ranks, dist):
         assert all(st[0] == 1 for st in stats), p.stdout
         assert sum(st[1] for st in stats) == glob, p.stdout  # each level-1 row on one rank
         assert all(st[4] < 6 * glob for st in stats), p.stdout  # level 2 all-reduced, not level 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,ranks,at", [(16, 2, 0), (16, 2, 4), (16, 4, 2), (16, 4, 9)])
+def test_config3_native_failure_inside_the_amg_build(n, ranks, at):
+    """Thread transport (tests/cxx/config3_native.cpp `inject`): rank 1 throws inside the coupled
+    AMG build at its at-th collective (FCG_AMG_INJECT_BUILD_FAIL, level 1 distributed); the host
+    never releases the other ranks' barriers, so a rank left inside a collective would hang until
+    the timeout -- every rank's fcg_dfcg_solve must return an error instead."""
+    if not os.path.exists(NATIVE):
+        subprocess.run(["make", "-s", "-C", CXX], check=True)
+    env = dict(os.environ, FCG_AMG_DIST="1", FCG_AMG_INJECT_BUILD_FAIL=f"1:{at}")
+    p = subprocess.run([NATIVE, str(n), str(ranks), "inject"], capture_output=True, text=True,
+                       timeout=120, env=env)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "PASS" in p.stdout, p.stdout

@@ -118,6 +118,27 @@ def test_async_evaluate_defers_errors():
     ev2.set_async(False)
 
 
+def test_async_element_error_survives_dirichlet_and_solver():
+    """The Newton order of INTEGRATION.md: evaluate (async) -> fcg_dirichlet_apply -> the solve's
+    block-Jacobi setup -> fcg_check_error.  The Dirichlet and solver kernels report through their
+    own flag word, so the failed element's flag (4C's throw) is still there when checked."""
+    dev = _dev()
+    mesh = fcg.BoxMesh(fcg.HEX8, (2, 2, 2))
+    mesh.node_x[:, 0] *= -1.0
+    ev = fcg.Evaluator(mesh, kinematics=fcg.LINEAR, youngs=E, poisson=NU)
+    ev.set_async(True)
+    u = torch.zeros(mesh.n_cols, dtype=torch.float64, device=dev)
+    f = torch.zeros(mesh.n_rows, dtype=torch.float64, device=dev)
+    K = torch.zeros(mesh.nnz, dtype=torch.float64, device=dev)
+    ev.evaluate_device(fcg.CALC_NLNSTIFF, fcg.OVERWRITE, u, f, K)
+    rows = torch.arange(0, 6, dtype=torch.int32, device=dev)
+    ev.dirichlet_apply(rows, K, f.clone())
+    with pytest.raises(fcg.FcgError) as ei:
+        ev.check_error()
+    assert ei.value.code == 1 and ei.value.bad_ele_gid == 0
+    ev.set_async(False)
+
+
 @pytest.mark.parametrize("threads", ["8", "0"])
 def test_host_overwrite_entry_point(threads):
     """fcg_evaluate_host(OVERWRITE): the caller's zero() fused -- garbage in K and f is
@@ -440,6 +461,37 @@ def test_coupled_amg_setup_failure_on_one_rank_fails_every_rank():
         assert ok is not True, (rank, ok)
     assert "another rank" in res[0][1], res[0][1][-400:]
     assert "injected" in res[1][1], res[1][1][-400:]
+
+
+@pytest.mark.parametrize("world,at", [(2, 0), (2, 3), (4, 1), (4, 6)])
+def test_coupled_amg_failure_inside_the_build_fails_every_rank(world, at):
+    """Rank 1 throws inside the coupled AMG build (FCG_AMG_INJECT_BUILD_FAIL="1:at": on reaching its
+    at-th collective of the build, with level 1 distributed so the build's exchanges run) while the
+    other ranks are inside the build's imports and exchanges.  The build runs over a transport
+    whose collectives are preceded by a status all-reduce, so every rank's solve returns an error
+    (rank 1 its own, the others "another rank") instead of leaving them waiting (gloo transport)."""
+    _dev()
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    qq = ctx.Queue()
+    port = 29700 + (os.getpid() + 11 + at) % 1000
+    with _env(FCG_AMG_INJECT_BUILD_FAIL=f"1:{at}", FCG_AMG_DIST="1"):
+        procs = [ctx.Process(target=_worker_solve, args=(r, world, port, qq, fcg.LINEAR, fcg.PATH_AUTO,
+                                                         "staged", "native")) for r in range(world)]
+        for p in procs:
+            p.start()
+    try:
+        res = sorted(qq.get(timeout=180) for _ in range(world))
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.terminate()
+    assert [r for r, _, _ in res] == list(range(world))
+    for rank, ok, _ in res:
+        assert ok is not True, (rank, ok)
+        want = "injected" if rank == 1 else "another rank"
+        assert want in res[rank][1], res[rank][1][-400:]
 
 
 @pytest.mark.parametrize("world", [4, 8])

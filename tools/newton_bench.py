@@ -209,7 +209,8 @@ out = {"config": f"{a.celltype}-{a.kinem}-{a.n}^3-cantilever", "forcing": a.forc
                          "block-Jacobi PCG"),
        "mesh": "renumbered (input-file order, no lattice)" if a.renumber else "GridGenerator box",
        "mg_levels": mg.describe() if mg else None, "elements": mesh.n_ele,
-       "dofs": mesh.n_rows, "nnz": mesh.nnz, "setup_s": t_setup, "setup_phases": setup_phases, "newton_s": t_newton,
+       "dofs": mesh.n_rows, "nnz": mesh.nnz, "h27_slabs": int(ev.info.h27_slabs),
+       "scratch_bytes": int(ev.info.scratch_bytes), "setup_s": t_setup, "setup_phases": setup_phases, "newton_s": t_newton,
        "newton_iterations": len(h) - 1,
        "assembly_ms_mean": float(np.mean([r["assembly_ms"] for r in h])),
        "assembly_elem_per_s": mesh.n_ele / (1e-3 * float(np.median([r["assembly_ms"] for r in h]))),
