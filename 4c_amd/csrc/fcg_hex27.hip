@@ -58,7 +58,10 @@ constexpr int kNpe = 27;
 constexpr int kNpair = 378;
 constexpr int kBlk = 256;
 constexpr int64_t kRec = kH27RecDoubles;  // 378 blocks x 9 | f 27 x 3 | pad
-constexpr int64_t kIncRec = 9 * kNpe + 3;  // increc: one owned incidence's 3 x 81 block row | f
+constexpr int64_t kIncRec = record_doubles(kNpe);  // increc: one owned incidence's 3 x 81 block row | f | pad
+#ifndef FCG_H27_REC_STORE
+#define FCG_H27_REC_STORE 0
+#endif
 
 __constant__ double c_dN[27 * 27 * 3];  // dN_c,d at Gauss point g: [g][c][d]
 __constant__ double c_w[27];
@@ -803,8 +806,14 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
 #pragma unroll
           for (int i = 0; i < 3; ++i)
 #pragma unroll
-            for (int j = 0; j < 3; ++j)  // streamed (nt): read once, by the row assembly
+            for (int j = 0; j < 3; ++j)
+            {
+#if FCG_H27_REC_STORE == 0  // streamed (nt): read once, by the row assembly
               __builtin_nontemporal_store(up ? v[i + 3 * j] : v[j + 3 * i], dst + 81 * i + j);
+#else  // plain: the pieces of a line meet in L2 before it is written back
+              dst[81 * i + j] = up ? v[i + 3 * j] : v[j + 3 * i];
+#endif
+            }
         }
       }
       else

@@ -14,7 +14,14 @@ namespace fcg {
 
 // Per-incidence scratch record written by the element kernel and consumed by the row-assembly
 // kernel: the element's block-row of node a (3 rows x 3*npe columns, b-major) then f_a (3).
-inline int64_t record_doubles(int npe) { return 9 * int64_t(npe) + 3; }
+// One owned incidence's block row (3 x 3 npe) and its 3 residual entries.  hex27: padded to
+// FCG_REC27 doubles so that records start on 128-byte lines (246 -> 256: one element's record
+// stores complete their lines instead of sharing the first and last line with a record that
+// another workgroup writes at another time).
+#ifndef FCG_REC27
+#define FCG_REC27 246
+#endif
+constexpr int64_t record_doubles(int npe) { return npe == 27 ? int64_t(FCG_REC27) : 9 * int64_t(npe) + 3; }
 
 struct DeviceMesh {
   int celltype = 0, kinem = 0, npe = 8;

@@ -458,7 +458,7 @@ __global__ __launch_bounds__(BLOCK, (NPE == 27 && MAT == 0) ? 3 : 1) void elemen
   constexpr int NGP = NPE;
   constexpr bool SYM = (NPE == 27);             // hex27: compute a<=b and mirror
   constexpr int NPAIR = SYM ? NPE * (NPE + 1) / 2 : NPE * NPE;
-  constexpr int REC = 9 * NPE + 3;
+  constexpr int REC = int(record_doubles(NPE));
   constexpr int ROWLEN = 3 * NPE;
   __shared__ ElementShared<NPE, KIN, MAT> sh;
   const int tid = threadIdx.x;
@@ -1255,7 +1255,7 @@ __global__ __launch_bounds__(64) void assemble27_kernel(AssembleArgs A)
 #ifndef FCG_A27_NB
 #define FCG_A27_NB 2
 #endif
-  constexpr int NPE = 27, REC = 9 * NPE + 3, NB = FCG_A27_NB;
+  constexpr int NPE = 27, REC = int(record_doubles(NPE)), NB = FCG_A27_NB;
   constexpr int NV2 = 2;  // double2 pieces per lane and record: 122 pieces of the 243 entries
   __shared__ double acc[WANT_K ? 3 * 375 : 1];
   const int lane = threadIdx.x;
@@ -1349,7 +1349,7 @@ __global__ __launch_bounds__(64) void assemble27_kernel(AssembleArgs A)
 template <int NPE, bool WANT_K, bool OVERWRITE>
 __global__ __launch_bounds__(64) void assemble_kernel(AssembleArgs A)
 {
-  constexpr int REC = 9 * NPE + 3;
+  constexpr int REC = int(record_doubles(NPE));
   constexpr int ROWLEN = 3 * NPE;
   constexpr int MAXROW = (NPE == 8) ? 81 : 375;
   __shared__ double acc[WANT_K ? 3 * MAXROW : 1];

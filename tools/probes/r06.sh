@@ -28,6 +28,26 @@ for step in "$@"; do
       run 900 bench.log python3 bench.py && grep '^{' $O/bench.log | tail -1 > $O/bench.json ;;
     benchp) # primary line only
       run 300 benchp.log python3 bench.py --only-primary && grep '^{' $O/benchp.log | tail -1 > $O/benchp.json ;;
+    h27ab)  # hex27 40^3 TotLag / linear evaluate, libraries $LIBS alternated over 2 rounds
+      for rep in 1 2; do for v in $LIBS; do for k in totlag linear; do
+        if [ "$v" = default ]; then unset FCG_LIB; else export FCG_LIB=$v; fi
+        r=$(timeout -k 10 150 python3 $ET --celltype hex27 --kinem $k --n 40 --reps 9 | tail -1) || exit 1
+        echo "$v $k $(echo "$r" | python3 -c 'import json,sys; d=json.load(sys.stdin); print(round(d["ms_evaluate"],4), round(d["ms_element"],4), round(d["ms_assemble"],4))')" | tee -a $O/h27ab.txt
+      done; done; done; unset FCG_LIB ;;
+    h27pmc) # hex27 40^3 TotLag counters (mem, occ) of the element and assembly kernels, library $PLIB
+      [ -n "$PLIB" ] && export FCG_LIB=$PLIB
+      run 300 h27pmc.log tools/pmc_kernel.sh r06/h27pmc_${PLIB:-default}_el h27_element_kernel mem,occ -- --n 40 --celltype hex27 --kinem totlag --reps 3
+      run 60 h27pmc.log python3 tools/pmc_summary.py gpurun_out/r06/h27pmc_${PLIB:-default}_el assemble27_kernel
+      unset FCG_LIB ;;
+    tsibis) # TSI two-field tangent (126^3) and 1M hex8 linear of the round-end builds r02..r05 and
+            # HEAD, alternated over 2 rounds on this box (bisect/<r>: each round's own python + lib)
+      for rep in 1 2; do for v in r02 r03 r04 r05 head; do
+        d=bisect/$v; [ $v = head ] && d=.
+        r=$(cd $d && timeout -k 10 200 python3 tools/tsi_bench.py --reps 20 | tail -1) || exit 1
+        echo "$v tsi $r" | tee -a $O/tsibis.txt
+        r=$(cd $d && timeout -k 10 120 python3 tools/eval_timing.py --n 100 --reps 40 | tail -1) || exit 1
+        echo "$v lin $(echo "$r" | python3 -c 'import json,sys; d=json.load(sys.stdin); print(round(d["ms_evaluate"],4))')" | tee -a $O/tsibis.txt
+      done; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
