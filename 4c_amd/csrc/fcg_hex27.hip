@@ -1643,10 +1643,16 @@ hipError_t launch_h27_element(const DeviceMesh& m, const double* d_u_col, bool w
   // so that every workgroup keeps several elements in its two-element pipeline
   const int64_t cap = m.h27_nslab > 1 ? m.h27_el_grid : 256 * 8;
   const dim3 grid(unsigned(n < cap ? n : cap)), block(kBlk);
+  // FCG_H27_DYNLDS=<bytes>: unused dynamic LDS per workgroup (occupancy probes: 20000 leaves one
+  // resident workgroup per CU)
+  static const unsigned dyn = [] {
+    const char* e = std::getenv("FCG_H27_DYNLDS");
+    return e ? unsigned(std::atoi(e)) : 0u;
+  }();
   if (m.kinem == 0)
-    hipLaunchKernelGGL((h27_element_kernel<0, 0>), grid, block, 0, stream, a);
+    hipLaunchKernelGGL((h27_element_kernel<0, 0>), grid, block, dyn, stream, a);
   else
-    hipLaunchKernelGGL((h27_element_kernel<1, 0>), grid, block, 0, stream, a);
+    hipLaunchKernelGGL((h27_element_kernel<1, 0>), grid, block, dyn, stream, a);
   return hipGetLastError();
 }
 

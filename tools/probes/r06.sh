@@ -48,6 +48,16 @@ for step in "$@"; do
         r=$(cd $d && timeout -k 10 120 python3 tools/eval_timing.py --n 100 --reps 40 | tail -1) || exit 1
         echo "$v lin $(echo "$r" | python3 -c 'import json,sys; d=json.load(sys.stdin); print(round(d["ms_evaluate"],4))')" | tee -a $O/tsibis.txt
       done; done ;;
+    h27occ) # hex27 40^3 element kernel at two resident workgroups per CU (default) and at one
+            # (FCG_H27_DYNLDS pads the LDS), alternated over 2 rounds
+      for rep in 1 2; do for v in 0 20000; do for k in totlag linear; do
+        r=$(FCG_H27_DYNLDS=$v timeout -k 10 150 python3 $ET --celltype hex27 --kinem $k --n 40 --reps 9 | tail -1) || exit 1
+        echo "dynlds=$v $k $(echo "$r" | python3 -c 'import json,sys; d=json.load(sys.stdin); print(round(d["ms_evaluate"],4), round(d["ms_element"],4), round(d["ms_assemble"],4))')" | tee -a $O/h27occ.txt
+      done; done; done ;;
+    gpmc)   # HEAD counter sets of the gather kernel (renumbered 1M hex8, PATH_GATHER), TotLag and linear
+      for k in totlag linear; do
+        run 600 gpmc.log tools/pmc_kernel.sh r06/gpmc_$k gather_h8_kernel occ,inst,flop,mem -- --n 100 --renumber --path gather --kinem $k --reps 3
+      done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
