@@ -859,6 +859,72 @@ void build_h27_ring(int64_t n_ele, int64_t S, int lag, const std::vector<int64_t
   }
 }
 
+// hex27 overlapped schedule (DeviceMesh::ovl_*, h27_element_kernel<KIN, 3>): the elements in chunks
+// of C consecutive elements, the chunks in bands of G; a row node can be assembled once every band
+// holding one of its incident elements is complete.  Rows are ordered by their last band (Morton
+// order inside a band, as the slab schedule), cut into row items of R rows, and the queue lists
+// band b's element chunks followed by the row items of band b - lag: a workgroup that claims a row
+// item then rarely finds a band of it still running (the resident workgroups hold about
+// `resident` chunks at a time, so lag ~ resident / G + 1 bands).
+struct H27Overlap {
+  int64_t nchunks = 0, nbands = 0;
+  std::vector<int32_t> queue, ritem, rows;
+};
+
+void build_h27_overlap(int64_t n_ele, int64_t C, int64_t G, int64_t R, int64_t lag,
+    const std::vector<int64_t>& inc_ptr, const std::vector<int32_t>& inc_ele,
+    const std::vector<int64_t>& morton, H27Overlap& O)
+{
+  const int64_t nrn = int64_t(inc_ptr.size()) - 1;
+  O.nchunks = (n_ele + C - 1) / C;
+  O.nbands = (O.nchunks + G - 1) / G;
+  const int64_t B = C * G;  // elements per band
+  std::vector<int32_t> blo(nrn, 0), bhi(nrn, 0);
+  parallel_for(nrn, [&](int64_t r) {
+    int64_t lo = INT64_MAX, hi = 0;
+    for (int64_t k = inc_ptr[r]; k < inc_ptr[r + 1]; ++k)
+    {
+      lo = std::min(lo, int64_t(inc_ele[k]) / B);
+      hi = std::max(hi, int64_t(inc_ele[k]) / B);
+    }
+    blo[r] = int32_t(lo == INT64_MAX ? 0 : lo);
+    bhi[r] = int32_t(hi);
+  });
+  std::vector<int64_t> ptr(O.nbands + 1, 0);
+  for (int64_t r = 0; r < nrn; ++r) ptr[bhi[r] + 1]++;
+  for (int64_t b = 0; b < O.nbands; ++b) ptr[b + 1] += ptr[b];
+  O.rows.assign(nrn, 0);
+  {
+    std::vector<int64_t> fill(ptr.begin(), ptr.end() - 1);
+    for (int64_t i = 0; i < nrn; ++i)
+    {
+      const int64_t r = morton[i];
+      O.rows[fill[bhi[r]]++] = int32_t(r);
+    }
+  }
+  // row items per band
+  std::vector<std::vector<int32_t>> items(O.nbands);  // item indices of band b
+  for (int64_t b = 0; b < O.nbands; ++b)
+    for (int64_t j = ptr[b]; j < ptr[b + 1]; j += R)
+    {
+      const int64_t j1 = std::min(ptr[b + 1], j + R);
+      int32_t lo = int32_t(b);
+      for (int64_t jj = j; jj < j1; ++jj) lo = std::min(lo, blo[O.rows[jj]]);
+      items[b].push_back(int32_t(O.ritem.size() / 4));
+      O.ritem.insert(O.ritem.end(), {int32_t(j), int32_t(j1), lo, int32_t(b)});
+    }
+  O.queue.reserve(size_t(O.nchunks + O.ritem.size() / 4));
+  auto rows_of = [&](int64_t b) {
+    for (const int32_t q : items[b]) O.queue.push_back(~q);
+  };
+  for (int64_t b = 0; b < O.nbands; ++b)
+  {
+    for (int64_t c = b * G; c < std::min(O.nchunks, (b + 1) * G); ++c) O.queue.push_back(int32_t(c));
+    if (b - lag >= 0) rows_of(b - lag);
+  }
+  for (int64_t b = std::max<int64_t>(0, O.nbands - lag); b < O.nbands; ++b) rows_of(b);
+}
+
 void free_mesh(fcg::DeviceMesh& m)
 {
   void* ptrs[] = {m.apply_ye, m.apply_dof, m.gather_dummy, m.multi_ptr, m.rec_row0, m.rec_meta, m.rec_base, m.rec_ele, m.rec_a, m.rec_tmap, m.ele_orig, m.inc_ele, m.inc_a, m.asm_order, m.ele_x,
@@ -866,7 +932,8 @@ void free_mesh(fcg::DeviceMesh& m)
       m.rownode_row0, m.inc_pos, m.rowptr, m.scratch, m.err, m.elem_at, m.lat_x, m.lat_dof,
       m.plane_rec,
       m.tables, m.stamps, m.col_lid, m.diag_pos, m.pcg_work, m.col_ele, m.ele_ft, m.inc_row0, m.ele_gp,
-      m.pen_ptr, m.ele_nb, m.h27_rows, m.h27_rslot0, m.h27_slot};
+      m.pen_ptr, m.ele_nb, m.h27_rows, m.h27_rslot0, m.h27_slot, m.ovl_queue, m.ovl_ritem,
+      m.ovl_rows, m.ovl_rmeta, m.ovl_sync};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (m.err_host) (void)hipHostFree(m.err_host);
@@ -1601,6 +1668,48 @@ int fcg_create(const fcg_desc* d, fcg_ctx** out)
         chk(upload(&m.h27_rslot0, R.rslot0.data(), nrn, bytes));
         chk(upload(&m.h27_slot, R.slot.data(), d->n_ele * 27, bytes));
       }
+      // FCG_H27_OVERLAP=1: the overlapped schedule (element chunks and row items in one launch,
+      // DESIGN §7e) with the full scratch.  Bitwise the same K and f, but slower than the two
+      // launches (40^3 TotLag 3.80 vs 3.45 ms, profiles/r06/r06_h27_overlap_v3_v4_ab.txt), so
+      // not the default.  Knobs for A/B runs: FCG_H27_CHUNK elements per chunk, FCG_H27_BAND
+      // chunks per band, FCG_H27_RITEM rows per row item, FCG_H27_LAG bands
+      const char* ov = std::getenv("FCG_H27_OVERLAP");
+      if (m.h27_increc && m.h27_nslab <= 1 && ov && ov[0] == '1')
+      {
+        auto knob = [](const char* name, int64_t dflt, int64_t lo = 1) {
+          const char* e = std::getenv(name);
+          return e ? std::max<int64_t>(lo, std::atoll(e)) : dflt;
+        };
+        const int64_t C = knob("FCG_H27_CHUNK", 8);
+        const int64_t nch = (d->n_ele + C - 1) / C;
+        const int64_t G = knob("FCG_H27_BAND", std::max<int64_t>(1, nch / 128));
+        const int64_t Rr = knob("FCG_H27_RITEM", 64);
+        const int64_t lag = knob("FCG_H27_LAG", 2 * ((m.h27_el_grid + G - 1) / G) + 1, 0);
+        H27Overlap O;
+        build_h27_overlap(d->n_ele, C, G, Rr, lag, inc_ptr, inc_ele, ord, O);
+        m.h27_ovl = true;
+        m.ovl_chunk = C;
+        m.ovl_nchunks = O.nchunks;
+        m.ovl_nbands = O.nbands;
+        m.ovl_band_chunks = int(G);
+        m.ovl_items = int64_t(O.queue.size());
+        chk(upload(&m.ovl_queue, O.queue.data(), m.ovl_items, bytes));
+        chk(upload(&m.ovl_ritem, O.ritem.data(), int64_t(O.ritem.size()), bytes));
+        chk(upload(&m.ovl_rows, O.rows.data(), nrn, bytes));
+        // per row position: {CSR offset of the node's rows, first row, first incidence,
+        // row length | incidences << 16} -- one load instead of a chain of three
+        std::vector<int64_t> meta(size_t(4) * nrn);
+        parallel_for(nrn, [&](int64_t j) {
+          const int64_t r = O.rows[j];
+          const int64_t base = d->rowptr[row0[r]];
+          meta[4 * j + 0] = base;
+          meta[4 * j + 1] = row0[r];
+          meta[4 * j + 2] = inc_ptr[r];
+          meta[4 * j + 3] = (d->rowptr[row0[r] + 1] - base) | ((inc_ptr[r + 1] - inc_ptr[r]) << 16);
+        });
+        chk(upload(&m.ovl_rmeta, meta.data(), 4 * nrn, bytes));
+        chk(upload<unsigned>(&m.ovl_sync, nullptr, 1 + O.nbands, bytes));
+      }
       chk(upload<double>(&m.scratch, nullptr,
           m.h27_increc ? n_slots * fcg::record_doubles(npe) : d->n_ele * fcg::kH27RecDoubles, bytes));
     }
@@ -1840,6 +1949,13 @@ int fcg_evaluate_device(fcg_ctx* ctx, int action, int mode, const double* d_u_co
     }
     if (T.enabled && he == hipSuccess) he = hipEventRecord(T.ev[1], s);
   }
+  else if (m.h27_ovl)
+  {
+    // hex27 overlapped schedule: elements and rows in one launch
+    if (he == hipSuccess)
+      he = fcg::launch_h27_overlap(m, d_u_col, want_k, mode == FCG_OVERWRITE, d_K_vals, d_fint_row, s);
+    if (T.enabled && he == hipSuccess) he = hipEventRecord(T.ev[1], s);
+  }
   else
   {
     if (he == hipSuccess)
@@ -1856,7 +1972,7 @@ int fcg_evaluate_device(fcg_ctx* ctx, int action, int mode, const double* d_u_co
     he = hipEventRecord(T.ev[2], s);
     T.pending = true;
     T.path = m.path;
-    T.fused = m.path == FCG_PATH_GENERAL && m.h27_nslab > 1;
+    T.fused = m.path == FCG_PATH_GENERAL && (m.h27_nslab > 1 || m.h27_ovl);
   }
   // async: the flags stay sticky on the device across queued evaluates and fcg_check_error reads
   // them once (a read-back per evaluate would put a copy between every two evaluates' kernels)

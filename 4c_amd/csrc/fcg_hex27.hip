@@ -106,13 +106,21 @@ __device__ inline double inv3(double* m)
 // waves 0-2 consume element s - 1 from gpf[(s - 1) & 1] into the K image.  Per-point factors:
 // T | W | V | M | R (offsets below) and fac.
 constexpr int OFF_T = 0, OFF_W = 243, OFF_V = 405, OFF_M = 567, OFF_R = 729, GPF = 972;
+constexpr int kRowImg = 3 * 375;  // one row node's 3 CSR rows (hex27 rows hold <= 375 columns)
 struct H27Shared {
   double dN[27 * 27 * 3];       // [g][c][d], loaded once per workgroup
-  double X[81], U[81];          // the produced element's coordinates and displacements
-  double J[243], Gu[243];       // producer scratch: J, du/dxi per Gauss point
-  double gpf[2][GPF];           // per-point factors of the produced / consumed element
-  double fac[2][27];
-  alignas(16) double kimg[kNpair * 9];  // consumed element's blocks a <= b (col-major 3 x 3)
+  union {
+    struct {
+      double X[81], U[81];          // the produced element's coordinates and displacements
+      double J[243], Gu[243];       // producer scratch: J, du/dxi per Gauss point
+      double gpf[2][GPF];           // per-point factors of the produced / consumed element
+      double fac[2][27];
+      alignas(16) double kimg[kNpair * 9];  // consumed element's blocks a <= b (col-major 3 x 3)
+    };
+    // overlapped schedule (ASM 3): the row images of the four waves' row nodes, used only while
+    // the element pipeline is drained
+    double rowimg[4][kRowImg];
+  };
   double dLn[9];                // 1D Lagrange derivatives at the nodes (nodal det J check)
   int32_t inc[3][27];           // incidence of (e, a), -1 = not owned, by sequence index mod 3
   // pencil output of the consumed element (by sequence parity): CSR offset of row (a, 0), row
@@ -125,6 +133,7 @@ struct H27Shared {
   int bad[2];
   int32_t nodal[27];            // nodal det J check of the produced element: 0 | 1 (<= 0) | 2 (= 0)
   uint8_t loc[27], latnode[27];
+  int32_t qitem[2];             // ASM 3: work items claimed from the queue (look-ahead slots)
   // views of gpf[b]: T(i, k) at 3i + k, W, V, M symmetric (xx yy zz xy yz zx), R(i, k) at 3i + k
   __device__ double* T(int b) { return gpf[b] + OFF_T; }
   __device__ double* W(int b) { return gpf[b] + OFF_W; }
@@ -160,6 +169,19 @@ struct H27Args {
   const int64_t* rowptr;
   double* K;
   double* fint;
+  // overlapped schedule (ASM 3): one work queue of element chunks and row items
+  const int32_t* queue;      // [n_items]: c >= 0 element chunk c, ~q < 0 row item q
+  int64_t n_items;
+  int64_t chunk;             // elements per chunk (the last one may be shorter)
+  int64_t n_chunks;
+  int band_chunks;           // chunks per band (the unit of completion counting)
+  unsigned* sync;            // [0] the claim counter, [1 + b] chunks of band b completed (zeroed)
+  const int32_t* ritem;      // [n_ritems][4]: rows[j0, j1) and the bands [lo, hi] they need
+  const int32_t* rows;       // row nodes by completing band, Morton order inside a band
+  const int64_t* rmeta;      // [rows][4]: CSR offset, first row, first incidence, length | n << 16
+  const int64_t* inc_ptr;    // row node -> its incidences (record slots)
+  const int32_t* rownode_row0;
+  int overwrite;
 };
 
 typedef double f64x4_t __attribute__((ext_vector_type(4)));
@@ -204,16 +226,195 @@ __device__ inline bool first_holder(int cls, uint32_t nb)
 #ifndef FCG_H27P_NV
 #define FCG_H27P_NV 9  // pencil output: entries in flight per lane
 #endif
+#ifndef FCG_H27_OVL_STORE
+// ASM 3 record stores: 0 write-through (sc1), 1 plain + release fence per chunk, 2 nt + release
+#define FCG_H27_OVL_STORE 2
+#endif
+#ifndef FCG_H27_OVL_NB
+#define FCG_H27_OVL_NB 2  // ASM 3 row work: records of a row loaded ahead (the rest when summed)
+#endif
+constexpr int32_t kQEnd = INT32_MIN;  // ASM 3: the queue is exhausted
+
+// ASM 3 record store: the bytes must reach memory before the chunk's completion count does, so
+// that a row node on another XCD (whose L2 is not coherent with this one) reads them
+__device__ inline void ovl_store(double* p, double v)
+{
+#if FCG_H27_OVL_STORE == 0
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_store sc1
+#elif FCG_H27_OVL_STORE == 1
+  *p = v;
+#else
+  __builtin_nontemporal_store(v, p);
+#endif
+}
+
+// ASM 3 row work of one wavefront: rows j, j + 4, ... < j1 of ovl_rows (j, j1 and the wave
+// uniform).  A row node's three CSR rows from its incidence records (assemble27_kernel's summation:
+// incidence order, bitwise the same K and f), the row image in this wave's part of the drained
+// pipeline's LDS (a wavefront's LDS operations complete in order: no barrier between the records'
+// sums and the read-out).  Pipelined two rows deep: the first NB records of the row after next
+// are loaded before this row is summed and written.  Vector-memory instructions complete in issue order, so
+// every load and store here is unconditional (clamped addresses, repeated stores of the same value)
+// and the compiler's wait for this row's records can leave the next row's loads and this row's
+// stores in flight; a row's metadata is one uniform (scalar) load, not a chain of three.
+// Lane l takes the record entries d = 2 v2 + h, v2 = l + 64 s2 (double2 pieces): entry d is row
+// i = d / 81 of the block row, node b = (d % 81) / 3, component j = d % 3 -- fixed per lane.
+__device__ inline void h27_rows(const H27Args& A, int64_t j, int64_t j1, double* acc, int lane_in)
+{
+  // opaque to the optimiser, so that nothing derived from the lane index is hoisted out of the
+  // kernel's loops and held live across the element pipeline
+  int lane = lane_in;
+  __asm__ volatile("" : "+v"(lane));
+  constexpr int NB = FCG_H27_OVL_NB, NV2 = 2;  // NV2 double2 pieces per lane: 122 of the 243 entries
+  constexpr int NOUT = (3 * 375 + 63) / 64;   // stores per lane of the longest row node's rows
+  struct Meta {
+    int64_t base, k0;
+    int32_t row0, rowlen, nk;
+  };
+  struct Recs {
+    double2 val[NB][NV2];
+    uint32_t pos[NB][NV2];  // the column positions of the lane's two entries, 16 bits each
+    double f[NB];
+  };
+  int32_t ent[NV2][2];  // i | b << 2 | j << 7 of the lane's entry (s2, h), -1 = none
+  int v2c[NV2];         // the lane's double2 pieces, clamped into the record
+#pragma unroll
+  for (int s2 = 0; s2 < NV2; ++s2)
+  {
+    v2c[s2] = min(lane + 64 * s2, 121);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+    {
+      const int d = 2 * (lane + 64 * s2) + h;
+      ent[s2][h] = d < 243 ? (d / 81) | (((d % 81) / 3) << 2) | ((d % 3) << 7) : -1;
+    }
+  }
+  auto meta = [&](int64_t jj, Meta& M) {
+    M.nk = 0;
+    M.k0 = 0;
+    M.base = 0;
+    M.row0 = 0;
+    M.rowlen = 1;
+    if (jj >= j1) return;
+    const int64_t* p = A.rmeta + 4 * jj;
+    M.base = p[0];
+    M.row0 = int32_t(p[1]);
+    M.k0 = p[2];
+    M.rowlen = int32_t(p[3] & 0xFFFF);
+    M.nk = int32_t(p[3] >> 16);
+  };
+  // records k0 + q0 + q, q < NB, each address clamped to a valid record (the surplus is not summed)
+  auto load = [&](const Meta& M, int q0, Recs& R) {
+    const int last = max(M.nk - 1, 0);
+#pragma unroll
+    for (int q = 0; q < NB; ++q)
+    {
+      const int64_t k = M.k0 + min(q0 + q, last);
+      const double* src = A.rec + k * kIncRec;
+      const uint16_t* posb = A.inc_pos + k * kNpe;
+      R.f[q] = src[243 + min(lane, 2)];
+#pragma unroll
+      for (int s2 = 0; s2 < NV2; ++s2)
+      {
+        R.val[q][s2] = *reinterpret_cast<const double2*>(src + 2 * v2c[s2]);
+        const uint32_t p0 = posb[ent[s2][0] < 0 ? 0 : (ent[s2][0] >> 2) & 31];
+        const uint32_t p1 = posb[ent[s2][1] < 0 ? 0 : (ent[s2][1] >> 2) & 31];
+        R.pos[q][s2] = p0 | (p1 << 16);
+      }
+    }
+  };
+  auto add = [&](const Meta& M, int q0, const Recs& R, double& f) {
+#pragma unroll
+    for (int q = 0; q < NB; ++q)
+    {
+      if (q0 + q >= M.nk) break;
+      f += R.f[q];
+      if (!A.want_k) continue;
+#pragma unroll
+      for (int s2 = 0; s2 < NV2; ++s2)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+        {
+          const int32_t e = ent[s2][h];
+          if (e < 0) continue;
+          const int dst = (e & 3) * M.rowlen + int((R.pos[q][s2] >> (16 * h)) & 0xFFFFu) + (e >> 7);
+          // one LDS add instruction (ds_add_f64) instead of a read, an add and a write; the
+          // lane's entries are distinct addresses, so the sum is the plain one, bitwise
+          __hip_atomic_fetch_add(acc + dst, h ? R.val[q][s2].y : R.val[q][s2].x, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+  };
+  Meta Mc, Mn, Mnn;
+  Recs Rc, Rn, Rnn;
+  meta(j, Mc);
+  load(Mc, 0, Rc);
+  meta(j + 4, Mn);
+  load(Mn, 0, Rn);
+  for (; Mc.nk > 0; j += 4)
+  {
+    meta(j + 8, Mnn);
+    load(Mnn, 0, Rnn);  // two rows ahead: in flight while this row and the next are done
+    const int n3 = 3 * Mc.rowlen;
+    if (A.want_k)
+#pragma unroll
+      for (int t = 0; t < NOUT; ++t) acc[min(lane + 64 * t, n3 - 1)] = 0.0;
+    double f = 0.0;
+    add(Mc, 0, Rc, f);
+    for (int q0 = NB; q0 < Mc.nk; q0 += NB)  // rows with more than NB incidences
+    {
+      load(Mc, q0, Rc);
+      add(Mc, q0, Rc, f);
+    }
+    if (A.overwrite)
+    {
+      if (A.want_k)
+      {
+        double* out = A.K + Mc.base;  // the node's 3 rows are contiguous (checked at setup)
+#pragma unroll
+        for (int t = 0; t < NOUT; ++t)
+        {
+          const int v = min(lane + 64 * t, n3 - 1);  // lanes past the end repeat the last entry
+          out[v] = acc[v];
+        }
+      }
+      A.fint[Mc.row0 + min(lane, 2)] = f;  // lanes past 2 repeat component 2
+    }
+    else
+    {
+      if (A.want_k)
+      {
+        double* out = A.K + Mc.base;
+        for (int v = lane; v < n3; v += 64) out[v] += acc[v];
+      }
+      if (lane < 3) A.fint[Mc.row0 + lane] += f;
+    }
+    Mc = Mn;
+    Rc = Rn;
+    Mn = Mnn;
+    Rn = Rnn;
+  }
+}
+
 // ASM: 0 = records for the row assembly; 1 = pencil order, add into K; 2 = pencil order, the first
-// holder writes (OVERWRITE)
+// holder writes (OVERWRITE); 3 = the overlapped schedule: records as ASM 0, and the row assembly in
+// the same launch.  ASM 3 workgroups take work items in queue order from one claim counter:
+// element chunks (runs of consecutive elements through the two-element pipeline, each chunk
+// counted complete in its band once its records have reached memory) and row items (a run of row
+// nodes whose incident elements all lie in completed bands, one row node per wave as
+// assemble27_kernel).  A workgroup that meets a row item drains its pipeline first, so it only
+// ever waits for chunks that running workgroups claimed before it: no cycle, no deadlock whatever
+// the number of resident workgroups.  The point: one workgroup's element work (latency-bound,
+// 1.28x slower alone on a CU than beside a second one) overlaps the other's row work (HBM-bound).
 template <int KIN, int ASM>
 __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
 {
+  constexpr bool PEN = ASM == 1 || ASM == 2, OVL = ASM == 3;
   __shared__ H27Shared sh;
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
   for (int v = tid; v < 27 * 27 * 3; v += kBlk) sh.dN[v] = c_dN[v];
-  if (ASM)
+  if (PEN)
     for (int v = tid; v < 27 * 27; v += kBlk)
     {
       const int a = v / 27;
@@ -234,16 +435,50 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
   // the pencils pen_begin + blockIdx.x + k gridDim.x, each walked in x order.  Every thread walks
   // the same sequence.
   int64_t pen = A.pen_begin + blockIdx.x, pos = -1, pend = -1;
+  // ASM 3: the current chunk ends at element ch_end; the next item waits in sh.qitem[qs] (claimed
+  // by thread 0 at least one barrier before it is read); stop = the item that ended the pipeline
+  int64_t ch_end = -1;
+  int qs = 0;
+  int32_t item = kQEnd, stop = kQEnd;
+  auto claim = [&](int slot) {  // thread 0 only
+    const unsigned q = __hip_atomic_fetch_add(&A.sync[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sh.qitem[slot] = int64_t(q) < A.n_items ? A.queue[q] : kQEnd;
+  };
   auto first_element = [&]() -> int64_t {
-    if (!ASM) return A.e_begin + blockIdx.x < A.e_end ? A.e_begin + blockIdx.x : -1;
+    if (OVL)
+    {
+      // item: an element chunk; claim the look-ahead item (read when this chunk runs out)
+      ch_end = min(A.n_ele, (int64_t(item) + 1) * A.chunk);
+      if (tid == 0) claim(qs);
+      __syncthreads();
+      return int64_t(item) * A.chunk;
+    }
+    if (!PEN) return A.e_begin + blockIdx.x < A.e_end ? A.e_begin + blockIdx.x : -1;
     if (pen >= A.pen_end) return -1;
     pos = A.pen_ptr[pen];
     pend = A.pen_ptr[pen + 1];
     return A.col_ele[pos];
   };
+  bool nx_last = false;  // ASM 3: next_element's argument was the last element of its chunk
   auto next_element = [&](int64_t e) -> int64_t {
+    nx_last = false;
     if (e < 0) return -1;
-    if (!ASM) return e + gridDim.x < A.e_end ? e + gridDim.x : -1;
+    if (OVL)
+    {
+      if (e + 1 < ch_end) return e + 1;
+      nx_last = true;
+      const int32_t x = __builtin_amdgcn_readfirstlane(sh.qitem[qs]);
+      qs ^= 1;  // that slot is read: the next claim goes to the other one
+      if (x < 0)
+      {
+        stop = x;  // a row item or the end: the pipeline drains
+        return -1;
+      }
+      ch_end = min(A.n_ele, (int64_t(x) + 1) * A.chunk);
+      if (tid == 0) claim(qs);
+      return int64_t(x) * A.chunk;
+    }
+    if (!PEN) return e + gridDim.x < A.e_end ? e + gridDim.x : -1;
     if (++pos < pend) return A.col_ele[pos];
     pen += gridDim.x;
     if (pen >= A.pen_end) return -1;
@@ -361,7 +596,17 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
         f2 += R[6] * d0 + R[7] * d1 + R[8] * d2;
       }
       const int32_t k = sh.inc[ib][a];
-      if (ASM)
+      if (OVL)
+      {
+        if (k >= 0)
+        {
+          double* o = A.rec + int64_t(k) * kIncRec + 243;
+          ovl_store(o, f0);
+          ovl_store(o + 1, f1);
+          ovl_store(o + 2, f2);
+        }
+      }
+      else if (PEN)
       {
         if (k >= 0)
         {
@@ -411,254 +656,372 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
     st_last = now;                                                                                 \
   }
 
-  // prologue: the first element's X, u, incidences
-  int64_t ep = first_element();  // element produced in this iteration (sequence index s)
-  if (wave == 3)
-  {
-    load_xu(ep);
-    store_xu(0);
-  }
-  int64_t ec = -1;                    // element consumed in this iteration (sequence index s - 1)
-  int64_t epp = next_element(ep);     // element produced in the next iteration
-  for (int s = 0; ec >= 0 || ep >= 0; ++s)
-  {
-    const int pb = s & 1, cb = pb ^ 1;              // factor buffers of ep, ec
-    const int pi = s % 3, ci = (s + 2) % 3, ni = (s + 1) % 3;  // incidence buffers of ep, ec, epp
-    __syncthreads();
-    H27_STAMP(0);
-    const bool cons = ec >= 0 && sh.bad[cb] == 0;
-    if (KIN == 0 && ep >= 0)
+  // ASM 3 row item ~it: wait until every chunk of the bands its rows need has been counted (thread
+  // 0 polls, bounded: a stuck count is reported as FCG_ERR_DEVICE instead of hanging), one agent
+  // acquire for this CU, then the rows, wave w taking rows j0 + w, j0 + w + 4, ...
+  auto ovl_rows = [&](int32_t it) {
+    const int64_t q = ~int64_t(it);
+    const int32_t j0 = A.ritem[4 * q], j1 = A.ritem[4 * q + 1];
+    const int32_t blo = A.ritem[4 * q + 2], bhi = A.ritem[4 * q + 3];
+    // FCG_STAMPS=1: thread 0's cycles polling (stamps[8]) and in its rows (stamps[9]), row items
+    // (stamps[10])
+    const unsigned long long t_in = A.stamps && tid == 0 ? __builtin_amdgcn_s_memtime() : 0ull;
+    if (tid == 0)
     {
-      // linear kinematics: the producer would be the longer side, so stage 1 of ep runs on all
-      // four waves first (wave 3 issues the next element's loads meanwhile)
-      if (wave == 3) load_xu(epp);
-      s1_task(tid);
-      __syncthreads();
+      for (int32_t b = blo; b <= bhi; ++b)
+      {
+        const unsigned target = unsigned(min(int64_t(A.band_chunks), A.n_chunks - int64_t(b) * A.band_chunks));
+        for (int spin = 0; __hip_atomic_load(&A.sync[1 + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++spin)
+        {
+          if (spin == (1 << 22))
+          {
+            atomicMax(&A.err[0], int32_t(FCG_ERR_DEVICE));
+            break;
+          }
+          __builtin_amdgcn_s_sleep(8);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    __syncthreads();
+    const unsigned long long t_go = A.stamps && tid == 0 ? __builtin_amdgcn_s_memtime() : 0ull;
+    const int w = __builtin_amdgcn_readfirstlane(wave);  // uniform: the rows' metadata loads are scalar
+    h27_rows(A, j0 + w, j1, sh.rowimg[w], lane);
+    if (A.stamps && tid == 0)
+    {
+      atomicAdd(&A.stamps[8], t_go - t_in);
+      atomicAdd(&A.stamps[9], __builtin_amdgcn_s_memtime() - t_go);
+      atomicAdd(&A.stamps[10], 1ull);
+    }
+  };
 
+  // ASM 3: the first item
+  if (OVL)
+  {
+    if (tid == 0) claim(0);
+    __syncthreads();
+    item = __builtin_amdgcn_readfirstlane(sh.qitem[0]);
+    qs = 1;
+  }
+  for (;;)  // ASM 3: one pass per run of element chunks between row items; the others: one pass
+  {
+    if (OVL)
+    {
+      // row items until the next element chunk (each claim read after a barrier)
+      while (item != kQEnd && item < 0)
+      {
+        ovl_rows(item);
+        if (tid == 0) claim(qs);
+        __syncthreads();
+        item = __builtin_amdgcn_readfirstlane(sh.qitem[qs]);
+        qs ^= 1;
+      }
+      if (A.stamps) st_last = __builtin_amdgcn_s_memtime();  // row work is not an element phase
+      if (item == kQEnd) break;
+    }
+    // prologue: the first element's X, u, incidences
+    int64_t ep = first_element();  // element produced in this iteration (sequence index s)
     if (wave == 3)
     {
-      // ---------------- producer: element ep
-      if (ep >= 0)
+      load_xu(ep);
+      store_xu(0);
+    }
+    int64_t ec = -1;                    // element consumed in this iteration (sequence index s - 1)
+    int64_t epp = next_element(ep);     // element produced in the next iteration
+    bool ep_last = nx_last, ec_last = false;  // ASM 3: ep / ec end their chunk
+    for (int s = 0; ec >= 0 || ep >= 0; ++s)
+    {
+      const int pb = s & 1, cb = pb ^ 1;              // factor buffers of ep, ec
+      const int pi = s % 3, ci = (s + 2) % 3, ni = (s + 1) % 3;  // incidence buffers of ep, ec, epp
+      __syncthreads();
+      H27_STAMP(0);
+      const bool cons = ec >= 0 && sh.bad[cb] == 0;
+      if (KIN == 0 && ep >= 0)
       {
-        ++st_n;
-        if (KIN == 1) load_xu(epp);  // lands while ep's stages run; stored after stage 1 has read X, u
-        if (lane == 0) sh.bad[pb] = 0;
-        // pencil output bookkeeping of ep (read by all waves when ep is consumed)
-        const uint32_t nb = ASM ? A.ele_nb[ep] : 0u;
-        if (ASM)
+        // linear kinematics: the producer would be the longer side, so stage 1 of ep runs on all
+        // four waves first (wave 3 issues the next element's loads meanwhile)
+        if (wave == 3) load_xu(epp);
+        s1_task(tid);
+        __syncthreads();
+      }
+
+      if (wave == 3)
+      {
+        // ---------------- producer: element ep
+        if (ep >= 0)
         {
-          uint32_t ipos_r[12];
-#pragma unroll
-          for (int q = 0; q < 12; ++q)
+          ++st_n;
+          if (KIN == 1) load_xu(epp);  // lands while ep's stages run; stored after stage 1 has read X, u
+          if (lane == 0) sh.bad[pb] = 0;
+          // pencil output bookkeeping of ep (read by all waves when ep is consumed)
+          const uint32_t nb = PEN ? A.ele_nb[ep] : 0u;
+          if (PEN)
           {
-            const int v = lane + 64 * q;
-            ipos_r[q] = 0u;
-            if (v < kNpe * kNpe)
+            uint32_t ipos_r[12];
+#pragma unroll
+            for (int q = 0; q < 12; ++q)
             {
-              const int a = v / kNpe;
-              const int32_t k = sh.inc[pi][a];
-              if (k >= 0) ipos_r[q] = A.inc_pos[int64_t(k) * kNpe + (v - kNpe * a)];
+              const int v = lane + 64 * q;
+              ipos_r[q] = 0u;
+              if (v < kNpe * kNpe)
+              {
+                const int a = v / kNpe;
+                const int32_t k = sh.inc[pi][a];
+                if (k >= 0) ipos_r[q] = A.inc_pos[int64_t(k) * kNpe + (v - kNpe * a)];
+              }
+            }
+            if (lane < kNpe)
+            {
+              const int32_t k = sh.inc[pi][lane];
+              int64_t rb = 0;
+              int32_t rl = 0;
+              if (k >= 0)
+              {
+                const int32_t r0 = A.inc_row0[k];
+                rb = A.rowptr[r0];
+                rl = int32_t(A.rowptr[r0 + 1] - rb);
+              }
+              sh.rbase[pb][lane] = rb;
+              sh.rlen[pb][lane] = rl;
+            }
+            if (ASM == 2)
+            {
+              const uint64_t m = __ballot(lane < 27 && first_holder(lane, nb));
+              if (lane == 0) sh.fmask[pb] = uint32_t(m);
+            }
+#pragma unroll
+            for (int q = 0; q < 12; ++q)
+            {
+              const int v = lane + 64 * q;
+              if (v < kNpe * kNpe) sh.ipos[pb][v] = uint16_t(ipos_r[q]);
             }
           }
+
+          // 1. (TotLag: here, by this wave; linear: by all four waves before the phase barrier)
+          if (KIN == 1)
+          {
+#pragma unroll 1
+            for (int q = 0; q < 3; ++q) s1_task(lane + 64 * q);
+            wave_lds_sync();
+          }
+          if (lane < kNpe && sh.nodal[lane] != 0) atomicMax(&sh.bad[pb], sh.nodal[lane]);
+          wave_lds_sync();
+
+          // 2. per Gauss point: J^-1, fac, strains, StVK stress and the folded 3 x 3 factors
           if (lane < kNpe)
           {
-            const int32_t k = sh.inc[pi][lane];
-            int64_t rb = 0;
-            int32_t rl = 0;
-            if (k >= 0)
-            {
-              const int32_t r0 = A.inc_row0[k];
-              rb = A.rowptr[r0];
-              rl = int32_t(A.rowptr[r0 + 1] - rb);
-            }
-            sh.rbase[pb][lane] = rb;
-            sh.rlen[pb][lane] = rl;
-          }
-          if (ASM == 2)
-          {
-            const uint64_t m = __ballot(lane < 27 && first_holder(lane, nb));
-            if (lane == 0) sh.fmask[pb] = uint32_t(m);
-          }
+            const int g = lane;
+            double iJ[9];
 #pragma unroll
-          for (int q = 0; q < 12; ++q)
-          {
-            const int v = lane + 64 * q;
-            if (v < kNpe * kNpe) sh.ipos[pb][v] = uint16_t(ipos_r[q]);
+            for (int kk = 0; kk < 9; ++kk) iJ[kk] = sh.J[9 * g + kk];
+            const double det = inv3(iJ);
+            if (det == 0.0) atomicMax(&sh.bad[pb], 2);
+            const double fac = det * c_w[g];
+            sh.fac[pb][g] = fac;
+            // grad u: Hu(i, j) = du_i / dX_j = sum_k J^-1(j, k) du_i / dxi_k
+            double Hu[3][3];
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+              for (int j = 0; j < 3; ++j)
+                Hu[i][j] = iJ[j] * sh.Gu[9 * g + 3 * i] + iJ[j + 3] * sh.Gu[9 * g + 3 * i + 1] +
+                           iJ[j + 6] * sh.Gu[9 * g + 3 * i + 2];
+            double E[6], F[3][3];
+            if (KIN == 0)
+            {
+              // evaluate_linear_gl_strain (calc_lib.hpp:682-695): engineering shear
+              E[0] = Hu[0][0];
+              E[1] = Hu[1][1];
+              E[2] = Hu[2][2];
+              E[3] = Hu[0][1] + Hu[1][0];
+              E[4] = Hu[1][2] + Hu[2][1];
+              E[5] = Hu[0][2] + Hu[2][0];
+#pragma unroll
+              for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) F[i][j] = i == j ? 1.0 : 0.0;
+            }
+            else
+            {
+              // F = I + u N_XYZ^T (hex27, calc_lib.hpp:579-605); F^-1 must exist (calc_lib.hpp:562)
+#pragma unroll
+              for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) F[i][j] = Hu[i][j] + (i == j ? 1.0 : 0.0);
+              double Fi[9];
+#pragma unroll
+              for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) Fi[i + 3 * j] = F[i][j];
+              if (inv3(Fi) == 0.0) atomicMax(&sh.bad[pb], 2);
+              // C = F^T F, E = (C - I) / 2 in strain-like Voigt form (calc_lib.hpp:639-676)
+              double C[3][3];
+#pragma unroll
+              for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) C[i][j] = F[0][i] * F[0][j] + F[1][i] * F[1][j] + F[2][i] * F[2][j];
+              E[0] = 0.5 * (C[0][0] - 1.0);
+              E[1] = 0.5 * (C[1][1] - 1.0);
+              E[2] = 0.5 * (C[2][2] - 1.0);
+              E[3] = C[0][1];
+              E[4] = C[1][2];
+              E[5] = C[0][2];
+            }
+            // S = C E (fill_cmat, 4C_mat_stvenantkirchhoff.cpp:115-145)
+            double S[3][3];
+            S[0][0] = A.cdiag * E[0] + A.lambda * (E[1] + E[2]);
+            S[1][1] = A.cdiag * E[1] + A.lambda * (E[0] + E[2]);
+            S[2][2] = A.cdiag * E[2] + A.lambda * (E[0] + E[1]);
+            S[0][1] = S[1][0] = A.mu * E[3];
+            S[1][2] = S[2][1] = A.mu * E[4];
+            S[0][2] = S[2][0] = A.mu * E[5];
+            // T = F J^-1, R = fac F S J^-1
+            double FS[3][3];
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+              for (int j = 0; j < 3; ++j) FS[i][j] = F[i][0] * S[0][j] + F[i][1] * S[1][j] + F[i][2] * S[2][j];
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+              for (int k = 0; k < 3; ++k)
+              {
+                sh.T(pb)[9 * g + 3 * i + k] = F[i][0] * iJ[3 * k] + F[i][1] * iJ[3 * k + 1] + F[i][2] * iJ[3 * k + 2];
+                sh.R(pb)[9 * g + 3 * i + k] =
+                    fac * (FS[i][0] * iJ[3 * k] + FS[i][1] * iJ[3 * k + 1] + FS[i][2] * iJ[3 * k + 2]);
+              }
+            if (KIN == 1)
+            {
+              // W = fac J^-T J^-1, V = fac J^-T S J^-1, M = F F^T  (xx yy zz xy yz zx)
+              double SJ[3][3];  // S J^-1
+#pragma unroll
+              for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int l = 0; l < 3; ++l) SJ[i][l] = S[i][0] * iJ[3 * l] + S[i][1] * iJ[3 * l + 1] + S[i][2] * iJ[3 * l + 2];
+              const int kk[6] = {0, 1, 2, 0, 1, 0}, ll[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+              for (int x = 0; x < 6; ++x)
+              {
+                const int k = kk[x], l = ll[x];
+                // J^-1(j, k) = iJ[j + 3 k]
+                sh.W(pb)[6 * g + x] = fac * (iJ[3 * k] * iJ[3 * l] + iJ[3 * k + 1] * iJ[3 * l + 1] + iJ[3 * k + 2] * iJ[3 * l + 2]);
+                sh.V(pb)[6 * g + x] = fac * (iJ[3 * k] * SJ[0][l] + iJ[3 * k + 1] * SJ[1][l] + iJ[3 * k + 2] * SJ[2][l]);
+                sh.M(pb)[6 * g + x] = F[k][0] * F[l][0] + F[k][1] * F[l][1] + F[k][2] * F[l][2];
+              }
+            }
           }
-        }
+          wave_lds_sync();
+          store_xu(ni);  // stage 1 has read X, u: the next element's take their place
 
-        // 1. (TotLag: here, by this wave; linear: by all four waves before the phase barrier)
+          emit_f(ep, pb, pi, nb);
+        }
+        H27_STAMP(5);
+      }
+      else if (cons && A.want_k)
+      {
+        // ---------------- consumers (waves 0-2): element ec's node-pair blocks on the matrix cores.
+        // Wave w takes the node ranges (0,0), (0,1), (1,1) of 16; lane (r16, kq) feeds A[r16][kq]
+        // and B[kq][r16] and holds D[kq + 4 r][r16], r = 0..3.  Operands come from the constant
+        // dN_a(xi_g) and the per-point 3 x 3 factors at clamped indices, always loaded and masked by
+        // multiplication (a load under a lane condition turns into a branch with its own wait).
+        const int at = wave == 2 ? 1 : 0, bt = wave == 0 ? 0 : 1;
+        const int r16 = lane & 15, kq = lane >> 4;
+        const int a_l = 16 * at + r16, b_l = 16 * bt + r16;
+        const bool va = a_l < 27, vb = b_l < 27;
+        const int a_c = va ? a_l : 0, b_c = vb ? b_l : 0;
+        const f64x4_t zero4 = {0.0, 0.0, 0.0, 0.0};
+        const int b = 16 * bt + r16;
+
+        // 3. TotLag: mu H + geo I.  Per Gauss point one MFMA over k (K = 3, padded to 4) gives
+        //    c_ab = d_a^T W d_b, and H += c_ab M_g on the lanes; a second MFMA with the same B operand
+        //    accumulates geo_ab += d_a^T V d_b in its C input.  Both go into the K image at once, so
+        //    that stage 4 holds only G.
         if (KIN == 1)
         {
-#pragma unroll 1
-          for (int q = 0; q < 3; ++q) s1_task(lane + 64 * q);
-          wave_lds_sync();
-        }
-        if (lane < kNpe && sh.nodal[lane] != 0) atomicMax(&sh.bad[pb], sh.nodal[lane]);
-        wave_lds_sync();
-
-        // 2. per Gauss point: J^-1, fac, strains, StVK stress and the folded 3 x 3 factors
-        if (lane < kNpe)
-        {
-          const int g = lane;
-          double iJ[9];
+          f64x4_t Hm[6];  // H per component (xx yy zz xy yz zx)
 #pragma unroll
-          for (int kk = 0; kk < 9; ++kk) iJ[kk] = sh.J[9 * g + kk];
-          const double det = inv3(iJ);
-          if (det == 0.0) atomicMax(&sh.bad[pb], 2);
-          const double fac = det * c_w[g];
-          sh.fac[pb][g] = fac;
-          // grad u: Hu(i, j) = du_i / dX_j = sum_k J^-1(j, k) du_i / dxi_k
-          double Hu[3][3];
+          for (int k = 0; k < 6; ++k) Hm[k] = zero4;
+          f64x4_t Geo = zero4;
+          const bool vk = kq < 3;
+          const int kc = vk ? kq : 0;
+          const double ma = (va && vk) ? 1.0 : 0.0, mb = (vb && vk) ? 1.0 : 0.0;
+          const int wr0 = kc == 0 ? 0 : (kc == 1 ? 3 : 5), wr1 = kc == 0 ? 3 : (kc == 1 ? 1 : 4),
+                    wr2 = kc == 0 ? 5 : (kc == 1 ? 4 : 2);  // row kc of the symmetric W, V
+#pragma unroll FCG_H27_HUNROLL
+          for (int g = 0; g < kNpe; ++g)
+          {
+            const double* da = sh.dN + 3 * (27 * g + a_c);
+            const double* Wg = sh.W(cb) + 6 * g;
+            const double* Vg = sh.V(cb) + 6 * g;
+            const double d0 = da[0], d1 = da[1], d2 = da[2];
+            const double av = (Wg[wr0] * d0 + Wg[wr1] * d1 + Wg[wr2] * d2) * ma;
+            const double avv = (Vg[wr0] * d0 + Vg[wr1] * d1 + Vg[wr2] * d2) * ma;
+            const double bv = sh.dN[3 * (27 * g + b_c) + kc] * mb;
+            const f64x4_t c = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, zero4, 0, 0, 0);
+            Geo = __builtin_amdgcn_mfma_f64_16x16x4f64(avv, bv, Geo, 0, 0, 0);
+            const double* Mg = sh.M(cb) + 6 * g;
+#pragma unroll
+            for (int x = 0; x < 6; ++x)
+            {
+              const double m = Mg[x];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) Hm[x][r] += c[r] * m;
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+          {
+            const int a = 16 * at + kq + 4 * r;
+            if (a < 27 && b < 27 && a <= b)
+            {
+              double* K = sh.kimg + 9 * pidx(a, b);
+              const double geo = Geo[r];
+              K[0] = mu * Hm[0][r] + geo;
+              K[4] = mu * Hm[1][r] + geo;
+              K[8] = mu * Hm[2][r] + geo;
+              K[1] = K[3] = mu * Hm[3][r];
+              K[5] = K[7] = mu * Hm[4][r];
+              K[2] = K[6] = mu * Hm[5][r];
+            }
+          }
+        }
+        H27_STAMP(1);
+
+        // 4. G_ij = sum_g fac q_a,i q_b,j (7 steps of 4 Gauss points; q_a = T_g d_a on the fly)
+        f64x4_t X[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) X[k] = zero4;
+#pragma unroll
+        for (int st = 0; st < 7; ++st)
+        {
+          const int g = 4 * st + kq;
+          const bool vg = g < 27;
+          const int gc = vg ? g : 0;
+          const double fg = sh.fac[cb][gc] * ((vg && va) ? 1.0 : 0.0);
+          const double mb = (vg && vb) ? 1.0 : 0.0;
+          const double* T = sh.T(cb) + 9 * gc;
+          const double* da = sh.dN + 3 * (27 * gc + a_c);
+          const double* db = sh.dN + 3 * (27 * gc + b_c);
+          const double a0 = da[0], a1 = da[1], a2 = da[2], b0 = db[0], b1 = db[1], b2 = db[2];
+          double av[3], bv[3];
+#pragma unroll
+          for (int i = 0; i < 3; ++i)
+          {
+            const double t0 = T[3 * i], t1 = T[3 * i + 1], t2 = T[3 * i + 2];
+            av[i] = fg * (t0 * a0 + t1 * a1 + t2 * a2);
+            bv[i] = mb * (t0 * b0 + t1 * b1 + t2 * b2);
+          }
 #pragma unroll
           for (int i = 0; i < 3; ++i)
 #pragma unroll
             for (int j = 0; j < 3; ++j)
-              Hu[i][j] = iJ[j] * sh.Gu[9 * g + 3 * i] + iJ[j + 3] * sh.Gu[9 * g + 3 * i + 1] +
-                         iJ[j + 6] * sh.Gu[9 * g + 3 * i + 2];
-          double E[6], F[3][3];
-          if (KIN == 0)
-          {
-            // evaluate_linear_gl_strain (calc_lib.hpp:682-695): engineering shear
-            E[0] = Hu[0][0];
-            E[1] = Hu[1][1];
-            E[2] = Hu[2][2];
-            E[3] = Hu[0][1] + Hu[1][0];
-            E[4] = Hu[1][2] + Hu[2][1];
-            E[5] = Hu[0][2] + Hu[2][0];
-#pragma unroll
-            for (int i = 0; i < 3; ++i)
-#pragma unroll
-              for (int j = 0; j < 3; ++j) F[i][j] = i == j ? 1.0 : 0.0;
-          }
-          else
-          {
-            // F = I + u N_XYZ^T (hex27, calc_lib.hpp:579-605); F^-1 must exist (calc_lib.hpp:562)
-#pragma unroll
-            for (int i = 0; i < 3; ++i)
-#pragma unroll
-              for (int j = 0; j < 3; ++j) F[i][j] = Hu[i][j] + (i == j ? 1.0 : 0.0);
-            double Fi[9];
-#pragma unroll
-            for (int i = 0; i < 3; ++i)
-#pragma unroll
-              for (int j = 0; j < 3; ++j) Fi[i + 3 * j] = F[i][j];
-            if (inv3(Fi) == 0.0) atomicMax(&sh.bad[pb], 2);
-            // C = F^T F, E = (C - I) / 2 in strain-like Voigt form (calc_lib.hpp:639-676)
-            double C[3][3];
-#pragma unroll
-            for (int i = 0; i < 3; ++i)
-#pragma unroll
-              for (int j = 0; j < 3; ++j) C[i][j] = F[0][i] * F[0][j] + F[1][i] * F[1][j] + F[2][i] * F[2][j];
-            E[0] = 0.5 * (C[0][0] - 1.0);
-            E[1] = 0.5 * (C[1][1] - 1.0);
-            E[2] = 0.5 * (C[2][2] - 1.0);
-            E[3] = C[0][1];
-            E[4] = C[1][2];
-            E[5] = C[0][2];
-          }
-          // S = C E (fill_cmat, 4C_mat_stvenantkirchhoff.cpp:115-145)
-          double S[3][3];
-          S[0][0] = A.cdiag * E[0] + A.lambda * (E[1] + E[2]);
-          S[1][1] = A.cdiag * E[1] + A.lambda * (E[0] + E[2]);
-          S[2][2] = A.cdiag * E[2] + A.lambda * (E[0] + E[1]);
-          S[0][1] = S[1][0] = A.mu * E[3];
-          S[1][2] = S[2][1] = A.mu * E[4];
-          S[0][2] = S[2][0] = A.mu * E[5];
-          // T = F J^-1, R = fac F S J^-1
-          double FS[3][3];
-#pragma unroll
-          for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int j = 0; j < 3; ++j) FS[i][j] = F[i][0] * S[0][j] + F[i][1] * S[1][j] + F[i][2] * S[2][j];
-#pragma unroll
-          for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int k = 0; k < 3; ++k)
-            {
-              sh.T(pb)[9 * g + 3 * i + k] = F[i][0] * iJ[3 * k] + F[i][1] * iJ[3 * k + 1] + F[i][2] * iJ[3 * k + 2];
-              sh.R(pb)[9 * g + 3 * i + k] =
-                  fac * (FS[i][0] * iJ[3 * k] + FS[i][1] * iJ[3 * k + 1] + FS[i][2] * iJ[3 * k + 2]);
-            }
-          if (KIN == 1)
-          {
-            // W = fac J^-T J^-1, V = fac J^-T S J^-1, M = F F^T  (xx yy zz xy yz zx)
-            double SJ[3][3];  // S J^-1
-#pragma unroll
-            for (int i = 0; i < 3; ++i)
-#pragma unroll
-              for (int l = 0; l < 3; ++l) SJ[i][l] = S[i][0] * iJ[3 * l] + S[i][1] * iJ[3 * l + 1] + S[i][2] * iJ[3 * l + 2];
-            const int kk[6] = {0, 1, 2, 0, 1, 0}, ll[6] = {0, 1, 2, 1, 2, 2};
-#pragma unroll
-            for (int x = 0; x < 6; ++x)
-            {
-              const int k = kk[x], l = ll[x];
-              // J^-1(j, k) = iJ[j + 3 k]
-              sh.W(pb)[6 * g + x] = fac * (iJ[3 * k] * iJ[3 * l] + iJ[3 * k + 1] * iJ[3 * l + 1] + iJ[3 * k + 2] * iJ[3 * l + 2]);
-              sh.V(pb)[6 * g + x] = fac * (iJ[3 * k] * SJ[0][l] + iJ[3 * k + 1] * SJ[1][l] + iJ[3 * k + 2] * SJ[2][l]);
-              sh.M(pb)[6 * g + x] = F[k][0] * F[l][0] + F[k][1] * F[l][1] + F[k][2] * F[l][2];
-            }
-          }
+              X[3 * i + j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[j], X[3 * i + j], 0, 0, 0);
         }
-        wave_lds_sync();
-        store_xu(ni);  // stage 1 has read X, u: the next element's take their place
+        H27_STAMP(2);
 
-        emit_f(ep, pb, pi, nb);
-      }
-      H27_STAMP(5);
-    }
-    else if (cons && A.want_k)
-    {
-      // ---------------- consumers (waves 0-2): element ec's node-pair blocks on the matrix cores.
-      // Wave w takes the node ranges (0,0), (0,1), (1,1) of 16; lane (r16, kq) feeds A[r16][kq]
-      // and B[kq][r16] and holds D[kq + 4 r][r16], r = 0..3.  Operands come from the constant
-      // dN_a(xi_g) and the per-point 3 x 3 factors at clamped indices, always loaded and masked by
-      // multiplication (a load under a lane condition turns into a branch with its own wait).
-      const int at = wave == 2 ? 1 : 0, bt = wave == 0 ? 0 : 1;
-      const int r16 = lane & 15, kq = lane >> 4;
-      const int a_l = 16 * at + r16, b_l = 16 * bt + r16;
-      const bool va = a_l < 27, vb = b_l < 27;
-      const int a_c = va ? a_l : 0, b_c = vb ? b_l : 0;
-      const f64x4_t zero4 = {0.0, 0.0, 0.0, 0.0};
-      const int b = 16 * bt + r16;
-
-      // 3. TotLag: mu H + geo I.  Per Gauss point one MFMA over k (K = 3, padded to 4) gives
-      //    c_ab = d_a^T W d_b, and H += c_ab M_g on the lanes; a second MFMA with the same B operand
-      //    accumulates geo_ab += d_a^T V d_b in its C input.  Both go into the K image at once, so
-      //    that stage 4 holds only G.
-      if (KIN == 1)
-      {
-        f64x4_t Hm[6];  // H per component (xx yy zz xy yz zx)
-#pragma unroll
-        for (int k = 0; k < 6; ++k) Hm[k] = zero4;
-        f64x4_t Geo = zero4;
-        const bool vk = kq < 3;
-        const int kc = vk ? kq : 0;
-        const double ma = (va && vk) ? 1.0 : 0.0, mb = (vb && vk) ? 1.0 : 0.0;
-        const int wr0 = kc == 0 ? 0 : (kc == 1 ? 3 : 5), wr1 = kc == 0 ? 3 : (kc == 1 ? 1 : 4),
-                  wr2 = kc == 0 ? 5 : (kc == 1 ? 4 : 2);  // row kc of the symmetric W, V
-#pragma unroll FCG_H27_HUNROLL
-        for (int g = 0; g < kNpe; ++g)
-        {
-          const double* da = sh.dN + 3 * (27 * g + a_c);
-          const double* Wg = sh.W(cb) + 6 * g;
-          const double* Vg = sh.V(cb) + 6 * g;
-          const double d0 = da[0], d1 = da[1], d2 = da[2];
-          const double av = (Wg[wr0] * d0 + Wg[wr1] * d1 + Wg[wr2] * d2) * ma;
-          const double avv = (Vg[wr0] * d0 + Vg[wr1] * d1 + Vg[wr2] * d2) * ma;
-          const double bv = sh.dN[3 * (27 * g + b_c) + kc] * mb;
-          const f64x4_t c = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, zero4, 0, 0, 0);
-          Geo = __builtin_amdgcn_mfma_f64_16x16x4f64(avv, bv, Geo, 0, 0, 0);
-          const double* Mg = sh.M(cb) + 6 * g;
-#pragma unroll
-          for (int x = 0; x < 6; ++x)
-          {
-            const double m = Mg[x];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) Hm[x][r] += c[r] * m;
-          }
-        }
+        // 5. K_ab = lambda G + mu G^T + (mu tr G I | mu H + geo I) into the LDS image, which leaves
+        //    as contiguous pieces: one store instruction covers 1 KB instead of 64 scattered entries
 #pragma unroll
         for (int r = 0; r < 4; ++r)
         {
@@ -666,167 +1029,138 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
           if (a < 27 && b < 27 && a <= b)
           {
             double* K = sh.kimg + 9 * pidx(a, b);
-            const double geo = Geo[r];
-            K[0] = mu * Hm[0][r] + geo;
-            K[4] = mu * Hm[1][r] + geo;
-            K[8] = mu * Hm[2][r] + geo;
-            K[1] = K[3] = mu * Hm[3][r];
-            K[5] = K[7] = mu * Hm[4][r];
-            K[2] = K[6] = mu * Hm[5][r];
-          }
-        }
-      }
-      H27_STAMP(1);
-
-      // 4. G_ij = sum_g fac q_a,i q_b,j (7 steps of 4 Gauss points; q_a = T_g d_a on the fly)
-      f64x4_t X[9];
-#pragma unroll
-      for (int k = 0; k < 9; ++k) X[k] = zero4;
-#pragma unroll
-      for (int st = 0; st < 7; ++st)
-      {
-        const int g = 4 * st + kq;
-        const bool vg = g < 27;
-        const int gc = vg ? g : 0;
-        const double fg = sh.fac[cb][gc] * ((vg && va) ? 1.0 : 0.0);
-        const double mb = (vg && vb) ? 1.0 : 0.0;
-        const double* T = sh.T(cb) + 9 * gc;
-        const double* da = sh.dN + 3 * (27 * gc + a_c);
-        const double* db = sh.dN + 3 * (27 * gc + b_c);
-        const double a0 = da[0], a1 = da[1], a2 = da[2], b0 = db[0], b1 = db[1], b2 = db[2];
-        double av[3], bv[3];
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-        {
-          const double t0 = T[3 * i], t1 = T[3 * i + 1], t2 = T[3 * i + 2];
-          av[i] = fg * (t0 * a0 + t1 * a1 + t2 * a2);
-          bv[i] = mb * (t0 * b0 + t1 * b1 + t2 * b2);
-        }
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-          for (int j = 0; j < 3; ++j)
-            X[3 * i + j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[j], X[3 * i + j], 0, 0, 0);
-      }
-      H27_STAMP(2);
-
-      // 5. K_ab = lambda G + mu G^T + (mu tr G I | mu H + geo I) into the LDS image, which leaves
-      //    as contiguous pieces: one store instruction covers 1 KB instead of 64 scattered entries
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-      {
-        const int a = 16 * at + kq + 4 * r;
-        if (a < 27 && b < 27 && a <= b)
-        {
-          double* K = sh.kimg + 9 * pidx(a, b);
-          double add[9];
-          if (KIN == 0)
-          {
-            const double tr = mu * (X[0][r] + X[4][r] + X[8][r]);
-#pragma unroll
-            for (int k = 0; k < 9; ++k) add[k] = (k == 0 || k == 4 || k == 8) ? tr : 0.0;
-          }
-          else
-          {
-#pragma unroll
-            for (int k = 0; k < 9; ++k) add[k] = K[k];  // mu H + geo I from stage 3
-          }
-#pragma unroll
-          for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int j = 0; j < 3; ++j)
-              K[i + 3 * j] = lam * X[3 * i + j][r] + mu * X[3 * j + i][r] + add[i + 3 * j];
-        }
-      }
-      H27_STAMP(3);
-    }
-    __syncthreads();
-
-    // 6. element ec's record(s) or rows, by all waves
-    if (ec >= 0 && sh.bad[cb] != 0)
-    {
-      if (tid == 0)
-      {
-        atomicMax(&A.err[0], sh.bad[cb]);
-        atomicMin(&A.err[1], int32_t(ec));
-      }
-    }
-    else if (cons && A.want_k)
-    {
-      if (ASM)
-      {
-        // straight into the owned rows: entry v = (a, i, c) of a's 3 rows over the 81 columns in
-        // lattice order (c / 3 = lattice node, so lanes v, v + 1 hit contiguous CSR columns in runs
-        // of 3 nodes); every load of a batch is issued before its stores.  The pencil's previous
-        // element wrote its shared rows in the previous iteration, from this workgroup.
-        constexpr int NV = FCG_H27P_NV;
-        const uint32_t fmask = sh.fmask[cb];
-        for (int v0 = 0; v0 < kNpe * 243; v0 += NV * kBlk)
-        {
-          int64_t addr[NV];
-          double val[NV];
-#pragma unroll
-          for (int k = 0; k < NV; ++k)
-          {
-            const int v = v0 + tid + kBlk * k;
-            addr[k] = -1;
-            val[k] = 0.0;
-            if (v >= kNpe * 243) continue;
-            const int a = v / 243;
-            if (sh.inc[ci][a] < 0) continue;
-            const int r = v - 243 * a;
-            const int i = r / 81, c = r - 81 * (r / 81);
-            const int b = sh.latnode[c / 3], j = c - 3 * (c / 3);
-            addr[k] = sh.rbase[cb][a] + int64_t(i * sh.rlen[cb][a] + sh.ipos[cb][kNpe * a + b] + j);
-            const bool up = a <= b;
-            val[k] = sh.kimg[9 * (up ? pidx(a, b) : pidx(b, a)) + (up ? i + 3 * j : j + 3 * i)];
-            if (ASM == 1 || !((fmask >> sh.pcls[kNpe * a + b]) & 1u)) val[k] += A.K[addr[k]];
-          }
-#pragma unroll
-          for (int k = 0; k < NV; ++k)
-            if (addr[k] >= 0) A.K[addr[k]] = val[k];
-        }
-      }
-      else if (A.increc)
-      {
-        // the owned incidences' block rows K_ab, b = 0..26 (K_ba^T for b < a), row-major 3 x 81:
-        // the record of the general path's assemble27_kernel.  One (a, b) block per lane: its 9
-        // entries from the image, then 3 pieces of 3 into the rows (lanes b, b + 1 contiguous)
-        for (int p = tid; p < kNpe * kNpe; p += kBlk)
-        {
-          const int a = p / kNpe, b = p - kNpe * a;
-          const int32_t k = sh.inc[ci][a];
-          if (k < 0) continue;
-          const bool up = a <= b;
-          const double* src = sh.kimg + 9 * (up ? pidx(a, b) : pidx(b, a));
-          double v[9];
-#pragma unroll
-          for (int q = 0; q < 9; ++q) v[q] = src[q];  // col-major K_(min,max)
-          double* dst = A.rec + int64_t(k) * kIncRec + 3 * b;
-#pragma unroll
-          for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int j = 0; j < 3; ++j)
+            double add[9];
+            if (KIN == 0)
             {
-#if FCG_H27_REC_STORE == 0  // streamed (nt): read once, by the row assembly
-              __builtin_nontemporal_store(up ? v[i + 3 * j] : v[j + 3 * i], dst + 81 * i + j);
-#else  // plain: the pieces of a line meet in L2 before it is written back
-              dst[81 * i + j] = up ? v[i + 3 * j] : v[j + 3 * i];
-#endif
+              const double tr = mu * (X[0][r] + X[4][r] + X[8][r]);
+#pragma unroll
+              for (int k = 0; k < 9; ++k) add[k] = (k == 0 || k == 4 || k == 8) ? tr : 0.0;
             }
+            else
+            {
+#pragma unroll
+              for (int k = 0; k < 9; ++k) add[k] = K[k];  // mu H + geo I from stage 3
+            }
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+              for (int j = 0; j < 3; ++j)
+                K[i + 3 * j] = lam * X[3 * i + j][r] + mu * X[3 * j + i][r] + add[i + 3 * j];
+          }
+        }
+        H27_STAMP(3);
+      }
+      __syncthreads();
+
+      // 6. element ec's record(s) or rows, by all waves
+      if (ec >= 0 && sh.bad[cb] != 0)
+      {
+        if (tid == 0)
+        {
+          atomicMax(&A.err[0], sh.bad[cb]);
+          atomicMin(&A.err[1], int32_t(ec));
         }
       }
-      else
+      else if (cons && A.want_k)
       {
-        const double2* src = reinterpret_cast<const double2*>(sh.kimg);
-        double2* dst = reinterpret_cast<double2*>(A.rec + ec * kRec);  // 16-byte aligned (kRec even)
-        for (int v = tid; v < kNpair * 9 / 2; v += kBlk) dst[v] = src[v];
+        if (PEN)
+        {
+          // straight into the owned rows: entry v = (a, i, c) of a's 3 rows over the 81 columns in
+          // lattice order (c / 3 = lattice node, so lanes v, v + 1 hit contiguous CSR columns in runs
+          // of 3 nodes); every load of a batch is issued before its stores.  The pencil's previous
+          // element wrote its shared rows in the previous iteration, from this workgroup.
+          constexpr int NV = FCG_H27P_NV;
+          const uint32_t fmask = sh.fmask[cb];
+          for (int v0 = 0; v0 < kNpe * 243; v0 += NV * kBlk)
+          {
+            int64_t addr[NV];
+            double val[NV];
+#pragma unroll
+            for (int k = 0; k < NV; ++k)
+            {
+              const int v = v0 + tid + kBlk * k;
+              addr[k] = -1;
+              val[k] = 0.0;
+              if (v >= kNpe * 243) continue;
+              const int a = v / 243;
+              if (sh.inc[ci][a] < 0) continue;
+              const int r = v - 243 * a;
+              const int i = r / 81, c = r - 81 * (r / 81);
+              const int b = sh.latnode[c / 3], j = c - 3 * (c / 3);
+              addr[k] = sh.rbase[cb][a] + int64_t(i * sh.rlen[cb][a] + sh.ipos[cb][kNpe * a + b] + j);
+              const bool up = a <= b;
+              val[k] = sh.kimg[9 * (up ? pidx(a, b) : pidx(b, a)) + (up ? i + 3 * j : j + 3 * i)];
+              if (ASM == 1 || !((fmask >> sh.pcls[kNpe * a + b]) & 1u)) val[k] += A.K[addr[k]];
+            }
+#pragma unroll
+            for (int k = 0; k < NV; ++k)
+              if (addr[k] >= 0) A.K[addr[k]] = val[k];
+          }
+        }
+        else if (A.increc)
+        {
+          // the owned incidences' block rows K_ab, b = 0..26 (K_ba^T for b < a), row-major 3 x 81:
+          // the record of the general path's assemble27_kernel.  One (a, b) block per lane: its 9
+          // entries from the image, then 3 pieces of 3 into the rows (lanes b, b + 1 contiguous)
+          for (int p = tid; p < kNpe * kNpe; p += kBlk)
+          {
+            const int a = p / kNpe, b = p - kNpe * a;
+            const int32_t k = sh.inc[ci][a];
+            if (k < 0) continue;
+            const bool up = a <= b;
+            const double* src = sh.kimg + 9 * (up ? pidx(a, b) : pidx(b, a));
+            double v[9];
+#pragma unroll
+            for (int q = 0; q < 9; ++q) v[q] = src[q];  // col-major K_(min,max)
+            double* dst = A.rec + int64_t(k) * kIncRec + 3 * b;
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+              for (int j = 0; j < 3; ++j)
+              {
+                if (OVL)
+                  ovl_store(dst + 81 * i + j, up ? v[i + 3 * j] : v[j + 3 * i]);
+                else
+#if FCG_H27_REC_STORE == 0  // streamed (nt): read once, by the row assembly
+                  __builtin_nontemporal_store(up ? v[i + 3 * j] : v[j + 3 * i], dst + 81 * i + j);
+#else  // plain: the pieces of a line meet in L2 before it is written back
+                  dst[81 * i + j] = up ? v[i + 3 * j] : v[j + 3 * i];
+#endif
+              }
+          }
+        }
+        else
+        {
+          const double2* src = reinterpret_cast<const double2*>(sh.kimg);
+          double2* dst = reinterpret_cast<double2*>(A.rec + ec * kRec);  // 16-byte aligned (kRec even)
+          for (int v = tid; v < kNpair * 9 / 2; v += kBlk) dst[v] = src[v];
+        }
       }
+      // ASM 3: ec ended its chunk -- once every wave's record stores (and the producer's f stores,
+      // issued an iteration earlier) have reached memory, the chunk counts in its band
+      if (OVL && ec >= 0 && ec_last)
+      {
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0)
+        {
+#if FCG_H27_OVL_STORE != 0
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+          const int64_t band = ec / A.chunk / A.band_chunks;
+          __hip_atomic_fetch_add(&A.sync[1 + band], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      H27_STAMP(4);
+      ec = ep;
+      ec_last = ep_last;
+      ep = epp;
+      epp = next_element(epp);
+      ep_last = nx_last;
     }
-    H27_STAMP(4);
-    ec = ep;
-    ep = epp;
-    epp = next_element(epp);
+    if (!OVL) break;
+    item = stop;  // a row item or the end
   }
   if (A.stamps && (tid == 0 || tid == 192))
   {
@@ -1653,6 +1987,55 @@ hipError_t launch_h27_element(const DeviceMesh& m, const double* d_u_col, bool w
     hipLaunchKernelGGL((h27_element_kernel<0, 0>), grid, block, dyn, stream, a);
   else
     hipLaunchKernelGGL((h27_element_kernel<1, 0>), grid, block, dyn, stream, a);
+  return hipGetLastError();
+}
+
+// hex27 overlapped schedule (DeviceMesh::ovl_*): element chunks and row items of one queue in one
+// launch of the resident workgroups; the claim counter and the band counts are zeroed first
+hipError_t launch_h27_overlap(const DeviceMesh& m, const double* d_u_col, bool want_k,
+    bool overwrite, double* d_K, double* d_fint, hipStream_t stream)
+{
+  if (m.n_ele == 0 && m.n_rownodes == 0) return hipSuccess;
+  hipError_t he = hipMemsetAsync(m.ovl_sync, 0, sizeof(unsigned) * size_t(1 + m.ovl_nbands), stream);
+  if (he != hipSuccess) return he;
+  H27Args a{};
+  a.n_ele = m.n_ele;
+  a.e_begin = 0;
+  a.e_end = m.n_ele;
+  a.ele_nodes = m.ele_nodes;
+  a.node_x = m.node_x;
+  a.node_dof_col = m.node_dof_col;
+  a.u_col = d_u_col;
+  a.rec = m.scratch;
+  a.inc_of = m.inc_of;
+  a.increc = 1;
+  a.err = m.err;
+  a.lambda = m.lambda;
+  a.mu = m.mu;
+  a.cdiag = m.cdiag;
+  a.want_k = want_k ? 1 : 0;
+  a.stamps = m.stamps;
+  a.inc_pos = m.inc_pos;
+  a.rowptr = m.rowptr;
+  a.K = d_K;
+  a.fint = d_fint;
+  a.queue = m.ovl_queue;
+  a.n_items = m.ovl_items;
+  a.chunk = m.ovl_chunk;
+  a.n_chunks = m.ovl_nchunks;
+  a.band_chunks = m.ovl_band_chunks;
+  a.sync = m.ovl_sync;
+  a.ritem = m.ovl_ritem;
+  a.rows = m.ovl_rows;
+  a.rmeta = m.ovl_rmeta;
+  a.inc_ptr = m.inc_ptr;
+  a.rownode_row0 = m.rownode_row0;
+  a.overwrite = overwrite ? 1 : 0;
+  const dim3 grid(unsigned(std::max(1, m.h27_el_grid))), block(kBlk);
+  if (m.kinem == 0)
+    hipLaunchKernelGGL((h27_element_kernel<0, 3>), grid, block, 0, stream, a);
+  else
+    hipLaunchKernelGGL((h27_element_kernel<1, 3>), grid, block, 0, stream, a);
   return hipGetLastError();
 }
 

@@ -15,11 +15,12 @@ namespace fcg {
 // Per-incidence scratch record written by the element kernel and consumed by the row-assembly
 // kernel: the element's block-row of node a (3 rows x 3*npe columns, b-major) then f_a (3).
 // One owned incidence's block row (3 x 3 npe) and its 3 residual entries.  hex27: padded to
-// FCG_REC27 doubles so that records start on 128-byte lines (246 -> 256: one element's record
-// stores complete their lines instead of sharing the first and last line with a record that
-// another workgroup writes at another time).
+// FCG_REC27 = 256 doubles so that records start on 128-byte lines: no line is shared by two
+// records, which the overlapped schedule needs (a row node on another XCD reads its records
+// while a neighbouring record's element may not have run yet; a shared line could then sit stale
+// in that XCD's L2).  Unpadded (246) measured the same (profiles/r06/r06_h27_record_store_ab.txt).
 #ifndef FCG_REC27
-#define FCG_REC27 246
+#define FCG_REC27 256
 #endif
 constexpr int64_t record_doubles(int npe) { return npe == 27 ? int64_t(FCG_REC27) : 9 * int64_t(npe) + 3; }
 
@@ -96,6 +97,19 @@ struct DeviceMesh {
   int32_t* h27_rows = nullptr;       // [n_rownodes] row nodes by completing slab, then Morton order
   int32_t* h27_rslot0 = nullptr;     // [n_rownodes] ring slot of the row node's first record
   int32_t* h27_slot = nullptr;       // [n_ele][27] ring slot of incidence (e, a), -1 = not owned
+  // hex27 overlapped schedule (FCG_H27_OVERLAP=1 with the full scratch; measured slower than the
+  // element launch + row-assembly launch): one queue of element chunks (ovl_chunk
+  // consecutive elements) and row items (runs of row nodes whose incident elements all lie in
+  // completed bands of ovl_band_chunks chunks)
+  bool h27_ovl = false;
+  int64_t ovl_items = 0, ovl_chunk = 0, ovl_nchunks = 0, ovl_nbands = 0;
+  int ovl_band_chunks = 1;
+  int32_t* ovl_queue = nullptr;     // [ovl_items] chunk c >= 0 | ~row item
+  int32_t* ovl_ritem = nullptr;     // [row items][4] rows [j0, j1) of ovl_rows, bands [lo, hi]
+  int32_t* ovl_rows = nullptr;      // [n_rownodes] by completing band, then Morton order
+  int64_t* ovl_rmeta = nullptr;     // [n_rownodes][4] of ovl_rows[j]: CSR offset, first row,
+                                    // first incidence, row length | incidences << 16
+  unsigned* ovl_sync = nullptr;     // [1 + ovl_nbands] claim counter, completed chunks per band
 
   // structured (row-block sweep) plan, hex8 only
   int path = FCG_PATH_GENERAL;
@@ -186,6 +200,9 @@ hipError_t launch_assemble27_slab(const DeviceMesh& m, int64_t s, bool want_k, b
     double* d_K, double* d_fint, hipStream_t stream);
 hipError_t launch_h27_assemble(const DeviceMesh& m, bool want_k, bool overwrite, double* d_K,
     double* d_fint, hipStream_t stream);
+// hex27 overlapped schedule: element chunks and row items of one queue in one launch
+hipError_t launch_h27_overlap(const DeviceMesh& m, const double* d_u_col, bool want_k,
+    bool overwrite, double* d_K, double* d_fint, hipStream_t stream);
 // hex27 StVK on a verified lattice: the same element kernel adding its blocks straight into the
 // CSR rows, four colour launches of pencils (runs of elements along x, one workgroup each)
 hipError_t launch_h27_pencil(const DeviceMesh& m, const double* d_u_col, bool want_k,

@@ -33,5 +33,12 @@ for kin in (fcg.LINEAR, fcg.TOTLAG):
             line += " cycles/element: " + " ".join(
                 f"{nm}={d[i] / ne:.0f}({100 * d[i] / tot:.0f}%)" for i, nm in enumerate(names[:5]))
             line += f" | {names[5]}={d[5] / ne:.0f}"
+            if len(d) > 10 and d[10]:
+                # overlapped schedule: thread 0's polling and row cycles per row item, and per
+                # workgroup against its element cycles (all evaluates summed)
+                wg = d[6]
+                line += (f" | row items={d[10] / 5:.0f}/evaluate poll/item={d[8] / d[10]:.0f}"
+                         f" rows/item={d[9] / d[10]:.0f} per-wg: elements={tot / wg:.0f}"
+                         f" poll={d[8] / wg:.0f} rows={d[9] / wg:.0f}")
         print(line, flush=True)
         ev.close()

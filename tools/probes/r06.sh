@@ -58,6 +58,15 @@ for step in "$@"; do
       for k in totlag linear; do
         run 600 gpmc.log tools/pmc_kernel.sh r06/gpmc_$k gather_h8_kernel occ,inst,flop,mem -- --n 100 --renumber --path gather --kinem $k --reps 3
       done ;;
+    ovlab)  # hex27 40^3 evaluate: the overlapped schedule (env knobs from $OVL_VARIANTS, "two" = the
+            # two launches) alternated over 2 rounds
+      for rep in 1 2; do for v in ${OVL_VARIANTS:-two default}; do for k in ${KINS:-totlag linear}; do
+        envs=""; [ "$v" = two ] && envs="FCG_H27_OVERLAP=0"; [ "$v" != two ] && [ "$v" != default ] && envs="${v//,/ }"
+        r=$(env $envs timeout -k 10 150 python3 $ET --celltype hex27 --kinem $k --n ${N27:-40} --reps 9 | tail -1) || exit 1
+        echo "$v $k $(echo "$r" | python3 -c 'import json,sys; d=json.load(sys.stdin); print(round(d["ms_evaluate"],4), round(d["ms_element"],4), round(d["ms_assemble"],4))')" | tee -a $O/ovlab.txt
+      done; done; done ;;
+    h27st)  # hex27 phase stamps (tools/h27_stamps.py, FCG_STAMPS=1), env $STENV
+      run 300 h27st.log env $STENV python3 tools/h27_stamps.py ${N27:-40} ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
