@@ -67,6 +67,9 @@ for step in "$@"; do
       done; done; done ;;
     h27st)  # hex27 phase stamps (tools/h27_stamps.py, FCG_STAMPS=1), env $STENV
       run 300 h27st.log env $STENV python3 tools/h27_stamps.py ${N27:-40} ;;
+    swst)   # sweep phase stamps (tools/stamps.py) and a HEAD counter set of the headline sweep
+      run 300 swst.log python3 tools/stamps.py 100
+      run 600 swst.log tools/pmc_kernel.sh r06/swpmc "sweep_h8_kernel<0" occ,inst,flop,mem -- --n 100 --reps 3 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
