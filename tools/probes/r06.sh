@@ -70,6 +70,13 @@ for step in "$@"; do
     swst)   # sweep phase stamps (tools/stamps.py) and a HEAD counter set of the headline sweep
       run 300 swst.log python3 tools/stamps.py 100
       run 600 swst.log tools/pmc_kernel.sh r06/swpmc "sweep_h8_kernel<0" occ,inst,flop,mem -- --n 100 --reps 3 ;;
+    libab)  # evaluate timing of libraries $LIBS (default = the product build) alternated over 2 rounds,
+            # tools/eval_timing.py arguments $ETARGS, label $ABTAG
+      for rep in 1 2; do for v in $LIBS; do
+        if [ "$v" = default ]; then unset FCG_LIB; else export FCG_LIB=$v; fi
+        r=$(timeout -k 10 150 python3 $ET $ETARGS | tail -1) || exit 1
+        echo "$v $ABTAG $(echo "$r" | python3 -c 'import json,sys; d=json.load(sys.stdin); print(round(d["ms_evaluate"],4), round(d["ms_element"],4), round(d["ms_assemble"],4))')" | tee -a $O/libab.txt
+      done; done; unset FCG_LIB ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
