@@ -77,6 +77,9 @@ for step in "$@"; do
         r=$(timeout -k 10 150 python3 $ET $ETARGS | tail -1) || exit 1
         echo "$v $ABTAG $(echo "$r" | python3 -c 'import json,sys; d=json.load(sys.stdin); print(round(d["ms_evaluate"],4), round(d["ms_element"],4), round(d["ms_assemble"],4))')" | tee -a $O/libab.txt
       done; done; unset FCG_LIB ;;
+    tsipmc) # HEAD counter sets of the TSI split passes (126^3): the structural sweep and the thermal pass
+      run 600 tsipmc.log tools/pmc_kernel.sh r06/tsipmc "sweep_h8_kernel<0, true, true, 2>" occ,inst,flop,mem -- --n 126 --tsi --reps 3
+      run 60 tsipmc.log python3 tools/pmc_summary.py gpurun_out/r06/tsipmc "sweep_h8_kernel<0, true, true, 0>" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
