@@ -17,6 +17,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -1191,7 +1192,10 @@ struct Xch {
 //     with the distributed A_1, P_1 = (I - w D^-1 A_1) T_1,ext (T_1's ghost rows imported once,
 //     P_1's per tangent in M1 fixed slots), and A_2 = P_1^T (A_1 P_1,ext) gathered by the all-reduce
 //     and solved redundantly by the replicated hierarchy (the replication moves down one level;
-//     with T_1 unsmoothed, 32^3 hex27 on 4 ranks took 184 FCG iterations against 130 on one).
+//     with T_1 unsmoothed, 32^3 hex27 on 4 ranks took 184 FCG iterations against 130 on one);
+//   * or, while level 2 is still past the replication threshold (distribute_level), level 2 is a
+//     Dist of its own (next) built the same way from C2, down to the level that is replicated:
+//     the replicated bytes then stay bounded by the threshold whatever the rank count.
 struct Dist {
   int R = 1, me = 0;
   std::vector<int64_t> agg_off;  // [R + 1]
@@ -1228,6 +1232,13 @@ struct Dist {
   double *p1_s = nullptr, *p1_r = nullptr;
   Bsr AP1;    // na x n2_tot
   Bsr C2;     // n2_tot x n2_tot: this rank's part of A_2 = P_1^T A P_1,ext
+  // the next level distributed in turn (its global size past the replication threshold): the
+  // columns of P_1 (and P_1,ext, AP_1, C2's rows and columns, agg1) are then numbered by the next
+  // level's LA (its NL entries) instead of the global level-2 ids, and C2 is its partial-rows input
+  int level = 1;
+  int64_t n2_cols = 0;  // the column space of P_1: n2_tot, or the next level's NL
+  Dist* next = nullptr;
+  ~Dist() { delete next; }
 };
 
 struct Coupled {
@@ -1616,21 +1627,27 @@ void build_replicated(fcg_amg* h, Coupled* c, std::vector<int64_t> gptr, std::ve
   c->ge = dalloc<double>(h, 6 * n_tot);
 }
 
-// FCG_AMG_DIST=1: distribute level 1 whenever the transport can exchange; 0: never; default: when
-// its global size passes FCG_AMG_DIST_MIN DOFs (50000).  The inputs are the same on every rank.
-bool distribute_level1(const fcg_transport* tr, int64_t n_agg_tot, int64_t min_agg_per_rank)
+// Is coarse level `level` (global size n_agg_tot block rows, at least min_agg_per_rank on every
+// rank) distributed across the ranks?  Default: when its global size passes FCG_AMG_DIST_MIN DOFs
+// (50000), so that the replicated level below stays under that size whatever the rank count.
+// FCG_AMG_DIST=1 forces level 1 (the deeper levels keep the size rule), 0 distributes none;
+// FCG_AMG_DIST_LEVELS caps the distributed levels (default 8).  The inputs are the same on every
+// rank, so every rank decides alike.
+bool distribute_level(const fcg_transport* tr, int level, int64_t n_agg_tot, int64_t min_agg_per_rank)
 {
   if (!tr->exchange_fn || min_agg_per_rank < 1) return false;
   const char* e = std::getenv("FCG_AMG_DIST");
   if (e && e[0] == '0') return false;
-  if (e && e[0] == '1') return true;
+  const char* lv = std::getenv("FCG_AMG_DIST_LEVELS");
+  if (level > (lv ? std::atoi(lv) : 8)) return false;
+  if (level == 1 && e && e[0] == '1') return true;
   const char* m = std::getenv("FCG_AMG_DIST_MIN");
   const int64_t min_dofs = m ? std::atoll(m) : 50000;
   return 6 * n_agg_tot > min_dofs;
 }
 
-void build_dist(fcg_amg* h, Coupled* c, const fcg_transport* tr, const std::vector<int64_t>& counts,
-    const std::vector<int64_t>& LA, hipStream_t s);
+Dist* build_dist(fcg_amg* h, Coupled* c, const fcg_transport* tr, const std::vector<int64_t>& counts,
+    const std::vector<int64_t>& LA, const Bsr& C, const std::vector<double>& ns, int level, hipStream_t s);
 
 void coupled_build(fcg_amg* h, const fcg_transport* tr, hipStream_t s)
 {
@@ -1658,7 +1675,7 @@ void coupled_build(fcg_amg* h, const fcg_transport* tr, hipStream_t s)
       min_agg = std::min(min_agg, counts[static_cast<size_t>(q)]);
     }
   }
-  const bool dist = distribute_level1(tr, c->n_agg_tot, min_agg);
+  const bool dist = distribute_level(tr, 1, c->n_agg_tot, min_agg);
   c->chan = dalloc<double>(h, 3 * nb0);
   c->chan_col = dalloc<double>(h, m.n_cols);
   c->q = dalloc<double>(h, 3 * nb0);
@@ -1725,7 +1742,7 @@ void coupled_build(fcg_amg* h, const fcg_transport* tr, hipStream_t s)
   symbolic(c->Pt, app, appc, n_p_cols, cp, cc);
   make_bsr(h, c->C, cp, cc, 6, 6, n_p_cols);
   if (dist)
-    build_dist(h, c, tr, counts, LA, s);
+    c->d = build_dist(h, c, tr, counts, LA, c->C, h->ns1, 1, s);
   else
   {
     std::vector<int64_t> gptr, pos;
@@ -1743,17 +1760,23 @@ void coupled_build(fcg_amg* h, const fcg_transport* tr, hipStream_t s)
   extend_values(h, c, st0.T, c->Text, 1, tr, s);
 }
 
-void build_dist(fcg_amg* h, Coupled* c, const fcg_transport* tr, const std::vector<int64_t>& counts,
-    const std::vector<int64_t>& LA, hipStream_t s)
+// Coarse level `level` distributed: its owned rows from the partial rows C of the level above (C's
+// rows and columns numbered by LA, this level's ids the level above's prolongator reaches, own
+// range included), its import plans, and the prolongator to the next level, which is distributed
+// in turn (d->next, recursively) or replicated (C2 gathered, the replicated hierarchy built).  ns:
+// the near-null space of this rank's nodes of the level (36 doubles each).
+Dist* build_dist(fcg_amg* h, Coupled* c, const fcg_transport* tr, const std::vector<int64_t>& counts,
+    const std::vector<int64_t>& LA, const Bsr& C, const std::vector<double>& ns, int level, hipStream_t s)
 {
   Dist* d = new Dist();
-  c->d = d;
+  std::unique_ptr<Dist> guard_d(d);  // freed if the build throws before it is linked
+  d->level = level;
   const int R = c->nranks, me = c->rank;
   d->R = R;
   d->me = me;
   d->agg_off.assign(static_cast<size_t>(R) + 1, 0);
   for (int q = 0; q < R; ++q) d->agg_off[static_cast<size_t>(q) + 1] = d->agg_off[static_cast<size_t>(q)] + counts[static_cast<size_t>(q)];
-  d->off = c->off;
+  for (int q = 0; q < me; ++q) d->off += counts[static_cast<size_t>(q)];
   d->na = counts[static_cast<size_t>(me)];
   d->NL = int64_t(LA.size());
   d->own0 = int64_t(std::lower_bound(LA.begin(), LA.end(), d->off) - LA.begin());
@@ -1763,7 +1786,6 @@ void build_dist(fcg_amg* h, Coupled* c, const fcg_transport* tr, const std::vect
   auto owner = [&](int64_t gid) {
     return int(std::upper_bound(d->agg_off.begin(), d->agg_off.end(), gid) - d->agg_off.begin()) - 1;
   };
-  const Bsr& C = c->C;
   d->c_lo = C.ptr_h[static_cast<size_t>(own0)];
   d->c_hi = C.ptr_h[static_cast<size_t>(own0 + na)];
   // 1. the partial rows of the other ranks' aggregates go to their owners: (row, column) pairs once
@@ -1927,29 +1949,32 @@ void build_dist(fcg_amg* h, Coupled* c, const fcg_transport* tr, const std::vect
     if (d->n2 <= 0) throw Fail{FCG_ERR_ARG, "coupled AMG: level-1 aggregation failed"};
     ns2.assign(static_cast<size_t>(d->n2) * 36, 0.0);
     int64_t nd = 0;
-    ck(fcg_amg_tentative(na, 6, h->ns1.data(), agg1.data(), d->n2, tent.data(), ns2.data(), &nd),
-        "fcg_amg_tentative (level 1)");
+    if (int64_t(ns.size()) != 36 * na) throw Fail{FCG_ERR_ARG, "coupled AMG: near-null space size"};
+    ck(fcg_amg_tentative(na, 6, ns.data(), agg1.data(), d->n2, tent.data(), ns2.data(), &nd),
+        "fcg_amg_tentative (distributed level)");
   }
   std::vector<int64_t> counts2(static_cast<size_t>(R), 0);
+  int64_t min2 = 0;
   {
     std::vector<double> v(static_cast<size_t>(R), 0.0);
     v[static_cast<size_t>(me)] = double(d->n2);
     host_allsum(tr, v, s);
+    min2 = int64_t(v[0]);
     for (int q = 0; q < R; ++q)
     {
       counts2[static_cast<size_t>(q)] = int64_t(v[static_cast<size_t>(q)]);
       if (q < me) d->off2 += counts2[static_cast<size_t>(q)];
       d->n2_tot += counts2[static_cast<size_t>(q)];
+      min2 = std::min(min2, counts2[static_cast<size_t>(q)]);
     }
   }
-  {
-    std::vector<int32_t> ag(static_cast<size_t>(na));
-    for (int64_t i = 0; i < na; ++i)
-      ag[static_cast<size_t>(i)] = agg1[static_cast<size_t>(i)] >= 0 ? int32_t(d->off2 + agg1[static_cast<size_t>(i)]) : -1;
-    d->agg1 = upload(h, ag);
-    d->tent1 = upload(h, tent);
-  }
+  // the next level distributed too when it is still large (and coarser than this one)
+  const int64_t n1_tot = d->agg_off.back();
+  const bool next_dist = d->n2_tot < n1_tot && distribute_level(tr, level + 1, d->n2_tot, min2);
   // T_1,ext: A's column rows of T_1 (global level-2 ids), the ghost ones from their owners once
+  std::vector<int64_t> eptr(static_cast<size_t>(d->NA) + 1, 0);
+  std::vector<int32_t> ecol;
+  std::vector<double> ev;
   {
     std::vector<std::vector<double>> rowsout(static_cast<size_t>(R));
     for (int q = 0, o = 0; q < R; ++q)
@@ -1964,9 +1989,6 @@ void build_dist(fcg_amg* h, Coupled* c, const fcg_transport* tr, const std::vect
     std::vector<double> gh;  // the ghost rows in DA order (ascending global id = rank order)
     for (int q = 0; q < R; ++q) gh.insert(gh.end(), rin[static_cast<size_t>(q)].begin(), rin[static_cast<size_t>(q)].end());
     if (int64_t(gh.size()) != 37 * d->imp.nr) throw Fail{FCG_ERR_ARG, "coupled AMG: T_1 ghost rows incomplete"};
-    std::vector<int64_t> eptr(static_cast<size_t>(d->NA) + 1, 0);
-    std::vector<int32_t> ecol;
-    std::vector<double> ev;
     for (int64_t j = 0, gi = 0; j < d->NA; ++j)
     {
       if (j >= d->d0 && j < d->d0 + na)
@@ -1989,30 +2011,21 @@ void build_dist(fcg_amg* h, Coupled* c, const fcg_transport* tr, const std::vect
       }
       eptr[static_cast<size_t>(j) + 1] = int64_t(ecol.size());
     }
-    make_bsr(h, d->T1ext, eptr, ecol, 6, 6, d->n2_tot);
-    if (!ev.empty())
-      ck(hipMemcpy(d->T1ext.vals, ev.data(), sizeof(double) * ev.size(), hipMemcpyHostToDevice), "hipMemcpy");
   }
   // P_1 = (I - w D^-1 A) T_1,ext on the pattern of A T_1,ext (smoothed with the distributed A_1:
   // its rows reach the neighbour ranks' level-2 aggregates), its transpose, and P_1,ext: the ghost
   // rows' patterns from their owners once (M1 column slots per row), their values per tangent
   std::vector<int64_t> a1p, tp, ep, ap1, c2p;
   std::vector<int32_t> a1c, tc, ec, ac1, c2c;
-  symbolic(d->A, d->T1ext.ptr_h, d->T1ext.col_h, d->n2_tot, a1p, a1c);
-  make_bsr(h, d->AT1, a1p, a1c, 6, 6, d->n2_tot);
-  make_bsr(h, d->P1, a1p, a1c, 6, 6, d->n2_tot);
+  symbolic(d->A, eptr, ecol, d->n2_tot, a1p, a1c);
   {
-    tp.assign(static_cast<size_t>(d->n2_tot) + 1, 0);
-    tc.assign(std::max<size_t>(1, a1c.size()), 0);
-    std::vector<int64_t> perm(std::max<size_t>(1, a1c.size()));
-    ck(fcg_bsr_transpose_pattern(na, d->n2_tot, a1p.data(), a1c.data(), tp.data(), tc.data(), perm.data()),
-        "fcg_bsr_transpose_pattern (P_1)");
-    tc.resize(a1c.size());
-    perm.resize(a1c.size());
-    make_bsr(h, d->P1t, tp, tc, 6, 6, na);
-    d->p1_perm = upload(h, perm);
+    std::vector<double> v(static_cast<size_t>(R), 0.0);
+    int64_t w = 0;
+    for (int64_t i = 0; i < na; ++i) w = std::max(w, a1p[static_cast<size_t>(i) + 1] - a1p[static_cast<size_t>(i)]);
+    v[static_cast<size_t>(me)] = double(w);
+    host_allsum(tr, v, s);
+    for (double x : v) d->M1 = std::max(d->M1, int(x));
   }
-  d->M1 = widest_over_ranks(d->P1, me, R, tr, s);
   {
     std::vector<std::vector<double>> rowsout(static_cast<size_t>(R));
     for (int q = 0, o = 0; q < R; ++q)
@@ -2046,24 +2059,74 @@ void build_dist(fcg_amg* h, Coupled* c, const fcg_transport* tr, const std::vect
       }
       ep[static_cast<size_t>(j) + 1] = int64_t(ec.size());
     }
-    make_bsr(h, d->P1ext, ep, ec, 6, 6, d->n2_tot);
-    d->p1_s = dalloc<double>(h, 36 * d->M1 * d->imp.ns);
-    d->p1_r = dalloc<double>(h, 36 * d->M1 * d->imp.nr);
   }
+  // the column space of P_1: the global level-2 ids (replicated next level), or the next level's
+  // LA -- the level-2 ids P_1,ext reaches, ascending (P_1's own rows reach every owned aggregate)
+  std::vector<int64_t> LA2;
+  d->n2_cols = d->n2_tot;
+  std::vector<int32_t> ag(static_cast<size_t>(na));
+  for (int64_t i = 0; i < na; ++i)
+    ag[static_cast<size_t>(i)] = agg1[static_cast<size_t>(i)] >= 0 ? int32_t(d->off2 + agg1[static_cast<size_t>(i)]) : -1;
+  if (next_dist)
+  {
+    LA2.assign(ec.begin(), ec.end());
+    std::sort(LA2.begin(), LA2.end());
+    LA2.erase(std::unique(LA2.begin(), LA2.end()), LA2.end());
+    auto g2l = [&](int32_t g) {
+      const auto it = std::lower_bound(LA2.begin(), LA2.end(), int64_t(g));
+      if (it == LA2.end() || *it != g) throw Fail{FCG_ERR_ARG, "coupled AMG: level-2 aggregate outside P_1,ext's columns"};
+      return int32_t(it - LA2.begin());
+    };
+    for (auto* v : {&ecol, &a1c, &ec})
+      for (auto& x : *v) x = g2l(x);
+    for (auto& x : ag)
+      if (x >= 0) x = g2l(x);
+    d->n2_cols = int64_t(LA2.size());
+  }
+  d->agg1 = upload(h, ag);
+  d->tent1 = upload(h, tent);
+  make_bsr(h, d->T1ext, eptr, ecol, 6, 6, d->n2_cols);
+  if (!ev.empty())
+    ck(hipMemcpy(d->T1ext.vals, ev.data(), sizeof(double) * ev.size(), hipMemcpyHostToDevice), "hipMemcpy");
+  make_bsr(h, d->AT1, a1p, a1c, 6, 6, d->n2_cols);
+  make_bsr(h, d->P1, a1p, a1c, 6, 6, d->n2_cols);
+  {
+    tp.assign(static_cast<size_t>(d->n2_cols) + 1, 0);
+    tc.assign(std::max<size_t>(1, a1c.size()), 0);
+    std::vector<int64_t> perm(std::max<size_t>(1, a1c.size()));
+    ck(fcg_bsr_transpose_pattern(na, d->n2_cols, a1p.data(), a1c.data(), tp.data(), tc.data(), perm.data()),
+        "fcg_bsr_transpose_pattern (P_1)");
+    tc.resize(a1c.size());
+    perm.resize(a1c.size());
+    make_bsr(h, d->P1t, tp, tc, 6, 6, na);
+    d->p1_perm = upload(h, perm);
+  }
+  make_bsr(h, d->P1ext, ep, ec, 6, 6, d->n2_cols);
+  d->p1_s = dalloc<double>(h, 36 * d->M1 * d->imp.ns);
+  d->p1_r = dalloc<double>(h, 36 * d->M1 * d->imp.nr);
   // this rank's part of A_2 = P_1^T (A P_1,ext): rows of every level-2 aggregate its P_1 reaches
-  symbolic(d->A, ep, ec, d->n2_tot, ap1, ac1);
-  make_bsr(h, d->AP1, ap1, ac1, 6, 6, d->n2_tot);
-  symbolic(d->P1t, ap1, ac1, d->n2_tot, c2p, c2c);
-  make_bsr(h, d->C2, c2p, c2c, 6, 6, d->n2_tot);
-  std::vector<int64_t> gptr, pos;
-  std::vector<int32_t> gcol;
-  gather_replicated(c, tr, c2p, c2c, 0, d->n2_tot, s, gptr, gcol, pos);
-  c->rep_part = &d->C2;
-  c->rep_pos = upload(h, pos);
-  std::vector<double> nsg(static_cast<size_t>(36 * d->n2_tot), 0.0);
-  std::copy(ns2.begin(), ns2.end(), nsg.begin() + 36 * d->off2);
-  host_allsum(tr, nsg, s);
-  build_replicated(h, c, std::move(gptr), std::move(gcol), d->n2_tot, std::move(nsg));
+  symbolic(d->A, ep, ec, d->n2_cols, ap1, ac1);
+  make_bsr(h, d->AP1, ap1, ac1, 6, 6, d->n2_cols);
+  symbolic(d->P1t, ap1, ac1, d->n2_cols, c2p, c2c);
+  make_bsr(h, d->C2, c2p, c2c, 6, 6, d->n2_cols);
+  if (next_dist)
+  {
+    std::vector<double> ns_next(ns2.begin(), ns2.begin() + 36 * d->n2);
+    d->next = build_dist(h, c, tr, counts2, LA2, d->C2, ns_next, level + 1, s);
+  }
+  else
+  {
+    std::vector<int64_t> gptr, pos;
+    std::vector<int32_t> gcol;
+    gather_replicated(c, tr, c2p, c2c, 0, d->n2_tot, s, gptr, gcol, pos);
+    c->rep_part = &d->C2;
+    c->rep_pos = upload(h, pos);
+    std::vector<double> nsg(static_cast<size_t>(36 * d->n2_tot), 0.0);
+    std::copy(ns2.begin(), ns2.end(), nsg.begin() + 36 * d->off2);
+    host_allsum(tr, nsg, s);
+    build_replicated(h, c, std::move(gptr), std::move(gcol), d->n2_tot, std::move(nsg));
+  }
+  return guard_d.release();
 }
 
 // y = A_1 x on the owned rows: x into the extended vector, its ghost entries imported
@@ -2089,11 +2152,9 @@ void dist_dinv(fcg_amg* h, const Dist* d, const double* r, double* z, double sca
 
 // numeric: A_1's owned rows from this rank's blocks and the partial rows of the other ranks, its
 // block Jacobi and lambda_max, P_1 and this rank's part of A_2
-void dist_setup(fcg_amg* h, const fcg_transport* tr, hipStream_t s)
+void dist_setup(fcg_amg* h, Dist* d, const Bsr& C, const fcg_transport* tr, hipStream_t s)
 {
   Coupled* c = h->cpl;
-  Dist* d = c->d;
-  const Bsr& C = c->C;
   ck(hipMemsetAsync(d->A.vals, 0, sizeof(double) * static_cast<size_t>(std::max<int64_t>(1, d->A.nnzb)) * 36, s), "memset");
   if (d->c_hi > d->c_lo)
     hipLaunchKernelGGL(add_blocks_kernel, dim3(blocks_for((d->c_hi - d->c_lo) * 36)), dim3(kBlock), 0, s,
@@ -2112,7 +2173,8 @@ void dist_setup(fcg_amg* h, const fcg_transport* tr, hipStream_t s)
   }
   ck(hipGetLastError(), "add_blocks_kernel");
   ck(fcg_bsr_block_jacobi_setup(h->device, 6, d->na, d->A.ptr, d->diag, d->A.vals, d->dinv, h->flag, s),
-      "coupled AMG level 1: singular diagonal block");
+      d->level == 1 ? "coupled AMG level 1: singular diagonal block"
+                    : "coupled AMG distributed level: singular diagonal block");
   Ops o{h, 1, nullptr, s, tr};
   o.dl = d;
   estimate_lmax(o);
@@ -2138,27 +2200,68 @@ void dist_setup(fcg_amg* h, const fcg_transport* tr, hipStream_t s)
          d->P1ext.vals, d->AP1.ptr, d->AP1.col, d->AP1.vals, s), "fcg_bsr_spgemm (A_1 P_1,ext)");
   ck(fcg_bsr_spgemm(h->device, 6, 6, 6, d->P1t.n, d->P1t.ptr, d->P1t.col, d->P1t.vals, d->AP1.ptr,
          d->AP1.col, d->AP1.vals, d->C2.ptr, d->C2.col, d->C2.vals, s), "fcg_bsr_spgemm (P_1^T A_1 P_1)");
+  if (d->next) dist_setup(h, d->next, d->C2, tr, s);
 }
 
-// one V-cycle of the distributed level 1: Chebyshev with A_1, the residual restricted by P_1^T into
-// the replicated level 2 (each rank's partial sums, completed by the all-reduce), the replicated
-// hierarchy, P_1 back, Chebyshev again
-void dist_vcycle(fcg_amg* h, const fcg_transport* tr, const double* b, double* x, hipStream_t s)
+void dist_vcycle(fcg_amg* h, const fcg_transport* tr, Dist* d, const double* b, double* x, hipStream_t s);
+
+// y (+)= P A_nd^-1 P^T x through the distributed level nd: the restriction by Pt into nd's LA (rows
+// of the level above, bs-wide blocks), whose other-rank entries go to their owners and are added
+// there (senders in rank order), nd's V-cycle, the reverse exchange, P back
+void dist_coarse(fcg_amg* h, const fcg_transport* tr, Dist* nd, int bs, const Bsr& Pt, const Bsr& P,
+    const double* x, double* y, int accumulate, hipStream_t s)
 {
   Coupled* c = h->cpl;
-  Dist* d = c->d;
+  const int64_t na = nd->na, own0 = nd->own0, tail = nd->NL - own0 - na;
+  ck(fcg_bsr_spmv(h->device, 6, bs, Pt.n, Pt.ptr, Pt.col, Pt.vals, x, nd->y, 1.0, 0, s), "restriction");
+  copy_dd(nd->b, nd->y + 6 * own0, 6 * na, s);
+  copy_dd(nd->pex_s, nd->y, 6 * own0, s);
+  copy_dd(nd->pex_s + 6 * own0, nd->y + 6 * (own0 + na), 6 * tail, s);
+  exchange_counted(c, tr, nd->pex, 6, false, nd->pex_s, nd->pex_r, s, "transport exchange (restriction)");
+  for (int q = 0, o = 0; q < nd->R; ++q)
+  {
+    const int64_t n = nd->pex.rcnt[static_cast<size_t>(q)];
+    if (n > 0)
+      hipLaunchKernelGGL(add_items_kernel, dim3(blocks_for(6 * n)), dim3(kBlock), 0, s, n, nd->pex_idx + o,
+          nd->pex_r + 6 * o, nd->b);
+    o += int(n);
+  }
+  ck(hipGetLastError(), "add_items_kernel");
+  dist_vcycle(h, tr, nd, nd->b, nd->x, s);
+  if (nd->pex.nr > 0)
+    hipLaunchKernelGGL(gather_items_kernel, dim3(blocks_for(6 * nd->pex.nr)), dim3(kBlock), 0, s, nd->pex.nr,
+        nd->pex_idx, nd->x, nd->pex_r);
+  ck(hipGetLastError(), "gather_items_kernel");
+  exchange_counted(c, tr, nd->pex, 6, true, nd->pex_r, nd->pex_s, s, "transport exchange (prolongation)");
+  copy_dd(nd->y + 6 * own0, nd->x, 6 * na, s);
+  copy_dd(nd->y, nd->pex_s, 6 * own0, s);
+  copy_dd(nd->y + 6 * (own0 + na), nd->pex_s + 6 * own0, 6 * tail, s);
+  ck(fcg_bsr_spmv(h->device, bs, 6, P.n, P.ptr, P.col, P.vals, nd->y, y, 1.0, accumulate, s), "prolongation");
+}
+
+// one V-cycle of a distributed level: Chebyshev with its A, the residual restricted by P_1^T into
+// the next level -- distributed in turn (dist_coarse), or replicated (each rank's partial sums,
+// completed by the all-reduce, and the replicated hierarchy) -- P_1 back, Chebyshev again
+void dist_vcycle(fcg_amg* h, const fcg_transport* tr, Dist* d, const double* b, double* x, hipStream_t s)
+{
+  Coupled* c = h->cpl;
   Ops o{h, 1, nullptr, s, tr};
   o.dl = d;
   cheb(h, o, b, x, true);
   o.spmv(x, d->r);
   const int64_t n = 6 * d->na;
   hipLaunchKernelGGL(rsub_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, s, b, d->r, n);
-  ck(fcg_bsr_spmv(h->device, 6, 6, d->P1t.n, d->P1t.ptr, d->P1t.col, d->P1t.vals, d->r, c->gb, 1.0, 0, s),
-      "restriction (level 1)");
-  allreduce_counted(c, tr, c->gb, 6 * d->n2_tot, s, "transport all-reduce (level 2)");
-  vcycle(c->g, 1, nullptr, c->gb, c->ge, s);
-  ck(fcg_bsr_spmv(h->device, 6, 6, d->P1.n, d->P1.ptr, d->P1.col, d->P1.vals, c->ge, x, 1.0, 1, s),
-      "prolongation (level 1)");
+  if (d->next)
+    dist_coarse(h, tr, d->next, 6, d->P1t, d->P1, d->r, x, 1, s);
+  else
+  {
+    ck(fcg_bsr_spmv(h->device, 6, 6, d->P1t.n, d->P1t.ptr, d->P1t.col, d->P1t.vals, d->r, c->gb, 1.0, 0, s),
+        "restriction (distributed level)");
+    allreduce_counted(c, tr, c->gb, 6 * d->n2_tot, s, "transport all-reduce (replicated level)");
+    vcycle(c->g, 1, nullptr, c->gb, c->ge, s);
+    ck(fcg_bsr_spmv(h->device, 6, 6, d->P1.n, d->P1.ptr, d->P1.col, d->P1.vals, c->ge, x, 1.0, 1, s),
+        "prolongation (distributed level)");
+  }
   cheb(h, o, b, x, false);
 }
 
@@ -2184,7 +2287,7 @@ void coupled_setup(fcg_amg* h, const double* K, const fcg_transport* tr, hipStre
          c->Pext.col, c->Pext.vals, c->AP.ptr, c->AP.col, c->AP.vals, s), "fcg_bsr_spgemm (A P_ext)");
   ck(fcg_bsr_spgemm(h->device, 6, 3, 6, c->Pt.n, c->Pt.ptr, c->Pt.col, c->Pt.vals, c->AP.ptr, c->AP.col,
          c->AP.vals, c->C.ptr, c->C.col, c->C.vals, s), "fcg_bsr_spgemm (P^T A P)");
-  if (c->d) dist_setup(h, tr, s);
+  if (c->d) dist_setup(h, c->d, c->C, tr, s);
   // the replicated operator: every rank's blocks scattered into a zeroed buffer, summed
   fcg_amg* g = c->g;
   Level& L1 = g->levels[0];
@@ -2193,9 +2296,9 @@ void coupled_setup(fcg_amg* h, const double* K, const fcg_transport* tr, hipStre
     hipLaunchKernelGGL(scatter_blocks_kernel, dim3(blocks_for(c->rep_part->nnzb * 36)), dim3(kBlock), 0, s,
         c->rep_part->nnzb, c->rep_pos, c->rep_part->vals, L1.A.vals);
   ck(hipGetLastError(), "scatter_blocks_kernel");
-  allreduce_counted(c, tr, L1.A.vals, c->rep_nnzb * 36, s, c->d ? "transport all-reduce (A_2)" : "transport all-reduce (A_1)");
+  allreduce_counted(c, tr, L1.A.vals, c->rep_nnzb * 36, s, c->d ? "transport all-reduce (replicated coarse level)" : "transport all-reduce (A_1)");
   ck(fcg_bsr_block_jacobi_setup(g->device, 6, L1.A.n, L1.A.ptr, L1.diag, L1.A.vals, L1.dinv, g->flag, s),
-      c->d ? "coupled AMG level 2: singular diagonal block" : "coupled AMG level 1: singular diagonal block");
+      c->d ? "coupled AMG replicated level: singular diagonal block" : "coupled AMG level 1: singular diagonal block");
   if (g->steps.size() > 1) estimate_lmax(Ops{g, 1, nullptr, s});
   galerkin_from(g, 1, nullptr, s);
   c->ar_setup = c->ctr_ar;
@@ -2219,31 +2322,7 @@ void coupled_coarse(fcg_amg* h, const fcg_transport* tr, const double* x, double
     ck(fcg_bsr_spmv(h->device, 3, 6, c->P.n, c->P.ptr, c->P.col, c->P.vals, c->ge, y, 1.0, 0, s), "prolongation");
     return;
   }
-  const int64_t na = d->na, own0 = d->own0, tail = d->NL - own0 - na;
-  ck(fcg_bsr_spmv(h->device, 6, 3, c->Pt.n, c->Pt.ptr, c->Pt.col, c->Pt.vals, x, d->y, 1.0, 0, s), "restriction");
-  copy_dd(d->b, d->y + 6 * own0, 6 * na, s);
-  copy_dd(d->pex_s, d->y, 6 * own0, s);
-  copy_dd(d->pex_s + 6 * own0, d->y + 6 * (own0 + na), 6 * tail, s);
-  exchange_counted(c, tr, d->pex, 6, false, d->pex_s, d->pex_r, s, "transport exchange (restriction)");
-  for (int q = 0, o = 0; q < d->R; ++q)
-  {
-    const int64_t n = d->pex.rcnt[static_cast<size_t>(q)];
-    if (n > 0)
-      hipLaunchKernelGGL(add_items_kernel, dim3(blocks_for(6 * n)), dim3(kBlock), 0, s, n, d->pex_idx + o,
-          d->pex_r + 6 * o, d->b);
-    o += int(n);
-  }
-  ck(hipGetLastError(), "add_items_kernel");
-  dist_vcycle(h, tr, d->b, d->x, s);
-  if (d->pex.nr > 0)
-    hipLaunchKernelGGL(gather_items_kernel, dim3(blocks_for(6 * d->pex.nr)), dim3(kBlock), 0, s, d->pex.nr,
-        d->pex_idx, d->x, d->pex_r);
-  ck(hipGetLastError(), "gather_items_kernel");
-  exchange_counted(c, tr, d->pex, 6, true, d->pex_r, d->pex_s, s, "transport exchange (prolongation)");
-  copy_dd(d->y + 6 * own0, d->x, 6 * na, s);
-  copy_dd(d->y, d->pex_s, 6 * own0, s);
-  copy_dd(d->y + 6 * (own0 + na), d->pex_s + 6 * own0, 6 * tail, s);
-  ck(fcg_bsr_spmv(h->device, 3, 6, c->P.n, c->P.ptr, c->P.col, c->P.vals, d->y, y, 1.0, 0, s), "prolongation");
+  dist_coarse(h, tr, d, 3, c->Pt, c->P, x, y, 0, s);
 }
 
 // y = A x with the global operator: the import of x into the column map, the rank's SpMV
@@ -2903,17 +2982,20 @@ int fcg_amg_precond_apply(fcg_amg* h, const double* d_K, const fcg_transport* tr
 
 int fcg_amg_coupled_levels(const fcg_amg* h)
 {
-  return h && h->cpl && h->cpl->g ? int(h->cpl->g->levels.size()) + (h->cpl->d ? 1 : 0) : 0;
+  if (!h || !h->cpl || !h->cpl->g) return 0;
+  int n = int(h->cpl->g->levels.size());
+  for (const fcg_amgs::Dist* d = h->cpl->d; d; d = d->next) ++n;
+  return n;
 }
 
 int fcg_amg_coupled_stats(const fcg_amg* h, int64_t* out, int n)
 {
   if (!h || !out || n < 0) return FCG_ERR_ARG;
   const fcg_amgs::Coupled* c = h->cpl;
-  int64_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int64_t v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   if (c && c->g)
   {
-    v[0] = c->d ? 1 : 0;
+    for (const fcg_amgs::Dist* d = c->d; d; d = d->next) ++v[0];
     v[1] = c->d ? c->d->na : c->n_agg_tot;
     v[2] = c->n_agg_tot;
     v[3] = c->ar_setup;
@@ -2921,8 +3003,9 @@ int fcg_amg_coupled_stats(const fcg_amg* h, int64_t* out, int n)
     v[5] = c->x_setup;
     v[6] = c->x_apply;
     v[7] = fcg_amgs::hierarchy_bytes(c->g);
+    v[8] = c->rep_n;
   }
-  const int k = std::min(n, 8);
+  const int k = std::min(n, 9);
   for (int i = 0; i < k; ++i) out[i] = v[i];
   return k;
 }

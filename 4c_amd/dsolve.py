@@ -237,14 +237,14 @@ class NativeDFCG:
 
     COUPLED_STATS = ("distributed_levels", "level1_rows_here", "level1_rows_global",
                      "allreduce_doubles_setup", "allreduce_doubles_apply", "exchange_doubles_setup",
-                     "exchange_doubles_apply", "replicated_bytes")
+                     "exchange_doubles_apply", "replicated_bytes", "replicated_rows")
 
     def coupled_stats(self):
         """fcg_amg_coupled_stats: what the coupled coarse levels store and move on this rank."""
         if self.amg is None:
             return {}
-        out = (ctypes.c_int64 * 8)()
-        n = fcg.lib().fcg_amg_coupled_stats(self.amg._h, out, 8)
+        out = (ctypes.c_int64 * len(self.COUPLED_STATS))()
+        n = fcg.lib().fcg_amg_coupled_stats(self.amg._h, out, len(self.COUPLED_STATS))
         return {k: int(out[i]) for i, k in enumerate(self.COUPLED_STATS[:max(0, n)])}
 
 

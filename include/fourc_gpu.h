@@ -696,8 +696,9 @@ typedef struct fcg_transport {
    * operator A_1 = P_0^T A P_0 is gathered by allreduce_fn and solved redundantly on every rank;
    * with it, level 1 is distributed (each rank owns the rows of its aggregates, its own import
    * plan, the partial rows of the other ranks' aggregates sent to their owners) once its global
-   * size passes FCG_AMG_DIST_MIN DOFs (default 50000; FCG_AMG_DIST=1 always, 0 never), and the
-   * replication moves down to level 2 = T_1^T A_1 T_1 (fcg_amg_coupled_stats). */
+   * size passes FCG_AMG_DIST_MIN DOFs (default 50000; FCG_AMG_DIST=1 always, 0 never), and so
+   * is every coarser level past that size (FCG_AMG_DIST_LEVELS caps the count, default 8): the
+   * first level under it is the one replicated (fcg_amg_coupled_stats). */
   int32_t rank;
   int32_t nranks;
   fcg_exchange_fn exchange_fn;  /* may be NULL */
@@ -716,15 +717,18 @@ int fcg_amg_apply(fcg_amg* amg, const double* d_K_vals, const double* d_r_row, d
  * (level 1 = the global A_1 and its coarsenings; 0 = none: single rank, or nranks <= 1). */
 int fcg_amg_coupled_levels(const fcg_amg* amg);
 /* What the coupled coarse levels cost this rank (after the first fcg_dfcg_solve), out[0..n):
- *   0 distributed levels (0: A_1 replicated, 1: A_1 distributed and A_2 replicated)
+ *   0 distributed levels (0: A_1 replicated, 1: A_1 distributed and A_2 replicated, k: levels
+ *     1..k distributed and A_{k+1} replicated)
  *   1 level-1 block rows (6 DOFs each) this rank stores: its own (distributed) or all (replicated)
  *   2 level-1 block rows over all ranks
  *   3 doubles all-reduced per numeric setup (the replicated level's Galerkin operator)
  *   4 doubles all-reduced per preconditioner application (the replicated level's right-hand side)
- *   5 doubles this rank sends per numeric setup through exchange_fn (partial level-1 rows)
- *   6 doubles this rank sends per application through exchange_fn (level-1 imports, restriction
- *     and prolongation)
+ *   5 doubles this rank sends per numeric setup through exchange_fn (partial rows of every
+ *     distributed level, P's ghost rows)
+ *   6 doubles this rank sends per application through exchange_fn (imports, restriction and
+ *     prolongation of every distributed level)
  *   7 bytes of the replicated hierarchy's matrices on this rank
+ *   8 block rows of the replicated level (the first coarse level not distributed)
  * Returns the number of entries written (<= n). */
 int fcg_amg_coupled_stats(const fcg_amg* amg, int64_t* out, int n);
 /* fcg_exchange_fn over RCCL (user = fcg_comm*): grouped ncclSend / ncclRecv on `stream`. */

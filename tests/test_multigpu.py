@@ -575,6 +575,66 @@ def test_distributed_level1_weak_scaling_stats():
     assert g4 >= 1.8 * g2, per
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_distributed_deeper_levels_coupled_amg(world):
+    """Levels 1..k of the coupled AMG distributed (FCG_AMG_DIST_MIN=0: every coarser level that
+    still shrinks is distributed too, FCG_AMG_DIST_LEVELS=3 caps them; each level a Dist of its own,
+    built from the partial rows of the level above): the 1-rank solution by GID, the FCG iterations
+    within 1.5x of one rank, and the stats against level 1 alone -- more distributed levels, a
+    smaller replicated level, fewer doubles all-reduced per application."""
+    box = "32,12,12"
+    with _env(FCG_TEST_SOLVE_BOX=box):
+        one = _one_rank_amg_iters(fcg.HEX8, fcg.LINEAR)
+    st1, stk = [], []
+    with _env(FCG_AMG_DIST="1", FCG_AMG_DIST_LEVELS="1", FCG_TEST_SOLVE_BOX=box):
+        it1 = _run_two_rank_solve(fcg.LINEAR, fcg.PATH_AUTO, "staged", "native", fcg.HEX8, world=world, stats=st1)
+    with _env(FCG_AMG_DIST="1", FCG_AMG_DIST_MIN="0", FCG_AMG_DIST_LEVELS="3", FCG_TEST_SOLVE_BOX=box):
+        itk = _run_two_rank_solve(fcg.LINEAR, fcg.PATH_AUTO, "staged", "native", fcg.HEX8, world=world, stats=stk)
+    n1, na, nk = sum(one), sum(i or 0 for i in it1[0]), sum(i or 0 for i in itk[0])
+    print(f"FCG iterations: 1 rank {one}, {world} ranks level 1 distributed {it1[0]}, levels 1..k {itk[0]}")
+    print("stats level 1", st1, "levels 1..k", stk)
+    assert na <= 1.5 * n1 and nk <= 1.5 * n1, (one, it1, itk)
+    for a, b in zip(st1, stk):
+        assert a["distributed_levels"] == 1 and b["distributed_levels"] >= 2, (a, b)
+        assert a["level1_rows_here"] == b["level1_rows_here"]
+        assert b["replicated_rows"] < a["replicated_rows"]
+        assert b["replicated_bytes"] < a["replicated_bytes"]
+        assert b["allreduce_doubles_apply"] == 6 * b["replicated_rows"]
+        assert b["allreduce_doubles_apply"] < a["allreduce_doubles_apply"]
+    assert len({s["distributed_levels"] for s in stk}) == 1  # every rank decided alike
+
+
+def test_distributed_levels_weak_scaling_replicated_bounded():
+    """Weak scaling with the replication threshold (a box of 12 x 12 x 12 hex8 per rank along x on
+    2, 4 and 8 ranks, FCG_AMG_DIST_MIN=72 DOFs): the levels past the threshold are distributed, so
+    the replicated level stays under it at every rank count (or at one aggregate per rank, the floor
+    of a rank-local aggregation), while with level 1 alone distributed the replicated level grows
+    with the ranks; the FCG iterations stay within 1.5x of one rank."""
+    thr = 72
+    per = {}
+    for world in (2, 4, 8):
+        box = f"{12 * world},12,12"
+        with _env(FCG_TEST_SOLVE_BOX=box):
+            one = _one_rank_amg_iters(fcg.HEX8, fcg.LINEAR)
+        st_k, st_1 = [], []
+        with _env(FCG_AMG_DIST="1", FCG_AMG_DIST_MIN=str(thr), FCG_TEST_SOLVE_BOX=box):
+            itk = _run_two_rank_solve(fcg.LINEAR, fcg.PATH_AUTO, "staged", "native", fcg.HEX8, world=world,
+                                      stats=st_k)
+        with _env(FCG_AMG_DIST="1", FCG_AMG_DIST_LEVELS="1", FCG_TEST_SOLVE_BOX=box):
+            _run_two_rank_solve(fcg.LINEAR, fcg.PATH_AUTO, "staged", "native", fcg.HEX8, world=world, stats=st_1)
+        n1, nk = sum(one), sum(i or 0 for i in itk[0])
+        print(world, "iterations 1 rank", one, "distributed", itk[0], "stats", st_k, "level 1 only", st_1)
+        assert nk <= 1.5 * n1, (world, one, itk)
+        per[world] = (st_k[0]["replicated_rows"], st_k[0]["distributed_levels"], st_1[0]["replicated_rows"],
+                      max(s["replicated_bytes"] for s in st_k), max(s["replicated_bytes"] for s in st_1))
+    print(per)
+    for world, (rk, lk, r1, bk, b1) in per.items():
+        assert 6 * rk <= max(thr, 6 * world), per  # under the threshold (or one aggregate per rank)
+        assert rk <= r1 and bk <= b1, per
+    assert per[8][1] >= 2 and per[8][0] < per[8][2], per  # 8 ranks: level 2 distributed too
+    assert per[8][2] >= 3 * per[2][2], per  # level 1 alone: the replicated level grows with the ranks
+
+
 def _one_rank_amg_iters(celltype, kinem):
     """The same Newton on one rank with the native AMG (fcg_amg_iterate): FCG iterations per step."""
     _dev()
