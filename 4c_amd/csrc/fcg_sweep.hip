@@ -360,6 +360,13 @@ __device__ inline void sweep_visit(const SH& sh, int slot, int a, int b1, int b2
     }
     if (KIN == 0)
     {
+#ifdef FCG_PROBE_NOG
+      // timing probe only (wrong results): the loads kept, 4 of the 18 FMAs
+      const double sa = a0 + a1 + a2;
+      acc1[0] += sa * (p0 + p1 + p2);
+      acc2[0] += sa * (q0 + q1 + q2);
+      return;
+#endif
       acc1[0] += a0 * p0; acc1[1] += a0 * p1; acc1[2] += a0 * p2;
       acc1[3] += a1 * p0; acc1[4] += a1 * p1; acc1[5] += a1 * p2;
       acc1[6] += a2 * p0; acc1[7] += a2 * p1; acc1[8] += a2 * p2;
@@ -521,7 +528,7 @@ __global__ __launch_bounds__(256, KIN ? 1 : FCG_SWEEP_WGS) void sweep_h8_kernel(
   constexpr int NLD = (NNODE * NC + 255) / 256;  // node-load items per lane
   constexpr int NF = TSI ? 4 : 3;                // residual rows per node: f_S (3) | f_T
   const int tid = threadIdx.x;
-  unsigned long long st_acc[2] = {0, 0};
+  unsigned long long st_acc[3] = {0, 0, 0};
   unsigned long long st_last = A.stamps ? __builtin_amdgcn_s_memtime() : 0ull;
   const int tile = blockIdx.x;
   const int tx = tile % A.tiles_x;
@@ -659,7 +666,12 @@ __global__ __launch_bounds__(256, KIN ? 1 : FCG_SWEEP_WGS) void sweep_h8_kernel(
     uint32_t rec_nxt[2];
     load_rec(L + 2, rec_nxt);
     // A. element stage
+#ifdef FCG_PROBE_NOSTAGEA
+    // timing probe only (wrong results): no element stage
+    if (a_lane && e_cur == -12345) sweep_stage_a<KIN, TSI>(sh, A, s, g, sx, sy, L, e_cur);
+#else
     if (a_lane) sweep_stage_a<KIN, TSI>(sh, A, s, g, sx, sy, L, e_cur);
+#endif
     __syncthreads();
     FCG_STAMP(0);
     // commit plane L+2 (nodes and record into plane L-1's ring slot)
@@ -670,6 +682,13 @@ __global__ __launch_bounds__(256, KIN ? 1 : FCG_SWEEP_WGS) void sweep_h8_kernel(
       dof_nxt[j] = dof_nn[j];
     }
     store_rec(L + 2, rec_nxt);
+    if (A.stamps)
+    {
+      // phase 2: the commit's wait for plane L+2's loads (and, behind them in vmcnt, the previous
+      // layer's K stores)
+      __asm__ volatile("" ::"v"(rec_nxt[0]), "v"(node_nxt[0]));
+      FCG_STAMP(2);
+    }
 
     // B. visit stage
     const bool wl = L >= kz0, wl1 = L + 1 < kz1;
@@ -784,15 +803,30 @@ __global__ __launch_bounds__(256, KIN ? 1 : FCG_SWEEP_WGS) void sweep_h8_kernel(
         if (!(to_l1 ? wl1 : wl) || row0 < 0 || pos == 0xFFFF) return;
         const int64_t base = int64_t(base_lo) | (int64_t(base_hi) << 32);
         const int64_t len = len32;
+#ifdef FCG_PROBE_KL2
+        // timing probe only (wrong results): the same stores, folded into 256 KB (L2-resident)
+        double* dst = A.K + ((base + pos) & 0x7FFF);
+#else
         double* dst = A.K + base + pos;
+#endif
+#ifdef FCG_PROBE_NOKSTORE
+        // timing probe only (wrong results): no K stores
+        if (Kb[0] == 12345.678) dst[0] = Kb[1];
+        if (false)
+#else
         if (!TH)
+#endif
 #pragma unroll
           for (int r = 0; r < 3; ++r)
 #pragma unroll
             for (int qq = 0; qq < 3; ++qq)
             {
               if (OVERWRITE)
+#ifdef FCG_PROBE_KNT  // timing probe: non-temporal K stores (4.2 ms instead of 0.98: partial lines)
+                __builtin_nontemporal_store(Kb[3 * r + qq], dst + r * len + qq);
+#else
                 dst[r * len + qq] = Kb[3 * r + qq];
+#endif
               else
                 dst[r * len + qq] += Kb[3 * r + qq];
             }
@@ -985,7 +1019,7 @@ __global__ __launch_bounds__(256, KIN ? 1 : FCG_SWEEP_WGS) void sweep_h8_kernel(
   }
   if (A.stamps && tid == 0)
   {
-    for (int i = 0; i < 2; ++i) atomicAdd(&A.stamps[i], st_acc[i]);
+    for (int i = 0; i < 3; ++i) atomicAdd(&A.stamps[i], st_acc[i]);
     atomicAdd(&A.stamps[5], 1ull);
   }
 }

@@ -9,7 +9,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 fcg = importlib.import_module("4c_amd").fcg
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 100
 dev = torch.device("cuda:0")
-names = ["elements", "visits"]
+names = ["elements", "visits", "commit"]
 for kin in (fcg.LINEAR, fcg.TOTLAG):
     m = fcg.BoxMesh(fcg.HEX8, (n, n, n), jitter=0.1)
     u = torch.from_numpy(m.u_col(1e-3)).to(dev)
@@ -30,7 +30,7 @@ for kin in (fcg.LINEAR, fcg.TOTLAG):
         line = (f"kin={kin} stamps={stamps} nlnstiff_ms={min(ts):.3f}/{sorted(ts)[2]:.3f} "
                 f"internalforce_ms={tf:.3f}")
         if d:
-            tot = sum(d[:2])
+            tot = sum(d[:3])
             wg = d[5]
             line += " per-WG kcycles: " + " ".join(
                 f"{nm}={d[i] / wg / 1e3:.1f}({100 * d[i] / tot:.0f}%)" for i, nm in enumerate(names))
