@@ -334,8 +334,8 @@ void run_rank(int n, int nranks, int rank, ThreadComm* tc, RankResult* out)
     ndu = std::sqrt(dd);
   }
   for (int64_t i = 0; i < nr; ++i) out->u[row_gid[i]] = u[size_t(i)];
-  out->coupled.assign(8, 0);
-  out->coupled.resize(size_t(std::max(0, fcg_amg_coupled_stats(amg, out->coupled.data(), 8))));
+  out->coupled.assign(9, 0);
+  out->coupled.resize(size_t(std::max(0, fcg_amg_coupled_stats(amg, out->coupled.data(), 9))));
   out->ok = conv;
   if (!conv) out->err = "Newton did not converge";
   for (void* p : {dK, du_row, du_col, df, drhs, ddu, ddbc, d_send, d_recv}) fcg_device_free(p);
@@ -423,7 +423,7 @@ int main(int argc, char** argv)
     report(nranks, resR, linR, uR);
     // fcg_amg_coupled_stats per rank: distributed levels, level-1 rows here / global, doubles
     // all-reduced per setup / application, doubles exchanged per setup / application, bytes of
-    // the replicated hierarchy
+    // the replicated hierarchy, block rows of the replicated level
     for (size_t r = 0; r < cst.size(); ++r)
     {
       std::printf("coupled AMG rank %zu:", r);

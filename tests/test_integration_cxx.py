@@ -42,7 +42,7 @@ NATIVE = os.path.join(CXX, "_build", "config3_native")
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,ranks,dist", [(8, 2, "auto"), (40, 2, "auto"), (32, 4, "auto"), (40, 2, "1"),
-                                          (32, 4, "1")])
+                                          (32, 4, "1"), (40, 2, "deep"), (32, 4, "deep")])
 def test_config3_native_cxx_host(n, ranks, dist):
     """BASELINE config 3's problem (hex27 StVK TotLag cube, x- clamped, traction -1 on x+) solved by
     a C++ host through the C ABI alone (tests/cxx/config3_native.cpp): Newton with fcg_dfcg_solve
@@ -50,11 +50,15 @@ def test_config3_native_cxx_host(n, ranks, dist):
     ranks converge quadratically to the same displacement by DOF GID (n = 40: config 3 at 40^3)
     within 1.5x the 1-rank FCG iterations.  dist "1": the AMG's level 1 distributed across the
     ranks (FCG_AMG_DIST=1; the host transport's exchange_fn) -- each rank then stores only its own
-    level-1 rows and all-reduces only level 2."""
+    level-1 rows and all-reduces only level 2.  dist "deep": every coarser level that still shrinks
+    distributed too (FCG_AMG_DIST_MIN=0) -- at least two distributed levels, a replicated level
+    smaller than level 2, the same 1.5x iteration bound."""
     if not os.path.exists(NATIVE):
         subprocess.run(["make", "-s", "-C", CXX], check=True)
     env = dict(os.environ)
-    if dist != "auto":
+    if dist == "deep":
+        env.update(FCG_AMG_DIST="1", FCG_AMG_DIST_MIN="0")
+    elif dist != "auto":
         env["FCG_AMG_DIST"] = dist
     p = subprocess.run([NATIVE, str(n), str(ranks)], capture_output=True, text=True, timeout=600, env=env)
     assert p.returncode == 0, p.stdout + p.stderr
@@ -62,6 +66,12 @@ def test_config3_native_cxx_host(n, ranks, dist):
     stats = [[int(v) for v in line.split(":")[1].split()] for line in p.stdout.splitlines()
              if line.startswith("coupled AMG rank")]
     assert len(stats) == ranks, p.stdout
+    print(p.stdout)
+    if dist == "deep":
+        glob = stats[0][2]
+        assert all(st[0] >= 2 and st[0] == stats[0][0] for st in stats), p.stdout
+        assert sum(st[1] for st in stats) == glob, p.stdout
+        assert all(st[8] * 6 == st[4] for st in stats), p.stdout  # the replicated level all-reduced
     if dist == "1":
         glob = stats[0][2]
         assert all(st[0] == 1 for st in stats), p.stdout
