@@ -682,6 +682,8 @@ __global__ __launch_bounds__(256, KIN ? 1 : FCG_SWEEP_WGS) void sweep_h8_kernel(
       dof_nxt[j] = dof_nn[j];
     }
     store_rec(L + 2, rec_nxt);
+#ifdef FCG_SWEEP_COMMIT_STAMP
+    // diagnostic builds only (it costs the fused TSI pass a spill)
     if (A.stamps)
     {
       // phase 2: the commit's wait for plane L+2's loads (and, behind them in vmcnt, the previous
@@ -689,6 +691,7 @@ __global__ __launch_bounds__(256, KIN ? 1 : FCG_SWEEP_WGS) void sweep_h8_kernel(
       __asm__ volatile("" ::"v"(rec_nxt[0]), "v"(node_nxt[0]));
       FCG_STAMP(2);
     }
+#endif
 
     // B. visit stage
     const bool wl = L >= kz0, wl1 = L + 1 < kz1;
@@ -848,6 +851,12 @@ __global__ __launch_bounds__(256, KIN ? 1 : FCG_SWEEP_WGS) void sweep_h8_kernel(
           // node start at base / 3 (length len / 3), its k_TS row at base / 3, its k_TT row at
           // base / 9; the neighbour's thermo column sits at pos / 3, its displacements at pos
           const int64_t bst = base / 3, lst = len / 3, pst = pos / 3;
+#ifdef FCG_PROBE_TSI_STORE_INTERLEAVED
+          if constexpr (true)  // timing probe: the order before round 6
+#else
+          if constexpr (false)
+#endif
+          {
 #pragma unroll
           for (int r = 0; r < 3; ++r)
           {
@@ -863,6 +872,31 @@ __global__ __launch_bounds__(256, KIN ? 1 : FCG_SWEEP_WGS) void sweep_h8_kernel(
               *d1 += Tv[r];
               *d2 += Tv[3 + r];
             }
+          }
+          }
+          else
+          {
+          // k_TS's three adjacent values first, with no k_ST store between them (the two arrays
+          // may alias as far as the compiler knows), so that they leave as one 16-byte and one
+          // 8-byte store instead of three 8-byte stores
+          double* d2 = A.Kts + bst + pos;
+#pragma unroll
+          for (int r = 0; r < 3; ++r)
+          {
+            if (OVERWRITE)
+              d2[r] = Tv[3 + r];
+            else
+              d2[r] += Tv[3 + r];
+          }
+#pragma unroll
+          for (int r = 0; r < 3; ++r)
+          {
+            double* d1 = A.Kst + bst + r * lst + pst;
+            if (OVERWRITE)
+              *d1 = Tv[r];
+            else
+              *d1 += Tv[r];
+          }
           }
           double* d3 = A.Ktt + base / 9 + pst;
           if (OVERWRITE)

@@ -9,7 +9,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 fcg = importlib.import_module("4c_amd").fcg
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 100
 dev = torch.device("cuda:0")
-names = ["elements", "visits", "commit"]
+names = ["elements", "visits", "commit"]  # commit: builds with -DFCG_SWEEP_COMMIT_STAMP
 for kin in (fcg.LINEAR, fcg.TOTLAG):
     m = fcg.BoxMesh(fcg.HEX8, (n, n, n), jitter=0.1)
     u = torch.from_numpy(m.u_col(1e-3)).to(dev)
