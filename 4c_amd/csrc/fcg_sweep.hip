@@ -918,7 +918,15 @@ __global__ __launch_bounds__(256, KIN ? 1 : FCG_SWEEP_WGS) void sweep_h8_kernel(
         nm_pre[0] = sh.neg[slot_of(vis0)];
         nm_pre[1] = sh.neg[slot_of(vis1)];
       }
-#pragma unroll 1
+      // the two visits unrolled where the registers allow it (the structural linear passes: 254
+      // VGPRs, no spills; the next visit's loads then overlap the first one's emit, -3 % on the
+      // headline kernel, profiles/r06/r06_sweep_visit_unroll_ab.txt); the TSI passes spill
+      // unrolled, and the TotLag ones keep the rolled loop (FCG_SWEEP_VISIT_UNROLL=0/1 overrides)
+#ifndef FCG_SWEEP_VISIT_UNROLL
+#define FCG_SWEEP_VISIT_UNROLL (!TSI && KIN == 0)
+#endif
+      constexpr int kVisitUnroll = (FCG_SWEEP_VISIT_UNROLL) ? 2 : 1;
+#pragma unroll kVisitUnroll
       for (int v = 0; v < 2; ++v)
       {
         const uint32_t w = v == 0 ? vis0 : vis1;
