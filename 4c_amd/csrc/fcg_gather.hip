@@ -448,7 +448,12 @@ __global__ __launch_bounds__(64, 2) void gather_h8_kernel(GatherArgs A)
       if (KIN == 1)
 #pragma unroll
         for (int k = 0; k < 6; ++k) H[k] = 0.0;
-#pragma unroll 4
+      // the 8 Gauss points fully unrolled (was 4: renumbered 1M box linear -1.8 %, TotLag -8 %, the
+      // same two waves per SIMD and no spills; profiles/r06/r06_gather_g_unroll_ab.txt)
+#ifndef FCG_GATHER_G_UNROLL
+#define FCG_GATHER_G_UNROLL 8
+#endif
+#pragma unroll FCG_GATHER_G_UNROLL
       for (int g = 0; g < 8; ++g)
       {
         const double* P = sh.GP(j, g);
