@@ -46,31 +46,46 @@ constexpr int kMaxRow = 81;  // hex8 node rows: 27 neighbour triples (fcg_create
 // LDS of one wave, one flat array with stage-dependent views (one wave per workgroup: its LDS
 // accesses are processed in program order, so a region is reused without a barrier between its
 // last read and the next write):
-//   linear:  [X | GP] (192) | C (192) | [NX (1600) | blk (585) + row (243) at 600]
-//   TotLag:  [X (384) + C (384) at 384 | GP (1600) | blk (585) + row (243) at 600]
+//   linear:  [X | GP] (192) | C (192) | [NX (1600) | blk (650) + row (243) at 656]
+//   TotLag:  [X (384) + C (384) at 384 | GP (1728) | blk (650) + row (243) at 656]
 // (TotLag forms its stage-3 terms from dN_b(xi_g) directly, with the Gauss point's J^-1 folded into
 // per-point 3 x 3 factors, instead of keeping NX: 13 KB instead of 31 KB.)  A node with more records (MULTI) keeps its row image in its own array.
 // Strides make every access pattern of the stages free of bank conflicts within each 32-lane group
 // (ds_read_b64 / ds_write_b64, bank = (address / 4) mod 64): per slot 24 (X, C), 200 (NX), 24 or
-// 200 (GP); per Gauss point 25 (NX), 3 or 25 (GP); per node 3.
+// 216 (GP); per Gauss point 25 (NX), 3 or 26 (GP); per node 3; per block 10 (blk).
+// TotLag's GP records and the blocks are 16-byte aligned, so that the compiler reads them as
+// ds_read_b128 (4 LDS cycles per 16 bytes) instead of pairing two entries into a ds_read2_b64 (8
+// cycles): renumbered 1M hex8 TotLag -4 %, linear -2.4 % (profiles/r06/r06_gather_lds_align_ab.txt).
+// GP stride 26 / slot stride 216 keep the b128 reads (8 lanes of a slot broadcast, 4 slots per lane
+// group at banks 0 / 48 / 32 / 16) and the stage-2 b128 stores (one slot's 8 points) conflict-free.
 template <int KIN, bool MULTI>
 struct GatherShared {
   static constexpr int kNs = KIN ? 2 : 1;
-  static constexpr int kGp = KIN ? 25 : 3;  // per (slot, GP): fac a | TotLag: fac F a, J^-T fac S a, F J^-T, F F^T, J^-T fac a
+#ifdef FCG_GATHER_TL_ODD
+  static constexpr int kGp = KIN ? 25 : 3;  // A/B probe: the round-5 strides (ds_read2_b64 pairs)
   static constexpr int kGpSlot = KIN ? 200 : 24;
+#else
+  static constexpr int kGp = KIN ? 26 : 3;  // per (slot, GP): fac a | TotLag: fac F a, J^-T fac S a, F J^-T, F F^T, J^-T fac a
+  static constexpr int kGpSlot = KIN ? 216 : 24;
+#endif
   static constexpr int kX = 0, kC = KIN ? 384 : 192, kGpOff = 0;
   static constexpr int kNX = KIN ? 0 : 384, kBlk = KIN ? 0 : 384, kRow = kBlk + 600;
-  static constexpr int kSize = KIN ? 8 * 200 : 384 + 1600;
-  double u[kSize];
+  static constexpr int kSize = KIN ? 8 * kGpSlot : 384 + 1600;
+  alignas(16) double u[kSize];
   double row_m[MULTI ? 3 * kMaxRow : 1];  // MULTI: the row image lives across records
-  double gp[8][4];                        // Gauss point coordinates | weight
+  alignas(16) double gp[8][4];            // Gauss point coordinates | weight
   uint32_t tmap[32];                      // triple t: element node b of slot s in nibble s, 8 = none
   __device__ double* X(int s, int j) { return u + kX + 192 * s + 24 * j; }
   __device__ double* C(int s, int j) { return u + kC + 192 * s + 24 * j; }
   __device__ double* GP(int j, int g) { return u + kGpOff + kGpSlot * j + kGp * g; }
   __device__ double* NX(int j, int g) { return u + kNX + 200 * j + 25 * g; }  // linear only
-  __device__ double* blk(int l) { return u + kBlk + 9 * l; }
-  __device__ double* row() { return MULTI ? row_m : u + kRow; }
+#ifdef FCG_GATHER_BLK9
+  static constexpr int kBs = 9;  // A/B probe: the round-5 block stride (ds_read2_b64 pairs)
+#else
+  static constexpr int kBs = 10;  // block stride: entry pairs (2p, 2p + 1) 16-byte aligned
+#endif
+  __device__ double* blk(int l) { return u + kBlk + kBs * l; }
+  __device__ double* row() { return MULTI ? row_m : u + kRow + (kBs - 9) * 56; }
 };
 
 struct GatherArgs {
@@ -551,16 +566,50 @@ __global__ __launch_bounds__(64, 2) void gather_h8_kernel(GatherArgs A)
         for (int sl = 0; sl < 8; ++sl)
         {
           const uint32_t b = (tm >> (4 * sl)) & 15u;
-          off[sl] = 9 * (b < 8u ? 8 * sl + int(b) : 64);
+          off[sl] = Sh::kBs * (b < 8u ? 8 * sl + int(b) : 64);
         }
         const double* blk = sh.blk(0);
+#ifndef FCG_GATHER_BLK9
+        // h = 0: entries 0, 1, 4, 5, 8; h = 1: entries 2, 3, 6, 7, 8 (both lanes write entry 8: the
+        // same value to the same address).  Each pair (2p, 2p + 1) is one 16-byte LDS read per slot
+        // instead of two entries 2 apart, which the compiler paired into a ds_read2_b64 (8 LDS cycles
+        // per 16 bytes against 4 for a ds_read_b128)
+        double xs[5];
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+        {
+          const int c0 = 4 * p + 2 * h;
+          double2 v = *reinterpret_cast<const double2*>(blk + off[0] + c0);
+          double x0 = v.x, x1 = v.y;
+#pragma unroll
+          for (int sl = 1; sl < 8; ++sl)
+          {
+            v = *reinterpret_cast<const double2*>(blk + off[sl] + c0);
+            x0 += v.x;
+            x1 += v.y;
+          }
+          xs[2 * p] = x0;
+          xs[2 * p + 1] = x1;
+        }
+        {
+          double x = blk[off[0] + 8];
+#pragma unroll
+          for (int sl = 1; sl < 8; ++sl) x += blk[off[sl] + 8];
+          xs[4] = x;
+        }
+#endif
 #pragma unroll
         for (int e5 = 0; e5 < 5; ++e5)
         {
+#ifdef FCG_GATHER_BLK9
           const int c = h ? min(2 * e5 + 1, 7) : 2 * e5;  // h = 1: entries 1, 3, 5, 7, 7
           double x = blk[off[0] + c];
 #pragma unroll
           for (int sl = 1; sl < 8; ++sl) x += blk[off[sl] + c];
+#else
+          const int c = e5 == 4 ? 8 : 4 * (e5 >> 1) + 2 * h + (e5 & 1);
+          const double x = xs[e5];
+#endif
           const int rr = c % 3, cc = c / 3;
           const int v = rr * len + 3 * t + cc;
           if (MULTI)
