@@ -105,15 +105,44 @@ __device__ inline double inv3(double* m)
 // wave 3 produces element s (its Jacobians in J | Gu, its per-point factors into gpf[s & 1]) while
 // waves 0-2 consume element s - 1 from gpf[(s - 1) & 1] into the K image.  Per-point factors:
 // T | W | V | M | R (offsets below) and fac.
-constexpr int OFF_T = 0, OFF_W = 243, OFF_V = 405, OFF_M = 567, OFF_R = 729, GPF = 972;
+// Layouts of the factor buffers and of the dN table (TotLag; linear kinematics keep the round-5
+// layouts, which measured 7-10 % faster for them: profiles/r06/r06_h27_lds_align_ab.txt).
+// T and R take kTs doubles per Gauss point: 10 (9 + a pad) keeps every point's 3 x 3 factor and
+// every buffer 16-byte aligned, so that the consumers read them as ds_read_b128 pieces instead of
+// ds_read2_b64 pairs (8 LDS cycles per 16 bytes against 4).  dN_c(xi_g): node c's 3 derivatives at
+// 4 c + 2 (c >> 3) of its Gauss point's 114-double row (16-byte aligned; nodes c and c + 8 on
+// different banks, so that 16 lanes reading 16 nodes' first two derivatives as one ds_read_b128
+// each do not conflict).  FCG_H27_GPF9 / FCG_H27_DN3: the round-5 layouts for TotLag too (A/B).
+template <int KIN>
+struct H27Layout {
+#ifdef FCG_H27_GPF9
+  static constexpr int kTs = 9;
+#else
+  static constexpr int kTs = KIN ? 10 : 9;
+#endif
+  static constexpr int OFF_T = 0, OFF_W = 27 * kTs, OFF_V = OFF_W + 162, OFF_M = OFF_V + 162,
+                       OFF_R = OFF_M + 162, GPF = OFF_R + 27 * kTs;
+#ifdef FCG_H27_DN3
+  static constexpr bool kDnPad = false;
+#else
+  static constexpr bool kDnPad = KIN == 1;
+#endif
+  static constexpr int kDnG = kDnPad ? 114 : 81;
+  __device__ __host__ static constexpr int dn_off(int g, int c)
+  {
+    return kDnPad ? 114 * g + 4 * c + 2 * (c >> 3) : 81 * g + 3 * c;
+  }
+};
 constexpr int kRowImg = 3 * 375;  // one row node's 3 CSR rows (hex27 rows hold <= 375 columns)
+template <int KIN>
 struct H27Shared {
-  double dN[27 * 27 * 3];       // [g][c][d], loaded once per workgroup
+  using L = H27Layout<KIN>;
+  alignas(16) double dN[27 * L::kDnG];  // dN_c,d(xi_g) at dn_off(g, c) + d, loaded once per workgroup
   union {
     struct {
       double X[81], U[81];          // the produced element's coordinates and displacements
       double J[243], Gu[243];       // producer scratch: J, du/dxi per Gauss point
-      double gpf[2][GPF];           // per-point factors of the produced / consumed element
+      alignas(16) double gpf[2][L::GPF];           // per-point factors of the produced / consumed element
       double fac[2][27];
       alignas(16) double kimg[kNpair * 9];  // consumed element's blocks a <= b (col-major 3 x 3)
     };
@@ -135,11 +164,11 @@ struct H27Shared {
   uint8_t loc[27], latnode[27];
   int32_t qitem[2];             // ASM 3: work items claimed from the queue (look-ahead slots)
   // views of gpf[b]: T(i, k) at 3i + k, W, V, M symmetric (xx yy zz xy yz zx), R(i, k) at 3i + k
-  __device__ double* T(int b) { return gpf[b] + OFF_T; }
-  __device__ double* W(int b) { return gpf[b] + OFF_W; }
-  __device__ double* V(int b) { return gpf[b] + OFF_V; }
-  __device__ double* M(int b) { return gpf[b] + OFF_M; }
-  __device__ double* R(int b) { return gpf[b] + OFF_R; }
+  __device__ double* T(int b) { return gpf[b] + L::OFF_T; }
+  __device__ double* W(int b) { return gpf[b] + L::OFF_W; }
+  __device__ double* V(int b) { return gpf[b] + L::OFF_V; }
+  __device__ double* M(int b) { return gpf[b] + L::OFF_M; }
+  __device__ double* R(int b) { return gpf[b] + L::OFF_R; }
 };
 
 struct H27Args {
@@ -410,10 +439,11 @@ template <int KIN, int ASM>
 __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
 {
   constexpr bool PEN = ASM == 1 || ASM == 2, OVL = ASM == 3;
-  __shared__ H27Shared sh;
+  __shared__ H27Shared<KIN> sh;
+  using L = H27Layout<KIN>;
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
-  for (int v = tid; v < 27 * 27 * 3; v += kBlk) sh.dN[v] = c_dN[v];
+  for (int v = tid; v < 27 * 27 * 3; v += kBlk) sh.dN[L::dn_off(v / 81, (v % 81) / 3) + v % 3] = c_dN[v];
   if (PEN)
     for (int v = tid; v < 27 * 27; v += kBlk)
     {
@@ -535,15 +565,16 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
       const int g = t / 6, rem = t - 6 * (t / 6);
       const int k = rem % 3, sx = rem / 3;
       const double* src = sx ? sh.U : sh.X;
-      const double* d = sh.dN + 81 * g;
+      const int gdn = g;
       double j0 = 0.0, j1 = 0.0, j2 = 0.0;
 #pragma unroll 9
       for (int c = 0; c < kNpe; ++c)
       {
         const double x = src[3 * c + k];
-        j0 += d[3 * c + 0] * x;
-        j1 += d[3 * c + 1] * x;
-        j2 += d[3 * c + 2] * x;
+        const double* d = sh.dN + L::dn_off(gdn, c);
+        j0 += d[0] * x;
+        j1 += d[1] * x;
+        j2 += d[2] * x;
       }
       double* dst = (sx ? sh.Gu : sh.J) + 9 * g + 3 * k;
       dst[0] = j0;
@@ -588,8 +619,8 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
 #pragma unroll 3
       for (int g = 0; g < kNpe; ++g)
       {
-        const double* R = sh.R(fb) + 9 * g;
-        const double* d = sh.dN + 3 * (27 * g + a);
+        const double* R = sh.R(fb) + L::kTs * g;
+        const double* d = sh.dN + L::dn_off(g, a);
         const double d0 = d[0], d1 = d[1], d2 = d[2];
         f0 += R[0] * d0 + R[1] * d1 + R[2] * d2;
         f1 += R[3] * d0 + R[4] * d1 + R[5] * d2;
@@ -887,8 +918,8 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
 #pragma unroll
               for (int k = 0; k < 3; ++k)
               {
-                sh.T(pb)[9 * g + 3 * i + k] = F[i][0] * iJ[3 * k] + F[i][1] * iJ[3 * k + 1] + F[i][2] * iJ[3 * k + 2];
-                sh.R(pb)[9 * g + 3 * i + k] =
+                sh.T(pb)[L::kTs * g + 3 * i + k] = F[i][0] * iJ[3 * k] + F[i][1] * iJ[3 * k + 1] + F[i][2] * iJ[3 * k + 2];
+                sh.R(pb)[L::kTs * g + 3 * i + k] =
                     fac * (FS[i][0] * iJ[3 * k] + FS[i][1] * iJ[3 * k + 1] + FS[i][2] * iJ[3 * k + 2]);
               }
             if (KIN == 1)
@@ -951,13 +982,13 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
 #pragma unroll FCG_H27_HUNROLL
           for (int g = 0; g < kNpe; ++g)
           {
-            const double* da = sh.dN + 3 * (27 * g + a_c);
+            const double* da = sh.dN + L::dn_off(g, a_c);
             const double* Wg = sh.W(cb) + 6 * g;
             const double* Vg = sh.V(cb) + 6 * g;
             const double d0 = da[0], d1 = da[1], d2 = da[2];
             const double av = (Wg[wr0] * d0 + Wg[wr1] * d1 + Wg[wr2] * d2) * ma;
             const double avv = (Vg[wr0] * d0 + Vg[wr1] * d1 + Vg[wr2] * d2) * ma;
-            const double bv = sh.dN[3 * (27 * g + b_c) + kc] * mb;
+            const double bv = sh.dN[L::dn_off(g, b_c) + kc] * mb;
             const f64x4_t c = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, zero4, 0, 0, 0);
             Geo = __builtin_amdgcn_mfma_f64_16x16x4f64(avv, bv, Geo, 0, 0, 0);
             const double* Mg = sh.M(cb) + 6 * g;
@@ -1000,9 +1031,9 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
           const int gc = vg ? g : 0;
           const double fg = sh.fac[cb][gc] * ((vg && va) ? 1.0 : 0.0);
           const double mb = (vg && vb) ? 1.0 : 0.0;
-          const double* T = sh.T(cb) + 9 * gc;
-          const double* da = sh.dN + 3 * (27 * gc + a_c);
-          const double* db = sh.dN + 3 * (27 * gc + b_c);
+          const double* T = sh.T(cb) + L::kTs * gc;
+          const double* da = sh.dN + L::dn_off(gc, a_c);
+          const double* db = sh.dN + L::dn_off(gc, b_c);
           const double a0 = da[0], a1 = da[1], a2 = da[2], b0 = db[0], b1 = db[1], b2 = db[2];
           double av[3], bv[3];
 #pragma unroll
@@ -1577,9 +1608,27 @@ __global__ __launch_bounds__(BT, BT == 64 ? 2 : 2) void h27_apply_sf_kernel(H27A
       __syncthreads();
   };
   constexpr int NSRC = KIN == 0 ? 2 : 3;  // X | x (linear) or X | u | x
+#ifdef FCG_H27_APPLY_OLD
+  // A/B probe: the round-5 layouts (node-major values, Q[g][3 x 3], 9 NSRC doubles per point),
+  // read as ds_read2_b64 pairs
   constexpr int NND = 81 * NSRC > 243 ? 81 * NSRC : 243;
-  __shared__ double nq[NE][NND];               // nodal X | (u) | x, then Q[g][9]
-  __shared__ double gr[NE][27][NSRC][3][3];     // d(src)_k / dxi_d at point l: [l][src][k][d]
+  constexpr int kGs = 9 * NSRC, kSs = 9;
+  auto nv = [](int src, int k, int l) { return 81 * src + 3 * l + k; };  // nodal value
+  auto qv = [](int g, int i, int k) { return 9 * g + 3 * i + k; };        // Q_ik at point g
+#else
+  // component-major: the 27 nodal values of one (source, component) and the 27 points' Q_ik are
+  // contiguous and 16-byte aligned rows of 28, and a point's gradients take 30 doubles (TotLag), so
+  // that the phases read ds_read_b128 pieces (4 LDS cycles per 16 bytes) instead of ds_read2_b64
+  // pairs (8) -- conflict-free for the lane groups of each phase
+  constexpr int NND = 252;
+  // (sources 10 apart, every 3 x 3 block 16-byte aligned with 22 / 30 per point: 2 % slower for
+  // TotLag, linear the same; profiles/r06/r06_h27_lds_align_ab.txt)
+  constexpr int kGs = NSRC == 3 ? 30 : 18, kSs = 9;
+  auto nv = [](int src, int k, int l) { return 84 * src + 28 * k + l; };
+  auto qv = [](int g, int i, int k) { return 28 * (3 * i + k) + g; };
+#endif
+  __shared__ alignas(16) double nq[NE][NND];      // nodal X | (u) | x, then Q
+  __shared__ alignas(16) double gr[NE][27 * kGs];  // d(src)_k / dxi_d at point l: l kGs + kSs src + 3 k + d
   __shared__ double tL[9], tdL[9], wl[27];
   __shared__ uint8_t lat[27], posl[27];  // lattice position -> node (= point) number, and back
   __shared__ int32_t incs[NE][27];        // the pass's incidences of (element, node), -1 = unowned
@@ -1674,7 +1723,7 @@ __global__ __launch_bounds__(BT, BT == 64 ? 2 : 2) void h27_apply_sf_kernel(H27A
       {
         const int sl = t / (81 * NSRC), r = t - 81 * NSRC * sl;
         const int src = r / 81, rr = r - 81 * src, a = rr / 3;
-        nq[sl][81 * src + 3 * posl[a] + rr - 3 * a] = pre[q];
+        nq[sl][nv(src, rr - 3 * a, posl[a])] = pre[q];
       }
     }
     if (tid < 27 * NE) incs[tid / 27][tid - 27 * (tid / 27)] = incp;
@@ -1711,17 +1760,17 @@ __global__ __launch_bounds__(BT, BT == 64 ? 2 : 2) void h27_apply_sf_kernel(H27A
 #pragma unroll
       for (int j = 0; j < 9; ++j)
         __asm__ volatile("" : "+v"(f0[j]), "+v"(f1[j]), "+v"(f2[j]));  // rebuilt per pass, not kept live
-      const double* v = nq[sg] + 81 * src;
 #pragma unroll 1
       for (int k = 0; k < 3; ++k)
       {
+        const double* v = nq[sg] + nv(src, k, 0);
         double w0[3] = {0.0, 0.0, 0.0}, w1[3] = {0.0, 0.0, 0.0}, w2[3] = {0.0, 0.0, 0.0};
 #pragma unroll
         for (int j = 0; j < 9; ++j)
 #pragma unroll
           for (int i0 = 0; i0 < 3; ++i0)
           {
-            const double x = v[3 * (i0 + 3 * j) + k];
+            const double x = v[nv(0, 0, i0 + 3 * j)];
             w0[i0] += f0[j] * x;
             w1[i0] += f1[j] * x;
             w2[i0] += f2[j] * x;
@@ -1729,7 +1778,7 @@ __global__ __launch_bounds__(BT, BT == 64 ? 2 : 2) void h27_apply_sf_kernel(H27A
 #pragma unroll
         for (int m0 = 0; m0 < 3; ++m0)
         {
-          double* o = &gr[sg][m0 + 3 * line][src][k][0];
+          double* o = gr[sg] + kGs * (m0 + 3 * line) + kSs * src + 3 * k;
           o[0] = dlx[m0][0] * w0[0] + dlx[m0][1] * w0[1] + dlx[m0][2] * w0[2];
           o[1] = lx[m0][0] * w1[0] + lx[m0][1] * w1[1] + lx[m0][2] * w1[2];
           o[2] = lx[m0][0] * w2[0] + lx[m0][1] * w2[1] + lx[m0][2] * w2[2];
@@ -1741,12 +1790,12 @@ __global__ __launch_bounds__(BT, BT == 64 ? 2 : 2) void h27_apply_sf_kernel(H27A
     if (s27 < NE && e0 + s27 < A.n_ele)
     {
       const int g = r27;  // lattice position of the point
-      const double* G = &gr[s27][g][0][0][0];
+      const double* G = gr[s27] + kGs * g;
       double iJ[9];
 #pragma unroll
       for (int q = 0; q < 9; ++q) iJ[q] = G[q];  // [k][d] row-major = J[d + 3k] col-major
       const double fac = inv3(iJ) * wl[g];
-      const double* Gx = G + 9 * (NSRC - 1);
+      const double* Gx = G + kSs * (NSRC - 1);
       double Hx[3][3], F[3][3];
 #pragma unroll
       for (int i = 0; i < 3; ++i)
@@ -1755,7 +1804,7 @@ __global__ __launch_bounds__(BT, BT == 64 ? 2 : 2) void h27_apply_sf_kernel(H27A
         {
           Hx[i][j] = iJ[j] * Gx[3 * i] + iJ[j + 3] * Gx[3 * i + 1] + iJ[j + 6] * Gx[3 * i + 2];
           F[i][j] = KIN == 0 ? 0.0
-                             : iJ[j] * G[9 + 3 * i] + iJ[j + 3] * G[9 + 3 * i + 1] + iJ[j + 6] * G[9 + 3 * i + 2];
+                             : iJ[j] * G[kSs + 3 * i] + iJ[j + 3] * G[kSs + 3 * i + 1] + iJ[j + 6] * G[kSs + 3 * i + 2];
         }
       double P[3][3];
       auto cmat = [&](const double* ev, double Sm[3][3]) {
@@ -1804,12 +1853,12 @@ __global__ __launch_bounds__(BT, BT == 64 ? 2 : 2) void h27_apply_sf_kernel(H27A
             P[i][j] = fac * (F[i][0] * dS[0][j] + F[i][1] * dS[1][j] + F[i][2] * dS[2][j] +
                              Hx[i][0] * S[0][j] + Hx[i][1] * S[1][j] + Hx[i][2] * S[2][j]);
       }
-      double* Q = nq[s27] + 9 * g;  // the nodal values are dead: the gradients are in gr
+      double* Q = nq[s27];  // the nodal values are dead: the gradients are in gr
 #pragma unroll
       for (int i = 0; i < 3; ++i)
 #pragma unroll
         for (int k = 0; k < 3; ++k)
-          Q[3 * i + k] = P[i][0] * iJ[3 * k] + P[i][1] * iJ[3 * k + 1] + P[i][2] * iJ[3 * k + 2];
+          Q[qv(g, i, k)] = P[i][0] * iJ[3 * k] + P[i][1] * iJ[3 * k + 1] + P[i][2] * iJ[3 * k + 2];
     }
     phase_sync();
     // ---- node lines: lanes (s27, line (a1, a2), component i)
@@ -1831,9 +1880,9 @@ __global__ __launch_bounds__(BT, BT == 64 ? 2 : 2) void h27_apply_sf_kernel(H27A
 #pragma unroll
           for (int m0 = 0; m0 < 3; ++m0)
           {
-            const double* q = Q + 9 * (m0 + 3 * m1 + 9 * m2) + 3 * i;
-            z0[m0] += c0 * q[0];
-            z12[m0] += c1 * q[1] + c2 * q[2];
+            const int m = m0 + 3 * m1 + 9 * m2;
+            z0[m0] += c0 * Q[qv(m, i, 0)];
+            z12[m0] += c1 * Q[qv(m, i, 1)] + c2 * Q[qv(m, i, 2)];
           }
         }
 #pragma unroll
