@@ -76,7 +76,14 @@ struct GatherShared {
   alignas(16) double gp[8][4];            // Gauss point coordinates | weight
   uint32_t tmap[32];                      // triple t: element node b of slot s in nibble s, 8 = none
   __device__ double* X(int s, int j) { return u + kX + 192 * s + 24 * j; }
-  __device__ double* C(int s, int j) { return u + kC + 192 * s + 24 * j; }
+  // C one double in (TotLag): the Jacobian reads c[3..23] then start 16-byte aligned and pair as
+  // ds_read_b128 instead of ds_read2_b64 (c[0], never read, moves into the pad; FCG_GATHER_C0 = A/B)
+#ifdef FCG_GATHER_C0
+  static constexpr int kCo = 0;
+#else
+  static constexpr int kCo = KIN ? 1 : 0;
+#endif
+  __device__ double* C(int s, int j) { return u + kC + 192 * s + 24 * j + kCo; }
   __device__ double* GP(int j, int g) { return u + kGpOff + kGpSlot * j + kGp * g; }
   __device__ double* NX(int j, int g) { return u + kNX + 200 * j + 25 * g; }  // linear only
 #ifdef FCG_GATHER_BLK9
