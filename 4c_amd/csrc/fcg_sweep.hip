@@ -127,14 +127,28 @@ struct SweepShared {
 #ifdef FCG_PROBE_WG3
   double hold[1][9][TSI ? (TH ? 9 : 18) : 9];  // timing probe only: one column's buffer for all
 #else
-  double hold[TX * TY][9][TSI ? (TH ? 9 : 18) : 9];
+  // structural rows 10 apart (16-byte aligned: the 9 held entries as 4 ds_read_b128 + 1
+  // ds_read_b64 and 4 ds_write_b128 + 1 ds_write_b64 instead of ds_read2_b64 / ds_write2_b64
+  // pairs): headline -0.1 to -0.6 %, TotLag -0.9 % (profiles/r06/r06_sweep_hold10_ab.txt);
+  // FCG_HOLD9 = the round-5 rows (A/B)
+#if defined(FCG_HOLD9)
+  static constexpr int kHs = 9;
+#else
+  static constexpr int kHs = 10;
+#endif
+  alignas(16) double hold[TX * TY][9][TSI ? (TH ? 9 : 18) : kHs];
 #endif
   // DEFER (rows not in lattice order): the blocks of node plane L+1's rows with the plane below
   // (dz = -1, finished in layer L) wait here and are written in layer L+1 beside the row's other
   // blocks, so that each row's cache lines are filled within one layer.  Slot (column, t) belongs
   // to the one lane that emits block t of that column every layer: it reads the held block
   // before it holds the next one (a wavefront's LDS operations execute in order), one buffer.
-  double hold_lo[DEFER ? TX * TY : 1][9][9];
+#ifdef FCG_HOLDLO9
+  double hold_lo[DEFER ? TX * TY : 1][9][9];  // A/B probe: the round-5 rows
+#else
+  // rows 10 apart, 16-byte aligned as hold: renumbered 1M box through AUTO 1.149 -> 1.085 ms
+  alignas(16) double hold_lo[DEFER ? TX * TY : 1][9][10];
+#endif
 };
 
 __device__ inline int ring(int p) { return (p % 3 + 3) % 3; }
