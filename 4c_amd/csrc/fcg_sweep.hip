@@ -136,6 +136,8 @@ struct SweepShared {
 #else
   static constexpr int kHs = 10;
 #endif
+  // (the thermal pass's 7 held values keep rows of 9: aligned rows of 10 measured +0.3 % on the
+  // two-field tangent, r06_sweep_hold10_ab.txt)
   alignas(16) double hold[TX * TY][9][TSI ? (TH ? 9 : 18) : kHs];
 #endif
   // DEFER (rows not in lattice order): the blocks of node plane L+1's rows with the plane below
