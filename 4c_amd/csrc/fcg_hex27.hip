@@ -128,6 +128,13 @@ struct H27Layout {
   static constexpr bool kDnPad = KIN == 1;
 #endif
   static constexpr int kDnG = kDnPad ? 114 : 81;
+  // K image blocks (a <= b), kKs doubles each: 10 for TotLag (16-byte aligned, the record phase
+  // reads a block as 4 ds_read_b128 + 1 ds_read_b64); FCG_H27_KIMG9 = rows of 9 (A/B)
+#ifdef FCG_H27_KIMG9
+  static constexpr int kKs = 9;
+#else
+  static constexpr int kKs = KIN ? 10 : 9;
+#endif
   __device__ __host__ static constexpr int dn_off(int g, int c)
   {
     return kDnPad ? 114 * g + 4 * c + 2 * (c >> 3) : 81 * g + 3 * c;
@@ -144,7 +151,7 @@ struct H27Shared {
       double J[243], Gu[243];       // producer scratch: J, du/dxi per Gauss point
       alignas(16) double gpf[2][L::GPF];           // per-point factors of the produced / consumed element
       double fac[2][27];
-      alignas(16) double kimg[kNpair * 9];  // consumed element's blocks a <= b (col-major 3 x 3)
+      alignas(16) double kimg[kNpair * L::kKs];  // consumed element's blocks a <= b (col-major 3 x 3)
     };
     // overlapped schedule (ASM 3): the row images of the four waves' row nodes, used only while
     // the element pipeline is drained
@@ -1006,7 +1013,7 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
             const int a = 16 * at + kq + 4 * r;
             if (a < 27 && b < 27 && a <= b)
             {
-              double* K = sh.kimg + 9 * pidx(a, b);
+              double* K = sh.kimg + L::kKs * pidx(a, b);
               const double geo = Geo[r];
               K[0] = mu * Hm[0][r] + geo;
               K[4] = mu * Hm[1][r] + geo;
@@ -1059,7 +1066,7 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
           const int a = 16 * at + kq + 4 * r;
           if (a < 27 && b < 27 && a <= b)
           {
-            double* K = sh.kimg + 9 * pidx(a, b);
+            double* K = sh.kimg + L::kKs * pidx(a, b);
             double add[9];
             if (KIN == 0)
             {
@@ -1120,7 +1127,7 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
               const int b = sh.latnode[c / 3], j = c - 3 * (c / 3);
               addr[k] = sh.rbase[cb][a] + int64_t(i * sh.rlen[cb][a] + sh.ipos[cb][kNpe * a + b] + j);
               const bool up = a <= b;
-              val[k] = sh.kimg[9 * (up ? pidx(a, b) : pidx(b, a)) + (up ? i + 3 * j : j + 3 * i)];
+              val[k] = sh.kimg[L::kKs * (up ? pidx(a, b) : pidx(b, a)) + (up ? i + 3 * j : j + 3 * i)];
               if (ASM == 1 || !((fmask >> sh.pcls[kNpe * a + b]) & 1u)) val[k] += A.K[addr[k]];
             }
 #pragma unroll
@@ -1139,7 +1146,7 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
             const int32_t k = sh.inc[ci][a];
             if (k < 0) continue;
             const bool up = a <= b;
-            const double* src = sh.kimg + 9 * (up ? pidx(a, b) : pidx(b, a));
+            const double* src = sh.kimg + L::kKs * (up ? pidx(a, b) : pidx(b, a));
             double v[9];
 #pragma unroll
             for (int q = 0; q < 9; ++q) v[q] = src[q];  // col-major K_(min,max)
@@ -1162,9 +1169,17 @@ __global__ __launch_bounds__(kBlk, 2) void h27_element_kernel(H27Args A)
         }
         else
         {
-          const double2* src = reinterpret_cast<const double2*>(sh.kimg);
-          double2* dst = reinterpret_cast<double2*>(A.rec + ec * kRec);  // 16-byte aligned (kRec even)
-          for (int v = tid; v < kNpair * 9 / 2; v += kBlk) dst[v] = src[v];
+          if constexpr (L::kKs == 9)
+          {
+            const double2* src = reinterpret_cast<const double2*>(sh.kimg);
+            double2* dst = reinterpret_cast<double2*>(A.rec + ec * kRec);  // 16-byte aligned (kRec even)
+            for (int v = tid; v < kNpair * 9 / 2; v += kBlk) dst[v] = src[v];
+          }
+          else
+          {
+            double* dst = A.rec + ec * kRec;  // the record keeps 9 doubles per block
+            for (int v = tid; v < kNpair * 9; v += kBlk) dst[v] = sh.kimg[L::kKs * (v / 9) + v % 9];
+          }
         }
       }
       // ASM 3: ec ended its chunk -- once every wave's record stores (and the producer's f stores,
