@@ -116,6 +116,9 @@ struct SweepShared {
   uint32_t prec[3][PLANE_REC_WORDS];  // plane records, ring by plane mod 3
   double gxi[8][4];  // Gauss point coordinates (stage A forms the shape derivatives from them)
   double Ng[TSI ? 8 : 1][8];  // TSI: shape values N_n at Gauss point g
+  // the same, node-major rows of 10 (16-byte aligned): the thermal pass's visit reads a node's
+  // values at Gauss points (2p, 2p + 1) as one ds_read_b128
+  alignas(16) double NgT[TSI ? 8 : 1][10];
   double w8[8];
   uint32_t neg[NSLOT];  // bit g set: fac < 0 at Gauss point g
   // lower-layer parts of the in-plane blocks (dz = 0) of node plane L+1: written by the D-side
@@ -333,13 +336,37 @@ template <int KIN, bool NEG, bool TSI, bool TH = false, class SH>
 __device__ inline void sweep_visit(const SH& sh, int slot, int a, int b1, int b2,
     uint32_t nm, double* acc1, double* acc2)
 {
+#ifndef FCG_TH_PAIRS
+#define FCG_TH_PAIRS 1
+#endif
+  // thermal pass: the shape values of nodes a, b1, b2 at all 8 Gauss points as 12 explicit
+  // 16-byte reads (the compiler paired the per-point 8-byte reads across points into
+  // ds_read2_b64, 8 LDS cycles per 16 bytes against 4)
+  double2 nA[TH && FCG_TH_PAIRS ? 4 : 1], n1[TH && FCG_TH_PAIRS ? 4 : 1], n2[TH && FCG_TH_PAIRS ? 4 : 1];
+  if constexpr (TH && FCG_TH_PAIRS)
+  {
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+    {
+      nA[p] = *reinterpret_cast<const double2*>(&sh.NgT[a][2 * p]);
+      n1[p] = *reinterpret_cast<const double2*>(&sh.NgT[b1][2 * p]);
+      n2[p] = *reinterpret_cast<const double2*>(&sh.NgT[b2][2 * p]);
+    }
+  }
   auto gp_body = [&](int g, double a0, double a1, double a2, double p0, double p1, double p2,
                      double q0, double q1, double q2) {
     if (TH)
     {
       const double* t = sh.tg[g][slot];
+#if FCG_TH_PAIRS
+      const double2 t01 = *reinterpret_cast<const double2*>(t), t23 = *reinterpret_cast<const double2*>(t + 2);
+      const double cf = t01.x, Tg = t01.y, qq = t23.x;
+      const double Na = (g & 1) ? nA[g >> 1].y : nA[g >> 1].x, N1 = (g & 1) ? n1[g >> 1].y : n1[g >> 1].x,
+                   N2 = (g & 1) ? n2[g >> 1].y : n2[g >> 1].x;
+#else
       const double cf = t[0], Tg = t[1], qq = t[2];
       const double Na = sh.Ng[g][a], N1 = sh.Ng[g][b1], N2 = sh.Ng[g][b2];
+#endif
       const double c1 = cf * N1, c2 = cf * N2, ct = cf * Na * Tg, qa = qq * Na;
       acc1[0] += c1 * a0; acc1[1] += c1 * a1; acc1[2] += c1 * a2;
       acc2[0] += c2 * a0; acc2[1] += c2 * a1; acc2[2] += c2 * a2;
@@ -558,7 +585,11 @@ __global__ __launch_bounds__(256, KIN ? 1 : FCG_SWEEP_WGS) void sweep_h8_kernel(
 
   if (tid < 24) sh.gxi[tid / 3][tid % 3] = A.tables[392 + tid];
   if (tid < 8) sh.w8[tid] = A.tables[384 + tid];
-  if (TSI && tid < 64) (&sh.Ng[0][0])[tid] = A.Ngp[tid];
+  if (TSI && tid < 64)
+  {
+    (&sh.Ng[0][0])[tid] = A.Ngp[tid];
+    sh.NgT[TSI ? (tid & 7) : 0][tid >> 3] = A.Ngp[tid];
+  }
 
   // stage-A lane: element slot s, Gauss point g
   const int s = tid >> 3, g = tid & 7;
